@@ -1,0 +1,647 @@
+// api.hip — libhdrf C-ABI (include/hdrf.h): context, batch orchestration, host views.
+//
+// One context = one DataNode's reduction state on one GPU: the index table (Redis in the
+// reference), the container arena (chunkDir files), the allocator ("blockID" key) and the
+// recipes.  All device work of a batch is enqueued on the context's stream; the host
+// synchronises once per batch to read back block counts and the allocator.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/hdrf.h"
+#include "launchers.hpp"
+
+using namespace hdrf;
+
+namespace {
+
+constexpr int kStages = 4;
+constexpr uint64_t kSlack = 64;   // readable bytes required past each block end
+
+struct ContainerInfo {
+    uint32_t slot;
+    uint32_t len;
+    int closed;
+};
+
+}  // namespace
+
+struct hdrf_ctx {
+    hdrf_cfg cfg{};
+    int H = 20, HW = 5;
+    hipStream_t st = nullptr;
+    int max_batch = 0, cap_blk = 0, ntiles = 0, spec_cap = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
+    // device buffers
+    BlockDesc *d_blocks = nullptr;
+    uint32_t *d_spec = nullptr;
+    SegMeta *d_meta = nullptr;
+    int32_t *d_sync = nullptr;
+    SegPlan *d_plan = nullptr;
+    BlockState *d_bst = nullptr;
+    uint32_t *d_off = nullptr, *d_dig = nullptr, *d_slot = nullptr, *d_pre = nullptr;
+    uint8_t *d_flags = nullptr;
+    uint32_t *d_tilesum = nullptr, *d_tilepre = nullptr;
+    uint64_t *d_store = nullptr;
+    RangeState *d_rstate = nullptr;
+    FlushEv *d_ev = nullptr;
+    ClosedRec *d_closed = nullptr;
+    uint32_t *d_nclosed = nullptr;
+    uint32_t *d_coll = nullptr, *d_ncoll = nullptr;
+    IndexEntry *d_tab = nullptr;
+    uint8_t *d_arena = nullptr;
+    AllocState *d_alloc = nullptr;
+    uint32_t *d_pcid = nullptr, *d_ppos = nullptr;
+    int *d_err = nullptr;
+    uint8_t *d_stage = nullptr;
+    uint64_t stage_cap = 0;
+    // host state
+    uint32_t batch = 0;
+    int have_alloc = 0;
+    int last_nblocks = 0;
+    std::vector<BlockState> h_bst;
+    std::vector<uint64_t> h_store;
+    AllocState h_alloc{};
+    std::map<uint32_t, ContainerInfo> containers;   // container id -> arena slot
+    std::map<uint32_t, uint32_t> slot_owner;         // arena slot -> container id
+    std::map<uint32_t, std::vector<uint8_t>> recipes; // longToBytes(blockId,4) -> recipe
+    std::map<uint32_t, int64_t> lengths;              // block length (recipe head)
+    // timing
+    bool timing = false;
+    hipEvent_t ev[kStages + 1] = {};
+    double stage_ms[kStages] = {};
+    std::string err;
+};
+
+#define HIPCK(x)                                                                       \
+    do {                                                                               \
+        hipError_t e_ = (x);                                                           \
+        if (e_ != hipSuccess) {                                                        \
+            ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);                 \
+            return HDRF_E_HIP;                                                         \
+        }                                                                              \
+    } while (0)
+
+static int set_err(hdrf_ctx *ctx, int code, const std::string &msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+template <class T>
+static int dalloc(hdrf_ctx *ctx, T **p, size_t count)
+{
+    size_t bytes = std::max<size_t>(count * sizeof(T), 256);
+    if (hipMalloc((void **)p, bytes) != hipSuccess) {
+        *p = nullptr;
+        ctx->err = "hipMalloc failed (" + std::to_string(bytes) + " bytes)";
+        return HDRF_E_NOMEM;
+    }
+    return 0;
+}
+
+extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
+{
+    if (!cfg) return HDRF_E_INVAL;
+    std::memset(cfg, 0, sizeof *cfg);
+    cfg->hasher = 0;
+    cfg->compressor = 1;
+    cfg->window = 700;
+    cfg->max_chunk = 1000000;
+    cfg->n_thread = 3;
+    cfg->min_mt_chunks = 25;
+    cfg->container_max = 1u << 25;
+    cfg->device = 0;
+    cfg->max_block_bytes = 128ll << 20;
+    cfg->max_batch_blocks = 8;
+    cfg->index_log2 = 22;
+    cfg->arena_slots = 16;
+    cfg->segment_bytes = 1 << 20;
+    cfg->keep_recipes = 1;
+    cfg->timing = 0;
+    return 0;
+}
+
+static void free_all(hdrf_ctx *ctx)
+{
+    void *ptrs[] = {ctx->d_blocks, ctx->d_spec, ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off,
+                    ctx->d_dig, ctx->d_slot, ctx->d_pre, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
+                    ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed, ctx->d_coll, ctx->d_ncoll, ctx->d_tab,
+                    ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_err, ctx->d_stage};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    for (auto &e : ctx->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->st) (void)hipStreamDestroy(ctx->st);
+}
+
+static int init_state(hdrf_ctx *ctx)
+{
+    HIPCK(hipMemsetAsync(ctx->d_tab, 0, sizeof(IndexEntry) << ctx->cfg.index_log2, ctx->st));
+    AllocState a{};
+    for (int t = 0; t < 4; t++) {
+        a.id[t] = (uint32_t)t << 22;                 // utilities.bytesToBlockID, absent key (DN/utilities.java:36-50)
+        a.slot[t] = (uint32_t)t * (uint32_t)(ctx->cfg.arena_slots / 4);   // per-range slot rings
+    }
+    HIPCK(hipMemcpyAsync(ctx->d_alloc, &a, sizeof a, hipMemcpyHostToDevice, ctx->st));
+    HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), ctx->st));
+    HIPCK(hipStreamSynchronize(ctx->st));
+    ctx->h_alloc = a;
+    ctx->batch = 0;
+    ctx->have_alloc = 0;
+    ctx->containers.clear();
+    ctx->slot_owner.clear();
+    ctx->recipes.clear();
+    ctx->lengths.clear();
+    ctx->last_nblocks = 0;
+    return 0;
+}
+
+extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
+{
+    if (!cfg_in || !out) return HDRF_E_INVAL;
+    *out = nullptr;
+    const hdrf_cfg &c = *cfg_in;
+    if ((c.hasher != 0 && c.hasher != 1) || c.window < 32 || c.window > 1000 || c.max_chunk <= c.window ||
+        c.n_thread < 1 || c.n_thread > 3 || c.max_batch_blocks < 1 || c.max_batch_blocks > kMaxBatch ||
+        c.index_log2 < 10 || c.index_log2 > 32 || c.arena_slots < 8 || c.max_block_bytes < 1 ||
+        c.max_block_bytes > (1ll << 30) || c.container_max <= (uint32_t)c.max_chunk + 1 || c.segment_bytes < (1 << 16))
+        return HDRF_E_INVAL;
+    if (c.compressor != 1) return HDRF_E_UNSUPPORTED;
+    hdrf_ctx *ctx = new (std::nothrow) hdrf_ctx();
+    if (!ctx) return HDRF_E_NOMEM;
+    ctx->cfg = c;
+    ctx->H = c.hasher == 0 ? 20 : 28;
+    ctx->HW = c.hasher == 0 ? 5 : 7;
+    int rc = 0;
+    if (hipSetDevice(c.device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return HDRF_E_HIP;
+    }
+    const int B = c.max_batch_blocks;
+    ctx->max_batch = B;
+    // minimum chunk is window+2 bytes; +2 for the drop-last/append rule and rounding
+    ctx->cap_blk = (int)(c.max_block_bytes / (c.window + 2) + 2);
+    ctx->ntiles = (ctx->cap_blk + 255) / 256;
+    ctx->spec_cap = (int)((2ll * c.segment_bytes) / (c.window + 2) + 4 + kOverrun);
+    ctx->ev_cap = (int)(B * (c.max_block_bytes / ((int64_t)c.container_max - c.max_chunk) + 2) + 16);
+    ctx->closed_cap = 3 * ctx->ev_cap;
+    ctx->coll_cap = 1 << 16;
+    const size_t nchunk = (size_t)B * ctx->cap_blk;
+    const size_t nseg = (size_t)B * kMaxSegs;
+    if ((rc = dalloc(ctx, &ctx->d_blocks, B)) || (rc = dalloc(ctx, &ctx->d_spec, nseg * ctx->spec_cap)) ||
+        (rc = dalloc(ctx, &ctx->d_meta, nseg)) || (rc = dalloc(ctx, &ctx->d_sync, nseg)) ||
+        (rc = dalloc(ctx, &ctx->d_plan, nseg)) || (rc = dalloc(ctx, &ctx->d_bst, B)) ||
+        (rc = dalloc(ctx, &ctx->d_off, nchunk)) || (rc = dalloc(ctx, &ctx->d_dig, nchunk * ctx->HW)) ||
+        (rc = dalloc(ctx, &ctx->d_slot, nchunk)) || (rc = dalloc(ctx, &ctx->d_pre, nchunk)) ||
+        (rc = dalloc(ctx, &ctx->d_flags, nchunk)) || (rc = dalloc(ctx, &ctx->d_tilesum, (size_t)B * ctx->ntiles)) ||
+        (rc = dalloc(ctx, &ctx->d_tilepre, (size_t)B * ctx->ntiles)) || (rc = dalloc(ctx, &ctx->d_store, B)) ||
+        (rc = dalloc(ctx, &ctx->d_rstate, (size_t)B * 4)) || (rc = dalloc(ctx, &ctx->d_ev, (size_t)3 * ctx->ev_cap)) ||
+        (rc = dalloc(ctx, &ctx->d_closed, ctx->closed_cap)) || (rc = dalloc(ctx, &ctx->d_nclosed, 1)) ||
+        (rc = dalloc(ctx, &ctx->d_coll, ctx->coll_cap)) || (rc = dalloc(ctx, &ctx->d_ncoll, 1)) ||
+        (rc = dalloc(ctx, &ctx->d_tab, (size_t)1 << c.index_log2)) ||
+        (rc = dalloc(ctx, &ctx->d_arena, (size_t)c.arena_slots * c.container_max + 256)) ||
+        (rc = dalloc(ctx, &ctx->d_alloc, 1)) || (rc = dalloc(ctx, &ctx->d_pcid, nchunk)) ||
+        (rc = dalloc(ctx, &ctx->d_ppos, nchunk)) || (rc = dalloc(ctx, &ctx->d_err, 1))) {
+        fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
+        free_all(ctx);
+        delete ctx;
+        return rc;
+    }
+    ctx->timing = c.timing != 0;
+    for (auto &e : ctx->ev)
+        if (hipEventCreate(&e) != hipSuccess) { free_all(ctx); delete ctx; return HDRF_E_HIP; }
+    if ((rc = init_state(ctx))) {
+        free_all(ctx);
+        delete ctx;
+        return rc;
+    }
+    *out = ctx;
+    return 0;
+}
+
+extern "C" int hdrf_close(hdrf_ctx *ctx)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    (void)hipStreamSynchronize(ctx->st);
+    free_all(ctx);
+    delete ctx;
+    return 0;
+}
+
+extern "C" const char *hdrf_last_error(const hdrf_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+extern "C" int hdrf_digest_len(const hdrf_ctx *ctx) { return ctx ? ctx->H : HDRF_E_INVAL; }
+
+extern "C" int hdrf_reset(hdrf_ctx *ctx)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    return init_state(ctx);
+}
+
+// container id -> slot bookkeeping after a batch
+static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t len, int closed)
+{
+    auto so = ctx->slot_owner.find(slot);
+    if (so != ctx->slot_owner.end() && so->second != id) ctx->containers.erase(so->second);
+    ctx->slot_owner[slot] = id;
+    ctx->containers[id] = ContainerInfo{slot, len, closed};
+}
+
+extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                                 const uint64_t *readable, const uint64_t *block_ids)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (nblocks < 1 || nblocks > ctx->max_batch || !dev_data || !len || !readable)
+        return set_err(ctx, HDRF_E_INVAL, "bad batch arguments");
+    const hdrf_cfg &c = ctx->cfg;
+    std::vector<BlockDesc> bd(nblocks);
+    int max_nseg = 1;
+    for (int b = 0; b < nblocks; b++) {
+        if ((int64_t)len[b] > c.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
+        if (readable[b] < len[b] + kSlack) return set_err(ctx, HDRF_E_INVAL, "readable must be >= len + 64");
+        if (((uintptr_t)dev_data[b] & 15) != 0) return set_err(ctx, HDRF_E_INVAL, "block data must be 16-B aligned");
+        bd[b].data = dev_data[b];
+        bd[b].len = len[b];
+        bd[b].readable = readable[b];
+        int nseg = (int)std::min<int64_t>(kMaxSegs, std::max<int64_t>(1, (int64_t)len[b] / c.segment_bytes));
+        int seg_len = (int)len[b];
+        if (nseg > 1) {
+            seg_len = (int)(((int64_t)len[b] / nseg) / (c.window + 2) * (c.window + 2));
+            if (seg_len < 4 * (c.window + 2)) { nseg = 1; seg_len = (int)len[b]; }
+        }
+        bd[b].nseg = nseg;
+        bd[b].seg_len = seg_len;
+        max_nseg = std::max(max_nseg, nseg);
+    }
+    const uint32_t cur = ++ctx->batch;
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(ctx->d_blocks, bd.data(), sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(ctx->d_nclosed, 0, sizeof(uint32_t), st));
+    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[0], st));
+    HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
+                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st));
+    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[1], st));
+    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_dig, st));
+    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[2], st));
+    HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_tab, c.index_log2,
+                       cur, ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags, ctx->d_tilesum,
+                       ctx->ntiles, ctx->d_err, st));
+    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[3], st));
+    StoreParams P;
+    P.nblocks = nblocks; P.cap_blk = ctx->cap_blk; P.ntiles = ctx->ntiles;
+    P.n_thread = c.n_thread; P.min_mt = c.min_mt_chunks; P.cmax = c.container_max;
+    P.nslots = (uint32_t)c.arena_slots; P.ev_cap = ctx->ev_cap; P.closed_cap = ctx->closed_cap;
+    HIPCK(launch_store(P, ctx->d_blocks, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre,
+                       ctx->d_store, ctx->d_pre, ctx->d_alloc, ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed,
+                       ctx->d_slot, ctx->d_tab, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, ctx->d_err, st));
+    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[4], st));
+    // read back small per-batch state
+    ctx->h_bst.resize(nblocks);
+    ctx->h_store.resize(nblocks);
+    int herr = 0;
+    uint32_t nclosed = 0;
+    HIPCK(hipMemcpyAsync(ctx->h_bst.data(), ctx->d_bst, sizeof(BlockState) * nblocks, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(ctx->h_store.data(), ctx->d_store, sizeof(uint64_t) * nblocks, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&ctx->h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&herr, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&nclosed, ctx->d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (ctx->timing) {
+        for (int i = 0; i < kStages; i++) {
+            float ms = 0;
+            HIPCK(hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]));
+            ctx->stage_ms[i] += ms;
+        }
+    }
+    ctx->last_nblocks = nblocks;
+    if (herr) {
+        HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), st));
+        return set_err(ctx, herr & 6 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
+                       "device reported error flags " + std::to_string(herr));
+    }
+    if ((int)nclosed > ctx->closed_cap) return set_err(ctx, HDRF_E_CAPACITY, "closed-container list overflow");
+    // container bookkeeping
+    if (nclosed) {
+        std::vector<ClosedRec> cl(nclosed);
+        HIPCK(hipMemcpy(cl.data(), ctx->d_closed, sizeof(ClosedRec) * nclosed, hipMemcpyDeviceToHost));
+        for (auto &r : cl) note_container(ctx, r.id, r.slot, r.len, 1);
+    }
+    bool any_store = false;
+    for (int b = 0; b < nblocks; b++) any_store |= ctx->h_store[b] != 0;
+    for (int t = 0; t < c.n_thread; t++)
+        if (ctx->h_alloc.exists[t]) note_container(ctx, ctx->h_alloc.id[t], ctx->h_alloc.slot[t], ctx->h_alloc.cur[t], 0);
+    (void)any_store;
+    ctx->have_alloc = 1;                              // storeDB always SETs "blockID" (:389)
+    // recipes (SET longToBytes(id,4) -> BE32 size | digests)
+    for (int b = 0; b < nblocks; b++) {
+        const uint32_t key = (uint32_t)(block_ids ? block_ids[b] : 0);
+        ctx->lengths[key] = (int64_t)len[b];
+        if (c.keep_recipes) {
+            const int64_t n = ctx->h_bst[b].n_chunks;
+            std::vector<uint8_t> r(4 + n * ctx->H);
+            r[0] = (uint8_t)(len[b] >> 24); r[1] = (uint8_t)(len[b] >> 16);
+            r[2] = (uint8_t)(len[b] >> 8); r[3] = (uint8_t)len[b];
+            std::vector<uint32_t> dw((size_t)n * ctx->HW);
+            HIPCK(hipMemcpy(dw.data(), ctx->d_dig + (size_t)b * ctx->cap_blk * ctx->HW, dw.size() * 4,
+                            hipMemcpyDeviceToHost));
+            std::memcpy(r.data() + 4, dw.data(), (size_t)n * ctx->H);
+            ctx->recipes[key] = std::move(r);
+        }
+    }
+    return 0;
+}
+
+static int check_b(hdrf_ctx *ctx, int32_t b)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (b < 0 || b >= ctx->last_nblocks) return set_err(ctx, HDRF_E_INVAL, "block index out of range");
+    return 0;
+}
+
+extern "C" int hdrf_batch_info(hdrf_ctx *ctx, int32_t b, int64_t *n_chunks, int64_t *store_size)
+{
+    if (int rc = check_b(ctx, b)) return rc;
+    if (n_chunks) *n_chunks = ctx->h_bst[b].n_chunks;
+    if (store_size) *store_size = (int64_t)ctx->h_store[b];
+    return 0;
+}
+
+extern "C" int hdrf_batch_offsets(hdrf_ctx *ctx, int32_t b, uint32_t *out, int64_t cap)
+{
+    if (int rc = check_b(ctx, b)) return rc;
+    const int64_t n = ctx->h_bst[b].n_chunks;
+    if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "offsets capacity");
+    HIPCK(hipMemcpy(out, ctx->d_off + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int hdrf_batch_digests(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap_bytes)
+{
+    if (int rc = check_b(ctx, b)) return rc;
+    const int64_t n = ctx->h_bst[b].n_chunks;
+    if (cap_bytes < n * ctx->H) return set_err(ctx, HDRF_E_CAPACITY, "digest capacity");
+    HIPCK(hipMemcpy(out, ctx->d_dig + (size_t)b * ctx->cap_blk * ctx->HW, n * ctx->H, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int hdrf_batch_is_new(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap)
+{
+    if (int rc = check_b(ctx, b)) return rc;
+    const int64_t n = ctx->h_bst[b].n_chunks;
+    if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "is_new capacity");
+    HIPCK(hipMemcpy(out, ctx->d_flags + (size_t)b * ctx->cap_blk, n, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++) out[i] &= 1;
+    return 0;
+}
+
+extern "C" int hdrf_batch_placement(hdrf_ctx *ctx, int32_t b, uint32_t *cid, uint32_t *pos, int64_t cap)
+{
+    if (int rc = check_b(ctx, b)) return rc;
+    const int64_t n = ctx->h_bst[b].n_chunks;
+    if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "placement capacity");
+    std::vector<uint8_t> f(n);
+    HIPCK(hipMemcpy(f.data(), ctx->d_flags + (size_t)b * ctx->cap_blk, n, hipMemcpyDeviceToHost));
+    if (cid) HIPCK(hipMemcpy(cid, ctx->d_pcid + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
+    if (pos) HIPCK(hipMemcpy(pos, ctx->d_ppos + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; i++)
+        if (!(f[i] & 1)) {
+            if (cid) cid[i] = 0;
+            if (pos) pos[i] = 0;
+        }
+    return 0;
+}
+
+extern "C" int hdrf_reduce_block(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *data, uint64_t len,
+                                 hdrf_block_result *out)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if ((int64_t)len > ctx->cfg.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
+    if (len && !data) return set_err(ctx, HDRF_E_INVAL, "null data");
+    const uint64_t need = len + 4096;
+    if (ctx->stage_cap < need) {
+        if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+        ctx->d_stage = nullptr;
+        ctx->stage_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(need, (uint64_t)ctx->cfg.max_block_bytes + 4096);
+        HIPCK(hipMalloc((void **)&ctx->d_stage, cap));
+        ctx->stage_cap = cap;
+    }
+    if (len) HIPCK(hipMemcpyAsync(ctx->d_stage, data, len, hipMemcpyHostToDevice, ctx->st));
+    HIPCK(hipMemsetAsync(ctx->d_stage + len, 0, 64, ctx->st));
+    const uint8_t *p = ctx->d_stage;
+    const uint64_t readable = ctx->stage_cap;
+    int rc = hdrf_reduce_batch(ctx, 1, &p, &len, &readable, &block_id);
+    if (rc) return rc;
+    if (out) {
+        int64_t n = 0, ss = 0;
+        hdrf_batch_info(ctx, 0, &n, &ss);
+        out->n_chunks = n;
+        out->store_size = ss;
+        if (out->capacity < n && (out->offsets || out->digests || out->is_new || out->container_id || out->container_pos))
+            return set_err(ctx, HDRF_E_CAPACITY, "result capacity too small");
+        if (out->offsets && (rc = hdrf_batch_offsets(ctx, 0, out->offsets, out->capacity))) return rc;
+        if (out->digests && (rc = hdrf_batch_digests(ctx, 0, out->digests, out->capacity * ctx->H))) return rc;
+        if (out->is_new && (rc = hdrf_batch_is_new(ctx, 0, out->is_new, out->capacity))) return rc;
+        if ((out->container_id || out->container_pos) &&
+            (rc = hdrf_batch_placement(ctx, 0, out->container_id, out->container_pos, out->capacity)))
+            return rc;
+    }
+    return 0;
+}
+
+// ---- index views ------------------------------------------------------------------------
+static void encode_value(const IndexEntry &e, uint8_t v[11])
+{
+    // chunkMeta.getMeta — DN/chunkMeta.java:62-77
+    v[0] = (uint8_t)e.ncopy;
+    v[1] = (uint8_t)(e.cid >> 16); v[2] = (uint8_t)(e.cid >> 8); v[3] = (uint8_t)e.cid;
+    v[4] = (uint8_t)(e.start >> 16); v[5] = (uint8_t)(e.start >> 8); v[6] = (uint8_t)e.start;
+    v[7] = (uint8_t)(e.stop >> 16); v[8] = (uint8_t)(e.stop >> 8); v[9] = (uint8_t)e.stop;
+    v[10] = (uint8_t)(((e.start >> 20) & 0xF0) | ((e.stop >> 24) & 0x0F));
+}
+
+static void entry_digest(const IndexEntry &e, int H, uint8_t *out)
+{
+    unsigned long long tag = (e.batch & 0x80000000u) ? 0ull : e.tag;
+    std::memcpy(out, &tag, 8);
+    std::memcpy(out + 8, e.dig, H - 8);
+}
+
+extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out11[11])
+{
+    if (!ctx || !digest) return HDRF_E_INVAL;
+    unsigned long long tag;
+    std::memcpy(&tag, digest, 8);
+    const uint32_t z = tag == 0 ? 0x80000000u : 0u;
+    if (tag == 0) tag = 1;
+    const uint64_t mask = (1ull << ctx->cfg.index_log2) - 1;
+    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - ctx->cfg.index_log2);
+    HIPCK(hipStreamSynchronize(ctx->st));
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+        IndexEntry e;
+        HIPCK(hipMemcpy(&e, ctx->d_tab + h, sizeof e, hipMemcpyDeviceToHost));
+        if (e.tag == 0) return 0;
+        if (e.tag == tag && (e.batch & 0x80000000u) == z && std::memcmp(e.dig, digest + 8, ctx->H - 8) == 0) {
+            if (out11) encode_value(e, out11);
+            return 1;
+        }
+        h = (h + 1) & mask;
+    }
+    return 0;
+}
+
+static int fetch_table(hdrf_ctx *ctx, std::vector<IndexEntry> &tab)
+{
+    tab.resize((size_t)1 << ctx->cfg.index_log2);
+    HIPCK(hipStreamSynchronize(ctx->st));
+    HIPCK(hipMemcpy(tab.data(), ctx->d_tab, tab.size() * sizeof(IndexEntry), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int64_t hdrf_index_count(hdrf_ctx *ctx)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    std::vector<IndexEntry> tab;
+    if (int rc = fetch_table(ctx, tab)) return rc;
+    int64_t n = 0;
+    for (auto &e : tab) n += e.tag != 0;
+    return n;
+}
+
+extern "C" int64_t hdrf_index_dump(hdrf_ctx *ctx, uint8_t *keys, uint8_t *vals, int64_t cap)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    std::vector<IndexEntry> tab;
+    if (int rc = fetch_table(ctx, tab)) return rc;
+    const int H = ctx->H;
+    std::vector<std::vector<uint8_t>> rows;
+    for (auto &e : tab) {
+        if (e.tag == 0) continue;
+        std::vector<uint8_t> r(H + 11);
+        entry_digest(e, H, r.data());
+        encode_value(e, r.data() + H);
+        rows.push_back(std::move(r));
+    }
+    if ((int64_t)rows.size() > cap) return set_err(ctx, HDRF_E_CAPACITY, "index dump capacity");
+    std::sort(rows.begin(), rows.end(),
+              [H](const std::vector<uint8_t> &a, const std::vector<uint8_t> &b) { return std::memcmp(a.data(), b.data(), H) < 0; });
+    for (size_t i = 0; i < rows.size(); i++) {
+        std::memcpy(keys + i * H, rows[i].data(), H);
+        std::memcpy(vals + i * 11, rows[i].data() + H, 11);
+    }
+    return (int64_t)rows.size();
+}
+
+extern "C" int hdrf_allocator(hdrf_ctx *ctx, uint8_t out24[24])
+{
+    if (!ctx || !out24) return HDRF_E_INVAL;
+    if (!ctx->have_alloc) return 0;
+    uint32_t v[8];
+    for (int t = 0; t < 4; t++) {
+        v[t] = ctx->h_alloc.id[t];
+        v[t + 4] = ctx->h_alloc.pos[t];
+    }
+    for (int i = 0; i < 8; i++) {                   // utilities.blockIDtoBytes (DN/utilities.java:66-75)
+        out24[3 * i] = (uint8_t)(v[i] >> 16);
+        out24[3 * i + 1] = (uint8_t)(v[i] >> 8);
+        out24[3 * i + 2] = (uint8_t)v[i];
+    }
+    return 1;
+}
+
+extern "C" int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    auto it = ctx->recipes.find((uint32_t)block_id);
+    if (it == ctx->recipes.end()) return 0;
+    const int64_t n = (int64_t)it->second.size();
+    if (!out || cap < n) return set_err(ctx, HDRF_E_CAPACITY, "recipe needs " + std::to_string(n) + " bytes");
+    std::memcpy(out, it->second.data(), n);
+    return n;
+}
+
+extern "C" int64_t hdrf_block_length(hdrf_ctx *ctx, uint64_t block_id)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    auto it = ctx->lengths.find((uint32_t)block_id);
+    return it == ctx->lengths.end() ? HDRF_E_NOTFOUND : it->second;
+}
+
+extern "C" int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t cap, int32_t *closed)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    auto it = ctx->containers.find(id);
+    if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_NOTFOUND, "container not resident");
+    if (closed) *closed = it->second.closed;
+    const int64_t n = it->second.len;
+    if (!out) return n;
+    if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "container capacity");
+    HIPCK(hipStreamSynchronize(ctx->st));
+    if (n) HIPCK(hipMemcpy(out, ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max, n, hipMemcpyDeviceToHost));
+    return n;
+}
+
+// ---- memory helpers, corpus, timing ------------------------------------------------------
+extern "C" int hdrf_dev_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
+{
+    if (!ctx || !out) return HDRF_E_INVAL;
+    HIPCK(hipMalloc(out, bytes));
+    return 0;
+}
+
+extern "C" int hdrf_dev_free(hdrf_ctx *ctx, void *p)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    HIPCK(hipStreamSynchronize(ctx->st));
+    HIPCK(hipFree(p));
+    return 0;
+}
+
+extern "C" int hdrf_memcpy_h2d(hdrf_ctx *ctx, void *dst, const void *src, uint64_t bytes)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    HIPCK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->st));
+    HIPCK(hipStreamSynchronize(ctx->st));
+    return 0;
+}
+
+extern "C" int hdrf_memcpy_d2h(hdrf_ctx *ctx, void *dst, const void *src, uint64_t bytes)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    HIPCK(hipStreamSynchronize(ctx->st));
+    HIPCK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int hdrf_synchronize(hdrf_ctx *ctx)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    HIPCK(hipStreamSynchronize(ctx->st));
+    return 0;
+}
+
+extern "C" int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
+                                int64_t segs_per_block, int64_t seg_bytes, uint64_t seed)
+{
+    if (!ctx || !dev || !roots_host || seg_bytes % 16 != 0) return HDRF_E_INVAL;
+    uint32_t *d_roots = nullptr;
+    const size_t n = (size_t)nblocks * segs_per_block;
+    HIPCK(hipMalloc((void **)&d_roots, n * 4));
+    HIPCK(hipMemcpyAsync(d_roots, roots_host, n * 4, hipMemcpyHostToDevice, ctx->st));
+    HIPCK(launch_corpus(dev, d_roots, nblocks, segs_per_block, seg_bytes, seed, ctx->st));
+    HIPCK(hipStreamSynchronize(ctx->st));
+    HIPCK(hipFree(d_roots));
+    return 0;
+}
+
+extern "C" int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    for (int i = 0; i < n && i < kStages; i++) ms[i] = ctx->stage_ms[i];
+    if (reset)
+        for (double &v : ctx->stage_ms) v = 0;
+    return 0;
+}

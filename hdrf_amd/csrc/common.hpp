@@ -1,0 +1,165 @@
+// common.hpp — shared device helpers and on-device layouts for libhdrf (gfx950 only).
+//
+// Data layout in HBM (one batch of up to 64 blocks):
+//   block bytes          caller's device buffers (16-B aligned), `readable` bytes each
+//   spec lists           [block][segment][SPEC_CAP] u32 cut offsets from the speculative walk
+//   offsets              [block][cap_blk] u32 chunk END offsets (reference chunking() output)
+//   digests              [block][cap_blk][H] bytes
+//   chunk meta           [block][cap_blk] slot / flags / prefix
+//   index table          2^k entries x 64 B, open addressing keyed by the first 8 digest bytes
+//   container arena      slots x container_max bytes (raw containers, DataDeduplicator.maxSize)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hdrf {
+
+constexpr int kWave = 64;
+constexpr int kMaxBatch = 64;        // one bit per block of the batch in IndexEntry::mask
+constexpr int kMaxSegs = 256;        // speculative chunking segments per block
+constexpr int kOverrun = 64;         // overrun cuts recorded past a segment end (one per lane)
+constexpr uint64_t kEmptyTag = 0;
+
+// Index entry: 64 B.  tag = first 8 digest bytes (0 remapped to 1 with flag bit 31 of `batch`);
+// `dig` holds digest bytes 8..27.  ncopy/cid/start/stop are the 11-byte Redis value
+// (chunkMeta.getMeta, DN/chunkMeta.java:62-77) in unpacked form.
+struct alignas(64) IndexEntry {
+    unsigned long long tag;
+    unsigned long long mask;    // batch-local: bit b = block b of the batch holds the digest
+    unsigned long long first;   // batch-local: max over ((63-b)<<32 | chunk index)
+    uint32_t batch;             // batch id that created the entry (| 0x80000000 if tag remapped)
+    uint32_t ncopy;
+    uint32_t cid;
+    uint32_t start;
+    uint32_t stop;
+    uint32_t dig[5];
+
+};
+static_assert(sizeof(IndexEntry) == 64, "IndexEntry must be one 64-B line");
+
+// Per-batch block descriptor (device side).
+struct BlockDesc {
+    const uint8_t *data;
+    uint64_t len;
+    uint64_t readable;       // bytes readable from data (>= len)
+    int32_t nseg;
+    int32_t seg_len;         // multiple of 702 (window + 2) so all-zero data syncs at once
+};
+
+// Speculative segment walk result.
+struct SegMeta {
+    int32_t n_main;          // cuts < next segment start
+    int32_t n_over;          // cuts >= next segment start (<= kOverrun)
+    int32_t ended;           // chain ended at block end
+    int32_t pad;
+};
+
+// Stitch plan per segment.
+struct SegPlan {
+    int32_t main_begin;      // first main index taken
+    int32_t main_count;
+    int32_t over_count;      // overrun entries taken
+    int32_t dst;             // destination index in the block's offsets
+};
+
+// Per-block state after chunking/stitching.
+struct BlockState {
+    int32_t n_cuts;          // true boundaries before the drop-last rule (stitched + fallback)
+    int32_t fail_dst;        // fallback writes from here (-1 = none)
+    uint32_t fail_p0;        // last true boundary before fallback
+    int32_t n_chunks;        // final chunk count (offsets list length)
+};
+
+// Container stream state per storer range t (lastBlockID[t], file length, lastBlockID[t+4]).
+struct AllocState {
+    uint32_t id[4];
+    uint32_t cur[4];         // open container length (file length)
+    uint32_t pos[4];         // lastBlockID[t+4] (bufferBB.position() of the last storing block)
+    uint32_t slot[4];        // arena slot of the open container
+    uint32_t next_slot;
+    uint32_t nclosed;        // containers closed so far (total)
+    uint32_t exists[4];      // open container file exists
+    uint32_t pad;
+};
+
+// Flush event inside one (block, range): container closes before chunk `chunk`.
+struct FlushEv {
+    int32_t chunk;
+    uint32_t new_id;
+    uint32_t new_slot;
+    uint32_t base;           // range-relative prefix (X0 of `chunk`)
+};
+
+struct RangeState {          // per (block, range t)
+    uint32_t id0, slot0, cur0;   // open container at the range start
+    int32_t nflush;              // flush events of this (block, range)
+    int32_t ev_begin;            // first event in the range-t event list
+    int32_t c_begin, c_end;      // chunk range [n*t/nT, n*(t+1)/nT)
+    uint32_t base;               // block prefix of new bytes before c_begin
+    uint32_t total;              // new bytes in range
+    int32_t active;              // storer t runs (storeSize != 0 and t < nThread)
+};
+
+struct ClosedRec {           // a container closed during a batch
+    uint32_t id, slot, len, range;
+};
+
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint32_t rdfirst(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// Wave-wide unsigned max (all lanes participate; result uniform).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+    // row_ror:1,2,4,8 -> every lane holds its 16-lane row max
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false));
+    uint32_t a = max(rdlane(v, 0), rdlane(v, 16));
+    uint32_t b = max(rdlane(v, 32), rdlane(v, 48));
+    return max(a, b);
+}
+
+// Inclusive wave prefix sum (u32) via shuffles.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    const int l = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t t = __shfl_up(v, d, 64);
+        if (l >= d) v += t;
+    }
+    return v;
+}
+
+__device__ __forceinline__ unsigned long long ballot64(bool p) { return __ballot(p); }
+
+// Bounds-checked 16-B load (bytes >= avail read as 0).
+__device__ __forceinline__ uint4 load16_guard(const uint8_t *base, int64_t off, int64_t avail)
+{
+    if (off + 16 <= avail) return *reinterpret_cast<const uint4 *>(base + off);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int i = 0; i < 16; i++)
+        if (off + i < avail) w[i >> 2] |= (uint32_t)base[off + i] << (8 * (i & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ uint32_t load4_guard(const uint8_t *base, int64_t off, int64_t avail)
+{
+    if (off + 4 <= avail) return *reinterpret_cast<const uint32_t *>(base + off);
+    uint32_t w = 0;
+    for (int i = 0; i < 4; i++)
+        if (off + i < avail) w |= (uint32_t)base[off + i] << (8 * i);
+    return w;
+}
+
+}  // namespace hdrf

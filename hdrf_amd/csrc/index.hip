@@ -1,0 +1,211 @@
+// index.hip — GPU-resident fingerprint index with HDRF's exact dedup semantics.
+//
+// Reference semantics:
+//   * index key = digest bytes, value = 11-byte chunkMeta (DN/chunkMeta.java:62-77);
+//   * a block's GETs all happen before its SETs (DN/DataDeduplicator.java:588-613 vs
+//     :702-818) and blocks are serialised by the FIFO (:124-158,197-204)
+//     => chunk is a duplicate  iff  its digest was stored by an EARLIER block;
+//   * duplicates inside one block are both "new" (identity HashMap, :338-367);
+//   * nCopy = (#distinct blocks holding the digest) mod 256; the location is the one SET by
+//     the first block's last occurrence (later SETs re-write the decoded location).
+//
+// Batched formulation (blocks b = 0..63 of a batch, in arrival order):
+//   claim  — probe open addressing by the 8-byte tag; CAS-claim empty slots
+//   apply  — verify the full digest; atomicOr(mask, 1<<b); atomicMax(first, (63-b)<<32|k)
+//   slow   — single-thread exact re-probe for the (astronomically rare) 8-byte tag collisions
+//   decide — is_new = entry created this batch && b == min block; designated = (min block,
+//            last chunk index) is the one chunk that writes the final value (in store.hip)
+#include "launchers.hpp"
+
+namespace hdrf {
+
+__device__ __forceinline__ unsigned long long make_tag(const uint32_t *dw, uint32_t &zflag)
+{
+    unsigned long long t = (unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32);
+    zflag = (t == 0) ? 0x80000000u : 0u;
+    return t == 0 ? 1ull : t;
+}
+
+__device__ __forceinline__ uint64_t home_slot(unsigned long long tag, int log2cap)
+{
+    return (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
+}
+
+template <int HW>
+__device__ __forceinline__ bool entry_matches(const IndexEntry &e, const uint32_t *dw, uint32_t z)
+{
+    if ((e.batch & 0x80000000u) != z) return false;
+#pragma unroll
+    for (int i = 2; i < HW; i++)
+        if (e.dig[i - 2] != dw[i]) return false;
+    return true;
+}
+
+// ---- claim: grid (ceil(cap_blk/256), nblocks) ---------------------------------------------
+template <int HW>
+__global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__restrict__ bst, int cap_blk,
+                                                        const uint32_t *__restrict__ digests,
+                                                        IndexEntry *__restrict__ tab, int log2cap, uint32_t cur,
+                                                        uint32_t *__restrict__ slot, int *__restrict__ err)
+{
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= bst[b].n_chunks) return;
+    const size_t c = (size_t)b * cap_blk + k;
+    uint32_t dw[HW];
+#pragma unroll
+    for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
+    uint32_t z;
+    const unsigned long long tag = make_tag(dw, z);
+    const uint64_t mask = (1ull << log2cap) - 1;
+    uint64_t h = home_slot(tag, log2cap);
+    for (uint64_t probe = 0;; probe++) {
+        if (probe > mask) { atomicOr(err, 2); return; }           // table full
+        IndexEntry *e = tab + h;
+        unsigned long long t = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == kEmptyTag) {
+            unsigned long long old = atomicCAS(&e->tag, kEmptyTag, tag);
+            if (old == kEmptyTag) {
+                e->batch = cur | z;
+#pragma unroll
+                for (int i = 2; i < 7; i++) e->dig[i - 2] = i < HW ? dw[i] : 0u;
+                break;
+            }
+            t = old;
+        }
+        if (t == tag) break;
+        h = (h + 1) & mask;
+    }
+    slot[c] = (uint32_t)h;
+}
+
+// ---- apply: verify full digest, record block membership / last occurrence ----------------
+template <int HW>
+__global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__restrict__ bst, int cap_blk,
+                                                        const uint32_t *__restrict__ digests,
+                                                        IndexEntry *__restrict__ tab, const uint32_t *__restrict__ slot,
+                                                        uint32_t *__restrict__ coll, uint32_t *__restrict__ ncoll,
+                                                        int coll_cap, int *__restrict__ err)
+{
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= bst[b].n_chunks) return;
+    const size_t c = (size_t)b * cap_blk + k;
+    uint32_t dw[HW];
+#pragma unroll
+    for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
+    uint32_t z;
+    (void)make_tag(dw, z);
+    IndexEntry *e = tab + slot[c];
+    if (entry_matches<HW>(*e, dw, z)) {
+        atomicOr(&e->mask, 1ull << b);
+        atomicMax(&e->first, ((unsigned long long)(63 - b) << 32) | (unsigned)k);
+    } else {
+        uint32_t i = atomicAdd(ncoll, 1u);
+        if ((int)i < coll_cap) coll[i] = (uint32_t)c;
+        else atomicOr(err, 4);
+    }
+}
+
+// ---- slow path: one thread, exact sequential re-probe of tag-collided chunks --------------
+template <int HW>
+__global__ void idx_slow_kernel(int cap_blk, const uint32_t *__restrict__ digests, IndexEntry *__restrict__ tab,
+                                int log2cap, uint32_t cur, uint32_t *__restrict__ slot,
+                                const uint32_t *__restrict__ coll, const uint32_t *__restrict__ ncoll, int coll_cap,
+                                int *__restrict__ err)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t n = min(*ncoll, (uint32_t)coll_cap);
+    const uint64_t mask = (1ull << log2cap) - 1;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t c = coll[i];
+        const int b = (int)(c / (uint32_t)cap_blk), k = (int)(c % (uint32_t)cap_blk);
+        uint32_t dw[HW];
+        for (int q = 0; q < HW; q++) dw[q] = digests[(size_t)c * HW + q];
+        uint32_t z;
+        const unsigned long long tag = make_tag(dw, z);
+        uint64_t h = (slot[c] + 1) & mask;
+        for (uint64_t probe = 0;; probe++) {
+            if (probe > mask) { *err |= 2; return; }
+            IndexEntry *e = tab + h;
+            if (e->tag == kEmptyTag) {
+                e->tag = tag; e->batch = cur | z; e->mask = 0; e->first = 0;
+                for (int q = 2; q < 7; q++) e->dig[q - 2] = q < HW ? dw[q] : 0u;
+                break;
+            }
+            if (e->tag == tag && entry_matches<HW>(*e, dw, z)) break;
+            h = (h + 1) & mask;
+        }
+        slot[c] = (uint32_t)h;
+        IndexEntry *e = tab + h;
+        e->mask |= 1ull << b;
+        const unsigned long long f = ((unsigned long long)(63 - b) << 32) | (unsigned)k;
+        if (f > e->first) e->first = f;
+    }
+}
+
+// ---- decide: is_new / designated + per-tile new-byte sums ---------------------------------
+// flags bit0 = is_new, bit1 = designated (writes the final index value), bit2 = entry created
+// this batch.  tilesum[b][tile] = sum of new-chunk lengths of the 256 chunks of this workgroup.
+__global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__restrict__ bst, int cap_blk,
+                                                         const uint32_t *__restrict__ offsets,
+                                                         const IndexEntry *__restrict__ tab,
+                                                         const uint32_t *__restrict__ slot, uint32_t cur,
+                                                         uint8_t *__restrict__ flags, uint32_t *__restrict__ tilesum,
+                                                         int ntiles)
+{
+    __shared__ uint32_t s_part[4];
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int n = bst[b].n_chunks;
+    uint32_t newlen = 0;
+    if (k < n) {
+        const size_t c = (size_t)b * cap_blk + k;
+        const IndexEntry *e = tab + slot[c];
+        const unsigned long long f = e->first;
+        const int minb = 63 - (int)(f >> 32);
+        const int maxk = (int)(uint32_t)f;
+        const bool created = (e->batch & 0x7fffffffu) == cur;
+        const bool is_new = created && b == minb;
+        const bool desig = (b == minb) && (k == maxk);
+        flags[c] = (uint8_t)((is_new ? 1 : 0) | (desig ? 2 : 0) | (created ? 4 : 0));
+        if (is_new) {
+            const uint32_t *off = offsets + (size_t)b * cap_blk;
+            newlen = off[k] - (k ? off[k - 1] : 0u);
+        }
+    }
+    // workgroup sum of new bytes
+    uint32_t v = newlen;
+    for (int d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
+    if (lane_id() == 0) s_part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        tilesum[(size_t)b * ntiles + blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+}
+
+hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
+                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t *slot,
+                        uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
+                        int ntiles, int *err, hipStream_t st)
+{
+    dim3 g(ntiles, nblocks);
+    (void)hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st);
+    if (hasher == 0) {
+        hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
+        hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
+                           coll_cap, err);
+        hipLaunchKernelGGL(idx_slow_kernel<5>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, slot,
+                           coll, ncoll, coll_cap, err);
+    } else {
+        hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
+        hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
+                           coll_cap, err);
+        hipLaunchKernelGGL(idx_slow_kernel<7>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, slot,
+                           coll, ncoll, coll_cap, err);
+    }
+    hipLaunchKernelGGL(idx_decide_kernel, g, dim3(256), 0, st, bst, cap_blk, offsets, tab, slot, cur, flags, tilesum,
+                       ntiles);
+    return hipGetLastError();
+}
+
+}  // namespace hdrf

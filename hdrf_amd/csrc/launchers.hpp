@@ -1,0 +1,33 @@
+// launchers.hpp — host-side kernel launchers shared by api.hip (one stream per context).
+#pragma once
+#include "common.hpp"
+
+namespace hdrf {
+
+struct StoreParams {
+    int nblocks, cap_blk, ntiles;
+    int n_thread, min_mt;      // DataDeduplicator.nThread (3), small-block threshold (25)
+    uint32_t cmax;             // DataDeduplicator.maxSize
+    uint32_t nslots;           // container arena slots
+    int ev_cap;                // flush events per range per batch
+    int closed_cap;            // closed containers per batch
+};
+
+hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg, int w, int maxlen,
+                           uint32_t *spec, int spec_cap, SegMeta *meta, int32_t *sync, SegPlan *plan,
+                           BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st);
+hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
+                      const BlockState *bst, int cap_blk, uint32_t *digests, hipStream_t st);
+hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
+                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t *slot,
+                        uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
+                        int ntiles, int *err, hipStream_t st);
+hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
+                        const uint32_t *offsets, const uint8_t *flags, const uint32_t *tilesum, uint32_t *tilepre,
+                        uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
+                        ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
+                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st);
+hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
+                         uint64_t seed, hipStream_t st);
+
+}  // namespace hdrf

@@ -1,0 +1,150 @@
+// sha.hip — per-chunk SHA-1 / SHA-224 fingerprints on gfx950 (integer VALU, no MFMA).
+//
+// Reference: threadedHasher.run, DN/DataDeduplicator.java:578-641 hashes chunk k =
+// [off[k-1], off[k]) with utilities.sha1hash (hasher==0) or sha224hash (hasher==1),
+// DN/utilities.java:98-137 (nayuki native compress + FIPS 180-4 padding).
+//
+// One lane owns one chunk and runs its compression chain; the wave's 64 chunks are adjacent
+// in the block, so a wave streams a contiguous ~60 KiB region.  Each 64-B message block is
+// fetched as 17 dword-aligned dwords and realigned + byte-swapped with one v_perm_b32 per
+// word.  Rotations are v_alignbit_b32, Ch/Maj are v_bfi_b32.
+#include "launchers.hpp"
+
+namespace hdrf {
+
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+__device__ __forceinline__ void sha1_compress(uint32_t st[5], uint32_t w[16])
+{
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
+#pragma unroll
+    for (int i = 0; i < 80; i++) {
+        if (i >= 16) w[i & 15] = rotl(w[(i - 3) & 15] ^ w[(i - 8) & 15] ^ w[(i - 14) & 15] ^ w[i & 15], 1);
+        uint32_t f, k;
+        if (i < 20)      { f = bfi(b, c, d);      k = 0x5A827999u; }
+        else if (i < 40) { f = b ^ c ^ d;         k = 0x6ED9EBA1u; }
+        else if (i < 60) { f = bfi(b ^ c, d, c);  k = 0x8F1BBCDCu; }
+        else             { f = b ^ c ^ d;         k = 0xCA62C1D6u; }
+        const uint32_t t = rotl(a, 5) + f + e + k + w[i & 15];
+        e = d; d = c; c = rotl(b, 30); b = a; a = t;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
+}
+
+__constant__ uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16])
+{
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        if (i >= 16) {
+            const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+            const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+            const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            w[i & 15] = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+        }
+        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t t1 = h + S1 + bfi(e, f, g) + kK256[i] + w[i & 15];
+        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t t2 = S0 + bfi(a ^ b, c, b);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Message block `bi` of a chunk [start, start+len) as 16 big-endian words, with FIPS 180-4
+// padding applied when the block reaches past the message end.
+__device__ __forceinline__ void load_block(const uint8_t *base, int64_t avail, int64_t start, int len, int bi,
+                                           int nblk, uint32_t m[16])
+{
+    const int64_t pos = start + 64 * (int64_t)bi;
+    const int64_t apos = pos & ~(int64_t)3;
+    const uint32_t sel = 0x00010203u + (uint32_t)(pos & 3) * 0x01010101u;
+    uint32_t d[17];
+    if (apos + 68 <= avail) {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(base + apos);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            u32x4a v = *reinterpret_cast<const u32x4a *>(p + 4 * q);
+            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+        }
+        d[16] = p[16];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 17; q++) d[q] = load4_guard(base, apos + 4 * q, avail);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+    const int off = 64 * bi;
+    if (off + 64 > len) {             // tail: zero past the end, 0x80 terminator, bit length
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int nv = len - (off + 4 * i);          // message bytes left at this word
+            uint32_t x = m[i];
+            if (nv <= 0) x = (nv == 0) ? 0x80000000u : 0u;
+            else if (nv < 4) x = (x & (0xffffffffu << (32 - 8 * nv))) | (0x80000000u >> (8 * nv));
+            m[i] = x;
+        }
+        if (bi == nblk - 1) {
+            m[14] = (uint32_t)((uint64_t)len >> 29);
+            m[15] = (uint32_t)len << 3;
+        }
+    }
+}
+
+template <int HW>   // digest words: 5 (SHA-1) or 7 (SHA-224)
+__global__ void __launch_bounds__(256) sha_kernel(const BlockDesc *__restrict__ blocks,
+                                                  const uint32_t *__restrict__ offsets,
+                                                  const BlockState *__restrict__ bst, int cap_blk,
+                                                  uint32_t *__restrict__ digests)
+{
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int n = bst[b].n_chunks;
+    if (k >= n) return;
+    const BlockDesc bd = blocks[b];
+    const uint32_t *off = offsets + (size_t)b * cap_blk;
+    const int64_t start = k ? off[k - 1] : 0;
+    const int len = (int)(off[k] - start);
+    const int nblk = (len + 8) / 64 + 1;
+    uint32_t st[8];
+    if (HW == 5) {
+        st[0] = 0x67452301u; st[1] = 0xEFCDAB89u; st[2] = 0x98BADCFEu; st[3] = 0x10325476u; st[4] = 0xC3D2E1F0u;
+    } else {
+        st[0] = 0xc1059ed8u; st[1] = 0x367cd507u; st[2] = 0x3070dd17u; st[3] = 0xf70e5939u;
+        st[4] = 0xffc00b31u; st[5] = 0x68581511u; st[6] = 0x64f98fa7u; st[7] = 0xbefa4fa4u;
+    }
+    for (int bi = 0; bi < nblk; bi++) {
+        uint32_t m[16];
+        load_block(bd.data, (int64_t)bd.readable, start, len, bi, nblk, m);
+        if (HW == 5) sha1_compress(st, m);
+        else sha256_compress(st, m);
+    }
+    uint32_t *dst = digests + ((size_t)b * cap_blk + k) * HW;
+#pragma unroll
+    for (int i = 0; i < HW; i++) dst[i] = __builtin_bswap32(st[i]);
+}
+
+hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
+                      const BlockState *bst, int cap_blk, uint32_t *digests, hipStream_t st)
+{
+    dim3 g((cap_blk + 255) / 256, nblocks);
+    if (hasher == 0) hipLaunchKernelGGL(sha_kernel<5>, g, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, digests);
+    else hipLaunchKernelGGL(sha_kernel<7>, g, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, digests);
+    return hipGetLastError();
+}
+
+}  // namespace hdrf

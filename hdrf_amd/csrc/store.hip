@@ -1,0 +1,292 @@
+// store.hip — container placement, gather and index finalisation on gfx950.
+//
+// Reference: threadedStorer.run, DN/DataDeduplicator.java:702-836 (driver storeChunksMT
+// :511-532).  Storer t owns chunk range [n*t/3, n*(t+1)/3) (1 range when n < 25) and the
+// container lastBlockID[t]; it appends each NEW chunk at curPos, and when
+// curPos + len > maxSize it closes the container (rewritten whole, :748-786), bumps the id and
+// restarts at 0 (:790-796).  The open container's tail is appended raw (:806-818) and
+// lastBlockID[t+4] = bytes appended by this block since its last flush (:808).  A block with
+// storeSize == 0 touches no container (:713-719).
+//
+// Because every storer t only ever appends to its own container chain, the placement of all
+// new chunks of a batch is a prefix sum per range plus a short sequential walk over the
+// flush points (each found with a 64-ary search over the prefix array):
+//   tile_scan   — per block: exclusive scan of the per-tile new-byte sums (from decide)
+//   chunk_scan  — per chunk: inclusive prefix of new bytes within its block
+//   flush       — one wave per range t walks the batch's blocks in order, finds flushes
+//   place       — per chunk: container id / position; wave-cooperative copy into the arena;
+//                 the designated chunk of each touched index entry writes its final value.
+#include "launchers.hpp"
+
+namespace hdrf {
+
+
+__device__ __forceinline__ void range_bounds(int n, int t, int n_thread, int min_mt, int &c0, int &c1, int &nT)
+{
+    nT = n < min_mt ? 1 : n_thread;
+    c0 = (int)((long long)n * t / nT);
+    c1 = (int)((long long)n * (t + 1) / nT);
+}
+
+// ---- tile_scan: grid nblocks, 256 threads ------------------------------------------------
+__global__ void __launch_bounds__(256) tile_scan_kernel(const BlockState *__restrict__ bst, int ntiles,
+                                                        const uint32_t *__restrict__ tilesum,
+                                                        uint32_t *__restrict__ tilepre, uint64_t *__restrict__ store_size,
+                                                        int cap_blk)
+{
+    __shared__ uint32_t s[256];
+    const int b = blockIdx.x;
+    const int used = (bst[b].n_chunks + 255) / 256;
+    uint32_t carry = 0;
+    for (int base = 0; base < used; base += 256) {
+        const int i = base + threadIdx.x;
+        const uint32_t v = i < used ? tilesum[(size_t)b * ntiles + i] : 0u;
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (int d = 1; d < 256; d <<= 1) {
+            uint32_t t = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0u;
+            __syncthreads();
+            s[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < used) tilepre[(size_t)b * ntiles + i] = carry + s[threadIdx.x] - v;
+        carry += s[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) store_size[b] = carry;
+}
+
+// ---- chunk_scan: grid (ntiles, nblocks) --------------------------------------------------
+__global__ void __launch_bounds__(256) chunk_scan_kernel(const BlockState *__restrict__ bst, int cap_blk, int ntiles,
+                                                         const uint32_t *__restrict__ offsets,
+                                                         const uint8_t *__restrict__ flags,
+                                                         const uint32_t *__restrict__ tilepre, uint32_t *__restrict__ pre)
+{
+    __shared__ uint32_t s_w[4];
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int n = bst[b].n_chunks;
+    if (blockIdx.x * 256 >= n) return;
+    const size_t c = (size_t)b * cap_blk + k;
+    uint32_t v = 0;
+    if (k < n && (flags[c] & 1)) {
+        const uint32_t *off = offsets + (size_t)b * cap_blk;
+        v = off[k] - (k ? off[k - 1] : 0u);
+    }
+    uint32_t incl = wave_incl_scan(v);
+    if (lane_id() == 63) s_w[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    const int wv = threadIdx.x >> 6;
+    uint32_t add = tilepre[(size_t)b * ntiles + blockIdx.x];
+    for (int i = 0; i < wv; i++) add += s_w[i];
+    if (k < n) pre[c] = incl + add;
+}
+
+// first index c in [lo, hi) with pre[c] > thr (exists by construction); one wave, uniform
+__device__ int wave_first_gt(const uint32_t *pre, int lo, int hi, uint64_t thr)
+{
+    const int l = lane_id();
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 63) / 64;
+        const int p = min(lo + (l + 1) * step - 1, hi - 1);
+        const bool ok = (uint64_t)pre[p] > thr;
+        const unsigned long long bal = ballot64(ok);
+        const int j = __builtin_ctzll(bal);          // bal != 0: pre[hi-1] > thr
+        const int nlo = lo + j * step;
+        hi = min(lo + (j + 1) * step, hi);
+        lo = nlo;
+    }
+    const bool ok = (lo + l < hi) && (uint64_t)pre[lo + l] > thr;
+    const unsigned long long bal = ballot64(ok);
+    return lo + __builtin_ctzll(bal);
+}
+
+// ---- flush: one workgroup, wave t handles range t ---------------------------------------
+__global__ void __launch_bounds__(256) flush_kernel(StoreParams P, const BlockState *__restrict__ bst,
+                                                    const uint64_t *__restrict__ store_size,
+                                                    const uint32_t *__restrict__ pre, AllocState *__restrict__ alloc,
+                                                    RangeState *__restrict__ rstate, FlushEv *__restrict__ events,
+                                                    ClosedRec *__restrict__ closed, uint32_t *__restrict__ nclosed,
+                                                    int *__restrict__ err)
+{
+    const int t = threadIdx.x >> 6;
+    if (t >= P.n_thread) return;
+    const int l = lane_id();
+    // per-lane prefetch of block-level quantities (lane = block, up to 64)
+    int n_l = 0, c0_l = 0, c1_l = 0, act_l = 0;
+    uint32_t base_l = 0, S_l = 0;
+    if (l < P.nblocks) {
+        n_l = bst[l].n_chunks;
+        int nT;
+        range_bounds(n_l, t, P.n_thread, P.min_mt, c0_l, c1_l, nT);
+        act_l = (store_size[l] != 0 && t < nT) ? 1 : 0;
+        const uint32_t *pb = pre + (size_t)l * P.cap_blk;
+        base_l = c0_l > 0 ? pb[c0_l - 1] : 0u;
+        S_l = (act_l && c1_l > c0_l) ? pb[c1_l - 1] - base_l : 0u;
+    }
+    uint32_t id = alloc->id[t], cur = alloc->cur[t], slot = alloc->slot[t], exists = alloc->exists[t];
+    uint32_t pos = alloc->pos[t];
+    int nev = 0;
+    FlushEv *ev = events + (size_t)t * P.ev_cap;
+    for (int b = 0; b < P.nblocks; b++) {
+        const int act = rdlane(act_l, b);
+        RangeState rs;
+        rs.c_begin = (int)rdlane(c0_l, b);
+        rs.c_end = (int)rdlane(c1_l, b);
+        rs.base = rdlane(base_l, b);
+        rs.active = act;
+        rs.ev_begin = nev;
+        rs.nflush = 0;
+        rs.id0 = id; rs.slot0 = slot; rs.cur0 = cur;
+        rs.total = 0;
+        if (act) {
+            if (!exists) { cur = 0; exists = 1; rs.cur0 = 0; }     // createNewFile (:726,736)
+            const uint32_t S = rdlane(S_l, b);
+            rs.total = S;
+            int64_t cs = -(int64_t)cur;                              // container start, range-relative
+            const uint32_t *pb = pre + (size_t)b * P.cap_blk;
+            for (int guard = 0; (int64_t)S - cs > (int64_t)P.cmax; guard++) {
+                if (guard > P.ev_cap) { if (l == 0) atomicOr(err, 8); break; }
+                const uint64_t thr = (uint64_t)((int64_t)rs.base + cs + (int64_t)P.cmax);
+                const int c = wave_first_gt(pb, rs.c_begin, rs.c_end, thr);
+                const uint32_t X0 = (c > rs.c_begin ? pb[c - 1] : rs.base) - rs.base;
+                if (l == 0) {
+                    uint32_t ci = atomicAdd(nclosed, 1u);
+                    if ((int)ci < P.closed_cap) {
+                        ClosedRec cr; cr.id = id; cr.slot = slot; cr.len = (uint32_t)((int64_t)X0 - cs); cr.range = t;
+                        closed[ci] = cr;
+                    }
+                }
+                id = id + 1;
+                // range t owns arena slots [t*per, (t+1)*per): a ring whose newest slot is its
+                // open container, so recycling only ever overwrites t's oldest closed ones
+                const uint32_t per = P.nslots / 4, base = (uint32_t)t * per;
+                slot = base + (slot - base + 1) % per;
+                cs = X0;
+                if (nev < P.ev_cap) {
+                    if (l == 0) { FlushEv e; e.chunk = c; e.new_id = id; e.new_slot = slot; e.base = X0; ev[nev] = e; }
+                } else if (l == 0) atomicOr(err, 8);
+                nev++;
+                rs.nflush++;
+            }
+            cur = (uint32_t)((int64_t)S - cs);
+            pos = (uint32_t)((int64_t)S - (cs > 0 ? cs : 0));      // lastBlockID[t+4] (:808)
+        }
+        if (l == 0) rstate[(size_t)b * 4 + t] = rs;
+    }
+    if (l == 0) {
+        alloc->id[t] = id; alloc->cur[t] = cur; alloc->slot[t] = slot; alloc->exists[t] = exists; alloc->pos[t] = pos;
+    }
+}
+
+// wave-cooperative unaligned copy (4-B words, src realigned with v_alignbyte)
+__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, int len)
+{
+    const int l = lane_id();
+    int h = (int)((4 - ((uintptr_t)dst & 3)) & 3);
+    if (h > len) h = len;
+    if (l < h) dst[l] = src[l];
+    const int body = (len - h) >> 2;
+    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + h);
+    const uintptr_t sa = (uintptr_t)(src + h);
+    const int sh = (int)(sa & 3);
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+    if (sh == 0) {
+        for (int i = l; i < body; i += 64) dw[i] = sw[i];
+    } else {
+        for (int i = l; i < body; i += 64) dw[i] = __builtin_amdgcn_alignbyte(sw[i + 1], sw[i], sh);
+    }
+    const int tb = h + (body << 2);
+    const int tail = len - tb;
+    if (l < tail) dst[tb + l] = src[tb + l];
+}
+
+// ---- place: grid (ntiles, nblocks) ------------------------------------------------------
+__global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDesc *__restrict__ blocks,
+                                                    const BlockState *__restrict__ bst,
+                                                    const uint32_t *__restrict__ offsets,
+                                                    const uint8_t *__restrict__ flags, const uint32_t *__restrict__ pre,
+                                                    const RangeState *__restrict__ rstate,
+                                                    const FlushEv *__restrict__ events, const uint32_t *__restrict__ slot,
+                                                    IndexEntry *__restrict__ tab, uint8_t *__restrict__ arena,
+                                                    uint32_t *__restrict__ place_cid, uint32_t *__restrict__ place_pos)
+{
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int n = bst[b].n_chunks;
+    if (blockIdx.x * 256 >= n) return;
+    const BlockDesc bd = blocks[b];
+    const size_t c = (size_t)b * P.cap_blk + k;
+    const uint32_t *off = offsets + (size_t)b * P.cap_blk;
+    uint8_t f = 0;
+    uint32_t start = 0, len = 0, cid = 0, pos = 0, aslot = 0;
+    bool do_copy = false;
+    if (k < n) {
+        f = flags[c];
+        start = k ? off[k - 1] : 0u;
+        len = off[k] - start;
+        if (f & 1) {
+            int c0, c1, nT, t = 0;
+            for (int tt = 0; tt < 3; tt++) {
+                range_bounds(n, tt, P.n_thread, P.min_mt, c0, c1, nT);
+                if (tt < nT && k >= c0 && k < c1) { t = tt; break; }
+            }
+            const RangeState rs = rstate[(size_t)b * 4 + t];
+            if (rs.active) {
+                const uint32_t X0 = pre[c] - len - rs.base;
+                cid = rs.id0; aslot = rs.slot0;
+                int64_t cs = -(int64_t)rs.cur0;
+                const FlushEv *ev = events + (size_t)t * P.ev_cap + rs.ev_begin;
+                for (int i = 0; i < rs.nflush; i++) {      // few events per (block, range)
+                    const FlushEv e = ev[i];
+                    if (e.chunk > k) break;
+                    cid = e.new_id; aslot = e.new_slot; cs = e.base;
+                }
+                pos = (uint32_t)((int64_t)X0 - cs);
+                do_copy = len > 0;
+            }
+            place_cid[c] = cid;
+            place_pos[c] = pos;
+        }
+        if (f & 2) {                                       // designated: final index value
+            IndexEntry *e = tab + slot[c];
+            const unsigned long long m = e->mask;
+            const uint32_t cnt = (uint32_t)__popcll(m);
+            if (f & 4) {
+                e->ncopy = cnt & 0xffu;
+                e->cid = cid; e->start = pos; e->stop = pos + ((f & 1) && do_copy ? len : 0u);
+            } else {
+                e->ncopy = (e->ncopy + cnt) & 0xffu;
+            }
+            e->mask = 0;
+            e->first = 0;
+        }
+    }
+    // cooperative copy of this wave's new chunks
+    unsigned long long todo = ballot64(do_copy);
+    while (todo) {
+        const int j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint32_t js = rdlane(start, j), jl = rdlane(len, j), jp = rdlane(pos, j), jslot = rdlane(aslot, j);
+        wave_copy(arena + (size_t)jslot * P.cmax + jp, bd.data + js, (int)jl);
+    }
+}
+
+hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
+                        const uint32_t *offsets, const uint8_t *flags, const uint32_t *tilesum, uint32_t *tilepre,
+                        uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
+                        ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
+                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st)
+{
+    dim3 g(P.ntiles, P.nblocks);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(P.nblocks), dim3(256), 0, st, bst, P.ntiles, tilesum, tilepre,
+                       store_size, P.cap_blk);
+    hipLaunchKernelGGL(chunk_scan_kernel, g, dim3(256), 0, st, bst, P.cap_blk, P.ntiles, offsets, flags, tilepre, pre);
+    hipLaunchKernelGGL(flush_kernel, dim3(1), dim3(256), 0, st, P, bst, store_size, pre, alloc, rstate, events, closed,
+                       nclosed, err);
+    hipLaunchKernelGGL(place_kernel, g, dim3(256), 0, st, P, d_blocks, bst, offsets, flags, pre, rstate, events, slot,
+                       tab, arena, place_cid, place_pos);
+    return hipGetLastError();
+}
+
+}  // namespace hdrf

@@ -1,0 +1,294 @@
+"""ctypes binding of libhdrf.so (include/hdrf.h) — the product path.
+
+There is no CPU fallback: if the HIP library is missing or no GPU is present the calls
+raise.  `build()` compiles the library in-tree for gfx950.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libhdrf.so")
+
+HDRF_ERRORS = {
+    -1: "HDRF_E_INVAL", -2: "HDRF_E_HIP", -3: "HDRF_E_NOMEM", -4: "HDRF_E_CAPACITY",
+    -5: "HDRF_E_NOTFOUND", -6: "HDRF_E_UNSUPPORTED", -7: "HDRF_E_DEVICE",
+}
+
+# every symbol include/hdrf.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "hdrf_default_cfg", "hdrf_open", "hdrf_close", "hdrf_last_error", "hdrf_digest_len",
+    "hdrf_reduce_block", "hdrf_reduce_batch", "hdrf_batch_info", "hdrf_batch_offsets",
+    "hdrf_batch_digests", "hdrf_batch_is_new", "hdrf_batch_placement", "hdrf_index_get",
+    "hdrf_index_count", "hdrf_index_dump", "hdrf_allocator", "hdrf_recipe_get", "hdrf_block_length",
+    "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
+    "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_stage_times", "hdrf_reset",
+]
+
+
+class HdrfError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{HDRF_ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("hasher", ctypes.c_int32), ("compressor", ctypes.c_int32), ("window", ctypes.c_int32),
+        ("max_chunk", ctypes.c_int32), ("n_thread", ctypes.c_int32), ("min_mt_chunks", ctypes.c_int32),
+        ("container_max", ctypes.c_uint32), ("device", ctypes.c_int32), ("max_block_bytes", ctypes.c_int64),
+        ("max_batch_blocks", ctypes.c_int32), ("index_log2", ctypes.c_int32), ("arena_slots", ctypes.c_int64),
+        ("segment_bytes", ctypes.c_int32), ("keep_recipes", ctypes.c_int32), ("timing", ctypes.c_int32),
+    ]
+
+
+class BlockResult(ctypes.Structure):
+    _fields_ = [
+        ("n_chunks", ctypes.c_int64), ("store_size", ctypes.c_int64), ("capacity", ctypes.c_int64),
+        ("offsets", ctypes.POINTER(ctypes.c_uint32)), ("digests", ctypes.POINTER(ctypes.c_uint8)),
+        ("is_new", ctypes.POINTER(ctypes.c_uint8)), ("container_id", ctypes.POINTER(ctypes.c_uint32)),
+        ("container_pos", ctypes.POINTER(ctypes.c_uint32)),
+    ]
+
+
+def build(verbose=False):
+    """Compile libhdrf.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    r = subprocess.run(["make", "-s", "-j8", "-C", _HERE], capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("libhdrf build failed:\n" + (r.stdout or "") + (r.stderr or ""))
+    return LIB_PATH
+
+
+_lib = None
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+
+
+def load():
+    """Load libhdrf.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libhdrf.so not built at {LIB_PATH}: run hdrf_amd.lib.build() "
+                           "(the HIP extension is required; there is no CPU path)")
+    L = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "hdrf_default_cfg": (ctypes.c_int, [ctypes.POINTER(Config)]),
+        "hdrf_open": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.POINTER(_vp)]),
+        "hdrf_close": (ctypes.c_int, [_vp]),
+        "hdrf_last_error": (ctypes.c_char_p, [_vp]),
+        "hdrf_digest_len": (ctypes.c_int, [_vp]),
+        "hdrf_reduce_block": (ctypes.c_int, [_vp, ctypes.c_uint64, _u8p, ctypes.c_uint64, ctypes.POINTER(BlockResult)]),
+        "hdrf_reduce_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
+        "hdrf_batch_info": (ctypes.c_int, [_vp, ctypes.c_int32, _i64p, _i64p]),
+        "hdrf_batch_offsets": (ctypes.c_int, [_vp, ctypes.c_int32, _u32p, ctypes.c_int64]),
+        "hdrf_batch_digests": (ctypes.c_int, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64]),
+        "hdrf_batch_is_new": (ctypes.c_int, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64]),
+        "hdrf_batch_placement": (ctypes.c_int, [_vp, ctypes.c_int32, _u32p, _u32p, ctypes.c_int64]),
+        "hdrf_index_get": (ctypes.c_int, [_vp, _u8p, _u8p]),
+        "hdrf_index_count": (ctypes.c_int64, [_vp]),
+        "hdrf_index_dump": (ctypes.c_int64, [_vp, _u8p, _u8p, ctypes.c_int64]),
+        "hdrf_allocator": (ctypes.c_int, [_vp, _u8p]),
+        "hdrf_recipe_get": (ctypes.c_int64, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
+        "hdrf_block_length": (ctypes.c_int64, [_vp, ctypes.c_uint64]),
+        "hdrf_container_read": (ctypes.c_int64, [_vp, ctypes.c_uint32, _u8p, ctypes.c_int64,
+                                                 ctypes.POINTER(ctypes.c_int32)]),
+        "hdrf_dev_alloc": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),
+        "hdrf_dev_free": (ctypes.c_int, [_vp, _vp]),
+        "hdrf_memcpy_h2d": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64]),
+        "hdrf_memcpy_d2h": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64]),
+        "hdrf_synchronize": (ctypes.c_int, [_vp]),
+        "hdrf_corpus_fill": (ctypes.c_int, [_vp, _vp, _u32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.c_uint64]),
+        "hdrf_stage_times": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int32]),
+        "hdrf_reset": (ctypes.c_int, [_vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def default_config(**kw):
+    cfg = Config()
+    load().hdrf_default_cfg(ctypes.byref(cfg))
+    for k, v in kw.items():
+        if not hasattr(cfg, k):
+            raise KeyError(k)
+        setattr(cfg, k, v)
+    return cfg
+
+
+def _p(a, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+def _u8(data):
+    if isinstance(data, (bytes, bytearray, memoryview)):
+        return np.frombuffer(data, dtype=np.uint8)
+    return np.ascontiguousarray(data, dtype=np.uint8)
+
+
+class Context:
+    """One DataNode's reduction state on one GPU (index, containers, allocator, recipes)."""
+
+    def __init__(self, cfg=None, **kw):
+        self.L = load()
+        self.cfg = cfg if cfg is not None else default_config(**kw)
+        h = _vp()
+        rc = self.L.hdrf_open(ctypes.byref(self.cfg), ctypes.byref(h))
+        if rc != 0:
+            raise HdrfError(rc, "hdrf_open failed")
+        self._h = h
+        self.H = self.L.hdrf_digest_len(h)
+
+    def _ck(self, rc):
+        if rc < 0:
+            raise HdrfError(rc, self.L.hdrf_last_error(self._h).decode())
+        return rc
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.L.hdrf_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- write path ---------------------------------------------------------------------
+    def reduce_block(self, data, block_id):
+        a = _u8(data)
+        buf = a if a.size else np.zeros(1, np.uint8)
+        cap = a.size // (self.cfg.window + 2) + 2
+        offs = np.zeros(cap, np.uint32)
+        digs = np.zeros(cap * self.H, np.uint8)
+        isnew = np.zeros(cap, np.uint8)
+        cid = np.zeros(cap, np.uint32)
+        pos = np.zeros(cap, np.uint32)
+        r = BlockResult(0, 0, cap, _p(offs, _u32p), _p(digs), _p(isnew), _p(cid, _u32p), _p(pos, _u32p))
+        self._ck(self.L.hdrf_reduce_block(self._h, block_id, _p(buf), a.size, ctypes.byref(r)))
+        n = r.n_chunks
+        return {"offsets": offs[:n].copy(), "digests": digs[:n * self.H].reshape(n, self.H).copy(),
+                "is_new": isnew[:n].copy(), "container_id": cid[:n].copy(), "container_pos": pos[:n].copy(),
+                "store_size": r.store_size}
+
+    def reduce_batch(self, dev_ptrs, lens, readable, block_ids):
+        n = len(dev_ptrs)
+        ptrs = (_vp * n)(*dev_ptrs)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        rd = np.ascontiguousarray(readable, np.uint64)
+        ids = np.ascontiguousarray(block_ids, np.uint64)
+        self._ck(self.L.hdrf_reduce_batch(self._h, n, ptrs, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p)))
+
+    def batch_info(self, b):
+        n, s = ctypes.c_int64(), ctypes.c_int64()
+        self._ck(self.L.hdrf_batch_info(self._h, b, ctypes.byref(n), ctypes.byref(s)))
+        return n.value, s.value
+
+    def batch_result(self, b):
+        n, ss = self.batch_info(b)
+        offs = np.zeros(max(n, 1), np.uint32)
+        digs = np.zeros(max(n, 1) * self.H, np.uint8)
+        isnew = np.zeros(max(n, 1), np.uint8)
+        cid = np.zeros(max(n, 1), np.uint32)
+        pos = np.zeros(max(n, 1), np.uint32)
+        self._ck(self.L.hdrf_batch_offsets(self._h, b, _p(offs, _u32p), n))
+        self._ck(self.L.hdrf_batch_digests(self._h, b, _p(digs), n * self.H))
+        self._ck(self.L.hdrf_batch_is_new(self._h, b, _p(isnew), n))
+        self._ck(self.L.hdrf_batch_placement(self._h, b, _p(cid, _u32p), _p(pos, _u32p), n))
+        return {"offsets": offs[:n], "digests": digs[:n * self.H].reshape(n, self.H), "is_new": isnew[:n],
+                "container_id": cid[:n], "container_pos": pos[:n], "store_size": ss}
+
+    # ---- Redis / chunkDir views ---------------------------------------------------------
+    def index_get(self, digest):
+        d = np.frombuffer(bytes(digest), np.uint8).copy()
+        out = np.zeros(11, np.uint8)
+        return out.tobytes() if self._ck(self.L.hdrf_index_get(self._h, _p(d), _p(out))) else None
+
+    def index_count(self):
+        return self._ck(self.L.hdrf_index_count(self._h))
+
+    def index_dump(self):
+        cnt = self.index_count()
+        keys = np.zeros(max(cnt, 1) * self.H, np.uint8)
+        vals = np.zeros(max(cnt, 1) * 11, np.uint8)
+        n = self._ck(self.L.hdrf_index_dump(self._h, _p(keys), _p(vals), cnt))
+        return keys[:n * self.H].reshape(n, self.H), vals[:n * 11].reshape(n, 11)
+
+    def allocator(self):
+        out = np.zeros(24, np.uint8)
+        return out.tobytes() if self._ck(self.L.hdrf_allocator(self._h, _p(out))) else None
+
+    def recipe(self, block_id):
+        n = self.L.hdrf_recipe_get(self._h, block_id, None, 0)
+        if n == 0:
+            return None
+        if n != -4:
+            self._ck(n)
+        need = 4 + self.H * (2 + int(self.cfg.max_block_bytes) // (self.cfg.window + 2))
+        out = np.zeros(need, np.uint8)
+        m = self._ck(self.L.hdrf_recipe_get(self._h, block_id, _p(out), need))
+        return out[:m].tobytes()
+
+    def block_length(self, block_id):
+        return self._ck(self.L.hdrf_block_length(self._h, block_id))
+
+    def container(self, cid):
+        closed = ctypes.c_int32(0)
+        n = self.L.hdrf_container_read(self._h, cid, None, 0, ctypes.byref(closed))
+        if n == -5:
+            return None, False
+        self._ck(n)
+        out = np.zeros(max(n, 1), np.uint8)
+        m = self._ck(self.L.hdrf_container_read(self._h, cid, _p(out), n, ctypes.byref(closed)))
+        return out[:m].tobytes(), bool(closed.value)
+
+    # ---- device memory / corpus / timing ------------------------------------------------
+    def dev_alloc(self, nbytes):
+        p = _vp()
+        self._ck(self.L.hdrf_dev_alloc(self._h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def dev_free(self, p):
+        self._ck(self.L.hdrf_dev_free(self._h, p))
+
+    def h2d(self, dev, data):
+        a = _u8(data)
+        self._ck(self.L.hdrf_memcpy_h2d(self._h, dev, a.ctypes.data, a.size))
+
+    def d2h(self, dev, nbytes):
+        out = np.zeros(nbytes, np.uint8)
+        self._ck(self.L.hdrf_memcpy_d2h(self._h, out.ctypes.data, dev, nbytes))
+        return out
+
+    def corpus_fill(self, dev, roots, nblocks, segs_per_block, seg_bytes, seed):
+        r = np.ascontiguousarray(roots, np.uint32)
+        self._ck(self.L.hdrf_corpus_fill(self._h, dev, _p(r, _u32p), nblocks, segs_per_block, seg_bytes, seed))
+
+    def synchronize(self):
+        self._ck(self.L.hdrf_synchronize(self._h))
+
+    def stage_times(self, reset=False):
+        out = (ctypes.c_double * 4)()
+        self._ck(self.L.hdrf_stage_times(self._h, out, 4, 1 if reset else 0))
+        return list(out)
+
+    def reset(self):
+        self._ck(self.L.hdrf_reset(self._h))

@@ -1,0 +1,130 @@
+/*
+ * hdrf.h — C-ABI of libhdrf, the MI355X (gfx950) reduction backend for HDRF's
+ * per-block write path (chunk -> fingerprint -> index -> container store).
+ *
+ * This is the drop-in boundary a DataNode binds through JNI.  Every
+ * entry point replaces a piece of the reference's Java path; `DN/` abbreviates
+ * hadoop-hdfs/src/main/java/org/apache/hadoop/hdfs/server/datanode/ in /root/reference.
+ *
+ * Conventions: plain pointers and sizes only; every function returns 0 on success or a
+ * negative HDRF_E* code; hdrf_last_error() describes the last failure of a context; no C++
+ * exception crosses this ABI.  A context is bound to one GPU and is NOT thread-safe: the
+ * reference serialises reductions through its FIFO (DN/DataDeduplicator.java:124-158,
+ * 197-204) and callers do the same (one context per DataNode, calls in block order).
+ */
+#ifndef HDRF_H
+#define HDRF_H
+#include <stdint.h>
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDRF_OK 0
+#define HDRF_E_INVAL (-1)      /* bad argument / configuration */
+#define HDRF_E_HIP (-2)        /* HIP runtime failure */
+#define HDRF_E_NOMEM (-3)      /* device or host allocation failed */
+#define HDRF_E_CAPACITY (-4)   /* index table, arena or event list full */
+#define HDRF_E_NOTFOUND (-5)   /* key / block / container absent */
+#define HDRF_E_UNSUPPORTED (-6)/* option not implemented in this build */
+#define HDRF_E_DEVICE (-7)     /* a kernel reported an inconsistency */
+
+typedef struct hdrf_ctx hdrf_ctx;
+
+/* Knobs of the reference, all compile-time statics there. */
+typedef struct {
+    int32_t hasher;          /* 0 SHA-1, 1 SHA-224          DataNode.hasher, DN/DataNode.java:446 */
+    int32_t compressor;      /* 1 dedup only (2 = +LZ4: not yet)   DataNode.compressor :438 */
+    int32_t window;          /* 700                         DataDeduplicator.chunking :266 */
+    int32_t max_chunk;       /* 1000000                     DataDeduplicator.chunking :272 */
+    int32_t n_thread;        /* 3                           DataDeduplicator.nThread :93 */
+    int32_t min_mt_chunks;   /* 25                          DataDeduplicator :316, :514 */
+    uint32_t container_max;  /* 2^25                        DataNode.maxSize :434 -> DataDeduplicator.maxSize */
+    int32_t device;          /* HIP device ordinal */
+    int64_t max_block_bytes; /* largest block (dfs.blocksize, 128 MiB) */
+    int32_t max_batch_blocks;/* <= 64 blocks per hdrf_reduce_batch call */
+    int32_t index_log2;      /* index table capacity = 2^index_log2 entries (64 B each) */
+    int64_t arena_slots;     /* container arena slots of container_max bytes each */
+    int32_t segment_bytes;   /* chunking speculation segment (default 1 MiB) */
+    int32_t keep_recipes;    /* keep recipes (SET blockId -> size|digests) on the host */
+    int32_t timing;          /* record per-stage HIP events */
+} hdrf_cfg;
+
+/* Per-block result of hdrf_reduce_block (caller-owned host arrays; NULL to skip). */
+typedef struct {
+    int64_t n_chunks;        /* out */
+    int64_t store_size;      /* out: bytes of new chunks (DataDeduplicator.storeSize :91,355) */
+    int64_t capacity;        /* in: entries available in the arrays below */
+    uint32_t *offsets;       /* chunk END offsets (DataDeduplicator.chunking :264-307) */
+    uint8_t *digests;        /* n * H bytes (threadedHasher :578-641) */
+    uint8_t *is_new;         /* chunkMeta.newChunk (DN/chunkMeta.java:35-60) */
+    uint32_t *container_id;  /* new chunks: chunkMeta.blockID (:799) */
+    uint32_t *container_pos; /* new chunks: chunkMeta.blockStart (:800) */
+} hdrf_block_result;
+
+int hdrf_default_cfg(hdrf_cfg *cfg);
+/* DataNode.initializeDD (DN/DataNode.java:486-534) + JedisPool("localhost") (DN/DataDeduplicator.java:119) */
+int hdrf_open(const hdrf_cfg *cfg, hdrf_ctx **out);
+int hdrf_close(hdrf_ctx *ctx);
+const char *hdrf_last_error(const hdrf_ctx *ctx);
+int hdrf_digest_len(const hdrf_ctx *ctx);              /* DataNode.hash_length (:528-532) */
+
+/* Write path, one block from host memory: replaces `new DataDeduplicator(bf1, blockId)`
+ * launched by DDRunner (DN/DDRunner.java:26-36, DN/BlockReceiver.java:1258-1261).
+ * Copies H2D, reduces, updates the index / containers / recipe / allocator. */
+int hdrf_reduce_block(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *data, uint64_t len,
+                      hdrf_block_result *out);
+
+/* Write path, a batch of device-resident blocks in arrival order (the FIFO order of
+ * DN/DataDeduplicator.java:124-158).  data[i] must stay valid until the call returns and
+ * provide readable[i] >= len[i] + 64 bytes.  Results of the batch stay on the device until
+ * the next reduce call and are read with hdrf_batch_*. */
+int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                      const uint64_t *readable, const uint64_t *block_ids);
+
+int hdrf_batch_info(hdrf_ctx *ctx, int32_t b, int64_t *n_chunks, int64_t *store_size);
+int hdrf_batch_offsets(hdrf_ctx *ctx, int32_t b, uint32_t *out, int64_t cap);
+int hdrf_batch_digests(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap_bytes);
+int hdrf_batch_is_new(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap);
+int hdrf_batch_placement(hdrf_ctx *ctx, int32_t b, uint32_t *cid, uint32_t *pos, int64_t cap);
+
+/* Index (Redis) views. GET digest -> 11-byte chunkMeta value (DN/chunkMeta.java:62-77).
+ * Returns 1 if found, 0 if absent, <0 on error. */
+int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out11[11]);
+int64_t hdrf_index_count(hdrf_ctx *ctx);
+/* All (digest, value) pairs sorted by digest; returns count (or HDRF_E_CAPACITY). */
+int64_t hdrf_index_dump(hdrf_ctx *ctx, uint8_t *keys, uint8_t *vals, int64_t cap);
+/* GET "blockID": 24-byte allocator (utilities.blockIDtoBytes, DN/utilities.java:66-75).
+ * Returns 1 if the key exists (a block was reduced), 0 otherwise. */
+int hdrf_allocator(hdrf_ctx *ctx, uint8_t out24[24]);
+/* GET longToBytes(blockId,4): recipe [BE32 size | digests] (DataDeduplicator.storeDB :372-392).
+ * Returns length, 0 if absent; HDRF_E_CAPACITY if cap is too small (needs keep_recipes). */
+int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap);
+/* FsDatasetImpl.getLength for 0-byte replicas (DN/fsdataset/impl/FsDatasetImpl.java:736-763). */
+int64_t hdrf_block_length(hdrf_ctx *ctx, uint64_t block_id);
+/* Container file chunkDir+id (raw bytes).  Returns length; *closed = 1 once it overflowed.
+ * HDRF_E_NOTFOUND if it never existed or its arena slot was recycled. */
+int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t cap, int32_t *closed);
+
+/* Device memory helpers for callers without their own allocator (bench, tests). */
+int hdrf_dev_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out);
+int hdrf_dev_free(hdrf_ctx *ctx, void *p);
+int hdrf_memcpy_h2d(hdrf_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int hdrf_memcpy_d2h(hdrf_ctx *ctx, void *dst, const void *src, uint64_t bytes);
+int hdrf_synchronize(hdrf_ctx *ctx);
+
+/* Synthetic corpus generator (BASELINE config 2; spec in DESIGN.md §Corpus):
+ * block b, segment s = splitmix64 words keyed by roots[b*segs_per_block+s]. */
+int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
+                     int64_t segs_per_block, int64_t seg_bytes, uint64_t seed);
+
+/* Per-stage device time (ms) accumulated since the last reset, measured with HIP events on
+ * the context's stream: [0] chunking, [1] fingerprint, [2] index, [3] store. */
+int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
+/* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis). */
+int hdrf_reset(hdrf_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,568 @@
+/*
+ * hdrf_oracle.c — CPU restatement of HDRF's per-block reduction path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see hdrf_oracle.h for the pinning status).
+ * Every function cites the reference lines it restates.  `DN/` abbreviates
+ * /root/reference/hadoop-hdfs/src/main/java/org/apache/hadoop/hdfs/server/datanode/.
+ *
+ * Redis (key/value server reached through Jedis 2.9.0, DN/DataDeduplicator.java:119)
+ * is restated as in-memory maps with GET/SET semantics; container files under
+ * DataNode.chunkDir are restated as in-memory byte vectors.
+ */
+#include "hdrf_oracle.h"
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* a1: DataDeduplicator.chunking — DN/DataDeduplicator.java:264-307 (literal transliteration). */
+int64_t hdrf_oracle_chunk(const uint8_t *data, int64_t size, uint32_t *out, int64_t out_cap)
+{
+    const int w = 700;                                   /* :266 */
+    const int mLength = 1000000;                         /* :272 */
+    int8_t mValue = size > 0 ? (int8_t)data[0] : 0;     /* :268  data.get(0) (a fresh direct buffer reads 0) */
+    int64_t mPos = w;                                    /* :269 */
+    int64_t count = -1;                                  /* :270 */
+    int64_t cLength = 0;                                 /* :271 */
+    /* offsetarray has capacity/w + 1 slots (:267); we keep every detected boundary. */
+    int64_t ocap = size / w + 2;
+    uint32_t *offsetarray = (uint32_t *)malloc((size_t)ocap * sizeof(uint32_t));
+    if (!offsetarray) return -2;
+    for (int64_t i = 0; i < size; i++) {                 /* :274 */
+        cLength++;                                       /* :275 */
+        int8_t b = (int8_t)data[i];
+        if (b >= mValue) {                               /* :276  signed Java byte compare */
+            if (i > mPos) {                              /* :277 */
+                count++;
+                offsetarray[count] = (uint32_t)(i + 1);  /* :279 */
+                mPos = i + w + 1;                        /* :280 */
+                mValue = 0;                              /* :281 */
+                cLength = 0;                             /* :282 */
+                continue;                                /* :283 */
+            } else {
+                mValue = b;                              /* :285 */
+            }
+        }
+        if (cLength > mLength) {                         /* :288-294 forced cut */
+            count++;
+            offsetarray[count] = (uint32_t)(i + 1);
+            mPos = i + w + 1;
+            mValue = 0;
+            cLength = 0;
+        }
+    }
+    /* :300-304 — the last detected boundary is dropped, then `size` is appended. */
+    int64_t n = (count > 0 ? count : 0) + 1;
+    if (n > out_cap) { free(offsetarray); return -1; }
+    for (int64_t i = 0; i < count; i++) out[i] = offsetarray[i];
+    out[n - 1] = (uint32_t)size;
+    free(offsetarray);
+    return n;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* a3: FIPS 180-4 SHA-1 and SHA-224 (utilities.sha1hash / sha224hash, DN/utilities.java:98-137;
+ * the native path is nayuki's sha1_compress_block / sha256_compress_block + standard padding). */
+static inline uint32_t rol32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static inline uint32_t ror32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+static inline uint32_t be32(const uint8_t *p)
+{
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+static void sha1_compress(uint32_t st[5], const uint8_t blk[64])
+{
+    uint32_t w[80];
+    for (int i = 0; i < 16; i++) w[i] = be32(blk + 4 * i);
+    for (int i = 16; i < 80; i++) w[i] = rol32(w[i - 3] ^ w[i - 8] ^ w[i - 14] ^ w[i - 16], 1);
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
+    for (int i = 0; i < 80; i++) {
+        uint32_t f, k;
+        if (i < 20)      { f = (b & c) | (~b & d);           k = 0x5A827999u; }
+        else if (i < 40) { f = b ^ c ^ d;                    k = 0x6ED9EBA1u; }
+        else if (i < 60) { f = (b & c) | (b & d) | (c & d);  k = 0x8F1BBCDCu; }
+        else             { f = b ^ c ^ d;                    k = 0xCA62C1D6u; }
+        uint32_t t = rol32(a, 5) + f + e + k + w[i];
+        e = d; d = c; c = rol32(b, 30); b = a; a = t;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e;
+}
+
+static const uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+static void sha256_compress(uint32_t st[8], const uint8_t blk[64])
+{
+    uint32_t w[64];
+    for (int i = 0; i < 16; i++) w[i] = be32(blk + 4 * i);
+    for (int i = 16; i < 64; i++) {
+        uint32_t s0 = ror32(w[i - 15], 7) ^ ror32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+        uint32_t s1 = ror32(w[i - 2], 17) ^ ror32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    for (int i = 0; i < 64; i++) {
+        uint32_t S1 = ror32(e, 6) ^ ror32(e, 11) ^ ror32(e, 25);
+        uint32_t ch = (e & f) ^ (~e & g);
+        uint32_t t1 = h + S1 + ch + K256[i] + w[i];
+        uint32_t S0 = ror32(a, 2) ^ ror32(a, 13) ^ ror32(a, 22);
+        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+        uint32_t t2 = S0 + mj;
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+/* Merkle–Damgård padding shared by both hashes: 0x80, zeros, 64-bit big-endian bit length. */
+static void md_hash(const uint8_t *msg, uint64_t len, uint32_t *st,
+                    void (*compress)(uint32_t *, const uint8_t *))
+{
+    uint64_t full = len / 64;
+    for (uint64_t i = 0; i < full; i++) compress(st, msg + 64 * i);
+    uint8_t tail[128];
+    uint64_t rem = len - 64 * full;
+    memset(tail, 0, sizeof tail);
+    if (rem) memcpy(tail, msg + 64 * full, (size_t)rem);
+    tail[rem] = 0x80;
+    uint64_t tl = (rem + 9 <= 64) ? 64 : 128;
+    uint64_t bits = len * 8;
+    for (int i = 0; i < 8; i++) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    compress(st, tail);
+    if (tl == 128) compress(st, tail + 64);
+}
+
+void hdrf_oracle_sha1(const uint8_t *msg, uint64_t len, uint8_t out[20])
+{
+    uint32_t st[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+    md_hash(msg, len, st, (void (*)(uint32_t *, const uint8_t *))sha1_compress);
+    for (int i = 0; i < 20; i++) out[i] = (uint8_t)(st[i / 4] >> (24 - 8 * (i % 4)));
+}
+
+void hdrf_oracle_sha224(const uint8_t *msg, uint64_t len, uint8_t out[28])
+{
+    uint32_t st[8] = {0xc1059ed8u, 0x367cd507u, 0x3070dd17u, 0xf70e5939u,
+                      0xffc00b31u, 0x68581511u, 0x64f98fa7u, 0xbefa4fa4u};
+    md_hash(msg, len, st, (void (*)(uint32_t *, const uint8_t *))sha256_compress);
+    for (int i = 0; i < 28; i++) out[i] = (uint8_t)(st[i / 4] >> (24 - 8 * (i % 4)));
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Redis restatement: a GET/SET map keyed by digest bytes (fixed length H) with 11-byte values. */
+typedef struct {
+    uint8_t *keys;    /* cap * H */
+    uint8_t *vals;    /* cap * 11 */
+    uint8_t *used;    /* cap */
+    int64_t cap, count;
+    int H;
+} kvmap;
+
+static uint64_t key_hash(const uint8_t *k, int H)
+{
+    uint64_t h = 1469598103934665603ull;
+    for (int i = 0; i < H; i++) { h ^= k[i]; h *= 1099511628211ull; }
+    return h ^ (h >> 29);
+}
+
+static int kv_init(kvmap *m, int H, int64_t cap)
+{
+    m->H = H; m->cap = cap; m->count = 0;
+    m->keys = (uint8_t *)calloc((size_t)cap, (size_t)H);
+    m->vals = (uint8_t *)calloc((size_t)cap, 11);
+    m->used = (uint8_t *)calloc((size_t)cap, 1);
+    return (m->keys && m->vals && m->used) ? 0 : -1;
+}
+
+static void kv_free(kvmap *m) { free(m->keys); free(m->vals); free(m->used); }
+
+static int64_t kv_find(const kvmap *m, const uint8_t *k)
+{
+    uint64_t i = key_hash(k, m->H) & (uint64_t)(m->cap - 1);
+    while (m->used[i]) {
+        if (memcmp(m->keys + i * m->H, k, (size_t)m->H) == 0) return (int64_t)i;
+        i = (i + 1) & (uint64_t)(m->cap - 1);
+    }
+    return -1 - (int64_t)i;
+}
+
+static int kv_set(kvmap *m, const uint8_t *k, const uint8_t *v11);
+
+static int kv_grow(kvmap *m)
+{
+    kvmap n;
+    if (kv_init(&n, m->H, m->cap * 2)) return -1;
+    for (int64_t i = 0; i < m->cap; i++)
+        if (m->used[i]) kv_set(&n, m->keys + i * m->H, m->vals + i * 11);
+    kv_free(m);
+    *m = n;
+    return 0;
+}
+
+static int kv_set(kvmap *m, const uint8_t *k, const uint8_t *v11)
+{
+    if ((m->count + 1) * 2 > m->cap && kv_grow(m)) return -1;
+    int64_t f = kv_find(m, k);
+    int64_t i = f >= 0 ? f : -1 - f;
+    if (f < 0) { m->used[i] = 1; memcpy(m->keys + i * m->H, k, (size_t)m->H); m->count++; }
+    memcpy(m->vals + i * 11, v11, 11);
+    return 0;
+}
+
+/* Container files (chunkDir + id): in-memory byte vectors keyed by 24-bit id. */
+typedef struct {
+    uint32_t id;
+    uint8_t *data;
+    int64_t len, cap;
+    int closed;
+} container;
+
+/* Recipes: SET longToBytes(blockId,4) -> [BE32 size | digests] (DataDeduplicator.storeDB :372-392). */
+typedef struct {
+    uint32_t key;
+    uint8_t *data;
+    int64_t len;
+} recipe;
+
+struct hdrf_oracle {
+    int hasher, compressor, H;
+    uint32_t max_size;
+    kvmap index;
+    int have_alloc;
+    uint8_t alloc[24];              /* Redis key "blockID" */
+    container *cont; int64_t ncont, ccap;
+    recipe *rec; int64_t nrec, rcap;
+};
+
+hdrf_oracle *hdrf_oracle_new(int hasher, int compressor, uint32_t max_size)
+{
+    if (hasher != 0 && hasher != 1) return NULL;
+    hdrf_oracle *o = (hdrf_oracle *)calloc(1, sizeof *o);
+    if (!o) return NULL;
+    o->hasher = hasher;
+    o->compressor = compressor;
+    o->H = hasher == 0 ? 20 : 28;                        /* DataNode.initializeDD :528-532 */
+    o->max_size = max_size;                              /* DataDeduplicator.maxSize = 2^25 :434,527 */
+    if (kv_init(&o->index, o->H, 1 << 16)) { free(o); return NULL; }
+    return o;
+}
+
+void hdrf_oracle_free(hdrf_oracle *o)
+{
+    if (!o) return;
+    kv_free(&o->index);
+    for (int64_t i = 0; i < o->ncont; i++) free(o->cont[i].data);
+    for (int64_t i = 0; i < o->nrec; i++) free(o->rec[i].data);
+    free(o->cont); free(o->rec); free(o);
+}
+
+static container *cont_find(hdrf_oracle *o, uint32_t id)
+{
+    for (int64_t i = o->ncont - 1; i >= 0; i--)
+        if (o->cont[i].id == id) return &o->cont[i];
+    return NULL;
+}
+
+static container *cont_create(hdrf_oracle *o, uint32_t id)
+{
+    if (o->ncont == o->ccap) {
+        o->ccap = o->ccap ? o->ccap * 2 : 16;
+        o->cont = (container *)realloc(o->cont, (size_t)o->ccap * sizeof(container));
+    }
+    container *c = &o->cont[o->ncont++];
+    memset(c, 0, sizeof *c);
+    c->id = id;
+    return c;
+}
+
+static void cont_append(container *c, const uint8_t *p, int64_t n)
+{
+    if (c->len + n > c->cap) {
+        int64_t nc = c->cap ? c->cap : 4096;
+        while (nc < c->len + n) nc *= 2;
+        c->data = (uint8_t *)realloc(c->data, (size_t)nc);
+        c->cap = nc;
+    }
+    memcpy(c->data + c->len, p, (size_t)n);
+    c->len += n;
+}
+
+/* chunkMeta — DN/chunkMeta.java:7-87 */
+typedef struct {
+    int newChunk;
+    int nCopy;
+    int64_t blockID;
+    int32_t blockStart, blockStop, bbStart, bbStop, length;
+} chunk_meta;
+
+/* chunkMeta.process(-1) — DN/chunkMeta.java:35-60 (decode an 11-byte Redis reply). */
+static void meta_process(chunk_meta *c, const uint8_t *v /* NULL = nil reply */)
+{
+    if (!v) { c->newChunk = 1; c->nCopy = 1; return; }
+    c->newChunk = 0;
+    c->nCopy = v[0] & 0xFF;
+    c->blockID = ((int64_t)v[1] << 16) | ((int64_t)v[2] << 8) | v[3];
+    c->blockStart = (int32_t)(((uint32_t)(v[10] & 0xF0) << 20) | ((uint32_t)v[4] << 16) | ((uint32_t)v[5] << 8) | v[6]);
+    c->blockStop = (int32_t)(((uint32_t)(v[10] & 0x0F) << 24) | ((uint32_t)v[7] << 16) | ((uint32_t)v[8] << 8) | v[9]);
+    c->length = c->blockStop - c->blockStart;
+    c->nCopy++;
+}
+
+/* chunkMeta.getMeta — DN/chunkMeta.java:62-77 (encode the 11-byte value). */
+static void meta_encode(const chunk_meta *c, uint8_t v[11])
+{
+    v[0] = (uint8_t)c->nCopy;
+    v[1] = (uint8_t)(c->blockID >> 16); v[2] = (uint8_t)(c->blockID >> 8); v[3] = (uint8_t)c->blockID;
+    v[4] = (uint8_t)(c->blockStart >> 16); v[5] = (uint8_t)(c->blockStart >> 8); v[6] = (uint8_t)c->blockStart;
+    v[7] = (uint8_t)(c->blockStop >> 16); v[8] = (uint8_t)(c->blockStop >> 8); v[9] = (uint8_t)c->blockStop;
+    v[10] = (uint8_t)(((c->blockStart >> 20) & 0xF0) | ((c->blockStop >> 24) & 0x0F));
+}
+
+/* utilities.bytesToBlockID / bytesToBlockPos — DN/utilities.java:36-65 */
+static int64_t bytes_to_slot(const uint8_t *b, int slot)
+{
+    return ((int64_t)b[slot * 3] << 16) | ((int64_t)b[slot * 3 + 1] << 8) | b[slot * 3 + 2];
+}
+
+/* DataDeduplicator(ByteBuffer, long) — DN/DataDeduplicator.java:108-217.
+ * Blocks are processed in call order (the FIFO AIWriteQueue, :124-158,197-204). */
+int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, int64_t block_id,
+                           int64_t cap, uint32_t *offsets_out, uint8_t *digests_out, uint8_t *is_new_out,
+                           uint8_t *values_out, int64_t *store_size_out)
+{
+    const int H = o->H;
+    /* :122 chunking */
+    int64_t ocap = size / 700 + 2;
+    uint32_t *off = (uint32_t *)malloc((size_t)ocap * sizeof(uint32_t));
+    if (!off) return -2;
+    int64_t n = hdrf_oracle_chunk(data, size, off, ocap);
+    if (n < 0 || n > cap) { free(off); return -1; }
+
+    /* :165-172 allocator: GET "blockID"; absent -> (t<<22, 0) */
+    int64_t lastBlockID[8];
+    for (int i = 0; i < 4; i++) {
+        lastBlockID[i] = o->have_alloc ? bytes_to_slot(o->alloc, i) : ((int64_t)i << 22);
+        lastBlockID[i + 4] = o->have_alloc ? bytes_to_slot(o->alloc, i + 4) : 0;
+    }
+
+    /* :174 chunkHash -> threadedHasher.run :578-641: hash every chunk, then the MULTI'd
+     * GETs are all answered before any of this block's SETs (storers start afterwards). */
+    chunk_meta *cm = (chunk_meta *)calloc((size_t)n, sizeof(chunk_meta));
+    uint8_t *dig = (uint8_t *)malloc((size_t)n * H + 1);
+    if (!cm || !dig) { free(off); free(cm); free(dig); return -2; }
+    int64_t cur = 0;
+    for (int64_t k = 0; k < n; k++) {
+        int64_t end = off[k];
+        if (o->hasher == 0) hdrf_oracle_sha1(data + cur, (uint64_t)(end - cur), dig + k * H);
+        else hdrf_oracle_sha224(data + cur, (uint64_t)(end - cur), dig + k * H);
+        cm[k].bbStart = (int32_t)cur; cm[k].bbStop = (int32_t)end; cm[k].length = (int32_t)(end - cur);
+        int64_t f = kv_find(&o->index, dig + k * H);
+        meta_process(&cm[k], f >= 0 ? o->index.vals + f * 11 : NULL);
+        cur = end;
+    }
+
+    /* :178 checkChunk :338-367 — identity-keyed HashMap: every chunk takes the else branch,
+     * so the only effect is storeSize = sum of new-chunk lengths. */
+    int64_t storeSize = 0;
+    for (int64_t k = 0; k < n; k++) if (cm[k].newChunk) storeSize += cm[k].length;
+
+    /* :184 storeChunksMT :511-532 -> threadedStorer.run :702-836 */
+    int nThread = n < 25 ? 1 : 3;
+    uint8_t *setv = (uint8_t *)malloc((size_t)n * 11 + 1);
+    for (int t = 0; t < nThread; t++) {
+        int64_t start = n * t / nThread, stop = n * (t + 1) / nThread;      /* :682-683 */
+        if (storeSize == 0) {                                               /* :713-719 */
+            for (int64_t k = start; k < stop; k++) meta_encode(&cm[k], setv + k * 11);
+            continue;
+        }
+        container *c = cont_find(o, (uint32_t)lastBlockID[t]);              /* :723-737 */
+        int64_t curPos;
+        if (c) curPos = c->len; else { c = cont_create(o, (uint32_t)lastBlockID[t]); curPos = 0; }
+        int64_t bufpos = 0;                                                 /* bufferBB.position() */
+        for (int64_t k = start; k < stop; k++) {
+            if (cm[k].newChunk) {
+                if (curPos + cm[k].length > (int64_t)o->max_size) {        /* :748 buffer full */
+                    c->closed = 1;                                          /* :754-786 rewrite prev||buf */
+                    bufpos = 0; curPos = 0;                                 /* :790-791 */
+                    lastBlockID[t]++;                                       /* :792 */
+                    lastBlockID[t + 4] = 0;                                 /* :793 */
+                    c = cont_find(o, (uint32_t)lastBlockID[t]);            /* :794-795 createNewFile */
+                    if (!c) c = cont_create(o, (uint32_t)lastBlockID[t]);
+                }
+                cont_append(c, data + cm[k].bbStart, cm[k].length);        /* :798 */
+                bufpos += cm[k].length;
+                cm[k].blockID = lastBlockID[t];                             /* :799 */
+                cm[k].blockStart = (int32_t)curPos;                         /* :800 setBlockStartStop */
+                cm[k].blockStop = (int32_t)(curPos + cm[k].length);
+                curPos += cm[k].length;                                     /* :801 */
+            }
+            meta_encode(&cm[k], setv + k * 11);                             /* :803 SET digest -> meta */
+        }
+        lastBlockID[t + 4] = bufpos;                                        /* :808 */
+    }
+    /* Pipelined SETs: thread 0's, then thread 1's, then thread 2's (each in chunk order).
+     * Cross-thread order is racy in the reference; this fixes "last occurrence in chunk order wins". */
+    for (int64_t k = 0; k < n; k++) kv_set(&o->index, dig + k * H, setv + k * 11);
+
+    /* :190 storeDB :372-392 */
+    for (int i = 0; i < 8; i++) {                                           /* utilities.blockIDtoBytes :66-75 */
+        o->alloc[i * 3] = (uint8_t)(lastBlockID[i] >> 16);
+        o->alloc[i * 3 + 1] = (uint8_t)(lastBlockID[i] >> 8);
+        o->alloc[i * 3 + 2] = (uint8_t)lastBlockID[i];
+    }
+    o->have_alloc = 1;
+    uint32_t rkey = (uint32_t)block_id;                                     /* longToBytes(filename,4) */
+    recipe *r = NULL;
+    for (int64_t i = 0; i < o->nrec; i++) if (o->rec[i].key == rkey) r = &o->rec[i];
+    if (!r) {
+        if (o->nrec == o->rcap) {
+            o->rcap = o->rcap ? o->rcap * 2 : 16;
+            o->rec = (recipe *)realloc(o->rec, (size_t)o->rcap * sizeof(recipe));
+        }
+        r = &o->rec[o->nrec++];
+        r->key = rkey; r->data = NULL;
+    }
+    free(r->data);
+    r->len = 4 + n * H;
+    r->data = (uint8_t *)malloc((size_t)r->len);
+    r->data[0] = (uint8_t)(size >> 24); r->data[1] = (uint8_t)(size >> 16);
+    r->data[2] = (uint8_t)(size >> 8);  r->data[3] = (uint8_t)size;
+    memcpy(r->data + 4, dig, (size_t)(n * H));
+
+    if (offsets_out) memcpy(offsets_out, off, (size_t)n * sizeof(uint32_t));
+    if (digests_out) memcpy(digests_out, dig, (size_t)(n * H));
+    if (is_new_out) for (int64_t k = 0; k < n; k++) is_new_out[k] = (uint8_t)cm[k].newChunk;
+    if (values_out) memcpy(values_out, setv, (size_t)n * 11);
+    if (store_size_out) *store_size_out = storeSize;
+    free(off); free(cm); free(dig); free(setv);
+    return n;
+}
+
+int hdrf_oracle_index_get(const hdrf_oracle *o, const uint8_t *digest, uint8_t out11[11])
+{
+    int64_t f = kv_find(&o->index, digest);
+    if (f < 0) return 0;
+    memcpy(out11, o->index.vals + f * 11, 11);
+    return 1;
+}
+
+int64_t hdrf_oracle_index_count(const hdrf_oracle *o) { return o->index.count; }
+
+static int g_sort_H;
+static int cmp_keyidx(const void *a, const void *b)
+{
+    const uint8_t *const *pa = (const uint8_t *const *)a, *const *pb = (const uint8_t *const *)b;
+    return memcmp(*pa, *pb, (size_t)g_sort_H);
+}
+
+int64_t hdrf_oracle_index_dump(const hdrf_oracle *o, uint8_t *keys, uint8_t *vals, int64_t cap)
+{
+    const kvmap *m = &o->index;
+    if (cap < m->count) return -m->count;
+    const uint8_t **ptr = (const uint8_t **)malloc((size_t)(m->count + 1) * sizeof(uint8_t *));
+    int64_t j = 0;
+    for (int64_t i = 0; i < m->cap; i++) if (m->used[i]) ptr[j++] = m->keys + i * m->H;
+    g_sort_H = m->H;
+    qsort(ptr, (size_t)j, sizeof(uint8_t *), cmp_keyidx);
+    for (int64_t i = 0; i < j; i++) {
+        int64_t slot = (ptr[i] - m->keys) / m->H;
+        memcpy(keys + i * m->H, ptr[i], (size_t)m->H);
+        memcpy(vals + i * 11, m->vals + slot * 11, 11);
+    }
+    free(ptr);
+    return j;
+}
+
+int hdrf_oracle_allocator(const hdrf_oracle *o, uint8_t out24[24])
+{
+    if (!o->have_alloc) return 0;
+    memcpy(out24, o->alloc, 24);
+    return 1;
+}
+
+int64_t hdrf_oracle_recipe(const hdrf_oracle *o, int64_t block_id, uint8_t *out, int64_t cap)
+{
+    for (int64_t i = 0; i < o->nrec; i++)
+        if (o->rec[i].key == (uint32_t)block_id) {
+            if (cap < o->rec[i].len) return -o->rec[i].len;
+            memcpy(out, o->rec[i].data, (size_t)o->rec[i].len);
+            return o->rec[i].len;
+        }
+    return 0;
+}
+
+int64_t hdrf_oracle_container(const hdrf_oracle *o, uint32_t id, uint8_t *out, int64_t cap, int *closed)
+{
+    for (int64_t i = 0; i < o->ncont; i++)
+        if (o->cont[i].id == id) {
+            const container *c = &o->cont[i];
+            if (closed) *closed = c->closed;
+            if (cap < c->len) return -(c->len + 2);
+            if (c->len) memcpy(out, c->data, (size_t)c->len);
+            return c->len;
+        }
+    return -1;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Synthetic corpus (BASELINE config 2; spec in DESIGN.md §Corpus). */
+uint64_t hdrf_oracle_mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void hdrf_oracle_corpus_roots(uint64_t seed, uint32_t dup_ppm, int64_t nblocks, int64_t spb, uint32_t *roots)
+{
+    for (int64_t b = 0; b < nblocks; b++)
+        for (int64_t s = 0; s < spb; s++) {
+            uint64_t g = (uint64_t)(b * spb + s);
+            uint64_t coin = hdrf_oracle_mix64(seed ^ 0xD1B54A32D192ED03ull ^ hdrf_oracle_mix64(g));
+            if (b > 0 && (coin % 1000000ull) < dup_ppm) {
+                uint64_t r1 = hdrf_oracle_mix64(coin);
+                uint64_t sb = r1 % (uint64_t)b;
+                uint64_t ss = hdrf_oracle_mix64(r1) % (uint64_t)spb;
+                roots[g] = roots[sb * spb + ss];
+            } else {
+                roots[g] = (uint32_t)g;
+            }
+        }
+}
+
+void hdrf_oracle_corpus_fill(uint64_t seed, const uint32_t *roots, int64_t block, int64_t spb,
+                             int64_t seg_bytes, uint8_t *out)
+{
+    for (int64_t s = 0; s < spb; s++) {
+        uint64_t key = hdrf_oracle_mix64(seed ^ hdrf_oracle_mix64((uint64_t)roots[block * spb + s] + 1));
+        uint8_t *dst = out + s * seg_bytes;
+        for (int64_t wi = 0; wi < seg_bytes / 8; wi++) {
+            uint64_t x = hdrf_oracle_mix64(key + (uint64_t)wi);
+            memcpy(dst + 8 * wi, &x, 8);            /* little-endian host */
+        }
+    }
+}
+
+/* java.util.Random — seed scramble, 48-bit LCG, nextInt(), nextBytes() (JDK 8 semantics). */
+void hdrf_oracle_java_random_bytes(int64_t seed, int32_t buffer_len, int64_t total, uint8_t *out)
+{
+    uint64_t s = ((uint64_t)seed ^ 0x5DEECE66Dull) & ((1ull << 48) - 1);
+    int64_t written = 0;
+    while (written < total) {
+        /* rb.nextBytes(toWrite): buffer_len bytes from ceil(buffer_len/4) nextInt() calls */
+        for (int32_t i = 0; i < buffer_len;) {
+            s = (s * 0x5DEECE66Dull + 0xBull) & ((1ull << 48) - 1);
+            int32_t rnd = (int32_t)(uint32_t)(s >> 16);
+            for (int nb = (buffer_len - i) < 4 ? (buffer_len - i) : 4; nb-- > 0; rnd >>= 8) {
+                if (written + i < total) out[written + i] = (uint8_t)rnd;
+                i++;
+            }
+        }
+        written += buffer_len;
+    }
+}

@@ -1,0 +1,76 @@
+/*
+ * hdrf_oracle.h — CPU restatement of HDRF's per-block reduction path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / CPU baseline.
+ * The product path (hdrf_amd/, libhdrf.so) never links or calls it.
+ *
+ * Pinning status:
+ *   - SHA-1 / SHA-224 digests: pinned to FIPS 180-4 known-answer vectors and to
+ *     Python hashlib (the survey verified the reference's native hasher equals
+ *     hashlib on 11 lengths).
+ *   - chunk boundaries, dedup decisions, index values, containers, recipes,
+ *     allocator: PARITY UNPINNED against the running reference (Java; no JDK,
+ *     Redis or Hadoop jars exist here and the reference ships no tests for this
+ *     path).  They are restated line by line from the cited Java sources and
+ *     cross-checked against an independent pure-Python transliteration
+ *     (oracle/pyref.py).
+ */
+#ifndef HDRF_ORACLE_H
+#define HDRF_ORACLE_H
+#include <stdint.h>
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* DataDeduplicator.chunking — DN/DataDeduplicator.java:264-307.
+ * Writes the chunk END offsets (last detected boundary dropped, `size` appended)
+ * into out[0..n); returns n, or -1 if out_cap is too small. */
+int64_t hdrf_oracle_chunk(const uint8_t *data, int64_t size, uint32_t *out, int64_t out_cap);
+
+/* FIPS 180-4 SHA-1 / SHA-224 (utilities.sha1hash/sha224hash, DN/utilities.java:98-137). */
+void hdrf_oracle_sha1(const uint8_t *msg, uint64_t len, uint8_t out[20]);
+void hdrf_oracle_sha224(const uint8_t *msg, uint64_t len, uint8_t out[28]);
+
+/* Whole write path: DataDeduplicator(ByteBuffer, long) — DN/DataDeduplicator.java:108-217,
+ * with Redis restated as an in-memory map and container files as in-memory byte vectors. */
+typedef struct hdrf_oracle hdrf_oracle;
+hdrf_oracle *hdrf_oracle_new(int hasher, int compressor, uint32_t max_size);
+void hdrf_oracle_free(hdrf_oracle *o);
+
+/* Reduce one block.  Optional outputs (NULL to skip), each sized for cap chunks:
+ *   offsets[n], digests[n*H], is_new[n], values[n*11] (the 11-byte value each chunk SETs).
+ * Returns n (number of chunks) or a negative error. */
+int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, int64_t block_id,
+                           int64_t cap, uint32_t *offsets, uint8_t *digests, uint8_t *is_new,
+                           uint8_t *values, int64_t *store_size);
+
+/* GET digest -> 11-byte value; returns 1 if present. */
+int hdrf_oracle_index_get(const hdrf_oracle *o, const uint8_t *digest, uint8_t out11[11]);
+int64_t hdrf_oracle_index_count(const hdrf_oracle *o);
+/* Dump every (digest, value) pair, sorted by digest bytes. Returns count (or -needed if cap small). */
+int64_t hdrf_oracle_index_dump(const hdrf_oracle *o, uint8_t *keys, uint8_t *vals, int64_t cap);
+/* GET "blockID" -> 24 bytes; returns 1 if the key exists. */
+int hdrf_oracle_allocator(const hdrf_oracle *o, uint8_t out24[24]);
+/* GET longToBytes(blockId,4) -> recipe bytes; returns length, 0 if absent, -needed if cap small. */
+int64_t hdrf_oracle_recipe(const hdrf_oracle *o, int64_t block_id, uint8_t *out, int64_t cap);
+/* Container file chunkDir+id: returns length (-1 absent, -(needed+2) if cap too small).
+ * *closed = 1 once the container was rewritten on overflow. Raw (uncompressed) bytes. */
+int64_t hdrf_oracle_container(const hdrf_oracle *o, uint32_t id, uint8_t *out, int64_t cap, int *closed);
+
+/* Synthetic corpus (shared spec with hdrf_amd corpus generator). */
+uint64_t hdrf_oracle_mix64(uint64_t z);
+void hdrf_oracle_corpus_roots(uint64_t seed, uint32_t dup_ppm, int64_t nblocks, int64_t segs_per_block,
+                              uint32_t *roots);
+void hdrf_oracle_corpus_fill(uint64_t seed, const uint32_t *roots, int64_t block, int64_t segs_per_block,
+                             int64_t seg_bytes, uint8_t *out);
+
+/* java.util.Random(seed).nextBytes in buffer_len pieces (DFSTestUtil.createFile,
+ * hadoop-hdfs/src/test/java/org/apache/hadoop/hdfs/DFSTestUtil.java:441-450). */
+void hdrf_oracle_java_random_bytes(int64_t seed, int32_t buffer_len, int64_t total, uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

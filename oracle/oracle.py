@@ -1,0 +1,195 @@
+"""ctypes wrapper around the CPU oracle (oracle/hdrf_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, never by the product package (hdrf_amd/).
+Pinning status: see oracle/hdrf_oracle.h and DESIGN.md §Oracle.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libhdrf_oracle.so")
+_lib = None
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.hdrf_oracle_chunk.argtypes = [_u8p, ctypes.c_int64, _u32p, ctypes.c_int64]
+        L.hdrf_oracle_chunk.restype = ctypes.c_int64
+        L.hdrf_oracle_sha1.argtypes = [_u8p, ctypes.c_uint64, _u8p]
+        L.hdrf_oracle_sha224.argtypes = [_u8p, ctypes.c_uint64, _u8p]
+        L.hdrf_oracle_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
+        L.hdrf_oracle_new.restype = ctypes.c_void_p
+        L.hdrf_oracle_free.argtypes = [ctypes.c_void_p]
+        L.hdrf_oracle_reduce.argtypes = [ctypes.c_void_p, _u8p, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.c_int64, _u32p, _u8p, _u8p, _u8p, _i64p]
+        L.hdrf_oracle_reduce.restype = ctypes.c_int64
+        L.hdrf_oracle_index_get.argtypes = [ctypes.c_void_p, _u8p, _u8p]
+        L.hdrf_oracle_index_get.restype = ctypes.c_int
+        L.hdrf_oracle_index_count.argtypes = [ctypes.c_void_p]
+        L.hdrf_oracle_index_count.restype = ctypes.c_int64
+        L.hdrf_oracle_index_dump.argtypes = [ctypes.c_void_p, _u8p, _u8p, ctypes.c_int64]
+        L.hdrf_oracle_index_dump.restype = ctypes.c_int64
+        L.hdrf_oracle_allocator.argtypes = [ctypes.c_void_p, _u8p]
+        L.hdrf_oracle_allocator.restype = ctypes.c_int
+        L.hdrf_oracle_recipe.argtypes = [ctypes.c_void_p, ctypes.c_int64, _u8p, ctypes.c_int64]
+        L.hdrf_oracle_recipe.restype = ctypes.c_int64
+        L.hdrf_oracle_container.argtypes = [ctypes.c_void_p, ctypes.c_uint32, _u8p, ctypes.c_int64,
+                                            ctypes.POINTER(ctypes.c_int)]
+        L.hdrf_oracle_container.restype = ctypes.c_int64
+        L.hdrf_oracle_mix64.argtypes = [ctypes.c_uint64]
+        L.hdrf_oracle_mix64.restype = ctypes.c_uint64
+        L.hdrf_oracle_corpus_roots.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64,
+                                               ctypes.c_int64, _u32p]
+        L.hdrf_oracle_corpus_fill.argtypes = [ctypes.c_uint64, _u32p, ctypes.c_int64, ctypes.c_int64,
+                                              ctypes.c_int64, _u8p]
+        L.hdrf_oracle_java_random_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _u8p]
+        _lib = L
+    return _lib
+
+
+def _p(a, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+def _as_u8(data):
+    a = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) \
+        else np.ascontiguousarray(data, dtype=np.uint8)
+    if a.size == 0:
+        a = np.zeros(1, dtype=np.uint8)[:0]
+    return a
+
+
+def chunk(data):
+    """DataDeduplicator.chunking (DN/DataDeduplicator.java:264-307) -> uint32 end offsets."""
+    a = _as_u8(data)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    cap = a.size // 700 + 2
+    out = np.zeros(cap, dtype=np.uint32)
+    n = lib().hdrf_oracle_chunk(_p(buf), a.size, _p(out, _u32p), cap)
+    assert n > 0
+    return out[:n].copy()
+
+
+def sha1(data):
+    a = _as_u8(data)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    out = np.zeros(20, np.uint8)
+    lib().hdrf_oracle_sha1(_p(buf), a.size, _p(out))
+    return out.tobytes()
+
+
+def sha224(data):
+    a = _as_u8(data)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    out = np.zeros(28, np.uint8)
+    lib().hdrf_oracle_sha224(_p(buf), a.size, _p(out))
+    return out.tobytes()
+
+
+def mix64(z):
+    return lib().hdrf_oracle_mix64(z & 0xFFFFFFFFFFFFFFFF)
+
+
+def corpus_roots(seed, dup_ppm, nblocks, segs_per_block):
+    roots = np.zeros(nblocks * segs_per_block, np.uint32)
+    lib().hdrf_oracle_corpus_roots(seed, dup_ppm, nblocks, segs_per_block, _p(roots, _u32p))
+    return roots
+
+
+def corpus_block(seed, roots, block, segs_per_block, seg_bytes):
+    out = np.empty(segs_per_block * seg_bytes, np.uint8)
+    lib().hdrf_oracle_corpus_fill(seed, _p(roots, _u32p), block, segs_per_block, seg_bytes, _p(out))
+    return out
+
+
+def java_random_bytes(seed, buffer_len, total):
+    out = np.empty(max(total, 1), np.uint8)
+    lib().hdrf_oracle_java_random_bytes(seed, buffer_len, total, _p(out))
+    return out[:total]
+
+
+class Oracle:
+    """Stateful restatement of DataDeduplicator + Redis + chunkDir (one DataNode)."""
+
+    def __init__(self, hasher=0, compressor=1, max_size=1 << 25):
+        self.H = 20 if hasher == 0 else 28
+        self.hasher = hasher
+        self._h = lib().hdrf_oracle_new(hasher, compressor, max_size)
+        assert self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().hdrf_oracle_free(h)
+            self._h = None
+
+    def reduce(self, data, block_id):
+        a = _as_u8(data)
+        buf = a if a.size else np.zeros(1, np.uint8)
+        cap = a.size // 700 + 2
+        offs = np.zeros(cap, np.uint32)
+        digs = np.zeros(cap * self.H, np.uint8)
+        isnew = np.zeros(cap, np.uint8)
+        vals = np.zeros(cap * 11, np.uint8)
+        ss = ctypes.c_int64(0)
+        n = lib().hdrf_oracle_reduce(self._h, _p(buf), a.size, block_id, cap, _p(offs, _u32p),
+                                     _p(digs), _p(isnew), _p(vals), ctypes.byref(ss))
+        assert n > 0, n
+        return {
+            "offsets": offs[:n].copy(),
+            "digests": digs[:n * self.H].reshape(n, self.H).copy(),
+            "is_new": isnew[:n].copy(),
+            "values": vals[:n * 11].reshape(n, 11).copy(),
+            "store_size": ss.value,
+        }
+
+    def index_get(self, digest):
+        d = np.frombuffer(bytes(digest), np.uint8).copy()
+        out = np.zeros(11, np.uint8)
+        return out.tobytes() if lib().hdrf_oracle_index_get(self._h, _p(d), _p(out)) else None
+
+    def index_dump(self):
+        cnt = lib().hdrf_oracle_index_count(self._h)
+        keys = np.zeros(max(cnt, 1) * self.H, np.uint8)
+        vals = np.zeros(max(cnt, 1) * 11, np.uint8)
+        n = lib().hdrf_oracle_index_dump(self._h, _p(keys), _p(vals), cnt)
+        assert n == cnt
+        return keys[:n * self.H].reshape(n, self.H), vals[:n * 11].reshape(n, 11)
+
+    def allocator(self):
+        out = np.zeros(24, np.uint8)
+        return out.tobytes() if lib().hdrf_oracle_allocator(self._h, _p(out)) else None
+
+    def recipe(self, block_id):
+        n = lib().hdrf_oracle_recipe(self._h, block_id, None, 0)
+        if n == 0:
+            return None
+        out = np.zeros(-n, np.uint8)
+        m = lib().hdrf_oracle_recipe(self._h, block_id, _p(out), -n)
+        return out[:m].tobytes()
+
+    def container(self, cid):
+        closed = ctypes.c_int(0)
+        n = lib().hdrf_oracle_container(self._h, cid, None, 0, ctypes.byref(closed))
+        if n == -1:
+            return None, False
+        need = -(n + 2) if n < 0 else 0
+        out = np.zeros(max(need, 1), np.uint8)
+        m = lib().hdrf_oracle_container(self._h, cid, _p(out), need, ctypes.byref(closed))
+        return out[:m].tobytes(), bool(closed.value)
