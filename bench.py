@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""bench.py — HDRF per-block reduction throughput on MI355X (BASELINE config 2).
+
+Workload (per GPU): a synthetic corpus of 512 blocks x 128 MiB (64 GiB) resident in HBM,
+1 MiB segments, 50% of them copies of a segment of an EARLIER block (cross-block
+duplicates).  One step = one DataNode reducing the whole corpus in block
+order from a fresh index: window-max chunking -> SHA-1 -> GPU index (exact HDRF dedup
+semantics) -> container placement + gather into the container arena, in batches of 64
+blocks.  value = logical bytes reduced per second over all ranks (GB = 1e9 B).
+
+Multi-GPU (`torch.distributed.run`): every rank is an independent DataNode with its own
+corpus shard and index (HDRF keeps one Redis index per DataNode, DN/DataDeduplicator.java:119),
+so there is no collective in the data path; scaling is weak.
+
+The line also carries the dominant kernel's roofline (HIP events on the library's stream)
+and the CPU oracle timed on this host on a bounded sample of the same corpus, whose
+per-block storeSize must equal the GPU's (bit-exact dedup ratio check).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "logical GB/s reduced per node (1/2/4/8 GPUs) at 50% dup, bit-exact dedup ratio"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--blocks", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--block-mib", type=int, default=128)
+    ap.add_argument("--seg-mib", type=int, default=1)
+    ap.add_argument("--dup-ppm", type=int, default=500000)
+    ap.add_argument("--seed", type=int, default=20251015)
+    ap.add_argument("--index-log2", type=int, default=27)
+    ap.add_argument("--hasher", type=int, default=0)
+    ap.add_argument("--cpu-sample-blocks", type=int, default=24)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+
+    from hdrf_amd.corpus import corpus_roots
+    from hdrf_amd.lib import STAGES, Context
+
+    S = a.block_mib << 20
+    seg = a.seg_mib << 20
+    spb = S // seg
+    nb, B = a.blocks, min(a.batch, a.blocks)
+    ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
+                  arena_slots=64, keep_recipes=0, timing=1)
+    seed = a.seed ^ (rank * 0x9E3779B9)
+    roots = corpus_roots(seed, a.dup_ppm, nb, spb)
+    total = nb * S + 4096
+    dev = ctx.dev_alloc(total)
+    ctx.corpus_fill(dev, roots, nb, spb, seg, seed)
+    batches = []
+    for b0 in range(0, nb, B):
+        k = min(B, nb - b0)
+        batches.append(([dev + (b0 + i) * S for i in range(k)], [S] * k,
+                        [total - (b0 + i) * S for i in range(k)], [b0 + i for i in range(k)]))
+
+    n_chunks = np.zeros(nb, np.int64)
+    store = np.zeros(nb, np.int64)
+
+    def step():
+        ctx.reset()                                      # a fresh DataNode index each step
+        j = 0
+        for ptrs, lens, rd, ids in batches:
+            ctx.reduce_batch(ptrs, lens, rd, ids)
+            for i in range(len(ptrs)):
+                n_chunks[j], store[j] = ctx.batch_info(i)
+                j += 1
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    ctx.stage_times(reset=True)
+    barrier()
+    torch.cuda.synchronize()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    stage_ms = ctx.stage_times(reset=True)
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms_step = el / a.steps * 1e3
+    logical = nb * S * world
+    value = logical / (el / a.steps) / 1e9
+
+    # ---- roofline of the dominant kernel (algorithmic bytes / HIP-event time) -----------------
+    nbatch = len(batches)
+    chunks_step = int(n_chunks.sum())
+    new_bytes = int(store.sum())
+    per_launch = {   # algorithmic HBM bytes per launch
+        STAGES[0]: (nb * S + 4 * chunks_step) / nbatch,                 # read block bytes, write cuts
+        STAGES[2]: (nb * S + 24 * chunks_step) / nbatch,                # read chunk bytes + offsets, write digests
+        STAGES[7]: (2 * new_bytes + 16 * chunks_step) / nbatch,         # read+write new bytes, chunk metadata
+    }
+    stages = {}
+    for name, ms in zip(STAGES, stage_ms):
+        avg_ms = ms / a.steps / nbatch
+        d = {"ms_per_step": round(ms / a.steps, 3), "avg_launch_ms": round(avg_ms, 4)}
+        if name in per_launch and avg_ms > 0:
+            d["GB_s"] = round(per_launch[name] / (avg_ms * 1e-3) / 1e9, 1)
+        stages[name] = d
+    dom = max(per_launch, key=lambda s: stage_ms[STAGES.index(s)])
+    dom_ms = stage_ms[STAGES.index(dom)] / a.steps / nbatch
+    achieved = per_launch[dom] / (dom_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "avg_launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(per_launch[dom])}
+
+    dedup = {"logical_bytes_per_gpu": nb * S, "stored_bytes_per_gpu": new_bytes,
+             "dedup_ratio": round(nb * S / max(new_bytes, 1), 6),
+             "dup_fraction": round(1 - new_bytes / (nb * S), 6), "target_dup_fraction": a.dup_ppm / 1e6,
+             "chunks_per_gpu": chunks_step, "mean_chunk_bytes": round(nb * S / max(chunks_step, 1), 1)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu and a.cpu_sample_blocks > 0:
+        cpu = cpu_baseline(ctx, dev, S, min(a.cpu_sample_blocks, nb), store, a.hasher)
+
+    if rank == 0:
+        line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
+                "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+                "config": {"workload": "config2: %d x %d MiB blocks per GPU, %d%% dup (%d MiB segments), "
+                                       "chunk+SHA-%s+local index+container store, fresh index per step"
+                                       % (nb, a.block_mib, a.dup_ppm // 10000, a.seg_mib,
+                                          "1" if a.hasher == 0 else "224"),
+                           "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks": B,
+                           "parallelism": "dp%d (one DataNode index per GPU)" % world},
+                "roofline": roofline, "cpu_baseline": cpu, "dedup": dedup, "stages": stages}
+        print(json.dumps(line), flush=True)
+    ctx.dev_free(dev)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ctx, dev, S, m, gpu_store, hasher):
+    """CPU oracle (single thread, C restatement of the reference) on the first m blocks of the
+    same corpus; also checks per-block storeSize == the GPU's (bit-exact dedup ratio)."""
+    import numpy as np
+
+    from oracle.oracle import Oracle
+    ora = Oracle(hasher=hasher, compressor=1)
+    t = 0.0
+    mism = 0
+    for b in range(m):
+        blk = ctx.d2h(dev + b * S, S)
+        t0 = time.perf_counter()
+        r = ora.reduce(blk, b)
+        t += time.perf_counter() - t0
+        mism += int(r["store_size"] != gpu_store[b])
+    return {"value": round(m * S / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "first %d of the same blocks (%.1f GiB), oracle/hdrf_oracle.c, 1 thread, %.1f s"
+                      % (m, m * S / 2**30, t),
+            "store_size_mismatches": mism, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

@@ -19,7 +19,7 @@ using namespace hdrf;
 
 namespace {
 
-constexpr int kStages = 4;
+constexpr int kStages = hdrf::kNumStages;
 constexpr uint64_t kSlack = 64;   // readable bytes required past each block end
 
 struct ContainerInfo {
@@ -280,24 +280,21 @@ extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
     hipStream_t st = ctx->st;
     HIPCK(hipMemcpyAsync(ctx->d_blocks, bd.data(), sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(ctx->d_nclosed, 0, sizeof(uint32_t), st));
-    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[0], st));
+    Marker mk;
+    mk.ev = ctx->timing ? ctx->ev : nullptr;
     HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
-                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st));
-    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[1], st));
-    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_dig, st));
-    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[2], st));
+                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
+    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_dig, st, &mk));
     HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_tab, c.index_log2,
                        cur, ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags, ctx->d_tilesum,
-                       ctx->ntiles, ctx->d_err, st));
-    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[3], st));
+                       ctx->ntiles, ctx->d_err, st, &mk));
     StoreParams P;
     P.nblocks = nblocks; P.cap_blk = ctx->cap_blk; P.ntiles = ctx->ntiles;
     P.n_thread = c.n_thread; P.min_mt = c.min_mt_chunks; P.cmax = c.container_max;
     P.nslots = (uint32_t)c.arena_slots; P.ev_cap = ctx->ev_cap; P.closed_cap = ctx->closed_cap;
     HIPCK(launch_store(P, ctx->d_blocks, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre,
                        ctx->d_store, ctx->d_pre, ctx->d_alloc, ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed,
-                       ctx->d_slot, ctx->d_tab, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, ctx->d_err, st));
-    if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[4], st));
+                       ctx->d_slot, ctx->d_tab, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, ctx->d_err, st, &mk));
     // read back small per-batch state
     ctx->h_bst.resize(nblocks);
     ctx->h_store.resize(nblocks);

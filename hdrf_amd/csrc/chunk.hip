@@ -404,10 +404,12 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
 namespace hdrf {
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg, int w, int maxlen,
                            uint32_t *spec, int spec_cap, SegMeta *meta, int32_t *sync, SegPlan *plan,
-                           BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st)
+                           BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk)
 {
+    mk->mark(st);
     dim3 g((max_nseg + 3) / 4, nblocks);
     hipLaunchKernelGGL(spec_walk_kernel, g, dim3(256), 0, st, d_blocks, w, maxlen, spec, spec_cap, meta);
+    mk->mark(st);
     hipLaunchKernelGGL(spec_sync_kernel, g, dim3(256), 0, st, d_blocks, spec, spec_cap, meta, sync);
     hipLaunchKernelGGL(spec_plan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, spec, spec_cap, meta, sync,
                        plan, bst);

@@ -186,20 +186,23 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
-                        int ntiles, int *err, hipStream_t st)
+                        int ntiles, int *err, hipStream_t st, Marker *mk)
 {
+    mk->mark(st);
     dim3 g(ntiles, nblocks);
     (void)hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st);
     if (hasher == 0) {
         hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
         hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
                            coll_cap, err);
+        mk->mark(st);
         hipLaunchKernelGGL(idx_slow_kernel<5>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, slot,
                            coll, ncoll, coll_cap, err);
     } else {
         hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
         hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
                            coll_cap, err);
+        mk->mark(st);
         hipLaunchKernelGGL(idx_slow_kernel<7>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, slot,
                            coll, ncoll, coll_cap, err);
     }

@@ -4,6 +4,19 @@
 
 namespace hdrf {
 
+// Stage markers: when timing is on, a HIP event is recorded on the launch stream at every
+// stage boundary (kernels of one stream run in order, so event deltas are kernel times).
+constexpr int kNumStages = 8;   // walk, stitch, sha, index(claim+apply), index(slow+decide), scan, flush, place
+struct Marker {
+    hipEvent_t *ev = nullptr;   // kNumStages + 1 events
+    int next = 0;
+    __host__ void mark(hipStream_t st)
+    {
+        if (ev) (void)hipEventRecord(ev[next], st);
+        next++;
+    }
+};
+
 struct StoreParams {
     int nblocks, cap_blk, ntiles;
     int n_thread, min_mt;      // DataDeduplicator.nThread (3), small-block threshold (25)
@@ -15,18 +28,18 @@ struct StoreParams {
 
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg, int w, int maxlen,
                            uint32_t *spec, int spec_cap, SegMeta *meta, int32_t *sync, SegPlan *plan,
-                           BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st);
+                           BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
-                      const BlockState *bst, int cap_blk, uint32_t *digests, hipStream_t st);
+                      const BlockState *bst, int cap_blk, uint32_t *digests, hipStream_t st, Marker *mk);
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
-                        int ntiles, int *err, hipStream_t st);
+                        int ntiles, int *err, hipStream_t st, Marker *mk);
 hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
                         const uint32_t *offsets, const uint8_t *flags, const uint32_t *tilesum, uint32_t *tilepre,
                         uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
                         ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
-                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st);
+                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk);
 hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
                          uint64_t seed, hipStream_t st);
 

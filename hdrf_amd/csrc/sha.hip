@@ -139,8 +139,9 @@ __global__ void __launch_bounds__(256) sha_kernel(const BlockDesc *__restrict__ 
 }
 
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
-                      const BlockState *bst, int cap_blk, uint32_t *digests, hipStream_t st)
+                      const BlockState *bst, int cap_blk, uint32_t *digests, hipStream_t st, Marker *mk)
 {
+    mk->mark(st);
     dim3 g((cap_blk + 255) / 256, nblocks);
     if (hasher == 0) hipLaunchKernelGGL(sha_kernel<5>, g, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, digests);
     else hipLaunchKernelGGL(sha_kernel<7>, g, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, digests);

@@ -276,16 +276,20 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
                         const uint32_t *offsets, const uint8_t *flags, const uint32_t *tilesum, uint32_t *tilepre,
                         uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
                         ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
-                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st)
+                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk)
 {
+    mk->mark(st);
     dim3 g(P.ntiles, P.nblocks);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(P.nblocks), dim3(256), 0, st, bst, P.ntiles, tilesum, tilepre,
                        store_size, P.cap_blk);
     hipLaunchKernelGGL(chunk_scan_kernel, g, dim3(256), 0, st, bst, P.cap_blk, P.ntiles, offsets, flags, tilepre, pre);
+    mk->mark(st);
     hipLaunchKernelGGL(flush_kernel, dim3(1), dim3(256), 0, st, P, bst, store_size, pre, alloc, rstate, events, closed,
                        nclosed, err);
+    mk->mark(st);
     hipLaunchKernelGGL(place_kernel, g, dim3(256), 0, st, P, d_blocks, bst, offsets, flags, pre, rstate, events, slot,
                        tab, arena, place_cid, place_pos);
+    mk->mark(st);
     return hipGetLastError();
 }
 

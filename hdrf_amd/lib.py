@@ -28,6 +28,12 @@ EXPORTS = [
 ]
 
 
+# per-stage timers of hdrf_stage_times (kernel names in parentheses)
+STAGES = ["walk(spec_walk_kernel)", "stitch(spec_sync/plan/copy/fallback)", "sha(sha_kernel)",
+          "index_claim_apply", "index_slow_decide", "scan(tile/chunk)", "flush(flush_kernel)",
+          "place(place_kernel)"]
+
+
 class HdrfError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"{HDRF_ERRORS.get(code, code)}: {msg}")
@@ -286,8 +292,8 @@ class Context:
         self._ck(self.L.hdrf_synchronize(self._h))
 
     def stage_times(self, reset=False):
-        out = (ctypes.c_double * 4)()
-        self._ck(self.L.hdrf_stage_times(self._h, out, 4, 1 if reset else 0))
+        out = (ctypes.c_double * len(STAGES))()
+        self._ck(self.L.hdrf_stage_times(self._h, out, len(STAGES), 1 if reset else 0))
         return list(out)
 
     def reset(self):

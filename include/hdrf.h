@@ -119,7 +119,9 @@ int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, in
                      int64_t segs_per_block, int64_t seg_bytes, uint64_t seed);
 
 /* Per-stage device time (ms) accumulated since the last reset, measured with HIP events on
- * the context's stream: [0] chunking, [1] fingerprint, [2] index, [3] store. */
+ * the context's stream (cfg.timing = 1): [0] chunk walk (spec_walk_kernel), [1] chunk stitch
+ * (sync/plan/copy/fallback), [2] fingerprint (sha_kernel), [3] index claim+apply, [4] index
+ * slow-path+decide, [5] new-byte scans, [6] container flush walk, [7] place+gather+finalise. */
 int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
 /* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis). */
 int hdrf_reset(hdrf_ctx *ctx);
