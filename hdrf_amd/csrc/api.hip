@@ -42,7 +42,7 @@ struct hdrf_ctx {
     int32_t *d_sync = nullptr;
     SegPlan *d_plan = nullptr;
     BlockState *d_bst = nullptr;
-    uint32_t *d_off = nullptr, *d_dig = nullptr, *d_slot = nullptr, *d_pre = nullptr;
+    uint32_t *d_off = nullptr, *d_dig = nullptr, *d_mid = nullptr, *d_slot = nullptr, *d_pre = nullptr;
     uint8_t *d_flags = nullptr;
     uint32_t *d_tilesum = nullptr, *d_tilepre = nullptr;
     uint64_t *d_store = nullptr;
@@ -128,7 +128,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
 static void free_all(hdrf_ctx *ctx)
 {
     void *ptrs[] = {ctx->d_blocks, ctx->d_spec, ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off,
-                    ctx->d_dig, ctx->d_slot, ctx->d_pre, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
+                    ctx->d_dig, ctx->d_mid, ctx->d_slot, ctx->d_pre, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
                     ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed, ctx->d_coll, ctx->d_ncoll, ctx->d_tab,
                     ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_err, ctx->d_stage};
     for (void *p : ptrs)
@@ -196,6 +196,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         (rc = dalloc(ctx, &ctx->d_meta, nseg)) || (rc = dalloc(ctx, &ctx->d_sync, nseg)) ||
         (rc = dalloc(ctx, &ctx->d_plan, nseg)) || (rc = dalloc(ctx, &ctx->d_bst, B)) ||
         (rc = dalloc(ctx, &ctx->d_off, nchunk)) || (rc = dalloc(ctx, &ctx->d_dig, nchunk * ctx->HW)) ||
+        (rc = dalloc(ctx, &ctx->d_mid, nchunk * 8)) ||
         (rc = dalloc(ctx, &ctx->d_slot, nchunk)) || (rc = dalloc(ctx, &ctx->d_pre, nchunk)) ||
         (rc = dalloc(ctx, &ctx->d_flags, nchunk)) || (rc = dalloc(ctx, &ctx->d_tilesum, (size_t)B * ctx->ntiles)) ||
         (rc = dalloc(ctx, &ctx->d_tilepre, (size_t)B * ctx->ntiles)) || (rc = dalloc(ctx, &ctx->d_store, B)) ||
@@ -284,7 +285,8 @@ extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
     mk.ev = ctx->timing ? ctx->ev : nullptr;
     HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
                           ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
-    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_dig, st, &mk));
+    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_mid, ctx->d_dig,
+                     st, &mk));
     HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_tab, c.index_log2,
                        cur, ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags, ctx->d_tilesum,
                        ctx->ntiles, ctx->d_err, st, &mk));

@@ -63,15 +63,20 @@ struct Walker {
     int w;         // window (700)
     int maxlen;    // forced-cut length (1,000,000)
     int T;         // tile A base (multiple of 1024)
-    uint4 A, B, C, D;
+    uint4 A, B;      // biased view [T, T+2048)
+    uint4 C, D;      // raw prefetch of [T+2048, T+4096)
     uint32_t gA, gB;
 
-    __device__ __forceinline__ uint4 tile(int X) const
+    // raw (unbiased) tile load; the bias is applied when the tile is promoted into the view so
+    // the load stays in flight (a use right after the load would force s_waitcnt vmcnt(0))
+    __device__ __forceinline__ uint4 tile_raw(int X) const
     {
-        int off = X + 16 * lane_id();
-        uint4 v;
-        if (off + 16 <= avail) v = *reinterpret_cast<const uint4 *>(base + off);
-        else v = load16_guard(base, off, avail);
+        const int off = X + 16 * lane_id();
+        if (X + 1024 <= avail) return ld16(base + off);       // wave-uniform fast path
+        return load16_guard(base, off, avail);
+    }
+    static __device__ __forceinline__ uint4 bias(uint4 v)
+    {
         v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
         return v;
     }
@@ -79,7 +84,8 @@ struct Walker {
     __device__ __forceinline__ void init(int p)
     {
         T = p & ~1023;
-        A = tile(T); B = tile(T + 1024); C = tile(T + 2048); D = tile(T + 3072);
+        A = tile_raw(T); B = tile_raw(T + 1024); C = tile_raw(T + 2048); D = tile_raw(T + 3072);
+        A = bias(A); B = bias(B);
         gA = gmax16(A); gB = gmax16(B);
     }
 
@@ -87,9 +93,9 @@ struct Walker {
     {
         T += 1024;
         A = B; gA = gB;
-        B = C; gB = gmax16(B);
+        B = bias(C); gB = gmax16(B);
         C = D;
-        D = tile(T + 3072);
+        D = tile_raw(T + 3072);
     }
 
     // 4 dwords of granule g (0..127) of the A|B view, as uniform scalars
@@ -220,6 +226,7 @@ __device__ __forceinline__ bool walk_chain(Walker &W, int p, bool first, ListSin
         else if (p + W.maxlen <= W.size - 1) cut = p + W.maxlen + 1;   // :288-294
         else return true;
         first = false;
+        cut = __builtin_amdgcn_readfirstlane(cut);
         if (!sink.push((uint32_t)cut)) return false;
         if (stop(cut, sink.cnt)) return false;
         p = cut;
@@ -233,7 +240,7 @@ __global__ void __launch_bounds__(256) spec_walk_kernel(const BlockDesc *__restr
                                                         SegMeta *__restrict__ meta)
 {
     const int b = blockIdx.y;
-    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.x * 4 + wave_id();
     const BlockDesc bd = blocks[b];
     if (k >= bd.nseg) return;
     const int size = (int)bd.len;
@@ -267,7 +274,7 @@ __global__ void __launch_bounds__(256) spec_sync_kernel(const BlockDesc *__restr
                                                         const SegMeta *__restrict__ meta, int32_t *__restrict__ sync)
 {
     const int b = blockIdx.y;
-    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.x * 4 + wave_id();
     const int l = lane_id();
     const BlockDesc bd = blocks[b];
     if (k + 1 >= bd.nseg) return;
@@ -357,7 +364,7 @@ __global__ void __launch_bounds__(256) spec_copy_kernel(const BlockDesc *__restr
                                                         uint32_t *__restrict__ offsets, int cap_blk)
 {
     const int b = blockIdx.y;
-    const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int k = blockIdx.x * 4 + wave_id();
     if (k >= blocks[b].nseg) return;
     const int idx = b * kMaxSegs + k;
     const SegPlan p = plan[idx];

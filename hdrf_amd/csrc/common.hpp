@@ -105,7 +105,33 @@ struct ClosedRec {           // a container closed during a batch
 };
 
 // ------------------------------------------------------------------------------------------
+// Global-address-space views: pointers that arrive inside structs are generic (flat) to the
+// compiler; flat loads also count in lgkmcnt and force vmcnt(0)-style waits.  Casting to
+// address_space(1) yields global_load_* with precise vmcnt accounting.
+#define HDRF_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ const HDRF_GLOBAL T *gptr(const void *p)
+{
+    return (const HDRF_GLOBAL T *)(p);
+}
+template <class T>
+__device__ __forceinline__ HDRF_GLOBAL T *gptr_w(void *p)
+{
+    return (HDRF_GLOBAL T *)(p);
+}
+
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+// 16-B global load (dword-aligned address is enough on gfx950)
+__device__ __forceinline__ uint4 ld16(const void *p)
+{
+    const u32x4v v = *(const HDRF_GLOBAL u32x4v *)(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t ld4(const void *p) { return *(const HDRF_GLOBAL uint32_t *)(p); }
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// wave index inside the workgroup, as a provably wave-uniform (scalar) value
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
 {
@@ -144,18 +170,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 __device__ __forceinline__ unsigned long long ballot64(bool p) { return __ballot(p); }
 
 // Bounds-checked 16-B load (bytes >= avail read as 0).
-__device__ __forceinline__ uint4 load16_guard(const uint8_t *base, int64_t off, int64_t avail)
+__device__ __noinline__ uint4 load16_guard(const uint8_t *base, int64_t off, int64_t avail)
 {
-    if (off + 16 <= avail) return *reinterpret_cast<const uint4 *>(base + off);
+    if (off + 16 <= avail) return ld16(base + off);
     uint32_t w[4] = {0, 0, 0, 0};
     for (int i = 0; i < 16; i++)
         if (off + i < avail) w[i >> 2] |= (uint32_t)base[off + i] << (8 * (i & 3));
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__device__ __forceinline__ uint32_t load4_guard(const uint8_t *base, int64_t off, int64_t avail)
+__device__ __noinline__ uint32_t load4_guard(const uint8_t *base, int64_t off, int64_t avail)
 {
-    if (off + 4 <= avail) return *reinterpret_cast<const uint32_t *>(base + off);
+    if (off + 4 <= avail) return ld4(base + off);
     uint32_t w = 0;
     for (int i = 0; i < 4; i++)
         if (off + i < avail) w |= (uint32_t)base[off + i] << (8 * i);

@@ -4,10 +4,16 @@
 // [off[k-1], off[k]) with utilities.sha1hash (hasher==0) or sha224hash (hasher==1),
 // DN/utilities.java:98-137 (nayuki native compress + FIPS 180-4 padding).
 //
-// One lane owns one chunk and runs its compression chain; the wave's 64 chunks are adjacent
-// in the block, so a wave streams a contiguous ~60 KiB region.  Each 64-B message block is
-// fetched as 17 dword-aligned dwords and realigned + byte-swapped with one v_perm_b32 per
-// word.  Rotations are v_alignbit_b32, Ch/Maj are v_bfi_b32.
+// Two kernels:
+//   sha_full — every FULL 64-B block of every chunk.  A lane owns one chunk's compression chain;
+//              a wave owns a pool of 64*kPool consecutive chunks and a lane that finishes its
+//              chunk immediately takes the next one from the pool (ballot + mbcnt), so lanes do
+//              not idle while the wave's longest chunk finishes.  No padding logic in this loop.
+//   sha_tail — one lane per chunk: the 1-2 padded final blocks (FIPS 180-4 padding) and the
+//              digest store.
+// Each 64-B block is fetched as 17 dword-aligned dwords (4 x dwordx4 + 1) and realigned +
+// byte-swapped with one v_perm_b32 per word.  Rotations are v_alignbit_b32, 3-way xor is
+// v_bitop3_b32 (gfx950), Ch/Maj lower to v_bfi/v_bitop3.
 #include "launchers.hpp"
 
 namespace hdrf {
@@ -17,18 +23,22 @@ typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // symmetric truth table: a ^ b ^ c
+}
 
 __device__ __forceinline__ void sha1_compress(uint32_t st[5], uint32_t w[16])
 {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4];
 #pragma unroll
     for (int i = 0; i < 80; i++) {
-        if (i >= 16) w[i & 15] = rotl(w[(i - 3) & 15] ^ w[(i - 8) & 15] ^ w[(i - 14) & 15] ^ w[i & 15], 1);
+        if (i >= 16) w[i & 15] = rotl(xor3(w[(i - 3) & 15], w[(i - 8) & 15], w[(i - 14) & 15]) ^ w[i & 15], 1);
         uint32_t f, k;
         if (i < 20)      { f = bfi(b, c, d);      k = 0x5A827999u; }
-        else if (i < 40) { f = b ^ c ^ d;         k = 0x6ED9EBA1u; }
+        else if (i < 40) { f = xor3(b, c, d);     k = 0x6ED9EBA1u; }
         else if (i < 60) { f = bfi(b ^ c, d, c);  k = 0x8F1BBCDCu; }
-        else             { f = b ^ c ^ d;         k = 0xCA62C1D6u; }
+        else             { f = xor3(b, c, d);     k = 0xCA62C1D6u; }
         const uint32_t t = rotl(a, 5) + f + e + k + w[i & 15];
         e = d; d = c; c = rotl(b, 30); b = a; a = t;
     }
@@ -52,13 +62,13 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16])
     for (int i = 0; i < 64; i++) {
         if (i >= 16) {
             const uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-            const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+            const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+            const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
             w[i & 15] = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
         }
-        const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+        const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
         const uint32_t t1 = h + S1 + bfi(e, f, g) + kK256[i] + w[i & 15];
-        const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+        const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
         const uint32_t t2 = S0 + bfi(a ^ b, c, b);
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
@@ -75,10 +85,10 @@ __device__ __forceinline__ void load_block(const uint8_t *base, int64_t avail, i
     const uint32_t sel = 0x00010203u + (uint32_t)(pos & 3) * 0x01010101u;
     uint32_t d[17];
     if (apos + 68 <= avail) {
-        const uint32_t *p = reinterpret_cast<const uint32_t *>(base + apos);
+        const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            u32x4a v = *reinterpret_cast<const u32x4a *>(p + 4 * q);
+            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
             d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
         }
         d[16] = p[16];
@@ -105,11 +115,103 @@ __device__ __forceinline__ void load_block(const uint8_t *base, int64_t avail, i
     }
 }
 
-template <int HW>   // digest words: 5 (SHA-1) or 7 (SHA-224)
-__global__ void __launch_bounds__(256) sha_kernel(const BlockDesc *__restrict__ blocks,
-                                                  const uint32_t *__restrict__ offsets,
-                                                  const BlockState *__restrict__ bst, int cap_blk,
-                                                  uint32_t *__restrict__ digests)
+// Full (unpadded) 64-B message block at byte `pos` of a block whose base is wave-uniform;
+// pos+68 <= len+4 <= readable, so no bounds guard is needed.
+__device__ __forceinline__ void load_full(const uint8_t *base, uint32_t pos, uint32_t m[16])
+{
+    const uint32_t apos = pos & ~3u;
+    const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
+    const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
+    uint32_t d[17];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+    d[16] = p[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+}
+
+template <int HW>
+__device__ __forceinline__ void set_iv(uint32_t st[8])
+{
+    if (HW == 5) {
+        st[0] = 0x67452301u; st[1] = 0xEFCDAB89u; st[2] = 0x98BADCFEu; st[3] = 0x10325476u; st[4] = 0xC3D2E1F0u;
+        st[5] = st[6] = st[7] = 0u;
+    } else {
+        st[0] = 0xc1059ed8u; st[1] = 0x367cd507u; st[2] = 0x3070dd17u; st[3] = 0xf70e5939u;
+        st[4] = 0xffc00b31u; st[5] = 0x68581511u; st[6] = 0x64f98fa7u; st[7] = 0xbefa4fa4u;
+    }
+}
+
+constexpr int kPool = 8;   // chunks per lane per wave pool
+
+// grid ((cap_blk + 256*kPool - 1) / (256*kPool), nblocks); 4 waves per workgroup, a pool each
+template <int HW>
+__global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restrict__ blocks,
+                                                       const uint32_t *__restrict__ offsets,
+                                                       const BlockState *__restrict__ bst, int cap_blk,
+                                                       uint32_t *__restrict__ mid)
+{
+    const int b = blockIdx.y;
+    const int c0 = (blockIdx.x * 4 + wave_id()) * 64 * kPool;
+    const int n = bst[b].n_chunks;
+    if (c0 >= n) return;
+    const int c1 = min(n, c0 + 64 * kPool);
+    const uint8_t *base = blocks[b].data;
+    const uint32_t *off = offsets + (size_t)b * cap_blk;
+    uint32_t *mb = mid + (size_t)b * cap_blk * 8;
+    const int l = lane_id();
+    int next = c0 + 64;
+    int k = c0 + l;
+    bool active = k < c1;
+    uint32_t pos = 0, r = 0;
+    uint32_t st[8];
+    set_iv<HW>(st);
+    if (active) {
+        pos = k ? off[k - 1] : 0u;
+        r = (off[k] - pos) >> 6;
+    }
+    for (;;) {
+        bool done = active && r == 0;
+        while (ballot64(done)) {                       // store finished chains, refill from the pool
+            if (done) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) mb[(size_t)k * 8 + i] = st[i];
+            }
+            const unsigned long long bal = ballot64(done);
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+            if (done) {
+                k = next + rank;
+                active = k < c1;
+                set_iv<HW>(st);
+                if (active) {
+                    pos = k ? off[k - 1] : 0u;
+                    r = (off[k] - pos) >> 6;
+                }
+            }
+            next += __popcll(bal);
+            done = active && r == 0;
+        }
+        if (!ballot64(active)) break;
+        if (active) {
+            uint32_t m[16];
+            load_full(base, pos, m);
+            if (HW == 5) sha1_compress(st, m);
+            else sha256_compress(st, m);
+            pos += 64;
+            r--;
+        }
+    }
+}
+
+// one lane per chunk: padded final block(s) + digest
+template <int HW>
+__global__ void __launch_bounds__(256) sha_tail_kernel(const BlockDesc *__restrict__ blocks,
+                                                       const uint32_t *__restrict__ offsets,
+                                                       const BlockState *__restrict__ bst, int cap_blk,
+                                                       const uint32_t *__restrict__ mid, uint32_t *__restrict__ digests)
 {
     const int b = blockIdx.y;
     const int k = blockIdx.x * 256 + threadIdx.x;
@@ -119,15 +221,13 @@ __global__ void __launch_bounds__(256) sha_kernel(const BlockDesc *__restrict__ 
     const uint32_t *off = offsets + (size_t)b * cap_blk;
     const int64_t start = k ? off[k - 1] : 0;
     const int len = (int)(off[k] - start);
-    const int nblk = (len + 8) / 64 + 1;
+    const int full = len >> 6;
+    const int nblk = (len + 8) / 64 + 1;              // total blocks incl. padding
     uint32_t st[8];
-    if (HW == 5) {
-        st[0] = 0x67452301u; st[1] = 0xEFCDAB89u; st[2] = 0x98BADCFEu; st[3] = 0x10325476u; st[4] = 0xC3D2E1F0u;
-    } else {
-        st[0] = 0xc1059ed8u; st[1] = 0x367cd507u; st[2] = 0x3070dd17u; st[3] = 0xf70e5939u;
-        st[4] = 0xffc00b31u; st[5] = 0x68581511u; st[6] = 0x64f98fa7u; st[7] = 0xbefa4fa4u;
-    }
-    for (int bi = 0; bi < nblk; bi++) {
+    const uint32_t *ms = mid + ((size_t)b * cap_blk + k) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = ms[i];
+    for (int bi = full; bi < nblk; bi++) {
         uint32_t m[16];
         load_block(bd.data, (int64_t)bd.readable, start, len, bi, nblk, m);
         if (HW == 5) sha1_compress(st, m);
@@ -139,12 +239,19 @@ __global__ void __launch_bounds__(256) sha_kernel(const BlockDesc *__restrict__ 
 }
 
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
-                      const BlockState *bst, int cap_blk, uint32_t *digests, hipStream_t st, Marker *mk)
+                      const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, hipStream_t st,
+                      Marker *mk)
 {
     mk->mark(st);
-    dim3 g((cap_blk + 255) / 256, nblocks);
-    if (hasher == 0) hipLaunchKernelGGL(sha_kernel<5>, g, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, digests);
-    else hipLaunchKernelGGL(sha_kernel<7>, g, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, digests);
+    dim3 gf((cap_blk + 256 * kPool - 1) / (256 * kPool), nblocks);
+    dim3 gt((cap_blk + 255) / 256, nblocks);
+    if (hasher == 0) {
+        hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid);
+        hipLaunchKernelGGL(sha_tail_kernel<5>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
+    } else {
+        hipLaunchKernelGGL(sha_full_kernel<7>, gf, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid);
+        hipLaunchKernelGGL(sha_tail_kernel<7>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
+    }
     return hipGetLastError();
 }
 

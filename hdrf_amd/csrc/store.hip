@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(256) flush_kernel(StoreParams P, const BlockSt
                                                     ClosedRec *__restrict__ closed, uint32_t *__restrict__ nclosed,
                                                     int *__restrict__ err)
 {
-    const int t = threadIdx.x >> 6;
+    const int t = wave_id();
     if (t >= P.n_thread) return;
     const int l = lane_id();
     // per-lane prefetch of block-level quantities (lane = block, up to 64)

@@ -1,0 +1,51 @@
+package org.apache.hadoop.hdfs.server.datanode;
+
+import java.io.IOException;
+import java.nio.ByteBuffer;
+
+/**
+ * MI355X backend: JNI over libhdrf.so (include/hdrf.h).  Selected where DataNode.compressor is
+ * tested (DataNode.java:438, BlockReceiver.java:822-879) in place of `new DDRunner(bf1, id)`.
+ * bf1 must be a direct ByteBuffer (BlockReceiver.java:877 allocates it with allocateDirect).
+ */
+public final class HipReductionScheme extends ReductionScheme {
+  static { System.loadLibrary("hdrf_jni"); }   // libhdrf_jni.so -> libhdrf.so
+
+  private long ctx;                            // hdrf_ctx*
+
+  public HipReductionScheme(int hasher, int device, long maxBlockBytes) throws IOException {
+    ctx = open0(hasher, device, maxBlockBytes);
+  }
+
+  @Override
+  public void reduce(ByteBuffer block, long blockId) throws IOException {
+    if (!block.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
+    reduce0(ctx, block, block.position(), blockId);   // H2D copy happens before return
+  }
+
+  @Override
+  public byte[] reconstruct(long blockId) throws IOException {
+    throw new IOException("reconstruction not implemented in this build (hdrf: HDRF_E_UNSUPPORTED)");
+  }
+
+  @Override
+  public long length(long blockId) throws IOException {
+    return length0(ctx, blockId);
+  }
+
+  /** GET blockId -> recipe [BE32 size | digests] (storeDB, DataDeduplicator.java:372-392). */
+  public byte[] recipe(long blockId) throws IOException {
+    return recipe0(ctx, blockId);
+  }
+
+  @Override
+  public void close() {
+    if (ctx != 0) { close0(ctx); ctx = 0; }
+  }
+
+  private static native long open0(int hasher, int device, long maxBlockBytes) throws IOException;
+  private static native void reduce0(long ctx, ByteBuffer direct, int len, long blockId) throws IOException;
+  private static native long length0(long ctx, long blockId) throws IOException;
+  private static native byte[] recipe0(long ctx, long blockId) throws IOException;
+  private static native void close0(long ctx);
+}

@@ -1,0 +1,77 @@
+/* hdrf_jni.c — JNI shim for HipReductionScheme over libhdrf.so (C-ABI in include/hdrf.h).
+ * Build (on a host with a JDK):
+ *   cc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
+ *      integration/jni/hdrf_jni.c -Lhdrf_amd/_build -lhdrf -o libhdrf_jni.so
+ * Errors become IOException; DDRunner-style callers may log and continue (DDRunner.java:27-31). */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "hdrf.h"
+
+static void throw_io(JNIEnv *env, hdrf_ctx *ctx, int rc)
+{
+    char msg[512];
+    snprintf(msg, sizeof msg, "hdrf error %d: %s", rc, ctx ? hdrf_last_error(ctx) : "open failed");
+    jclass c = (*env)->FindClass(env, "java/io/IOException");
+    if (c) (*env)->ThrowNew(env, c, msg);
+}
+
+#define JFN(name) Java_org_apache_hadoop_hdfs_server_datanode_HipReductionScheme_##name
+
+JNIEXPORT jlong JNICALL JFN(open0)(JNIEnv *env, jclass cls, jint hasher, jint device, jlong max_block)
+{
+    (void)cls;
+    hdrf_cfg cfg;
+    hdrf_default_cfg(&cfg);
+    cfg.hasher = hasher;              /* DataNode.hasher  (DataNode.java:446) */
+    cfg.compressor = 1;               /* dedup only (DataNode.java:438) */
+    cfg.device = device;
+    cfg.max_block_bytes = max_block;  /* dfs.blocksize */
+    cfg.max_batch_blocks = 1;
+    hdrf_ctx *ctx = NULL;
+    int rc = hdrf_open(&cfg, &ctx);
+    if (rc) { throw_io(env, NULL, rc); return 0; }
+    return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void JNICALL JFN(reduce0)(JNIEnv *env, jclass cls, jlong h, jobject buf, jint len, jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
+    if (!p) { throw_io(env, ctx, HDRF_E_INVAL); return; }
+    int rc = hdrf_reduce_block(ctx, (uint64_t)id, p, (uint64_t)len, NULL);
+    if (rc) throw_io(env, ctx, rc);
+}
+
+JNIEXPORT jlong JNICALL JFN(length0)(JNIEnv *env, jclass cls, jlong h, jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int64_t n = hdrf_block_length(ctx, (uint64_t)id);
+    if (n < 0) throw_io(env, ctx, (int)n);
+    return (jlong)n;
+}
+
+JNIEXPORT jbyteArray JNICALL JFN(recipe0)(JNIEnv *env, jclass cls, jlong h, jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int64_t len = hdrf_block_length(ctx, (uint64_t)id);
+    if (len < 0) return NULL;
+    int64_t cap = 4 + (int64_t)hdrf_digest_len(ctx) * (len / 702 + 2);
+    uint8_t *tmp = (uint8_t *)malloc((size_t)cap);
+    int64_t n = hdrf_recipe_get(ctx, (uint64_t)id, tmp, cap);
+    if (n < 0) { free(tmp); throw_io(env, ctx, (int)n); return NULL; }
+    jbyteArray out = (*env)->NewByteArray(env, (jsize)n);
+    (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);
+    free(tmp);
+    return out;
+}
+
+JNIEXPORT void JNICALL JFN(close0)(JNIEnv *env, jclass cls, jlong h)
+{
+    (void)env; (void)cls;
+    hdrf_close((hdrf_ctx *)(intptr_t)h);
+}
