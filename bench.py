@@ -123,10 +123,10 @@ def main():
     nbatch = len(batches)
     chunks_step = int(n_chunks.sum())
     new_bytes = int(store.sum())
-    per_launch = {   # algorithmic HBM bytes per launch (DESIGN.md §Roofline)
+    per_launch = {   # algorithmic HBM bytes per launch (DESIGN.md §5)
         STAGES[0]: (nb * S + 4 * chunks_step) / nbatch,                 # read block bytes, write cuts
-        STAGES[2]: (nb * S + 24 * chunks_step) / nbatch,                # read chunk bytes + offsets, write digests
-        STAGES[7]: (2 * new_bytes + 16 * chunks_step) / nbatch,         # read+write new bytes, chunk metadata
+        STAGES[2]: (nb * S + 40 * chunks_step) / nbatch,                # read chunk bytes + offsets, write mid-state
+        STAGES[9]: (2 * new_bytes + 16 * chunks_step) / nbatch,         # read+write new bytes, chunk metadata
     }
     stages = {}
     for name, ms in zip(STAGES, stage_ms):

@@ -48,6 +48,20 @@ __device__ __forceinline__ uint32_t swar_ge(uint32_t w, uint32_t C)
     return ((w & C) | ((w | C) & s)) & 0x80808080u;
 }
 
+// 16-bit mask of the bytes of a biased granule equal to 0xFF (raw 0x7F = signed 127, the
+// largest possible byte); exact zero-byte test on ~v, then bits 7/15/23/31 packed into a nibble
+__device__ __forceinline__ uint32_t ff_nibble(uint32_t v)
+{
+    const uint32_t z = ~v;
+    uint32_t t = ((z & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z | 0x7f7f7f7fu;
+    t = (~t) >> 7;                                   // bits 0, 8, 16, 24
+    return (t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xfu;
+}
+__device__ __forceinline__ uint32_t ffmask16(uint4 v)
+{
+    return ff_nibble(v.x) | (ff_nibble(v.y) << 4) | (ff_nibble(v.z) << 8) | (ff_nibble(v.w) << 12);
+}
+
 // keep bytes i (0..3) with a <= i <= b, as bit-7 flags
 __device__ __forceinline__ uint32_t byte_range_mask(int a, int b)
 {
@@ -65,7 +79,8 @@ struct Walker {
     int T;         // tile A base (multiple of 1024)
     uint4 A, B;      // biased view [T, T+2048)
     uint4 C, D;      // raw prefetch of [T+2048, T+4096)
-    uint32_t gA, gB;
+    uint32_t gA, gB;   // granule max (biased)
+    uint32_t fA, fB;   // granule 0xFF-byte masks (biased 0xFF = raw 0x7F)
 
     // raw (unbiased) tile load; the bias is applied when the tile is promoted into the view so
     // the load stays in flight (a use right after the load would force s_waitcnt vmcnt(0))
@@ -87,13 +102,14 @@ struct Walker {
         A = tile_raw(T); B = tile_raw(T + 1024); C = tile_raw(T + 2048); D = tile_raw(T + 3072);
         A = bias(A); B = bias(B);
         gA = gmax16(A); gB = gmax16(B);
+        fA = ffmask16(A); fB = ffmask16(B);
     }
 
     __device__ __forceinline__ void advance()
     {
         T += 1024;
-        A = B; gA = gB;
-        B = bias(C); gB = gmax16(B);
+        A = B; gA = gB; fA = fB;
+        B = bias(C); gB = gmax16(B); fB = ffmask16(B);
         C = D;
         D = tile_raw(T + 3072);
     }
@@ -154,6 +170,35 @@ struct Walker {
         h = swar_ge(w3, C) & byte_range_mask(lo - 12, hi - 12);
         if (h) return 12 + (__builtin_ctz(h) >> 3);
         return -1;
+    }
+
+    // first j in [x, lim] whose biased byte is 0xFF (raw 0x7F); may advance tiles. -1 if none.
+    // Fast path of the chain: when the window holds such a byte, M(p) = 127 is the largest
+    // possible value and the cut is simply the next 0x7F byte after the window.
+    __device__ __forceinline__ int next_ff(int x, int lim)
+    {
+        const int l = lane_id();
+        for (;;) {
+            const int vend = T + 2047;
+            const int hi = min(lim, vend);
+            if (x <= hi) {
+                const int g = (x - T) >> 4, o = (x - T) & 15;
+                const uint32_t a = (l > g) ? fA : ((l == g) ? (fA & (0xffffu << o)) : 0u);
+                const uint32_t c = (l + 64 > g) ? fB : ((l + 64 == g) ? (fB & (0xffffu << o)) : 0u);
+                const unsigned long long ba = ballot64(a != 0u), bb = ballot64(c != 0u);
+                if (ba | bb) {
+                    int L;
+                    uint32_t bits;
+                    if (ba) { L = __builtin_ctzll(ba); bits = rdlane(a, L); }
+                    else { L = __builtin_ctzll(bb); bits = rdlane(c, L); L += 64; }
+                    const int pos = T + 16 * L + __builtin_ctz(bits);
+                    return pos <= hi ? pos : -1;
+                }
+            }
+            if (lim <= vend) return -1;
+            advance();
+            x = max(x, T + 1024);
+        }
     }
 
     // first j in [q, lim] with biased byte >= m; may advance tiles. -1 if none.
@@ -218,9 +263,14 @@ __device__ __forceinline__ bool walk_chain(Walker &W, int p, bool first, ListSin
         while (p >= W.T + 1024) W.advance();
         const int e = p + W.w;
         if (e >= W.size) return true;                    // window incomplete: no more cuts
-        const uint32_t m = W.window_max(p, first);
         const int lim = min(p + W.maxlen, W.size - 1);
-        const int j = W.find(e + 1, lim, m);
+        int j;
+        if (W.next_ff(p, e) >= 0) {
+            j = W.next_ff(e + 1, lim);                    // M(p) = 127: next 0x7F byte
+        } else {
+            const uint32_t m = W.window_max(p, first);
+            j = W.find(e + 1, lim, m);
+        }
         int cut;
         if (j >= 0) cut = j + 1;                         // :276-283
         else if (p + W.maxlen <= W.size - 1) cut = p + W.maxlen + 1;   // :288-294

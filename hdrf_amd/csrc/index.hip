@@ -193,6 +193,7 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
     (void)hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st);
     if (hasher == 0) {
         hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
+        mk->mark(st);
         hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
                            coll_cap, err);
         mk->mark(st);
@@ -200,6 +201,7 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                            coll, ncoll, coll_cap, err);
     } else {
         hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
+        mk->mark(st);
         hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
                            coll_cap, err);
         mk->mark(st);

@@ -6,7 +6,7 @@ namespace hdrf {
 
 // Stage markers: when timing is on, a HIP event is recorded on the launch stream at every
 // stage boundary (kernels of one stream run in order, so event deltas are kernel times).
-constexpr int kNumStages = 8;   // walk, stitch, sha, index(claim+apply), index(slow+decide), scan, flush, place
+constexpr int kNumStages = 11;  // walk, stitch, sha_full, sha_tail, claim, apply, slow+decide, scan, flush, place, (spare)
 struct Marker {
     hipEvent_t *ev = nullptr;   // kNumStages + 1 events
     int next = 0;

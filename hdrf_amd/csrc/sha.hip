@@ -247,9 +247,11 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     dim3 gt((cap_blk + 255) / 256, nblocks);
     if (hasher == 0) {
         hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid);
+        mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<5>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     } else {
         hipLaunchKernelGGL(sha_full_kernel<7>, gf, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid);
+        mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<7>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     }
     return hipGetLastError();

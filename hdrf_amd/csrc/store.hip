@@ -290,6 +290,7 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
     hipLaunchKernelGGL(place_kernel, g, dim3(256), 0, st, P, d_blocks, bst, offsets, flags, pre, rstate, events, slot,
                        tab, arena, place_cid, place_pos);
     mk->mark(st);
+    mk->mark(st);   // spare stage (kept so stage indices stay stable)
     return hipGetLastError();
 }
 

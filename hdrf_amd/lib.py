@@ -29,9 +29,10 @@ EXPORTS = [
 
 
 # per-stage timers of hdrf_stage_times (kernel names in parentheses)
-STAGES = ["walk(spec_walk_kernel)", "stitch(spec_sync/plan/copy/fallback)", "sha(sha_kernel)",
-          "index_claim_apply", "index_slow_decide", "scan(tile/chunk)", "flush(flush_kernel)",
-          "place(place_kernel)"]
+STAGES = ["walk(spec_walk_kernel)", "stitch(spec_sync/plan/copy/fallback)", "sha_full(sha_full_kernel)",
+          "sha_tail(sha_tail_kernel)", "index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
+          "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
+          "place(place_kernel)", "spare"]
 
 
 class HdrfError(RuntimeError):

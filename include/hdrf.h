@@ -119,9 +119,9 @@ int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, in
                      int64_t segs_per_block, int64_t seg_bytes, uint64_t seed);
 
 /* Per-stage device time (ms) accumulated since the last reset, measured with HIP events on
- * the context's stream (cfg.timing = 1): [0] chunk walk (spec_walk_kernel), [1] chunk stitch
- * (sync/plan/copy/fallback), [2] fingerprint (sha_kernel), [3] index claim+apply, [4] index
- * slow-path+decide, [5] new-byte scans, [6] container flush walk, [7] place+gather+finalise. */
+ * the context's stream (cfg.timing = 1): [0] spec_walk_kernel, [1] stitch (sync/plan/copy/
+ * fallback), [2] sha_full_kernel, [3] sha_tail_kernel, [4] idx_claim_kernel, [5] idx_apply_kernel,
+ * [6] idx_slow+decide, [7] new-byte scans, [8] flush_kernel, [9] place_kernel, [10] spare. */
 int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
 /* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis). */
 int hdrf_reset(hdrf_ctx *ctx);
