@@ -179,26 +179,52 @@ __global__ void __launch_bounds__(256) flush_kernel(StoreParams P, const BlockSt
     }
 }
 
-// wave-cooperative unaligned copy (4-B words, src realigned with v_alignbyte)
-__device__ __forceinline__ void wave_copy(uint8_t *dst, const uint8_t *src, int len)
+// 16 output bytes from an arbitrarily aligned source: two aligned 16-B loads + a funnel shift by
+// sh = src & 15 (uniform per run, since destination words are 16-B aligned within a run).
+__device__ __forceinline__ uint4 load16_shift(const uint8_t *src_aligned, int sh)
 {
-    const int l = lane_id();
-    int h = (int)((4 - ((uintptr_t)dst & 3)) & 3);
-    if (h > len) h = len;
-    if (l < h) dst[l] = src[l];
-    const int body = (len - h) >> 2;
-    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + h);
-    const uintptr_t sa = (uintptr_t)(src + h);
-    const int sh = (int)(sa & 3);
-    const uint32_t *sw = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
-    if (sh == 0) {
-        for (int i = l; i < body; i += 64) dw[i] = sw[i];
-    } else {
-        for (int i = l; i < body; i += 64) dw[i] = __builtin_amdgcn_alignbyte(sw[i + 1], sw[i], sh);
+    const uint4 x = ld16(src_aligned);
+    if (sh == 0) return x;
+    const uint4 y = ld16(src_aligned + 16);
+    const uint32_t r = (uint32_t)(sh & 3);
+#define AB(hi, lo) __builtin_amdgcn_alignbyte((hi), (lo), r)
+    switch (sh >> 2) {                                   // uniform per run
+    case 0: return make_uint4(AB(x.y, x.x), AB(x.z, x.y), AB(x.w, x.z), AB(y.x, x.w));
+    case 1: return make_uint4(AB(x.z, x.y), AB(x.w, x.z), AB(y.x, x.w), AB(y.y, y.x));
+    case 2: return make_uint4(AB(x.w, x.z), AB(y.x, x.w), AB(y.y, y.x), AB(y.z, y.y));
+    default: return make_uint4(AB(y.x, x.w), AB(y.y, y.x), AB(y.z, y.y), AB(y.w, y.z));
     }
-    const int tb = h + (body << 2);
-    const int tail = len - tb;
-    if (l < tail) dst[tb + l] = src[tb + l];
+#undef AB
+}
+
+__device__ __forceinline__ void st16(void *p, uint4 v)
+{
+    u32x4v w = {v.x, v.y, v.z, v.w};
+    *(HDRF_GLOBAL u32x4v *)p = w;
+}
+
+// workgroup-cooperative copy of one contiguous run (16-B aligned destination stores)
+__device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32_t len)
+{
+    const int t = threadIdx.x;
+    uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
+    if (head > len) head = len;
+    if ((uint32_t)t < head) dst[t] = src[t];
+    uint8_t *d = dst + head;
+    const uint8_t *sp = src + head;
+    const uint32_t n16 = (len - head) >> 4;
+    const int sh = (int)((uintptr_t)sp & 15);
+    const uint8_t *sa = sp - sh;
+    uint32_t i = t;
+    for (; i + 256 < n16; i += 512) {               // two 16-B words per thread in flight
+        const uint4 v0 = load16_shift(sa + 16 * (size_t)i, sh);
+        const uint4 v1 = load16_shift(sa + 16 * (size_t)(i + 256), sh);
+        st16(d + 16 * (size_t)i, v0);
+        st16(d + 16 * (size_t)(i + 256), v1);
+    }
+    for (; i < n16; i += 256) st16(d + 16 * (size_t)i, load16_shift(sa + 16 * (size_t)i, sh));
+    const uint32_t tb = head + 16 * n16;
+    if ((uint32_t)t < len - tb) dst[tb + t] = src[tb + t];
 }
 
 // ---- place: grid (ntiles, nblocks) ------------------------------------------------------
@@ -262,13 +288,38 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
             e->first = 0;
         }
     }
-    // cooperative copy of this wave's new chunks
-    unsigned long long todo = ballot64(do_copy);
-    while (todo) {
-        const int j = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        const uint32_t js = rdlane(start, j), jl = rdlane(len, j), jp = rdlane(pos, j), jslot = rdlane(aslot, j);
-        wave_copy(arena + (size_t)jslot * P.cmax + jp, bd.data + js, (int)jl);
+    // ---- runs: consecutive new chunks of this tile that are contiguous in one container are
+    //      one contiguous source span and one contiguous destination span -> one copy each
+    __shared__ uint32_t s_cid[256], s_pend[256], s_flag[256];
+    __shared__ uint32_t r_src[256], r_end[256], r_dst_lo[256], r_dst_hi[256];
+    __shared__ uint32_t s_wsum[4];
+    const int tid = threadIdx.x;
+    s_cid[tid] = do_copy ? cid : 0xffffffffu;
+    s_pend[tid] = pos + len;
+    __syncthreads();
+    const bool cont = do_copy && tid > 0 && s_cid[tid - 1] == cid && s_pend[tid - 1] == pos;
+    const bool rstart = do_copy && !cont;
+    s_flag[tid] = cont ? 1u : 0u;
+    // exclusive scan of run starts (wave scan + cross-wave sums)
+    const uint32_t incl = wave_incl_scan(rstart ? 1u : 0u);
+    if (lane_id() == 63) s_wsum[tid >> 6] = incl;
+    __syncthreads();
+    uint32_t base_idx = 0;
+    for (int i = 0; i < (tid >> 6); i++) base_idx += s_wsum[i];
+    const uint32_t nruns = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    const uint32_t ridx = base_idx + incl - (rstart ? 1u : 0u);
+    if (rstart) {
+        const uint64_t dsto = (uint64_t)aslot * P.cmax + pos;
+        r_src[ridx] = start;
+        r_dst_lo[ridx] = (uint32_t)dsto;
+        r_dst_hi[ridx] = (uint32_t)(dsto >> 32);
+    }
+    const bool last = do_copy && !(tid + 1 < 256 && s_flag[tid + 1]);
+    if (last) r_end[base_idx + incl - 1] = start + len;       // run index of this (continuing) run
+    __syncthreads();
+    for (uint32_t r = 0; r < nruns; r++) {
+        const uint64_t dsto = ((uint64_t)r_dst_hi[r] << 32) | r_dst_lo[r];
+        wg_copy(arena + dsto, bd.data + r_src[r], r_end[r] - r_src[r]);
     }
 }
 
