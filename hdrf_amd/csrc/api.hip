@@ -54,7 +54,7 @@ struct hdrf_ctx {
     IndexEntry *d_tab = nullptr;
     uint8_t *d_arena = nullptr;
     AllocState *d_alloc = nullptr;
-    uint32_t *d_pcid = nullptr, *d_ppos = nullptr;
+    uint32_t *d_pcid = nullptr, *d_ppos = nullptr, *d_queue = nullptr;
     int *d_err = nullptr;
     uint8_t *d_stage = nullptr;
     uint64_t stage_cap = 0;
@@ -84,6 +84,12 @@ struct hdrf_ctx {
             return HDRF_E_HIP;                                                         \
         }                                                                              \
     } while (0)
+
+static unsigned long long tag_mask(const hdrf_ctx *ctx)
+{
+    const int bits = ctx->cfg.debug_tag_bits;
+    return (bits <= 0 || bits >= 64) ? ~0ull : ((1ull << bits) - 1);
+}
 
 static int set_err(hdrf_ctx *ctx, int code, const std::string &msg)
 {
@@ -130,7 +136,7 @@ static void free_all(hdrf_ctx *ctx)
     void *ptrs[] = {ctx->d_blocks, ctx->d_spec, ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off,
                     ctx->d_dig, ctx->d_mid, ctx->d_slot, ctx->d_pre, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
                     ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed, ctx->d_coll, ctx->d_ncoll, ctx->d_tab,
-                    ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_err, ctx->d_stage};
+                    ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_queue, ctx->d_err, ctx->d_stage};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (auto &e : ctx->ev)
@@ -167,8 +173,9 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     const hdrf_cfg &c = *cfg_in;
     if ((c.hasher != 0 && c.hasher != 1) || c.window < 32 || c.window > 1000 || c.max_chunk <= c.window ||
         c.n_thread < 1 || c.n_thread > 3 || c.max_batch_blocks < 1 || c.max_batch_blocks > kMaxBatch ||
-        c.index_log2 < 10 || c.index_log2 > 32 || c.arena_slots < 8 || c.max_block_bytes < 1 ||
-        c.max_block_bytes > (1ll << 30) || c.container_max <= (uint32_t)c.max_chunk + 1 || c.segment_bytes < (1 << 16))
+        c.index_log2 < 10 || c.index_log2 > 31 || c.arena_slots < 8 || c.max_block_bytes < 1 ||
+        c.max_block_bytes > (1ll << 30) || c.container_max <= (uint32_t)c.max_chunk + 1 || c.segment_bytes < (1 << 16) ||
+        c.debug_tag_bits < 0 || c.debug_tag_bits > 64 || (c.debug_tag_bits && c.hasher != 0))
         return HDRF_E_INVAL;
     if (c.compressor != 1) return HDRF_E_UNSUPPORTED;
     hdrf_ctx *ctx = new (std::nothrow) hdrf_ctx();
@@ -206,7 +213,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         (rc = dalloc(ctx, &ctx->d_tab, (size_t)1 << c.index_log2)) ||
         (rc = dalloc(ctx, &ctx->d_arena, (size_t)c.arena_slots * c.container_max + 256)) ||
         (rc = dalloc(ctx, &ctx->d_alloc, 1)) || (rc = dalloc(ctx, &ctx->d_pcid, nchunk)) ||
-        (rc = dalloc(ctx, &ctx->d_ppos, nchunk)) || (rc = dalloc(ctx, &ctx->d_err, 1))) {
+        (rc = dalloc(ctx, &ctx->d_ppos, nchunk)) || (rc = dalloc(ctx, &ctx->d_queue, 64)) || (rc = dalloc(ctx, &ctx->d_err, 1))) {
         fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
         free_all(ctx);
         delete ctx;
@@ -286,10 +293,10 @@ extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
     HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
                           ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
     HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_mid, ctx->d_dig,
-                     st, &mk));
+                     ctx->d_queue, st, &mk));
     HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_tab, c.index_log2,
-                       cur, ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags, ctx->d_tilesum,
-                       ctx->ntiles, ctx->d_err, st, &mk));
+                       cur, tag_mask(ctx), ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags,
+                       ctx->d_tilesum, ctx->ntiles, ctx->d_err, st, &mk));
     StoreParams P;
     P.nblocks = nblocks; P.cap_blk = ctx->cap_blk; P.ntiles = ctx->ntiles;
     P.n_thread = c.n_thread; P.min_mt = c.min_mt_chunks; P.cmax = c.container_max;
@@ -464,9 +471,13 @@ static void encode_value(const IndexEntry &e, uint8_t v[11])
 
 static void entry_digest(const IndexEntry &e, int H, uint8_t *out)
 {
-    unsigned long long tag = (e.batch & 0x80000000u) ? 0ull : e.tag;
-    std::memcpy(out, &tag, 8);
-    std::memcpy(out + 8, e.dig, H - 8);
+    if (H == 20) {                                   // SHA-1: bytes 0..7 kept in dig[3..4]
+        std::memcpy(out, &e.dig[3], 8);
+    } else {
+        unsigned long long tag = (e.batch & 0x80000000u) ? 0ull : e.tag;
+        std::memcpy(out, &tag, 8);
+    }
+    std::memcpy(out + 8, e.dig, H == 20 ? 12 : H - 8);
 }
 
 extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out11[11])
@@ -474,6 +485,7 @@ extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out1
     if (!ctx || !digest) return HDRF_E_INVAL;
     unsigned long long tag;
     std::memcpy(&tag, digest, 8);
+    tag &= tag_mask(ctx);
     const uint32_t z = tag == 0 ? 0x80000000u : 0u;
     if (tag == 0) tag = 1;
     const uint64_t mask = (1ull << ctx->cfg.index_log2) - 1;
@@ -483,7 +495,9 @@ extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out1
         IndexEntry e;
         HIPCK(hipMemcpy(&e, ctx->d_tab + h, sizeof e, hipMemcpyDeviceToHost));
         if (e.tag == 0) return 0;
-        if (e.tag == tag && (e.batch & 0x80000000u) == z && std::memcmp(e.dig, digest + 8, ctx->H - 8) == 0) {
+        uint8_t full[28];
+        entry_digest(e, ctx->H, full);
+        if (e.tag == tag && (e.batch & 0x80000000u) == z && std::memcmp(full, digest, ctx->H) == 0) {
             if (out11) encode_value(e, out11);
             return 1;
         }

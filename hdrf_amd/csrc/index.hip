@@ -19,9 +19,13 @@
 
 namespace hdrf {
 
-__device__ __forceinline__ unsigned long long make_tag(const uint32_t *dw, uint32_t &zflag)
+// tag = first 8 digest bytes (masked by tag_mask: all ones except under the collision test hook);
+// a zero tag is remapped to 1 with bit 31 of `batch` set.  For SHA-1 the entry's spare dig[3..4]
+// also hold digest bytes 0..7, so verification never depends on the tag alone.
+__device__ __forceinline__ unsigned long long make_tag(const uint32_t *dw, uint32_t &zflag,
+                                                       unsigned long long tag_mask)
 {
-    unsigned long long t = (unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32);
+    unsigned long long t = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
     zflag = (t == 0) ? 0x80000000u : 0u;
     return t == 0 ? 1ull : t;
 }
@@ -38,15 +42,41 @@ __device__ __forceinline__ bool entry_matches(const IndexEntry &e, const uint32_
 #pragma unroll
     for (int i = 2; i < HW; i++)
         if (e.dig[i - 2] != dw[i]) return false;
+    if (HW == 5 && (e.dig[3] != dw[0] || e.dig[4] != dw[1])) return false;
     return true;
 }
 
+// Block b holds the digest: set its batch-mask bit.  Only a REPEAT inside one block (the bit was
+// already set) records its key in `first` = max((63-b)<<32 | k+1); decide completes the max over
+// the minimum block's occurrences when that block has repeats.  One returning atomic per chunk.
+__device__ __forceinline__ void record_occurrence(IndexEntry *e, int b, int k)
+{
+    const unsigned long long bit = 1ull << b;
+    const unsigned long long old = atomicOr(&e->mask, bit);
+    if (old & bit) atomicMax(&e->first, ((unsigned long long)(63 - b) << 32) | (unsigned)(k + 1));
+}
+
+template <int HW>
+__device__ __forceinline__ void store_dig(IndexEntry *e, const uint32_t *dw)
+{
+#pragma unroll
+    for (int i = 2; i < HW; i++) e->dig[i - 2] = dw[i];
+    if (HW == 5) { e->dig[3] = dw[0]; e->dig[4] = dw[1]; }
+}
+
 // ---- claim: grid (ceil(cap_blk/256), nblocks) ---------------------------------------------
+// Probe by tag; CAS-claim empty slots.  The chunk's block bit / last occurrence are applied right
+// here when the digest is known to match: the claimer (its digest IS the entry's), or an entry
+// created by an earlier batch (its digest bytes are immutable).  Only tag hits on entries created
+// in this batch by another lane are deferred to apply (their digest bytes may not be visible yet).
+// flags bit 3 = applied.
 template <int HW>
 __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                         const uint32_t *__restrict__ digests,
                                                         IndexEntry *__restrict__ tab, int log2cap, uint32_t cur,
-                                                        uint32_t *__restrict__ slot, int *__restrict__ err)
+                                                        unsigned long long tag_mask,
+                                                        uint32_t *__restrict__ slot, uint8_t *__restrict__ flags,
+                                                        int *__restrict__ err)
 {
     const int b = blockIdx.y;
     const int k = blockIdx.x * 256 + threadIdx.x;
@@ -56,9 +86,10 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
     uint32_t z;
-    const unsigned long long tag = make_tag(dw, z);
+    const unsigned long long tag = make_tag(dw, z, tag_mask);
     const uint64_t mask = (1ull << log2cap) - 1;
     uint64_t h = home_slot(tag, log2cap);
+    bool mine = false;
     for (uint64_t probe = 0;; probe++) {
         if (probe > mask) { atomicOr(err, 2); return; }           // table full
         IndexEntry *e = tab + h;
@@ -67,8 +98,8 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
             unsigned long long old = atomicCAS(&e->tag, kEmptyTag, tag);
             if (old == kEmptyTag) {
                 e->batch = cur | z;
-#pragma unroll
-                for (int i = 2; i < 7; i++) e->dig[i - 2] = i < HW ? dw[i] : 0u;
+                store_dig<HW>(e, dw);
+                mine = true;
                 break;
             }
             t = old;
@@ -77,13 +108,23 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
         h = (h + 1) & mask;
     }
     slot[c] = (uint32_t)h;
+    IndexEntry *e = tab + h;
+    bool apply = mine;
+    if (!mine) {
+        // batch only moves 0 -> cur inside this launch; a stale 0 just defers the chunk
+        const uint32_t bt = e->batch & 0x7fffffffu;
+        apply = bt != 0 && bt != cur && entry_matches<HW>(*e, dw, z);
+    }
+    if (apply) record_occurrence(e, b, k);
+    flags[c] = apply ? 8 : 0;
 }
 
-// ---- apply: verify full digest, record block membership / last occurrence ----------------
+// ---- apply: deferred chunks — verify full digest, record block membership / last occurrence
 template <int HW>
 __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                         const uint32_t *__restrict__ digests,
                                                         IndexEntry *__restrict__ tab, const uint32_t *__restrict__ slot,
+                                                        const uint8_t *__restrict__ flags, unsigned long long tag_mask,
                                                         uint32_t *__restrict__ coll, uint32_t *__restrict__ ncoll,
                                                         int coll_cap, int *__restrict__ err)
 {
@@ -91,15 +132,15 @@ __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__rest
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= bst[b].n_chunks) return;
     const size_t c = (size_t)b * cap_blk + k;
+    if (flags[c] & 8) return;
     uint32_t dw[HW];
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
     uint32_t z;
-    (void)make_tag(dw, z);
+    (void)make_tag(dw, z, tag_mask);
     IndexEntry *e = tab + slot[c];
     if (entry_matches<HW>(*e, dw, z)) {
-        atomicOr(&e->mask, 1ull << b);
-        atomicMax(&e->first, ((unsigned long long)(63 - b) << 32) | (unsigned)k);
+        record_occurrence(e, b, k);
     } else {
         uint32_t i = atomicAdd(ncoll, 1u);
         if ((int)i < coll_cap) coll[i] = (uint32_t)c;
@@ -110,7 +151,7 @@ __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__rest
 // ---- slow path: one thread, exact sequential re-probe of tag-collided chunks --------------
 template <int HW>
 __global__ void idx_slow_kernel(int cap_blk, const uint32_t *__restrict__ digests, IndexEntry *__restrict__ tab,
-                                int log2cap, uint32_t cur, uint32_t *__restrict__ slot,
+                                int log2cap, uint32_t cur, unsigned long long tag_mask, uint32_t *__restrict__ slot,
                                 const uint32_t *__restrict__ coll, const uint32_t *__restrict__ ncoll, int coll_cap,
                                 int *__restrict__ err)
 {
@@ -123,14 +164,14 @@ __global__ void idx_slow_kernel(int cap_blk, const uint32_t *__restrict__ digest
         uint32_t dw[HW];
         for (int q = 0; q < HW; q++) dw[q] = digests[(size_t)c * HW + q];
         uint32_t z;
-        const unsigned long long tag = make_tag(dw, z);
+        const unsigned long long tag = make_tag(dw, z, tag_mask);
         uint64_t h = (slot[c] + 1) & mask;
         for (uint64_t probe = 0;; probe++) {
             if (probe > mask) { *err |= 2; return; }
             IndexEntry *e = tab + h;
             if (e->tag == kEmptyTag) {
                 e->tag = tag; e->batch = cur | z; e->mask = 0; e->first = 0;
-                for (int q = 2; q < 7; q++) e->dig[q - 2] = q < HW ? dw[q] : 0u;
+                store_dig<HW>(e, dw);
                 break;
             }
             if (e->tag == tag && entry_matches<HW>(*e, dw, z)) break;
@@ -138,18 +179,21 @@ __global__ void idx_slow_kernel(int cap_blk, const uint32_t *__restrict__ digest
         }
         slot[c] = (uint32_t)h;
         IndexEntry *e = tab + h;
-        e->mask |= 1ull << b;
-        const unsigned long long f = ((unsigned long long)(63 - b) << 32) | (unsigned)k;
-        if (f > e->first) e->first = f;
+        const unsigned long long bit = 1ull << b;
+        if (e->mask & bit) {
+            const unsigned long long f = ((unsigned long long)(63 - b) << 32) | (unsigned)(k + 1);
+            if (f > e->first) e->first = f;
+        }
+        e->mask |= bit;
     }
 }
 
 // ---- decide: is_new / designated + per-tile new-byte sums ---------------------------------
-// flags bit0 = is_new, bit1 = designated (writes the final index value), bit2 = entry created
-// this batch.  tilesum[b][tile] = sum of new-chunk lengths of the 256 chunks of this workgroup.
+// flags bit0 = is_new, bit1 = in the entry's min block, bit2 = entry created this batch,
+// bit4 = the min block repeats the digest (designated = its last occurrence, see place_kernel).  tilesum[b][tile] = sum of new-chunk lengths of the 256 chunks of this workgroup.
 __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                          const uint32_t *__restrict__ offsets,
-                                                         const IndexEntry *__restrict__ tab,
+                                                         IndexEntry *__restrict__ tab,
                                                          const uint32_t *__restrict__ slot, uint32_t cur,
                                                          uint8_t *__restrict__ flags, uint32_t *__restrict__ tilesum,
                                                          int ntiles)
@@ -161,14 +205,18 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
     uint32_t newlen = 0;
     if (k < n) {
         const size_t c = (size_t)b * cap_blk + k;
-        const IndexEntry *e = tab + slot[c];
+        IndexEntry *e = tab + slot[c];
+        const unsigned long long m = e->mask;
         const unsigned long long f = e->first;
-        const int minb = 63 - (int)(f >> 32);
-        const int maxk = (int)(uint32_t)f;
+        const int minb = __builtin_ctzll(m);            // first block of the batch holding it
         const bool created = (e->batch & 0x7fffffffu) == cur;
         const bool is_new = created && b == minb;
-        const bool desig = (b == minb) && (k == maxk);
-        flags[c] = (uint8_t)((is_new ? 1 : 0) | (desig ? 2 : 0) | (created ? 4 : 0));
+        // the min block repeats the digest: every occurrence there joins the max so the
+        // designated writer (last occurrence, chunkMeta SET order) is known after this kernel
+        const bool rep = b == minb && f != 0 && (63 - (int)(f >> 32)) == minb;
+        if (rep) atomicMax(&e->first, ((unsigned long long)(63 - b) << 32) | (unsigned)(k + 1));
+        // bit1: in the min block (designated unless it has repeats: resolved in place_kernel)
+        flags[c] = (uint8_t)((is_new ? 1 : 0) | (b == minb ? 2 : 0) | (created ? 4 : 0) | (rep ? 16 : 0));
         if (is_new) {
             const uint32_t *off = offsets + (size_t)b * cap_blk;
             newlen = off[k] - (k ? off[k - 1] : 0u);
@@ -184,7 +232,8 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
 }
 
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
-                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t *slot,
+                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,
+                        unsigned long long tag_mask, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
                         int ntiles, int *err, hipStream_t st, Marker *mk)
 {
@@ -192,20 +241,24 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
     dim3 g(ntiles, nblocks);
     (void)hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st);
     if (hasher == 0) {
-        hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
+        hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
+                           slot, flags, err);
         mk->mark(st);
-        hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
+        hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, tag_mask, coll,
+                           ncoll,
                            coll_cap, err);
         mk->mark(st);
-        hipLaunchKernelGGL(idx_slow_kernel<5>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, slot,
+        hipLaunchKernelGGL(idx_slow_kernel<5>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, tag_mask, slot,
                            coll, ncoll, coll_cap, err);
     } else {
-        hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, slot, err);
+        hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
+                           slot, flags, err);
         mk->mark(st);
-        hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, coll, ncoll,
+        hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, tag_mask, coll,
+                           ncoll,
                            coll_cap, err);
         mk->mark(st);
-        hipLaunchKernelGGL(idx_slow_kernel<7>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, slot,
+        hipLaunchKernelGGL(idx_slow_kernel<7>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, tag_mask, slot,
                            coll, ncoll, coll_cap, err);
     }
     hipLaunchKernelGGL(idx_decide_kernel, g, dim3(256), 0, st, bst, cap_blk, offsets, tab, slot, cur, flags, tilesum,

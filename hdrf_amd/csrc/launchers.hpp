@@ -30,10 +30,11 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg,
                            uint32_t *spec, int spec_cap, SegMeta *meta, int32_t *sync, SegPlan *plan,
                            BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
-                      const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, hipStream_t st,
-                      Marker *mk);
+                      const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
+                      hipStream_t st, Marker *mk);
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
-                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t *slot,
+                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,
+                        unsigned long long tag_mask, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
                         int ntiles, int *err, hipStream_t st, Marker *mk);
 hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,

@@ -14,6 +14,9 @@
 // Each 64-B block is fetched as 17 dword-aligned dwords (4 x dwordx4 + 1) and realigned +
 // byte-swapped with one v_perm_b32 per word.  Rotations are v_alignbit_b32, 3-way xor is
 // v_bitop3_b32 (gfx950), Ch/Maj lower to v_bfi/v_bitop3.
+#include <algorithm>
+#include <cstdlib>
+
 #include "launchers.hpp"
 
 namespace hdrf {
@@ -145,54 +148,72 @@ __device__ __forceinline__ void set_iv(uint32_t st[8])
     }
 }
 
-constexpr int kPool = 8;   // chunks per lane per wave pool
+// persistent waves per block: enough for ~32 waves per CU whatever the batch size
 
-// grid ((cap_blk + 256*kPool - 1) / (256*kPool), nblocks); 4 waves per workgroup, a pool each
+// grid (waves_per_block/4, nblocks); every wave serves chunks of block b from the block's work
+// counter, reserving 64 chunk indices per atomicAdd and handing them to lanes as their chains end
 template <int HW>
 __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restrict__ blocks,
                                                        const uint32_t *__restrict__ offsets,
                                                        const BlockState *__restrict__ bst, int cap_blk,
-                                                       uint32_t *__restrict__ mid)
+                                                       uint32_t *__restrict__ mid, uint32_t *__restrict__ queue)
 {
+    extern __shared__ uint32_t s_occupancy_cap[];   // unused; sized by the launch to cap occupancy
+    (void)s_occupancy_cap;
     const int b = blockIdx.y;
-    const int c0 = (blockIdx.x * 4 + wave_id()) * 64 * kPool;
     const int n = bst[b].n_chunks;
-    if (c0 >= n) return;
-    const int c1 = min(n, c0 + 64 * kPool);
     const uint8_t *base = blocks[b].data;
     const uint32_t *off = offsets + (size_t)b * cap_blk;
     uint32_t *mb = mid + (size_t)b * cap_blk * 8;
     const int l = lane_id();
-    int next = c0 + 64;
-    int k = c0 + l;
-    bool active = k < c1;
+    int res_next = 0, res_end = 0;            // current reservation (uniform)
+    bool exhausted = false;
+    int k = 0;
+    bool active = false;                      // lane owns a chain with blocks left or just finished
     uint32_t pos = 0, r = 0;
     uint32_t st[8];
     set_iv<HW>(st);
-    if (active) {
-        pos = k ? off[k - 1] : 0u;
-        r = (off[k] - pos) >> 6;
-    }
     for (;;) {
-        bool done = active && r == 0;
-        while (ballot64(done)) {                       // store finished chains, refill from the pool
+        // store finished chains; hand out new chunks to idle lanes (may repeat for empty chains)
+        for (;;) {
+            const bool done = active && r == 0;
             if (done) {
 #pragma unroll
                 for (int i = 0; i < 8; i++) mb[(size_t)k * 8 + i] = st[i];
             }
-            const unsigned long long bal = ballot64(done);
+            const bool idle = !active || done;
+            const unsigned long long bal = ballot64(idle);
+            if (!bal || exhausted) {
+                if (done) active = false;
+                break;
+            }
+            if (res_next == res_end) {
+                uint32_t got = 0;
+                if (l == 0) got = atomicAdd(queue + b, 64u);
+                got = rdfirst(got);
+                if ((int)got >= n) {
+                    exhausted = true;
+                    if (done) active = false;
+                    break;
+                }
+                res_next = (int)got;
+                res_end = min((int)got + 64, n);
+            }
             const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-            if (done) {
-                k = next + rank;
-                active = k < c1;
-                set_iv<HW>(st);
-                if (active) {
+            const int avail = res_end - res_next;
+            if (idle) {
+                if (rank < avail) {
+                    k = res_next + rank;
+                    active = true;
+                    set_iv<HW>(st);
                     pos = k ? off[k - 1] : 0u;
                     r = (off[k] - pos) >> 6;
+                } else {
+                    active = false;
                 }
             }
-            next += __popcll(bal);
-            done = active && r == 0;
+            res_next += min(__popcll(bal), (long long)avail);
+            if (!ballot64(active && r == 0)) break;
         }
         if (!ballot64(active)) break;
         if (active) {
@@ -239,18 +260,22 @@ __global__ void __launch_bounds__(256) sha_tail_kernel(const BlockDesc *__restri
 }
 
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
-                      const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, hipStream_t st,
-                      Marker *mk)
+                      const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
+                      hipStream_t st, Marker *mk)
 {
+    (void)hipMemsetAsync(queue, 0, sizeof(uint32_t) * nblocks, st);
     mk->mark(st);
-    dim3 gf((cap_blk + 256 * kPool - 1) / (256 * kPool), nblocks);
+    const int wpb = std::min(2048, std::max(128, 8192 / nblocks));
+    dim3 gf(wpb / 4, nblocks);
+    // occupancy cap for the scattered per-lane streams (experiment knob): LDS bytes per workgroup
+    static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     dim3 gt((cap_blk + 255) / 256, nblocks);
     if (hasher == 0) {
-        hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid);
+        hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue);
         mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<5>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     } else {
-        hipLaunchKernelGGL(sha_full_kernel<7>, gf, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid);
+        hipLaunchKernelGGL(sha_full_kernel<7>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue);
         mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<7>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     }

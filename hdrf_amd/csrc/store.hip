@@ -274,8 +274,11 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
             place_cid[c] = cid;
             place_pos[c] = pos;
         }
-        if (f & 2) {                                       // designated: final index value
-            IndexEntry *e = tab + slot[c];
+        bool desig = (f & 2) != 0;                         // in the entry's min block ...
+        IndexEntry *e = tab + slot[c];
+        if (desig && (f & 16))                             // ... and its last occurrence there
+            desig = (uint32_t)e->first == (uint32_t)(k + 1);
+        if (desig) {                                       // designated: final index value
             const unsigned long long m = e->mask;
             const uint32_t cnt = (uint32_t)__popcll(m);
             if (f & 4) {

@@ -48,6 +48,7 @@ class Config(ctypes.Structure):
         ("container_max", ctypes.c_uint32), ("device", ctypes.c_int32), ("max_block_bytes", ctypes.c_int64),
         ("max_batch_blocks", ctypes.c_int32), ("index_log2", ctypes.c_int32), ("arena_slots", ctypes.c_int64),
         ("segment_bytes", ctypes.c_int32), ("keep_recipes", ctypes.c_int32), ("timing", ctypes.c_int32),
+        ("debug_tag_bits", ctypes.c_int32),
     ]
 
 

@@ -48,6 +48,8 @@ typedef struct {
     int32_t segment_bytes;   /* chunking speculation segment (default 1 MiB) */
     int32_t keep_recipes;    /* keep recipes (SET blockId -> size|digests) on the host */
     int32_t timing;          /* record per-stage HIP events */
+    int32_t debug_tag_bits;  /* test hook (SHA-1 only): keep only this many index-tag bits to force
+                                tag collisions through the exact slow path; 0 = full 64-bit tag */
 } hdrf_cfg;
 
 /* Per-block result of hdrf_reduce_block (caller-owned host arrays; NULL to skip). */

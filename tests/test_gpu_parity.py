@@ -141,3 +141,25 @@ def test_errors_fail_loudly():
     with pytest.raises(HdrfError):
         ctx.reduce_batch([0x1001], [10], [10], [1])                   # unaligned, no slack
     ctx.close()
+
+
+@pytest.mark.parametrize("bits", [16, 20])
+def test_index_tag_collisions_take_exact_slow_path(bits):
+    # test hook: index tags truncated to `bits` bits, so distinct digests collide on the tag and
+    # must be told apart by the stored digest bytes (apply verify + single-thread slow path)
+    roots = corpus_roots(21, 400000, 8, 8)
+    blocks = [corpus_block_host(21, roots, b, 8, 1 << 19) for b in range(8)]
+    run_sequence(blocks, debug_tag_bits=bits)
+    # batched too (collisions between blocks of one batch)
+    ctx = Context(debug_tag_bits=bits, **SMALL)
+    ora = Oracle()
+    size = len(blocks[0])
+    dev = ctx.dev_alloc(size * 8 + 4096)
+    ctx.h2d(dev, np.concatenate(blocks))
+    ctx.reduce_batch([dev + i * size for i in range(8)], [size] * 8, [size * (8 - i) + 4096 for i in range(8)],
+                     list(range(40, 48)))
+    for i in range(8):
+        compare_block(ctx.batch_result(i), ora.reduce(blocks[i], 40 + i), tag=f"coll batch {i}")
+    compare_state(ctx, ora, list(range(40, 48)))
+    ctx.dev_free(dev)
+    ctx.close()
