@@ -70,167 +70,190 @@ __device__ __forceinline__ uint32_t byte_range_mask(int a, int b)
     return lo & hi & 0x80808080u;
 }
 
-struct Walker {
+// ---- the chain walker ---------------------------------------------------------------------
+// A wave streams its region as 1 KiB tiles (lane l holds bytes [16l, 16l+16) of a tile).  The
+// "view" is two biased tiles A = [T, T+1024), B = [T+1024, T+2048); two more raw tiles are in
+// flight.  Tiles rotate through four register sets (R0..R3) in a 4-way unrolled loop, so there is
+// exactly one advance site per phase and no register copies.  Per tile only the 0xFF-byte mask
+// is computed (44 VALU); the granule max needed by the general path is computed on demand.
+
+struct WalkCfg {
     const uint8_t *base;
     int avail;     // readable bytes
     int size;      // block length
     int w;         // window (700)
     int maxlen;    // forced-cut length (1,000,000)
-    int T;         // tile A base (multiple of 1024)
-    uint4 A, B;      // biased view [T, T+2048)
-    uint4 C, D;      // raw prefetch of [T+2048, T+4096)
-    uint32_t gA, gB;   // granule max (biased)
-    uint32_t fA, fB;   // granule 0xFF-byte masks (biased 0xFF = raw 0x7F)
-
-    // raw (unbiased) tile load; the bias is applied when the tile is promoted into the view so
-    // the load stays in flight (a use right after the load would force s_waitcnt vmcnt(0))
-    __device__ __forceinline__ uint4 tile_raw(int X) const
-    {
-        const int off = X + 16 * lane_id();
-        if (X + 1024 <= avail) return ld16(base + off);       // wave-uniform fast path
-        return load16_guard(base, off, avail);
-    }
-    static __device__ __forceinline__ uint4 bias(uint4 v)
-    {
-        v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
-        return v;
-    }
-
-    __device__ __forceinline__ void init(int p)
-    {
-        T = p & ~1023;
-        A = tile_raw(T); B = tile_raw(T + 1024); C = tile_raw(T + 2048); D = tile_raw(T + 3072);
-        A = bias(A); B = bias(B);
-        gA = gmax16(A); gB = gmax16(B);
-        fA = ffmask16(A); fB = ffmask16(B);
-    }
-
-    __device__ __forceinline__ void advance()
-    {
-        T += 1024;
-        A = B; gA = gB; fA = fB;
-        B = bias(C); gB = gmax16(B); fB = ffmask16(B);
-        C = D;
-        D = tile_raw(T + 3072);
-    }
-
-    // 4 dwords of granule g (0..127) of the A|B view, as uniform scalars
-    __device__ __forceinline__ void granule(int g, uint32_t &w0, uint32_t &w1, uint32_t &w2, uint32_t &w3) const
-    {
-        const int l = g & 63;
-        if (g < 64) { w0 = rdlane(A.x, l); w1 = rdlane(A.y, l); w2 = rdlane(A.z, l); w3 = rdlane(A.w, l); }
-        else        { w0 = rdlane(B.x, l); w1 = rdlane(B.y, l); w2 = rdlane(B.z, l); w3 = rdlane(B.w, l); }
-    }
-
-    __device__ __forceinline__ uint32_t partial_max(int g, int lo, int hi) const
-    {
-        uint32_t w0, w1, w2, w3;
-        granule(g, w0, w1, w2, w3);
-        uint32_t m = 0;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            uint32_t wd = i < 4 ? w0 : i < 8 ? w1 : i < 12 ? w2 : w3;
-            uint32_t bv = (wd >> (8 * (i & 3))) & 0xffu;
-            if (i >= lo && i <= hi) m = max(m, bv);
-        }
-        return m;
-    }
-
-    // M(p) in biased form; requires T <= p < T+1024 and p+w < size.
-    __device__ __forceinline__ uint32_t window_max(int p, bool first) const
-    {
-        const int e = p + w;
-        const int gp = (p - T) >> 4, ge = (e - T) >> 4;
-        const int l = lane_id();
-        uint32_t va = (l > gp && l < ge) ? gA : 0u;
-        uint32_t vb = (l + 64 > gp && l + 64 < ge) ? gB : 0u;
-        uint32_t m = wave_max_u32(max(va, vb));
-        uint32_t gpm = rdlane(gp < 64 ? gA : gB, gp & 63);
-        uint32_t gem = rdlane(ge < 64 ? gA : gB, ge & 63);
-        if (gpm > m) m = max(m, partial_max(gp, (p - T) & 15, 15));
-        if (gem > m) m = max(m, partial_max(ge, 0, (e - T) & 15));
-        if (!first) m = max(m, 0x80u);   // mValue reset to 0 after a cut (:281)
-        return m;
-    }
-
-    // first byte index in [lo,hi] of granule g whose biased value >= m, or -1
-    __device__ __forceinline__ int first_ge(int g, int lo, int hi, uint32_t m) const
-    {
-        if (m == 0) return lo;
-        uint32_t w0, w1, w2, w3;
-        granule(g, w0, w1, w2, w3);
-        const uint32_t C = (256u - m) * 0x01010101u;
-        uint32_t h;
-        h = swar_ge(w0, C) & byte_range_mask(lo, hi);
-        if (h) return (__builtin_ctz(h) >> 3);
-        h = swar_ge(w1, C) & byte_range_mask(lo - 4, hi - 4);
-        if (h) return 4 + (__builtin_ctz(h) >> 3);
-        h = swar_ge(w2, C) & byte_range_mask(lo - 8, hi - 8);
-        if (h) return 8 + (__builtin_ctz(h) >> 3);
-        h = swar_ge(w3, C) & byte_range_mask(lo - 12, hi - 12);
-        if (h) return 12 + (__builtin_ctz(h) >> 3);
-        return -1;
-    }
-
-    // first j in [x, lim] whose biased byte is 0xFF (raw 0x7F); may advance tiles. -1 if none.
-    // Fast path of the chain: when the window holds such a byte, M(p) = 127 is the largest
-    // possible value and the cut is simply the next 0x7F byte after the window.
-    __device__ __forceinline__ int next_ff(int x, int lim)
-    {
-        const int l = lane_id();
-        for (;;) {
-            const int vend = T + 2047;
-            const int hi = min(lim, vend);
-            if (x <= hi) {
-                const int g = (x - T) >> 4, o = (x - T) & 15;
-                const uint32_t a = (l > g) ? fA : ((l == g) ? (fA & (0xffffu << o)) : 0u);
-                const uint32_t c = (l + 64 > g) ? fB : ((l + 64 == g) ? (fB & (0xffffu << o)) : 0u);
-                const unsigned long long ba = ballot64(a != 0u), bb = ballot64(c != 0u);
-                if (ba | bb) {
-                    int L;
-                    uint32_t bits;
-                    if (ba) { L = __builtin_ctzll(ba); bits = rdlane(a, L); }
-                    else { L = __builtin_ctzll(bb); bits = rdlane(c, L); L += 64; }
-                    const int pos = T + 16 * L + __builtin_ctz(bits);
-                    return pos <= hi ? pos : -1;
-                }
-            }
-            if (lim <= vend) return -1;
-            advance();
-            x = max(x, T + 1024);
-        }
-    }
-
-    // first j in [q, lim] with biased byte >= m; may advance tiles. -1 if none.
-    __device__ __forceinline__ int find(int q, int lim, uint32_t m)
-    {
-        for (;;) {
-            const int vend = T + 2047;
-            const int hi = min(lim, vend);
-            if (q <= hi) {
-                const int gq = (q - T) >> 4, gh = (hi - T) >> 4;
-                unsigned long long ma = ballot64(gA >= m);
-                unsigned long long mb = ballot64(gB >= m);
-                // restrict to granules [gq, gh]
-                if (gq >= 64) ma = 0; else ma &= ~0ull << gq;
-                if (gq > 64) mb &= ~0ull << (gq - 64);
-                if (gh < 64) { mb = 0; ma &= (gh == 63) ? ~0ull : ((1ull << (gh + 1)) - 1); }
-                else if (gh < 127) mb &= (1ull << (gh - 63)) - 1;
-                while (ma | mb) {
-                    int g = ma ? __builtin_ctzll(ma) : 64 + __builtin_ctzll(mb);
-                    int lo = (g == gq) ? ((q - T) & 15) : 0;
-                    int hb = (g == gh) ? ((hi - T) & 15) : 15;
-                    int r = first_ge(g, lo, hb, m);
-                    if (r >= 0) return T + 16 * g + r;
-                    if (g < 64) ma &= ma - 1; else mb &= mb - 1;
-                }
-            }
-            if (lim <= vend) return -1;
-            advance();
-            q = max(q, T + 1024);
-        }
-    }
 };
+
+enum : int { kWindow = 0, kSearchFF = 1, kSearchGen = 2 };
+
+struct Chain {
+    int p;         // last cut (chunk start)
+    int state;
+    int q, lim;    // pending search range
+    uint32_t m;    // threshold (biased) of a general search
+    bool first;    // the very first chunk of a block: M has no 0 floor
+    bool ended;    // chain ended because the data ended
+};
+
+__device__ __forceinline__ uint4 tile_raw(const WalkCfg &c, int X)
+{
+    const int off = X + 16 * lane_id();
+    if (X + 1024 <= c.avail) return ld16(c.base + off);       // wave-uniform fast path
+    return load16_guard(c.base, off, c.avail);
+}
+__device__ __forceinline__ uint4 bias(uint4 v)
+{
+    v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
+    return v;
+}
+
+// 4 dwords of granule g (0..127) of the view, as uniform scalars
+__device__ __forceinline__ void granule(const uint4 &A, const uint4 &B, int g, uint32_t &w0, uint32_t &w1,
+                                        uint32_t &w2, uint32_t &w3)
+{
+    const int l = g & 63;
+    if (g < 64) { w0 = rdlane(A.x, l); w1 = rdlane(A.y, l); w2 = rdlane(A.z, l); w3 = rdlane(A.w, l); }
+    else        { w0 = rdlane(B.x, l); w1 = rdlane(B.y, l); w2 = rdlane(B.z, l); w3 = rdlane(B.w, l); }
+}
+
+__device__ __forceinline__ uint32_t partial_max(const uint4 &A, const uint4 &B, int g, int lo, int hi)
+{
+    uint32_t w0, w1, w2, w3;
+    granule(A, B, g, w0, w1, w2, w3);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uint32_t wd = i < 4 ? w0 : i < 8 ? w1 : i < 12 ? w2 : w3;
+        const uint32_t bv = (wd >> (8 * (i & 3))) & 0xffu;
+        if (i >= lo && i <= hi) m = max(m, bv);
+    }
+    return m;
+}
+
+// M(p) in biased form (general path); requires T <= p < T+1024 and p+w < size.
+__device__ __forceinline__ uint32_t window_max(const uint4 &A, const uint4 &B, int T, int p, int w, bool first)
+{
+    const uint32_t gA = gmax16(A), gB = gmax16(B);
+    const int e = p + w;
+    const int gp = (p - T) >> 4, ge = (e - T) >> 4;
+    const int l = lane_id();
+    const uint32_t va = (l > gp && l < ge) ? gA : 0u;
+    const uint32_t vb = (l + 64 > gp && l + 64 < ge) ? gB : 0u;
+    uint32_t m = wave_max_u32(max(va, vb));
+    const uint32_t gpm = rdlane(gp < 64 ? gA : gB, gp & 63);
+    const uint32_t gem = rdlane(ge < 64 ? gA : gB, ge & 63);
+    if (gpm > m) m = max(m, partial_max(A, B, gp, (p - T) & 15, 15));
+    if (gem > m) m = max(m, partial_max(A, B, ge, 0, (e - T) & 15));
+    if (!first) m = max(m, 0x80u);   // mValue reset to 0 after a cut (:281)
+    return m;
+}
+
+// first byte index in [lo,hi] of granule g whose biased value >= m, or -1
+__device__ __forceinline__ int first_ge(const uint4 &A, const uint4 &B, int g, int lo, int hi, uint32_t m)
+{
+    if (m == 0) return lo;
+    uint32_t w0, w1, w2, w3;
+    granule(A, B, g, w0, w1, w2, w3);
+    const uint32_t C = (256u - m) * 0x01010101u;
+    uint32_t h;
+    h = swar_ge(w0, C) & byte_range_mask(lo, hi);
+    if (h) return (__builtin_ctz(h) >> 3);
+    h = swar_ge(w1, C) & byte_range_mask(lo - 4, hi - 4);
+    if (h) return 4 + (__builtin_ctz(h) >> 3);
+    h = swar_ge(w2, C) & byte_range_mask(lo - 8, hi - 8);
+    if (h) return 8 + (__builtin_ctz(h) >> 3);
+    h = swar_ge(w3, C) & byte_range_mask(lo - 12, hi - 12);
+    if (h) return 12 + (__builtin_ctz(h) >> 3);
+    return -1;
+}
+
+// first j in [q, hi] (inside the view) with biased byte >= m, or -1 (general path)
+__device__ __forceinline__ int ge_in_view(const uint4 &A, const uint4 &B, int T, int q, int hi, uint32_t m)
+{
+    const uint32_t gA = gmax16(A), gB = gmax16(B);
+    const int gq = (q - T) >> 4, gh = (hi - T) >> 4;
+    unsigned long long ma = ballot64(gA >= m);
+    unsigned long long mb = ballot64(gB >= m);
+    if (gq >= 64) ma = 0; else ma &= ~0ull << gq;
+    if (gq > 64) mb &= ~0ull << (gq - 64);
+    if (gh < 64) { mb = 0; ma &= (gh == 63) ? ~0ull : ((1ull << (gh + 1)) - 1); }
+    else if (gh < 127) mb &= (1ull << (gh - 63)) - 1;
+    while (ma | mb) {
+        const int g = ma ? __builtin_ctzll(ma) : 64 + __builtin_ctzll(mb);
+        const int lo = (g == gq) ? ((q - T) & 15) : 0;
+        const int hb = (g == gh) ? ((hi - T) & 15) : 15;
+        const int r = first_ge(A, B, g, lo, hb, m);
+        if (r >= 0) return T + 16 * g + r;
+        if (g < 64) ma &= ma - 1; else mb &= mb - 1;
+    }
+    return -1;
+}
+
+// first j in [x, hi] (inside the view) whose biased byte is 0xFF (raw 0x7F), or -1.  When the
+// window holds such a byte, M(p) = 127 is the largest possible value and the cut is simply the
+// next 0x7F byte after the window.
+__device__ __forceinline__ int ff_in_view(uint32_t fA, uint32_t fB, int T, int x, int hi)
+{
+    const int l = lane_id();
+    const int g = (x - T) >> 4, o = (x - T) & 15;
+    const uint32_t a = (l > g) ? fA : ((l == g) ? (fA & (0xffffu << o)) : 0u);
+    const uint32_t c = (l + 64 > g) ? fB : ((l + 64 == g) ? (fB & (0xffffu << o)) : 0u);
+    const unsigned long long ba = ballot64(a != 0u), bb = ballot64(c != 0u);
+    if (!(ba | bb)) return -1;
+    int L;
+    uint32_t bits;
+    if (ba) { L = __builtin_ctzll(ba); bits = rdlane(a, L); }
+    else { L = __builtin_ctzll(bb); bits = rdlane(c, L); L += 64; }
+    const int pos = T + 16 * L + __builtin_ctz(bits);
+    return pos <= hi ? pos : -1;
+}
+
+struct ListSink;
+
+// Advance the chain as far as the view [T, T+2048) allows.  Returns true when the view must
+// advance (the chain continues), false when the chain ended (ch.ended) or the sink/stop said stop.
+template <class Sink, class Stop>
+__device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const uint4 &A, const uint4 &B,
+                                             uint32_t fA, uint32_t fB, int T, Sink &sink, Stop &stop)
+{
+    for (;;) {
+        if (ch.state == kWindow) {
+            if (ch.p >= T + 1024) return true;
+            const int e = ch.p + c.w;
+            if (e >= c.size) { ch.ended = true; return false; }       // window incomplete: no more cuts
+            ch.lim = min(ch.p + c.maxlen, c.size - 1);
+            ch.q = e + 1;
+            if (ff_in_view(fA, fB, T, ch.p, e) >= 0) {
+                ch.state = kSearchFF;                                  // M(p) = 127
+            } else {
+                ch.m = window_max(A, B, T, ch.p, c.w, ch.first);
+                ch.state = kSearchGen;
+            }
+        }
+        const int vend = T + 2047;
+        const int hi = min(ch.lim, vend);
+        int j = -1;
+        if (ch.q <= hi)
+            j = ch.state == kSearchFF ? ff_in_view(fA, fB, T, ch.q, hi) : ge_in_view(A, B, T, ch.q, hi, ch.m);
+        int cut;
+        if (j >= 0) {
+            cut = j + 1;                                               // :276-283
+        } else if (ch.lim <= vend) {
+            if (ch.p + c.maxlen <= c.size - 1) cut = ch.p + c.maxlen + 1;   // forced cut :288-294
+            else { ch.ended = true; return false; }
+        } else {
+            ch.q = max(ch.q, T + 2048);                                // continue after the advance
+            return true;
+        }
+        cut = __builtin_amdgcn_readfirstlane(cut);
+        ch.first = false;
+        ch.state = kWindow;
+        ch.p = cut;
+        if (!sink.push((uint32_t)cut)) return false;
+        if (stop(cut, sink.cnt)) return false;
+    }
+}
 
 // Cut sink that stages 64 cuts in a VGPR and writes them coalesced.
 struct ListSink {
@@ -256,31 +279,25 @@ struct ListSink {
 // Walk the chain from p (a cut, or the block start when first) calling sink.push(cut) for
 // every cut until the data ends (returns true) or the sink/stop predicate says stop (false).
 template <class Stop>
-__device__ __forceinline__ bool walk_chain(Walker &W, int p, bool first, ListSink &sink, Stop stop)
+__device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, ListSink &sink, Stop stop)
 {
-    W.init(p);
+    Chain ch;
+    ch.p = p; ch.state = kWindow; ch.q = 0; ch.lim = 0; ch.m = 0; ch.first = first; ch.ended = false;
+    int T = p & ~1023;
+    uint4 R0 = tile_raw(c, T), R1 = tile_raw(c, T + 1024), R2 = tile_raw(c, T + 2048), R3 = tile_raw(c, T + 3072);
+    R0 = bias(R0); R1 = bias(R1);
+    uint32_t f0 = ffmask16(R0), f1 = ffmask16(R1), f2 = 0, f3 = 0;
     for (;;) {
-        while (p >= W.T + 1024) W.advance();
-        const int e = p + W.w;
-        if (e >= W.size) return true;                    // window incomplete: no more cuts
-        const int lim = min(p + W.maxlen, W.size - 1);
-        int j;
-        if (W.next_ff(p, e) >= 0) {
-            j = W.next_ff(e + 1, lim);                    // M(p) = 127: next 0x7F byte
-        } else {
-            const uint32_t m = W.window_max(p, first);
-            j = W.find(e + 1, lim, m);
-        }
-        int cut;
-        if (j >= 0) cut = j + 1;                         // :276-283
-        else if (p + W.maxlen <= W.size - 1) cut = p + W.maxlen + 1;   // :288-294
-        else return true;
-        first = false;
-        cut = __builtin_amdgcn_readfirstlane(cut);
-        if (!sink.push((uint32_t)cut)) return false;
-        if (stop(cut, sink.cnt)) return false;
-        p = cut;
+        if (!process_view(c, ch, R0, R1, f0, f1, T, sink, stop)) break;
+        T += 1024; R2 = bias(R2); f2 = ffmask16(R2); R0 = tile_raw(c, T + 3072);
+        if (!process_view(c, ch, R1, R2, f1, f2, T, sink, stop)) break;
+        T += 1024; R3 = bias(R3); f3 = ffmask16(R3); R1 = tile_raw(c, T + 3072);
+        if (!process_view(c, ch, R2, R3, f2, f3, T, sink, stop)) break;
+        T += 1024; R0 = bias(R0); f0 = ffmask16(R0); R2 = tile_raw(c, T + 3072);
+        if (!process_view(c, ch, R3, R0, f3, f0, T, sink, stop)) break;
+        T += 1024; R1 = bias(R1); f1 = ffmask16(R1); R3 = tile_raw(c, T + 3072);
     }
+    return ch.ended;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -296,7 +313,7 @@ __global__ void __launch_bounds__(256) spec_walk_kernel(const BlockDesc *__restr
     const int size = (int)bd.len;
     const int s_k = k * bd.seg_len;
     const int s_next = (k + 1 == bd.nseg) ? 0x7fffffff : (k + 1) * bd.seg_len;  // last: every cut is main
-    Walker W;
+    WalkCfg W;
     W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = size;
     W.w = w; W.maxlen = maxlen;
     ListSink sink;
@@ -434,7 +451,7 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
     BlockState s = bst[b];
     uint32_t *off = offsets + (size_t)b * cap_blk;
     if (s.fail_dst >= 0) {
-        Walker W;
+        WalkCfg W;
         W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
         W.w = w; W.maxlen = maxlen;
         ListSink sink;
