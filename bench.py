@@ -27,6 +27,19 @@ sys.path.insert(0, ROOT)
 
 METRIC = "logical GB/s reduced per node (1/2/4/8 GPUs) at 50% dup, bit-exact dedup ratio"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_WI_NS = 1033.0       # v_add_u32 wave-instructions/ns, chip-wide (tools/valu_peak.hip)
+KERNEL_OF = {"walk(spec_walk_kernel)": "spec_walk_kernel", "sha_full(sha_full_kernel)": "sha_full_kernel",
+             "place(place_kernel)": "place_kernel"}
+
+
+def load_pmc():
+    """Per-launch PMC figures of the newest committed rocprofv3 pass (scripts/pmc.sh ->
+    scripts/traffic.py -> profiles/*_traffic.json), measured on this same workload."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))   # names sort by round, version
+    if not files:
+        return {}, None
+    return json.load(open(files[-1])), os.path.relpath(files[-1], ROOT)
 
 
 def parse():
@@ -138,9 +151,21 @@ def main():
     dom = max(per_launch, key=lambda s: stage_ms[STAGES.index(s)])
     dom_ms = stage_ms[STAGES.index(dom)] / a.steps / nbatch
     achieved = per_launch[dom] / (dom_ms * 1e-3) / 1e9
+    pmc, pmc_src = load_pmc()
+    kname = KERNEL_OF[dom] + ("<5>" if a.hasher == 0 else "<7>") * (dom in (STAGES[2],))
+    prof = pmc.get(kname, {})
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": prof.get("hbm_bytes_per_launch"), "traffic_source": pmc_src,
                 "avg_launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(per_launch[dom])}
+    if dom == STAGES[2] and prof.get("sq_insts_valu"):
+        # SHA is integer-VALU bound: wave-instructions per launch (PMC SQ_INSTS_VALU) over the
+        # measured launch time, against the full-rate v_add_u32 peak (profiles/r01_valu_peak.txt)
+        wi_ns = prof["sq_insts_valu"] / (dom_ms * 1e6)
+        roofline["limiter"] = "int-VALU"
+        roofline["valu"] = {"wave_instr_per_ns": round(wi_ns, 1), "peak": VALU_PEAK_WI_NS,
+                            "frac": round(wi_ns / VALU_PEAK_WI_NS, 4),
+                            "sq_insts_valu_per_launch": int(prof["sq_insts_valu"])}
 
     dedup = {"logical_bytes_per_gpu": nb * S, "stored_bytes_per_gpu": new_bytes,
              "dedup_ratio": round(nb * S / max(new_bytes, 1), 6),
