@@ -69,6 +69,19 @@ struct hdrf_ctx {
     std::map<uint32_t, uint32_t> slot_owner;         // arena slot -> container id
     std::map<uint32_t, std::vector<uint8_t>> recipes; // longToBytes(blockId,4) -> recipe
     std::map<uint32_t, int64_t> lengths;              // block length (recipe head)
+    // node-global index (gx.hip): scratch aggregation table, owner-side per-record arrays
+    int G = 1, rank = 0;
+    IndexEntry *d_scratch = nullptr;
+    int scratch_log2 = 0;
+    int64_t gx_cap = 0;
+    unsigned long long *d_gx_counts = nullptr;   // [G] records emitted per peer
+    int64_t *d_gx_rcounts = nullptr;             // [G] records received per peer
+    uint32_t *d_oslot = nullptr;
+    uint8_t *d_oflags = nullptr;
+    const uint32_t *gx_x2 = nullptr;             // responses of the current batch (caller's buffer)
+    int gx_phase = 0;                            // 1 front, 2 owner, 3 decide, 4 flush, 5 place
+    int gx_nblocks = 0;
+    std::vector<uint64_t> gx_ids, gx_lens;
     // timing
     bool timing = false;
     hipEvent_t ev[kStages + 1] = {};
@@ -128,6 +141,8 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
     cfg->segment_bytes = 1 << 20;
     cfg->keep_recipes = 1;
     cfg->timing = 0;
+    cfg->n_ranks = 1;
+    cfg->rank = 0;
     return 0;
 }
 
@@ -136,7 +151,8 @@ static void free_all(hdrf_ctx *ctx)
     void *ptrs[] = {ctx->d_blocks, ctx->d_spec, ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off,
                     ctx->d_dig, ctx->d_mid, ctx->d_slot, ctx->d_pre, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
                     ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed, ctx->d_coll, ctx->d_ncoll, ctx->d_tab,
-                    ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_queue, ctx->d_err, ctx->d_stage};
+                    ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_queue, ctx->d_err, ctx->d_stage,
+                    ctx->d_scratch, ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (auto &e : ctx->ev)
@@ -150,6 +166,7 @@ static int init_state(hdrf_ctx *ctx)
     AllocState a{};
     for (int t = 0; t < 4; t++) {
         a.id[t] = (uint32_t)t << 22;                 // utilities.bytesToBlockID, absent key (DN/utilities.java:36-50)
+        // (node-global mode: the one allocator of the node, carried rank to rank by hdrf_gx_flush)
         a.slot[t] = (uint32_t)t * (uint32_t)(ctx->cfg.arena_slots / 4);   // per-range slot rings
     }
     HIPCK(hipMemcpyAsync(ctx->d_alloc, &a, sizeof a, hipMemcpyHostToDevice, ctx->st));
@@ -163,6 +180,7 @@ static int init_state(hdrf_ctx *ctx)
     ctx->recipes.clear();
     ctx->lengths.clear();
     ctx->last_nblocks = 0;
+    ctx->gx_phase = 0;
     return 0;
 }
 
@@ -175,7 +193,8 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         c.n_thread < 1 || c.n_thread > 3 || c.max_batch_blocks < 1 || c.max_batch_blocks > kMaxBatch ||
         c.index_log2 < 10 || c.index_log2 > 31 || c.arena_slots < 8 || c.max_block_bytes < 1 ||
         c.max_block_bytes > (1ll << 30) || c.container_max <= (uint32_t)c.max_chunk + 1 || c.segment_bytes < (1 << 16) ||
-        c.debug_tag_bits < 0 || c.debug_tag_bits > 64 || (c.debug_tag_bits && c.hasher != 0))
+        c.debug_tag_bits < 0 || c.debug_tag_bits > 64 || (c.debug_tag_bits && c.hasher != 0) ||
+        c.n_ranks < 1 || c.n_ranks > 64 || c.rank < 0 || c.rank >= c.n_ranks)
         return HDRF_E_INVAL;
     if (c.compressor != 1) return HDRF_E_UNSUPPORTED;
     hdrf_ctx *ctx = new (std::nothrow) hdrf_ctx();
@@ -219,6 +238,26 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         delete ctx;
         return rc;
     }
+    ctx->G = c.n_ranks;
+    ctx->rank = c.rank;
+    if (ctx->G > 1) {
+        // scratch table for the batch's local aggregation: >= 1.5x the expected distinct chunks
+        // (mean chunk ~949 B on random data; a table-full condition is reported, never silent)
+        const double expect = 1.5 * (double)B * (double)c.max_block_bytes / 900.0;
+        int lg = 16;
+        while (lg < 31 && (double)(1ull << lg) < expect) lg++;
+        ctx->scratch_log2 = lg;
+        ctx->gx_cap = (int64_t)nchunk;
+        const size_t nrec = (size_t)ctx->G * (size_t)ctx->gx_cap;
+        if ((rc = dalloc(ctx, &ctx->d_scratch, (size_t)1 << lg)) || (rc = dalloc(ctx, &ctx->d_gx_counts, 64)) ||
+            (rc = dalloc(ctx, &ctx->d_gx_rcounts, 64)) || (rc = dalloc(ctx, &ctx->d_oslot, nrec)) ||
+            (rc = dalloc(ctx, &ctx->d_oflags, nrec))) {
+            fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
+            free_all(ctx);
+            delete ctx;
+            return rc;
+        }
+    }
     ctx->timing = c.timing != 0;
     for (auto &e : ctx->ev)
         if (hipEventCreate(&e) != hipSuccess) { free_all(ctx); delete ctx; return HDRF_E_HIP; }
@@ -258,10 +297,10 @@ static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t l
     ctx->containers[id] = ContainerInfo{slot, len, closed};
 }
 
-extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
-                                 const uint64_t *readable, const uint64_t *block_ids)
+// Validate a batch and upload its block descriptors; returns the largest segment count.
+static int prepare_blocks(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                          const uint64_t *readable, int *max_nseg_out)
 {
-    if (!ctx) return HDRF_E_INVAL;
     if (nblocks < 1 || nblocks > ctx->max_batch || !dev_data || !len || !readable)
         return set_err(ctx, HDRF_E_INVAL, "bad batch arguments");
     const hdrf_cfg &c = ctx->cfg;
@@ -284,27 +323,36 @@ extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
         bd[b].seg_len = seg_len;
         max_nseg = std::max(max_nseg, nseg);
     }
-    const uint32_t cur = ++ctx->batch;
-    hipStream_t st = ctx->st;
-    HIPCK(hipMemcpyAsync(ctx->d_blocks, bd.data(), sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
-    HIPCK(hipMemsetAsync(ctx->d_nclosed, 0, sizeof(uint32_t), st));
-    Marker mk;
-    mk.ev = ctx->timing ? ctx->ev : nullptr;
-    HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
-                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
-    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_mid, ctx->d_dig,
-                     ctx->d_queue, st, &mk));
-    HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_tab, c.index_log2,
-                       cur, tag_mask(ctx), ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags,
-                       ctx->d_tilesum, ctx->ntiles, ctx->d_err, st, &mk));
+    HIPCK(hipMemcpyAsync(ctx->d_blocks, bd.data(), sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, ctx->st));
+    *max_nseg_out = max_nseg;
+    return 0;
+}
+
+static StoreParams store_params(const hdrf_ctx *ctx, int nblocks)
+{
+    const hdrf_cfg &c = ctx->cfg;
     StoreParams P;
     P.nblocks = nblocks; P.cap_blk = ctx->cap_blk; P.ntiles = ctx->ntiles;
     P.n_thread = c.n_thread; P.min_mt = c.min_mt_chunks; P.cmax = c.container_max;
     P.nslots = (uint32_t)c.arena_slots; P.ev_cap = ctx->ev_cap; P.closed_cap = ctx->closed_cap;
-    HIPCK(launch_store(P, ctx->d_blocks, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre,
-                       ctx->d_store, ctx->d_pre, ctx->d_alloc, ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed,
-                       ctx->d_slot, ctx->d_tab, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, ctx->d_err, st, &mk));
-    // read back small per-batch state
+    return P;
+}
+
+static void accumulate_stages(hdrf_ctx *ctx, int nmarks)
+{
+    if (!ctx->timing) return;
+    for (int i = 0; i + 1 < nmarks && i < kStages; i++) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) ctx->stage_ms[i] += ms;
+    }
+}
+
+// After the store kernels of a batch: read back block counts / allocator, record closed
+// containers, recipes and block lengths (the host-side Redis + chunkDir views).
+static int finish_batch(hdrf_ctx *ctx, int32_t nblocks, const uint64_t *len, const uint64_t *block_ids, int nmarks)
+{
+    const hdrf_cfg &c = ctx->cfg;
+    hipStream_t st = ctx->st;
     ctx->h_bst.resize(nblocks);
     ctx->h_store.resize(nblocks);
     int herr = 0;
@@ -315,31 +363,21 @@ extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
     HIPCK(hipMemcpyAsync(&herr, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(&nclosed, ctx->d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    if (ctx->timing) {
-        for (int i = 0; i < kStages; i++) {
-            float ms = 0;
-            HIPCK(hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]));
-            ctx->stage_ms[i] += ms;
-        }
-    }
+    accumulate_stages(ctx, nmarks);
     ctx->last_nblocks = nblocks;
     if (herr) {
         HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), st));
-        return set_err(ctx, herr & 6 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
+        return set_err(ctx, herr & 22 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
                        "device reported error flags " + std::to_string(herr));
     }
     if ((int)nclosed > ctx->closed_cap) return set_err(ctx, HDRF_E_CAPACITY, "closed-container list overflow");
-    // container bookkeeping
     if (nclosed) {
         std::vector<ClosedRec> cl(nclosed);
         HIPCK(hipMemcpy(cl.data(), ctx->d_closed, sizeof(ClosedRec) * nclosed, hipMemcpyDeviceToHost));
         for (auto &r : cl) note_container(ctx, r.id, r.slot, r.len, 1);
     }
-    bool any_store = false;
-    for (int b = 0; b < nblocks; b++) any_store |= ctx->h_store[b] != 0;
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) note_container(ctx, ctx->h_alloc.id[t], ctx->h_alloc.slot[t], ctx->h_alloc.cur[t], 0);
-    (void)any_store;
     ctx->have_alloc = 1;                              // storeDB always SETs "blockID" (:389)
     // recipes (SET longToBytes(id,4) -> BE32 size | digests)
     for (int b = 0; b < nblocks; b++) {
@@ -357,6 +395,203 @@ extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
             ctx->recipes[key] = std::move(r);
         }
     }
+    return 0;
+}
+
+extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                                 const uint64_t *readable, const uint64_t *block_ids)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
+    const hdrf_cfg &c = ctx->cfg;
+    int max_nseg = 1;
+    if (int rc = prepare_blocks(ctx, nblocks, dev_data, len, readable, &max_nseg)) return rc;
+    const uint32_t cur = ++ctx->batch;
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemsetAsync(ctx->d_nclosed, 0, sizeof(uint32_t), st));
+    Marker mk;
+    mk.ev = ctx->timing ? ctx->ev : nullptr;
+    HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
+                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
+    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_mid, ctx->d_dig,
+                     ctx->d_queue, st, &mk));
+    HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_tab, c.index_log2,
+                       cur, tag_mask(ctx), ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags,
+                       ctx->d_tilesum, ctx->ntiles, ctx->d_err, st, &mk));
+    const StoreParams P = store_params(ctx, nblocks);
+    HIPCK(launch_store(P, ctx->d_blocks, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre,
+                       ctx->d_store, ctx->d_pre, ctx->d_alloc, ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed,
+                       ctx->d_slot, ctx->d_tab, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, ctx->d_err, st, &mk));
+    return finish_batch(ctx, nblocks, len, block_ids, kStages + 1);
+}
+
+// ---- node-global index phases (include/hdrf.h, gx.hip) ------------------------------------
+static_assert(sizeof(AllocState) <= HDRF_ALLOC_STATE_BYTES, "allocator state exchange size");
+
+static int gx_check(hdrf_ctx *ctx, int phase_before)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
+    if (ctx->gx_phase != phase_before)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* phases called out of order (phase " +
+                                              std::to_string(ctx->gx_phase) + ")");
+    return 0;
+}
+
+static int64_t max_count(const int64_t *counts, int G)
+{
+    int64_t m = 0;
+    for (int i = 0; i < G; i++) m = std::max(m, counts[i]);
+    return m;
+}
+
+extern "C" int hdrf_gx_layout_get(hdrf_ctx *ctx, hdrf_gx_layout *out)
+{
+    if (!ctx || !out) return HDRF_E_INVAL;
+    out->cap = ctx->gx_cap;
+    out->x1_words = ctx->HW + 2;
+    out->x2_words = 2;
+    out->x3_words = 4;
+    return 0;
+}
+
+extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                             const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send,
+                             int64_t *send_counts)
+{
+    if (ctx && ctx->gx_phase == 6) ctx->gx_phase = 0;
+    if (int rc = gx_check(ctx, 0)) return rc;
+    if (!x1_send || !send_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    const hdrf_cfg &c = ctx->cfg;
+    int max_nseg = 1;
+    if (int rc = prepare_blocks(ctx, nblocks, dev_data, len, readable, &max_nseg)) return rc;
+    ++ctx->batch;
+    hipStream_t st = ctx->st;
+    Marker mk;
+    mk.ev = ctx->timing ? ctx->ev : nullptr;
+    HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
+                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
+    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_mid, ctx->d_dig,
+                     ctx->d_queue, st, &mk));
+    // local aggregation: a fresh scratch table, every entry "created" in batch 1
+    HIPCK(hipMemsetAsync(ctx->d_scratch, 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
+    HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_scratch,
+                       ctx->scratch_log2, 1u, tag_mask(ctx), ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap,
+                       ctx->d_flags, ctx->d_tilesum, ctx->ntiles, ctx->d_err, st, &mk));
+    HIPCK(launch_gx_emit(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->ntiles, ctx->d_dig, ctx->d_scratch,
+                         ctx->d_slot, ctx->d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gx_counts, ctx->d_err, st));
+    mk.mark(st);
+    std::vector<unsigned long long> cnt(ctx->G);
+    int herr = 0;
+    HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&herr, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    accumulate_stages(ctx, mk.next);
+    if (herr) {
+        HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), st));
+        return set_err(ctx, herr & 22 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
+                       "device reported error flags " + std::to_string(herr));
+    }
+    for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
+    ctx->gx_nblocks = nblocks;
+    ctx->gx_lens.assign(len, len + nblocks);
+    ctx->gx_ids.assign(nblocks, 0);
+    if (block_ids) ctx->gx_ids.assign(block_ids, block_ids + nblocks);
+    ctx->gx_phase = 1;
+    return 0;
+}
+
+extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send)
+{
+    if (int rc = gx_check(ctx, 1)) return rc;
+    if (!x1_recv || !recv_counts || !x2_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    for (int s = 0; s < ctx->G; s++)
+        if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
+    HIPCK(launch_gx_owner(ctx->cfg.hasher, x1_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap,
+                          ctx->G, ctx->d_tab, ctx->cfg.index_log2, ctx->batch, tag_mask(ctx), ctx->d_oslot,
+                          ctx->d_oflags, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, x2_send, ctx->d_err, st));
+    int herr = 0;
+    HIPCK(hipMemcpyAsync(&herr, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (herr) {
+        HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), st));
+        return set_err(ctx, herr & 22 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
+                       "device reported error flags " + std::to_string(herr));
+    }
+    ctx->gx_phase = 2;
+    return 0;
+}
+
+extern "C" int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv)
+{
+    if (int rc = gx_check(ctx, 2)) return rc;
+    if (!x2_recv) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    hipStream_t st = ctx->st;
+    const int nb = ctx->gx_nblocks;
+    HIPCK(launch_gx_decide(ctx->d_bst, nb, ctx->cap_blk, ctx->ntiles, ctx->d_off, ctx->d_scratch, ctx->d_slot, x2_recv,
+                           ctx->d_flags, ctx->d_tilesum, st));
+    const StoreParams P = store_params(ctx, nb);
+    HIPCK(launch_store_scan(P, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
+                            ctx->d_pre, st));
+    ctx->gx_x2 = x2_recv;
+    ctx->gx_phase = 3;
+    return 0;
+}
+
+extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out)
+{
+    if (int rc = gx_check(ctx, 3)) return rc;
+    hipStream_t st = ctx->st;
+    if (alloc_in) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_in, sizeof(AllocState), hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(ctx->d_nclosed, 0, sizeof(uint32_t), st));
+    const StoreParams P = store_params(ctx, ctx->gx_nblocks);
+    HIPCK(launch_store_flush(P, ctx->d_bst, ctx->d_store, ctx->d_pre, ctx->d_alloc, ctx->d_rstate, ctx->d_ev,
+                             ctx->d_closed, ctx->d_nclosed, ctx->d_err, st));
+    AllocState a{};
+    HIPCK(hipMemcpyAsync(&a, ctx->d_alloc, sizeof a, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (alloc_out) {
+        std::memset(alloc_out, 0, HDRF_ALLOC_STATE_BYTES);
+        std::memcpy(alloc_out, &a, sizeof a);
+    }
+    ctx->gx_phase = 4;
+    return 0;
+}
+
+extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts)
+{
+    if (int rc = gx_check(ctx, 4)) return rc;
+    if (!x3_send || !send_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    hipStream_t st = ctx->st;
+    const int nb = ctx->gx_nblocks;
+    const StoreParams P = store_params(ctx, nb);
+    GxPlace gx;
+    gx.x2 = ctx->gx_x2; gx.x3 = x3_send; gx.cap = ctx->gx_cap; gx.counts = ctx->d_gx_counts; gx.G = ctx->G;
+    HIPCK(launch_store_place(P, ctx->d_blocks, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_pre, ctx->d_rstate,
+                             ctx->d_ev, ctx->d_slot, ctx->d_scratch, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, gx, st));
+    // the node's allocator after the last rank (the next batch and the "blockID" view start here)
+    if (alloc_final) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_final, sizeof(AllocState), hipMemcpyHostToDevice, st));
+    std::vector<unsigned long long> cnt(ctx->G);
+    HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    if (int rc = finish_batch(ctx, nb, ctx->gx_lens.data(), ctx->gx_ids.data(), 0)) return rc;
+    for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
+    ctx->gx_phase = 5;
+    return 0;
+}
+
+extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts)
+{
+    if (int rc = gx_check(ctx, 5)) return rc;
+    if (!x3_recv || !recv_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    for (int s = 0; s < ctx->G; s++)
+        if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
+    HIPCK(launch_gx_commit(x3_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap, ctx->G, ctx->d_tab, st));
+    HIPCK(hipStreamSynchronize(st));
+    ctx->gx_phase = 6;
     return 0;
 }
 
@@ -424,6 +659,7 @@ extern "C" int hdrf_reduce_block(hdrf_ctx *ctx, uint64_t block_id, const uint8_t
                                  hdrf_block_result *out)
 {
     if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
     if ((int64_t)len > ctx->cfg.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
     if (len && !data) return set_err(ctx, HDRF_E_INVAL, "null data");
     const uint64_t need = len + 4096;

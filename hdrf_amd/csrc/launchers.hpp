@@ -37,11 +37,46 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                         unsigned long long tag_mask, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
                         int ntiles, int *err, hipStream_t st, Marker *mk);
+// node-global index mode (gx.hip): place_kernel emits (owner slot, cid, start, stop) for new entries
+struct GxPlace {
+    const uint32_t *x2 = nullptr;          // owner responses, indexed by scratch IndexEntry::cid
+    uint32_t *x3 = nullptr;                // [G][cap][4] location records (nullptr: classic mode)
+    int64_t cap = 0;
+    unsigned long long *counts = nullptr;  // [G]
+    int G = 1;
+};
+
 hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
                         const uint32_t *offsets, const uint8_t *flags, const uint32_t *tilesum, uint32_t *tilepre,
                         uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
                         ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
-                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk);
+                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk,
+                        const GxPlace *gx = nullptr);
+// flush only / place only (the node-global mode chains the flush walk across ranks)
+hipError_t launch_store_scan(const StoreParams &P, const BlockState *bst, const uint32_t *offsets, const uint8_t *flags,
+                             const uint32_t *tilesum, uint32_t *tilepre, uint64_t *store_size, uint32_t *pre,
+                             hipStream_t st);
+hipError_t launch_store_flush(const StoreParams &P, const BlockState *bst, const uint64_t *store_size, const uint32_t *pre,
+                              AllocState *alloc, RangeState *rstate, FlushEv *events, ClosedRec *closed,
+                              uint32_t *nclosed, int *err, hipStream_t st);
+hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
+                              const uint32_t *offsets, const uint8_t *flags, const uint32_t *pre,
+                              const RangeState *rstate, const FlushEv *events, const uint32_t *slot, IndexEntry *tab,
+                              uint8_t *arena, uint32_t *place_cid, uint32_t *place_pos, const GxPlace &gx,
+                              hipStream_t st);
+hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int cap_blk, int ntiles,
+                          const uint32_t *digests, IndexEntry *scratch, const uint32_t *slot, const uint8_t *flags,
+                          uint32_t gbase, int G, uint32_t *x1, int64_t cap, unsigned long long *counts, int *err,
+                          hipStream_t st);
+hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts, int64_t max_count, int64_t cap, int G,
+                           IndexEntry *tab, int log2cap, uint32_t cur, unsigned long long tag_mask, uint32_t *oslot,
+                           uint8_t *oflags, uint32_t *coll, uint32_t *ncoll, int coll_cap, uint32_t *x2, int *err,
+                           hipStream_t st);
+hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int ntiles, const uint32_t *offsets,
+                            const IndexEntry *scratch, const uint32_t *slot, const uint32_t *x2, uint8_t *flags,
+                            uint32_t *tilesum, hipStream_t st);
+hipError_t launch_gx_commit(const uint32_t *x3, const int64_t *counts, int64_t max_count, int64_t cap, int G,
+                            IndexEntry *tab, hipStream_t st);
 hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
                          uint64_t seed, hipStream_t st);
 

@@ -235,7 +235,8 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
                                                     const RangeState *__restrict__ rstate,
                                                     const FlushEv *__restrict__ events, const uint32_t *__restrict__ slot,
                                                     IndexEntry *__restrict__ tab, uint8_t *__restrict__ arena,
-                                                    uint32_t *__restrict__ place_cid, uint32_t *__restrict__ place_pos)
+                                                    uint32_t *__restrict__ place_cid, uint32_t *__restrict__ place_pos,
+                                                    GxPlace gx)
 {
     const int b = blockIdx.y;
     const int k = blockIdx.x * 256 + threadIdx.x;
@@ -278,7 +279,16 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
         IndexEntry *e = tab + slot[c];
         if (desig && (f & 16))                             // ... and its last occurrence there
             desig = (uint32_t)e->first == (uint32_t)(k + 1);
-        if (desig) {                                       // designated: final index value
+        if (desig && gx.x3) {                              // node-global index (gx.hip): the
+            if (f & 4) {                                   // owner commits the new entry's location
+                const uint32_t ri = e->cid;
+                const int d = (int)(ri / (uint64_t)gx.cap);
+                const unsigned long long i = atomicAdd(gx.counts + d, 1ull);
+                uint32_t *rec = gx.x3 + ((size_t)d * gx.cap + i) * 4;
+                rec[0] = gx.x2[2 * (size_t)ri];
+                rec[1] = cid; rec[2] = pos; rec[3] = pos + ((f & 1) && do_copy ? len : 0u);
+            }
+        } else if (desig) {                                // designated: final index value
             const unsigned long long m = e->mask;
             const uint32_t cnt = (uint32_t)__popcll(m);
             if (f & 4) {
@@ -326,26 +336,57 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
     }
 }
 
+hipError_t launch_store_scan(const StoreParams &P, const BlockState *bst, const uint32_t *offsets, const uint8_t *flags,
+                             const uint32_t *tilesum, uint32_t *tilepre, uint64_t *store_size, uint32_t *pre,
+                             hipStream_t st)
+{
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(P.nblocks), dim3(256), 0, st, bst, P.ntiles, tilesum, tilepre,
+                       store_size, P.cap_blk);
+    hipLaunchKernelGGL(chunk_scan_kernel, dim3(P.ntiles, P.nblocks), dim3(256), 0, st, bst, P.cap_blk, P.ntiles,
+                       offsets, flags, tilepre, pre);
+    return hipGetLastError();
+}
+
+hipError_t launch_store_flush(const StoreParams &P, const BlockState *bst, const uint64_t *store_size, const uint32_t *pre,
+                              AllocState *alloc, RangeState *rstate, FlushEv *events, ClosedRec *closed,
+                              uint32_t *nclosed, int *err, hipStream_t st)
+{
+    hipLaunchKernelGGL(flush_kernel, dim3(1), dim3(256), 0, st, P, bst, store_size, pre, alloc, rstate, events, closed,
+                       nclosed, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
+                              const uint32_t *offsets, const uint8_t *flags, const uint32_t *pre,
+                              const RangeState *rstate, const FlushEv *events, const uint32_t *slot, IndexEntry *tab,
+                              uint8_t *arena, uint32_t *place_cid, uint32_t *place_pos, const GxPlace &gx,
+                              hipStream_t st)
+{
+    if (gx.x3) (void)hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st);
+    hipLaunchKernelGGL(place_kernel, dim3(P.ntiles, P.nblocks), dim3(256), 0, st, P, d_blocks, bst, offsets, flags, pre,
+                       rstate, events, slot, tab, arena, place_cid, place_pos, gx);
+    return hipGetLastError();
+}
+
 hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
                         const uint32_t *offsets, const uint8_t *flags, const uint32_t *tilesum, uint32_t *tilepre,
                         uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
                         ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
-                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk)
+                        uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk,
+                        const GxPlace *gx)
 {
+    const GxPlace gxp = gx ? *gx : GxPlace{};
     mk->mark(st);
-    dim3 g(P.ntiles, P.nblocks);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(P.nblocks), dim3(256), 0, st, bst, P.ntiles, tilesum, tilepre,
-                       store_size, P.cap_blk);
-    hipLaunchKernelGGL(chunk_scan_kernel, g, dim3(256), 0, st, bst, P.cap_blk, P.ntiles, offsets, flags, tilepre, pre);
+    hipError_t e = launch_store_scan(P, bst, offsets, flags, tilesum, tilepre, store_size, pre, st);
     mk->mark(st);
-    hipLaunchKernelGGL(flush_kernel, dim3(1), dim3(256), 0, st, P, bst, store_size, pre, alloc, rstate, events, closed,
-                       nclosed, err);
+    if (e == hipSuccess) e = launch_store_flush(P, bst, store_size, pre, alloc, rstate, events, closed, nclosed, err, st);
     mk->mark(st);
-    hipLaunchKernelGGL(place_kernel, g, dim3(256), 0, st, P, d_blocks, bst, offsets, flags, pre, rstate, events, slot,
-                       tab, arena, place_cid, place_pos);
+    if (e == hipSuccess)
+        e = launch_store_place(P, d_blocks, bst, offsets, flags, pre, rstate, events, slot, tab, arena, place_cid,
+                               place_pos, gxp, st);
     mk->mark(st);
     mk->mark(st);   // spare stage (kept so stage indices stay stable)
-    return hipGetLastError();
+    return e;
 }
 
 }  // namespace hdrf

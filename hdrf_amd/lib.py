@@ -25,7 +25,11 @@ EXPORTS = [
     "hdrf_index_count", "hdrf_index_dump", "hdrf_allocator", "hdrf_recipe_get", "hdrf_block_length",
     "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_stage_times", "hdrf_reset",
+    "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
+    "hdrf_gx_place", "hdrf_gx_commit",
 ]
+
+ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
 
 
 # per-stage timers of hdrf_stage_times (kernel names in parentheses)
@@ -48,8 +52,13 @@ class Config(ctypes.Structure):
         ("container_max", ctypes.c_uint32), ("device", ctypes.c_int32), ("max_block_bytes", ctypes.c_int64),
         ("max_batch_blocks", ctypes.c_int32), ("index_log2", ctypes.c_int32), ("arena_slots", ctypes.c_int64),
         ("segment_bytes", ctypes.c_int32), ("keep_recipes", ctypes.c_int32), ("timing", ctypes.c_int32),
-        ("debug_tag_bits", ctypes.c_int32),
+        ("debug_tag_bits", ctypes.c_int32), ("n_ranks", ctypes.c_int32), ("rank", ctypes.c_int32),
     ]
+
+
+class GxLayout(ctypes.Structure):
+    _fields_ = [("cap", ctypes.c_int64), ("x1_words", ctypes.c_int32), ("x2_words", ctypes.c_int32),
+                ("x3_words", ctypes.c_int32)]
 
 
 class BlockResult(ctypes.Structure):
@@ -116,6 +125,14 @@ def load():
                                             ctypes.c_uint64]),
         "hdrf_stage_times": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int32]),
         "hdrf_reset": (ctypes.c_int, [_vp]),
+        "hdrf_gx_layout_get": (ctypes.c_int, [_vp, ctypes.POINTER(GxLayout)]),
+        "hdrf_gx_front": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p,
+                                         ctypes.c_uint32, _vp, _i64p]),
+        "hdrf_gx_owner": (ctypes.c_int, [_vp, _vp, _i64p, _vp]),
+        "hdrf_gx_decide": (ctypes.c_int, [_vp, _vp]),
+        "hdrf_gx_flush": (ctypes.c_int, [_vp, _u8p, _u8p]),
+        "hdrf_gx_place": (ctypes.c_int, [_vp, _u8p, _vp, _i64p]),
+        "hdrf_gx_commit": (ctypes.c_int, [_vp, _vp, _i64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -300,3 +317,43 @@ class Context:
 
     def reset(self):
         self._ck(self.L.hdrf_reset(self._h))
+
+    # ---- node-global index phases (include/hdrf.h; orchestrated by hdrf_amd/node.py) -----
+    def gx_layout(self):
+        lay = GxLayout()
+        self._ck(self.L.hdrf_gx_layout_get(self._h, ctypes.byref(lay)))
+        return lay
+
+    def gx_front(self, dev_ptrs, lens, readable, block_ids, gbase, x1_send):
+        n = len(dev_ptrs)
+        ptrs = (_vp * n)(*dev_ptrs)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        rd = np.ascontiguousarray(readable, np.uint64)
+        ids = np.ascontiguousarray(block_ids, np.uint64)
+        cnt = np.zeros(self.cfg.n_ranks, np.int64)
+        self._ck(self.L.hdrf_gx_front(self._h, n, ptrs, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p), gbase,
+                                      x1_send, _p(cnt, _i64p)))
+        return cnt
+
+    def gx_owner(self, x1_recv, recv_counts, x2_send):
+        rc = np.ascontiguousarray(recv_counts, np.int64)
+        self._ck(self.L.hdrf_gx_owner(self._h, x1_recv, _p(rc, _i64p), x2_send))
+
+    def gx_decide(self, x2_recv):
+        self._ck(self.L.hdrf_gx_decide(self._h, x2_recv))
+
+    def gx_flush(self, alloc_in=None):
+        out = np.zeros(ALLOC_STATE_BYTES, np.uint8)
+        ain = None if alloc_in is None else _p(np.ascontiguousarray(alloc_in, np.uint8))
+        self._ck(self.L.hdrf_gx_flush(self._h, ain, _p(out)))
+        return out
+
+    def gx_place(self, alloc_final, x3_send):
+        cnt = np.zeros(self.cfg.n_ranks, np.int64)
+        af = None if alloc_final is None else _p(np.ascontiguousarray(alloc_final, np.uint8))
+        self._ck(self.L.hdrf_gx_place(self._h, af, x3_send, _p(cnt, _i64p)))
+        return cnt
+
+    def gx_commit(self, x3_recv, recv_counts):
+        rc = np.ascontiguousarray(recv_counts, np.int64)
+        self._ck(self.L.hdrf_gx_commit(self._h, x3_recv, _p(rc, _i64p)))

@@ -1,0 +1,138 @@
+"""Node-global reduction over G GPUs: one fingerprint index partitioned by digest prefix.
+
+Reference behaviour (BASELINE config 3): all DataNodes of one host share one
+Redis (`JedisPool("localhost")`, DN/DataDeduplicator.java:119), one "blockID" allocator
+(:165-172, :389), one chunkDir and one static FIFO (:124-158, :197-204), so the node is ONE
+reduction over the global block sequence.  Here each GPU is a rank: it reduces its own shard
+of every global batch and owns the index partition {digest : first digest word mod G == rank};
+the three record exchanges of a batch are all-to-alls over RCCL (xGMI) — or gloo when the
+ranks share a device in tests — and the container allocator is handed rank to rank.  The
+result is byte-identical to one sequential run over the global order (rank-major within a
+global batch), which is what tests/test_node.py checks against the oracle.
+
+The phases themselves are C-ABI calls into libhdrf (include/hdrf.h, hdrf_gx_*); this module
+only moves bytes between ranks.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .lib import ALLOC_STATE_BYTES
+
+
+class Exchange:
+    """all-to-all of variable-length record regions laid out [G][cap][words] (int32 words)."""
+
+    def __init__(self, G, rank, device):
+        self.G, self.rank, self.device = G, rank, device      # default process group, rank = GPU
+        self.nccl = dist.get_backend() == "nccl"
+        if self.nccl and (device is None or device.type != "cuda"):
+            raise ValueError("the nccl (RCCL) exchange needs a GPU device")
+
+    def counts(self, send_counts):
+        """Every rank's send counts -> this rank's receive counts (int64[G])."""
+        if self.nccl:
+            s = torch.as_tensor(np.asarray(send_counts, np.int64), device=self.device)
+        else:
+            s = torch.as_tensor(np.asarray(send_counts, np.int64))
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s)
+        return r.cpu().numpy()
+
+    def records(self, send, recv, send_counts, recv_counts, cap, words):
+        G = self.G
+        if self.nccl:
+            sv = [send[d * cap * words:(d * cap + int(send_counts[d])) * words] for d in range(G)]
+            rv = [recv[s * cap * words:(s * cap + int(recv_counts[s])) * words] for s in range(G)]
+            dist.all_to_all(rv, sv)
+            torch.cuda.current_stream(self.device).synchronize()
+            return
+        # (a CPU device is allowed here: the multi-process CPU tests drive this path directly)
+        # gloo: stage through host memory, packed for all_to_all_single
+        packed = torch.cat([send[d * cap * words:(d * cap + int(send_counts[d])) * words].cpu() for d in range(G)])
+        out = torch.empty(int(np.sum(recv_counts)) * words, dtype=send.dtype)
+        dist.all_to_all_single(out, packed, [int(c) * words for c in recv_counts],
+                               [int(c) * words for c in send_counts])
+        o = 0
+        for s in range(G):
+            n = int(recv_counts[s]) * words
+            if n:
+                recv[s * cap * words:s * cap * words + n].copy_(out[o:o + n])
+            o += n
+        if recv.is_cuda:
+            torch.cuda.current_stream(recv.device).synchronize()
+
+    def chain_alloc(self, alloc_prev_batch, flush):
+        """Rank r flushes after rank r-1 (rank 0 starts from the node's state); returns the node's
+        allocator state after the last rank, known to every rank."""
+        G, r = self.G, self.rank
+        dev = self.device if self.nccl else None
+        if r == 0:
+            a_in = alloc_prev_batch
+        else:
+            t = torch.empty(ALLOC_STATE_BYTES, dtype=torch.uint8, device=dev)
+            dist.recv(t, src=r - 1)
+            a_in = t.cpu().numpy()
+        a_out = flush(a_in)
+        if r + 1 < G:
+            t = torch.as_tensor(a_out, device=dev)
+            dist.send(t, dst=r + 1)
+        fin = torch.as_tensor(a_out, device=dev) if r == G - 1 else torch.empty(ALLOC_STATE_BYTES, dtype=torch.uint8,
+                                                                                 device=dev)
+        dist.broadcast(fin, src=G - 1)
+        return fin.cpu().numpy()
+
+
+class NodeRank:
+    """One GPU's share of a node-global reduction (ctx must be opened with n_ranks = G > 1)."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        self.G = int(ctx.cfg.n_ranks)
+        self.rank = int(ctx.cfg.rank)
+        if self.G < 2:
+            raise ValueError("NodeRank needs a context opened with n_ranks > 1")
+        self.device = torch.device("cuda", int(ctx.cfg.device))
+        self.xc = Exchange(self.G, self.rank, self.device)
+        lay = ctx.gx_layout()
+        self.cap, self.w = int(lay.cap), (int(lay.x1_words), int(lay.x2_words), int(lay.x3_words))
+        n = self.G * self.cap
+        mk = lambda w: torch.empty(n * w, dtype=torch.int32, device=self.device)  # noqa: E731
+        self.x1s, self.x1r = mk(self.w[0]), mk(self.w[0])
+        self.x2s, self.x2r = mk(self.w[1]), mk(self.w[1])
+        self.x3s, self.x3r = mk(self.w[2]), mk(self.w[2])
+        self.alloc = None          # node allocator after the last batch (None: initial state)
+
+    def reset(self):
+        self.ctx.reset()
+        self.alloc = None
+
+    def reduce_batch(self, dev_ptrs, lens, readable, block_ids, gbase):
+        """Reduce this rank's blocks of one global batch; gbase = its first batch position."""
+        ctx, xc, cap, (w1, w2, w3) = self.ctx, self.xc, self.cap, self.w
+        torch.cuda.current_stream(self.device).synchronize()
+        c1 = ctx.gx_front(dev_ptrs, lens, readable, block_ids, gbase, self.x1s.data_ptr())
+        r1 = xc.counts(c1)
+        xc.records(self.x1s, self.x1r, c1, r1, cap, w1)
+        ctx.gx_owner(self.x1r.data_ptr(), r1, self.x2s.data_ptr())
+        xc.records(self.x2s, self.x2r, r1, c1, cap, w2)           # responses retrace X1
+        ctx.gx_decide(self.x2r.data_ptr())
+        self.alloc = xc.chain_alloc(self.alloc, ctx.gx_flush)
+        c3 = ctx.gx_place(self.alloc, self.x3s.data_ptr())
+        r3 = xc.counts(c3)
+        xc.records(self.x3s, self.x3r, c3, r3, cap, w3)
+        ctx.gx_commit(self.x3r.data_ptr(), r3)
+
+    def batch_base(self, nblocks):
+        """Rank-major batch positions: gbase of this rank given every rank's block count."""
+        t = torch.tensor([nblocks], dtype=torch.int64, device=self.device if self.xc.nccl else None)
+        allc = [torch.empty_like(t) for _ in range(self.G)]
+        dist.all_gather(allc, t)
+        counts = [int(x.item()) for x in allc]
+        return sum(counts[:self.rank]), counts
+
+
+def global_block(local, rank, G, B):
+    """Global sequence number of rank's local block `local` when every global batch takes B
+    blocks from each rank, rank-major (rank 0's B blocks, then rank 1's, ...)."""
+    return (local // B) * G * B + rank * B + (local % B)

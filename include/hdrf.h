@@ -50,6 +50,8 @@ typedef struct {
     int32_t timing;          /* record per-stage HIP events */
     int32_t debug_tag_bits;  /* test hook (SHA-1 only): keep only this many index-tag bits to force
                                 tag collisions through the exact slow path; 0 = full 64-bit tag */
+    int32_t n_ranks;         /* GPUs sharing ONE node-global index (1 = this GPU is the whole node) */
+    int32_t rank;            /* this GPU's rank in [0, n_ranks) = index partition it owns */
 } hdrf_cfg;
 
 /* Per-block result of hdrf_reduce_block (caller-owned host arrays; NULL to skip). */
@@ -127,6 +129,42 @@ int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, in
 int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
 /* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis). */
 int hdrf_reset(hdrf_ctx *ctx);
+
+/* ---- Node-global index over n_ranks GPUs (BASELINE config 3) -------------------
+ * All DataNodes of one host share one Redis (JedisPool("localhost"), DN/DataDeduplicator.java:119),
+ * one "blockID" allocator (:165-172,:389), one chunkDir and one FIFO (:124-158): the node is ONE
+ * reduction over the global block sequence.  With n_ranks > 1 each context owns the index
+ * partition {digest : first digest word mod n_ranks == rank} and reduces the blocks it receives;
+ * a global batch is rank-major (rank r's blocks take batch positions [gbase_r, gbase_r + nblocks_r)).
+ * The caller moves the records between ranks (all-to-all over RCCL/xGMI, hdrf_amd/node.py).
+ * Buffers are device pointers laid out [n_ranks][cap][words] (region d = peer d); counts are
+ * host int64[n_ranks].  Per global batch, every rank calls, in order:
+ *   hdrf_gx_front  -> X1 send (records for each owner)      all-to-all X1
+ *   hdrf_gx_owner  <- X1 recv, -> X2 send (responses)        all-to-all X2 (reverse counts)
+ *   hdrf_gx_decide <- X2 recv
+ *   hdrf_gx_flush  (rank order: rank r gets rank r-1's allocator state, rank 0 the node's)
+ *   hdrf_gx_place  -> X3 send (locations of new entries)     all-to-all X3
+ *   hdrf_gx_commit <- X3 recv
+ * hdrf_reduce_block / hdrf_reduce_batch return HDRF_E_INVAL on such a context. */
+#define HDRF_ALLOC_STATE_BYTES 128
+typedef struct {
+    int64_t cap;             /* records per peer region (all three exchanges) */
+    int32_t x1_words;        /* u32 words per X1 record (digest words + batch position + count) */
+    int32_t x2_words;        /* 2: owner slot, flags */
+    int32_t x3_words;        /* 4: owner slot, container id, start, stop */
+} hdrf_gx_layout;
+int hdrf_gx_layout_get(hdrf_ctx *ctx, hdrf_gx_layout *out);
+int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                  const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send,
+                  int64_t *send_counts);
+int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send);
+int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv);
+/* alloc_in: HDRF_ALLOC_STATE_BYTES from the previous rank (NULL: this context's own state);
+ * alloc_out receives the state after this rank's blocks. */
+int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out);
+/* alloc_final: the node's state after the last rank's flush (becomes this context's state). */
+int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts);
+int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,49 @@
+"""World-size-2 gloo worker for tests/test_node.py::test_exchange_gloo_cpu_world2 (CPU only)."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hdrf_amd.lib import ALLOC_STATE_BYTES  # noqa: E402
+from hdrf_amd.node import Exchange  # noqa: E402
+
+
+def main():
+    dist.init_process_group("gloo")
+    r, G = dist.get_rank(), dist.get_world_size()
+    xc = Exchange(G, r, None)
+    cap, w = 50, 3
+    send = torch.full((G * cap * w,), -1, dtype=torch.int32)
+    counts = np.array([(r * 7 + d * 3) % 11 + d for d in range(G)], np.int64)
+    for d in range(G):
+        for i in range(int(counts[d])):
+            send[(d * cap + i) * w:(d * cap + i + 1) * w] = torch.tensor([r, d, i], dtype=torch.int32)
+    rc = xc.counts(counts)
+    expect_rc = np.array([(s * 7 + r * 3) % 11 + r for s in range(G)], np.int64)
+    assert np.array_equal(rc, expect_rc), (rc, expect_rc)
+    recv = torch.full((G * cap * w,), -1, dtype=torch.int32)
+    xc.records(send, recv, counts, rc, cap, w)
+    for s in range(G):
+        for i in range(int(rc[s])):
+            got = recv[(s * cap + i) * w:(s * cap + i + 1) * w].tolist()
+            assert got == [s, r, i], (s, i, got)
+        assert int(recv[(s * cap + int(rc[s])) * w]) == -1      # nothing past the count
+    # allocator hand-off: each rank adds its rank+1 to byte 0; everyone sees the last rank's state
+    start = np.zeros(ALLOC_STATE_BYTES, np.uint8)
+
+    def flush(a_in):
+        a = np.array(a_in if a_in is not None else start, np.uint8)
+        a[0] += r + 1
+        a[1 + r] = 0xA0 + r
+        return a
+    fin = xc.chain_alloc(start, flush)
+    assert int(fin[0]) == G * (G + 1) // 2 and all(int(fin[1 + q]) == 0xA0 + q for q in range(G)), fin[:4]
+    print("exchange ok", r, flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

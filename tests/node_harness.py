@@ -1,0 +1,119 @@
+"""Node-global (multi-GPU) test harness: G ranks' contexts driven phase by phase, in one
+process (loopback exchange: torch copies between the ranks' record buffers) or one rank per
+process (hdrf_amd.node.NodeRank over torch.distributed), and the merge of the ranks' views
+into the single-node view the oracle produces for the global block sequence."""
+import numpy as np
+import torch
+
+from hdrf_amd.lib import Context
+from helpers import make_block
+
+
+def open_ranks(G, device=0, **cfg):
+    return [Context(device=device, n_ranks=G, rank=r, **cfg) for r in range(G)]
+
+
+class Loopback:
+    """All G ranks in this process: the X1/X2/X3 all-to-alls become region copies."""
+
+    def __init__(self, ctxs):
+        self.ctxs = ctxs
+        self.G = len(ctxs)
+        lay = ctxs[0].gx_layout()
+        self.cap, self.w = int(lay.cap), (int(lay.x1_words), int(lay.x2_words), int(lay.x3_words))
+        dev = torch.device("cuda", int(ctxs[0].cfg.device))
+        n = self.G * self.cap
+
+        def mk(w):
+            return [torch.zeros(n * w, dtype=torch.int32, device=dev) for _ in range(self.G)]
+        self.x1s, self.x1r = mk(self.w[0]), mk(self.w[0])
+        self.x2s, self.x2r = mk(self.w[1]), mk(self.w[1])
+        self.x3s, self.x3r = mk(self.w[2]), mk(self.w[2])
+        self.alloc = None
+
+    def _a2a(self, send, recv, counts, w):
+        """counts[s][d] records from rank s to rank d; returns recv counts [d][s]."""
+        cap, G = self.cap, self.G
+        for s in range(G):
+            for d in range(G):
+                n = int(counts[s][d]) * w
+                if n:
+                    recv[d][s * cap * w:s * cap * w + n].copy_(send[s][d * cap * w:d * cap * w + n])
+        torch.cuda.synchronize()
+        return [[int(counts[s][d]) for s in range(G)] for d in range(G)]
+
+    def batch(self, per_rank):
+        """per_rank[r] = (dev_ptrs, lens, readable, block_ids) of rank r's blocks, rank-major."""
+        G, ctxs = self.G, self.ctxs
+        gb = np.cumsum([0] + [len(p[0]) for p in per_rank])
+        c1 = [ctxs[r].gx_front(*per_rank[r], int(gb[r]), self.x1s[r].data_ptr()) for r in range(G)]
+        r1 = self._a2a(self.x1s, self.x1r, c1, self.w[0])
+        for d in range(G):
+            ctxs[d].gx_owner(self.x1r[d].data_ptr(), r1[d], self.x2s[d].data_ptr())
+        self._a2a(self.x2s, self.x2r, r1, self.w[1])
+        for r in range(G):
+            ctxs[r].gx_decide(self.x2r[r].data_ptr())
+        a = self.alloc
+        for r in range(G):
+            a = ctxs[r].gx_flush(a)
+        self.alloc = a
+        c3 = [ctxs[r].gx_place(a, self.x3s[r].data_ptr()) for r in range(G)]
+        r3 = self._a2a(self.x3s, self.x3r, c3, self.w[2])
+        for d in range(G):
+            ctxs[d].gx_commit(self.x3r[d].data_ptr(), r3[d])
+
+
+def merged_index(ctxs):
+    """Union of the ranks' index partitions, sorted by digest (the node's Redis)."""
+    ks, vs = zip(*[c.index_dump() for c in ctxs])
+    k = np.concatenate(ks)
+    v = np.concatenate(vs)
+    order = np.lexsort(k.T[::-1])
+    return k[order], v[order]
+
+
+def assemble_containers(pieces):
+    """pieces: (cid, pos, bytes) of every new chunk on every rank -> {cid: container bytes}."""
+    out = {}
+    for cid, pos, data in pieces:
+        buf = out.setdefault(cid, bytearray())
+        end = pos + len(data)
+        if len(buf) < end:
+            buf.extend(b"\0" * (end - len(buf)))
+        buf[pos:end] = data
+    return {k: bytes(v) for k, v in out.items()}
+
+
+def mixed_blocks(seed, nblk, size):
+    """Blocks with cross-block duplicates (copies of earlier blocks' pieces), intra-block
+    repeats and a few non-random kinds."""
+    rng = np.random.default_rng(seed)
+    pool = [make_block("random", seed * 100 + i, size) for i in range(4)]
+    out = []
+    for i in range(nblk):
+        kind = i % 5
+        if kind == 3:
+            out.append(make_block("text", seed + i, size // 2))
+            continue
+        parts = []
+        for _ in range(4):
+            src = pool[int(rng.integers(len(pool)))] if (i and rng.random() < 0.5) else \
+                make_block("random", seed * 1000 + i * 10 + len(parts), size)
+            a = int(rng.integers(0, size // 2))
+            parts.append(src[a:a + size // 4])
+        blk = np.concatenate(parts)
+        if kind == 4:
+            blk = np.concatenate([blk[: size // 3], blk[: size // 3]])      # intra-block repeat
+        out.append(blk)
+        pool.append(blk)
+    return out
+
+
+def plan(nblocks_per_rank_per_batch):
+    """Global sequence of (batch, rank, local index) in rank-major order."""
+    seq = []
+    for j, per in enumerate(nblocks_per_rank_per_batch):
+        for r, n in enumerate(per):
+            for i in range(n):
+                seq.append((j, r, i))
+    return seq

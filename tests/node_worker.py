@@ -1,0 +1,82 @@
+"""One rank of tests/test_node.py::test_node_two_processes_gloo: a real torch.distributed rank
+(gloo; both ranks share cuda:0) reducing its shard through hdrf_amd.node.NodeRank, then saving its
+per-block results and views for the parent test to merge and check against the oracle."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCHED = [[2, 2], [1, 2], [2, 1]]
+CMAX = 1 << 20
+SIZE = 600_000
+
+
+def blocks():
+    from node_harness import mixed_blocks, plan
+    seq = plan(SCHED)
+    return seq, mixed_blocks(31, len(seq), SIZE)
+
+
+def main(out):
+    import torch.distributed as dist
+    from hdrf_amd.lib import Context
+    from hdrf_amd.node import NodeRank
+    dist.init_process_group("gloo")
+    r, G = dist.get_rank(), dist.get_world_size()
+    seq, blks = blocks()
+    ctx = Context(device=0, n_ranks=G, rank=r, container_max=CMAX, max_block_bytes=2 << 20, max_batch_blocks=4,
+                  index_log2=20, arena_slots=128)
+    node = NodeRank(ctx)
+    res = {}
+    for j, per in enumerate(SCHED):
+        mine = [gi for gi, (jj, rr, _) in enumerate(seq) if jj == j and rr == r]
+        ptrs, lens, rd, ids = [], [], [], []
+        for gi in mine:
+            p = ctx.dev_alloc(len(blks[gi]) + 4096)
+            ctx.h2d(p, blks[gi])
+            ptrs.append(p); lens.append(len(blks[gi])); rd.append(len(blks[gi]) + 4096); ids.append(0x900 + gi)
+        gbase, _ = node.batch_base(len(mine))
+        node.reduce_batch(ptrs, lens, rd, ids, gbase)
+        for i, gi in enumerate(mine):
+            b = ctx.batch_result(i)
+            for k in ("offsets", "digests", "is_new", "container_id", "container_pos"):
+                res[f"b{gi}_{k}"] = b[k]
+            res[f"b{gi}_store"] = np.array([b["store_size"]])
+            res[f"b{gi}_recipe"] = np.frombuffer(ctx.recipe(0x900 + gi), np.uint8)
+        for p in ptrs:
+            ctx.dev_free(p)
+    k, v = ctx.index_dump()
+    res["index_keys"], res["index_vals"] = k, v
+    res["alloc"] = np.frombuffer(ctx.allocator(), np.uint8)
+    np.savez(os.path.join(out, f"rank{r}.npz"), **res)
+    ctx.close()
+    dist.destroy_process_group()
+
+
+def check_outputs(out, G):
+    from helpers import compare_block
+    from oracle.oracle import Oracle
+    seq, blks = blocks()
+    ranks = [np.load(os.path.join(out, f"rank{r}.npz")) for r in range(G)]
+    ora = Oracle(hasher=0, compressor=1, max_size=CMAX)
+    for gi, (_, r, _) in enumerate(seq):
+        o = ora.reduce(blks[gi], 0x900 + gi)
+        z = ranks[r]
+        g = {k: z[f"b{gi}_{k}"] for k in ("offsets", "digests", "is_new", "container_id", "container_pos")}
+        g["store_size"] = int(z[f"b{gi}_store"][0])
+        compare_block(g, o, tag=f"global block {gi} on rank {r}")
+        assert z[f"b{gi}_recipe"].tobytes() == ora.recipe(0x900 + gi)
+    k = np.concatenate([z["index_keys"] for z in ranks])
+    v = np.concatenate([z["index_vals"] for z in ranks])
+    order = np.lexsort(k.T[::-1])
+    ok, ov = ora.index_dump()
+    assert np.array_equal(k[order], ok) and np.array_equal(v[order], ov), "node index differs"
+    for z in ranks:
+        assert z["alloc"].tobytes() == ora.allocator()
+
+
+if __name__ == "__main__":
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    main(sys.argv[1])

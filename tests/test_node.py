@@ -1,0 +1,128 @@
+"""Node-global index over G ranks (BASELINE config 3): G contexts that share one
+index partitioned by digest prefix must reproduce, byte for byte, ONE sequential reduction of the
+global block sequence (the oracle): chunk boundaries, digests, dedup decisions, storeSize,
+container placement and bytes, every index value (nCopy + location), allocator and recipes.
+
+GPU tests drive the ranks' HIP contexts on one device, either in one process (loopback copies
+between the ranks' exchange buffers) or as real ranks over torch.distributed (gloo staging, the
+same NodeRank code the 8-GPU bench runs over RCCL).  The CPU test covers the exchange plumbing
+of hdrf_amd/node.py with world_size 2 on gloo."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from helpers import compare_block, make_block
+from node_harness import mixed_blocks as _mixed_blocks, plan as _plan
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,hasher,sched", [
+    (2, 0, [[2, 3], [3, 1], [1, 1]]),
+    (3, 1, [[2, 2, 2], [1, 3, 2]]),
+    (4, 0, [[1, 2, 1, 2], [2, 1, 1, 1]]),
+])
+def test_node_loopback_matches_single_sequence(G, hasher, sched):
+    import torch  # noqa: F401
+    from node_harness import Loopback, assemble_containers, merged_index, open_ranks
+    from oracle.oracle import Oracle
+
+    cmax = 1 << 20                                   # small containers: many flushes across ranks
+    seq = _plan(sched)
+    blocks = _mixed_blocks(7 + G, len(seq), 700_000)
+    ctxs = open_ranks(G, hasher=hasher, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=4,
+                      index_log2=20, arena_slots=256)
+    lb = Loopback(ctxs)
+    ora = Oracle(hasher=hasher, compressor=1, max_size=cmax)
+    devs = []
+    pieces = []
+    g = 0
+    for j, per in enumerate(sched):
+        per_rank, gidx = [], []
+        for r, n in enumerate(per):
+            ptrs, lens, rd, ids = [], [], [], []
+            for i in range(n):
+                blk = blocks[g + len(gidx)]
+                gidx.append((r, i, g + len(gidx)))
+                p = ctxs[r].dev_alloc(len(blk) + 4096)
+                ctxs[r].h2d(p, blk)
+                devs.append((ctxs[r], p))
+                ptrs.append(p); lens.append(len(blk)); rd.append(len(blk) + 4096); ids.append(0x500 + 3 * (g + len(gidx) - 1))
+            per_rank.append((ptrs, lens, rd, ids))
+        lb.batch(per_rank)
+        for r, i, gi in gidx:
+            res = ctxs[r].batch_result(i)
+            o = ora.reduce(blocks[gi], 0x500 + 3 * gi)
+            compare_block(res, o, tag=f"G={G} batch {j} rank {r} block {i} (global {gi})")
+            offs = res["offsets"]
+            for k in np.nonzero(res["is_new"])[0]:
+                a = int(offs[k - 1]) if k else 0
+                pieces.append((int(res["container_id"][k]), int(res["container_pos"][k]),
+                               blocks[gi][a:int(offs[k])].tobytes()))
+        g += len(gidx)
+    gk, gv = merged_index(ctxs)
+    ok, ov = ora.index_dump()
+    assert gk.shape == ok.shape and np.array_equal(gk, ok), "node index keys differ"
+    bad = np.nonzero((gv != ov).any(axis=1))[0]
+    assert bad.size == 0, f"index values differ at {bad[:5]}: {gv[bad[:3]]} vs {ov[bad[:3]]}"
+    for c in ctxs:
+        assert c.allocator() == ora.allocator(), "allocator differs"
+    for gi in range(len(seq)):
+        bid = 0x500 + 3 * gi
+        owner = ctxs[seq[gi][1]]
+        assert owner.recipe(bid) == ora.recipe(bid), f"recipe of global block {gi}"
+    conts = assemble_containers(pieces)
+    for cid, data in conts.items():
+        od, _ = ora.container(cid)
+        assert od is not None and od == data, f"container {cid:#x} bytes differ"
+    alloc = ora.allocator()
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, _ = ora.container(cid)
+            if od:
+                assert cid in conts, f"container {cid:#x} missing"
+    for c, p in devs:
+        c.dev_free(p)
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_node_context_rejects_single_node_calls():
+    from hdrf_amd.lib import Context, HdrfError
+    ctx = Context(n_ranks=2, rank=1, max_block_bytes=1 << 20, max_batch_blocks=2, index_log2=16, arena_slots=16,
+                  container_max=1 << 21)
+    with pytest.raises(HdrfError):
+        ctx.reduce_block(make_block("random", 1, 5000), 1)
+    with pytest.raises(HdrfError):                      # phases out of order
+        ctx.gx_decide(0)
+    ctx.close()
+
+
+@pytest.mark.gpu
+def test_node_two_processes_gloo(tmp_path):
+    """Two real ranks (one process each, both on cuda:0, gloo staging) through NodeRank."""
+    out = str(tmp_path)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", "29631", os.path.join(ROOT, "tests", "node_worker.py"), out]
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.path.join(ROOT, "tests"))
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    from node_worker import check_outputs
+    check_outputs(out, 2)
+
+
+def test_exchange_gloo_cpu_world2():
+    """hdrf_amd.node.Exchange on CPU tensors, world_size 2 over gloo: counts, variable regions and
+    the allocator hand-off chain."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", "29641", os.path.join(ROOT, "tests", "exchange_worker.py")]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("exchange ok") == 2, r.stdout[-2000:]
