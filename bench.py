@@ -8,9 +8,13 @@ order from a fresh index: window-max chunking -> SHA-1 -> GPU index (exact HDRF 
 semantics) -> container placement + gather into the container arena, in batches of 64
 blocks.  value = logical bytes reduced per second over all ranks (GB = 1e9 B).
 
-Multi-GPU (`torch.distributed.run`): every rank is an independent DataNode with its own
-corpus shard and index (HDRF keeps one Redis index per DataNode, DN/DataDeduplicator.java:119),
-so there is no collective in the data path; scaling is weak.
+Multi-GPU (`torch.distributed.run`, BASELINE config 3): the GPUs of the node are ranks of ONE
+reduction, as the DataNodes of one host share one Redis, allocator and chunkDir in the reference
+(DN/DataDeduplicator.java:119,165-172): a global corpus of N x 512 blocks sharded by block, each
+global batch takes 64 blocks from every rank, and the fingerprint index is partitioned by digest
+prefix with three RCCL all-to-alls per batch over xGMI (hdrf_amd/node.py).  Work per GPU is
+fixed as N grows: scaling is weak.  (HDRF_BENCH_SAME_DEVICE=1 puts every rank on cuda:0 over gloo:
+a one-GPU rehearsal of the multi-rank path, not a measurement.)
 
 The line also carries the dominant kernel's roofline (HIP events on the library's stream)
 and the CPU oracle timed on this host on a bounded sample of the same corpus, whose
@@ -71,8 +75,12 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+        if os.environ.get("HDRF_BENCH_SAME_DEVICE") == "1":
+            local = 0
+            dist.init_process_group(backend="gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
 
     from hdrf_amd.corpus import corpus_roots
     from hdrf_amd.lib import STAGES, Context
@@ -81,10 +89,24 @@ def main():
     seg = a.seg_mib << 20
     spb = S // seg
     nb, B = a.blocks, min(a.batch, a.blocks)
+    if nb % B:
+        raise SystemExit("--blocks must be a multiple of --batch")
+    # One node, one index: at N > 1 the GPUs are ranks of ONE reduction over the global block
+    # sequence (hdrf_amd/node.py): a global corpus of world*nb blocks, every global batch takes B
+    # blocks from each rank (rank-major), the index is partitioned by digest prefix.
     ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
-                  arena_slots=64, keep_recipes=0, timing=1)
-    seed = a.seed ^ (rank * 0x9E3779B9)
-    roots = corpus_roots(seed, a.dup_ppm, nb, spb)
+                  arena_slots=64, keep_recipes=0, timing=1, n_ranks=world, rank=rank)
+    node = None
+    if world > 1:
+        from hdrf_amd.node import NodeRank, global_block
+        node = NodeRank(ctx)
+    seed = a.seed
+    groots = corpus_roots(seed, a.dup_ppm, nb * world, spb).reshape(nb * world, spb)
+    if world > 1:
+        mine = [global_block(L, rank, world, B) for L in range(nb)]
+        roots = groots[mine].reshape(-1)
+    else:
+        roots = groots.reshape(-1)
     total = nb * S + 4096
     dev = ctx.dev_alloc(total)
     ctx.corpus_fill(dev, roots, nb, spb, seg, seed)
@@ -98,10 +120,16 @@ def main():
     store = np.zeros(nb, np.int64)
 
     def step():
-        ctx.reset()                                      # a fresh DataNode index each step
+        if node is None:
+            ctx.reset()                                  # a fresh DataNode index each step
+        else:
+            node.reset()
         j = 0
         for ptrs, lens, rd, ids in batches:
-            ctx.reduce_batch(ptrs, lens, rd, ids)
+            if node is None:
+                ctx.reduce_batch(ptrs, lens, rd, ids)
+            else:
+                node.reduce_batch(ptrs, lens, rd, ids, rank * B)
             for i in range(len(ptrs)):
                 n_chunks[j], store[j] = ctx.batch_info(i)
                 j += 1
@@ -125,7 +153,7 @@ def main():
     el = time.perf_counter() - t0
     stage_ms = ctx.stage_times(reset=True)
     if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     ms_step = el / a.steps * 1e3
@@ -152,6 +180,9 @@ def main():
     dom_ms = stage_ms[STAGES.index(dom)] / a.steps / nbatch
     achieved = per_launch[dom] / (dom_ms * 1e-3) / 1e9
     pmc, pmc_src = load_pmc()
+    want = {"blocks": nb, "block_mib": a.block_mib, "batch": B, "n_gpus": world, "hasher": a.hasher}
+    if any(pmc.get("_config", {}).get(k) != v for k, v in want.items()):
+        pmc, pmc_src = {}, None                        # profiled on another workload: not this one's traffic
     kname = KERNEL_OF[dom] + ("<5>" if a.hasher == 0 else "<7>") * (dom in (STAGES[2],))
     prof = pmc.get(kname, {})
     roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -167,10 +198,17 @@ def main():
                             "frac": round(wi_ns / VALU_PEAK_WI_NS, 4),
                             "sq_insts_valu_per_launch": int(prof["sq_insts_valu"])}
 
-    dedup = {"logical_bytes_per_gpu": nb * S, "stored_bytes_per_gpu": new_bytes,
-             "dedup_ratio": round(nb * S / max(new_bytes, 1), 6),
-             "dup_fraction": round(1 - new_bytes / (nb * S), 6), "target_dup_fraction": a.dup_ppm / 1e6,
-             "chunks_per_gpu": chunks_step, "mean_chunk_bytes": round(nb * S / max(chunks_step, 1), 1)}
+    node_new, node_chunks = new_bytes, chunks_step
+    if dist is not None:
+        t = torch.tensor([new_bytes, chunks_step], dtype=torch.int64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t)
+        node_new, node_chunks = int(t[0].item()), int(t[1].item())
+    dedup = {"logical_bytes": nb * S * world, "stored_bytes": node_new,
+             "dedup_ratio": round(nb * S * world / max(node_new, 1), 6),
+             "dup_fraction": round(1 - node_new / (nb * S * world), 6), "target_dup_fraction": a.dup_ppm / 1e6,
+             "chunks": node_chunks, "mean_chunk_bytes": round(nb * S * world / max(node_chunks, 1), 1),
+             "index": "one node-global index over %d GPU(s), partitioned by digest prefix" % world}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_sample_blocks > 0:
@@ -180,12 +218,14 @@ def main():
         line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-                "config": {"workload": "config2: %d x %d MiB blocks per GPU, %d%% dup (%d MiB segments), "
-                                       "chunk+SHA-%s+local index+container store, fresh index per step"
-                                       % (nb, a.block_mib, a.dup_ppm // 10000, a.seg_mib,
-                                          "1" if a.hasher == 0 else "224"),
-                           "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks": B,
-                           "parallelism": "dp%d (one DataNode index per GPU)" % world},
+                "config": {"workload": "config%d: %d x %d MiB blocks per GPU, %d%% dup (%d MiB segments), "
+                                       "chunk+SHA-%s+%s index+container store, fresh index per step"
+                                       % (2 if world == 1 else 3, nb, a.block_mib, a.dup_ppm // 10000, a.seg_mib,
+                                          "1" if a.hasher == 0 else "224",
+                                          "local" if world == 1 else "node-global (RCCL all-to-all)"),
+                           "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks_per_gpu": B,
+                           "parallelism": "dp%d: blocks sharded by rank; one index partitioned by digest prefix"
+                                          % world},
                 "roofline": roofline, "cpu_baseline": cpu, "dedup": dedup, "stages": stages}
         print(json.dumps(line), flush=True)
     ctx.dev_free(dev)

@@ -3,7 +3,7 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  MI355X_MICROARCH.md (HBM section): on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it is doubled;
 WRITE_SIZE is exact for 16-B-per-lane stores.  Usage:
-    python scripts/traffic.py gpurun_out/pmc_TAG profiles/TAG_traffic.json
+    python scripts/traffic.py gpurun_out/pmc_TAG profiles/TAG_traffic.json ['{"blocks": 512, ...}']
 """
 import collections
 import csv
@@ -26,5 +26,8 @@ for k, d in out.items():
     w = d.get("write_size_kib_raw", 0.0) * 1024
     d["hbm_bytes_per_launch"] = int(f + w)
     d["note"] = "2*FETCH_SIZE + WRITE_SIZE (KiB->B), mean per dispatch"
+# the workload the passes ran (bench.py attaches these figures only to the same workload)
+out["_config"] = json.loads(sys.argv[3]) if len(sys.argv) > 3 else {
+    "blocks": 512, "block_mib": 128, "batch": 64, "n_gpus": 1, "hasher": 0}
 json.dump(out, open(sys.argv[2], "w"), indent=1, sort_keys=True)
-print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in out.items()}, indent=1))
+print(json.dumps({k: v["hbm_bytes_per_launch"] for k, v in out.items() if k != "_config"}, indent=1))
