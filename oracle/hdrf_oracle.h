@@ -56,8 +56,19 @@ int hdrf_oracle_allocator(const hdrf_oracle *o, uint8_t out24[24]);
 /* GET longToBytes(blockId,4) -> recipe bytes; returns length, 0 if absent, -needed if cap small. */
 int64_t hdrf_oracle_recipe(const hdrf_oracle *o, int64_t block_id, uint8_t *out, int64_t cap);
 /* Container file chunkDir+id: returns length (-1 absent, -(needed+2) if cap too small).
- * *closed = 1 once the container was rewritten on overflow. Raw (uncompressed) bytes. */
+ * *closed = 1 once the container was rewritten on overflow.  Raw bytes, except a closed
+ * container under compressor 2, which is the Lz4Codec file (hdrf_oracle_hadoop_lz4_frame). */
 int64_t hdrf_oracle_container(const hdrf_oracle *o, uint32_t id, uint8_t *out, int64_t cap, int *closed);
+
+/* Compression stage (compressor == 2, DN/DataDeduplicator.java:770-779): lz4 r123 LZ4_compress
+ * and Hadoop BlockCompressorStream framing (Lz4Codec, 256 KiB buffer).  Third-party, not in the
+ * reference tree: compressed-byte parity vs Hadoop UNPINNED; see hdrf_oracle.c. */
+int64_t hdrf_oracle_lz4_bound(int64_t n);
+int64_t hdrf_oracle_lz4_compress(const uint8_t *src, int64_t n, uint8_t *dst);
+int64_t hdrf_oracle_lz4_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+int64_t hdrf_oracle_hadoop_lz4_bound(int64_t n);
+int64_t hdrf_oracle_hadoop_lz4_frame(const uint8_t *src, int64_t n, uint8_t *dst);
+int64_t hdrf_oracle_hadoop_lz4_unframe(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
 
 /* Synthetic corpus (shared spec with hdrf_amd corpus generator). */
 uint64_t hdrf_oracle_mix64(uint64_t z);

@@ -59,6 +59,15 @@ def lib():
         L.hdrf_oracle_corpus_fill.argtypes = [ctypes.c_uint64, _u32p, ctypes.c_int64, ctypes.c_int64,
                                               ctypes.c_int64, _u8p]
         L.hdrf_oracle_java_random_bytes.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _u8p]
+        for name in ("hdrf_oracle_lz4_bound", "hdrf_oracle_hadoop_lz4_bound"):
+            getattr(L, name).argtypes = [ctypes.c_int64]
+            getattr(L, name).restype = ctypes.c_int64
+        for name in ("hdrf_oracle_lz4_compress", "hdrf_oracle_hadoop_lz4_frame"):
+            getattr(L, name).argtypes = [_u8p, ctypes.c_int64, _u8p]
+            getattr(L, name).restype = ctypes.c_int64
+        for name in ("hdrf_oracle_lz4_decompress", "hdrf_oracle_hadoop_lz4_unframe"):
+            getattr(L, name).argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
+            getattr(L, name).restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -122,6 +131,38 @@ def java_random_bytes(seed, buffer_len, total):
     out = np.empty(max(total, 1), np.uint8)
     lib().hdrf_oracle_java_random_bytes(seed, buffer_len, total, _p(out))
     return out[:total]
+
+
+def lz4_block(data):
+    """lz4 r123 LZ4_compress (hadoop-common 3.1.0 native Lz4Compressor) -> block bytes."""
+    a = _as_u8(data)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    out = np.zeros(lib().hdrf_oracle_lz4_bound(a.size), np.uint8)
+    n = lib().hdrf_oracle_lz4_compress(_p(buf), a.size, _p(out))
+    return out[:n].tobytes()
+
+
+def lz4_block_decode(data, size):
+    a = _as_u8(data)
+    out = np.zeros(max(size, 1), np.uint8)
+    n = lib().hdrf_oracle_lz4_decompress(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), size)
+    return None if n < 0 else out[:n].tobytes()
+
+
+def hadoop_lz4(data):
+    """Lz4Codec BlockCompressorStream: write(data); close() -> file bytes (DN/DataDeduplicator.java:770-779)."""
+    a = _as_u8(data)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    out = np.zeros(lib().hdrf_oracle_hadoop_lz4_bound(a.size), np.uint8)
+    n = lib().hdrf_oracle_hadoop_lz4_frame(_p(buf), a.size, _p(out))
+    return out[:n].tobytes()
+
+
+def hadoop_lz4_decode(data, cap):
+    a = _as_u8(data)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = lib().hdrf_oracle_hadoop_lz4_unframe(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), cap)
+    return None if n < 0 else out[:n].tobytes()
 
 
 class Oracle:

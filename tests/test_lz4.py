@@ -1,0 +1,113 @@
+"""Compression stage oracle (compressor == 2): lz4 r123 LZ4_compress + Hadoop Lz4Codec
+BlockCompressorStream framing (DN/DataDeduplicator.java:770-779).  Hadoop 3.1.0's bundled lz4
+is not in this image, so compressed-byte parity vs Hadoop is UNPINNED; these tests pin the
+restatement by (1) exact round trips through liblz4 1.9.3's independent LZ4_decompress_safe,
+(2) the framing's structure, (3) the LZ4 format invariants (last 5 bytes literals, offsets
+<= 65535, no match starts in the last 12 bytes)."""
+import ctypes
+import ctypes.util
+
+import numpy as np
+import pytest
+
+from helpers import make_block
+from oracle.oracle import hadoop_lz4, hadoop_lz4_decode, lz4_block, lz4_block_decode
+
+KINDS = ["random", "zeros", "ff", "text", "lowent", "periodic", "sparse", "binary"]
+SIZES = [0, 1, 5, 12, 13, 14, 100, 4096, 65535, 65546, 65547, 65548, 200_000, 261_100]
+
+
+def _liblz4():
+    for name in ("liblz4.so.1", ctypes.util.find_library("lz4")):
+        if not name:
+            continue
+        try:
+            L = ctypes.CDLL(name)
+            L.LZ4_decompress_safe.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+            L.LZ4_decompress_safe.restype = ctypes.c_int
+            return L
+        except OSError:
+            continue
+    return None
+
+
+def _parse_sequences(blk):
+    """Walk an LZ4 block: yields (literal_len, offset or None, match_len)."""
+    i, out = 0, []
+    while i < len(blk):
+        tok = blk[i]; i += 1
+        lit = tok >> 4
+        if lit == 15:
+            while True:
+                b = blk[i]; i += 1; lit += b
+                if b != 255:
+                    break
+        i += lit
+        if i == len(blk):
+            out.append((lit, None, 0))
+            break
+        off = blk[i] | (blk[i + 1] << 8); i += 2
+        ml = tok & 15
+        if ml == 15:
+            while True:
+                b = blk[i]; i += 1; ml += b
+                if b != 255:
+                    break
+        out.append((lit, off, ml + 4))
+    return out
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("n", SIZES)
+def test_lz4_block_round_trip_liblz4(kind, n):
+    data = make_block(kind, n + 11, n).tobytes()
+    blk = lz4_block(data)
+    assert len(blk) <= n + n // 255 + 16
+    assert lz4_block_decode(blk, n) == data
+    L = _liblz4()
+    if L is None:
+        pytest.skip("liblz4 not present")
+    out = ctypes.create_string_buffer(max(n, 1))
+    got = L.LZ4_decompress_safe(blk, out, len(blk), n)
+    assert got == n and out.raw[:n] == data
+
+
+@pytest.mark.parametrize("kind", ["random", "text", "zeros", "binary", "lowent"])
+def test_lz4_format_invariants(kind):
+    n = 150_000
+    data = make_block(kind, 5, n).tobytes()
+    seqs = _parse_sequences(lz4_block(data))
+    pos = 0
+    for lit, off, ml in seqs:
+        pos += lit
+        if off is None:
+            break
+        assert 1 <= off <= 65535
+        assert pos <= n - 12, "a match starts inside the last MFLIMIT bytes"
+        pos += ml
+        assert pos <= n - 5, "a match covers the last LASTLITERALS bytes"
+    assert pos == n
+    if kind in ("zeros", "lowent", "binary"):
+        assert len(seqs) > 1          # compressible data produces matches
+
+
+def test_hadoop_framing_structure():
+    for n in (0, 1, 1000, 261_100, 261_101, 522_200, 600_000, 3 * 1024 * 1024):
+        data = make_block("text", n, n).tobytes()
+        f = hadoop_lz4(data)
+        assert int.from_bytes(f[:4], "big") == n
+        if n == 0:
+            assert f == b"\0\0\0\0"
+            continue
+        i, segs = 4, []
+        while i < len(f):
+            c = int.from_bytes(f[i:i + 4], "big")
+            if c == 0:
+                assert i + 4 == len(f) and n > 261_100       # close() trailer after segmented writes
+                break
+            segs.append(f[i + 4:i + 4 + c]); i += 4 + c
+        assert len(segs) == (n + 261_099) // 261_100
+        assert b"".join(lz4_block_decode(s, 261_100) for s in segs) == data
+        assert hadoop_lz4_decode(f, n) == data
+        if n <= 261_100:
+            assert i == len(f)                                 # no trailer for a single segment
