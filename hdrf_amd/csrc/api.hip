@@ -26,6 +26,7 @@ struct ContainerInfo {
     uint32_t slot;
     uint32_t len;
     int closed;
+    uint32_t clen;           // compressor 2, closed: Lz4Codec file length (compressed arena slot)
 };
 
 }  // namespace
@@ -53,6 +54,9 @@ struct hdrf_ctx {
     uint32_t *d_coll = nullptr, *d_ncoll = nullptr;
     IndexEntry *d_tab = nullptr;
     uint8_t *d_arena = nullptr;
+    uint8_t *d_carena = nullptr;                 // compressor 2: Lz4Codec files of closed containers
+    uint64_t cslot = 0;
+    uint32_t *d_segclen = nullptr, *d_filelen = nullptr;
     AllocState *d_alloc = nullptr;
     uint32_t *d_pcid = nullptr, *d_ppos = nullptr, *d_queue = nullptr;
     int *d_err = nullptr;
@@ -152,7 +156,8 @@ static void free_all(hdrf_ctx *ctx)
                     ctx->d_dig, ctx->d_mid, ctx->d_slot, ctx->d_pre, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
                     ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed, ctx->d_coll, ctx->d_ncoll, ctx->d_tab,
                     ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_queue, ctx->d_err, ctx->d_stage,
-                    ctx->d_scratch, ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags};
+                    ctx->d_scratch, ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags,
+                    ctx->d_carena, ctx->d_segclen, ctx->d_filelen};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (auto &e : ctx->ev)
@@ -196,7 +201,10 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         c.debug_tag_bits < 0 || c.debug_tag_bits > 64 || (c.debug_tag_bits && c.hasher != 0) ||
         c.n_ranks < 1 || c.n_ranks > 64 || c.rank < 0 || c.rank >= c.n_ranks)
         return HDRF_E_INVAL;
-    if (c.compressor != 1) return HDRF_E_UNSUPPORTED;
+    // 1 = dedup, 2 = dedup + Lz4Codec containers (single-node contexts; the node-global mode
+    // assembles containers from several GPUs and compresses them in a later step: unsupported yet)
+    if (c.compressor != 1 && c.compressor != 2) return HDRF_E_UNSUPPORTED;
+    if (c.compressor == 2 && c.n_ranks > 1) return HDRF_E_UNSUPPORTED;
     hdrf_ctx *ctx = new (std::nothrow) hdrf_ctx();
     if (!ctx) return HDRF_E_NOMEM;
     ctx->cfg = c;
@@ -237,6 +245,18 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         free_all(ctx);
         delete ctx;
         return rc;
+    }
+    if (c.compressor == 2) {
+        ctx->cslot = lz4_slot_bytes(c.container_max);
+        const int nseg = (int)((c.container_max + 261099) / 261100);
+        if ((rc = dalloc(ctx, &ctx->d_carena, (size_t)c.arena_slots * ctx->cslot + 256)) ||
+            (rc = dalloc(ctx, &ctx->d_segclen, (size_t)ctx->closed_cap * nseg)) ||
+            (rc = dalloc(ctx, &ctx->d_filelen, (size_t)ctx->closed_cap))) {
+            fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
+            free_all(ctx);
+            delete ctx;
+            return rc;
+        }
     }
     ctx->G = c.n_ranks;
     ctx->rank = c.rank;
@@ -289,12 +309,12 @@ extern "C" int hdrf_reset(hdrf_ctx *ctx)
 }
 
 // container id -> slot bookkeeping after a batch
-static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t len, int closed)
+static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t len, int closed, uint32_t clen = 0)
 {
     auto so = ctx->slot_owner.find(slot);
     if (so != ctx->slot_owner.end() && so->second != id) ctx->containers.erase(so->second);
     ctx->slot_owner[slot] = id;
-    ctx->containers[id] = ContainerInfo{slot, len, closed};
+    ctx->containers[id] = ContainerInfo{slot, len, closed, clen};
 }
 
 // Validate a batch and upload its block descriptors; returns the largest segment count.
@@ -373,8 +393,23 @@ static int finish_batch(hdrf_ctx *ctx, int32_t nblocks, const uint64_t *len, con
     if ((int)nclosed > ctx->closed_cap) return set_err(ctx, HDRF_E_CAPACITY, "closed-container list overflow");
     if (nclosed) {
         std::vector<ClosedRec> cl(nclosed);
+        std::vector<uint32_t> flen(nclosed, 0);
         HIPCK(hipMemcpy(cl.data(), ctx->d_closed, sizeof(ClosedRec) * nclosed, hipMemcpyDeviceToHost));
-        for (auto &r : cl) note_container(ctx, r.id, r.slot, r.len, 1);
+        if (c.compressor == 2) {
+            // compression stage: each closed container is rewritten as an Lz4Codec file (:770-779)
+            if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[0], st));
+            HIPCK(launch_lz4(ctx->d_closed, (int)nclosed, c.container_max, ctx->d_arena, ctx->d_carena, ctx->cslot,
+                             ctx->d_segclen, ctx->d_filelen, st));
+            if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[1], st));
+            HIPCK(hipMemcpyAsync(flen.data(), ctx->d_filelen, sizeof(uint32_t) * nclosed, hipMemcpyDeviceToHost, st));
+            HIPCK(hipStreamSynchronize(st));
+            if (ctx->timing) {
+                float ms = 0;
+                HIPCK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+                ctx->stage_ms[10] += ms;
+            }
+        }
+        for (uint32_t i = 0; i < nclosed; i++) note_container(ctx, cl[i].id, cl[i].slot, cl[i].len, 1, flen[i]);
     }
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) note_container(ctx, ctx->h_alloc.id[t], ctx->h_alloc.slot[t], ctx->h_alloc.cur[t], 0);
@@ -825,11 +860,14 @@ extern "C" int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out,
     auto it = ctx->containers.find(id);
     if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_NOTFOUND, "container not resident");
     if (closed) *closed = it->second.closed;
-    const int64_t n = it->second.len;
+    const bool lz = ctx->cfg.compressor == 2 && it->second.closed;     // the file is the Lz4Codec stream
+    const int64_t n = lz ? it->second.clen : it->second.len;
     if (!out) return n;
     if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "container capacity");
     HIPCK(hipStreamSynchronize(ctx->st));
-    if (n) HIPCK(hipMemcpy(out, ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max, n, hipMemcpyDeviceToHost));
+    const uint8_t *src = lz ? ctx->d_carena + (size_t)it->second.slot * ctx->cslot
+                            : ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max;
+    if (n) HIPCK(hipMemcpy(out, src, n, hipMemcpyDeviceToHost));
     return n;
 }
 

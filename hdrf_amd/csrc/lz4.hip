@@ -1,0 +1,304 @@
+// lz4.hip — compression stage (compressor == 2) on gfx950: closed containers -> Lz4Codec files.
+//
+// Reference: DataDeduplicator.java:748-786 — when a container overflows it is rewritten whole as
+// codec.createOutputStream(file).write(prevData || buf); close() with Hadoop's Lz4Codec, i.e.
+// BlockCompressorStream framing (MAX_INPUT_SIZE 261,100) around lz4 r123 LZ4_compress blocks
+// (hadoop-common 3.1.0 native Lz4Compressor).  tests/ check the output byte for byte against the
+// CPU restatement in oracle/; parity vs Hadoop itself is unpinned.
+//
+// Every 261,100-B segment is an independent LZ4 block with a fresh hash table, so one wave owns
+// one segment (table in LDS).  The greedy parse is sequential, but its expensive parts are made
+// wave-parallel:
+//   * match search: the positions the search loop visits do not depend on the data until a match
+//     is found (ip += attempts++ >> 6), so 64 attempts are evaluated at once (lane i = attempt i):
+//     hashes and the 4-byte candidate compare are one gather each; the table reads/writes are
+//     replayed in attempt order (single-lane LDS ops, program order = reference order) and the
+//     writes of attempts after the first match are undone in reverse order;
+//   * match extension, catch-up and literal copies are 64-lane compares / 16-B-per-lane copies.
+//   lz4_pack then frames the segments ([BE32 len] ([BE32 clen] block)* [BE32 0]) in place.
+#include "launchers.hpp"
+
+namespace hdrf {
+
+constexpr int kLzMaxIn = 261100;                 // BlockCompressorStream MAX_INPUT_SIZE (256 KiB buffer)
+constexpr int kLzSegBound = kLzMaxIn + kLzMaxIn / 255 + 16;
+constexpr int kLzSegStride = kLzSegBound + 4;    // per-segment stride of the unpacked layout
+constexpr int kMfLimit = 12, kLastLit = 5, kMaxDist = 65535, k64KLimit = 65536 + kMfLimit - 1;
+
+__device__ __forceinline__ uint32_t rd32u(const uint8_t *p)
+{
+    const uintptr_t a = (uintptr_t)p;
+    const HDRF_GLOBAL uint32_t *q = gptr<uint32_t>((const void *)(a & ~(uintptr_t)3));
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+__device__ __forceinline__ uint32_t rd8(const uint8_t *p) { return *(const HDRF_GLOBAL uint8_t *)p; }
+__device__ __forceinline__ void wr8(uint8_t *p, uint32_t v) { *(HDRF_GLOBAL uint8_t *)p = (uint8_t)v; }
+
+// wave-cooperative copy of n bytes (arbitrary alignments; 16-B aligned destination words)
+__device__ void wave_copy(uint8_t *dst, const uint8_t *src, int n)
+{
+    const int l = lane_id();
+    int head = (int)((16 - ((uintptr_t)dst & 15)) & 15);
+    if (head > n) head = n;
+    if (l < head) wr8(dst + l, rd8(src + l));
+    uint8_t *d = dst + head;
+    const uint8_t *sp = src + head;
+    const int n16 = (n - head) >> 4;
+    const int sh = (int)((uintptr_t)sp & 15);
+    const uint8_t *sa = sp - sh;
+    int i = l;
+    for (; i + 192 < n16; i += 256) {                 // four 16-B words per lane in flight
+        const uint4 v0 = load16_shift(sa + 16 * (size_t)i, sh);
+        const uint4 v1 = load16_shift(sa + 16 * (size_t)(i + 64), sh);
+        const uint4 v2 = load16_shift(sa + 16 * (size_t)(i + 128), sh);
+        const uint4 v3 = load16_shift(sa + 16 * (size_t)(i + 192), sh);
+        st16(d + 16 * (size_t)i, v0);
+        st16(d + 16 * (size_t)(i + 64), v1);
+        st16(d + 16 * (size_t)(i + 128), v2);
+        st16(d + 16 * (size_t)(i + 192), v3);
+    }
+    for (; i < n16; i += 64) st16(d + 16 * (size_t)i, load16_shift(sa + 16 * (size_t)i, sh));
+    const int tb = head + 16 * n16;
+    for (int k = tb + l; k < n; k += 64) wr8(dst + k, rd8(src + k));
+}
+
+// length >= 15 continuation bytes (255 ... rest); returns the new output offset
+__device__ __forceinline__ int put_len(uint8_t *out, int op, int len)
+{
+    const int n255 = len / 255;
+    const int l = lane_id();
+    for (int k = l; k < n255; k += 64) wr8(out + op + k, 255);
+    if (l == 0) wr8(out + op + n255, (uint32_t)(len - 255 * n255));
+    return op + n255 + 1;
+}
+
+// One LZ4 block (lz4 r123 LZ4_compress, noDict): returns the compressed size.  Uniform control
+// flow; `tab` is this wave's LDS hash table (u32 entries, byU32, or u16 entries, byU16).
+__device__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint32_t *tab)
+{
+    const int l = lane_id();
+    const bool u16 = n < k64KLimit;
+    const int hshift = u16 ? 32 - 13 : 32 - 12;
+    unsigned short *tab16 = (unsigned short *)tab;
+    for (int i = l; i < 4096; i += 64) tab[i] = 0;
+    __builtin_amdgcn_s_waitcnt(0);
+    asm volatile("" ::: "memory");
+    auto tget = [&](uint32_t h) -> int { return u16 ? (int)tab16[h] : (int)tab[h]; };
+    auto tput = [&](uint32_t h, int p) { if (u16) tab16[h] = (unsigned short)p; else tab[h] = (uint32_t)p; };
+    auto hash = [&](uint32_t v) -> uint32_t { return (v * 2654435761u) >> hshift; };
+
+    const int mflimit = n - kMfLimit, matchlimit = n - kLastLit;
+    int op = 0, anchor = 0, ip = 0;
+    if (n >= kMfLimit + 1) {
+        if (l == 0) tput(hash(rd32u(src)), 0);        // first byte
+        ip = 1;
+        int fip = ip, attempts = (1 << 6) + 3;
+        for (;;) {
+            // ---- match search: 64 attempts at once --------------------------------------
+            const int a0 = attempts;
+            const int step = (a0 + l) >> 6;
+            const int ipl = fip + (int)wave_incl_scan((uint32_t)step) - step;   // this lane's attempt
+            const bool valid = ipl + step <= mflimit;
+            const uint32_t v = valid ? rd32u(src + ipl) : 0u;
+            const uint32_t h = hash(v);
+            const unsigned long long vmask = ballot64(valid);
+            const int nv = vmask == ~0ull ? 64 : __builtin_ctzll(~vmask);   // valid lanes are a prefix
+            int ref = 0;
+            asm volatile("" ::: "memory");
+            for (int i = 0; i < nv; i++) {                // table replay in attempt order
+                if (l == i) { ref = tget(h); tput(h, ipl); }
+                asm volatile("" ::: "memory");            // keep the LDS ops in program order
+            }
+            asm volatile("" ::: "memory");
+            bool ok = false;
+            if (valid && ref + kMaxDist >= ipl) ok = rd32u(src + ref) == v;
+            const unsigned long long okm = ballot64(ok);
+            if (okm) {
+                const int istar = __builtin_ctzll(okm);
+                for (int i = nv - 1; i > istar; i--) {    // undo the attempts after the match
+                    if (l == i) tput(h, ref);
+                    asm volatile("" ::: "memory");
+                }
+                asm volatile("" ::: "memory");
+                ip = (int)rdlane((uint32_t)ipl, istar);
+                int mref = (int)rdlane((uint32_t)ref, istar);
+                // ---- catch up ----------------------------------------------------------
+                for (;;) {
+                    const int k = l + 1;
+                    const bool c = ip - k >= anchor && mref - k >= 0 && rd8(src + ip - k) == rd8(src + mref - k);
+                    const unsigned long long bad = ballot64(!c);
+                    const int back = bad ? __builtin_ctzll(bad) : 64;
+                    ip -= back; mref -= back;
+                    if (back < 64) break;
+                }
+                // ---- literals ----------------------------------------------------------
+                int tpos = op++;
+                const int lit = ip - anchor;
+                uint32_t tok;
+                if (lit >= 15) { tok = 15u << 4; op = put_len(out, op, lit - 15); }
+                else tok = (uint32_t)lit << 4;
+                wave_copy(out + op, src + anchor, lit);
+                op += lit;
+                for (;;) {                                 // _next_match
+                    if (l == 0) { wr8(out + op, (uint32_t)(ip - mref)); wr8(out + op + 1, (uint32_t)(ip - mref) >> 8); }
+                    op += 2;
+                    ip += 4; mref += 4;
+                    anchor = ip;
+                    for (;;) {                             // match extension
+                        const int p = ip + 4 * l;
+                        uint32_t x = 0;
+                        bool stop = p + 4 > matchlimit;
+                        if (!stop) x = rd32u(src + p) ^ rd32u(src + mref + 4 * l);
+                        else if (p < matchlimit) {
+                            x = rd32u(src + p) ^ rd32u(src + mref + 4 * l);
+                            x |= 0xffffffffu << (8 * (matchlimit - p));   // bytes past matchlimit differ
+                        } else {
+                            x = 0xffffffffu;
+                        }
+                        const unsigned long long mm = ballot64(x != 0u || stop);
+                        if (!mm) { ip += 256; mref += 256; continue; }
+                        const int L = __builtin_ctzll(mm);
+                        const uint32_t xl = rdlane(x, L);
+                        const int eq = xl ? (__builtin_ctz(xl) >> 3) : 4;
+                        ip += 4 * L + eq;
+                        mref += 4 * L + eq;
+                        break;
+                    }
+                    int ml = ip - anchor;
+                    if (ml >= 15) {
+                        tok += 15;
+                        ml -= 15;
+                        const int n510 = ml > 509 ? (ml - 510) / 510 + 1 : 0;   // pairs of 255
+                        for (int k = l; k < 2 * n510; k += 64) wr8(out + op + k, 255);
+                        op += 2 * n510;
+                        ml -= 510 * n510;
+                        if (ml >= 255) { if (l == 0) wr8(out + op, 255); op++; ml -= 255; }
+                        if (l == 0) wr8(out + op, (uint32_t)ml);
+                        op++;
+                    } else {
+                        tok += (uint32_t)ml;
+                    }
+                    if (l == 0) wr8(out + tpos, tok);
+                    if (ip > mflimit) { anchor = ip; goto last_literals; }
+                    // fill table; test next position
+                    const uint32_t v2 = rd32u(src + ip - 2), v0 = rd32u(src + ip);
+                    int r = 0;
+                    asm volatile("" ::: "memory");
+                    if (l == 0) { tput(hash(v2), ip - 2); r = tget(hash(v0)); tput(hash(v0), ip); }
+                    asm volatile("" ::: "memory");
+                    r = (int)rdlane((uint32_t)r, 0);
+                    if (r + kMaxDist >= ip && rd32u(src + r) == v0) {
+                        mref = r;
+                        tpos = op++;
+                        tok = 0;
+                        continue;
+                    }
+                    break;
+                }
+                anchor = ip++;
+                fip = ip;
+                attempts = (1 << 6) + 3;
+                continue;
+            }
+            if (nv < 64) break;                            // the next attempt passes mflimit
+            fip = (int)rdlane((uint32_t)(ipl + step), 63);
+            attempts = a0 + 64;
+        }
+    }
+last_literals:
+    {
+        int run = n - anchor;
+        const int tpos = op++;
+        if (run >= 15) {
+            if (l == 0) wr8(out + tpos, 15u << 4);
+            op = put_len(out, op, run - 15);
+        } else if (l == 0) {
+            wr8(out + tpos, (uint32_t)run << 4);
+        }
+        wave_copy(out + op, src + anchor, run);
+        op += run;
+    }
+    return op;
+}
+
+// grid (nseg_max, nclosed) x 64 threads: segment s of closed container c
+__global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed, const uint8_t *__restrict__ arena,
+                                                     uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
+                                                     uint32_t *__restrict__ seg_clen, int nseg_max)
+{
+    __shared__ uint32_t tab[4096];
+    const int c = blockIdx.y, s = blockIdx.x;
+    const ClosedRec r = closed[c];
+    const int64_t off = (int64_t)s * kLzMaxIn;
+    if (off >= (int64_t)r.len) return;
+    const int n = (int)min((int64_t)kLzMaxIn, (int64_t)r.len - off);
+    const uint8_t *src = arena + (size_t)r.slot * cmax + off;
+    uint8_t *out = carena + (size_t)r.slot * cslot + 8 + (size_t)s * kLzSegStride;
+    const int cl = lz4_block(src, n, out, tab);
+    if (lane_id() == 0) seg_clen[(size_t)c * nseg_max + s] = (uint32_t)cl;
+}
+
+__device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v)
+{
+    wr8(p, v >> 24); wr8(p + 1, v >> 16); wr8(p + 2, v >> 8); wr8(p + 3, v);
+}
+
+// grid nclosed x 256 threads: frame the segments in place, [BE32 len] ([BE32 clen] block)* [BE32 0]
+__global__ void __launch_bounds__(256) lz4_pack_kernel(const ClosedRec *__restrict__ closed, uint8_t *__restrict__ carena,
+                                                       uint64_t cslot, const uint32_t *__restrict__ seg_clen, int nseg_max,
+                                                       uint32_t *__restrict__ file_len)
+{
+    const int c = blockIdx.x, t = threadIdx.x;
+    const ClosedRec r = closed[c];
+    uint8_t *base = carena + (size_t)r.slot * cslot;
+    const int nseg = r.len ? (int)((r.len + kLzMaxIn - 1) / kLzMaxIn) : 0;
+    if (t == 0) put_be32(base, r.len);
+    uint32_t pos = 4;
+    for (int s = 0; s < nseg; s++) {
+        const uint32_t cl = seg_clen[(size_t)c * nseg_max + s];
+        const uint32_t from = 8 + (uint32_t)s * kLzSegStride;
+        const uint32_t to = pos + 4;
+        if (to != from) {                                  // to < from: forward tiles, load then store
+            for (uint32_t o = 0; o < cl; o += 256 * 16) {
+                uint8_t v[16];
+                const uint32_t q = o + 16 * t;
+#pragma unroll
+                for (int k = 0; k < 16; k++) v[k] = (q + k < cl) ? base[from + q + k] : 0;
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (q + k < cl) base[to + q + k] = v[k];
+                __syncthreads();
+            }
+        }
+        if (t == 0) put_be32(base + pos, cl);
+        __syncthreads();
+        pos = to + cl;
+    }
+    if (r.len > (uint32_t)kLzMaxIn) {                      // segmented write: close() trailer
+        if (t == 0) put_be32(base + pos, 0);
+        pos += 4;
+    }
+    if (r.len == 0) pos = 4;
+    if (t == 0) file_len[c] = pos;
+}
+
+uint64_t lz4_slot_bytes(uint32_t cmax)
+{
+    const uint64_t nseg = (cmax + kLzMaxIn - 1) / kLzMaxIn + 1;
+    return 16 + nseg * (uint64_t)kLzSegStride;
+}
+
+hipError_t launch_lz4(const ClosedRec *closed, int nclosed, uint32_t cmax, const uint8_t *arena, uint8_t *carena,
+                      uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len, hipStream_t st)
+{
+    if (nclosed <= 0) return hipSuccess;
+    const int nseg_max = (int)((cmax + kLzMaxIn - 1) / kLzMaxIn);
+    hipLaunchKernelGGL(lz4_seg_kernel, dim3(nseg_max, nclosed), dim3(64), 0, st, closed, arena, (uint64_t)cmax, carena,
+                       cslot, seg_clen, nseg_max);
+    hipLaunchKernelGGL(lz4_pack_kernel, dim3(nclosed), dim3(256), 0, st, closed, carena, cslot, seg_clen, nseg_max,
+                       file_len);
+    return hipGetLastError();
+}
+
+}  // namespace hdrf

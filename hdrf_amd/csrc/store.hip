@@ -179,30 +179,6 @@ __global__ void __launch_bounds__(256) flush_kernel(StoreParams P, const BlockSt
     }
 }
 
-// 16 output bytes from an arbitrarily aligned source: two aligned 16-B loads + a funnel shift by
-// sh = src & 15 (uniform per run, since destination words are 16-B aligned within a run).
-__device__ __forceinline__ uint4 load16_shift(const uint8_t *src_aligned, int sh)
-{
-    const uint4 x = ld16(src_aligned);
-    if (sh == 0) return x;
-    const uint4 y = ld16(src_aligned + 16);
-    const uint32_t r = (uint32_t)(sh & 3);
-#define AB(hi, lo) __builtin_amdgcn_alignbyte((hi), (lo), r)
-    switch (sh >> 2) {                                   // uniform per run
-    case 0: return make_uint4(AB(x.y, x.x), AB(x.z, x.y), AB(x.w, x.z), AB(y.x, x.w));
-    case 1: return make_uint4(AB(x.z, x.y), AB(x.w, x.z), AB(y.x, x.w), AB(y.y, y.x));
-    case 2: return make_uint4(AB(x.w, x.z), AB(y.x, x.w), AB(y.y, y.x), AB(y.z, y.y));
-    default: return make_uint4(AB(y.x, x.w), AB(y.y, y.x), AB(y.z, y.y), AB(y.w, y.z));
-    }
-#undef AB
-}
-
-__device__ __forceinline__ void st16(void *p, uint4 v)
-{
-    u32x4v w = {v.x, v.y, v.z, v.w};
-    *(HDRF_GLOBAL u32x4v *)p = w;
-}
-
 // workgroup-cooperative copy of one contiguous run (16-B aligned destination stores)
 __device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32_t len)
 {

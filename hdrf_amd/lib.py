@@ -36,7 +36,7 @@ ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
 STAGES = ["walk(spec_walk_kernel)", "stitch(spec_sync/plan/copy/fallback)", "sha_full(sha_full_kernel)",
           "sha_tail(sha_tail_kernel)", "index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
           "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
-          "place(place_kernel)", "spare"]
+          "place(place_kernel)", "compress(lz4_seg/lz4_pack)"]
 
 
 class HdrfError(RuntimeError):

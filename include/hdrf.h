@@ -34,7 +34,7 @@ typedef struct hdrf_ctx hdrf_ctx;
 /* Knobs of the reference, all compile-time statics there. */
 typedef struct {
     int32_t hasher;          /* 0 SHA-1, 1 SHA-224          DataNode.hasher, DN/DataNode.java:446 */
-    int32_t compressor;      /* 1 dedup only (2 = +LZ4: not yet)   DataNode.compressor :438 */
+    int32_t compressor;      /* 1 dedup, 2 dedup + Lz4Codec closed containers   DataNode.compressor :438 */
     int32_t window;          /* 700                         DataDeduplicator.chunking :266 */
     int32_t max_chunk;       /* 1000000                     DataDeduplicator.chunking :272 */
     int32_t n_thread;        /* 3                           DataDeduplicator.nThread :93 */
@@ -106,7 +106,8 @@ int hdrf_allocator(hdrf_ctx *ctx, uint8_t out24[24]);
 int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap);
 /* FsDatasetImpl.getLength for 0-byte replicas (DN/fsdataset/impl/FsDatasetImpl.java:736-763). */
 int64_t hdrf_block_length(hdrf_ctx *ctx, uint64_t block_id);
-/* Container file chunkDir+id (raw bytes).  Returns length; *closed = 1 once it overflowed.
+/* Container file chunkDir+id.  Returns length; *closed = 1 once it overflowed.  Raw bytes, except
+ * closed containers under compressor 2: the Lz4Codec file the storer rewrote (:770-779).
  * HDRF_E_NOTFOUND if it never existed or its arena slot was recycled. */
 int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t cap, int32_t *closed);
 
@@ -125,7 +126,7 @@ int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, in
 /* Per-stage device time (ms) accumulated since the last reset, measured with HIP events on
  * the context's stream (cfg.timing = 1): [0] spec_walk_kernel, [1] stitch (sync/plan/copy/
  * fallback), [2] sha_full_kernel, [3] sha_tail_kernel, [4] idx_claim_kernel, [5] idx_apply_kernel,
- * [6] idx_slow+decide, [7] new-byte scans, [8] flush_kernel, [9] place_kernel, [10] spare. */
+ * [6] idx_slow+decide, [7] new-byte scans, [8] flush_kernel, [9] place_kernel, [10] lz4 (compressor 2). */
 int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
 /* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis). */
 int hdrf_reset(hdrf_ctx *ctx);

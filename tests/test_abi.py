@@ -36,8 +36,12 @@ def test_default_config_and_bad_config_are_rejected_without_gpu():
     bad = lib.default_config(window=5)
     h = ctypes.c_void_p()
     assert lib.load().hdrf_open(ctypes.byref(bad), ctypes.byref(h)) == -1
-    unsupported = lib.default_config(compressor=2)
+    unsupported = lib.default_config(compressor=3)          # stream codecs: not in this build
     assert lib.load().hdrf_open(ctypes.byref(unsupported), ctypes.byref(h)) == -6
+    node_lz4 = lib.default_config(compressor=2, n_ranks=2, rank=0)
+    assert lib.load().hdrf_open(ctypes.byref(node_lz4), ctypes.byref(h)) == -6
+    bad_rank = lib.default_config(n_ranks=2, rank=2)
+    assert lib.load().hdrf_open(ctypes.byref(bad_rank), ctypes.byref(h)) == -1
 
 
 def test_product_package_does_not_import_oracle():

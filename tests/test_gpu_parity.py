@@ -14,11 +14,11 @@ pytestmark = pytest.mark.gpu
 SMALL = dict(max_block_bytes=16 << 20, max_batch_blocks=8, index_log2=20, arena_slots=64)
 
 
-def run_sequence(blocks, hasher=0, container_max=1 << 25, **cfg):
+def run_sequence(blocks, hasher=0, container_max=1 << 25, compressor=1, **cfg):
     kw = dict(SMALL)
     kw.update(cfg)
-    ctx = Context(hasher=hasher, container_max=container_max, **kw)
-    ora = Oracle(hasher=hasher, compressor=1, max_size=container_max)
+    ctx = Context(hasher=hasher, container_max=container_max, compressor=compressor, **kw)
+    ora = Oracle(hasher=hasher, compressor=compressor, max_size=container_max)
     ids = []
     for i, blk in enumerate(blocks):
         bid = 0x1000 + 7 * i
@@ -163,3 +163,25 @@ def test_index_tag_collisions_take_exact_slow_path(bits):
     compare_state(ctx, ora, list(range(40, 48)))
     ctx.dev_free(dev)
     ctx.close()
+
+
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_compression_stage_lz4_containers(hasher):
+    """compressor == 2: every closed container is the Lz4Codec file of its bytes
+    (DN/DataDeduplicator.java:770-779), byte-identical to the oracle's lz4 r123 + Hadoop framing."""
+    rng = np.random.default_rng(5 + hasher)
+    kinds = ["random", "lowent", "text", "binary", "sparse", "random", "lowent", "binary"]
+    blocks = []
+    for i, k in enumerate(kinds):
+        b = make_block(k, 40 + i, 900_000 + int(rng.integers(0, 100_000)))
+        if i >= 4:                                     # cross-block duplicates
+            b = np.concatenate([blocks[i - 4][:300_000], b[:600_000]])
+        blocks.append(b)
+    run_sequence(blocks, hasher=hasher, container_max=1 << 20, compressor=2)
+
+
+def test_compression_stage_large_container():
+    """32 MiB containers (129 LZ4 segments each, close() trailer) on mixed data."""
+    blocks = [np.concatenate([make_block(k, 70 + i, 6 << 20) for k in ("lowent", "random", "binary")])
+              for i in range(3)]
+    run_sequence(blocks, compressor=2, max_block_bytes=32 << 20, arena_slots=16)
