@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--hasher", type=int, default=0)
     ap.add_argument("--cpu-sample-blocks", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", choices=["config2", "config4"], default="config2",
+                    help="config4: mixed-entropy blocks (random/text/binary), dedup + Lz4Codec containers")
     return ap.parse_args()
 
 
@@ -94,8 +96,12 @@ def main():
     # One node, one index: at N > 1 the GPUs are ranks of ONE reduction over the global block
     # sequence (hdrf_amd/node.py): a global corpus of world*nb blocks, every global batch takes B
     # blocks from each rank (rank-major), the index is partitioned by digest prefix.
+    mixed = a.workload == "config4"
+    if mixed and world > 1:
+        raise SystemExit("config4 (compression stage) runs on single-node contexts only")
+    compressor = 2 if mixed else 1
     ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
-                  arena_slots=64, keep_recipes=0, timing=1, n_ranks=world, rank=rank)
+                  arena_slots=64, keep_recipes=0, timing=1, n_ranks=world, rank=rank, compressor=compressor)
     node = None
     if world > 1:
         from hdrf_amd.node import NodeRank, global_block
@@ -109,7 +115,7 @@ def main():
         roots = groots.reshape(-1)
     total = nb * S + 4096
     dev = ctx.dev_alloc(total)
-    ctx.corpus_fill(dev, roots, nb, spb, seg, seed)
+    ctx.corpus_fill(dev, roots, nb, spb, seg, seed, mixed=mixed)
     batches = []
     for b0 in range(0, nb, B):
         k = min(B, nb - b0)
@@ -210,23 +216,36 @@ def main():
              "chunks": node_chunks, "mean_chunk_bytes": round(nb * S * world / max(node_chunks, 1), 1),
              "index": "one node-global index over %d GPU(s), partitioned by digest prefix" % world}
 
+    compression = None
+    if mixed:
+        st = ctx.stats()
+        stored = st["closed_file_bytes"] + st["open_bytes"]
+        compression = {"closed_containers": st["closed_containers"], "closed_raw_bytes": st["closed_raw_bytes"],
+                       "closed_file_bytes": st["closed_file_bytes"], "open_raw_bytes": st["open_bytes"],
+                       "lz4_ratio_closed": round(st["closed_raw_bytes"] / max(st["closed_file_bytes"], 1), 6),
+                       "node_ratio": round(st["logical_bytes"] / max(stored, 1), 6),
+                       "node_ratio_def": "logical / (closed Lz4Codec files + open raw containers)"}
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_sample_blocks > 0:
-        cpu = cpu_baseline(ctx, dev, S, min(a.cpu_sample_blocks, nb), store, a.hasher)
+        cpu = cpu_baseline(ctx, dev, S, min(a.cpu_sample_blocks, nb), store, a.hasher, compressor)
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-                "config": {"workload": "config%d: %d x %d MiB blocks per GPU, %d%% dup (%d MiB segments), "
-                                       "chunk+SHA-%s+%s index+container store, fresh index per step"
-                                       % (2 if world == 1 else 3, nb, a.block_mib, a.dup_ppm // 10000, a.seg_mib,
-                                          "1" if a.hasher == 0 else "224",
-                                          "local" if world == 1 else "node-global (RCCL all-to-all)"),
+                "config": {"workload": "config%d: %d x %d MiB %sblocks per GPU, %d%% dup (%d MiB segments), "
+                                       "chunk+SHA-%s+%s index+container store%s, fresh index per step"
+                                       % (4 if mixed else (2 if world == 1 else 3), nb, a.block_mib,
+                                          "mixed-entropy (random/text/binary) " if mixed else "",
+                                          a.dup_ppm // 10000, a.seg_mib, "1" if a.hasher == 0 else "224",
+                                          "local" if world == 1 else "node-global (RCCL all-to-all)",
+                                          " + Lz4Codec on closed containers" if mixed else ""),
                            "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks_per_gpu": B,
                            "parallelism": "dp%d: blocks sharded by rank; one index partitioned by digest prefix"
                                           % world},
                 "roofline": roofline, "cpu_baseline": cpu, "dedup": dedup, "stages": stages}
+        if compression:
+            line["compression"] = compression
         print(json.dumps(line), flush=True)
     ctx.dev_free(dev)
     ctx.close()
@@ -234,13 +253,13 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(ctx, dev, S, m, gpu_store, hasher):
+def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1):
     """CPU oracle (single thread, C restatement of the reference) on the first m blocks of the
-    same corpus; also checks per-block storeSize == the GPU's (bit-exact dedup ratio)."""
-    import numpy as np
-
+    same corpus; also checks per-block storeSize == the GPU's (bit-exact dedup ratio) and, for the
+    compression stage, that a fresh GPU context reducing the same m blocks writes byte-identical
+    container files (closed Lz4Codec files and open raw containers)."""
     from oracle.oracle import Oracle
-    ora = Oracle(hasher=hasher, compressor=1)
+    ora = Oracle(hasher=hasher, compressor=compressor)
     t = 0.0
     mism = 0
     for b in range(m):
@@ -249,10 +268,35 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher):
         r = ora.reduce(blk, b)
         t += time.perf_counter() - t0
         mism += int(r["store_size"] != gpu_store[b])
-    return {"value": round(m * S / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "first %d of the same blocks (%.1f GiB), oracle/hdrf_oracle.c, 1 thread, %.1f s"
-                      % (m, m * S / 2**30, t),
-            "store_size_mismatches": mism, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    out = {"value": round(m * S / t / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": "first %d of the same blocks (%.1f GiB), oracle/hdrf_oracle.c%s, 1 thread, %.1f s"
+                     % (m, m * S / 2**30, " with lz4 r123 containers" if compressor == 2 else "", t),
+           "store_size_mismatches": mism, "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+    if compressor == 2:
+        out["container_file_mismatches"], out["containers_checked"] = _check_containers(ctx, dev, S, m, ora, hasher)
+    return out
+
+
+def _check_containers(ctx, dev, S, m, ora, hasher):
+    from hdrf_amd.lib import Context
+    v = Context(device=int(ctx.cfg.device), hasher=hasher, compressor=2, max_block_bytes=S, max_batch_blocks=8,
+                index_log2=24, arena_slots=256, keep_recipes=0)
+    for b0 in range(0, m, 8):
+        k = min(8, m - b0)
+        v.reduce_batch([dev + (b0 + i) * S for i in range(k)], [S] * k, [S + 4096] * k, list(range(b0, b0 + k)))
+    alloc = ora.allocator()
+    bad = checked = 0
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, oc = ora.container(cid)
+            if od is None:
+                continue
+            gd, gc = v.container(cid)
+            checked += 1
+            bad += int(gd != od or gc != oc)
+    v.close()
+    return bad, checked
 
 
 def _cpu_model():

@@ -40,14 +40,46 @@ def corpus_roots(seed, dup_ppm, nblocks, segs_per_block):
     return roots
 
 
-def corpus_block_host(seed, roots, block, segs_per_block, seg_bytes):
-    """Host copy of one block (tests / CPU baseline input); same bytes as hdrf_corpus_fill."""
+_WORDS = None
+
+
+def _text_words():
+    """The 512 eight-byte 'text' slots of the mixed-entropy corpus (7 letters + space)."""
+    global _WORDS
+    if _WORDS is None:
+        m = mix64(np.arange(512, dtype=np.uint64) ^ np.uint64(0x7E57))
+        w = np.zeros(512, np.uint64)
+        for j in range(7):
+            letter = (m >> np.uint64(5 * j)) % np.uint64(26) + np.uint64(ord("a"))
+            w |= letter << np.uint64(8 * j)
+        _WORDS = w | (np.uint64(ord(" ")) << np.uint64(56))
+    return _WORDS
+
+
+def segment_kind(root):
+    """Mixed-entropy corpus (config 4): 0 random, 1 text, 2 binary records."""
+    return int(mix64(np.uint64(int(root)) ^ np.uint64(0x5BD1E995)) % np.uint64(3))
+
+
+def corpus_block_host(seed, roots, block, segs_per_block, seg_bytes, mixed=False):
+    """Host copy of one block (tests / CPU baseline input); same bytes as hdrf_corpus_fill(_kind)."""
     out = np.empty(segs_per_block * seg_bytes, dtype=np.uint8)
     nw = seg_bytes // 8
     wi = np.arange(nw, dtype=np.uint64)
     for s in range(segs_per_block):
-        key = mix64(np.uint64(seed) ^ mix64(np.uint64(int(roots[block * segs_per_block + s]) + 1)))
+        root = int(roots[block * segs_per_block + s])
+        key = mix64(np.uint64(seed) ^ mix64(np.uint64(root + 1)))
         with np.errstate(over="ignore"):
             words = mix64(key + wi)
+        if mixed:
+            kind = segment_kind(root)
+            if kind == 1:
+                words = _text_words()[(words & np.uint64(511)).astype(np.int64)]
+            elif kind == 2:
+                a, b = words[0::2], words[1::2]
+                idx = np.arange(nw // 2, dtype=np.uint64)
+                words = words.copy()
+                words[0::2] = idx | ((a % np.uint64(200)) << np.uint64(32))
+                words[1::2] = b % np.uint64(4)
         out[s * seg_bytes:(s + 1) * seg_bytes] = words.view(np.uint8)
     return out

@@ -86,6 +86,7 @@ struct hdrf_ctx {
     int gx_phase = 0;                            // 1 front, 2 owner, 3 decide, 4 flush, 5 place
     int gx_nblocks = 0;
     std::vector<uint64_t> gx_ids, gx_lens;
+    hdrf_stats stats{};                          // cumulative since the last reset
     // timing
     bool timing = false;
     hipEvent_t ev[kStages + 1] = {};
@@ -186,6 +187,7 @@ static int init_state(hdrf_ctx *ctx)
     ctx->lengths.clear();
     ctx->last_nblocks = 0;
     ctx->gx_phase = 0;
+    ctx->stats = hdrf_stats{};
     return 0;
 }
 
@@ -409,11 +411,26 @@ static int finish_batch(hdrf_ctx *ctx, int32_t nblocks, const uint64_t *len, con
                 ctx->stage_ms[10] += ms;
             }
         }
-        for (uint32_t i = 0; i < nclosed; i++) note_container(ctx, cl[i].id, cl[i].slot, cl[i].len, 1, flen[i]);
+        for (uint32_t i = 0; i < nclosed; i++) {
+            note_container(ctx, cl[i].id, cl[i].slot, cl[i].len, 1, flen[i]);
+            ctx->stats.closed_containers++;
+            ctx->stats.closed_raw_bytes += cl[i].len;
+            ctx->stats.closed_file_bytes += c.compressor == 2 ? flen[i] : cl[i].len;
+        }
     }
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) note_container(ctx, ctx->h_alloc.id[t], ctx->h_alloc.slot[t], ctx->h_alloc.cur[t], 0);
     ctx->have_alloc = 1;                              // storeDB always SETs "blockID" (:389)
+    for (int b = 0; b < nblocks; b++) {
+        ctx->stats.blocks++;
+        ctx->stats.logical_bytes += len[b];
+        ctx->stats.new_bytes += ctx->h_store[b];
+        ctx->stats.chunks += ctx->h_bst[b].n_chunks;
+        ctx->stats.recipe_bytes += 4 + (uint64_t)ctx->h_bst[b].n_chunks * ctx->H;
+    }
+    ctx->stats.open_bytes = 0;
+    for (int t = 0; t < c.n_thread; t++)
+        if (ctx->h_alloc.exists[t]) ctx->stats.open_bytes += ctx->h_alloc.cur[t];
     // recipes (SET longToBytes(id,4) -> BE32 size | digests)
     for (int b = 0; b < nblocks; b++) {
         const uint32_t key = (uint32_t)(block_ids ? block_ids[b] : 0);
@@ -913,14 +930,27 @@ extern "C" int hdrf_synchronize(hdrf_ctx *ctx)
 extern "C" int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
                                 int64_t segs_per_block, int64_t seg_bytes, uint64_t seed)
 {
+    return hdrf_corpus_fill_kind(ctx, dev, roots_host, nblocks, segs_per_block, seg_bytes, seed, 0);
+}
+
+extern "C" int hdrf_corpus_fill_kind(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
+                                     int64_t segs_per_block, int64_t seg_bytes, uint64_t seed, int32_t mixed)
+{
     if (!ctx || !dev || !roots_host || seg_bytes % 16 != 0) return HDRF_E_INVAL;
     uint32_t *d_roots = nullptr;
     const size_t n = (size_t)nblocks * segs_per_block;
     HIPCK(hipMalloc((void **)&d_roots, n * 4));
     HIPCK(hipMemcpyAsync(d_roots, roots_host, n * 4, hipMemcpyHostToDevice, ctx->st));
-    HIPCK(launch_corpus(dev, d_roots, nblocks, segs_per_block, seg_bytes, seed, ctx->st));
+    HIPCK(launch_corpus(dev, d_roots, nblocks, segs_per_block, seg_bytes, seed, mixed ? 1 : 0, ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipFree(d_roots));
+    return 0;
+}
+
+extern "C" int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out)
+{
+    if (!ctx || !out) return HDRF_E_INVAL;
+    *out = ctx->stats;
     return 0;
 }
 

@@ -82,6 +82,6 @@ uint64_t lz4_slot_bytes(uint32_t cmax);
 hipError_t launch_lz4(const ClosedRec *closed, int nclosed, uint32_t cmax, const uint8_t *arena, uint8_t *carena,
                       uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len, hipStream_t st);
 hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
-                         uint64_t seed, hipStream_t st);
+                         uint64_t seed, int mixed, hipStream_t st);
 
 }  // namespace hdrf

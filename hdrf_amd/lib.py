@@ -24,9 +24,9 @@ EXPORTS = [
     "hdrf_batch_digests", "hdrf_batch_is_new", "hdrf_batch_placement", "hdrf_index_get",
     "hdrf_index_count", "hdrf_index_dump", "hdrf_allocator", "hdrf_recipe_get", "hdrf_block_length",
     "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
-    "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_stage_times", "hdrf_reset",
+    "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
-    "hdrf_gx_place", "hdrf_gx_commit",
+    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -54,6 +54,11 @@ class Config(ctypes.Structure):
         ("segment_bytes", ctypes.c_int32), ("keep_recipes", ctypes.c_int32), ("timing", ctypes.c_int32),
         ("debug_tag_bits", ctypes.c_int32), ("n_ranks", ctypes.c_int32), ("rank", ctypes.c_int32),
     ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in ("blocks", "chunks", "logical_bytes", "new_bytes", "closed_containers",
+                                             "closed_raw_bytes", "closed_file_bytes", "open_bytes", "recipe_bytes")]
 
 
 class GxLayout(ctypes.Structure):
@@ -123,8 +128,11 @@ def load():
         "hdrf_synchronize": (ctypes.c_int, [_vp]),
         "hdrf_corpus_fill": (ctypes.c_int, [_vp, _vp, _u32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                             ctypes.c_uint64]),
+        "hdrf_corpus_fill_kind": (ctypes.c_int, [_vp, _vp, _u32p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                                 ctypes.c_uint64, ctypes.c_int32]),
         "hdrf_stage_times": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int32]),
         "hdrf_reset": (ctypes.c_int, [_vp]),
+        "hdrf_get_stats": (ctypes.c_int, [_vp, ctypes.POINTER(Stats)]),
         "hdrf_gx_layout_get": (ctypes.c_int, [_vp, ctypes.POINTER(GxLayout)]),
         "hdrf_gx_front": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p,
                                          ctypes.c_uint32, _vp, _i64p]),
@@ -303,9 +311,10 @@ class Context:
         self._ck(self.L.hdrf_memcpy_d2h(self._h, out.ctypes.data, dev, nbytes))
         return out
 
-    def corpus_fill(self, dev, roots, nblocks, segs_per_block, seg_bytes, seed):
+    def corpus_fill(self, dev, roots, nblocks, segs_per_block, seg_bytes, seed, mixed=False):
         r = np.ascontiguousarray(roots, np.uint32)
-        self._ck(self.L.hdrf_corpus_fill(self._h, dev, _p(r, _u32p), nblocks, segs_per_block, seg_bytes, seed))
+        self._ck(self.L.hdrf_corpus_fill_kind(self._h, dev, _p(r, _u32p), nblocks, segs_per_block, seg_bytes, seed,
+                                              1 if mixed else 0))
 
     def synchronize(self):
         self._ck(self.L.hdrf_synchronize(self._h))
@@ -317,6 +326,11 @@ class Context:
 
     def reset(self):
         self._ck(self.L.hdrf_reset(self._h))
+
+    def stats(self):
+        st = Stats()
+        self._ck(self.L.hdrf_get_stats(self._h, ctypes.byref(st)))
+        return {f: getattr(st, f) for f, _ in Stats._fields_}
 
     # ---- node-global index phases (include/hdrf.h; orchestrated by hdrf_amd/node.py) -----
     def gx_layout(self):

@@ -122,12 +122,29 @@ int hdrf_synchronize(hdrf_ctx *ctx);
  * block b, segment s = splitmix64 words keyed by roots[b*segs_per_block+s]. */
 int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
                      int64_t segs_per_block, int64_t seg_bytes, uint64_t seed);
+/* Same with mixed != 0: BASELINE config 4's mixed-entropy segments (random / text / binary). */
+int hdrf_corpus_fill_kind(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
+                          int64_t segs_per_block, int64_t seg_bytes, uint64_t seed, int32_t mixed);
 
 /* Per-stage device time (ms) accumulated since the last reset, measured with HIP events on
  * the context's stream (cfg.timing = 1): [0] spec_walk_kernel, [1] stitch (sync/plan/copy/
  * fallback), [2] sha_full_kernel, [3] sha_tail_kernel, [4] idx_claim_kernel, [5] idx_apply_kernel,
  * [6] idx_slow+decide, [7] new-byte scans, [8] flush_kernel, [9] place_kernel, [10] lz4 (compressor 2). */
 int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
+/* Reduction totals since the last reset (this context's blocks): the dedup / compression ratio
+ * of the node is logical_bytes / (closed_file_bytes + open_bytes [+ recipe_bytes]). */
+typedef struct {
+    int64_t blocks, chunks;
+    int64_t logical_bytes;       /* bytes of the reduced blocks */
+    int64_t new_bytes;           /* sum of storeSize (DataDeduplicator.storeSize :355) */
+    int64_t closed_containers;
+    int64_t closed_raw_bytes;    /* container bytes of closed containers */
+    int64_t closed_file_bytes;   /* their file sizes (Lz4Codec stream under compressor 2) */
+    int64_t open_bytes;          /* raw bytes of the open containers (lastBlockID[0..2]) */
+    int64_t recipe_bytes;        /* recipes: BE32 size + digests (storeDB :372-392) */
+} hdrf_stats;
+int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out);
+
 /* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis). */
 int hdrf_reset(hdrf_ctx *ctx);
 

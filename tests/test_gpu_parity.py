@@ -185,3 +185,33 @@ def test_compression_stage_large_container():
     blocks = [np.concatenate([make_block(k, 70 + i, 6 << 20) for k in ("lowent", "random", "binary")])
               for i in range(3)]
     run_sequence(blocks, compressor=2, max_block_bytes=32 << 20, arena_slots=16)
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_device_corpus_matches_host_and_reduces(mixed):
+    """hdrf_corpus_fill(_kind) == hdrf_amd.corpus.corpus_block_host byte for byte (configs 2 and 4),
+    and the config-4 batch path (dedup + Lz4Codec containers) matches the oracle."""
+    nb, spb, seg = 10, 8, 1 << 18
+    roots = corpus_roots(33, 500000, nb, spb)
+    ctx = Context(compressor=2 if mixed else 1, container_max=1 << 20, **SMALL)
+    size = spb * seg
+    dev = ctx.dev_alloc(size * nb + 4096)
+    ctx.corpus_fill(dev, roots, nb, spb, seg, 33, mixed=mixed)
+    blocks = [corpus_block_host(33, roots, b, spb, seg, mixed=mixed) for b in range(nb)]
+    for b in range(nb):
+        assert np.array_equal(ctx.d2h(dev + b * size, size), blocks[b]), f"corpus block {b}"
+    ora = Oracle(compressor=2 if mixed else 1, max_size=1 << 20)
+    ids = list(range(700, 700 + nb))
+    for start in range(0, nb, 4):
+        k = min(4, nb - start)
+        ctx.reduce_batch([dev + (start + i) * size for i in range(k)], [size] * k,
+                         [size * (nb - start - i) + 4096 for i in range(k)], ids[start:start + k])
+        for i in range(k):
+            compare_block(ctx.batch_result(i), ora.reduce(blocks[start + i], ids[start + i]), tag=f"block {start + i}")
+    compare_state(ctx, ora, ids)
+    st = ctx.stats()
+    assert st["blocks"] == nb and st["logical_bytes"] == nb * size
+    if mixed:
+        assert st["closed_containers"] > 0 and st["closed_file_bytes"] < st["closed_raw_bytes"]
+    ctx.dev_free(dev)
+    ctx.close()
