@@ -6,9 +6,9 @@
 //
 // Two kernels:
 //   sha_full — every FULL 64-B block of every chunk.  A lane owns one chunk's compression chain;
-//              a wave owns a pool of 64*kPool consecutive chunks and a lane that finishes its
-//              chunk immediately takes the next one from the pool (ballot + mbcnt), so lanes do
-//              not idle while the wave's longest chunk finishes.  No padding logic in this loop.
+//              a lane that finishes its chunk immediately takes the next one from the wave's
+//              register pool of reserved chunks (ballot + mbcnt + ds_bpermute), so lanes do not
+//              idle while the wave's longest chunk finishes.  No padding logic in this loop.
 //   sha_tail — one lane per chunk: the 1-2 padded final blocks (FIPS 180-4 padding) and the
 //              digest store.
 // Each 64-B block is fetched as 17 dword-aligned dwords (4 x dwordx4 + 1) and realigned +
@@ -148,72 +148,76 @@ __device__ __forceinline__ void set_iv(uint32_t st[8])
     }
 }
 
-// persistent waves per block: enough for ~32 waves per CU whatever the batch size
-
-// grid (waves_per_block/4, nblocks); every wave serves chunks of block b from the block's work
-// counter, reserving 64 chunk indices per atomicAdd and handing them to lanes as their chains end
+// grid (waves_per_block/4, nblocks): every wave serves chunks of block b.  A lane owns one chunk's
+// compression chain; chunk offsets come from coalesced per-wave reservations of 64 chunks kept in
+// registers (pool P, with the next reservation Q fetched while P is consumed), so a lane that
+// finishes its chain takes the next chunk with two ds_bpermutes and no memory round trip.
 template <int HW>
 __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restrict__ blocks,
                                                        const uint32_t *__restrict__ offsets,
                                                        const BlockState *__restrict__ bst, int cap_blk,
                                                        uint32_t *__restrict__ mid, uint32_t *__restrict__ queue)
 {
-    extern __shared__ uint32_t s_occupancy_cap[];   // unused; sized by the launch to cap occupancy
-    (void)s_occupancy_cap;
     const int b = blockIdx.y;
     const int n = bst[b].n_chunks;
     const uint8_t *base = blocks[b].data;
     const uint32_t *off = offsets + (size_t)b * cap_blk;
     uint32_t *mb = mid + (size_t)b * cap_blk * 8;
     const int l = lane_id();
-    int res_next = 0, res_end = 0;            // current reservation (uniform)
-    bool exhausted = false;
+    int kbP, cntP, kbQ, cntQ;
+    uint32_t SP, EP, SQ, EQ;
+    auto reserve = [&](int &kb, int &cnt, uint32_t &S, uint32_t &E) {
+        uint32_t got = 0;
+        if (l == 0) got = atomicAdd(queue + b, 64u);
+        kb = (int)rdfirst(got);
+        cnt = max(0, min(64, n - kb));
+        const int k = kb + l;
+        E = l < cnt ? ld4(off + k) : 0u;
+        S = (l < cnt && k > 0) ? ld4(off + k - 1) : 0u;
+    };
+    reserve(kbP, cntP, SP, EP);
+    reserve(kbQ, cntQ, SQ, EQ);
+    int head = 0;
+    bool active = false;
     int k = 0;
-    bool active = false;                      // lane owns a chain with blocks left or just finished
     uint32_t pos = 0, r = 0;
     uint32_t st[8];
     set_iv<HW>(st);
     for (;;) {
-        // store finished chains; hand out new chunks to idle lanes (may repeat for empty chains)
-        for (;;) {
-            const bool done = active && r == 0;
-            if (done) {
+        if (active && r == 0) {                   // chain done: mid-state for sha_tail
 #pragma unroll
-                for (int i = 0; i < 8; i++) mb[(size_t)k * 8 + i] = st[i];
+            for (int i = 0; i < (HW == 5 ? 5 : 8); i++) mb[(size_t)k * 8 + i] = st[i];
+            active = false;
+        }
+        for (;;) {                                 // offer chunks to idle lanes
+            const unsigned long long idle = ballot64(!active);
+            if (!idle) break;
+            if (head >= cntP) {                   // pool P exhausted: rotate in Q, fetch the next
+                if (cntQ == 0) break;
+                kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
+                reserve(kbQ, cntQ, SQ, EQ);
             }
-            const bool idle = !active || done;
-            const unsigned long long bal = ballot64(idle);
-            if (!bal || exhausted) {
-                if (done) active = false;
-                break;
-            }
-            if (res_next == res_end) {
-                uint32_t got = 0;
-                if (l == 0) got = atomicAdd(queue + b, 64u);
-                got = rdfirst(got);
-                if ((int)got >= n) {
-                    exhausted = true;
-                    if (done) active = false;
-                    break;
-                }
-                res_next = (int)got;
-                res_end = min((int)got + 64, n);
-            }
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-            const int avail = res_end - res_next;
-            if (idle) {
-                if (rank < avail) {
-                    k = res_next + rank;
-                    active = true;
-                    set_iv<HW>(st);
-                    pos = k ? off[k - 1] : 0u;
-                    r = (off[k] - pos) >> 6;
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
+            const int avail = cntP - head;
+            const int idx = min(head + rank, 63);
+            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), s0 = (uint32_t)__shfl((int)SP, idx, 64);
+            bool zero = false;
+            if (!active && rank < avail) {
+                k = kbP + head + rank;
+                pos = s0;
+                r = (e - s0) >> 6;
+                set_iv<HW>(st);
+                if (r == 0) {                     // no full block: sha_tail starts from the IV
+#pragma unroll
+                    for (int i = 0; i < (HW == 5 ? 5 : 8); i++) mb[(size_t)k * 8 + i] = st[i];
+                    zero = true;
                 } else {
-                    active = false;
+                    active = true;
                 }
             }
-            res_next += min(__popcll(bal), (long long)avail);
-            if (!ballot64(active && r == 0)) break;
+            const int nidle = __popcll(idle);
+            head += min(nidle, avail);
+            if (!ballot64(zero) && nidle <= avail) break;
         }
         if (!ballot64(active)) break;
         if (active) {
@@ -247,7 +251,7 @@ __global__ void __launch_bounds__(256) sha_tail_kernel(const BlockDesc *__restri
     uint32_t st[8];
     const uint32_t *ms = mid + ((size_t)b * cap_blk + k) * 8;
 #pragma unroll
-    for (int i = 0; i < 8; i++) st[i] = ms[i];
+    for (int i = 0; i < (HW == 5 ? 5 : 8); i++) st[i] = ms[i];          // chaining state words
     for (int bi = full; bi < nblk; bi++) {
         uint32_t m[16];
         load_block(bd.data, (int64_t)bd.readable, start, len, bi, nblk, m);
@@ -265,10 +269,13 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
 {
     (void)hipMemsetAsync(queue, 0, sizeof(uint32_t) * nblocks, st);
     mk->mark(st);
-    const int wpb = std::min(2048, std::max(128, 8192 / nblocks));
-    dim3 gf(wpb / 4, nblocks);
-    // occupancy cap for the scattered per-lane streams (experiment knob): LDS bytes per workgroup
+    // 4 waves per SIMD measured faster than 8 (fewer concurrent per-lane streams: less L2
+    // thrashing of the 128-B lines two consecutive compressions of a lane share); env knobs for
+    // experiments: HDRF_SHA_WAVES (waves per SIMD over 1024 SIMDs), HDRF_SHA_LDS (bytes per WG)
+    static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : 4; }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
+    const int wpb = std::max(4, (per_simd * 1024 / nblocks) & ~3);
+    dim3 gf(wpb / 4, nblocks);
     dim3 gt((cap_blk + 255) / 256, nblocks);
     if (hasher == 0) {
         hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue);
