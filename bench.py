@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--hasher", type=int, default=0)
     ap.add_argument("--cpu-sample-blocks", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--arena-slots", type=int, default=512,
+                    help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers")
     ap.add_argument("--workload", choices=["config2", "config4"], default="config2",
                     help="config4: mixed-entropy blocks (random/text/binary), dedup + Lz4Codec containers")
     return ap.parse_args()
@@ -101,7 +103,7 @@ def main():
         raise SystemExit("config4 (compression stage) runs on single-node contexts only")
     compressor = 2 if mixed else 1
     ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
-                  arena_slots=64, keep_recipes=0, timing=1, n_ranks=world, rank=rank, compressor=compressor)
+                  arena_slots=a.arena_slots, keep_recipes=0, timing=1, n_ranks=world, rank=rank, compressor=compressor)
     node = None
     if world > 1:
         from hdrf_amd.node import NodeRank, global_block
@@ -131,14 +133,26 @@ def main():
         else:
             node.reset()
         j = 0
-        for ptrs, lens, rd, ids in batches:
-            if node is None:
-                ctx.reduce_batch(ptrs, lens, rd, ids)
-            else:
-                node.reduce_batch(ptrs, lens, rd, ids, rank * B)
-            for i in range(len(ptrs)):
+
+        def collect():
+            nonlocal j
+            for i in range(ctx.last_nblocks()):
                 n_chunks[j], store[j] = ctx.batch_info(i)
                 j += 1
+
+        if node is None:
+            # pipelined: chunking + SHA of batch k+1 overlap the index/store stage of batch k
+            for k, (ptrs, lens, rd, ids) in enumerate(batches):
+                ctx.submit_batch(ptrs, lens, rd, ids)
+                if k:
+                    ctx.wait_batch()
+                    collect()
+            ctx.wait_batch()
+            collect()
+        else:
+            for ptrs, lens, rd, ids in batches:
+                node.reduce_batch(ptrs, lens, rd, ids, rank * B)
+                collect()
 
     def barrier():
         if dist is not None:

@@ -1,9 +1,18 @@
-// api.hip — libhdrf C-ABI (include/hdrf.h): context, batch orchestration, host views.
+// api.hip — libhdrf C-ABI (include/hdrf.h): context, batch pipeline, host views.
 //
 // One context = one DataNode's reduction state on one GPU: the index table (Redis in the
 // reference), the container arena (chunkDir files), the allocator ("blockID" key) and the
-// recipes.  All device work of a batch is enqueued on the context's stream; the host
-// synchronises once per batch to read back block counts and the allocator.
+// recipes.
+//
+// Batches run as a two-stage pipeline over two HIP streams and two buffer slots:
+//   front (stream A): descriptor upload, chunking, SHA            -> per-slot arrays only
+//   back  (stream B): index, placement/gather, compression, read-back of the batch's small state
+// Batch k's front waits only for the back of batch k-2 (its slot's previous user); its back waits
+// for its own front and, by stream order, for batch k-1's back (the index, allocator and arena
+// are updated strictly in block order: the reference's FIFO, DN/DataDeduplicator.java:124-158).
+// So while batch k is being indexed and stored, batch k+1 is already being chunked and hashed.
+// hdrf_submit_batch enqueues; hdrf_wait_batch completes the oldest batch (host bookkeeping);
+// hdrf_reduce_batch does both.
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -21,6 +30,8 @@ namespace {
 
 constexpr int kStages = hdrf::kNumStages;
 constexpr uint64_t kSlack = 64;   // readable bytes required past each block end
+constexpr int kSlots = 2;         // batches in flight
+constexpr int kErrCapacity = 2 | 4 | 8 | 16 | 32;  // device error bits that mean "a buffer is too small"
 
 struct ContainerInfo {
     uint32_t slot;
@@ -29,14 +40,8 @@ struct ContainerInfo {
     uint32_t clen;           // compressor 2, closed: Lz4Codec file length (compressed arena slot)
 };
 
-}  // namespace
-
-struct hdrf_ctx {
-    hdrf_cfg cfg{};
-    int H = 20, HW = 5;
-    hipStream_t st = nullptr;
-    int max_batch = 0, cap_blk = 0, ntiles = 0, spec_cap = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
-    // device buffers
+// Per-batch buffers (device) and read-back (pinned host) of one pipeline slot.
+struct Slot {
     BlockDesc *d_blocks = nullptr;
     uint32_t *d_spec = nullptr;
     SegMeta *d_meta = nullptr;
@@ -52,22 +57,49 @@ struct hdrf_ctx {
     ClosedRec *d_closed = nullptr;
     uint32_t *d_nclosed = nullptr;
     uint32_t *d_coll = nullptr, *d_ncoll = nullptr;
+    uint32_t *d_pcid = nullptr, *d_ppos = nullptr, *d_queue = nullptr;
+    uint32_t *d_segclen = nullptr, *d_filelen = nullptr;
+    int *d_err = nullptr;
+    // pinned read-back, filled by stream B before back_done
+    BlockState *h_bst = nullptr;
+    uint64_t *h_store = nullptr;
+    AllocState *h_alloc = nullptr;
+    int *h_err = nullptr;
+    uint32_t *h_nclosed = nullptr;
+    ClosedRec *h_closed = nullptr;
+    uint32_t *h_filelen = nullptr;
+    BlockDesc *h_desc = nullptr;
+    // host metadata of the batch in this slot
+    std::vector<uint64_t> ids, lens;
+    int nblocks = 0;
+    bool pending = false;
+    hipEvent_t front_done = nullptr, back_done = nullptr;
+    hipEvent_t evA[5] = {}, evB[9] = {};   // stage markers (timing)
+};
+
+}  // namespace
+
+struct hdrf_ctx {
+    hdrf_cfg cfg{};
+    int H = 20, HW = 5;
+    hipStream_t st = nullptr;    // stream A: front stage (also every synchronous helper)
+    hipStream_t stB = nullptr;   // stream B: back stage
+    int max_batch = 0, cap_blk = 0, ntiles = 0, spec_cap = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
+    Slot sl[kSlots];
+    uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
+    int res = 0;                   // slot of the last completed batch (hdrf_batch_* views)
+    // node state (shared by all batches)
     IndexEntry *d_tab = nullptr;
     uint8_t *d_arena = nullptr;
     uint8_t *d_carena = nullptr;                 // compressor 2: Lz4Codec files of closed containers
     uint64_t cslot = 0;
-    uint32_t *d_segclen = nullptr, *d_filelen = nullptr;
     AllocState *d_alloc = nullptr;
-    uint32_t *d_pcid = nullptr, *d_ppos = nullptr, *d_queue = nullptr;
-    int *d_err = nullptr;
     uint8_t *d_stage = nullptr;
     uint64_t stage_cap = 0;
     // host state
     uint32_t batch = 0;
     int have_alloc = 0;
     int last_nblocks = 0;
-    std::vector<BlockState> h_bst;
-    std::vector<uint64_t> h_store;
     AllocState h_alloc{};
     std::map<uint32_t, ContainerInfo> containers;   // container id -> arena slot
     std::map<uint32_t, uint32_t> slot_owner;         // arena slot -> container id
@@ -85,11 +117,9 @@ struct hdrf_ctx {
     const uint32_t *gx_x2 = nullptr;             // responses of the current batch (caller's buffer)
     int gx_phase = 0;                            // 1 front, 2 owner, 3 decide, 4 flush, 5 place
     int gx_nblocks = 0;
-    std::vector<uint64_t> gx_ids, gx_lens;
     hdrf_stats stats{};                          // cumulative since the last reset
     // timing
     bool timing = false;
-    hipEvent_t ev[kStages + 1] = {};
     double stage_ms[kStages] = {};
     std::string err;
 };
@@ -115,6 +145,14 @@ static int set_err(hdrf_ctx *ctx, int code, const std::string &msg)
     return code;
 }
 
+static int device_error(hdrf_ctx *ctx, int herr)
+{
+    std::string m = "device reported error flags " + std::to_string(herr);
+    if (herr & 32) m += " (arena_slots too small: a storer range closed more containers in one batch than its ring holds)";
+    if (herr & 2) m += " (index table full)";
+    return set_err(ctx, (herr & kErrCapacity) ? HDRF_E_CAPACITY : HDRF_E_DEVICE, m);
+}
+
 template <class T>
 static int dalloc(hdrf_ctx *ctx, T **p, size_t count)
 {
@@ -124,6 +162,18 @@ static int dalloc(hdrf_ctx *ctx, T **p, size_t count)
         ctx->err = "hipMalloc failed (" + std::to_string(bytes) + " bytes)";
         return HDRF_E_NOMEM;
     }
+    return 0;
+}
+
+template <class T>
+static int halloc(hdrf_ctx *ctx, T **p, size_t count)
+{
+    if (hipHostMalloc((void **)p, std::max<size_t>(count * sizeof(T), 64), hipHostMallocDefault) != hipSuccess) {
+        *p = nullptr;
+        ctx->err = "hipHostMalloc failed";
+        return HDRF_E_NOMEM;
+    }
+    std::memset(*p, 0, std::max<size_t>(count * sizeof(T), 64));
     return 0;
 }
 
@@ -151,23 +201,92 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
     return 0;
 }
 
+static void free_slot(Slot &S)
+{
+    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_sync, S.d_plan, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
+                   S.d_pre, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
+                   S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err};
+    for (void *p : dev)
+        if (p) (void)hipFree(p);
+    void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_closed, S.h_filelen, S.h_desc};
+    for (void *p : host)
+        if (p) (void)hipHostFree(p);
+    hipEvent_t evs[] = {S.front_done, S.back_done};
+    for (auto e : evs)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : S.evA)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : S.evB)
+        if (e) (void)hipEventDestroy(e);
+}
+
 static void free_all(hdrf_ctx *ctx)
 {
-    void *ptrs[] = {ctx->d_blocks, ctx->d_spec, ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off,
-                    ctx->d_dig, ctx->d_mid, ctx->d_slot, ctx->d_pre, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
-                    ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed, ctx->d_coll, ctx->d_ncoll, ctx->d_tab,
-                    ctx->d_arena, ctx->d_alloc, ctx->d_pcid, ctx->d_ppos, ctx->d_queue, ctx->d_err, ctx->d_stage,
-                    ctx->d_scratch, ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags,
-                    ctx->d_carena, ctx->d_segclen, ctx->d_filelen};
+    for (auto &S : ctx->sl) free_slot(S);
+    void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_scratch, ctx->d_gx_counts,
+                    ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags, ctx->d_carena};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
-    for (auto &e : ctx->ev)
-        if (e) (void)hipEventDestroy(e);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
+    if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
+}
+
+static int alloc_slot(hdrf_ctx *ctx, Slot &S)
+{
+    const hdrf_cfg &c = ctx->cfg;
+    const int B = ctx->max_batch;
+    const size_t nchunk = (size_t)B * ctx->cap_blk;
+    const size_t nseg = (size_t)B * kMaxSegs;
+    const int nseg_lz = (int)((c.container_max + 261099) / 261100);
+    int rc = 0;
+    if ((rc = dalloc(ctx, &S.d_blocks, B)) || (rc = dalloc(ctx, &S.d_spec, nseg * ctx->spec_cap)) ||
+        (rc = dalloc(ctx, &S.d_meta, nseg)) || (rc = dalloc(ctx, &S.d_sync, nseg)) ||
+        (rc = dalloc(ctx, &S.d_plan, nseg)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
+        (rc = dalloc(ctx, &S.d_off, nchunk)) || (rc = dalloc(ctx, &S.d_dig, nchunk * ctx->HW)) ||
+        (rc = dalloc(ctx, &S.d_mid, nchunk * 8)) || (rc = dalloc(ctx, &S.d_slot, nchunk)) ||
+        (rc = dalloc(ctx, &S.d_pre, nchunk)) || (rc = dalloc(ctx, &S.d_flags, nchunk)) ||
+        (rc = dalloc(ctx, &S.d_tilesum, (size_t)B * ctx->ntiles)) ||
+        (rc = dalloc(ctx, &S.d_tilepre, (size_t)B * ctx->ntiles)) || (rc = dalloc(ctx, &S.d_store, B)) ||
+        (rc = dalloc(ctx, &S.d_rstate, (size_t)B * 4)) || (rc = dalloc(ctx, &S.d_ev, (size_t)3 * ctx->ev_cap)) ||
+        (rc = dalloc(ctx, &S.d_closed, ctx->closed_cap)) || (rc = dalloc(ctx, &S.d_nclosed, 1)) ||
+        (rc = dalloc(ctx, &S.d_coll, ctx->coll_cap)) || (rc = dalloc(ctx, &S.d_ncoll, 1)) ||
+        (rc = dalloc(ctx, &S.d_pcid, nchunk)) || (rc = dalloc(ctx, &S.d_ppos, nchunk)) ||
+        (rc = dalloc(ctx, &S.d_queue, 64)) || (rc = dalloc(ctx, &S.d_err, 1)) ||
+        (rc = halloc(ctx, &S.h_bst, B)) || (rc = halloc(ctx, &S.h_store, B)) || (rc = halloc(ctx, &S.h_alloc, 1)) ||
+        (rc = halloc(ctx, &S.h_err, 1)) || (rc = halloc(ctx, &S.h_nclosed, 1)) ||
+        (rc = halloc(ctx, &S.h_closed, ctx->closed_cap)) || (rc = halloc(ctx, &S.h_filelen, ctx->closed_cap)) ||
+        (rc = halloc(ctx, &S.h_desc, B)))
+        return rc;
+    if (c.compressor == 2 && ((rc = dalloc(ctx, &S.d_segclen, (size_t)ctx->closed_cap * nseg_lz)) ||
+                              (rc = dalloc(ctx, &S.d_filelen, (size_t)ctx->closed_cap))))
+        return rc;
+    if (hipEventCreateWithFlags(&S.front_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess)
+        return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
+    for (auto &e : S.evA)
+        if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
+    for (auto &e : S.evB)
+        if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
+    if (hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->st) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "memset");
+    return 0;
+}
+
+static int wait_one(hdrf_ctx *ctx);
+
+// complete every batch in flight (views, reset, the node-global phases need a quiet context)
+static int drain(hdrf_ctx *ctx)
+{
+    int rc = 0;
+    while (ctx->nwait < ctx->nsub)
+        if (int r = wait_one(ctx)) rc = rc ? rc : r;
+    HIPCK(hipStreamSynchronize(ctx->st));
+    HIPCK(hipStreamSynchronize(ctx->stB));
+    return rc;
 }
 
 static int init_state(hdrf_ctx *ctx)
 {
+    (void)drain(ctx);
     HIPCK(hipMemsetAsync(ctx->d_tab, 0, sizeof(IndexEntry) << ctx->cfg.index_log2, ctx->st));
     AllocState a{};
     for (int t = 0; t < 4; t++) {
@@ -176,7 +295,7 @@ static int init_state(hdrf_ctx *ctx)
         a.slot[t] = (uint32_t)t * (uint32_t)(ctx->cfg.arena_slots / 4);   // per-range slot rings
     }
     HIPCK(hipMemcpyAsync(ctx->d_alloc, &a, sizeof a, hipMemcpyHostToDevice, ctx->st));
-    HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), ctx->st));
+    for (auto &S : ctx->sl) HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
     ctx->h_alloc = a;
     ctx->batch = 0;
@@ -213,7 +332,9 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     ctx->H = c.hasher == 0 ? 20 : 28;
     ctx->HW = c.hasher == 0 ? 5 : 7;
     int rc = 0;
-    if (hipSetDevice(c.device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(c.device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stB, hipStreamNonBlocking) != hipSuccess) {
+        free_all(ctx);
         delete ctx;
         return HDRF_E_HIP;
     }
@@ -227,42 +348,19 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     ctx->closed_cap = 3 * ctx->ev_cap;
     ctx->coll_cap = 1 << 16;
     const size_t nchunk = (size_t)B * ctx->cap_blk;
-    const size_t nseg = (size_t)B * kMaxSegs;
-    if ((rc = dalloc(ctx, &ctx->d_blocks, B)) || (rc = dalloc(ctx, &ctx->d_spec, nseg * ctx->spec_cap)) ||
-        (rc = dalloc(ctx, &ctx->d_meta, nseg)) || (rc = dalloc(ctx, &ctx->d_sync, nseg)) ||
-        (rc = dalloc(ctx, &ctx->d_plan, nseg)) || (rc = dalloc(ctx, &ctx->d_bst, B)) ||
-        (rc = dalloc(ctx, &ctx->d_off, nchunk)) || (rc = dalloc(ctx, &ctx->d_dig, nchunk * ctx->HW)) ||
-        (rc = dalloc(ctx, &ctx->d_mid, nchunk * 8)) ||
-        (rc = dalloc(ctx, &ctx->d_slot, nchunk)) || (rc = dalloc(ctx, &ctx->d_pre, nchunk)) ||
-        (rc = dalloc(ctx, &ctx->d_flags, nchunk)) || (rc = dalloc(ctx, &ctx->d_tilesum, (size_t)B * ctx->ntiles)) ||
-        (rc = dalloc(ctx, &ctx->d_tilepre, (size_t)B * ctx->ntiles)) || (rc = dalloc(ctx, &ctx->d_store, B)) ||
-        (rc = dalloc(ctx, &ctx->d_rstate, (size_t)B * 4)) || (rc = dalloc(ctx, &ctx->d_ev, (size_t)3 * ctx->ev_cap)) ||
-        (rc = dalloc(ctx, &ctx->d_closed, ctx->closed_cap)) || (rc = dalloc(ctx, &ctx->d_nclosed, 1)) ||
-        (rc = dalloc(ctx, &ctx->d_coll, ctx->coll_cap)) || (rc = dalloc(ctx, &ctx->d_ncoll, 1)) ||
-        (rc = dalloc(ctx, &ctx->d_tab, (size_t)1 << c.index_log2)) ||
-        (rc = dalloc(ctx, &ctx->d_arena, (size_t)c.arena_slots * c.container_max + 256)) ||
-        (rc = dalloc(ctx, &ctx->d_alloc, 1)) || (rc = dalloc(ctx, &ctx->d_pcid, nchunk)) ||
-        (rc = dalloc(ctx, &ctx->d_ppos, nchunk)) || (rc = dalloc(ctx, &ctx->d_queue, 64)) || (rc = dalloc(ctx, &ctx->d_err, 1))) {
-        fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
-        free_all(ctx);
-        delete ctx;
-        return rc;
+    for (auto &S : ctx->sl)
+        if (!rc) rc = alloc_slot(ctx, S);
+    if (!rc && ((rc = dalloc(ctx, &ctx->d_tab, (size_t)1 << c.index_log2)) ||
+                (rc = dalloc(ctx, &ctx->d_arena, (size_t)c.arena_slots * c.container_max + 256)) ||
+                (rc = dalloc(ctx, &ctx->d_alloc, 1)))) {
     }
-    if (c.compressor == 2) {
+    if (!rc && c.compressor == 2) {
         ctx->cslot = lz4_slot_bytes(c.container_max);
-        const int nseg = (int)((c.container_max + 261099) / 261100);
-        if ((rc = dalloc(ctx, &ctx->d_carena, (size_t)c.arena_slots * ctx->cslot + 256)) ||
-            (rc = dalloc(ctx, &ctx->d_segclen, (size_t)ctx->closed_cap * nseg)) ||
-            (rc = dalloc(ctx, &ctx->d_filelen, (size_t)ctx->closed_cap))) {
-            fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
-            free_all(ctx);
-            delete ctx;
-            return rc;
-        }
+        rc = dalloc(ctx, &ctx->d_carena, (size_t)c.arena_slots * ctx->cslot + 256);
     }
     ctx->G = c.n_ranks;
     ctx->rank = c.rank;
-    if (ctx->G > 1) {
+    if (!rc && ctx->G > 1) {
         // scratch table for the batch's local aggregation: >= 1.5x the expected distinct chunks
         // (mean chunk ~949 B on random data; a table-full condition is reported, never silent)
         const double expect = 1.5 * (double)B * (double)c.max_block_bytes / 900.0;
@@ -274,16 +372,12 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         if ((rc = dalloc(ctx, &ctx->d_scratch, (size_t)1 << lg)) || (rc = dalloc(ctx, &ctx->d_gx_counts, 64)) ||
             (rc = dalloc(ctx, &ctx->d_gx_rcounts, 64)) || (rc = dalloc(ctx, &ctx->d_oslot, nrec)) ||
             (rc = dalloc(ctx, &ctx->d_oflags, nrec))) {
-            fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
-            free_all(ctx);
-            delete ctx;
-            return rc;
         }
     }
     ctx->timing = c.timing != 0;
-    for (auto &e : ctx->ev)
-        if (hipEventCreate(&e) != hipSuccess) { free_all(ctx); delete ctx; return HDRF_E_HIP; }
-    if ((rc = init_state(ctx))) {
+    if (!rc) rc = init_state(ctx);
+    if (rc) {
+        fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
         free_all(ctx);
         delete ctx;
         return rc;
@@ -295,7 +389,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
 extern "C" int hdrf_close(hdrf_ctx *ctx)
 {
     if (!ctx) return HDRF_E_INVAL;
-    (void)hipStreamSynchronize(ctx->st);
+    (void)drain(ctx);
     free_all(ctx);
     delete ctx;
     return 0;
@@ -319,33 +413,34 @@ static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t l
     ctx->containers[id] = ContainerInfo{slot, len, closed, clen};
 }
 
-// Validate a batch and upload its block descriptors; returns the largest segment count.
-static int prepare_blocks(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
-                          const uint64_t *readable, int *max_nseg_out)
+// Validate a batch and fill the slot's (pinned) descriptors; returns the largest segment count.
+static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t *const *dev_data,
+                          const uint64_t *len, const uint64_t *readable, int *max_nseg_out)
 {
     if (nblocks < 1 || nblocks > ctx->max_batch || !dev_data || !len || !readable)
         return set_err(ctx, HDRF_E_INVAL, "bad batch arguments");
     const hdrf_cfg &c = ctx->cfg;
-    std::vector<BlockDesc> bd(nblocks);
     int max_nseg = 1;
     for (int b = 0; b < nblocks; b++) {
         if ((int64_t)len[b] > c.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
         if (readable[b] < len[b] + kSlack) return set_err(ctx, HDRF_E_INVAL, "readable must be >= len + 64");
         if (((uintptr_t)dev_data[b] & 15) != 0) return set_err(ctx, HDRF_E_INVAL, "block data must be 16-B aligned");
-        bd[b].data = dev_data[b];
-        bd[b].len = len[b];
-        bd[b].readable = readable[b];
+    }
+    for (int b = 0; b < nblocks; b++) {
+        BlockDesc &d = S.h_desc[b];
+        d.data = dev_data[b];
+        d.len = len[b];
+        d.readable = readable[b];
         int nseg = (int)std::min<int64_t>(kMaxSegs, std::max<int64_t>(1, (int64_t)len[b] / c.segment_bytes));
         int seg_len = (int)len[b];
         if (nseg > 1) {
             seg_len = (int)(((int64_t)len[b] / nseg) / (c.window + 2) * (c.window + 2));
             if (seg_len < 4 * (c.window + 2)) { nseg = 1; seg_len = (int)len[b]; }
         }
-        bd[b].nseg = nseg;
-        bd[b].seg_len = seg_len;
+        d.nseg = nseg;
+        d.seg_len = seg_len;
         max_nseg = std::max(max_nseg, nseg);
     }
-    HIPCK(hipMemcpyAsync(ctx->d_blocks, bd.data(), sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, ctx->st));
     *max_nseg_out = max_nseg;
     return 0;
 }
@@ -360,88 +455,131 @@ static StoreParams store_params(const hdrf_ctx *ctx, int nblocks)
     return P;
 }
 
-static void accumulate_stages(hdrf_ctx *ctx, int nmarks)
+static float elapsed(hipEvent_t a, hipEvent_t b)
 {
-    if (!ctx->timing) return;
-    for (int i = 0; i + 1 < nmarks && i < kStages; i++) {
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, ctx->ev[i], ctx->ev[i + 1]) == hipSuccess) ctx->stage_ms[i] += ms;
-    }
+    float ms = 0;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.f;
 }
 
-// After the store kernels of a batch: read back block counts / allocator, record closed
-// containers, recipes and block lengths (the host-side Redis + chunkDir views).
-static int finish_batch(hdrf_ctx *ctx, int32_t nblocks, const uint64_t *len, const uint64_t *block_ids, int nmarks)
+// Enqueue one batch: front on stream A, back on stream B (see the file comment).
+static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                  const uint64_t *readable, const uint64_t *block_ids)
+{
+    if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)
+        if (int rc = wait_one(ctx)) return rc;
+    Slot &S = ctx->sl[ctx->nsub % kSlots];
+    const hdrf_cfg &c = ctx->cfg;
+    int max_nseg = 1;
+    if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable, &max_nseg)) return rc;
+    S.ids.assign(nblocks, 0);
+    if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
+    S.lens.assign(len, len + nblocks);
+    S.nblocks = nblocks;
+    const uint32_t cur = ++ctx->batch;
+    hipStream_t A = ctx->st, Bst = ctx->stB;
+    // ---- front: the slot's previous batch has completed (wait_one ran), so A may overwrite it
+    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, A));
+    Marker ma;
+    ma.ev = ctx->timing ? S.evA : nullptr;
+    HIPCK(launch_chunking(S.d_blocks, nblocks, max_nseg, c.window, c.max_chunk, S.d_spec, ctx->spec_cap, S.d_meta,
+                          S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, A, &ma));
+    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig, S.d_queue, A,
+                     &ma));
+    ma.mark(A);
+    HIPCK(hipEventRecord(S.front_done, A));
+    // ---- back: in block order on stream B
+    HIPCK(hipStreamWaitEvent(Bst, S.front_done, 0));
+    HIPCK(hipMemsetAsync(S.d_nclosed, 0, sizeof(uint32_t), Bst));
+    Marker mb;
+    mb.ev = ctx->timing ? S.evB : nullptr;
+    HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_tab, c.index_log2, cur,
+                       tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap, S.d_flags, S.d_tilesum, ctx->ntiles,
+                       S.d_err, Bst, &mb));
+    const StoreParams P = store_params(ctx, nblocks);
+    HIPCK(launch_store(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_pre,
+                       ctx->d_alloc, S.d_rstate, S.d_ev, S.d_closed, S.d_nclosed, S.d_slot, ctx->d_tab, ctx->d_arena,
+                       S.d_pcid, S.d_ppos, S.d_err, Bst, &mb));
+    if (c.compressor == 2)      // compression stage: closed containers -> Lz4Codec files (:770-779)
+        HIPCK(launch_lz4(S.d_closed, S.d_nclosed, ctx->closed_cap, c.container_max, ctx->d_arena, ctx->d_carena,
+                         ctx->cslot, S.d_segclen, S.d_filelen, Bst));
+    mb.mark(Bst);
+    HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nblocks, hipMemcpyDeviceToHost, Bst));
+    HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nblocks, hipMemcpyDeviceToHost, Bst));
+    HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, Bst));
+    HIPCK(hipMemcpyAsync(S.h_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, Bst));
+    HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, Bst));
+    HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, Bst));
+    if (c.compressor == 2)
+        HIPCK(hipMemcpyAsync(S.h_filelen, S.d_filelen, sizeof(uint32_t) * ctx->closed_cap, hipMemcpyDeviceToHost, Bst));
+    HIPCK(hipEventRecord(S.back_done, Bst));
+    S.pending = true;
+    ctx->nsub++;
+    return 0;
+}
+
+static int complete_state(hdrf_ctx *ctx, Slot &S);
+
+// After a batch's read-back landed: container / recipe / allocator bookkeeping.
+static int complete_slot(hdrf_ctx *ctx, int si, bool timed)
+{
+    Slot &S = ctx->sl[si];
+    const int nblocks = S.nblocks;
+    if (ctx->timing && timed) {
+        for (int i = 0; i < 4; i++) ctx->stage_ms[i] += elapsed(S.evA[i], S.evA[i + 1]);
+        for (int i = 0; i < 6; i++) ctx->stage_ms[4 + i] += elapsed(S.evB[i], S.evB[i + 1]);
+        ctx->stage_ms[10] += elapsed(S.evB[7], S.evB[8]);
+    }
+    ctx->res = si;
+    ctx->last_nblocks = nblocks;
+    ctx->h_alloc = *S.h_alloc;
+    const int herr = *S.h_err;
+    if (herr) {
+        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->stB));
+        HIPCK(hipStreamSynchronize(ctx->stB));
+        *S.h_err = 0;
+        return device_error(ctx, herr);
+    }
+    return complete_state(ctx, S);
+}
+static int complete_state(hdrf_ctx *ctx, Slot &S)
 {
     const hdrf_cfg &c = ctx->cfg;
-    hipStream_t st = ctx->st;
-    ctx->h_bst.resize(nblocks);
-    ctx->h_store.resize(nblocks);
-    int herr = 0;
-    uint32_t nclosed = 0;
-    HIPCK(hipMemcpyAsync(ctx->h_bst.data(), ctx->d_bst, sizeof(BlockState) * nblocks, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(ctx->h_store.data(), ctx->d_store, sizeof(uint64_t) * nblocks, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(&ctx->h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(&herr, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(&nclosed, ctx->d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
-    accumulate_stages(ctx, nmarks);
-    ctx->last_nblocks = nblocks;
-    if (herr) {
-        HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), st));
-        return set_err(ctx, herr & 22 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
-                       "device reported error flags " + std::to_string(herr));
-    }
+    const int nblocks = S.nblocks;
+    const uint32_t nclosed = *S.h_nclosed;
     if ((int)nclosed > ctx->closed_cap) return set_err(ctx, HDRF_E_CAPACITY, "closed-container list overflow");
-    if (nclosed) {
-        std::vector<ClosedRec> cl(nclosed);
-        std::vector<uint32_t> flen(nclosed, 0);
-        HIPCK(hipMemcpy(cl.data(), ctx->d_closed, sizeof(ClosedRec) * nclosed, hipMemcpyDeviceToHost));
-        if (c.compressor == 2) {
-            // compression stage: each closed container is rewritten as an Lz4Codec file (:770-779)
-            if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[0], st));
-            HIPCK(launch_lz4(ctx->d_closed, (int)nclosed, c.container_max, ctx->d_arena, ctx->d_carena, ctx->cslot,
-                             ctx->d_segclen, ctx->d_filelen, st));
-            if (ctx->timing) HIPCK(hipEventRecord(ctx->ev[1], st));
-            HIPCK(hipMemcpyAsync(flen.data(), ctx->d_filelen, sizeof(uint32_t) * nclosed, hipMemcpyDeviceToHost, st));
-            HIPCK(hipStreamSynchronize(st));
-            if (ctx->timing) {
-                float ms = 0;
-                HIPCK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
-                ctx->stage_ms[10] += ms;
-            }
-        }
-        for (uint32_t i = 0; i < nclosed; i++) {
-            note_container(ctx, cl[i].id, cl[i].slot, cl[i].len, 1, flen[i]);
-            ctx->stats.closed_containers++;
-            ctx->stats.closed_raw_bytes += cl[i].len;
-            ctx->stats.closed_file_bytes += c.compressor == 2 ? flen[i] : cl[i].len;
-        }
+    for (uint32_t i = 0; i < nclosed; i++) {
+        const ClosedRec &r = S.h_closed[i];
+        const uint32_t flen = c.compressor == 2 ? S.h_filelen[i] : r.len;
+        note_container(ctx, r.id, r.slot, r.len, 1, flen);
+        ctx->stats.closed_containers++;
+        ctx->stats.closed_raw_bytes += r.len;
+        ctx->stats.closed_file_bytes += flen;
     }
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) note_container(ctx, ctx->h_alloc.id[t], ctx->h_alloc.slot[t], ctx->h_alloc.cur[t], 0);
     ctx->have_alloc = 1;                              // storeDB always SETs "blockID" (:389)
     for (int b = 0; b < nblocks; b++) {
         ctx->stats.blocks++;
-        ctx->stats.logical_bytes += len[b];
-        ctx->stats.new_bytes += ctx->h_store[b];
-        ctx->stats.chunks += ctx->h_bst[b].n_chunks;
-        ctx->stats.recipe_bytes += 4 + (uint64_t)ctx->h_bst[b].n_chunks * ctx->H;
+        ctx->stats.logical_bytes += S.lens[b];
+        ctx->stats.new_bytes += S.h_store[b];
+        ctx->stats.chunks += S.h_bst[b].n_chunks;
+        ctx->stats.recipe_bytes += 4 + (uint64_t)S.h_bst[b].n_chunks * ctx->H;
     }
     ctx->stats.open_bytes = 0;
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) ctx->stats.open_bytes += ctx->h_alloc.cur[t];
-    // recipes (SET longToBytes(id,4) -> BE32 size | digests)
+    // recipes (SET longToBytes(id,4) -> BE32 size | digests); the slot is not reused before
+    // this returns (submit waits for it), so its digests are still intact
     for (int b = 0; b < nblocks; b++) {
-        const uint32_t key = (uint32_t)(block_ids ? block_ids[b] : 0);
-        ctx->lengths[key] = (int64_t)len[b];
+        const uint32_t key = (uint32_t)S.ids[b];
+        const uint64_t ln = S.lens[b];
+        ctx->lengths[key] = (int64_t)ln;
         if (c.keep_recipes) {
-            const int64_t n = ctx->h_bst[b].n_chunks;
+            const int64_t n = S.h_bst[b].n_chunks;
             std::vector<uint8_t> r(4 + n * ctx->H);
-            r[0] = (uint8_t)(len[b] >> 24); r[1] = (uint8_t)(len[b] >> 16);
-            r[2] = (uint8_t)(len[b] >> 8); r[3] = (uint8_t)len[b];
+            r[0] = (uint8_t)(ln >> 24); r[1] = (uint8_t)(ln >> 16); r[2] = (uint8_t)(ln >> 8); r[3] = (uint8_t)ln;
             std::vector<uint32_t> dw((size_t)n * ctx->HW);
-            HIPCK(hipMemcpy(dw.data(), ctx->d_dig + (size_t)b * ctx->cap_blk * ctx->HW, dw.size() * 4,
+            HIPCK(hipMemcpy(dw.data(), S.d_dig + (size_t)b * ctx->cap_blk * ctx->HW, dw.size() * 4,
                             hipMemcpyDeviceToHost));
             std::memcpy(r.data() + 4, dw.data(), (size_t)n * ctx->H);
             ctx->recipes[key] = std::move(r);
@@ -450,31 +588,43 @@ static int finish_batch(hdrf_ctx *ctx, int32_t nblocks, const uint64_t *len, con
     return 0;
 }
 
+
+// Complete the oldest batch in flight (its slot is reusable once this returns).
+static int wait_one(hdrf_ctx *ctx)
+{
+    if (ctx->nwait >= ctx->nsub) return set_err(ctx, HDRF_E_INVAL, "no batch in flight");
+    const int si = (int)(ctx->nwait % kSlots);
+    Slot &S = ctx->sl[si];
+    ctx->nwait++;
+    S.pending = false;
+    HIPCK(hipEventSynchronize(S.back_done));
+    return complete_slot(ctx, si, true);
+}
+
+extern "C" int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                                 const uint64_t *readable, const uint64_t *block_ids)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
+    return submit(ctx, nblocks, dev_data, len, readable, block_ids);
+}
+
+extern "C" int hdrf_wait_batch(hdrf_ctx *ctx)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    return wait_one(ctx);
+}
+
+extern "C" int hdrf_batch_nblocks(hdrf_ctx *ctx) { return ctx ? ctx->last_nblocks : HDRF_E_INVAL; }
+
 extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                                  const uint64_t *readable, const uint64_t *block_ids)
 {
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
-    const hdrf_cfg &c = ctx->cfg;
-    int max_nseg = 1;
-    if (int rc = prepare_blocks(ctx, nblocks, dev_data, len, readable, &max_nseg)) return rc;
-    const uint32_t cur = ++ctx->batch;
-    hipStream_t st = ctx->st;
-    HIPCK(hipMemsetAsync(ctx->d_nclosed, 0, sizeof(uint32_t), st));
-    Marker mk;
-    mk.ev = ctx->timing ? ctx->ev : nullptr;
-    HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
-                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
-    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_mid, ctx->d_dig,
-                     ctx->d_queue, st, &mk));
-    HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_tab, c.index_log2,
-                       cur, tag_mask(ctx), ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, ctx->d_flags,
-                       ctx->d_tilesum, ctx->ntiles, ctx->d_err, st, &mk));
-    const StoreParams P = store_params(ctx, nblocks);
-    HIPCK(launch_store(P, ctx->d_blocks, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre,
-                       ctx->d_store, ctx->d_pre, ctx->d_alloc, ctx->d_rstate, ctx->d_ev, ctx->d_closed, ctx->d_nclosed,
-                       ctx->d_slot, ctx->d_tab, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, ctx->d_err, st, &mk));
-    return finish_batch(ctx, nblocks, len, block_ids, kStages + 1);
+    if (int rc = drain(ctx)) return rc;
+    if (int rc = submit(ctx, nblocks, dev_data, len, readable, block_ids)) return rc;
+    return wait_one(ctx);
 }
 
 // ---- node-global index phases (include/hdrf.h, gx.hip) ------------------------------------
@@ -513,42 +663,47 @@ extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *cons
 {
     if (ctx && ctx->gx_phase == 6) ctx->gx_phase = 0;
     if (int rc = gx_check(ctx, 0)) return rc;
+    if (int rc = drain(ctx)) return rc;
+    Slot &S = ctx->sl[0];                              // the node-global phases use slot 0, stream A
     if (!x1_send || !send_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     const hdrf_cfg &c = ctx->cfg;
     int max_nseg = 1;
-    if (int rc = prepare_blocks(ctx, nblocks, dev_data, len, readable, &max_nseg)) return rc;
+    if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable, &max_nseg)) return rc;
     ++ctx->batch;
     hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
     Marker mk;
-    mk.ev = ctx->timing ? ctx->ev : nullptr;
-    HIPCK(launch_chunking(ctx->d_blocks, nblocks, max_nseg, c.window, c.max_chunk, ctx->d_spec, ctx->spec_cap,
-                          ctx->d_meta, ctx->d_sync, ctx->d_plan, ctx->d_bst, ctx->d_off, ctx->cap_blk, ctx->d_err, st, &mk));
-    HIPCK(launch_sha(c.hasher, ctx->d_blocks, nblocks, ctx->d_off, ctx->d_bst, ctx->cap_blk, ctx->d_mid, ctx->d_dig,
-                     ctx->d_queue, st, &mk));
+    mk.ev = ctx->timing ? S.evB : nullptr;             // 8 markers: walk .. slow+decide, end
+    HIPCK(launch_chunking(S.d_blocks, nblocks, max_nseg, c.window, c.max_chunk, S.d_spec, ctx->spec_cap,
+                          S.d_meta, S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, st, &mk));
+    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
+                     S.d_queue, st, &mk));
     // local aggregation: a fresh scratch table, every entry "created" in batch 1
     HIPCK(hipMemsetAsync(ctx->d_scratch, 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
-    HIPCK(launch_index(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->d_off, ctx->d_dig, ctx->d_scratch,
-                       ctx->scratch_log2, 1u, tag_mask(ctx), ctx->d_slot, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap,
-                       ctx->d_flags, ctx->d_tilesum, ctx->ntiles, ctx->d_err, st, &mk));
-    HIPCK(launch_gx_emit(c.hasher, ctx->d_bst, nblocks, ctx->cap_blk, ctx->ntiles, ctx->d_dig, ctx->d_scratch,
-                         ctx->d_slot, ctx->d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gx_counts, ctx->d_err, st));
+    HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_scratch,
+                       ctx->scratch_log2, 1u, tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap,
+                       S.d_flags, S.d_tilesum, ctx->ntiles, S.d_err, st, &mk));
+    HIPCK(launch_gx_emit(c.hasher, S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, S.d_dig, ctx->d_scratch,
+                         S.d_slot, S.d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gx_counts, S.d_err, st));
     mk.mark(st);
     std::vector<unsigned long long> cnt(ctx->G);
     int herr = 0;
     HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(&herr, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    accumulate_stages(ctx, mk.next);
+    if (ctx->timing)
+        for (int i = 0; i + 1 < mk.next && i < 7; i++) ctx->stage_ms[i] += elapsed(S.evB[i], S.evB[i + 1]);
     if (herr) {
-        HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), st));
-        return set_err(ctx, herr & 22 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
-                       "device reported error flags " + std::to_string(herr));
+        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
+        HIPCK(hipStreamSynchronize(st));
+        return device_error(ctx, herr);
     }
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
     ctx->gx_nblocks = nblocks;
-    ctx->gx_lens.assign(len, len + nblocks);
-    ctx->gx_ids.assign(nblocks, 0);
-    if (block_ids) ctx->gx_ids.assign(block_ids, block_ids + nblocks);
+    S.nblocks = nblocks;
+    S.lens.assign(len, len + nblocks);
+    S.ids.assign(nblocks, 0);
+    if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
     ctx->gx_phase = 1;
     return 0;
 }
@@ -556,6 +711,7 @@ extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *cons
 extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send)
 {
     if (int rc = gx_check(ctx, 1)) return rc;
+    Slot &S = ctx->sl[0];
     if (!x1_recv || !recv_counts || !x2_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     for (int s = 0; s < ctx->G; s++)
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
@@ -563,14 +719,14 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
     HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
     HIPCK(launch_gx_owner(ctx->cfg.hasher, x1_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap,
                           ctx->G, ctx->d_tab, ctx->cfg.index_log2, ctx->batch, tag_mask(ctx), ctx->d_oslot,
-                          ctx->d_oflags, ctx->d_coll, ctx->d_ncoll, ctx->coll_cap, x2_send, ctx->d_err, st));
+                          ctx->d_oflags, S.d_coll, S.d_ncoll, ctx->coll_cap, x2_send, S.d_err, st));
     int herr = 0;
-    HIPCK(hipMemcpyAsync(&herr, ctx->d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     if (herr) {
-        HIPCK(hipMemsetAsync(ctx->d_err, 0, sizeof(int), st));
-        return set_err(ctx, herr & 22 ? HDRF_E_CAPACITY : HDRF_E_DEVICE,
-                       "device reported error flags " + std::to_string(herr));
+        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
+        HIPCK(hipStreamSynchronize(st));
+        return device_error(ctx, herr);
     }
     ctx->gx_phase = 2;
     return 0;
@@ -579,14 +735,15 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
 extern "C" int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv)
 {
     if (int rc = gx_check(ctx, 2)) return rc;
+    Slot &S = ctx->sl[0];
     if (!x2_recv) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     hipStream_t st = ctx->st;
     const int nb = ctx->gx_nblocks;
-    HIPCK(launch_gx_decide(ctx->d_bst, nb, ctx->cap_blk, ctx->ntiles, ctx->d_off, ctx->d_scratch, ctx->d_slot, x2_recv,
-                           ctx->d_flags, ctx->d_tilesum, st));
+    HIPCK(launch_gx_decide(S.d_bst, nb, ctx->cap_blk, ctx->ntiles, S.d_off, ctx->d_scratch, S.d_slot, x2_recv,
+                           S.d_flags, S.d_tilesum, st));
     const StoreParams P = store_params(ctx, nb);
-    HIPCK(launch_store_scan(P, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_tilesum, ctx->d_tilepre, ctx->d_store,
-                            ctx->d_pre, st));
+    HIPCK(launch_store_scan(P, S.d_bst, S.d_off, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store,
+                            S.d_pre, st));
     ctx->gx_x2 = x2_recv;
     ctx->gx_phase = 3;
     return 0;
@@ -595,12 +752,13 @@ extern "C" int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv)
 extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out)
 {
     if (int rc = gx_check(ctx, 3)) return rc;
+    Slot &S = ctx->sl[0];
     hipStream_t st = ctx->st;
     if (alloc_in) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_in, sizeof(AllocState), hipMemcpyHostToDevice, st));
-    HIPCK(hipMemsetAsync(ctx->d_nclosed, 0, sizeof(uint32_t), st));
+    HIPCK(hipMemsetAsync(S.d_nclosed, 0, sizeof(uint32_t), st));
     const StoreParams P = store_params(ctx, ctx->gx_nblocks);
-    HIPCK(launch_store_flush(P, ctx->d_bst, ctx->d_store, ctx->d_pre, ctx->d_alloc, ctx->d_rstate, ctx->d_ev,
-                             ctx->d_closed, ctx->d_nclosed, ctx->d_err, st));
+    HIPCK(launch_store_flush(P, S.d_bst, S.d_store, S.d_pre, ctx->d_alloc, S.d_rstate, S.d_ev,
+                             S.d_closed, S.d_nclosed, S.d_err, st));
     AllocState a{};
     HIPCK(hipMemcpyAsync(&a, ctx->d_alloc, sizeof a, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
@@ -615,19 +773,27 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
 extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts)
 {
     if (int rc = gx_check(ctx, 4)) return rc;
+    Slot &S = ctx->sl[0];
     if (!x3_send || !send_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     hipStream_t st = ctx->st;
     const int nb = ctx->gx_nblocks;
     const StoreParams P = store_params(ctx, nb);
     GxPlace gx;
     gx.x2 = ctx->gx_x2; gx.x3 = x3_send; gx.cap = ctx->gx_cap; gx.counts = ctx->d_gx_counts; gx.G = ctx->G;
-    HIPCK(launch_store_place(P, ctx->d_blocks, ctx->d_bst, ctx->d_off, ctx->d_flags, ctx->d_pre, ctx->d_rstate,
-                             ctx->d_ev, ctx->d_slot, ctx->d_scratch, ctx->d_arena, ctx->d_pcid, ctx->d_ppos, gx, st));
+    HIPCK(launch_store_place(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_pre, S.d_rstate, S.d_ev, S.d_slot,
+                             ctx->d_scratch, ctx->d_arena, S.d_pcid, S.d_ppos, gx, st));
     // the node's allocator after the last rank (the next batch and the "blockID" view start here)
     if (alloc_final) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_final, sizeof(AllocState), hipMemcpyHostToDevice, st));
     std::vector<unsigned long long> cnt(ctx->G);
     HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
-    if (int rc = finish_batch(ctx, nb, ctx->gx_lens.data(), ctx->gx_ids.data(), 0)) return rc;
+    HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nb, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nb, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(S.h_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (int rc = complete_slot(ctx, 0, false)) return rc;
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
     ctx->gx_phase = 5;
     return 0;
@@ -636,6 +802,7 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
 extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts)
 {
     if (int rc = gx_check(ctx, 5)) return rc;
+    
     if (!x3_recv || !recv_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     for (int s = 0; s < ctx->G; s++)
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
@@ -657,35 +824,39 @@ static int check_b(hdrf_ctx *ctx, int32_t b)
 extern "C" int hdrf_batch_info(hdrf_ctx *ctx, int32_t b, int64_t *n_chunks, int64_t *store_size)
 {
     if (int rc = check_b(ctx, b)) return rc;
-    if (n_chunks) *n_chunks = ctx->h_bst[b].n_chunks;
-    if (store_size) *store_size = (int64_t)ctx->h_store[b];
+    const Slot &R = ctx->sl[ctx->res];
+    if (n_chunks) *n_chunks = R.h_bst[b].n_chunks;
+    if (store_size) *store_size = (int64_t)R.h_store[b];
     return 0;
 }
 
 extern "C" int hdrf_batch_offsets(hdrf_ctx *ctx, int32_t b, uint32_t *out, int64_t cap)
 {
     if (int rc = check_b(ctx, b)) return rc;
-    const int64_t n = ctx->h_bst[b].n_chunks;
+    const Slot &R = ctx->sl[ctx->res];
+    const int64_t n = R.h_bst[b].n_chunks;
     if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "offsets capacity");
-    HIPCK(hipMemcpy(out, ctx->d_off + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(out, R.d_off + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
     return 0;
 }
 
 extern "C" int hdrf_batch_digests(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap_bytes)
 {
     if (int rc = check_b(ctx, b)) return rc;
-    const int64_t n = ctx->h_bst[b].n_chunks;
+    const Slot &R = ctx->sl[ctx->res];
+    const int64_t n = R.h_bst[b].n_chunks;
     if (cap_bytes < n * ctx->H) return set_err(ctx, HDRF_E_CAPACITY, "digest capacity");
-    HIPCK(hipMemcpy(out, ctx->d_dig + (size_t)b * ctx->cap_blk * ctx->HW, n * ctx->H, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(out, R.d_dig + (size_t)b * ctx->cap_blk * ctx->HW, n * ctx->H, hipMemcpyDeviceToHost));
     return 0;
 }
 
 extern "C" int hdrf_batch_is_new(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap)
 {
     if (int rc = check_b(ctx, b)) return rc;
-    const int64_t n = ctx->h_bst[b].n_chunks;
+    const Slot &R = ctx->sl[ctx->res];
+    const int64_t n = R.h_bst[b].n_chunks;
     if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "is_new capacity");
-    HIPCK(hipMemcpy(out, ctx->d_flags + (size_t)b * ctx->cap_blk, n, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(out, R.d_flags + (size_t)b * ctx->cap_blk, n, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; i++) out[i] &= 1;
     return 0;
 }
@@ -693,12 +864,13 @@ extern "C" int hdrf_batch_is_new(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t
 extern "C" int hdrf_batch_placement(hdrf_ctx *ctx, int32_t b, uint32_t *cid, uint32_t *pos, int64_t cap)
 {
     if (int rc = check_b(ctx, b)) return rc;
-    const int64_t n = ctx->h_bst[b].n_chunks;
+    const Slot &R = ctx->sl[ctx->res];
+    const int64_t n = R.h_bst[b].n_chunks;
     if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "placement capacity");
     std::vector<uint8_t> f(n);
-    HIPCK(hipMemcpy(f.data(), ctx->d_flags + (size_t)b * ctx->cap_blk, n, hipMemcpyDeviceToHost));
-    if (cid) HIPCK(hipMemcpy(cid, ctx->d_pcid + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
-    if (pos) HIPCK(hipMemcpy(pos, ctx->d_ppos + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(f.data(), R.d_flags + (size_t)b * ctx->cap_blk, n, hipMemcpyDeviceToHost));
+    if (cid) HIPCK(hipMemcpy(cid, R.d_pcid + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
+    if (pos) HIPCK(hipMemcpy(pos, R.d_ppos + (size_t)b * ctx->cap_blk, n * 4, hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < n; i++)
         if (!(f[i] & 1)) {
             if (cid) cid[i] = 0;
@@ -778,7 +950,7 @@ extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out1
     if (tag == 0) tag = 1;
     const uint64_t mask = (1ull << ctx->cfg.index_log2) - 1;
     uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - ctx->cfg.index_log2);
-    HIPCK(hipStreamSynchronize(ctx->st));
+    if (int rc = drain(ctx)) return rc;
     for (uint64_t probe = 0; probe <= mask; probe++) {
         IndexEntry e;
         HIPCK(hipMemcpy(&e, ctx->d_tab + h, sizeof e, hipMemcpyDeviceToHost));
@@ -797,7 +969,7 @@ extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out1
 static int fetch_table(hdrf_ctx *ctx, std::vector<IndexEntry> &tab)
 {
     tab.resize((size_t)1 << ctx->cfg.index_log2);
-    HIPCK(hipStreamSynchronize(ctx->st));
+    if (int rc = drain(ctx)) return rc;
     HIPCK(hipMemcpy(tab.data(), ctx->d_tab, tab.size() * sizeof(IndexEntry), hipMemcpyDeviceToHost));
     return 0;
 }
@@ -881,7 +1053,7 @@ extern "C" int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out,
     const int64_t n = lz ? it->second.clen : it->second.len;
     if (!out) return n;
     if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "container capacity");
-    HIPCK(hipStreamSynchronize(ctx->st));
+    if (int rc = drain(ctx)) return rc;
     const uint8_t *src = lz ? ctx->d_carena + (size_t)it->second.slot * ctx->cslot
                             : ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max;
     if (n) HIPCK(hipMemcpy(out, src, n, hipMemcpyDeviceToHost));
@@ -899,7 +1071,7 @@ extern "C" int hdrf_dev_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
 extern "C" int hdrf_dev_free(hdrf_ctx *ctx, void *p)
 {
     if (!ctx) return HDRF_E_INVAL;
-    HIPCK(hipStreamSynchronize(ctx->st));
+    if (int rc = drain(ctx)) return rc;
     HIPCK(hipFree(p));
     return 0;
 }
@@ -916,6 +1088,7 @@ extern "C" int hdrf_memcpy_d2h(hdrf_ctx *ctx, void *dst, const void *src, uint64
 {
     if (!ctx) return HDRF_E_INVAL;
     HIPCK(hipStreamSynchronize(ctx->st));
+    HIPCK(hipStreamSynchronize(ctx->stB));
     HIPCK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return 0;
 }
@@ -923,8 +1096,7 @@ extern "C" int hdrf_memcpy_d2h(hdrf_ctx *ctx, void *dst, const void *src, uint64
 extern "C" int hdrf_synchronize(hdrf_ctx *ctx)
 {
     if (!ctx) return HDRF_E_INVAL;
-    HIPCK(hipStreamSynchronize(ctx->st));
-    return 0;
+    return drain(ctx);                                 // completes every batch in flight
 }
 
 extern "C" int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,

@@ -79,8 +79,9 @@ hipError_t launch_gx_commit(const uint32_t *x3, const int64_t *counts, int64_t m
                             IndexEntry *tab, hipStream_t st);
 // compression stage (lz4.hip): closed containers -> Lz4Codec files in the compressed arena
 uint64_t lz4_slot_bytes(uint32_t cmax);
-hipError_t launch_lz4(const ClosedRec *closed, int nclosed, uint32_t cmax, const uint8_t *arena, uint8_t *carena,
-                      uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len, hipStream_t st);
+hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
+                      const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
+                      hipStream_t st);
 hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
                          uint64_t seed, int mixed, hipStream_t st);
 

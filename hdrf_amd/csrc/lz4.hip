@@ -222,12 +222,14 @@ last_literals:
 }
 
 // grid (nseg_max, nclosed) x 64 threads: segment s of closed container c
-__global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed, const uint8_t *__restrict__ arena,
+__global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed,
+                                                     const uint32_t *__restrict__ nclosed, const uint8_t *__restrict__ arena,
                                                      uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
                                                      uint32_t *__restrict__ seg_clen, int nseg_max)
 {
     __shared__ uint32_t tab[4096];
     const int c = blockIdx.y, s = blockIdx.x;
+    if ((uint32_t)c >= *nclosed) return;                   // grid sized for closed_cap
     const ClosedRec r = closed[c];
     const int64_t off = (int64_t)s * kLzMaxIn;
     if (off >= (int64_t)r.len) return;
@@ -244,11 +246,13 @@ __device__ __forceinline__ void put_be32(uint8_t *p, uint32_t v)
 }
 
 // grid nclosed x 256 threads: frame the segments in place, [BE32 len] ([BE32 clen] block)* [BE32 0]
-__global__ void __launch_bounds__(256) lz4_pack_kernel(const ClosedRec *__restrict__ closed, uint8_t *__restrict__ carena,
+__global__ void __launch_bounds__(256) lz4_pack_kernel(const ClosedRec *__restrict__ closed,
+                                                       const uint32_t *__restrict__ nclosed, uint8_t *__restrict__ carena,
                                                        uint64_t cslot, const uint32_t *__restrict__ seg_clen, int nseg_max,
                                                        uint32_t *__restrict__ file_len)
 {
     const int c = blockIdx.x, t = threadIdx.x;
+    if ((uint32_t)c >= *nclosed) return;
     const ClosedRec r = closed[c];
     uint8_t *base = carena + (size_t)r.slot * cslot;
     const int nseg = r.len ? (int)((r.len + kLzMaxIn - 1) / kLzMaxIn) : 0;
@@ -289,15 +293,17 @@ uint64_t lz4_slot_bytes(uint32_t cmax)
     return 16 + nseg * (uint64_t)kLzSegStride;
 }
 
-hipError_t launch_lz4(const ClosedRec *closed, int nclosed, uint32_t cmax, const uint8_t *arena, uint8_t *carena,
-                      uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len, hipStream_t st)
+hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
+                      const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
+                      hipStream_t st)
 {
-    if (nclosed <= 0) return hipSuccess;
+    // grid covers closed_cap containers; workgroups past the device-side count exit at once, so
+    // the compression stays in stream order with the batch (no host round trip)
     const int nseg_max = (int)((cmax + kLzMaxIn - 1) / kLzMaxIn);
-    hipLaunchKernelGGL(lz4_seg_kernel, dim3(nseg_max, nclosed), dim3(64), 0, st, closed, arena, (uint64_t)cmax, carena,
-                       cslot, seg_clen, nseg_max);
-    hipLaunchKernelGGL(lz4_pack_kernel, dim3(nclosed), dim3(256), 0, st, closed, carena, cslot, seg_clen, nseg_max,
-                       file_len);
+    hipLaunchKernelGGL(lz4_seg_kernel, dim3(nseg_max, closed_cap), dim3(64), 0, st, closed, nclosed, arena,
+                       (uint64_t)cmax, carena, cslot, seg_clen, nseg_max);
+    hipLaunchKernelGGL(lz4_pack_kernel, dim3(closed_cap), dim3(256), 0, st, closed, nclosed, carena, cslot, seg_clen,
+                       nseg_max, file_len);
     return hipGetLastError();
 }
 

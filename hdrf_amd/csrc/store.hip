@@ -170,6 +170,9 @@ __global__ void __launch_bounds__(256) flush_kernel(StoreParams P, const BlockSt
                 rs.nflush++;
             }
             cur = (uint32_t)((int64_t)S - cs);
+            // the ring of range t must hold every container this batch closes plus the open one,
+            // or a closed container's bytes would be overwritten before the host sees them
+            if (nev >= (int)(P.nslots / 4) - 1 && l == 0) atomicOr(err, 32);
             pos = (uint32_t)((int64_t)S - (cs > 0 ? cs : 0));      // lastBlockID[t+4] (:808)
         }
         if (l == 0) rstate[(size_t)b * 4 + t] = rs;

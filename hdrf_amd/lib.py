@@ -26,7 +26,8 @@ EXPORTS = [
     "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
-    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats",
+    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
+    "hdrf_batch_nblocks",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -108,6 +109,9 @@ def load():
         "hdrf_digest_len": (ctypes.c_int, [_vp]),
         "hdrf_reduce_block": (ctypes.c_int, [_vp, ctypes.c_uint64, _u8p, ctypes.c_uint64, ctypes.POINTER(BlockResult)]),
         "hdrf_reduce_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
+        "hdrf_submit_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
+        "hdrf_wait_batch": (ctypes.c_int, [_vp]),
+        "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
         "hdrf_batch_info": (ctypes.c_int, [_vp, ctypes.c_int32, _i64p, _i64p]),
         "hdrf_batch_offsets": (ctypes.c_int, [_vp, ctypes.c_int32, _u32p, ctypes.c_int64]),
         "hdrf_batch_digests": (ctypes.c_int, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64]),
@@ -229,6 +233,22 @@ class Context:
         rd = np.ascontiguousarray(readable, np.uint64)
         ids = np.ascontiguousarray(block_ids, np.uint64)
         self._ck(self.L.hdrf_reduce_batch(self._h, n, ptrs, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p)))
+
+    def submit_batch(self, dev_ptrs, lens, readable, block_ids):
+        """Enqueue a batch (two in flight at most); complete it with wait_batch() in order."""
+        n = len(dev_ptrs)
+        ptrs = (_vp * n)(*dev_ptrs)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        rd = np.ascontiguousarray(readable, np.uint64)
+        ids = np.ascontiguousarray(block_ids, np.uint64)
+        self._ck(self.L.hdrf_submit_batch(self._h, n, ptrs, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p)))
+
+    def wait_batch(self):
+        self._ck(self.L.hdrf_wait_batch(self._h))
+
+    def last_nblocks(self):
+        """Blocks of the batch hdrf_batch_* currently report."""
+        return self._ck(self.L.hdrf_batch_nblocks(self._h))
 
     def batch_info(self, b):
         n, s = ctypes.c_int64(), ctypes.c_int64()

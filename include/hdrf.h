@@ -86,6 +86,18 @@ int hdrf_reduce_block(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *data, uin
 int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                       const uint64_t *readable, const uint64_t *block_ids);
 
+/* Pipelined form of hdrf_reduce_batch: hdrf_submit_batch enqueues the batch (chunking + SHA on one
+ * HIP stream, index + store on a second one, in block order) and returns; hdrf_wait_batch
+ * completes the OLDEST submitted batch and makes it the one hdrf_batch_* report.  At most two
+ * batches are in flight (a third submit first completes the oldest); the device buffers of a
+ * batch must stay valid until it is completed.  Chunking and hashing of batch k+1 overlap the
+ * index/store stage of batch k.  Views (index, containers, allocator) complete all batches first. */
+int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                      const uint64_t *readable, const uint64_t *block_ids);
+int hdrf_wait_batch(hdrf_ctx *ctx);
+/* Number of blocks of the batch hdrf_batch_* report (the last completed one). */
+int hdrf_batch_nblocks(hdrf_ctx *ctx);
+
 int hdrf_batch_info(hdrf_ctx *ctx, int32_t b, int64_t *n_chunks, int64_t *store_size);
 int hdrf_batch_offsets(hdrf_ctx *ctx, int32_t b, uint32_t *out, int64_t cap);
 int hdrf_batch_digests(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap_bytes);
@@ -145,7 +157,8 @@ typedef struct {
 } hdrf_stats;
 int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out);
 
-/* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis). */
+/* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis); completes
+ * the batches in flight first. */
 int hdrf_reset(hdrf_ctx *ctx);
 
 /* ---- Node-global index over n_ranks GPUs (BASELINE config 3) -------------------

@@ -215,3 +215,44 @@ def test_device_corpus_matches_host_and_reduces(mixed):
         assert st["closed_containers"] > 0 and st["closed_file_bytes"] < st["closed_raw_bytes"]
     ctx.dev_free(dev)
     ctx.close()
+
+
+def test_pipelined_submit_wait_matches_sequential_oracle():
+    """hdrf_submit_batch / hdrf_wait_batch: two batches in flight (chunking + SHA of batch k+1 on
+    one stream while batch k is indexed and stored on the other) give the same results as the
+    sequential oracle, including when a third submit completes the oldest batch implicitly."""
+    nb, spb, seg = 14, 8, 1 << 18
+    roots = corpus_roots(77, 500000, nb, spb)
+    blocks = [corpus_block_host(77, roots, b, spb, seg) for b in range(nb)]
+    ctx = Context(container_max=1 << 20, **SMALL)
+    ora = Oracle(max_size=1 << 20)
+    size = spb * seg
+    dev = ctx.dev_alloc(size * nb + 4096)
+    ctx.h2d(dev, np.concatenate(blocks))
+    groups = [list(range(s, min(s + 3, nb))) for s in range(0, nb, 3)]
+    ids = [900 + b for b in range(nb)]
+
+    def check(group):
+        assert ctx.last_nblocks() == len(group)
+        for i, b in enumerate(group):
+            compare_block(ctx.batch_result(i), ora.reduce(blocks[b], ids[b]), tag=f"pipelined block {b}")
+
+    pending = []
+    for gi, g in enumerate(groups):
+        if len(pending) == 2:                # this submit completes the oldest batch itself
+            for b in pending.pop(0):
+                ora.reduce(blocks[b], ids[b])
+        ctx.submit_batch([dev + b * size for b in g], [size] * len(g), [size * (nb - b) + 4096 for b in g],
+                         [ids[b] for b in g])
+        pending.append(g)
+        if gi % 3 == 1:                      # sometimes let a third submit complete the oldest
+            continue
+        while len(pending) > 1:
+            ctx.wait_batch()
+            check(pending.pop(0))
+    while pending:
+        ctx.wait_batch()
+        check(pending.pop(0))
+    compare_state(ctx, ora, ids)
+    ctx.dev_free(dev)
+    ctx.close()
