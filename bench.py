@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--hasher", type=int, default=0)
     ap.add_argument("--cpu-sample-blocks", type=int, default=24)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="one batch at a time (no stream overlap): clean per-kernel stage times")
     ap.add_argument("--arena-slots", type=int, default=512,
                     help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers")
     ap.add_argument("--workload", choices=["config2", "config4"], default="config2",
@@ -140,7 +142,11 @@ def main():
                 n_chunks[j], store[j] = ctx.batch_info(i)
                 j += 1
 
-        if node is None:
+        if node is None and a.serial:
+            for ptrs, lens, rd, ids in batches:
+                ctx.reduce_batch(ptrs, lens, rd, ids)
+                collect()
+        elif node is None:
             # pipelined: chunking + SHA of batch k+1 overlap the index/store stage of batch k
             for k, (ptrs, lens, rd, ids) in enumerate(batches):
                 ctx.submit_batch(ptrs, lens, rd, ids)

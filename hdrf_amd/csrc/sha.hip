@@ -13,7 +13,9 @@
 //              digest store.
 // Each 64-B block is fetched as 17 dword-aligned dwords (4 x dwordx4 + 1) and realigned +
 // byte-swapped with one v_perm_b32 per word.  Rotations are v_alignbit_b32, 3-way xor is
-// v_bitop3_b32 (gfx950), Ch/Maj lower to v_bfi/v_bitop3.
+// v_bitop3_b32 (gfx950), and so are Ch and Maj (one v_bitop3 each: 618 VALU per SHA-1 block).
+// Measured against tools/sha_peak.hip (the same compression on register-resident data, no memory):
+// a software-pipelined prefetch variant and a two-chains-per-lane variant were both slower.
 #include <algorithm>
 #include <cstdlib>
 
@@ -26,6 +28,9 @@ typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, 32 - n); }
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+// one v_bitop3_b32 each (truth tables over src0 = 0xF0, src1 = 0xCC, src2 = 0xAA)
+__device__ __forceinline__ uint32_t ch(uint32_t x, uint32_t y, uint32_t z) { return __builtin_amdgcn_bitop3_b32(x, y, z, 0xCA); }
+__device__ __forceinline__ uint32_t maj(uint32_t x, uint32_t y, uint32_t z) { return __builtin_amdgcn_bitop3_b32(x, y, z, 0xE8); }
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // symmetric truth table: a ^ b ^ c
@@ -38,9 +43,9 @@ __device__ __forceinline__ void sha1_compress(uint32_t st[5], uint32_t w[16])
     for (int i = 0; i < 80; i++) {
         if (i >= 16) w[i & 15] = rotl(xor3(w[(i - 3) & 15], w[(i - 8) & 15], w[(i - 14) & 15]) ^ w[i & 15], 1);
         uint32_t f, k;
-        if (i < 20)      { f = bfi(b, c, d);      k = 0x5A827999u; }
+        if (i < 20)      { f = ch(b, c, d);       k = 0x5A827999u; }
         else if (i < 40) { f = xor3(b, c, d);     k = 0x6ED9EBA1u; }
-        else if (i < 60) { f = bfi(b ^ c, d, c);  k = 0x8F1BBCDCu; }
+        else if (i < 60) { f = maj(b, c, d);      k = 0x8F1BBCDCu; }
         else             { f = xor3(b, c, d);     k = 0xCA62C1D6u; }
         const uint32_t t = rotl(a, 5) + f + e + k + w[i & 15];
         e = d; d = c; c = rotl(b, 30); b = a; a = t;
@@ -70,9 +75,9 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16])
             w[i & 15] = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
         }
         const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
-        const uint32_t t1 = h + S1 + bfi(e, f, g) + kK256[i] + w[i & 15];
+        const uint32_t t1 = h + S1 + ch(e, f, g) + kK256[i] + w[i & 15];
         const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
-        const uint32_t t2 = S0 + bfi(a ^ b, c, b);
+        const uint32_t t2 = S0 + maj(a, b, c);
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
