@@ -5,7 +5,7 @@ import glob
 import sys
 
 d = collections.defaultdict(list)
-for f in glob.glob(sys.argv[1] + "/*/run_counter_collection.csv"):
+for f in glob.glob(sys.argv[1] + "/*/run_counter_collection.csv") + glob.glob(sys.argv[1] + "/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("hdrf::", "")
         if "rocclr" in k:
