@@ -96,6 +96,8 @@ struct hdrf_ctx {
     AllocState *d_alloc = nullptr;
     uint8_t *d_stage = nullptr;
     uint64_t stage_cap = 0;
+    uint8_t *d_rd = nullptr;                     // reconstruction scratch (grows)
+    uint64_t rd_cap = 0;
     // host state
     uint32_t batch = 0;
     int have_alloc = 0;
@@ -223,7 +225,7 @@ static void free_slot(Slot &S)
 static void free_all(hdrf_ctx *ctx)
 {
     for (auto &S : ctx->sl) free_slot(S);
-    void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_scratch, ctx->d_gx_counts,
+    void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch, ctx->d_gx_counts,
                     ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags, ctx->d_carena};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
@@ -1058,6 +1060,74 @@ extern "C" int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out,
                             : ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max;
     if (n) HIPCK(hipMemcpy(out, src, n, hipMemcpyDeviceToHost));
     return n;
+}
+
+// ---- read side: DataConstructor (DN/DataConstructor.java:73-250, 360-531) --------------------
+static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need)
+{
+    if (*cap >= need) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HIPCK(hipMalloc((void **)p, need));
+    *cap = need;
+    return 0;
+}
+
+extern "C" int64_t hdrf_reconstruct(hdrf_ctx *ctx, const uint8_t *recipe, int64_t recipe_len, uint8_t *dev_out,
+                                    int64_t cap)
+{
+    if (!ctx || !recipe || recipe_len < 4) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "reconstruction on node-global contexts: not yet");
+    if (int rc = drain(ctx)) return rc;
+    const int64_t size = ((int64_t)recipe[0] << 24) | (recipe[1] << 16) | (recipe[2] << 8) | recipe[3];
+    const int64_t n = recipe_len / ctx->H;             // t1data.length / hash_length (:223)
+    if (size > cap || (size && !dev_out)) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
+    if (n == 0) return size == 0 ? 0 : set_err(ctx, HDRF_E_DEVICE, "recipe without digests");
+    // resident containers, sorted by id (std::map order)
+    std::vector<uint32_t> map;
+    for (auto &kv : ctx->containers) map.push_back(kv.first);
+    for (auto &kv : ctx->containers) map.push_back(kv.second.slot);
+    const int ncont = (int)ctx->containers.size();
+    const uint64_t o_dig = 0, dig_b = (uint64_t)n * ctx->HW * 4;
+    const uint64_t o_ch = (dig_b + 255) & ~255ull, ch_b = (uint64_t)n * rd_chunk_bytes();
+    const uint64_t o_map = (o_ch + ch_b + 255) & ~255ull, map_b = (uint64_t)std::max(1, 2 * ncont) * 4;
+    const uint64_t o_tot = (o_map + map_b + 255) & ~255ull;
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_tot + 256)) return rc;
+    uint8_t *R = ctx->d_rd;
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(R + o_dig, recipe + 4, (size_t)n * ctx->H, hipMemcpyHostToDevice, st));
+    if (ncont) HIPCK(hipMemcpyAsync(R + o_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(R + o_tot, 0, 16, st));
+    const uint32_t *cids = (const uint32_t *)(R + o_map);
+    HIPCK(launch_reconstruct(ctx->cfg.hasher, (const uint32_t *)(R + o_dig), (int)n, ctx->d_tab, ctx->cfg.index_log2,
+                             tag_mask(ctx), cids, cids + ncont, ncont, R + o_ch, (uint64_t *)(R + o_tot), ctx->d_arena,
+                             ctx->cfg.container_max, dev_out, (int *)(R + o_tot + 8), st, false));
+    uint64_t tot[2] = {0, 0};
+    HIPCK(hipMemcpyAsync(tot, R + o_tot, 16, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if ((int)tot[1]) return set_err(ctx, HDRF_E_NOTFOUND, "a recipe digest or its container is not resident");
+    if ((int64_t)tot[0] != size) return set_err(ctx, HDRF_E_DEVICE, "chunk lengths do not add up to the recipe size");
+    HIPCK(launch_reconstruct(ctx->cfg.hasher, nullptr, (int)n, nullptr, 0, 0, nullptr, nullptr, 0, R + o_ch, nullptr,
+                             ctx->d_arena, ctx->cfg.container_max, dev_out, nullptr, st, true));
+    HIPCK(hipStreamSynchronize(st));
+    return size;
+}
+
+extern "C" int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (int rc = drain(ctx)) return rc;
+    auto it = ctx->recipes.find((uint32_t)block_id);     // GET longToBytes(blockId,4) (DN/BlockSender.java:292-328)
+    if (it == ctx->recipes.end()) return set_err(ctx, HDRF_E_NOTFOUND, "no recipe for this block (keep_recipes?)");
+    const std::vector<uint8_t> &rec = it->second;
+    const int64_t size = ((int64_t)rec[0] << 24) | (rec[1] << 16) | (rec[2] << 8) | rec[3];
+    if (!out || cap < size) return set_err(ctx, HDRF_E_CAPACITY, "needs " + std::to_string(size) + " bytes");
+    if (int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, (uint64_t)size + 4096)) return rc;
+    const int64_t got = hdrf_reconstruct(ctx, rec.data(), (int64_t)rec.size(), ctx->d_stage, size);
+    if (got < 0) return got;
+    if (got) HIPCK(hipMemcpy(out, ctx->d_stage, got, hipMemcpyDeviceToHost));
+    return got;
 }
 
 // ---- memory helpers, corpus, timing ------------------------------------------------------

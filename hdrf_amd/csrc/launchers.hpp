@@ -82,6 +82,12 @@ uint64_t lz4_slot_bytes(uint32_t cmax);
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
                       const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
                       hipStream_t st);
+// read side (read.hip): lookup + scan (gather = false), then the copy (gather = true)
+size_t rd_chunk_bytes();
+hipError_t launch_reconstruct(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
+                              unsigned long long tag_mask, const uint32_t *cids, const uint32_t *slots, int ncont,
+                              void *chunks, uint64_t *total, const uint8_t *arena, uint64_t cmax, uint8_t *out,
+                              int *err, hipStream_t st, bool gather);
 hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
                          uint64_t seed, int mixed, hipStream_t st);
 

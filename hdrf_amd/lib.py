@@ -27,7 +27,7 @@ EXPORTS = [
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
-    "hdrf_batch_nblocks",
+    "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -112,6 +112,8 @@ def load():
         "hdrf_submit_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
         "hdrf_wait_batch": (ctypes.c_int, [_vp]),
         "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
+        "hdrf_reconstruct": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
+        "hdrf_reconstruct_block": (ctypes.c_int64, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
         "hdrf_batch_info": (ctypes.c_int, [_vp, ctypes.c_int32, _i64p, _i64p]),
         "hdrf_batch_offsets": (ctypes.c_int, [_vp, ctypes.c_int32, _u32p, ctypes.c_int64]),
         "hdrf_batch_digests": (ctypes.c_int, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64]),
@@ -299,6 +301,17 @@ class Context:
         out = np.zeros(need, np.uint8)
         m = self._ck(self.L.hdrf_recipe_get(self._h, block_id, _p(out), need))
         return out[:m].tobytes()
+
+    def reconstruct_block(self, block_id):
+        """DataConstructor(blkID, recipe).data: the block rebuilt from the index + containers."""
+        n = self.block_length(block_id)
+        out = np.zeros(max(n, 1), np.uint8)
+        m = self._ck(self.L.hdrf_reconstruct_block(self._h, block_id, _p(out), n))
+        return out[:m]
+
+    def reconstruct(self, recipe, dev_out, cap):
+        r = np.frombuffer(bytes(recipe), np.uint8).copy()
+        return self._ck(self.L.hdrf_reconstruct(self._h, _p(r), r.size, dev_out, cap))
 
     def block_length(self, block_id):
         return self._ck(self.L.hdrf_block_length(self._h, block_id))

@@ -123,6 +123,15 @@ int64_t hdrf_block_length(hdrf_ctx *ctx, uint64_t block_id);
  * HDRF_E_NOTFOUND if it never existed or its arena slot was recycled. */
 int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t cap, int32_t *closed);
 
+/* Read side: DataConstructor(blkID, recipe).data (DN/DataConstructor.java:73-250, 360-531), the
+ * rebuild BlockSender serves on READ_BLOCK (DN/BlockSender.java:612-619).  Every recipe digest
+ * is looked up in the index; its chunk, container[start, stop), lands at the running sum of the
+ * chunk lengths.  hdrf_reconstruct writes to device memory and returns the block size;
+ * hdrf_reconstruct_block uses the context's stored recipe and copies to host memory.  The
+ * containers must still be resident (HDRF_E_NOTFOUND otherwise).  Single-node contexts. */
+int64_t hdrf_reconstruct(hdrf_ctx *ctx, const uint8_t *recipe, int64_t recipe_len, uint8_t *dev_out, int64_t cap);
+int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap);
+
 /* Device memory helpers for callers without their own allocator (bench, tests). */
 int hdrf_dev_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out);
 int hdrf_dev_free(hdrf_ctx *ctx, void *p);
