@@ -11,7 +11,7 @@ block in arrival order.
 """
 import abc
 
-from .lib import Context, HdrfError
+from .lib import Context
 
 
 class ReductionScheme(abc.ABC):
@@ -31,10 +31,11 @@ class ReductionScheme(abc.ABC):
 
 
 class HipReductionScheme(ReductionScheme):
-    """GPU-backed scheme: dedup-only (`compressor == 1`, DN/DataNode.java:438)."""
+    """GPU-backed scheme: `compressor` 1 (dedup) or 2 (dedup + Lz4Codec containers),
+    DN/DataNode.java:438."""
 
-    def __init__(self, hasher=0, device=0, **cfg):
-        self.ctx = Context(hasher=hasher, compressor=1, device=device, **cfg)
+    def __init__(self, hasher=0, device=0, compressor=1, **cfg):
+        self.ctx = Context(hasher=hasher, compressor=compressor, device=device, **cfg)
         self.last = None
 
     def reduce(self, block, block_id):
@@ -42,7 +43,7 @@ class HipReductionScheme(ReductionScheme):
         return self.last
 
     def reconstruct(self, block_id):
-        raise HdrfError(-6, "reconstruction (DataConstructor) is the next scheduled row (SURVEY.md §8f rank 1)")
+        return self.ctx.reconstruct_block(block_id).tobytes()
 
     def length(self, block_id):
         return self.ctx.block_length(block_id)

@@ -43,7 +43,7 @@ class ReductionScheme {
     virtual int64_t length(uint64_t block_id) = 0;
 };
 
-// MI355X backend (compressor == 1, dedup only).
+// MI355X backend (compressor 1 = dedup, 2 = dedup + Lz4Codec containers).
 class HipReductionScheme final : public ReductionScheme {
   public:
     explicit HipReductionScheme(const hdrf_cfg *cfg = nullptr)
@@ -90,9 +90,15 @@ class HipReductionScheme final : public ReductionScheme {
         return r;
     }
 
-    std::vector<uint8_t> reconstruct(uint64_t) override
+    std::vector<uint8_t> reconstruct(uint64_t block_id) override
     {
-        throw Error(HDRF_E_UNSUPPORTED, "DataConstructor read path: next scheduled row (SURVEY.md §8f rank 1)");
+        const int64_t len = hdrf_block_length(ctx_, block_id);
+        if (len < 0) check((int)len);
+        std::vector<uint8_t> out((size_t)len);
+        const int64_t n = hdrf_reconstruct_block(ctx_, block_id, out.data(), len);
+        if (n < 0) check((int)n);
+        out.resize((size_t)n);
+        return out;
     }
 
     int64_t length(uint64_t block_id) override

@@ -13,8 +13,9 @@ public final class HipReductionScheme extends ReductionScheme {
 
   private long ctx;                            // hdrf_ctx*
 
-  public HipReductionScheme(int hasher, int device, long maxBlockBytes) throws IOException {
-    ctx = open0(hasher, device, maxBlockBytes);
+  /** hasher: DataNode.hasher (0 SHA-1, 1 SHA-224); compressor: DataNode.compressor (1, 2). */
+  public HipReductionScheme(int hasher, int compressor, int device, long maxBlockBytes) throws IOException {
+    ctx = open0(hasher, compressor, device, maxBlockBytes);
   }
 
   @Override
@@ -25,7 +26,7 @@ public final class HipReductionScheme extends ReductionScheme {
 
   @Override
   public byte[] reconstruct(long blockId) throws IOException {
-    throw new IOException("reconstruction not implemented in this build (hdrf: HDRF_E_UNSUPPORTED)");
+    return reconstruct0(ctx, blockId);          // DataConstructor(blkID, recipe).data
   }
 
   @Override
@@ -43,7 +44,8 @@ public final class HipReductionScheme extends ReductionScheme {
     if (ctx != 0) { close0(ctx); ctx = 0; }
   }
 
-  private static native long open0(int hasher, int device, long maxBlockBytes) throws IOException;
+  private static native long open0(int hasher, int compressor, int device, long maxBlockBytes) throws IOException;
+  private static native byte[] reconstruct0(long ctx, long blockId) throws IOException;
   private static native void reduce0(long ctx, ByteBuffer direct, int len, long blockId) throws IOException;
   private static native long length0(long ctx, long blockId) throws IOException;
   private static native byte[] recipe0(long ctx, long blockId) throws IOException;

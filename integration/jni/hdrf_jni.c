@@ -19,13 +19,15 @@ static void throw_io(JNIEnv *env, hdrf_ctx *ctx, int rc)
 
 #define JFN(name) Java_org_apache_hadoop_hdfs_server_datanode_HipReductionScheme_##name
 
-JNIEXPORT jlong JNICALL JFN(open0)(JNIEnv *env, jclass cls, jint hasher, jint device, jlong max_block)
+JNIEXPORT jlong JNICALL JFN(open0)(JNIEnv *env, jclass cls, jint hasher, jint compressor, jint device,
+                                   jlong max_block)
 {
     (void)cls;
     hdrf_cfg cfg;
     hdrf_default_cfg(&cfg);
     cfg.hasher = hasher;              /* DataNode.hasher  (DataNode.java:446) */
-    cfg.compressor = 1;               /* dedup only (DataNode.java:438) */
+    cfg.compressor = compressor;      /* 1 dedup, 2 dedup + Lz4Codec (DataNode.java:438) */
+    cfg.arena_slots = 64;             /* resident containers for the read side */
     cfg.device = device;
     cfg.max_block_bytes = max_block;  /* dfs.blocksize */
     cfg.max_batch_blocks = 1;
@@ -63,6 +65,22 @@ JNIEXPORT jbyteArray JNICALL JFN(recipe0)(JNIEnv *env, jclass cls, jlong h, jlon
     int64_t cap = 4 + (int64_t)hdrf_digest_len(ctx) * (len / 702 + 2);
     uint8_t *tmp = (uint8_t *)malloc((size_t)cap);
     int64_t n = hdrf_recipe_get(ctx, (uint64_t)id, tmp, cap);
+    if (n < 0) { free(tmp); throw_io(env, ctx, (int)n); return NULL; }
+    jbyteArray out = (*env)->NewByteArray(env, (jsize)n);
+    (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);
+    free(tmp);
+    return out;
+}
+
+/* DataConstructor(blkID, recipe).data, served by BlockSender (DN/BlockSender.java:612-619) */
+JNIEXPORT jbyteArray JNICALL JFN(reconstruct0)(JNIEnv *env, jclass cls, jlong h, jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int64_t len = hdrf_block_length(ctx, (uint64_t)id);
+    if (len < 0) { throw_io(env, ctx, (int)len); return NULL; }
+    uint8_t *tmp = (uint8_t *)malloc((size_t)(len ? len : 1));
+    int64_t n = hdrf_reconstruct_block(ctx, (uint64_t)id, tmp, len);
     if (n < 0) { free(tmp); throw_io(env, ctx, (int)n); return NULL; }
     jbyteArray out = (*env)->NewByteArray(env, (jsize)n);
     (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);

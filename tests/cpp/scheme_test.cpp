@@ -60,11 +60,16 @@ int main()
         std::printf("block %zu: n=%lld store=%lld %s\n", i, (long long)n, (long long)ss, ok ? "OK" : "MISMATCH");
         fails += !ok;
     }
+    for (size_t i = 0; i < blocks.size(); i++) {                   // DataConstructor round trip
+        const bool ok = scheme.reconstruct(100 + i) == blocks[i];
+        std::printf("reconstruct %zu: %s\n", i, ok ? "OK" : "MISMATCH");
+        fails += !ok;
+    }
     try {
-        scheme.reconstruct(100);
+        scheme.reconstruct(999);
         fails++;
     } catch (const hdrf::Error &e) {
-        std::printf("reconstruct -> %s\n", e.what());
+        std::printf("reconstruct unknown -> %s\n", e.what());
     }
     hdrf_oracle_free(ora);
     std::printf(fails ? "FAIL\n" : "PASS\n");

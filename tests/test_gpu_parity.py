@@ -294,3 +294,24 @@ def test_reconstruct_round_trip(hasher, compressor):
                 n += 1
         assert n > 0
     ctx.close()
+
+
+@pytest.mark.parametrize("compressor", [1, 2])
+def test_scheme_plugin_round_trip(compressor):
+    """The Python mirror of the plugin API (hdrf_amd/scheme.py): reduce -> length -> reconstruct
+    in DataNode order, against the oracle's recipes."""
+    from hdrf_amd.scheme import HipReductionScheme
+    blocks = [make_block("random", 400, 900_000), make_block("text", 401, 600_000)]
+    blocks.append(np.concatenate([blocks[0][:300_000], blocks[1]]))
+    sch = HipReductionScheme(hasher=0, compressor=compressor, container_max=1 << 20, **SMALL)
+    ora = Oracle(hasher=0, compressor=compressor, max_size=1 << 20)
+    for i, b in enumerate(blocks):
+        sch.reduce(b, 700 + i)
+        ora.reduce(b, 700 + i)
+    for i, b in enumerate(blocks):
+        assert sch.length(700 + i) == len(b)
+        assert sch.recipe(700 + i) == ora.recipe(700 + i)
+        assert sch.reconstruct(700 + i) == b.tobytes()
+    with pytest.raises(HdrfError):
+        sch.reconstruct(12345)
+    sch.close()
