@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="one batch at a time (no stream overlap): clean per-kernel stage times")
+    ap.add_argument("--depth", type=int, default=2, help="batches in flight (1..3, pipelined mode)")
     ap.add_argument("--arena-slots", type=int, default=512,
                     help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers")
     ap.add_argument("--workload", choices=["config2", "config4"], default="config2",
@@ -147,14 +148,16 @@ def main():
                 ctx.reduce_batch(ptrs, lens, rd, ids)
                 collect()
         elif node is None:
-            # pipelined: chunking + SHA of batch k+1 overlap the index/store stage of batch k
+            # pipelined: chunking of batch k+2, SHA of batch k+1 and index/store of batch k overlap
+            depth = a.depth
             for k, (ptrs, lens, rd, ids) in enumerate(batches):
                 ctx.submit_batch(ptrs, lens, rd, ids)
-                if k:
+                if k >= depth - 1:
                     ctx.wait_batch()
                     collect()
-            ctx.wait_batch()
-            collect()
+            for _ in range(min(depth - 1, len(batches))):
+                ctx.wait_batch()
+                collect()
         else:
             for ptrs, lens, rd, ids in batches:
                 node.reduce_batch(ptrs, lens, rd, ids, rank * B)

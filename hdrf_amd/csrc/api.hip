@@ -30,7 +30,7 @@ namespace {
 
 constexpr int kStages = hdrf::kNumStages;
 constexpr uint64_t kSlack = 64;   // readable bytes required past each block end
-constexpr int kSlots = 2;         // batches in flight
+constexpr int kSlots = 3;         // batches in flight (walk | SHA | index+store)
 constexpr int kErrCapacity = 2 | 4 | 8 | 16 | 32;  // device error bits that mean "a buffer is too small"
 
 struct ContainerInfo {
@@ -73,8 +73,8 @@ struct Slot {
     std::vector<uint64_t> ids, lens;
     int nblocks = 0;
     bool pending = false;
-    hipEvent_t front_done = nullptr, back_done = nullptr;
-    hipEvent_t evA[5] = {}, evB[9] = {};   // stage markers (timing)
+    hipEvent_t walk_done = nullptr, front_done = nullptr, back_done = nullptr;
+    hipEvent_t evW[3] = {}, evA[3] = {}, evB[9] = {};   // stage markers (timing)
 };
 
 }  // namespace
@@ -82,8 +82,9 @@ struct Slot {
 struct hdrf_ctx {
     hdrf_cfg cfg{};
     int H = 20, HW = 5;
-    hipStream_t st = nullptr;    // stream A: front stage (also every synchronous helper)
-    hipStream_t stB = nullptr;   // stream B: back stage
+    hipStream_t st = nullptr;    // stream A: SHA stage (also every synchronous helper)
+    hipStream_t stB = nullptr;   // stream B: back stage (index + store)
+    hipStream_t stW = nullptr;   // stream W: chunking stage
     int max_batch = 0, cap_blk = 0, ntiles = 0, spec_cap = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
     Slot sl[kSlots];
     uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
@@ -213,8 +214,10 @@ static void free_slot(Slot &S)
     void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_closed, S.h_filelen, S.h_desc};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
-    hipEvent_t evs[] = {S.front_done, S.back_done};
+    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done};
     for (auto e : evs)
+        if (e) (void)hipEventDestroy(e);
+    for (auto e : S.evW)
         if (e) (void)hipEventDestroy(e);
     for (auto e : S.evA)
         if (e) (void)hipEventDestroy(e);
@@ -231,6 +234,7 @@ static void free_all(hdrf_ctx *ctx)
         if (p) (void)hipFree(p);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
+    if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
 }
 
 static int alloc_slot(hdrf_ctx *ctx, Slot &S)
@@ -262,9 +266,12 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
     if (c.compressor == 2 && ((rc = dalloc(ctx, &S.d_segclen, (size_t)ctx->closed_cap * nseg_lz)) ||
                               (rc = dalloc(ctx, &S.d_filelen, (size_t)ctx->closed_cap))))
         return rc;
-    if (hipEventCreateWithFlags(&S.front_done, hipEventDisableTiming) != hipSuccess ||
+    if (hipEventCreateWithFlags(&S.walk_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.front_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
+    for (auto &e : S.evW)
+        if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
     for (auto &e : S.evA)
         if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
     for (auto &e : S.evB)
@@ -281,6 +288,7 @@ static int drain(hdrf_ctx *ctx)
     int rc = 0;
     while (ctx->nwait < ctx->nsub)
         if (int r = wait_one(ctx)) rc = rc ? rc : r;
+    HIPCK(hipStreamSynchronize(ctx->stW));
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
     return rc;
@@ -289,16 +297,17 @@ static int drain(hdrf_ctx *ctx)
 static int init_state(hdrf_ctx *ctx)
 {
     (void)drain(ctx);
-    HIPCK(hipMemsetAsync(ctx->d_tab, 0, sizeof(IndexEntry) << ctx->cfg.index_log2, ctx->st));
     AllocState a{};
     for (int t = 0; t < 4; t++) {
         a.id[t] = (uint32_t)t << 22;                 // utilities.bytesToBlockID, absent key (DN/utilities.java:36-50)
         // (node-global mode: the one allocator of the node, carried rank to rank by hdrf_gx_flush)
         a.slot[t] = (uint32_t)t * (uint32_t)(ctx->cfg.arena_slots / 4);   // per-range slot rings
     }
-    HIPCK(hipMemcpyAsync(ctx->d_alloc, &a, sizeof a, hipMemcpyHostToDevice, ctx->st));
     for (auto &S : ctx->sl) HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
+    // the index and allocator belong to the back stream (node-global phases run on stream A)
+    hipStream_t ist = ctx->G > 1 ? ctx->st : ctx->stB;
+    HIPCK(launch_index_clear(ctx->d_tab, ctx->cfg.index_log2, ctx->d_alloc, a, ist));
     ctx->h_alloc = a;
     ctx->batch = 0;
     ctx->have_alloc = 0;
@@ -334,8 +343,19 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     ctx->H = c.hasher == 0 ? 20 : 28;
     ctx->HW = c.hasher == 0 ? 5 : 7;
     int rc = 0;
-    if (hipSetDevice(c.device) != hipSuccess || hipStreamCreateWithFlags(&ctx->st, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stB, hipStreamNonBlocking) != hipSuccess) {
+    // Stages per batch: chunking (W, scalar-unit bound), SHA (A, VALU-bound), index + store (B,
+    // memory-bound).  By default W is A (two stages: front = chunking + SHA, back = index + store);
+    // the front is the critical path, B has slack.  HDRF_PRIO: 1 = W, A high (default), 0 = equal,
+    // 2 = B high.
+    int lo_prio = 0, hi_prio = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
+    const char *pe = std::getenv("HDRF_PRIO");
+    const int prio_mode = pe ? std::atoi(pe) : 1;
+    const int pa = prio_mode == 1 ? hi_prio : lo_prio, pb = prio_mode == 2 ? hi_prio : lo_prio;
+    if (hipSetDevice(c.device) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, pa) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stB, hipStreamNonBlocking, pb) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pa) != hipSuccess) {
         free_all(ctx);
         delete ctx;
         return HDRF_E_HIP;
@@ -478,13 +498,22 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     S.lens.assign(len, len + nblocks);
     S.nblocks = nblocks;
     const uint32_t cur = ++ctx->batch;
-    hipStream_t A = ctx->st, Bst = ctx->stB;
-    // ---- front: the slot's previous batch has completed (wait_one ran), so A may overwrite it
-    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, A));
+    // chunking shares stream A with SHA unless HDRF_STREAMS=3 (measured: co-running the walk's
+    // readlane/scalar chains with SHA's VALU stream slows both; two stages are faster)
+    static const int nstreams = [] { const char *e = getenv("HDRF_STREAMS"); return e ? atoi(e) : 2; }();
+    hipStream_t W = nstreams == 3 ? ctx->stW : ctx->st, A = ctx->st, Bst = ctx->stB;
+    // ---- chunking on W: the slot's previous batch has completed (wait_one ran), so W may overwrite it
+    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, W));
+    Marker mw;
+    mw.ev = ctx->timing ? S.evW : nullptr;
+    HIPCK(launch_chunking(S.d_blocks, nblocks, max_nseg, c.window, c.max_chunk, S.d_spec, ctx->spec_cap, S.d_meta,
+                          S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, W, &mw));
+    mw.mark(W);
+    HIPCK(hipEventRecord(S.walk_done, W));
+    // ---- fingerprints on A
+    HIPCK(hipStreamWaitEvent(A, S.walk_done, 0));
     Marker ma;
     ma.ev = ctx->timing ? S.evA : nullptr;
-    HIPCK(launch_chunking(S.d_blocks, nblocks, max_nseg, c.window, c.max_chunk, S.d_spec, ctx->spec_cap, S.d_meta,
-                          S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, A, &ma));
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig, S.d_queue, A,
                      &ma));
     ma.mark(A);
@@ -527,7 +556,8 @@ static int complete_slot(hdrf_ctx *ctx, int si, bool timed)
     Slot &S = ctx->sl[si];
     const int nblocks = S.nblocks;
     if (ctx->timing && timed) {
-        for (int i = 0; i < 4; i++) ctx->stage_ms[i] += elapsed(S.evA[i], S.evA[i + 1]);
+        for (int i = 0; i < 2; i++) ctx->stage_ms[i] += elapsed(S.evW[i], S.evW[i + 1]);
+        for (int i = 0; i < 2; i++) ctx->stage_ms[2 + i] += elapsed(S.evA[i], S.evA[i + 1]);
         for (int i = 0; i < 6; i++) ctx->stage_ms[4 + i] += elapsed(S.evB[i], S.evB[i + 1]);
         ctx->stage_ms[10] += elapsed(S.evB[7], S.evB[8]);
     }

@@ -25,7 +25,8 @@
 
 namespace hdrf {
 
-// ---- byte helpers (tiles hold bytes XOR 0x80 so signed order == unsigned order) ----------
+// ---- byte helpers (the general path works on biased bytes, XOR 0x80, so signed order ==
+// unsigned order; tiles themselves stay raw) -----------------------------------------------
 typedef unsigned short us2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ us2 as_us2(uint32_t x) { return __builtin_bit_cast(us2, x); }
@@ -48,18 +49,21 @@ __device__ __forceinline__ uint32_t swar_ge(uint32_t w, uint32_t C)
     return ((w & C) | ((w | C) & s)) & 0x80808080u;
 }
 
-// 16-bit mask of the bytes of a biased granule equal to 0xFF (raw 0x7F = signed 127, the
-// largest possible byte); exact zero-byte test on ~v, then bits 7/15/23/31 packed into a nibble
-__device__ __forceinline__ uint32_t ff_nibble(uint32_t v)
+// 16-bit mask of the bytes of a RAW granule equal to 0x7F (signed 127, the largest possible
+// byte): exact zero-byte test of d ^ 0x7F7F7F7F (flag = bit 7 of the byte; no carries cross bytes),
+// then v_dot4_u32_u8 with byte weights 1,2,4,8 / 16..128 gathers the 16 flags.  ~18 VALU per tile.
+__device__ __forceinline__ uint32_t ff_flags(uint32_t d)
 {
-    const uint32_t z = ~v;
-    uint32_t t = ((z & 0x7f7f7f7fu) + 0x7f7f7f7fu) | z | 0x7f7f7f7fu;
-    t = (~t) >> 7;                                   // bits 0, 8, 16, 24
-    return (t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xfu;
+    const uint32_t s = (~d & 0x7f7f7f7fu) + 0x7f7f7f7fu;   // bit 7 clear <=> low 7 bits all set
+    return ~s & ~d & 0x80808080u;
 }
 __device__ __forceinline__ uint32_t ffmask16(uint4 v)
 {
-    return ff_nibble(v.x) | (ff_nibble(v.y) << 4) | (ff_nibble(v.z) << 8) | (ff_nibble(v.w) << 12);
+    const uint32_t lo = __builtin_amdgcn_udot4(ff_flags(v.y), 0x80402010u,
+                                               __builtin_amdgcn_udot4(ff_flags(v.x), 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(ff_flags(v.w), 0x80402010u,
+                                               __builtin_amdgcn_udot4(ff_flags(v.z), 0x08040201u, 0u, false), false);
+    return (lo | (hi << 8)) >> 7;                     // 0x80 * weight: bits 7..14 and 15..22
 }
 
 // keep bytes i (0..3) with a <= i <= b, as bit-7 flags
@@ -74,8 +78,9 @@ __device__ __forceinline__ uint32_t byte_range_mask(int a, int b)
 // A wave streams its region as 1 KiB tiles (lane l holds bytes [16l, 16l+16) of a tile).  The
 // "view" is two biased tiles A = [T, T+1024), B = [T+1024, T+2048); two more raw tiles are in
 // flight.  Tiles rotate through four register sets (R0..R3) in a 4-way unrolled loop, so there is
-// exactly one advance site per phase and no register copies.  Per tile only the 0xFF-byte mask
-// is computed (44 VALU); the granule max needed by the general path is computed on demand.
+// exactly one advance site per phase and no register copies.  Per tile only the 0x7F-byte mask and
+// its lane ballot are computed (~19 VALU); the biased granule maxima needed by the general path
+// (windows without a 0x7F byte, ~6% of random-data chunks) are computed on demand.
 
 struct WalkCfg {
     const uint8_t *base;
@@ -107,6 +112,15 @@ __device__ __forceinline__ uint4 bias(uint4 v)
     v.x ^= 0x80808080u; v.y ^= 0x80808080u; v.z ^= 0x80808080u; v.w ^= 0x80808080u;
     return v;
 }
+// Biased copies of the view for the general (no-0x7F) path.  The empty asm pins the copies (and
+// everything computed from them) inside that rarely taken path, so the compiler cannot hoist the
+// granule maxima into the per-tile stream.
+__device__ __forceinline__ void biased_view(const uint4 &A, const uint4 &B, uint4 &a, uint4 &b)
+{
+    a = A; b = B;
+    asm volatile("" : "+v"(a.x), "+v"(a.y), "+v"(a.z), "+v"(a.w), "+v"(b.x), "+v"(b.y), "+v"(b.z), "+v"(b.w));
+    a = bias(a); b = bias(b);
+}
 
 // 4 dwords of granule g (0..127) of the view, as uniform scalars
 __device__ __forceinline__ void granule(const uint4 &A, const uint4 &B, int g, uint32_t &w0, uint32_t &w1,
@@ -132,8 +146,10 @@ __device__ __forceinline__ uint32_t partial_max(const uint4 &A, const uint4 &B, 
 }
 
 // M(p) in biased form (general path); requires T <= p < T+1024 and p+w < size.
-__device__ __forceinline__ uint32_t window_max(const uint4 &A, const uint4 &B, int T, int p, int w, bool first)
+__device__ __forceinline__ uint32_t window_max(const uint4 &rA, const uint4 &rB, int T, int p, int w, bool first)
 {
+    uint4 A, B;
+    biased_view(rA, rB, A, B);
     const uint32_t gA = gmax16(A), gB = gmax16(B);
     const int e = p + w;
     const int gp = (p - T) >> 4, ge = (e - T) >> 4;
@@ -169,8 +185,10 @@ __device__ __forceinline__ int first_ge(const uint4 &A, const uint4 &B, int g, i
 }
 
 // first j in [q, hi] (inside the view) with biased byte >= m, or -1 (general path)
-__device__ __forceinline__ int ge_in_view(const uint4 &A, const uint4 &B, int T, int q, int hi, uint32_t m)
+__device__ __forceinline__ int ge_in_view(const uint4 &rA, const uint4 &rB, int T, int q, int hi, uint32_t m)
 {
+    uint4 A, B;
+    biased_view(rA, rB, A, B);
     const uint32_t gA = gmax16(A), gB = gmax16(B);
     const int gq = (q - T) >> 4, gh = (hi - T) >> 4;
     unsigned long long ma = ballot64(gA >= m);
@@ -190,23 +208,37 @@ __device__ __forceinline__ int ge_in_view(const uint4 &A, const uint4 &B, int T,
     return -1;
 }
 
-// first j in [x, hi] (inside the view) whose biased byte is 0xFF (raw 0x7F), or -1.  When the
-// window holds such a byte, M(p) = 127 is the largest possible value and the cut is simply the
-// next 0x7F byte after the window.
-__device__ __forceinline__ int ff_in_view(uint32_t fA, uint32_t fB, int T, int x, int hi)
+// First 0x7F byte at a position >= x (T <= x < T+2048) inside the view, or INT_MAX.  fA/fB are the
+// per-lane 0x7F masks of the two tiles, bA/bB the per-tile ballots of lanes holding one (computed
+// once per tile), so a query is one or two v_readlane plus scalar bit scans.  When the window
+// holds a 0x7F byte, M(p) = 127 and the cut is simply the next 0x7F after the window.
+__device__ __forceinline__ int next_ff(uint32_t fA, uint32_t fB, unsigned long long bA, unsigned long long bB, int T,
+                                       int x)
 {
-    const int l = lane_id();
-    const int g = (x - T) >> 4, o = (x - T) & 15;
-    const uint32_t a = (l > g) ? fA : ((l == g) ? (fA & (0xffffu << o)) : 0u);
-    const uint32_t c = (l + 64 > g) ? fB : ((l + 64 == g) ? (fB & (0xffffu << o)) : 0u);
-    const unsigned long long ba = ballot64(a != 0u), bb = ballot64(c != 0u);
-    if (!(ba | bb)) return -1;
-    int L;
-    uint32_t bits;
-    if (ba) { L = __builtin_ctzll(ba); bits = rdlane(a, L); }
-    else { L = __builtin_ctzll(bb); bits = rdlane(c, L); L += 64; }
-    const int pos = T + 16 * L + __builtin_ctz(bits);
-    return pos <= hi ? pos : -1;
+    const int r = x - T, g = r >> 4, o = r & 15;
+    if (g < 64) {
+        const uint32_t w = rdlane(fA, g) & (0xffffu << o);
+        if (w) return T + 16 * g + __builtin_ctz(w);
+        const unsigned long long m = bA & (~1ull << g);          // lanes after g
+        if (m) {
+            const int L = __builtin_ctzll(m);
+            return T + 16 * L + __builtin_ctz(rdlane(fA, L));
+        }
+        if (bB) {
+            const int L = __builtin_ctzll(bB);
+            return T + 1024 + 16 * L + __builtin_ctz(rdlane(fB, L));
+        }
+        return 0x7fffffff;
+    }
+    const int gb = g - 64;
+    const uint32_t w = rdlane(fB, gb) & (0xffffu << o);
+    if (w) return T + 16 * g + __builtin_ctz(w);
+    const unsigned long long m = bB & (~1ull << gb);
+    if (m) {
+        const int L = __builtin_ctzll(m);
+        return T + 1024 + 16 * L + __builtin_ctz(rdlane(fB, L));
+    }
+    return 0x7fffffff;
 }
 
 struct ListSink;
@@ -215,16 +247,48 @@ struct ListSink;
 // advance (the chain continues), false when the chain ended (ch.ended) or the sink/stop said stop.
 template <class Sink, class Stop>
 __device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const uint4 &A, const uint4 &B,
-                                             uint32_t fA, uint32_t fB, int T, Sink &sink, Stop &stop)
+                                             uint32_t fA, uint32_t fB, unsigned long long bA, unsigned long long bB,
+                                             int T, Sink &sink, Stop &stop)
 {
     for (;;) {
         if (ch.state == kWindow) {
+            // Fast path: windows holding a 0x7F byte (M = 127): cut = next 0x7F after the window + 1.
+            // Scalar only, one exit test per condition; the general state machine below takes over
+            // (from the same p) when a window has no 0x7F, the search leaves the view or reaches
+            // lim, the data ends, or a cut crosses the stop predicate's thresholds.
+            {
+                int p = ch.p, cnt = sink.cnt;
+                uint32_t stage = sink.stage;
+                const int pe = min(T + 1024, c.size - c.w);            // window complete & inside the view
+                const int hiv = min(T + 2047, c.size - 1);
+                const int cut_thr = stop.cut_thr(), cnt_thr = min(stop.cnt_thr(), sink.cap);
+                bool pushed = false;
+                while (p < pe && cnt < cnt_thr) {
+                    const int e = p + c.w;
+                    if (next_ff(fA, fB, bA, bB, T, p) > e) break;      // no 0x7F in the window
+                    const int f2 = next_ff(fA, fB, bA, bB, T, e + 1);
+                    if (f2 > min(p + c.maxlen, hiv)) break;
+                    p = f2 + 1;                                        // :276-283
+                    if (lane_id() == (cnt & 63)) stage = (uint32_t)p;
+                    cnt++;
+                    if ((cnt & 63) == 0) sink.out[cnt - 64 + lane_id()] = stage;
+                    pushed = true;
+                    if (p >= cut_thr) break;
+                }
+                sink.cnt = cnt;
+                sink.stage = stage;
+                if (pushed) {
+                    ch.p = p;
+                    ch.first = false;
+                    if (stop(p, cnt)) return false;
+                }
+            }
             if (ch.p >= T + 1024) return true;
             const int e = ch.p + c.w;
             if (e >= c.size) { ch.ended = true; return false; }       // window incomplete: no more cuts
             ch.lim = min(ch.p + c.maxlen, c.size - 1);
             ch.q = e + 1;
-            if (ff_in_view(fA, fB, T, ch.p, e) >= 0) {
+            if (next_ff(fA, fB, bA, bB, T, ch.p) <= e) {
                 ch.state = kSearchFF;                                  // M(p) = 127
             } else {
                 ch.m = window_max(A, B, T, ch.p, c.w, ch.first);
@@ -234,8 +298,14 @@ __device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const 
         const int vend = T + 2047;
         const int hi = min(ch.lim, vend);
         int j = -1;
-        if (ch.q <= hi)
-            j = ch.state == kSearchFF ? ff_in_view(fA, fB, T, ch.q, hi) : ge_in_view(A, B, T, ch.q, hi, ch.m);
+        if (ch.q <= hi) {
+            if (ch.state == kSearchFF) {
+                const int f = next_ff(fA, fB, bA, bB, T, ch.q);
+                j = f <= hi ? f : -1;
+            } else {
+                j = ge_in_view(A, B, T, ch.q, hi, ch.m);
+            }
+        }
         int cut;
         if (j >= 0) {
             cut = j + 1;                                               // :276-283
@@ -276,60 +346,83 @@ struct ListSink {
     }
 };
 
+// Stop predicates: operator() is evaluated after every cut; cut_thr/cnt_thr tell the fast path the
+// first cut position / count at which the predicate can change, so it only asks then.
+struct SpecStop {          // segment walk: cuts past s_next are overrun; stop after kOverrun of them
+    int s_next;
+    int n_main;
+    __device__ __forceinline__ bool operator()(int cut, int cnt)
+    {
+        if (n_main < 0 && cut >= s_next) n_main = cnt - 1;
+        return n_main >= 0 && cnt - n_main >= kOverrun;
+    }
+    __device__ __forceinline__ int cut_thr() const { return n_main < 0 ? s_next : 0x7fffffff; }
+    __device__ __forceinline__ int cnt_thr() const { return n_main < 0 ? 0x7fffffff : n_main + kOverrun; }
+};
+struct NoStop {
+    __device__ __forceinline__ bool operator()(int, int) { return false; }
+    __device__ __forceinline__ int cut_thr() const { return 0x7fffffff; }
+    __device__ __forceinline__ int cnt_thr() const { return 0x7fffffff; }
+};
+
 // Walk the chain from p (a cut, or the block start when first) calling sink.push(cut) for
 // every cut until the data ends (returns true) or the sink/stop predicate says stop (false).
 template <class Stop>
-__device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, ListSink &sink, Stop stop)
+__device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, ListSink &sink, Stop &stop)
 {
     Chain ch;
     ch.p = p; ch.state = kWindow; ch.q = 0; ch.lim = 0; ch.m = 0; ch.first = first; ch.ended = false;
     int T = p & ~1023;
     uint4 R0 = tile_raw(c, T), R1 = tile_raw(c, T + 1024), R2 = tile_raw(c, T + 2048), R3 = tile_raw(c, T + 3072);
-    R0 = bias(R0); R1 = bias(R1);
     uint32_t f0 = ffmask16(R0), f1 = ffmask16(R1), f2 = 0, f3 = 0;
+    unsigned long long b0 = ballot64(f0 != 0), b1 = ballot64(f1 != 0), b2 = 0, b3 = 0;
     for (;;) {
-        if (!process_view(c, ch, R0, R1, f0, f1, T, sink, stop)) break;
-        T += 1024; R2 = bias(R2); f2 = ffmask16(R2); R0 = tile_raw(c, T + 3072);
-        if (!process_view(c, ch, R1, R2, f1, f2, T, sink, stop)) break;
-        T += 1024; R3 = bias(R3); f3 = ffmask16(R3); R1 = tile_raw(c, T + 3072);
-        if (!process_view(c, ch, R2, R3, f2, f3, T, sink, stop)) break;
-        T += 1024; R0 = bias(R0); f0 = ffmask16(R0); R2 = tile_raw(c, T + 3072);
-        if (!process_view(c, ch, R3, R0, f3, f0, T, sink, stop)) break;
-        T += 1024; R1 = bias(R1); f1 = ffmask16(R1); R3 = tile_raw(c, T + 3072);
+        if (!process_view(c, ch, R0, R1, f0, f1, b0, b1, T, sink, stop)) break;
+        T += 1024; f2 = ffmask16(R2); b2 = ballot64(f2 != 0); R0 = tile_raw(c, T + 3072);
+        if (!process_view(c, ch, R1, R2, f1, f2, b1, b2, T, sink, stop)) break;
+        T += 1024; f3 = ffmask16(R3); b3 = ballot64(f3 != 0); R1 = tile_raw(c, T + 3072);
+        if (!process_view(c, ch, R2, R3, f2, f3, b2, b3, T, sink, stop)) break;
+        T += 1024; f0 = ffmask16(R0); b0 = ballot64(f0 != 0); R2 = tile_raw(c, T + 3072);
+        if (!process_view(c, ch, R3, R0, f3, f0, b3, b0, T, sink, stop)) break;
+        T += 1024; f1 = ffmask16(R1); b1 = ballot64(f1 != 0); R3 = tile_raw(c, T + 3072);
     }
     return ch.ended;
 }
 
 // ------------------------------------------------------------------------------------------
-// 1. speculative walk: grid (ceil(maxseg/4), nblocks), 256 threads = 4 waves, one per segment.
-__global__ void __launch_bounds__(256) spec_walk_kernel(const BlockDesc *__restrict__ blocks, int w, int maxlen,
+// 1. speculative walk: a pool of waves (HDRF_WALK_WAVES per SIMD, default 8 = one segment per
+//    wave for a 64 x 128 MiB batch) strides over the (block, segment) pairs.  The walk is bound
+//    by the scalar unit (one SALU issue per SIMD per 4 cycles), so it wants every wave slot.
+__global__ void __launch_bounds__(256) spec_walk_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
+                                                        int max_nseg, int w, int maxlen,
                                                         uint32_t *__restrict__ spec, int spec_cap,
                                                         SegMeta *__restrict__ meta)
 {
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * 4 + wave_id();
-    const BlockDesc bd = blocks[b];
-    if (k >= bd.nseg) return;
-    const int size = (int)bd.len;
-    const int s_k = k * bd.seg_len;
-    const int s_next = (k + 1 == bd.nseg) ? 0x7fffffff : (k + 1) * bd.seg_len;  // last: every cut is main
-    WalkCfg W;
-    W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = size;
-    W.w = w; W.maxlen = maxlen;
-    ListSink sink;
-    const int idx = b * kMaxSegs + k;
-    sink.out = spec + (size_t)idx * spec_cap; sink.cap = spec_cap; sink.cnt = 0; sink.stage = 0;
-    int n_main = -1;
-    bool ended = walk_chain(W, s_k, k == 0, sink, [&](int cut, int cnt) {
-        if (n_main < 0 && cut >= s_next) n_main = cnt - 1;
-        return n_main >= 0 && cnt - n_main >= kOverrun;
-    });
-    sink.flush();
-    if (n_main < 0) n_main = sink.cnt;
-    if (lane_id() == 0) {
-        SegMeta m;
-        m.n_main = n_main; m.n_over = sink.cnt - n_main; m.ended = ended ? 1 : 0; m.pad = 0;
-        meta[idx] = m;
+    const int total = nblocks * max_nseg;
+    const int nw = gridDim.x * 4;
+    for (int t = blockIdx.x * 4 + wave_id(); t < total; t += nw) {
+        const int b = t / max_nseg;
+        const int k = t - b * max_nseg;
+        const BlockDesc bd = blocks[b];
+        if (k >= bd.nseg) continue;
+        const int size = (int)bd.len;
+        const int s_k = k * bd.seg_len;
+        const int s_next = (k + 1 == bd.nseg) ? 0x7fffffff : (k + 1) * bd.seg_len;  // last: every cut is main
+        WalkCfg W;
+        W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = size;
+        W.w = w; W.maxlen = maxlen;
+        ListSink sink;
+        const int idx = b * kMaxSegs + k;
+        sink.out = spec + (size_t)idx * spec_cap; sink.cap = spec_cap; sink.cnt = 0; sink.stage = 0;
+        SpecStop stop{s_next, -1};
+        bool ended = walk_chain(W, s_k, k == 0, sink, stop);
+        sink.flush();
+        const int n_main = stop.n_main < 0 ? sink.cnt : stop.n_main;
+        if (lane_id() == 0) {
+            SegMeta m;
+            m.n_main = n_main; m.n_over = sink.cnt - n_main; m.ended = ended ? 1 : 0; m.pad = 0;
+            meta[idx] = m;
+        }
     }
 }
 
@@ -456,7 +549,8 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
         W.w = w; W.maxlen = maxlen;
         ListSink sink;
         sink.out = off + s.fail_dst; sink.cap = cap_blk - s.fail_dst; sink.cnt = 0; sink.stage = 0;
-        bool ok = walk_chain(W, (int)s.fail_p0, false, sink, [](int, int) { return false; });
+        NoStop nostop;
+        bool ok = walk_chain(W, (int)s.fail_p0, false, sink, nostop);
         sink.flush();
         if (!ok && lane_id() == 0) atomicOr(err, 1);
         s.n_cuts = s.fail_dst + sink.cnt;
@@ -482,7 +576,11 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg,
 {
     mk->mark(st);
     dim3 g((max_nseg + 3) / 4, nblocks);
-    hipLaunchKernelGGL(spec_walk_kernel, g, dim3(256), 0, st, d_blocks, w, maxlen, spec, spec_cap, meta);
+    static const int per_simd = [] { const char *e = getenv("HDRF_WALK_WAVES"); return e ? atoi(e) : 8; }();
+    const int total = nblocks * max_nseg;
+    const int nwg = std::max(1, std::min((total + 3) / 4, per_simd * 1024 / 4));
+    hipLaunchKernelGGL(spec_walk_kernel, dim3(nwg), dim3(256), 0, st, d_blocks, nblocks, max_nseg, w, maxlen, spec,
+                       spec_cap, meta);
     mk->mark(st);
     hipLaunchKernelGGL(spec_sync_kernel, g, dim3(256), 0, st, d_blocks, spec, spec_cap, meta, sync);
     hipLaunchKernelGGL(spec_plan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, spec, spec_cap, meta, sync,

@@ -231,6 +231,35 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
         tilesum[(size_t)b * ntiles + blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
 }
 
+// A fresh DataNode (empty Redis): zero the table with 16-B streaming stores (rocclr's fill
+// reached ~1 TB/s on the 8.6 GB table) and seed the allocator, both on the stream that owns
+// the index, so the front half of the next batch overlaps the clear.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__global__ void __launch_bounds__(256) idx_clear_kernel(u32x4 *__restrict__ p, uint64_t n16, AllocState *alloc,
+                                                        AllocState a)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        __builtin_nontemporal_store(z, p + i);
+        __builtin_nontemporal_store(z, p + i + stride);
+        __builtin_nontemporal_store(z, p + i + 2 * stride);
+        __builtin_nontemporal_store(z, p + i + 3 * stride);
+    }
+    for (; i < n16; i += stride) __builtin_nontemporal_store(z, p + i);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *alloc = a;
+}
+
+hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st)
+{
+    const uint64_t n16 = (sizeof(IndexEntry) << log2cap) / 16;
+    uint64_t g = (n16 + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(idx_clear_kernel, dim3((unsigned)g), dim3(256), 0, st, (u32x4 *)tab, n16, d_alloc, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,
                         unsigned long long tag_mask, uint32_t *slot,

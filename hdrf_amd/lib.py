@@ -10,7 +10,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libhdrf.so")
+LIB_PATH = os.environ.get("HDRF_LIB_PATH") or os.path.join(_HERE, "_build", "libhdrf.so")   # env: A/B builds
 
 HDRF_ERRORS = {
     -1: "HDRF_E_INVAL", -2: "HDRF_E_HIP", -3: "HDRF_E_NOMEM", -4: "HDRF_E_CAPACITY",
@@ -31,6 +31,7 @@ EXPORTS = [
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
+PIPELINE_DEPTH = 3          # HDRF_PIPELINE_DEPTH: batches in flight
 
 
 # per-stage timers of hdrf_stage_times (kernel names in parentheses)
@@ -237,7 +238,7 @@ class Context:
         self._ck(self.L.hdrf_reduce_batch(self._h, n, ptrs, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p)))
 
     def submit_batch(self, dev_ptrs, lens, readable, block_ids):
-        """Enqueue a batch (two in flight at most); complete it with wait_batch() in order."""
+        """Enqueue a batch (PIPELINE_DEPTH in flight at most); complete it with wait_batch() in order."""
         n = len(dev_ptrs)
         ptrs = (_vp * n)(*dev_ptrs)
         ln = np.ascontiguousarray(lens, np.uint64)

@@ -86,12 +86,14 @@ int hdrf_reduce_block(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *data, uin
 int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                       const uint64_t *readable, const uint64_t *block_ids);
 
-/* Pipelined form of hdrf_reduce_batch: hdrf_submit_batch enqueues the batch (chunking + SHA on one
- * HIP stream, index + store on a second one, in block order) and returns; hdrf_wait_batch
- * completes the OLDEST submitted batch and makes it the one hdrf_batch_* report.  At most two
- * batches are in flight (a third submit first completes the oldest); the device buffers of a
- * batch must stay valid until it is completed.  Chunking and hashing of batch k+1 overlap the
- * index/store stage of batch k.  Views (index, containers, allocator) complete all batches first. */
+/* Pipelined form of hdrf_reduce_batch: hdrf_submit_batch enqueues the batch (chunking, SHA and
+ * index + store on three HIP streams, in block order) and returns; hdrf_wait_batch completes the
+ * OLDEST submitted batch and makes it the one hdrf_batch_* report.  At most HDRF_PIPELINE_DEPTH
+ * batches are in flight (one more submit first completes the oldest); the device buffers of a
+ * batch must stay valid until it is completed.  Chunking of batch k+2, hashing of batch k+1 and
+ * the index/store stage of batch k run concurrently (scalar units, vector units and memory).
+ * Views (index, containers, allocator) complete all batches first. */
+#define HDRF_PIPELINE_DEPTH 3
 int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                       const uint64_t *readable, const uint64_t *block_ids);
 int hdrf_wait_batch(hdrf_ctx *ctx);

@@ -218,9 +218,10 @@ def test_device_corpus_matches_host_and_reduces(mixed):
 
 
 def test_pipelined_submit_wait_matches_sequential_oracle():
-    """hdrf_submit_batch / hdrf_wait_batch: two batches in flight (chunking + SHA of batch k+1 on
-    one stream while batch k is indexed and stored on the other) give the same results as the
-    sequential oracle, including when a third submit completes the oldest batch implicitly."""
+    """hdrf_submit_batch / hdrf_wait_batch: up to PIPELINE_DEPTH batches in flight (chunking of
+    batch k+2, SHA of k+1 and index/store of k on three streams) give the same results as the
+    sequential oracle, including when a submit beyond the depth completes the oldest batch."""
+    from hdrf_amd.lib import PIPELINE_DEPTH as D
     nb, spb, seg = 14, 8, 1 << 18
     roots = corpus_roots(77, 500000, nb, spb)
     blocks = [corpus_block_host(77, roots, b, spb, seg) for b in range(nb)]
@@ -229,7 +230,7 @@ def test_pipelined_submit_wait_matches_sequential_oracle():
     size = spb * seg
     dev = ctx.dev_alloc(size * nb + 4096)
     ctx.h2d(dev, np.concatenate(blocks))
-    groups = [list(range(s, min(s + 3, nb))) for s in range(0, nb, 3)]
+    groups = [list(range(s, min(s + 2, nb))) for s in range(0, nb, 2)]
     ids = [900 + b for b in range(nb)]
 
     def check(group):
@@ -239,13 +240,13 @@ def test_pipelined_submit_wait_matches_sequential_oracle():
 
     pending = []
     for gi, g in enumerate(groups):
-        if len(pending) == 2:                # this submit completes the oldest batch itself
+        if len(pending) == D:                # this submit completes the oldest batch itself
             for b in pending.pop(0):
                 ora.reduce(blocks[b], ids[b])
         ctx.submit_batch([dev + b * size for b in g], [size] * len(g), [size * (nb - b) + 4096 for b in g],
                          [ids[b] for b in g])
         pending.append(g)
-        if gi % 3 == 1:                      # sometimes let a third submit complete the oldest
+        if gi % 4 != 3:                      # mostly keep the pipeline full
             continue
         while len(pending) > 1:
             ctx.wait_batch()
