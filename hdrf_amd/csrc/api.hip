@@ -526,7 +526,13 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_tab, c.index_log2, cur,
                        tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap, S.d_flags, S.d_tilesum, ctx->ntiles,
                        S.d_err, Bst, &mb));
-    const StoreParams P = store_params(ctx, nblocks);
+    StoreParams P = store_params(ctx, nblocks);
+    // When batches are pipelined (one already in flight), this batch's place kernel overlaps the
+    // next batch's front stage (the critical path): a dynamic-LDS reservation caps place at one
+    // wave per SIMD so SHA keeps its wave slots (measured +1.5-2% on the config-2 bench; alone,
+    // place wants full occupancy).  HDRF_PLACE_LDS overrides the reservation (bytes).
+    static const int place_lds = [] { const char *e = getenv("HDRF_PLACE_LDS"); return e ? atoi(e) : 40960; }();
+    if (ctx->nsub > ctx->nwait) P.place_lds = place_lds;
     HIPCK(launch_store(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_pre,
                        ctx->d_alloc, S.d_rstate, S.d_ev, S.d_closed, S.d_nclosed, S.d_slot, ctx->d_tab, ctx->d_arena,
                        S.d_pcid, S.d_ppos, S.d_err, Bst, &mb));

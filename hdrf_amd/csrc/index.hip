@@ -15,6 +15,8 @@
 //   slow   — single-thread exact re-probe for the (astronomically rare) 8-byte tag collisions
 //   decide — is_new = entry created this batch && b == min block; designated = (min block,
 //            last chunk index) is the one chunk that writes the final value (in store.hip)
+#include <cstdlib>
+
 #include "launchers.hpp"
 
 namespace hdrf {
@@ -268,9 +270,10 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
 {
     mk->mark(st);
     dim3 g(ntiles, nblocks);
+    static const int lds = [] { const char *e = getenv("HDRF_CLAIM_LDS"); return e ? atoi(e) : 0; }();
     (void)hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st);
     if (hasher == 0) {
-        hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
+        hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
                            slot, flags, err);
         mk->mark(st);
         hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, tag_mask, coll,
@@ -280,7 +283,7 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
         hipLaunchKernelGGL(idx_slow_kernel<5>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, tag_mask, slot,
                            coll, ncoll, coll_cap, err);
     } else {
-        hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
+        hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
                            slot, flags, err);
         mk->mark(st);
         hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, tag_mask, coll,

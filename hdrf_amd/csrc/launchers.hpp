@@ -24,6 +24,7 @@ struct StoreParams {
     uint32_t nslots;           // container arena slots
     int ev_cap;                // flush events per range per batch
     int closed_cap;            // closed containers per batch
+    int place_lds = 0;         // dynamic LDS per place workgroup (occupancy throttle, 0 = none)
 };
 
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg, int w, int maxlen,

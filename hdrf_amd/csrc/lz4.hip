@@ -10,10 +10,11 @@
 // one segment (table in LDS).  The greedy parse is sequential, but its expensive parts are made
 // wave-parallel:
 //   * match search: the positions the search loop visits do not depend on the data until a match
-//     is found (ip += attempts++ >> 6), so 64 attempts are evaluated at once (lane i = attempt i):
-//     hashes and the 4-byte candidate compare are one gather each; the table reads/writes are
-//     replayed in attempt order (single-lane LDS ops, program order = reference order) and the
-//     writes of attempts after the first match are undone in reverse order;
+//     is found (ip += attempts++ >> 6), so a batch of 16, 32, then 64 attempts is evaluated at once
+//     (lane i = attempt i, positions in closed form): hashes and the 4-byte candidate compare are
+//     one gather each.  When the batch's hashes are distinct the table update is one LDS gather +
+//     one scatter (attempts after the first match restore the old entry); otherwise the reads and
+//     writes are replayed lane by lane in attempt order and the writes after the match undone;
 //   * match extension, catch-up and literal copies are 64-lane compares / 16-B-per-lane copies.
 //   lz4_pack then frames the segments ([BE32 len] ([BE32 clen] block)* [BE32 0]) in place.
 #include "launchers.hpp"
@@ -24,6 +25,7 @@ constexpr int kLzMaxIn = 261100;                 // BlockCompressorStream MAX_IN
 constexpr int kLzSegBound = kLzMaxIn + kLzMaxIn / 255 + 16;
 constexpr int kLzSegStride = kLzSegBound + 4;    // per-segment stride of the unpacked layout
 constexpr int kMfLimit = 12, kLastLit = 5, kMaxDist = 65535, k64KLimit = 65536 + kMfLimit - 1;
+constexpr int kLzFirstBatch = 16;                // attempts per batch after a match (then 32, 64)
 
 __device__ __forceinline__ uint32_t rd32u(const uint8_t *p)
 {
@@ -92,32 +94,61 @@ __device__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint32_t *tab)
     if (n >= kMfLimit + 1) {
         if (l == 0) tput(hash(rd32u(src)), 0);        // first byte
         ip = 1;
-        int fip = ip, attempts = (1 << 6) + 3;
+        int fip = ip, attempts = (1 << 6) + 3, m = kLzFirstBatch;
         for (;;) {
-            // ---- match search: 64 attempts at once --------------------------------------
+            // ---- match search: a batch of m attempts at once ------------------------------
+            // attempt l advances by step_l = (a0 + l) >> 6, which takes only the values q and
+            // q + 1 inside one batch, so the attempt positions have a closed form (no scan)
             const int a0 = attempts;
-            const int step = (a0 + l) >> 6;
-            const int ipl = fip + (int)wave_incl_scan((uint32_t)step) - step;   // this lane's attempt
-            const bool valid = ipl + step <= mflimit;
+            const int q = a0 >> 6, rr = a0 & 63;
+            const int step = q + (l >= 64 - rr ? 1 : 0);
+            const int ipl = fip + l * q + max(0, l - (64 - rr));       // this lane's attempt
+            const bool valid = l < m && ipl + step <= mflimit;
             const uint32_t v = valid ? rd32u(src + ipl) : 0u;
             const uint32_t h = hash(v);
             const unsigned long long vmask = ballot64(valid);
             const int nv = vmask == ~0ull ? 64 : __builtin_ctzll(~vmask);   // valid lanes are a prefix
-            int ref = 0;
+            int ref = 0, old = 0;
+            // Table replay in attempt order.  Fast path (u32 table): if the batch's hashes are
+            // pairwise distinct, every attempt reads the pre-batch entry and the writes commute,
+            // so one gather + one scatter do it.  Distinctness is checked by scattering lane tags
+            // (positions never have bit 31 set) and reading them back; otherwise the entries are
+            // restored and the replay runs lane by lane.
+            bool slow = u16;
+            if (!u16) {
+                if (valid) old = (int)tab[h];
+                asm volatile("" ::: "memory");
+                if (valid) tab[h] = 0x80000000u | (uint32_t)l;
+                asm volatile("" ::: "memory");
+                const uint32_t t = valid ? tab[h] : 0u;
+                slow = ballot64(valid && t != (0x80000000u | (uint32_t)l)) != 0;
+                asm volatile("" ::: "memory");
+                if (slow && valid) tab[h] = (uint32_t)old;         // equal hashes carry equal olds
+                ref = old;
+            }
             asm volatile("" ::: "memory");
-            for (int i = 0; i < nv; i++) {                // table replay in attempt order
-                if (l == i) { ref = tget(h); tput(h, ipl); }
-                asm volatile("" ::: "memory");            // keep the LDS ops in program order
+            if (slow) {
+                for (int i = 0; i < nv; i++) {            // sequential replay
+                    if (l == i) { ref = tget(h); tput(h, ipl); }
+                    asm volatile("" ::: "memory");        // keep the LDS ops in program order
+                }
             }
             asm volatile("" ::: "memory");
             bool ok = false;
             if (valid && ref + kMaxDist >= ipl) ok = rd32u(src + ref) == v;
             const unsigned long long okm = ballot64(ok);
+            if (!slow) {                                  // commit: attempts up to the first match
+                const int last = okm ? __builtin_ctzll(okm) : 63;
+                if (valid) tab[h] = l <= last ? (uint32_t)ipl : (uint32_t)old;
+                asm volatile("" ::: "memory");
+            }
             if (okm) {
                 const int istar = __builtin_ctzll(okm);
-                for (int i = nv - 1; i > istar; i--) {    // undo the attempts after the match
-                    if (l == i) tput(h, ref);
-                    asm volatile("" ::: "memory");
+                if (slow) {
+                    for (int i = nv - 1; i > istar; i--) {    // undo the attempts after the match
+                        if (l == i) tput(h, ref);
+                        asm volatile("" ::: "memory");
+                    }
                 }
                 asm volatile("" ::: "memory");
                 ip = (int)rdlane((uint32_t)ipl, istar);
@@ -198,11 +229,13 @@ __device__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint32_t *tab)
                 anchor = ip++;
                 fip = ip;
                 attempts = (1 << 6) + 3;
+                m = kLzFirstBatch;
                 continue;
             }
-            if (nv < 64) break;                            // the next attempt passes mflimit
-            fip = (int)rdlane((uint32_t)(ipl + step), 63);
-            attempts = a0 + 64;
+            if (nv < m) break;                             // the next attempt passes mflimit
+            fip = (int)rdlane((uint32_t)(ipl + step), m - 1);
+            attempts = a0 + m;
+            m = min(64, 2 * m);
         }
     }
 last_literals:

@@ -16,6 +16,8 @@
 //   flush       — one wave per range t walks the batch's blocks in order, finds flushes
 //   place       — per chunk: container id / position; wave-cooperative copy into the arena;
 //                 the designated chunk of each touched index entry writes its final value.
+#include <cstdlib>
+
 #include "launchers.hpp"
 
 namespace hdrf {
@@ -342,7 +344,7 @@ hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, c
                               hipStream_t st)
 {
     if (gx.x3) (void)hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st);
-    hipLaunchKernelGGL(place_kernel, dim3(P.ntiles, P.nblocks), dim3(256), 0, st, P, d_blocks, bst, offsets, flags, pre,
+    hipLaunchKernelGGL(place_kernel, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst, offsets, flags, pre,
                        rstate, events, slot, tab, arena, place_cid, place_pos, gx);
     return hipGetLastError();
 }
