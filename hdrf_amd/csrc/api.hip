@@ -74,6 +74,9 @@ struct Slot {
     int nblocks = 0;
     bool pending = false;
     hipEvent_t walk_done = nullptr, front_done = nullptr, back_done = nullptr;
+    hipEvent_t copy_done = nullptr;          // host path: the batch's H2D copies landed
+    uint8_t *d_hstage = nullptr;              // host path: device copies of the batch's blocks
+    uint64_t hstage_stride = 0;
     hipEvent_t evW[3] = {}, evA[3] = {}, evB[9] = {};   // stage markers (timing)
 };
 
@@ -85,6 +88,7 @@ struct hdrf_ctx {
     hipStream_t st = nullptr;    // stream A: SHA stage (also every synchronous helper)
     hipStream_t stB = nullptr;   // stream B: back stage (index + store)
     hipStream_t stW = nullptr;   // stream W: chunking stage
+    hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
     int max_batch = 0, cap_blk = 0, ntiles = 0, spec_cap = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
     Slot sl[kSlots];
     uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
@@ -214,7 +218,8 @@ static void free_slot(Slot &S)
     void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_closed, S.h_filelen, S.h_desc};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
-    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done};
+    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done};
+    if (S.d_hstage) (void)hipFree(S.d_hstage);
     for (auto e : evs)
         if (e) (void)hipEventDestroy(e);
     for (auto e : S.evW)
@@ -235,6 +240,7 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
     if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
+    if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
 }
 
 static int alloc_slot(hdrf_ctx *ctx, Slot &S)
@@ -267,6 +273,7 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
                               (rc = dalloc(ctx, &S.d_filelen, (size_t)ctx->closed_cap))))
         return rc;
     if (hipEventCreateWithFlags(&S.walk_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.copy_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.front_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
@@ -288,6 +295,7 @@ static int drain(hdrf_ctx *ctx)
     int rc = 0;
     while (ctx->nwait < ctx->nsub)
         if (int r = wait_one(ctx)) rc = rc ? rc : r;
+    HIPCK(hipStreamSynchronize(ctx->stC));
     HIPCK(hipStreamSynchronize(ctx->stW));
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
@@ -355,7 +363,8 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     if (hipSetDevice(c.device) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, pa) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stB, hipStreamNonBlocking, pb) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pa) != hipSuccess) {
+        hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pa) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess) {
         free_all(ctx);
         delete ctx;
         return HDRF_E_HIP;
@@ -485,7 +494,7 @@ static float elapsed(hipEvent_t a, hipEvent_t b)
 
 // Enqueue one batch: front on stream A, back on stream B (see the file comment).
 static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
-                  const uint64_t *readable, const uint64_t *block_ids)
+                  const uint64_t *readable, const uint64_t *block_ids, bool after_copy = false)
 {
     if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)
         if (int rc = wait_one(ctx)) return rc;
@@ -503,6 +512,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     static const int nstreams = [] { const char *e = getenv("HDRF_STREAMS"); return e ? atoi(e) : 2; }();
     hipStream_t W = nstreams == 3 ? ctx->stW : ctx->st, A = ctx->st, Bst = ctx->stB;
     // ---- chunking on W: the slot's previous batch has completed (wait_one ran), so W may overwrite it
+    if (after_copy) HIPCK(hipStreamWaitEvent(W, S.copy_done, 0));
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, W));
     Marker mw;
     mw.ev = ctx->timing ? S.evW : nullptr;
@@ -645,6 +655,54 @@ extern "C" int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
     return submit(ctx, nblocks, dev_data, len, readable, block_ids);
+}
+
+// Host-resident batch: the blocks are copied into the slot's device staging buffer on stream C
+// (hipMemcpyAsync; overlapped with the kernels of the batches in flight when the host memory is
+// pinned), then reduced exactly like hdrf_submit_batch.
+extern "C" int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
+                                const uint64_t *block_ids)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
+    if (nblocks < 1 || nblocks > ctx->max_batch || !host_data || !len) return set_err(ctx, HDRF_E_INVAL, "bad batch arguments");
+    for (int b = 0; b < nblocks; b++) {
+        if ((int64_t)len[b] > ctx->cfg.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
+        if (len[b] && !host_data[b]) return set_err(ctx, HDRF_E_INVAL, "null block data");
+    }
+    if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)
+        if (int rc = wait_one(ctx)) return rc;
+    Slot &S = ctx->sl[ctx->nsub % kSlots];
+    const uint64_t stride = ((uint64_t)ctx->cfg.max_block_bytes + kSlack + 255) & ~(uint64_t)255;
+    if (!S.d_hstage) {                                 // first host batch of this slot
+        HIPCK(hipMalloc((void **)&S.d_hstage, stride * ctx->max_batch));
+        S.hstage_stride = stride;
+    }
+    std::vector<const uint8_t *> ptrs(nblocks);
+    std::vector<uint64_t> rd(nblocks);
+    for (int b = 0; b < nblocks; b++) {
+        uint8_t *d = S.d_hstage + (uint64_t)b * stride;
+        if (len[b]) HIPCK(hipMemcpyAsync(d, host_data[b], len[b], hipMemcpyHostToDevice, ctx->stC));
+        HIPCK(hipMemsetAsync(d + len[b], 0, kSlack, ctx->stC));
+        ptrs[b] = d;
+        rd[b] = stride * (uint64_t)(ctx->max_batch - b);
+    }
+    HIPCK(hipEventRecord(S.copy_done, ctx->stC));
+    return submit(ctx, nblocks, ptrs.data(), len, rd.data(), block_ids, true);
+}
+
+extern "C" int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
+{
+    if (!ctx || !out) return HDRF_E_INVAL;
+    HIPCK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return 0;
+}
+
+extern "C" int hdrf_host_free(hdrf_ctx *ctx, void *p)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (p) HIPCK(hipHostFree(p));
+    return 0;
 }
 
 extern "C" int hdrf_wait_batch(hdrf_ctx *ctx)

@@ -27,7 +27,8 @@ EXPORTS = [
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
-    "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block",
+    "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
+    "hdrf_host_alloc", "hdrf_host_free",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -112,6 +113,9 @@ def load():
         "hdrf_reduce_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
         "hdrf_submit_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
         "hdrf_wait_batch": (ctypes.c_int, [_vp]),
+        "hdrf_submit_host": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p]),
+        "hdrf_host_alloc": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),
+        "hdrf_host_free": (ctypes.c_int, [_vp, _vp]),
         "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
         "hdrf_reconstruct": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_reconstruct_block": (ctypes.c_int64, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
@@ -189,6 +193,7 @@ class Context:
             raise HdrfError(rc, "hdrf_open failed")
         self._h = h
         self.H = self.L.hdrf_digest_len(h)
+        self._pinned = {}
 
     def _ck(self, rc):
         if rc < 0:
@@ -245,6 +250,29 @@ class Context:
         rd = np.ascontiguousarray(readable, np.uint64)
         ids = np.ascontiguousarray(block_ids, np.uint64)
         self._ck(self.L.hdrf_submit_batch(self._h, n, ptrs, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p)))
+
+    def submit_host(self, host_ptrs, lens, block_ids):
+        """Enqueue a batch of HOST-resident blocks (addresses; pinned memory from host_alloc()
+        overlaps the copies with the batches in flight).  The buffers must stay intact until the
+        batch is completed with wait_batch()."""
+        n = len(host_ptrs)
+        ptrs = (_vp * n)(*host_ptrs)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        ids = np.ascontiguousarray(block_ids, np.uint64)
+        self._ck(self.L.hdrf_submit_host(self._h, n, ptrs, _p(ln, _u64p), _p(ids, _u64p)))
+
+    def host_alloc(self, nbytes):
+        """Pinned host buffer as a numpy uint8 array view (free with host_free(array))."""
+        p = _vp()
+        self._ck(self.L.hdrf_host_alloc(self._h, nbytes, ctypes.byref(p)))
+        buf = (ctypes.c_uint8 * max(nbytes, 1)).from_address(p.value)
+        a = np.frombuffer(buf, np.uint8, count=nbytes)
+        self._pinned[a.ctypes.data] = p.value
+        return a
+
+    def host_free(self, a):
+        p = self._pinned.pop(a.ctypes.data)
+        self._ck(self.L.hdrf_host_free(self._h, p))
 
     def wait_batch(self):
         self._ck(self.L.hdrf_wait_batch(self._h))

@@ -97,6 +97,17 @@ int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_
 int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                       const uint64_t *readable, const uint64_t *block_ids);
 int hdrf_wait_batch(hdrf_ctx *ctx);
+/* The streaming DataNode write path (BASELINE config 5; the hook's bf1 handed over at
+ * DN/BlockReceiver.java:1258-1261): host-resident blocks are copied H2D on a side stream
+ * (hipMemcpyAsync from pinned memory overlaps the kernels of the batches in flight) into the
+ * batch slot's staging buffer, then reduced exactly as hdrf_submit_batch.  The host buffers must
+ * stay valid and unmodified until the batch completes (hdrf_wait_batch).  No 16-B alignment or
+ * slack is required of host buffers. */
+int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
+                     const uint64_t *block_ids);
+/* Pinned (page-locked) host memory for hdrf_submit_host buffers. */
+int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out);
+int hdrf_host_free(hdrf_ctx *ctx, void *p);
 /* Number of blocks of the batch hdrf_batch_* report (the last completed one). */
 int hdrf_batch_nblocks(hdrf_ctx *ctx);
 

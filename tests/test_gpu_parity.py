@@ -316,3 +316,51 @@ def test_scheme_plugin_round_trip(compressor):
     with pytest.raises(HdrfError):
         sch.reconstruct(12345)
     sch.close()
+
+
+def test_submit_host_streaming_matches_sequential_oracle():
+    """The streaming write path (hdrf_submit_host, BASELINE config 5): host-resident blocks of
+    ragged lengths, pinned and pageable, copied H2D on the side stream while earlier batches are
+    reduced, give exactly the sequential oracle's results and state."""
+    from hdrf_amd.lib import PIPELINE_DEPTH as D
+    rng = np.random.default_rng(5)
+    base = [make_block(k, 70 + i, 600_000) for i, k in enumerate(["random", "text", "lowent", "binary"])]
+    blocks = []
+    for i in range(15):
+        n = [0, 1, 700, 701, 4097, 333_333, 1_000_003][i % 7]
+        parts = [base[int(rng.integers(4))][int(rng.integers(0, 200_000)):][:n // 2],
+                 make_block("random", 500 + i, n - n // 2)]
+        blocks.append(np.concatenate(parts)[:n])
+    ctx = Context(container_max=1 << 20, **SMALL)
+    ora = Oracle(max_size=1 << 20)
+    pinned = ctx.host_alloc(sum(len(b) for b in blocks) + 1)
+    ptrs, o = [], 0
+    for i, b in enumerate(blocks):
+        if i % 2:                                   # odd blocks from pinned memory, odd offsets
+            pinned[o:o + len(b)] = b
+            ptrs.append(pinned.ctypes.data + o)
+            o += len(b) + 1
+        else:
+            ptrs.append(b.ctypes.data if len(b) else 0)
+    ids = [1000 + i for i in range(len(blocks))]
+    groups = [list(range(s, min(s + 4, len(blocks)))) for s in range(0, len(blocks), 4)]
+    pending = []
+
+    def check(g):
+        for i, b in enumerate(g):
+            compare_block(ctx.batch_result(i), ora.reduce(blocks[b], ids[b]), tag=f"host block {b}")
+
+    for g in groups:
+        if len(pending) == D:
+            ctx.wait_batch()
+            check(pending.pop(0))
+        ctx.submit_host([ptrs[b] for b in g], [len(blocks[b]) for b in g], [ids[b] for b in g])
+        pending.append(g)
+    while pending:
+        ctx.wait_batch()
+        check(pending.pop(0))
+    compare_state(ctx, ora, ids)
+    for i, b in enumerate(blocks):
+        assert np.array_equal(ctx.reconstruct_block(ids[i]), b)
+    ctx.host_free(pinned)
+    ctx.close()
