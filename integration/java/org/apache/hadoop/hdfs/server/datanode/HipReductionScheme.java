@@ -24,6 +24,23 @@ public final class HipReductionScheme extends ReductionScheme {
     reduce0(ctx, block, block.position(), blockId);   // H2D copy happens before return
   }
 
+  /**
+   * Streaming write path (BASELINE config 5): enqueue the received block and return at once; its
+   * H2D copy runs on a side stream overlapped with the blocks already in flight.  `block` must
+   * stay untouched until awaitOldest() has returned for it (keep a reference; BlockReceiver
+   * allocates a fresh bf1 per block).  Completion is in submission order, like the FIFO
+   * (DataDeduplicator.java:124-158).
+   */
+  public void reduceAsync(ByteBuffer block, long blockId) throws IOException {
+    if (!block.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
+    submit0(ctx, block, block.position(), blockId);
+  }
+
+  /** Complete the oldest block submitted with reduceAsync (its index/containers/recipe are final). */
+  public void awaitOldest() throws IOException {
+    wait0(ctx);
+  }
+
   @Override
   public byte[] reconstruct(long blockId) throws IOException {
     return reconstruct0(ctx, blockId);          // DataConstructor(blkID, recipe).data
@@ -47,6 +64,8 @@ public final class HipReductionScheme extends ReductionScheme {
   private static native long open0(int hasher, int compressor, int device, long maxBlockBytes) throws IOException;
   private static native byte[] reconstruct0(long ctx, long blockId) throws IOException;
   private static native void reduce0(long ctx, ByteBuffer direct, int len, long blockId) throws IOException;
+  private static native void submit0(long ctx, ByteBuffer direct, int len, long blockId) throws IOException;
+  private static native void wait0(long ctx) throws IOException;
   private static native long length0(long ctx, long blockId) throws IOException;
   private static native byte[] recipe0(long ctx, long blockId) throws IOException;
   private static native void close0(long ctx);

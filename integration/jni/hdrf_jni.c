@@ -47,6 +47,25 @@ JNIEXPORT void JNICALL JFN(reduce0)(JNIEnv *env, jclass cls, jlong h, jobject bu
     if (rc) throw_io(env, ctx, rc);
 }
 
+/* reduceAsync: hdrf_submit_host on the direct buffer (copied H2D on a side stream) */
+JNIEXPORT void JNICALL JFN(submit0)(JNIEnv *env, jclass cls, jlong h, jobject buf, jint len, jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
+    const uint64_t n = (uint64_t)len, bid = (uint64_t)id;
+    int rc = hdrf_submit_host(ctx, 1, &p, &n, &bid);
+    if (rc) throw_io(env, ctx, rc);
+}
+
+JNIEXPORT void JNICALL JFN(wait0)(JNIEnv *env, jclass cls, jlong h)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int rc = hdrf_wait_batch(ctx);
+    if (rc) throw_io(env, ctx, rc);
+}
+
 JNIEXPORT jlong JNICALL JFN(length0)(JNIEnv *env, jclass cls, jlong h, jlong id)
 {
     (void)cls;
