@@ -691,6 +691,81 @@ extern "C" int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *c
     return submit(ctx, nblocks, ptrs.data(), len, rd.data(), block_ids, true);
 }
 
+static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need);
+
+// Stream mode (compressor 4, DN/BlockReceiver.java:846-855,887-894,1238-1256): the block as
+// Lz4Codec.createOutputStream(file).write(packet) per received packet, then close().  The
+// BlockCompressorStream decisions (hadoop-common 3.1.0) depend only on the write sizes, so the
+// host plans the pieces (groups of buffered packets, or <= MAX_INPUT slices of one large write)
+// and the GPU compresses all pieces of the block at once (one wave per piece), then frames them.
+extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data,
+                                     uint64_t len, uint64_t readable, const uint64_t *writes, int32_t nwrites,
+                                     uint8_t *out, int64_t cap)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (codec != 4) return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: only 4 (Lz4Codec) is implemented");
+    if (nwrites < 0 || (nwrites && !writes) || (len && !dev_data) || readable < len + kSlack)
+        return set_err(ctx, HDRF_E_INVAL, "bad stream arguments (readable must be >= len + 64)");
+    constexpr int64_t kMaxIn = 261100;                  // BlockCompressorStream MAX_INPUT_SIZE
+    std::vector<LzPiece> pieces;
+    std::vector<LzOut> outs;
+    uint64_t off = 0, gs = 0, lim = 0;
+    auto piece = [&](uint64_t src, uint64_t n, uint32_t hval, uint32_t hlen) {
+        pieces.push_back(LzPiece{src, (uint32_t)n, 0});
+        outs.push_back(LzOut{0, hval, hlen});
+    };
+    for (int w = 0; w < nwrites; w++) {
+        const uint64_t n = writes[w];
+        if (lim > 0 && n + lim > (uint64_t)kMaxIn) { piece(gs, lim, (uint32_t)lim, 4); lim = 0; }   // finish()
+        if (n > (uint64_t)kMaxIn) {                                                               // segmented write
+            for (uint64_t o = 0; o < n; o += kMaxIn)
+                piece(off + o, std::min<uint64_t>(kMaxIn, n - o), (uint32_t)n, o == 0 ? 4u : 0u);
+            off += n;
+            continue;
+        }
+        if (lim == 0) gs = off;
+        lim += n;
+        off += n;
+    }
+    if (off != len) return set_err(ctx, HDRF_E_INVAL, "write sizes do not add up to the block length");
+    const bool trailer = lim == 0;                     // close(): BE32 0 when nothing is buffered
+    if (!trailer) piece(gs, lim, (uint32_t)lim, 4);
+    const int n = (int)pieces.size();
+    const uint64_t stride = lz4_piece_stride();
+    const uint64_t a_pieces = 0, a_outs = ((uint64_t)n * sizeof(LzPiece) + 255) & ~255ull;
+    const uint64_t a_clen = a_outs + (((uint64_t)n * sizeof(LzOut) + 255) & ~255ull);
+    const uint64_t a_stage = a_clen + (((uint64_t)n * 4 + 255) & ~255ull);
+    const uint64_t a_file = a_stage + (uint64_t)n * stride;
+    const uint64_t need = a_file + (uint64_t)n * (stride + 8) + 16;
+    if (int rc = drain(ctx)) return rc;
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, need)) return rc;
+    uint8_t *R = ctx->d_rd;
+    hipStream_t st = ctx->st;
+    std::vector<uint32_t> clen(n);
+    if (n) {
+        HIPCK(hipMemcpyAsync(R + a_pieces, pieces.data(), n * sizeof(LzPiece), hipMemcpyHostToDevice, st));
+        HIPCK(launch_lz4_stream((const LzPiece *)(R + a_pieces), n, dev_data, R + a_stage, (uint32_t *)(R + a_clen), st));
+        HIPCK(hipMemcpyAsync(clen.data(), R + a_clen, n * 4, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+    }
+    uint64_t pos = 0;
+    for (int i = 0; i < n; i++) {
+        outs[i].dst = pos;
+        pos += outs[i].hlen + 4 + clen[i];
+    }
+    const int64_t total = (int64_t)pos + (trailer ? 4 : 0);
+    if (!out || cap < total) return set_err(ctx, HDRF_E_CAPACITY, "stream file needs " + std::to_string(total) + " bytes");
+    if (n) {
+        HIPCK(hipMemcpyAsync(R + a_outs, outs.data(), n * sizeof(LzOut), hipMemcpyHostToDevice, st));
+        HIPCK(launch_lz4_emit((const LzOut *)(R + a_outs), n, R + a_stage, (const uint32_t *)(R + a_clen), R + a_file, st));
+        HIPCK(hipMemcpyAsync(out, R + a_file, pos, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+    }
+    if (trailer) std::memset(out + pos, 0, 4);
+    ctx->lengths[(uint32_t)block_id] = (int64_t)len;   // SET id -> BE32(len) (:1238-1256)
+    return total;
+}
+
 extern "C" int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
 {
     if (!ctx || !out) return HDRF_E_INVAL;

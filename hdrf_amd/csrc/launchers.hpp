@@ -79,6 +79,22 @@ hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int
                             uint32_t *tilesum, hipStream_t st);
 hipError_t launch_gx_commit(const uint32_t *x3, const int64_t *counts, int64_t max_count, int64_t cap, int G,
                             IndexEntry *tab, hipStream_t st);
+// stream mode (compressor 4): pieces of one block -> LZ4 blocks (stage) -> framed file
+struct LzPiece {
+    uint64_t src;            // offset in the block
+    uint32_t len;            // <= 261,100
+    uint32_t pad;
+};
+struct LzOut {
+    uint64_t dst;            // offset of the piece's bytes in the file
+    uint32_t hval;           // BE32 word before the size word (raw length), if hlen == 4
+    uint32_t hlen;           // 0 or 4
+};
+hipError_t launch_lz4_stream(const LzPiece *pieces, int n, const uint8_t *base, uint8_t *stage, uint32_t *clen,
+                             hipStream_t st);
+hipError_t launch_lz4_emit(const LzOut *outs, int n, const uint8_t *stage, const uint32_t *clen, uint8_t *file,
+                           hipStream_t st);
+uint64_t lz4_piece_stride();
 // compression stage (lz4.hip): closed containers -> Lz4Codec files in the compressed arena
 uint64_t lz4_slot_bytes(uint32_t cmax);
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,

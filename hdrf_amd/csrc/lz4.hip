@@ -326,6 +326,56 @@ uint64_t lz4_slot_bytes(uint32_t cmax)
     return 16 + nseg * (uint64_t)kLzSegStride;
 }
 
+// ---- stream mode (compressor 4): arbitrary pieces of one block -----------------------------
+// grid n x 64: piece i of the block -> LZ4 block at stage + i * kLzSegStride, size -> clen[i]
+__global__ void __launch_bounds__(64) lz4_list_kernel(const LzPiece *__restrict__ pieces, int n,
+                                                      const uint8_t *__restrict__ base, uint8_t *__restrict__ stage,
+                                                      uint32_t *__restrict__ clen)
+{
+    __shared__ uint32_t tab[4096];
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const LzPiece pc = pieces[i];
+    const int c = lz4_block(base + pc.src, (int)pc.len, stage + (size_t)i * kLzSegStride, tab);
+    if (lane_id() == 0) clen[i] = (uint32_t)c;
+}
+
+// grid n x 256: piece i -> file at its offset: [BE32 hval if hlen] [BE32 clen] [block]
+__global__ void __launch_bounds__(256) lz4_emit_kernel(const LzOut *__restrict__ outs, int n,
+                                                       const uint8_t *__restrict__ stage,
+                                                       const uint32_t *__restrict__ clen, uint8_t *__restrict__ file)
+{
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const LzOut o = outs[i];
+    uint8_t *p = file + o.dst;
+    const int c = (int)clen[i];
+    if (threadIdx.x == 0) {
+        if (o.hlen) put_be32(p, o.hval);
+        put_be32(p + o.hlen, (uint32_t)c);
+    }
+    // four waves copy four quarters of the block
+    const int w = wave_id(), q = (c + 3) / 4;
+    const int a = min(c, w * q), b = min(c, a + q);
+    if (b > a) wave_copy(p + o.hlen + 4 + a, stage + (size_t)i * kLzSegStride + a, b - a);
+}
+
+hipError_t launch_lz4_stream(const LzPiece *pieces, int n, const uint8_t *base, uint8_t *stage, uint32_t *clen,
+                             hipStream_t st)
+{
+    if (n > 0) hipLaunchKernelGGL(lz4_list_kernel, dim3(n), dim3(64), 0, st, pieces, n, base, stage, clen);
+    return hipGetLastError();
+}
+
+hipError_t launch_lz4_emit(const LzOut *outs, int n, const uint8_t *stage, const uint32_t *clen, uint8_t *file,
+                           hipStream_t st)
+{
+    if (n > 0) hipLaunchKernelGGL(lz4_emit_kernel, dim3(n), dim3(256), 0, st, outs, n, stage, clen, file);
+    return hipGetLastError();
+}
+
+uint64_t lz4_piece_stride() { return kLzSegStride; }
+
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
                       const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
                       hipStream_t st)

@@ -28,7 +28,7 @@ EXPORTS = [
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
-    "hdrf_host_alloc", "hdrf_host_free",
+    "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -116,6 +116,8 @@ def load():
         "hdrf_submit_host": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p]),
         "hdrf_host_alloc": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),
         "hdrf_host_free": (ctypes.c_int, [_vp, _vp]),
+        "hdrf_stream_block": (ctypes.c_int64, [_vp, ctypes.c_int32, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                               ctypes.c_uint64, _u64p, ctypes.c_int32, _u8p, ctypes.c_int64]),
         "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
         "hdrf_reconstruct": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_reconstruct_block": (ctypes.c_int64, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
@@ -276,6 +278,17 @@ class Context:
 
     def wait_batch(self):
         self._ck(self.L.hdrf_wait_batch(self._h))
+
+    def stream_block(self, codec, block_id, dev, nbytes, readable, writes):
+        """Stream-mode scheme (compressor 4 = Lz4Codec): the file the reference writes for a block
+        received as write()s of the given sizes -> bytes."""
+        w = np.ascontiguousarray(writes, np.uint64)
+        wp = _p(w if w.size else np.zeros(1, np.uint64), _u64p)
+        cap = 16 + nbytes + nbytes // 200 + 16 * (len(w) + nbytes // 261100 + 2)
+        out = np.zeros(cap, np.uint8)
+        n = self._ck(self.L.hdrf_stream_block(self._h, codec, block_id, dev, nbytes, readable, wp, len(w), _p(out),
+                                              cap))
+        return out[:n].tobytes()
 
     def last_nblocks(self):
         """Blocks of the batch hdrf_batch_* currently report."""

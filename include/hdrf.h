@@ -105,6 +105,14 @@ int hdrf_wait_batch(hdrf_ctx *ctx);
  * slack is required of host buffers. */
 int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
                      const uint64_t *block_ids);
+/* Stream-mode schemes (DataNode.compressor 0/3/4/5: the whole block through a Hadoop codec,
+ * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec: the file the reference writes to
+ * chunkDir+id when the block arrives as write()s of the given sizes (one per packet, summing to
+ * len) followed by close().  dev_data needs len + 64 readable bytes.  Returns the file length
+ * (written to out), HDRF_E_CAPACITY if cap is too small, HDRF_E_UNSUPPORTED for codecs 0/3/5.
+ * Records the block length (SET id -> BE32(len)) for hdrf_block_length. */
+int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data, uint64_t len,
+                          uint64_t readable, const uint64_t *writes, int32_t nwrites, uint8_t *out, int64_t cap);
 /* Pinned (page-locked) host memory for hdrf_submit_host buffers. */
 int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out);
 int hdrf_host_free(hdrf_ctx *ctx, void *p);

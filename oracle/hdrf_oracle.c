@@ -746,6 +746,56 @@ int64_t hdrf_oracle_hadoop_lz4_frame(const uint8_t *src, int64_t n, uint8_t *dst
     return p - dst;
 }
 
+/* Stream mode: BlockCompressorStream.write(b, off, len) per packet (hadoop-common 3.1.0
+ * BlockCompressorStream.java, Lz4Compressor with its 256 KiB buffer):
+ *   limlen = bytes buffered since the last reset
+ *   if (len + limlen > MAX_INPUT && limlen > 0) { finish(); reset(); }
+ *   if (len > MAX_INPUT) { BE32 len; per <= MAX_INPUT piece: BE32 clen, LZ4 block; reset() }
+ *   else buffer (the 262,144-B buffer cannot fill below MAX_INPUT, so needsInput() stays true)
+ * finish() = BE32 limlen, BE32 clen, LZ4 block of the buffered bytes; close() = finish(), which
+ * writes BE32 0 when nothing is buffered (empty block, or a big write last). */
+int64_t hdrf_oracle_hadoop_lz4_stream_bound(int64_t n, int64_t nwrites)
+{
+    return hdrf_oracle_hadoop_lz4_bound(n) + 24 * (nwrites + 1) + 16 * (n / HADOOP_LZ4_MAX_INPUT + 1);
+}
+
+static uint8_t *lz4_group(uint8_t *p, const uint8_t *src, int64_t n)
+{
+    p = put_be32(p, (uint32_t)n);
+    const int64_t c = hdrf_oracle_lz4_compress(src, n, p + 4);
+    put_be32(p, (uint32_t)c);
+    return p + 4 + c;
+}
+
+int64_t hdrf_oracle_hadoop_lz4_stream(const uint8_t *src, const int64_t *writes, int64_t nwrites, uint8_t *dst)
+{
+    uint8_t *p = dst;
+    int64_t off = 0, gs = 0, lim = 0;
+    for (int64_t w = 0; w < nwrites; w++) {
+        const int64_t len = writes[w];
+        if (lim > 0 && len + lim > HADOOP_LZ4_MAX_INPUT) {      /* finish(); compressor.reset() */
+            p = lz4_group(p, src + gs, lim);
+            lim = 0;
+        }
+        if (len > HADOOP_LZ4_MAX_INPUT) {                         /* segmented write */
+            p = put_be32(p, (uint32_t)len);
+            for (int64_t o = 0; o < len; o += HADOOP_LZ4_MAX_INPUT) {
+                const int64_t m = len - o < HADOOP_LZ4_MAX_INPUT ? len - o : HADOOP_LZ4_MAX_INPUT;
+                const int64_t c = hdrf_oracle_lz4_compress(src + off + o, m, p + 4);
+                put_be32(p, (uint32_t)c);
+                p += 4 + c;
+            }
+            off += len;
+            continue;
+        }
+        if (lim == 0) gs = off;
+        lim += len;
+        off += len;
+    }
+    p = lim > 0 ? lz4_group(p, src + gs, lim) : put_be32(p, 0);   /* close() */
+    return p - dst;
+}
+
 /* BlockDecompressorStream over the frame above; returns the decoded length or -1 */
 int64_t hdrf_oracle_hadoop_lz4_unframe(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap)
 {

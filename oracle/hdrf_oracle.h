@@ -69,6 +69,11 @@ int64_t hdrf_oracle_lz4_decompress(const uint8_t *src, int64_t n, uint8_t *dst, 
 int64_t hdrf_oracle_hadoop_lz4_bound(int64_t n);
 int64_t hdrf_oracle_hadoop_lz4_frame(const uint8_t *src, int64_t n, uint8_t *dst);
 int64_t hdrf_oracle_hadoop_lz4_unframe(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+/* Stream mode (compressor == 4, DN/BlockReceiver.java:846-855,887-894,1238-1256): the block goes
+ * through Lz4Codec.createOutputStream(file) as one write() per received packet (sizes `writes`,
+ * summing to the block length), then close().  Decodes with hdrf_oracle_hadoop_lz4_unframe. */
+int64_t hdrf_oracle_hadoop_lz4_stream_bound(int64_t n, int64_t nwrites);
+int64_t hdrf_oracle_hadoop_lz4_stream(const uint8_t *src, const int64_t *writes, int64_t nwrites, uint8_t *dst);
 
 /* Synthetic corpus (shared spec with hdrf_amd corpus generator). */
 uint64_t hdrf_oracle_mix64(uint64_t z);

@@ -65,6 +65,10 @@ def lib():
         for name in ("hdrf_oracle_lz4_compress", "hdrf_oracle_hadoop_lz4_frame"):
             getattr(L, name).argtypes = [_u8p, ctypes.c_int64, _u8p]
             getattr(L, name).restype = ctypes.c_int64
+        L.hdrf_oracle_hadoop_lz4_stream_bound.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        L.hdrf_oracle_hadoop_lz4_stream_bound.restype = ctypes.c_int64
+        L.hdrf_oracle_hadoop_lz4_stream.argtypes = [_u8p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, _u8p]
+        L.hdrf_oracle_hadoop_lz4_stream.restype = ctypes.c_int64
         for name in ("hdrf_oracle_lz4_decompress", "hdrf_oracle_hadoop_lz4_unframe"):
             getattr(L, name).argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
             getattr(L, name).restype = ctypes.c_int64
@@ -155,6 +159,19 @@ def hadoop_lz4(data):
     buf = a if a.size else np.zeros(1, np.uint8)
     out = np.zeros(lib().hdrf_oracle_hadoop_lz4_bound(a.size), np.uint8)
     n = lib().hdrf_oracle_hadoop_lz4_frame(_p(buf), a.size, _p(out))
+    return out[:n].tobytes()
+
+
+def hadoop_lz4_stream(data, writes):
+    """Stream mode (compressor 4): Lz4Codec output stream, one write() per packet of the given
+    sizes, then close() -> file bytes (DN/BlockReceiver.java:846-855,887-894,1238-1256)."""
+    a = _as_u8(data)
+    w = np.ascontiguousarray(writes, np.int64)
+    assert int(w.sum()) == a.size
+    buf = a if a.size else np.zeros(1, np.uint8)
+    out = np.zeros(lib().hdrf_oracle_hadoop_lz4_stream_bound(a.size, w.size), np.uint8)
+    n = lib().hdrf_oracle_hadoop_lz4_stream(_p(buf), w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), w.size,
+                                            _p(out))
     return out[:n].tobytes()
 
 

@@ -364,3 +364,28 @@ def test_submit_host_streaming_matches_sequential_oracle():
         assert np.array_equal(ctx.reconstruct_block(ids[i]), b)
     ctx.host_free(pinned)
     ctx.close()
+
+
+@pytest.mark.parametrize("case", ["packets", "ragged", "single", "empty", "tail_large"])
+def test_stream_mode_lz4_file_matches_oracle(case):
+    """Stream-mode scheme compressor 4 (DN/BlockReceiver.java:846-855,887-894,1238-1256): the GPU
+    writes the oracle's Lz4Codec file byte for byte for every write pattern, and records the
+    block length."""
+    from oracle.oracle import hadoop_lz4_stream
+    n = {"packets": 3_000_000, "ragged": 1_200_000, "single": 700_000, "empty": 0, "tail_large": 900_000}[case]
+    parts = [make_block(k, 80 + i, n // 4 + 1) for i, k in enumerate(["text", "random", "binary", "zeros"])]
+    d = np.concatenate(parts)[:n]
+    writes = {"packets": [64_512] * (n // 64_512) + [n % 64_512],
+              "ragged": [1000, 0, 50_000, 600_000, 249_000, 300_000], "single": [n], "empty": [],
+              "tail_large": [1000, 899_000]}[case]
+    ctx = Context(**SMALL)
+    dev = ctx.dev_alloc(n + 4096)
+    if n:
+        ctx.h2d(dev, d)
+    f = ctx.stream_block(4, 77, dev, n, n + 4096, writes)
+    assert f == hadoop_lz4_stream(d, writes)
+    assert ctx.block_length(77) == n
+    with pytest.raises(HdrfError):
+        ctx.stream_block(5, 78, dev, n, n + 4096, writes)          # gzip: not built
+    ctx.dev_free(dev)
+    ctx.close()

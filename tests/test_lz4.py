@@ -111,3 +111,52 @@ def test_hadoop_framing_structure():
         assert hadoop_lz4_decode(f, n) == data
         if n <= 261_100:
             assert i == len(f)                                 # no trailer for a single segment
+
+
+# ---- stream mode (compressor 4): Lz4Codec output stream fed one write() per packet ----------
+PKT = 64_512          # HDFS packet payload: 126 chunks x 512 B (64 KiB packets incl. checksums)
+
+
+@pytest.mark.parametrize("n", [0, 1, 100, 261_100, 261_101, 600_000])
+def test_stream_single_write_equals_one_shot_frame(n):
+    """One write() of the whole block is exactly the dedup-mode container framing."""
+    from oracle.oracle import hadoop_lz4_stream
+    d = make_block("text", n + 3, n).tobytes()
+    assert hadoop_lz4_stream(d, [n] if n else []) == hadoop_lz4(d)
+
+
+@pytest.mark.parametrize("kind", ["random", "text", "zeros", "binary"])
+def test_stream_packets_structure_and_round_trip(kind):
+    """Packet writes: groups of whole packets up to MAX_INPUT (261,100 B), each
+    [BE32 raw][BE32 clen][block], no trailer; decodes (oracle + framing decoder) to the block."""
+    from oracle.oracle import hadoop_lz4_stream
+    n = 1_500_000
+    d = make_block(kind, 9, n).tobytes()
+    writes = [PKT] * (n // PKT) + ([n % PKT] if n % PKT else [])
+    f = hadoop_lz4_stream(d, writes)
+    assert hadoop_lz4_decode(f, n) == d
+    per = 261_100 // PKT                          # whole packets per group (4)
+    i = o = 0
+    groups = 0
+    while i < len(f):
+        raw = int.from_bytes(f[i:i + 4], "big")
+        c = int.from_bytes(f[i + 4:i + 8], "big")
+        assert raw == min(per * PKT, n - o)
+        assert lz4_block_decode(f[i + 8:i + 8 + c], raw) == d[o:o + raw]
+        i += 8 + c
+        o += raw
+        groups += 1
+    assert o == n and groups == -(-n // (per * PKT))
+
+
+def test_stream_ragged_writes_with_large_write():
+    """Zero-length writes are no-ops; a write > MAX_INPUT flushes the buffered group, is sliced
+    under one BE32 length header, and a trailing large write leaves close()'s BE32 0."""
+    from oracle.oracle import hadoop_lz4_stream
+    d = make_block("lowent", 4, 900_000).tobytes()
+    writes = [1000, 0, 50_000, 600_000, 249_000]
+    f = hadoop_lz4_stream(d, writes)
+    assert hadoop_lz4_decode(f, len(d)) == d
+    assert f[:4] == (51_000).to_bytes(4, "big")                 # first group: 1000 + 0 + 50,000
+    f2 = hadoop_lz4_stream(d, [1000, 899_000])
+    assert f2.endswith(b"\0\0\0\0") and hadoop_lz4_decode(f2, len(d)) == d
