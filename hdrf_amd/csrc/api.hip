@@ -112,6 +112,8 @@ struct hdrf_ctx {
     std::map<uint32_t, uint32_t> slot_owner;         // arena slot -> container id
     std::map<uint32_t, std::vector<uint8_t>> recipes; // longToBytes(blockId,4) -> recipe
     std::map<uint32_t, int64_t> lengths;              // block length (recipe head)
+    struct Loaded { uint8_t *ptr; uint64_t len; };
+    std::map<uint32_t, Loaded> loaded;               // containers loaded back from files (read side)
     // node-global index (gx.hip): scratch aggregation table, owner-side per-record arrays
     int G = 1, rank = 0;
     IndexEntry *d_scratch = nullptr;
@@ -233,6 +235,8 @@ static void free_slot(Slot &S)
 static void free_all(hdrf_ctx *ctx)
 {
     for (auto &S : ctx->sl) free_slot(S);
+    for (auto &kv : ctx->loaded) (void)hipFree(kv.second.ptr);
+    ctx->loaded.clear();
     void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch, ctx->d_gx_counts,
                     ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags, ctx->d_carena};
     for (void *p : ptrs)
@@ -321,6 +325,8 @@ static int init_state(hdrf_ctx *ctx)
     ctx->have_alloc = 0;
     ctx->containers.clear();
     ctx->slot_owner.clear();
+    for (auto &kv : ctx->loaded) (void)hipFree(kv.second.ptr);
+    ctx->loaded.clear();
     ctx->recipes.clear();
     ctx->lengths.clear();
     ctx->last_nblocks = 0;
@@ -764,6 +770,107 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
     if (trailer) std::memset(out + pos, 0, 4);
     ctx->lengths[(uint32_t)block_id] = (int64_t)len;   // SET id -> BE32(len) (:1238-1256)
     return total;
+}
+
+// Hadoop Lz4Codec file (BlockCompressorStream framing: [BE32 raw] ([BE32 clen] block)* groups)
+// -> the LZ4 blocks it holds.  A group's raw length is sliced at MAX_INPUT (261,100), exactly as
+// the stream wrote it; returns false on a malformed frame.
+static bool plan_lz4_frame(const uint8_t *f, int64_t n, std::vector<LzDec> &items, uint64_t *raw_total)
+{
+    constexpr uint64_t kMaxIn = 261100;
+    auto be32 = [&](int64_t i) { return ((uint64_t)f[i] << 24) | ((uint64_t)f[i + 1] << 16) | ((uint64_t)f[i + 2] << 8) | f[i + 3]; };
+    int64_t i = 0;
+    uint64_t o = 0;
+    items.clear();
+    while (i + 4 <= n) {
+        const uint64_t total = be32(i);
+        i += 4;
+        uint64_t got = 0;
+        while (got < total) {
+            if (i + 4 > n) return false;
+            const uint64_t c = be32(i);
+            i += 4;
+            if (i + (int64_t)c > n) return false;
+            const uint64_t raw = std::min(kMaxIn, total - got);
+            items.push_back(LzDec{(uint64_t)i, o + got, (uint32_t)c, (uint32_t)raw});
+            i += (int64_t)c;
+            got += raw;
+        }
+        o += total;
+    }
+    *raw_total = o;
+    return i == n;
+}
+
+// decode a host-resident Lz4Codec file into device memory (dev_out, cap bytes); returns raw length
+static int64_t decode_file(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap)
+{
+    std::vector<LzDec> items;
+    uint64_t raw = 0;
+    if (flen < 0 || (flen && !file) || !plan_lz4_frame(file, flen, items, &raw))
+        return set_err(ctx, HDRF_E_INVAL, "malformed Lz4Codec frame");
+    if ((int64_t)raw > cap || (raw && !dev_out)) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
+    if (items.empty()) return (int64_t)raw;
+    const int n = (int)items.size();
+    const uint64_t o_items = 0, o_err = ((uint64_t)n * sizeof(LzDec) + 255) & ~255ull, o_file = o_err + 256;
+    if (int rc = drain(ctx)) return rc;
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_file + (uint64_t)flen + 64)) return rc;
+    uint8_t *R = ctx->d_rd;
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(R + o_file, file, (size_t)flen, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(R + o_items, items.data(), (size_t)n * sizeof(LzDec), hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(R + o_err, 0, 4, st));
+    HIPCK(launch_lz4_decode((const LzDec *)(R + o_items), n, R + o_file, dev_out, (int *)(R + o_err), st));
+    int err = 0;
+    HIPCK(hipMemcpyAsync(&err, R + o_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (err) return set_err(ctx, HDRF_E_INVAL, "corrupt LZ4 block in the Lz4Codec file");
+    return (int64_t)raw;
+}
+
+// Read side for files: the Lz4Codec input stream DataConstructor opens for closed containers under
+// compressor 2 (DN/DataConstructor.java:495-500) and for stream-mode blocks (:171-176).
+extern "C" int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    return decode_file(ctx, file, flen, dev_out, cap);
+}
+
+// Make container `id` readable for reconstruction from its chunkDir file (raw, or a closed
+// container's Lz4Codec file): a DataNode that restarted, or whose arena slot was reused.
+extern "C" int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4)
+{
+    if (!ctx || flen < 0 || (flen && !file)) return HDRF_E_INVAL;
+    uint64_t raw = (uint64_t)flen;
+    if (lz4) {
+        std::vector<LzDec> items;
+        if (!plan_lz4_frame(file, flen, items, &raw)) return set_err(ctx, HDRF_E_INVAL, "malformed Lz4Codec frame");
+    }
+    if (raw > ctx->cfg.container_max) return set_err(ctx, HDRF_E_INVAL, "container larger than container_max");
+    if (int rc = drain(ctx)) return rc;
+    uint8_t *p = nullptr;
+    HIPCK(hipMalloc((void **)&p, raw + 64));
+    int64_t got = (int64_t)raw;
+    if (lz4) got = decode_file(ctx, file, flen, p, (int64_t)raw);
+    else if (raw) {
+        if (hipMemcpy(p, file, raw, hipMemcpyHostToDevice) != hipSuccess) got = set_err(ctx, HDRF_E_HIP, "H2D copy");
+    }
+    if (got < 0) { (void)hipFree(p); return (int)got; }
+    auto it = ctx->loaded.find(id);
+    if (it != ctx->loaded.end()) (void)hipFree(it->second.ptr);
+    ctx->loaded[id] = hdrf_ctx::Loaded{p, raw};
+    return 0;
+}
+
+extern "C" int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (int rc = drain(ctx)) return rc;
+    auto it = ctx->loaded.find(id);
+    if (it == ctx->loaded.end()) return set_err(ctx, HDRF_E_NOTFOUND, "container not loaded");
+    (void)hipFree(it->second.ptr);
+    ctx->loaded.erase(it);
+    return 0;
 }
 
 extern "C" int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
@@ -1253,32 +1360,40 @@ extern "C" int64_t hdrf_reconstruct(hdrf_ctx *ctx, const uint8_t *recipe, int64_
     const int64_t n = recipe_len / ctx->H;             // t1data.length / hash_length (:223)
     if (size > cap || (size && !dev_out)) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
     if (n == 0) return size == 0 ? 0 : set_err(ctx, HDRF_E_DEVICE, "recipe without digests");
-    // resident containers, sorted by id (std::map order)
-    std::vector<uint32_t> map;
-    for (auto &kv : ctx->containers) map.push_back(kv.first);
-    for (auto &kv : ctx->containers) map.push_back(kv.second.slot);
-    const int ncont = (int)ctx->containers.size();
+    // readable containers sorted by id: arena-resident ones, then those loaded back from files
+    std::map<uint32_t, uint64_t> rdbl;
+    for (auto &kv : ctx->loaded) rdbl[kv.first] = (uint64_t)(uintptr_t)kv.second.ptr;
+    for (auto &kv : ctx->containers)
+        rdbl[kv.first] = (uint64_t)(uintptr_t)(ctx->d_arena + (size_t)kv.second.slot * ctx->cfg.container_max);
+    std::vector<uint32_t> cid;
+    std::vector<uint64_t> base;
+    for (auto &kv : rdbl) { cid.push_back(kv.first); base.push_back(kv.second); }
+    const int ncont = (int)cid.size();
     const uint64_t o_dig = 0, dig_b = (uint64_t)n * ctx->HW * 4;
     const uint64_t o_ch = (dig_b + 255) & ~255ull, ch_b = (uint64_t)n * rd_chunk_bytes();
-    const uint64_t o_map = (o_ch + ch_b + 255) & ~255ull, map_b = (uint64_t)std::max(1, 2 * ncont) * 4;
-    const uint64_t o_tot = (o_map + map_b + 255) & ~255ull;
+    const uint64_t o_base = (o_ch + ch_b + 255) & ~255ull, base_b = (uint64_t)std::max(1, ncont) * 8;
+    const uint64_t o_cid = (o_base + base_b + 255) & ~255ull, cid_b = (uint64_t)std::max(1, ncont) * 4;
+    const uint64_t o_tot = (o_cid + cid_b + 255) & ~255ull;
     if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_tot + 256)) return rc;
     uint8_t *R = ctx->d_rd;
     hipStream_t st = ctx->st;
     HIPCK(hipMemcpyAsync(R + o_dig, recipe + 4, (size_t)n * ctx->H, hipMemcpyHostToDevice, st));
-    if (ncont) HIPCK(hipMemcpyAsync(R + o_map, map.data(), map.size() * 4, hipMemcpyHostToDevice, st));
+    if (ncont) {
+        HIPCK(hipMemcpyAsync(R + o_cid, cid.data(), cid.size() * 4, hipMemcpyHostToDevice, st));
+        HIPCK(hipMemcpyAsync(R + o_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, st));
+    }
     HIPCK(hipMemsetAsync(R + o_tot, 0, 16, st));
-    const uint32_t *cids = (const uint32_t *)(R + o_map);
+    const uint64_t *bases = (const uint64_t *)(R + o_base);
     HIPCK(launch_reconstruct(ctx->cfg.hasher, (const uint32_t *)(R + o_dig), (int)n, ctx->d_tab, ctx->cfg.index_log2,
-                             tag_mask(ctx), cids, cids + ncont, ncont, R + o_ch, (uint64_t *)(R + o_tot), ctx->d_arena,
-                             ctx->cfg.container_max, dev_out, (int *)(R + o_tot + 8), st, false));
+                             tag_mask(ctx), (const uint32_t *)(R + o_cid), bases, ncont, R + o_ch,
+                             (uint64_t *)(R + o_tot), dev_out, (int *)(R + o_tot + 8), st, false));
     uint64_t tot[2] = {0, 0};
     HIPCK(hipMemcpyAsync(tot, R + o_tot, 16, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    if ((int)tot[1]) return set_err(ctx, HDRF_E_NOTFOUND, "a recipe digest or its container is not resident");
+    if ((int)tot[1]) return set_err(ctx, HDRF_E_NOTFOUND, "a recipe digest or its container is not readable");
     if ((int64_t)tot[0] != size) return set_err(ctx, HDRF_E_DEVICE, "chunk lengths do not add up to the recipe size");
-    HIPCK(launch_reconstruct(ctx->cfg.hasher, nullptr, (int)n, nullptr, 0, 0, nullptr, nullptr, 0, R + o_ch, nullptr,
-                             ctx->d_arena, ctx->cfg.container_max, dev_out, nullptr, st, true));
+    HIPCK(launch_reconstruct(ctx->cfg.hasher, nullptr, (int)n, nullptr, 0, 0, nullptr, bases, 0, R + o_ch, nullptr,
+                             dev_out, nullptr, st, true));
     HIPCK(hipStreamSynchronize(st));
     return size;
 }

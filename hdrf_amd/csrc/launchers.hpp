@@ -95,6 +95,11 @@ hipError_t launch_lz4_stream(const LzPiece *pieces, int n, const uint8_t *base, 
 hipError_t launch_lz4_emit(const LzOut *outs, int n, const uint8_t *stage, const uint32_t *clen, uint8_t *file,
                            hipStream_t st);
 uint64_t lz4_piece_stride();
+struct LzDec {               // one LZ4 block of a Lz4Codec file -> raw bytes
+    uint64_t src, dst;       // offsets in the file / in the output
+    uint32_t clen, rawlen;
+};
+hipError_t launch_lz4_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
 // compression stage (lz4.hip): closed containers -> Lz4Codec files in the compressed arena
 uint64_t lz4_slot_bytes(uint32_t cmax);
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
@@ -103,9 +108,8 @@ hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int clos
 // read side (read.hip): lookup + scan (gather = false), then the copy (gather = true)
 size_t rd_chunk_bytes();
 hipError_t launch_reconstruct(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
-                              unsigned long long tag_mask, const uint32_t *cids, const uint32_t *slots, int ncont,
-                              void *chunks, uint64_t *total, const uint8_t *arena, uint64_t cmax, uint8_t *out,
-                              int *err, hipStream_t st, bool gather);
+                              unsigned long long tag_mask, const uint32_t *cids, const uint64_t *bases, int ncont,
+                              void *chunks, uint64_t *total, uint8_t *out, int *err, hipStream_t st, bool gather);
 hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
                          uint64_t seed, int mixed, hipStream_t st);
 

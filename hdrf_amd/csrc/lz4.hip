@@ -360,6 +360,93 @@ __global__ void __launch_bounds__(256) lz4_emit_kernel(const LzOut *__restrict__
     if (b > a) wave_copy(p + o.hlen + 4 + a, stage + (size_t)i * kLzSegStride + a, b - a);
 }
 
+// ---- decoder (read side: DataConstructor's Lz4Codec input stream, DN/DataConstructor.java:
+//      171-176,495-500): one wave per LZ4 block.  The sequence headers are parsed from an 8 KiB
+//      LDS window of the compressed stream (refilled with coalesced loads), literals and matches
+//      are wave-wide copies; a match may read output written moments before, so each match is
+//      preceded by a fence.  Malformed input (bounds, zero offset, wrong decoded size) sets *err.
+constexpr int kDecWin = 8192;
+
+__global__ void __launch_bounds__(64) lz4_decode_kernel(const LzDec *__restrict__ items, int n,
+                                                        const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                        int *__restrict__ err)
+{
+    __shared__ uint8_t win[kDecWin];
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const LzDec d = items[i];
+    const uint8_t *in = src + d.src;
+    uint8_t *out = dst + d.dst;
+    const int64_t iend = d.clen, oend = d.rawlen;
+    const int l = lane_id();
+    int64_t wbase = -kDecWin;                            // window covers in[wbase, wbase + kDecWin)
+    auto byte = [&](int64_t pos) -> uint32_t {          // wave-uniform pos < iend
+        if (pos >= wbase + kDecWin) {
+            wbase = pos & ~(int64_t)15;
+            __builtin_amdgcn_s_waitcnt(0);
+            asm volatile("" ::: "memory");
+            for (int k = l * 16; k < kDecWin; k += 64 * 16) {
+                const int64_t g = wbase + k;
+                for (int b = 0; b < 16; b++) win[k + b] = g + b < iend ? rd8(in + g + b) : 0u;
+            }
+            __builtin_amdgcn_s_waitcnt(0);
+            asm volatile("" ::: "memory");
+        }
+        return win[pos - wbase];
+    };
+    int64_t ip = 0, op = 0;
+    bool bad = false;
+    for (;;) {
+        if (ip >= iend) { bad = true; break; }
+        const uint32_t token = byte(ip++);
+        int64_t lit = token >> 4;
+        if (lit == 15) {
+            uint32_t b;
+            do {
+                if (ip >= iend) { bad = true; break; }
+                b = byte(ip++);
+                lit += b;
+            } while (b == 255);
+            if (bad) break;
+        }
+        if (ip + lit > iend || op + lit > oend) { bad = true; break; }
+        wave_copy(out + op, in + ip, (int)lit);
+        ip += lit;
+        op += lit;
+        if (ip == iend) break;                           // the last sequence has literals only
+        if (ip + 2 > iend) { bad = true; break; }
+        const int64_t off = (int64_t)byte(ip) | ((int64_t)byte(ip + 1) << 8);
+        ip += 2;
+        int64_t ml = token & 15;
+        if (ml == 15) {
+            uint32_t b;
+            do {
+                if (ip >= iend) { bad = true; break; }
+                b = byte(ip++);
+                ml += b;
+            } while (b == 255);
+            if (bad) break;
+        }
+        ml += 4;
+        if (off == 0 || off > op || op + ml > oend) { bad = true; break; }
+        __threadfence();
+        if (off >= ml) {
+            wave_copy(out + op, out + op - off, (int)ml);
+        } else {                                         // overlapping: the last `off` bytes repeat
+            for (int64_t k = l; k < ml; k += 64) wr8(out + op + k, rd8(out + op - off + (k % off)));
+        }
+        __threadfence();
+        op += ml;
+    }
+    if ((bad || op != oend) && l == 0) atomicOr(err, 1);
+}
+
+hipError_t launch_lz4_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st)
+{
+    if (n > 0) hipLaunchKernelGGL(lz4_decode_kernel, dim3(n), dim3(64), 0, st, items, n, src, dst, err);
+    return hipGetLastError();
+}
+
 hipError_t launch_lz4_stream(const LzPiece *pieces, int n, const uint8_t *base, uint8_t *stage, uint32_t *clen,
                              hipStream_t st)
 {

@@ -8,7 +8,8 @@
 // data[bbStart, bbStop) (:474-531).
 //
 //   rd_lookup — one lane per chunk: probe the index (same open addressing as index.hip), decode
-//               (container id, start, stop), and the arena slot of the container
+//               (container id, start, stop), and the readable copy of the container (an arena
+//               slot, or a container loaded back from its file with hdrf_container_load)
 //   rd_scan   — one workgroup: exclusive prefix of the chunk lengths (block offsets) + total
 //   rd_gather — one wave per chunk: 16-B-per-lane copy arena -> output block
 #include "launchers.hpp"
@@ -16,7 +17,7 @@
 namespace hdrf {
 
 struct RdChunk {
-    uint32_t slot;       // arena slot of the container (0xffffffff: digest or container missing)
+    uint32_t slot;       // index of the container in the readable list (0xffffffff: missing)
     uint32_t start, len;
     uint32_t off;        // offset in the rebuilt block
 };
@@ -25,8 +26,7 @@ template <int HW>
 __global__ void __launch_bounds__(256) rd_lookup_kernel(const uint32_t *__restrict__ dig, int n,
                                                         const IndexEntry *__restrict__ tab, int log2cap,
                                                         unsigned long long tag_mask, const uint32_t *__restrict__ cids,
-                                                        const uint32_t *__restrict__ slots, int ncont,
-                                                        RdChunk *__restrict__ out, int *__restrict__ err)
+                                                        int ncont, RdChunk *__restrict__ out, int *__restrict__ err)
 {
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
@@ -52,12 +52,12 @@ __global__ void __launch_bounds__(256) rd_lookup_kernel(const uint32_t *__restri
             found = true;
             r.start = e.start;
             r.len = e.stop - e.start;                  // chunkMeta.length = blockStop - blockStart
-            int lo = 0, hi = ncont;                   // resident container -> arena slot
+            int lo = 0, hi = ncont;                   // readable container list, sorted by id
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
                 if (cids[mid] < e.cid) lo = mid + 1; else hi = mid;
             }
-            if (lo < ncont && cids[lo] == e.cid) r.slot = slots[lo];
+            if (lo < ncont && cids[lo] == e.cid) r.slot = (uint32_t)lo;
             break;
         }
         h = (h + 1) & mask;
@@ -96,14 +96,13 @@ __global__ void __launch_bounds__(1024) rd_scan_kernel(RdChunk *__restrict__ c, 
 
 // grid ceil(n/4) x 256: wave w of the workgroup copies chunk 4*blockIdx.x + w
 __global__ void __launch_bounds__(256) rd_gather_kernel(const RdChunk *__restrict__ c, int n,
-                                                        const uint8_t *__restrict__ arena, uint64_t cmax,
-                                                        uint8_t *__restrict__ out)
+                                                        const uint64_t *__restrict__ bases, uint8_t *__restrict__ out)
 {
     const int k = blockIdx.x * 4 + wave_id();
     if (k >= n) return;
     const RdChunk r = c[k];
     if (r.slot == 0xffffffffu) return;
-    const uint8_t *src = arena + (size_t)r.slot * cmax + r.start;
+    const uint8_t *src = (const uint8_t *)(uintptr_t)bases[r.slot] + r.start;
     uint8_t *dst = out + r.off;
     const int l = lane_id();
     const uint32_t len = r.len;
@@ -121,23 +120,22 @@ __global__ void __launch_bounds__(256) rd_gather_kernel(const RdChunk *__restric
 }
 
 hipError_t launch_reconstruct(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
-                              unsigned long long tag_mask, const uint32_t *cids, const uint32_t *slots, int ncont,
-                              void *chunks, uint64_t *total, const uint8_t *arena, uint64_t cmax, uint8_t *out,
-                              int *err, hipStream_t st, bool gather)
+                              unsigned long long tag_mask, const uint32_t *cids, const uint64_t *bases, int ncont,
+                              void *chunks, uint64_t *total, uint8_t *out, int *err, hipStream_t st, bool gather)
 {
     RdChunk *c = (RdChunk *)chunks;
     if (n <= 0) return hipSuccess;
     if (!gather) {
         const dim3 g((n + 255) / 256);
         if (hasher == 0)
-            hipLaunchKernelGGL(rd_lookup_kernel<5>, g, dim3(256), 0, st, dig, n, tab, log2cap, tag_mask, cids, slots,
-                               ncont, c, err);
+            hipLaunchKernelGGL(rd_lookup_kernel<5>, g, dim3(256), 0, st, dig, n, tab, log2cap, tag_mask, cids, ncont, c,
+                               err);
         else
-            hipLaunchKernelGGL(rd_lookup_kernel<7>, g, dim3(256), 0, st, dig, n, tab, log2cap, tag_mask, cids, slots,
-                               ncont, c, err);
+            hipLaunchKernelGGL(rd_lookup_kernel<7>, g, dim3(256), 0, st, dig, n, tab, log2cap, tag_mask, cids, ncont, c,
+                               err);
         hipLaunchKernelGGL(rd_scan_kernel, dim3(1), dim3(1024), 0, st, c, n, total);
     } else {
-        hipLaunchKernelGGL(rd_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, st, c, n, arena, cmax, out);
+        hipLaunchKernelGGL(rd_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, st, c, n, bases, out);
     }
     return hipGetLastError();
 }

@@ -28,7 +28,8 @@ EXPORTS = [
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
-    "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block",
+    "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_lz4_file_decode", "hdrf_container_load",
+    "hdrf_container_unload",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -116,6 +117,9 @@ def load():
         "hdrf_submit_host": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p]),
         "hdrf_host_alloc": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),
         "hdrf_host_free": (ctypes.c_int, [_vp, _vp]),
+        "hdrf_lz4_file_decode": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
+        "hdrf_container_load": (ctypes.c_int, [_vp, ctypes.c_uint32, _u8p, ctypes.c_int64, ctypes.c_int32]),
+        "hdrf_container_unload": (ctypes.c_int, [_vp, ctypes.c_uint32]),
         "hdrf_stream_block": (ctypes.c_int64, [_vp, ctypes.c_int32, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                                ctypes.c_uint64, _u64p, ctypes.c_int32, _u8p, ctypes.c_int64]),
         "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
@@ -278,6 +282,25 @@ class Context:
 
     def wait_batch(self):
         self._ck(self.L.hdrf_wait_batch(self._h))
+
+    def lz4_file_decode(self, file, raw_cap):
+        """Decode a Hadoop Lz4Codec file on the GPU -> raw bytes."""
+        f = _u8(file)
+        dev = self.dev_alloc(raw_cap + 64)
+        try:
+            n = self._ck(self.L.hdrf_lz4_file_decode(self._h, _p(f if f.size else np.zeros(1, np.uint8)), f.size,
+                                                     dev, raw_cap))
+            return self.d2h(dev, n).tobytes() if n else b""
+        finally:
+            self.dev_free(dev)
+
+    def container_load(self, cid, file, lz4):
+        f = _u8(file)
+        self._ck(self.L.hdrf_container_load(self._h, cid, _p(f if f.size else np.zeros(1, np.uint8)), f.size,
+                                            1 if lz4 else 0))
+
+    def container_unload(self, cid):
+        self._ck(self.L.hdrf_container_unload(self._h, cid))
 
     def stream_block(self, codec, block_id, dev, nbytes, readable, writes):
         """Stream-mode scheme (compressor 4 = Lz4Codec): the file the reference writes for a block

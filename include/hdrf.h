@@ -113,6 +113,16 @@ int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_
  * Records the block length (SET id -> BE32(len)) for hdrf_block_length. */
 int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data, uint64_t len,
                           uint64_t readable, const uint64_t *writes, int32_t nwrites, uint8_t *out, int64_t cap);
+/* Read side for container / block FILES (DataConstructor's Lz4Codec input stream,
+ * DN/DataConstructor.java:171-176,495-500): hdrf_lz4_file_decode decodes a Hadoop Lz4Codec file
+ * (BlockCompressorStream framing, as written by compressor 2 containers and compressor 4 blocks)
+ * on the GPU into dev_out; returns the raw length (HDRF_E_INVAL on a malformed file).
+ * hdrf_container_load makes container `id` readable for hdrf_reconstruct* again from its chunkDir
+ * file (lz4 = 1 for a closed container's Lz4Codec file, 0 for raw bytes) after its arena slot was
+ * reused or the DataNode restarted; hdrf_container_unload frees that copy. */
+int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap);
+int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4);
+int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id);
 /* Pinned (page-locked) host memory for hdrf_submit_host buffers. */
 int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out);
 int hdrf_host_free(hdrf_ctx *ctx, void *p);

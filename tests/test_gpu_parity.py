@@ -389,3 +389,63 @@ def test_stream_mode_lz4_file_matches_oracle(case):
         ctx.stream_block(5, 78, dev, n, n + 4096, writes)          # gzip: not built
     ctx.dev_free(dev)
     ctx.close()
+
+
+@pytest.mark.parametrize("kind", ["random", "text", "zeros", "lowent", "binary", "periodic"])
+def test_lz4_file_decode_round_trip(kind):
+    """GPU Lz4Codec decoder (read side, DN/DataConstructor.java:171-176,495-500): the oracle's
+    container framing and stream-mode framing (packet writes, a large write) decode to the raw
+    bytes; a corrupted file is rejected."""
+    from oracle.oracle import hadoop_lz4, hadoop_lz4_stream
+    n = 1_300_000
+    d = make_block(kind, 31, n).tobytes()
+    ctx = Context(**SMALL)
+    for f in (hadoop_lz4(d), hadoop_lz4(d[:5000]), hadoop_lz4(b""),
+              hadoop_lz4_stream(d, [64_512] * (n // 64_512) + [n % 64_512]),
+              hadoop_lz4_stream(d, [1000, 700_000, n - 701_000])):
+        out = ctx.lz4_file_decode(f, n)
+        assert out == d[:len(out)] and len(out) in (0, 5000, n)
+    good = hadoop_lz4(d)
+    for bad in (good[:-1],                            # truncated
+                good[:4] + (int.from_bytes(good[4:8], "big") - 1).to_bytes(4, "big") + good[8:-1],   # short block
+                good[:4] + b"\x7f\xff\xff\xff" + good[8:]):      # block length past the end
+        with pytest.raises(HdrfError):
+            ctx.lz4_file_decode(bad, n)
+    ctx.close()
+
+
+def test_reconstruct_from_loaded_container_files():
+    """A context whose arena slots were reused (small arena) cannot rebuild early blocks from
+    device memory; after loading the chunkDir files of the missing containers (closed ones as
+    Lz4Codec files, decoded on the GPU) every block reconstructs byte for byte."""
+    cmax = 1 << 20
+    blocks = [make_block(["random", "text", "binary"][i % 3], 600 + i, 900_000) for i in range(14)]
+    ctx = Context(compressor=2, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=2, index_log2=20,
+                  arena_slots=12)
+    ora = Oracle(compressor=2, max_size=cmax)
+    for i, b in enumerate(blocks):
+        ctx.reduce_block(b, 40 + i)
+        ora.reduce(b, 40 + i)
+    missing = []
+    for i, b in enumerate(blocks):
+        try:
+            assert np.array_equal(ctx.reconstruct_block(40 + i), b)
+        except HdrfError:
+            missing.append(i)
+    assert missing, "the small arena should have evicted early containers"
+    alloc = ora.allocator()
+    loaded = 0
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            data, closed = ora.container(cid)
+            if data is None:
+                continue
+            gd, _ = ctx.container(cid)
+            if gd is None:                              # not resident any more: load its file
+                ctx.container_load(cid, data, closed)
+                loaded += 1
+    assert loaded > 0
+    for i in missing:
+        assert np.array_equal(ctx.reconstruct_block(40 + i), blocks[i]), f"block {i}"
+    ctx.close()
