@@ -202,6 +202,14 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     stage_ms = ctx.stage_times(reset=True)
+    alone_ms = None
+    if node is None and not a.serial and not host:
+        # one extra, untimed serial pass (one batch at a time): the same kernels without the
+        # co-running batch, for the per-kernel "alone" rooflines next to the in-pipeline ones
+        ctx.reset()
+        for ptrs, lens, rd, ids in batches:
+            ctx.reduce_batch(ptrs, lens, rd, ids)
+        alone_ms = ctx.stage_times(reset=True)
     if dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -239,6 +247,22 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": prof.get("hbm_bytes_per_launch"), "traffic_source": pmc_src,
                 "avg_launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(per_launch[dom])}
+    if alone_ms is not None:
+        # per-kernel figures of the untimed serial pass (not part of `value`)
+        ra = {}
+        for name in per_launch:
+            ms = alone_ms[STAGES.index(name)] / nbatch
+            if ms > 0:
+                ach = per_launch[name] / (ms * 1e-3) / 1e9
+                ra[name] = {"avg_launch_ms": round(ms, 4), "achieved_GB_s": round(ach, 1),
+                            "frac_hbm": round(ach / HBM_PEAK_GBS, 4)}
+                sha_prof = pmc.get(KERNEL_OF[name] + ("<5>" if a.hasher == 0 else "<7>"), {})
+                if name == STAGES[2] and sha_prof.get("sq_insts_valu"):
+                    wi_ns = sha_prof["sq_insts_valu"] / (ms * 1e6)
+                    ra[name]["valu_frac"] = round(wi_ns / VALU_PEAK_WI_NS, 4)
+        roofline["alone"] = ra
+        roofline["alone_note"] = ("same kernels in one untimed serial pass (one batch at a time); the "
+                                  "in-pipeline figures above include co-running batches")
     if dom == STAGES[2] and prof.get("sq_insts_valu"):
         # SHA is integer-VALU bound: wave-instructions per launch (PMC SQ_INSTS_VALU) over the
         # measured launch time, against the full-rate v_add_u32 peak (profiles/r01_valu_peak.txt)

@@ -1303,6 +1303,77 @@ extern "C" int hdrf_allocator(hdrf_ctx *ctx, uint8_t out24[24])
     return 1;
 }
 
+// ---- restore (index persistence: a DataNode restarting on its Redis dump + chunkDir) -------
+// SET digest -> value for n entries (the rows of hdrf_index_dump) on a context whose index does
+// not hold these digests yet (a fresh or reset context).
+extern "C" int hdrf_index_load(hdrf_ctx *ctx, const uint8_t *keys, const uint8_t *vals, int64_t n)
+{
+    if (!ctx || n < 0 || (n && (!keys || !vals))) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "restore on node-global contexts: not yet");
+    if (int rc = drain(ctx)) return rc;
+    if (n == 0) return 0;
+    const uint64_t o_dw = 0, dw_b = (uint64_t)n * ctx->HW * 4;
+    const uint64_t o_v = (dw_b + 255) & ~255ull, o_err = (o_v + (uint64_t)n * 11 + 255) & ~255ull;
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_err + 256)) return rc;
+    uint8_t *R = ctx->d_rd;
+    hipStream_t st = ctx->st;
+    std::vector<uint8_t> dw(dw_b, 0);                  // digest bytes as u32 words (SHA-224: 28 B)
+    for (int64_t k = 0; k < n; k++) std::memcpy(dw.data() + (size_t)k * ctx->HW * 4, keys + (size_t)k * ctx->H, ctx->H);
+    HIPCK(hipMemcpyAsync(R + o_dw, dw.data(), dw_b, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(R + o_v, vals, (size_t)n * 11, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(R + o_err, 0, 4, st));
+    HIPCK(launch_index_load(ctx->cfg.hasher, (const uint32_t *)(R + o_dw), R + o_v, (int)n, ctx->d_tab,
+                            ctx->cfg.index_log2, tag_mask(ctx), (int *)(R + o_err), st));
+    int err = 0;
+    HIPCK(hipMemcpyAsync(&err, R + o_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (err) return set_err(ctx, HDRF_E_CAPACITY, "index table full (index_log2 too small)");
+    return 0;
+}
+
+// SET "blockID" (the 24-B allocator, DN/utilities.java:66-75) and reopen the three storer
+// ranges' open containers from their chunkDir files (open_len[t] < 0: no file): the storer
+// appends to them exactly as threadedStorer does after reading prevData (:723-737).
+extern "C" int hdrf_allocator_load(hdrf_ctx *ctx, const uint8_t alloc24[24], const uint8_t *const *open_files,
+                                   const int64_t *open_len)
+{
+    if (!ctx || !alloc24 || !open_len) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "restore on node-global contexts: not yet");
+    if (int rc = drain(ctx)) return rc;
+    AllocState a{};
+    for (int i = 0; i < 8; i++) {
+        const uint32_t v = ((uint32_t)alloc24[3 * i] << 16) | ((uint32_t)alloc24[3 * i + 1] << 8) | alloc24[3 * i + 2];
+        if (i < 4) a.id[i] = v; else a.pos[i - 4] = v;
+    }
+    for (int t = 0; t < 4; t++) a.slot[t] = (uint32_t)t * (uint32_t)(ctx->cfg.arena_slots / 4);
+    for (int t = 0; t < ctx->cfg.n_thread; t++) {
+        if (open_len[t] < 0) continue;
+        if ((uint64_t)open_len[t] > ctx->cfg.container_max || (open_len[t] && (!open_files || !open_files[t])))
+            return set_err(ctx, HDRF_E_INVAL, "bad open container file");
+        if (open_len[t])
+            HIPCK(hipMemcpy(ctx->d_arena + (size_t)a.slot[t] * ctx->cfg.container_max, open_files[t],
+                            (size_t)open_len[t], hipMemcpyHostToDevice));
+        a.cur[t] = (uint32_t)open_len[t];
+        a.exists[t] = 1;
+    }
+    HIPCK(hipMemcpy(ctx->d_alloc, &a, sizeof a, hipMemcpyHostToDevice));
+    ctx->h_alloc = a;
+    ctx->have_alloc = 1;
+    for (int t = 0; t < ctx->cfg.n_thread; t++)
+        if (a.exists[t]) note_container(ctx, a.id[t], a.slot[t], a.cur[t], 0);
+    return 0;
+}
+
+// SET longToBytes(blockId,4) -> recipe (storeDB, DN/DataDeduplicator.java:372-392)
+extern "C" int hdrf_recipe_load(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *recipe, int64_t len)
+{
+    if (!ctx || !recipe || len < 4 || (len - 4) % ctx->H) return HDRF_E_INVAL;
+    const uint32_t key = (uint32_t)block_id;
+    ctx->recipes[key].assign(recipe, recipe + len);
+    ctx->lengths[key] = ((int64_t)recipe[0] << 24) | (recipe[1] << 16) | (recipe[2] << 8) | recipe[3];
+    return 0;
+}
+
 extern "C" int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap)
 {
     if (!ctx) return HDRF_E_INVAL;

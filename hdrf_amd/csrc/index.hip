@@ -253,6 +253,56 @@ __global__ void __launch_bounds__(256) idx_clear_kernel(u32x4 *__restrict__ p, u
     if (blockIdx.x == 0 && threadIdx.x == 0) *alloc = a;
 }
 
+// Restore (a Redis dump of the index: digest -> 11-byte chunkMeta value): one thread per entry,
+// claim the first empty slot of the digest's probe sequence, then fill the entry at rest (no
+// batch-local state; batch 0 precedes every batch the context will run).  Digests are unique.
+template <int HW>
+__global__ void __launch_bounds__(256) idx_load_kernel(const uint32_t *__restrict__ dw_all,
+                                                       const uint8_t *__restrict__ vals, int n,
+                                                       IndexEntry *__restrict__ tab, int log2cap,
+                                                       unsigned long long tag_mask, int *__restrict__ err)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    uint32_t dw[HW];
+#pragma unroll
+    for (int i = 0; i < HW; i++) dw[i] = dw_all[(size_t)k * HW + i];
+    unsigned long long tag = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
+    const uint32_t z = tag == 0 ? 0x80000000u : 0u;
+    if (tag == 0) tag = 1;
+    const uint64_t mask = (1ull << log2cap) - 1;
+    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
+    for (uint64_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
+        if (atomicCAS(&tab[h].tag, kEmptyTag, tag) != kEmptyTag) continue;
+        IndexEntry &e = tab[h];
+        const uint8_t *v = vals + (size_t)k * 11;           // chunkMeta.process, DN/chunkMeta.java:35-60
+        e.mask = 0;
+        e.first = 0;
+        e.batch = z;
+        e.ncopy = v[0];
+        e.cid = ((uint32_t)v[1] << 16) | ((uint32_t)v[2] << 8) | v[3];
+        e.start = ((uint32_t)v[4] << 16) | ((uint32_t)v[5] << 8) | v[6] | ((uint32_t)(v[10] & 0xF0) << 20);
+        e.stop = ((uint32_t)v[7] << 16) | ((uint32_t)v[8] << 8) | v[9] | ((uint32_t)(v[10] & 0x0F) << 24);
+#pragma unroll
+        for (int i = 2; i < HW; i++) e.dig[i - 2] = dw[i];
+        if (HW == 5) { e.dig[3] = dw[0]; e.dig[4] = dw[1]; }
+        return;
+    }
+    atomicOr(err, 2);                                       // table full
+}
+
+hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals, int n, IndexEntry *tab, int log2cap,
+                             unsigned long long tag_mask, int *err, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    const dim3 g((n + 255) / 256);
+    if (hasher == 0)
+        hipLaunchKernelGGL(idx_load_kernel<5>, g, dim3(256), 0, st, dw, vals, n, tab, log2cap, tag_mask, err);
+    else
+        hipLaunchKernelGGL(idx_load_kernel<7>, g, dim3(256), 0, st, dw, vals, n, tab, log2cap, tag_mask, err);
+    return hipGetLastError();
+}
+
 hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st)
 {
     const uint64_t n16 = (sizeof(IndexEntry) << log2cap) / 16;

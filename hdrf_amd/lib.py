@@ -29,7 +29,7 @@ EXPORTS = [
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
     "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_lz4_file_decode", "hdrf_container_load",
-    "hdrf_container_unload",
+    "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -120,6 +120,9 @@ def load():
         "hdrf_lz4_file_decode": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_container_load": (ctypes.c_int, [_vp, ctypes.c_uint32, _u8p, ctypes.c_int64, ctypes.c_int32]),
         "hdrf_container_unload": (ctypes.c_int, [_vp, ctypes.c_uint32]),
+        "hdrf_index_load": (ctypes.c_int, [_vp, _u8p, _u8p, ctypes.c_int64]),
+        "hdrf_allocator_load": (ctypes.c_int, [_vp, _u8p, ctypes.POINTER(_vp), _i64p]),
+        "hdrf_recipe_load": (ctypes.c_int, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
         "hdrf_stream_block": (ctypes.c_int64, [_vp, ctypes.c_int32, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                                ctypes.c_uint64, _u64p, ctypes.c_int32, _u8p, ctypes.c_int64]),
         "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
@@ -301,6 +304,26 @@ class Context:
 
     def container_unload(self, cid):
         self._ck(self.L.hdrf_container_unload(self._h, cid))
+
+    # ---- restore (index persistence) --------------------------------------------------------
+    def index_load(self, keys, vals):
+        k = np.ascontiguousarray(keys, np.uint8).reshape(-1)
+        v = np.ascontiguousarray(vals, np.uint8).reshape(-1)
+        n = v.size // 11
+        self._ck(self.L.hdrf_index_load(self._h, _p(k if k.size else np.zeros(1, np.uint8)),
+                                        _p(v if v.size else np.zeros(1, np.uint8)), n))
+
+    def allocator_load(self, alloc24, open_files):
+        """open_files[t]: bytes of storer range t's open container file, or None."""
+        a = np.frombuffer(bytes(alloc24), np.uint8).copy()
+        bufs = [np.frombuffer(f, np.uint8).copy() if f else np.zeros(1, np.uint8) for f in open_files]
+        ptrs = (_vp * len(bufs))(*[b.ctypes.data for b in bufs])
+        lens = np.array([len(f) if f is not None else -1 for f in open_files], np.int64)
+        self._ck(self.L.hdrf_allocator_load(self._h, _p(a), ptrs, _p(lens, _i64p)))
+
+    def recipe_load(self, block_id, recipe):
+        r = np.frombuffer(bytes(recipe), np.uint8).copy()
+        self._ck(self.L.hdrf_recipe_load(self._h, block_id, _p(r), r.size))
 
     def stream_block(self, codec, block_id, dev, nbytes, readable, writes):
         """Stream-mode scheme (compressor 4 = Lz4Codec): the file the reference writes for a block

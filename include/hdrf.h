@@ -123,6 +123,16 @@ int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const
 int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap);
 int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4);
 int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id);
+/* Restore a DataNode from its persisted state (the Redis keys + chunkDir files), on a fresh or
+ * reset context: hdrf_index_load SETs digest -> 11-B value for n rows (keys n*H bytes, vals n*11,
+ * e.g. the output of hdrf_index_dump); hdrf_allocator_load SETs "blockID" (24 B, as returned by
+ * hdrf_allocator) and reopens each storer range's open container from its file (open_len[t] < 0:
+ * no file); hdrf_recipe_load SETs longToBytes(id,4) -> recipe.  Blocks reduced afterwards, and
+ * their containers, are those of a DataNode that never stopped. */
+int hdrf_index_load(hdrf_ctx *ctx, const uint8_t *keys, const uint8_t *vals, int64_t n);
+int hdrf_allocator_load(hdrf_ctx *ctx, const uint8_t alloc24[24], const uint8_t *const *open_files,
+                        const int64_t *open_len);
+int hdrf_recipe_load(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *recipe, int64_t len);
 /* Pinned (page-locked) host memory for hdrf_submit_host buffers. */
 int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out);
 int hdrf_host_free(hdrf_ctx *ctx, void *p);

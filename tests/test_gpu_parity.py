@@ -449,3 +449,61 @@ def test_reconstruct_from_loaded_container_files():
     for i in missing:
         assert np.array_equal(ctx.reconstruct_block(40 + i), blocks[i]), f"block {i}"
     ctx.close()
+
+
+@pytest.mark.parametrize("hasher,compressor", [(0, 1), (1, 2)])
+def test_restart_from_persisted_state(hasher, compressor):
+    """Index persistence: a second context restored from the first one's Redis
+    state (index rows, "blockID" allocator, recipes) and the open containers' chunkDir files
+    continues exactly like a DataNode that never stopped: later blocks dedup against the restored
+    index, append to the reopened containers, and every value, container, recipe and the
+    allocator match the sequential oracle; old blocks reconstruct once their files are loaded."""
+    cmax = 1 << 20
+    rng = np.random.default_rng(3)
+    base = [make_block(k, 90 + i, 800_000) for i, k in enumerate(["random", "text", "binary"])]
+    blocks = []
+    for i in range(14):
+        parts = [base[int(rng.integers(3))][int(rng.integers(0, 300_000)):][:250_000] for _ in range(2)]
+        blocks.append(np.concatenate(parts + [make_block("random", 700 + i, 300_000)]))
+    ids = [2000 + i for i in range(len(blocks))]
+    kw = dict(hasher=hasher, compressor=compressor, container_max=cmax, **SMALL)
+    ctx1 = Context(**kw)
+    ora = Oracle(hasher=hasher, compressor=compressor, max_size=cmax)
+    for b, i in zip(blocks[:7], ids[:7]):
+        ctx1.reduce_block(b, i)
+        ora.reduce(b, i)
+    keys, vals = ctx1.index_dump()
+    alloc = ctx1.allocator()
+    recipes = {i: ctx1.recipe(i) for i in ids[:7]}
+    files = {}
+    for t in range(3):
+        for cid in range(t << 22, int.from_bytes(alloc[3 * t:3 * t + 3], "big") + 1):
+            d, closed = ctx1.container(cid)
+            if d is not None:
+                files[cid] = (d, closed)
+    opens = []
+    for t in range(3):
+        cid = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        d = files.get(cid)
+        opens.append(d[0] if d is not None and not d[1] else None)
+    ctx1.close()
+    ctx2 = Context(**kw)                                 # the restarted DataNode
+    ctx2.index_load(keys, vals)
+    ctx2.allocator_load(alloc, opens)
+    for i, r in recipes.items():
+        ctx2.recipe_load(i, r)
+    for b, i in zip(blocks[7:], ids[7:]):
+        compare_block(ctx2.reduce_block(b, i), ora.reduce(b, i), tag=f"after restart, block {i}")
+    gk, gv = ctx2.index_dump()
+    ok, ov = ora.index_dump()
+    assert np.array_equal(gk, ok) and np.array_equal(gv, ov)
+    assert ctx2.allocator() == ora.allocator()
+    for i in ids:
+        assert ctx2.recipe(i) == ora.recipe(i)
+    for cid, (d, closed) in files.items():               # chunkDir: closed files of the first run
+        gd, _ = ctx2.container(cid)
+        if gd is None:
+            ctx2.container_load(cid, d, closed and compressor == 2)
+    for i, b in zip(ids, blocks):
+        assert np.array_equal(ctx2.reconstruct_block(i), b), f"block {i}"
+    ctx2.close()
