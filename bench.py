@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--serial", action="store_true",
                     help="one batch at a time (no stream overlap): clean per-kernel stage times")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight (1..3, pipelined mode)")
+    ap.add_argument("--alone", action="store_true",
+                    help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
+                         "batches (off by default so a rocprof summary of the bench matches its in-pipeline averages)")
     ap.add_argument("--arena-slots", type=int, default=512,
                     help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
@@ -203,7 +206,7 @@ def main():
     el = time.perf_counter() - t0
     stage_ms = ctx.stage_times(reset=True)
     alone_ms = None
-    if node is None and not a.serial and not host:
+    if a.alone and node is None and not a.serial and not host:
         # one extra, untimed serial pass (one batch at a time): the same kernels without the
         # co-running batch, for the per-kernel "alone" rooflines next to the in-pipeline ones
         ctx.reset()
