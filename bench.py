@@ -182,10 +182,14 @@ def main():
             for _ in range(min(depth - 1, len(batches))):
                 ctx.wait_batch()
                 collect()
-        else:
+        elif a.serial:
             for ptrs, lens, rd, ids in batches:
                 node.reduce_batch(ptrs, lens, rd, ids, rank * B)
                 collect()
+        else:
+            # pipelined: the front half of global batch k+1 overlaps batch k's exchanges + store
+            node.reduce_batches([(ptrs, lens, rd, ids, rank * B) for ptrs, lens, rd, ids in batches],
+                                lambda k: collect())
 
     def barrier():
         if dist is not None:

@@ -73,6 +73,7 @@ struct Slot {
     std::vector<uint64_t> ids, lens;
     int nblocks = 0;
     bool pending = false;
+    uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
     hipEvent_t walk_done = nullptr, front_done = nullptr, back_done = nullptr;
     hipEvent_t copy_done = nullptr;          // host path: the batch's H2D copies landed
     uint8_t *d_hstage = nullptr;              // host path: device copies of the batch's blocks
@@ -116,16 +117,19 @@ struct hdrf_ctx {
     std::map<uint32_t, Loaded> loaded;               // containers loaded back from files (read side)
     // node-global index (gx.hip): scratch aggregation table, owner-side per-record arrays
     int G = 1, rank = 0;
-    IndexEntry *d_scratch = nullptr;
+    // Two batches can be in the node-global pipeline: the front half of batch k+1 (slot (k+1)%2,
+    // stream A) runs while batch k goes through its exchanges and back phases (slot k%2, stream B).
+    IndexEntry *d_scratch[2] = {nullptr, nullptr};   // per-slot local aggregation table
     int scratch_log2 = 0;
     int64_t gx_cap = 0;
-    unsigned long long *d_gx_counts = nullptr;   // [G] records emitted per peer
+    unsigned long long *d_gxe[2] = {nullptr, nullptr};  // [G] X1 records emitted per peer, per slot
+    unsigned long long *d_gx_counts = nullptr;   // [G] X3 records emitted per peer (back phases)
     int64_t *d_gx_rcounts = nullptr;             // [G] records received per peer
     uint32_t *d_oslot = nullptr;
     uint8_t *d_oflags = nullptr;
-    const uint32_t *gx_x2 = nullptr;             // responses of the current batch (caller's buffer)
-    int gx_phase = 0;                            // 1 front, 2 owner, 3 decide, 4 flush, 5 place
-    int gx_nblocks = 0;
+    const uint32_t *gx_x2 = nullptr;             // responses of the back batch (caller's buffer)
+    uint64_t gx_nfront = 0, gx_nfwait = 0, gx_nback = 0;   // fronts launched / waited, batches committed
+    int gx_bphase = 0;                           // back batch: 0 owner next, 1 decide, 2 flush, 3 place, 4 commit
     hdrf_stats stats{};                          // cumulative since the last reset
     // timing
     bool timing = false;
@@ -237,8 +241,9 @@ static void free_all(hdrf_ctx *ctx)
     for (auto &S : ctx->sl) free_slot(S);
     for (auto &kv : ctx->loaded) (void)hipFree(kv.second.ptr);
     ctx->loaded.clear();
-    void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch, ctx->d_gx_counts,
-                    ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags, ctx->d_carena};
+    void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch[0],
+                    ctx->d_scratch[1], ctx->d_gxe[0], ctx->d_gxe[1], ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot,
+                    ctx->d_oflags, ctx->d_carena};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -317,8 +322,8 @@ static int init_state(hdrf_ctx *ctx)
     }
     for (auto &S : ctx->sl) HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
-    // the index and allocator belong to the back stream (node-global phases run on stream A)
-    hipStream_t ist = ctx->G > 1 ? ctx->st : ctx->stB;
+    // the index and allocator belong to the back stream (also for the node-global back phases)
+    hipStream_t ist = ctx->stB;
     HIPCK(launch_index_clear(ctx->d_tab, ctx->cfg.index_log2, ctx->d_alloc, a, ist));
     ctx->h_alloc = a;
     ctx->batch = 0;
@@ -330,7 +335,8 @@ static int init_state(hdrf_ctx *ctx)
     ctx->recipes.clear();
     ctx->lengths.clear();
     ctx->last_nblocks = 0;
-    ctx->gx_phase = 0;
+    ctx->gx_nfront = ctx->gx_nfwait = ctx->gx_nback = 0;
+    ctx->gx_bphase = 0;
     ctx->stats = hdrf_stats{};
     return 0;
 }
@@ -406,7 +412,9 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         ctx->scratch_log2 = lg;
         ctx->gx_cap = (int64_t)nchunk;
         const size_t nrec = (size_t)ctx->G * (size_t)ctx->gx_cap;
-        if ((rc = dalloc(ctx, &ctx->d_scratch, (size_t)1 << lg)) || (rc = dalloc(ctx, &ctx->d_gx_counts, 64)) ||
+        if ((rc = dalloc(ctx, &ctx->d_scratch[0], (size_t)1 << lg)) || (rc = dalloc(ctx, &ctx->d_scratch[1], (size_t)1 << lg)) ||
+            (rc = dalloc(ctx, &ctx->d_gxe[0], 64)) || (rc = dalloc(ctx, &ctx->d_gxe[1], 64)) ||
+            (rc = dalloc(ctx, &ctx->d_gx_counts, 64)) ||
             (rc = dalloc(ctx, &ctx->d_gx_rcounts, 64)) || (rc = dalloc(ctx, &ctx->d_oslot, nrec)) ||
             (rc = dalloc(ctx, &ctx->d_oflags, nrec))) {
         }
@@ -908,13 +916,14 @@ extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
 // ---- node-global index phases (include/hdrf.h, gx.hip) ------------------------------------
 static_assert(sizeof(AllocState) <= HDRF_ALLOC_STATE_BYTES, "allocator state exchange size");
 
-static int gx_check(hdrf_ctx *ctx, int phase_before)
+// back phases run on the oldest batch whose front was waited, in order owner..commit
+static int gx_check(hdrf_ctx *ctx, int bphase)
 {
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
-    if (ctx->gx_phase != phase_before)
-        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* phases called out of order (phase " +
-                                              std::to_string(ctx->gx_phase) + ")");
+    if (ctx->gx_nfwait <= ctx->gx_nback || ctx->gx_bphase != bphase)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* phases called out of order (back phase " +
+                                              std::to_string(ctx->gx_bphase) + ")");
     return 0;
 }
 
@@ -935,19 +944,23 @@ extern "C" int hdrf_gx_layout_get(hdrf_ctx *ctx, hdrf_gx_layout *out)
     return 0;
 }
 
-extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
-                             const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send,
-                             int64_t *send_counts)
+// Front half of a node-global batch (chunking, SHA, local aggregation, X1 records), launched on
+// stream A into slot nfront % 2 without waiting: it overlaps the previous batch's back phases.
+extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                                    const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase,
+                                    uint32_t *x1_send)
 {
-    if (ctx && ctx->gx_phase == 6) ctx->gx_phase = 0;
-    if (int rc = gx_check(ctx, 0)) return rc;
-    if (int rc = drain(ctx)) return rc;
-    Slot &S = ctx->sl[0];                              // the node-global phases use slot 0, stream A
-    if (!x1_send || !send_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
+    if (ctx->gx_nfront != ctx->gx_nfwait || ctx->gx_nfront - ctx->gx_nback >= 2)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front_launch: a front is pending or two batches are in flight");
+    if (!x1_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    const int si = (int)(ctx->gx_nfront % 2);
+    Slot &S = ctx->sl[si];
     const hdrf_cfg &c = ctx->cfg;
     int max_nseg = 1;
     if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable, &max_nseg)) return rc;
-    ++ctx->batch;
+    S.gx_batch = ++ctx->batch;
     hipStream_t st = ctx->st;
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
     Marker mk;
@@ -957,46 +970,68 @@ extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *cons
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
                      S.d_queue, st, &mk));
     // local aggregation: a fresh scratch table, every entry "created" in batch 1
-    HIPCK(hipMemsetAsync(ctx->d_scratch, 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
-    HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_scratch,
+    HIPCK(hipMemsetAsync(ctx->d_scratch[si], 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
+    HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_scratch[si],
                        ctx->scratch_log2, 1u, tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap,
                        S.d_flags, S.d_tilesum, ctx->ntiles, S.d_err, st, &mk));
-    HIPCK(launch_gx_emit(c.hasher, S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, S.d_dig, ctx->d_scratch,
-                         S.d_slot, S.d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gx_counts, S.d_err, st));
+    HIPCK(launch_gx_emit(c.hasher, S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, S.d_dig, ctx->d_scratch[si],
+                         S.d_slot, S.d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gxe[si], S.d_err, st));
     mk.mark(st);
+    HIPCK(hipEventRecord(S.front_done, st));
+    S.nblocks = nblocks;
+    S.lens.assign(len, len + nblocks);
+    S.ids.assign(nblocks, 0);
+    if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
+    ctx->gx_nfront++;
+    return 0;
+}
+
+// Wait for the launched front; its per-peer X1 record counts -> send_counts[G].
+extern "C" int hdrf_gx_front_wait(hdrf_ctx *ctx, int64_t *send_counts)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->gx_nfront != ctx->gx_nfwait + 1) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front_wait: no front pending");
+    if (!send_counts) return set_err(ctx, HDRF_E_INVAL, "null counts");
+    const int si = (int)(ctx->gx_nfwait % 2);
+    Slot &S = ctx->sl[si];
+    hipStream_t st = ctx->st;
     std::vector<unsigned long long> cnt(ctx->G);
     int herr = 0;
-    HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gxe[si], sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    ctx->gx_nfwait++;
     if (ctx->timing)
-        for (int i = 0; i + 1 < mk.next && i < 7; i++) ctx->stage_ms[i] += elapsed(S.evB[i], S.evB[i + 1]);
+        for (int i = 0; i < 7; i++) ctx->stage_ms[i] += elapsed(S.evB[i], S.evB[i + 1]);
     if (herr) {
         HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
         HIPCK(hipStreamSynchronize(st));
         return device_error(ctx, herr);
     }
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
-    ctx->gx_nblocks = nblocks;
-    S.nblocks = nblocks;
-    S.lens.assign(len, len + nblocks);
-    S.ids.assign(nblocks, 0);
-    if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
-    ctx->gx_phase = 1;
     return 0;
+}
+
+extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                             const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send,
+                             int64_t *send_counts)
+{
+    if (!send_counts) return ctx ? set_err(ctx, HDRF_E_INVAL, "null counts") : HDRF_E_INVAL;
+    if (int rc = hdrf_gx_front_launch(ctx, nblocks, dev_data, len, readable, block_ids, gbase, x1_send)) return rc;
+    return hdrf_gx_front_wait(ctx, send_counts);
 }
 
 extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send)
 {
-    if (int rc = gx_check(ctx, 1)) return rc;
-    Slot &S = ctx->sl[0];
+    if (int rc = gx_check(ctx, 0)) return rc;
+    Slot &S = ctx->sl[ctx->gx_nback % 2];
     if (!x1_recv || !recv_counts || !x2_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     for (int s = 0; s < ctx->G; s++)
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
-    hipStream_t st = ctx->st;
+    hipStream_t st = ctx->stB;
     HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
     HIPCK(launch_gx_owner(ctx->cfg.hasher, x1_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap,
-                          ctx->G, ctx->d_tab, ctx->cfg.index_log2, ctx->batch, tag_mask(ctx), ctx->d_oslot,
+                          ctx->G, ctx->d_tab, ctx->cfg.index_log2, S.gx_batch, tag_mask(ctx), ctx->d_oslot,
                           ctx->d_oflags, S.d_coll, S.d_ncoll, ctx->coll_cap, x2_send, S.d_err, st));
     int herr = 0;
     HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -1006,35 +1041,36 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
         HIPCK(hipStreamSynchronize(st));
         return device_error(ctx, herr);
     }
-    ctx->gx_phase = 2;
+    ctx->gx_bphase = 1;
     return 0;
 }
 
 extern "C" int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv)
 {
-    if (int rc = gx_check(ctx, 2)) return rc;
-    Slot &S = ctx->sl[0];
+    if (int rc = gx_check(ctx, 1)) return rc;
+    const int si = (int)(ctx->gx_nback % 2);
+    Slot &S = ctx->sl[si];
     if (!x2_recv) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
-    hipStream_t st = ctx->st;
-    const int nb = ctx->gx_nblocks;
-    HIPCK(launch_gx_decide(S.d_bst, nb, ctx->cap_blk, ctx->ntiles, S.d_off, ctx->d_scratch, S.d_slot, x2_recv,
+    hipStream_t st = ctx->stB;
+    const int nb = S.nblocks;
+    HIPCK(launch_gx_decide(S.d_bst, nb, ctx->cap_blk, ctx->ntiles, S.d_off, ctx->d_scratch[si], S.d_slot, x2_recv,
                            S.d_flags, S.d_tilesum, st));
     const StoreParams P = store_params(ctx, nb);
     HIPCK(launch_store_scan(P, S.d_bst, S.d_off, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store,
                             S.d_pre, st));
     ctx->gx_x2 = x2_recv;
-    ctx->gx_phase = 3;
+    ctx->gx_bphase = 2;
     return 0;
 }
 
 extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out)
 {
-    if (int rc = gx_check(ctx, 3)) return rc;
-    Slot &S = ctx->sl[0];
-    hipStream_t st = ctx->st;
+    if (int rc = gx_check(ctx, 2)) return rc;
+    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    hipStream_t st = ctx->stB;
     if (alloc_in) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_in, sizeof(AllocState), hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(S.d_nclosed, 0, sizeof(uint32_t), st));
-    const StoreParams P = store_params(ctx, ctx->gx_nblocks);
+    const StoreParams P = store_params(ctx, S.nblocks);
     HIPCK(launch_store_flush(P, S.d_bst, S.d_store, S.d_pre, ctx->d_alloc, S.d_rstate, S.d_ev,
                              S.d_closed, S.d_nclosed, S.d_err, st));
     AllocState a{};
@@ -1044,22 +1080,23 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
         std::memset(alloc_out, 0, HDRF_ALLOC_STATE_BYTES);
         std::memcpy(alloc_out, &a, sizeof a);
     }
-    ctx->gx_phase = 4;
+    ctx->gx_bphase = 3;
     return 0;
 }
 
 extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts)
 {
-    if (int rc = gx_check(ctx, 4)) return rc;
-    Slot &S = ctx->sl[0];
+    if (int rc = gx_check(ctx, 3)) return rc;
+    const int si = (int)(ctx->gx_nback % 2);
+    Slot &S = ctx->sl[si];
     if (!x3_send || !send_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
-    hipStream_t st = ctx->st;
-    const int nb = ctx->gx_nblocks;
+    hipStream_t st = ctx->stB;
+    const int nb = S.nblocks;
     const StoreParams P = store_params(ctx, nb);
     GxPlace gx;
     gx.x2 = ctx->gx_x2; gx.x3 = x3_send; gx.cap = ctx->gx_cap; gx.counts = ctx->d_gx_counts; gx.G = ctx->G;
     HIPCK(launch_store_place(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_pre, S.d_rstate, S.d_ev, S.d_slot,
-                             ctx->d_scratch, ctx->d_arena, S.d_pcid, S.d_ppos, gx, st));
+                             ctx->d_scratch[si], ctx->d_arena, S.d_pcid, S.d_ppos, gx, st));
     // the node's allocator after the last rank (the next batch and the "blockID" view start here)
     if (alloc_final) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_final, sizeof(AllocState), hipMemcpyHostToDevice, st));
     std::vector<unsigned long long> cnt(ctx->G);
@@ -1071,24 +1108,24 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    if (int rc = complete_slot(ctx, 0, false)) return rc;
+    if (int rc = complete_slot(ctx, si, false)) return rc;
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
-    ctx->gx_phase = 5;
+    ctx->gx_bphase = 4;
     return 0;
 }
 
 extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts)
 {
-    if (int rc = gx_check(ctx, 5)) return rc;
-    
+    if (int rc = gx_check(ctx, 4)) return rc;
     if (!x3_recv || !recv_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     for (int s = 0; s < ctx->G; s++)
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
-    hipStream_t st = ctx->st;
+    hipStream_t st = ctx->stB;
     HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
     HIPCK(launch_gx_commit(x3_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap, ctx->G, ctx->d_tab, st));
     HIPCK(hipStreamSynchronize(st));
-    ctx->gx_phase = 6;
+    ctx->gx_bphase = 0;
+    ctx->gx_nback++;
     return 0;
 }
 

@@ -25,7 +25,7 @@ EXPORTS = [
     "hdrf_index_count", "hdrf_index_dump", "hdrf_allocator", "hdrf_recipe_get", "hdrf_block_length",
     "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
-    "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
+    "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_front_launch", "hdrf_gx_front_wait", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
     "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_lz4_file_decode", "hdrf_container_load",
@@ -154,6 +154,9 @@ def load():
         "hdrf_reset": (ctypes.c_int, [_vp]),
         "hdrf_get_stats": (ctypes.c_int, [_vp, ctypes.POINTER(Stats)]),
         "hdrf_gx_layout_get": (ctypes.c_int, [_vp, ctypes.POINTER(GxLayout)]),
+        "hdrf_gx_front_launch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p,
+                                                ctypes.c_uint32, _vp]),
+        "hdrf_gx_front_wait": (ctypes.c_int, [_vp, _i64p]),
         "hdrf_gx_front": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p,
                                          ctypes.c_uint32, _vp, _i64p]),
         "hdrf_gx_owner": (ctypes.c_int, [_vp, _vp, _i64p, _vp]),
@@ -468,6 +471,22 @@ class Context:
         cnt = np.zeros(self.cfg.n_ranks, np.int64)
         self._ck(self.L.hdrf_gx_front(self._h, n, ptrs, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p), gbase,
                                       x1_send, _p(cnt, _i64p)))
+        return cnt
+
+    def gx_front_launch(self, dev_ptrs, lens, readable, block_ids, gbase, x1_send):
+        """Launch the front half of a node-global batch without waiting (overlaps the previous
+        batch's back phases); gx_front_wait() returns its X1 send counts."""
+        n = len(dev_ptrs)
+        self._gx_keep = (_vp * n)(*dev_ptrs)
+        ln = np.ascontiguousarray(lens, np.uint64)
+        rd = np.ascontiguousarray(readable, np.uint64)
+        ids = np.ascontiguousarray(block_ids, np.uint64)
+        self._ck(self.L.hdrf_gx_front_launch(self._h, n, self._gx_keep, _p(ln, _u64p), _p(rd, _u64p), _p(ids, _u64p),
+                                             gbase, x1_send))
+
+    def gx_front_wait(self):
+        cnt = np.zeros(self.cfg.n_ranks, np.int64)
+        self._ck(self.L.hdrf_gx_front_wait(self._h, _p(cnt, _i64p)))
         return cnt
 
     def gx_owner(self, x1_recv, recv_counts, x2_send):

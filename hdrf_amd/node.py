@@ -99,6 +99,7 @@ class NodeRank:
         n = self.G * self.cap
         mk = lambda w: torch.empty(n * w, dtype=torch.int32, device=self.device)  # noqa: E731
         self.x1s, self.x1r = mk(self.w[0]), mk(self.w[0])
+        self.x1s2 = mk(self.w[0])      # second X1 send buffer: the next batch's front fills it
         self.x2s, self.x2r = mk(self.w[1]), mk(self.w[1])
         self.x3s, self.x3r = mk(self.w[2]), mk(self.w[2])
         self.alloc = None          # node allocator after the last batch (None: initial state)
@@ -109,11 +110,15 @@ class NodeRank:
 
     def reduce_batch(self, dev_ptrs, lens, readable, block_ids, gbase):
         """Reduce this rank's blocks of one global batch; gbase = its first batch position."""
-        ctx, xc, cap, (w1, w2, w3) = self.ctx, self.xc, self.cap, self.w
         torch.cuda.current_stream(self.device).synchronize()
-        c1 = ctx.gx_front(dev_ptrs, lens, readable, block_ids, gbase, self.x1s.data_ptr())
+        c1 = self.ctx.gx_front(dev_ptrs, lens, readable, block_ids, gbase, self.x1s.data_ptr())
+        self._back(c1, self.x1s)
+
+    def _back(self, c1, x1s):
+        """Exchanges and back phases of the batch whose front was waited (X1 counts c1)."""
+        ctx, xc, cap, (w1, w2, w3) = self.ctx, self.xc, self.cap, self.w
         r1 = xc.counts(c1)
-        xc.records(self.x1s, self.x1r, c1, r1, cap, w1)
+        xc.records(x1s, self.x1r, c1, r1, cap, w1)
         ctx.gx_owner(self.x1r.data_ptr(), r1, self.x2s.data_ptr())
         xc.records(self.x2s, self.x2r, r1, c1, cap, w2)           # responses retrace X1
         ctx.gx_decide(self.x2r.data_ptr())
@@ -122,6 +127,27 @@ class NodeRank:
         r3 = xc.counts(c3)
         xc.records(self.x3s, self.x3r, c3, r3, cap, w3)
         ctx.gx_commit(self.x3r.data_ptr(), r3)
+
+    def reduce_batches(self, batches, done=None):
+        """Pipelined node-global reduction of a sequence of this rank's batches
+        [(dev_ptrs, lens, readable, block_ids, gbase), ...]: the front half (chunking, SHA, local
+        aggregation) of batch k+1 runs on the GPU while batch k is exchanged and stored.
+        done(k) is called after batch k committed (its hdrf_batch_* views are valid then)."""
+        ctx = self.ctx
+        bufs = (self.x1s, self.x1s2)
+        torch.cuda.current_stream(self.device).synchronize()
+        if not batches:
+            return
+        ctx.gx_front_launch(*batches[0], bufs[0].data_ptr())
+        c1 = ctx.gx_front_wait()
+        for k in range(len(batches)):
+            if k + 1 < len(batches):
+                ctx.gx_front_launch(*batches[k + 1], bufs[(k + 1) % 2].data_ptr())
+            self._back(c1, bufs[k % 2])
+            if done is not None:
+                done(k)
+            if k + 1 < len(batches):
+                c1 = ctx.gx_front_wait()
 
     def batch_base(self, nblocks):
         """Rank-major batch positions: gbase of this rank given every rank's block count."""

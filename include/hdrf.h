@@ -238,6 +238,12 @@ int hdrf_gx_layout_get(hdrf_ctx *ctx, hdrf_gx_layout *out);
 int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                   const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send,
                   int64_t *send_counts);
+/* hdrf_gx_front split in two: launch the front half of batch k+1 (stream A, its own slot) before
+ * running batch k's owner .. commit phases (stream B), then wait for its X1 send counts.  At most
+ * two batches are in the node-global pipeline; the phases of a batch stay in order. */
+int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
+                         const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send);
+int hdrf_gx_front_wait(hdrf_ctx *ctx, int64_t *send_counts);
 int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send);
 int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv);
 /* alloc_in: HDRF_ALLOC_STATE_BYTES from the previous rank (NULL: this context's own state);

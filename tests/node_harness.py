@@ -63,6 +63,45 @@ class Loopback:
             ctxs[d].gx_commit(self.x3r[d].data_ptr(), r3[d])
 
 
+    def batches_pipelined(self, per_rank_batches, done=None):
+        """per_rank_batches[j][r] = rank r's share of global batch j.  Front halves of batch j+1
+        are launched before batch j's exchanges (hdrf_gx_front_launch / _wait), as NodeRank does."""
+        G, ctxs = self.G, self.ctxs
+        n = len(per_rank_batches)
+        x1b = [self.x1s, [torch.zeros_like(t) for t in self.x1s]]
+
+        def launch(j):
+            per = per_rank_batches[j]
+            gb = np.cumsum([0] + [len(p[0]) for p in per])
+            for r in range(G):
+                ctxs[r].gx_front_launch(*per[r], int(gb[r]), x1b[j % 2][r].data_ptr())
+
+        launch(0)
+        c1 = [ctxs[r].gx_front_wait() for r in range(G)]
+        for j in range(n):
+            if j + 1 < n:
+                launch(j + 1)
+            send = x1b[j % 2]
+            r1 = self._a2a(send, self.x1r, c1, self.w[0])
+            for d in range(G):
+                ctxs[d].gx_owner(self.x1r[d].data_ptr(), r1[d], self.x2s[d].data_ptr())
+            self._a2a(self.x2s, self.x2r, r1, self.w[1])
+            for r in range(G):
+                ctxs[r].gx_decide(self.x2r[r].data_ptr())
+            a = self.alloc
+            for r in range(G):
+                a = ctxs[r].gx_flush(a)
+            self.alloc = a
+            c3 = [ctxs[r].gx_place(a, self.x3s[r].data_ptr()) for r in range(G)]
+            r3 = self._a2a(self.x3s, self.x3r, c3, self.w[2])
+            for d in range(G):
+                ctxs[d].gx_commit(self.x3r[d].data_ptr(), r3[d])
+            if done is not None:
+                done(j)
+            if j + 1 < n:
+                c1 = [ctxs[r].gx_front_wait() for r in range(G)]
+
+
 def merged_index(ctxs):
     """Union of the ranks' index partitions, sorted by digest (the node's Redis)."""
     ks, vs = zip(*[c.index_dump() for c in ctxs])

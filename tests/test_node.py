@@ -93,6 +93,57 @@ def test_node_loopback_matches_single_sequence(G, hasher, sched):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("G,hasher", [(2, 1), (3, 0)])
+def test_node_loopback_pipelined_matches_single_sequence(G, hasher):
+    """The pipelined phase order (hdrf_gx_front_launch of batch j+1 before batch j's exchanges,
+    two slots, front on stream A, back phases on stream B) gives the same bytes as the oracle."""
+    import torch  # noqa: F401
+    from node_harness import Loopback, merged_index, open_ranks
+    from oracle.oracle import Oracle
+
+    cmax = 1 << 20
+    sched = [[2, 1, 2][:G], [1, 2, 1][:G], [2, 2, 1][:G], [1, 1, 2][:G]]
+    seq = _plan(sched)
+    blocks = _mixed_blocks(41 + G, len(seq), 600_000)
+    ctxs = open_ranks(G, hasher=hasher, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=4,
+                      index_log2=20, arena_slots=256)
+    lb = Loopback(ctxs)
+    ora = Oracle(hasher=hasher, compressor=1, max_size=cmax)
+    devs, per_batch, where = [], [], []
+    g = 0
+    for j, per in enumerate(sched):
+        pr, wj = [], []
+        for r, n in enumerate(per):
+            ptrs, lens, rd, ids = [], [], [], []
+            for i in range(n):
+                blk = blocks[g]
+                p = ctxs[r].dev_alloc(len(blk) + 4096)
+                ctxs[r].h2d(p, blk)
+                devs.append((ctxs[r], p))
+                ptrs.append(p); lens.append(len(blk)); rd.append(len(blk) + 4096); ids.append(0x700 + g)
+                wj.append((r, i, g))
+                g += 1
+            pr.append((ptrs, lens, rd, ids))
+        per_batch.append(pr)
+        where.append(wj)
+
+    def done(j):
+        for r, i, gi in where[j]:
+            compare_block(ctxs[r].batch_result(i), ora.reduce(blocks[gi], 0x700 + gi),
+                          tag=f"pipelined G={G} batch {j} rank {r} block {i}")
+    lb.batches_pipelined(per_batch, done)
+    gk, gv = merged_index(ctxs)
+    ok, ov = ora.index_dump()
+    assert np.array_equal(gk, ok) and np.array_equal(gv, ov), "node index differs"
+    for c in ctxs:
+        assert c.allocator() == ora.allocator()
+    for c, p in devs:
+        c.dev_free(p)
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.gpu
 def test_node_context_rejects_single_node_calls():
     from hdrf_amd.lib import Context, HdrfError
     ctx = Context(n_ranks=2, rank=1, max_block_bytes=1 << 20, max_batch_blocks=2, index_log2=16, arena_slots=16,
