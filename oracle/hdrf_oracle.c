@@ -10,6 +10,8 @@
  * DataNode.chunkDir are restated as in-memory byte vectors.
  */
 #include "hdrf_oracle.h"
+#include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -332,17 +334,54 @@ static int64_t bytes_to_slot(const uint8_t *b, int slot)
 
 /* DataDeduplicator(ByteBuffer, long) — DN/DataDeduplicator.java:108-217.
  * Blocks are processed in call order (the FIFO AIWriteQueue, :124-158,197-204). */
-int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, int64_t block_id,
-                           int64_t cap, uint32_t *offsets_out, uint8_t *digests_out, uint8_t *is_new_out,
-                           uint8_t *values_out, int64_t *store_size_out)
+/* :122 chunking + :174 threadedHasher digests: the part of a block's reduction that does not
+ * touch Redis (the reference runs it before the FIFO wait, DN/DataDeduplicator.java:122-124).
+ * Returns n (off/dig malloc'ed, caller frees) or < 0. */
+static int64_t chunk_and_hash(int hasher, int H, const uint8_t *data, int64_t size, uint32_t **off_out,
+                              uint8_t **dig_out)
 {
-    const int H = o->H;
-    /* :122 chunking */
     int64_t ocap = size / 700 + 2;
     uint32_t *off = (uint32_t *)malloc((size_t)ocap * sizeof(uint32_t));
     if (!off) return -2;
     int64_t n = hdrf_oracle_chunk(data, size, off, ocap);
-    if (n < 0 || n > cap) { free(off); return -1; }
+    if (n < 0) { free(off); return -1; }
+    uint8_t *dig = (uint8_t *)malloc((size_t)n * H + 1);
+    if (!dig) { free(off); return -2; }
+    int64_t cur = 0;
+    for (int64_t k = 0; k < n; k++) {
+        if (hasher == 0) hdrf_oracle_sha1(data + cur, (uint64_t)(off[k] - cur), dig + k * H);
+        else hdrf_oracle_sha224(data + cur, (uint64_t)(off[k] - cur), dig + k * H);
+        cur = off[k];
+    }
+    *off_out = off;
+    *dig_out = dig;
+    return n;
+}
+
+static int64_t reduce_hashed(hdrf_oracle *o, const uint8_t *data, int64_t size, int64_t block_id, uint32_t *off,
+                             int64_t n, uint8_t *dig, uint32_t *offsets_out, uint8_t *digests_out,
+                             uint8_t *is_new_out, uint8_t *values_out, int64_t *store_size_out);
+
+int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, int64_t block_id,
+                           int64_t cap, uint32_t *offsets_out, uint8_t *digests_out, uint8_t *is_new_out,
+                           uint8_t *values_out, int64_t *store_size_out)
+{
+    uint32_t *off = NULL;
+    uint8_t *dig = NULL;
+    int64_t n = chunk_and_hash(o->hasher, o->H, data, size, &off, &dig);
+    if (n < 0) return n;
+    if (n > cap) { free(off); free(dig); return -1; }
+    return reduce_hashed(o, data, size, block_id, off, n, dig, offsets_out, digests_out, is_new_out, values_out,
+                         store_size_out);
+}
+
+/* The ordered part (FIFO turn, :124-204): Redis lookups, checkChunk, storers, SETs, storeDB.
+ * Takes ownership of off/dig. */
+static int64_t reduce_hashed(hdrf_oracle *o, const uint8_t *data, int64_t size, int64_t block_id, uint32_t *off,
+                             int64_t n, uint8_t *dig, uint32_t *offsets_out, uint8_t *digests_out,
+                             uint8_t *is_new_out, uint8_t *values_out, int64_t *store_size_out)
+{
+    const int H = o->H;
 
     /* :165-172 allocator: GET "blockID"; absent -> (t<<22, 0) */
     int64_t lastBlockID[8];
@@ -354,13 +393,10 @@ int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, in
     /* :174 chunkHash -> threadedHasher.run :578-641: hash every chunk, then the MULTI'd
      * GETs are all answered before any of this block's SETs (storers start afterwards). */
     chunk_meta *cm = (chunk_meta *)calloc((size_t)n, sizeof(chunk_meta));
-    uint8_t *dig = (uint8_t *)malloc((size_t)n * H + 1);
-    if (!cm || !dig) { free(off); free(cm); free(dig); return -2; }
+    if (!cm) { free(off); free(dig); return -2; }
     int64_t cur = 0;
     for (int64_t k = 0; k < n; k++) {
         int64_t end = off[k];
-        if (o->hasher == 0) hdrf_oracle_sha1(data + cur, (uint64_t)(end - cur), dig + k * H);
-        else hdrf_oracle_sha224(data + cur, (uint64_t)(end - cur), dig + k * H);
         cm[k].bbStart = (int32_t)cur; cm[k].bbStop = (int32_t)end; cm[k].length = (int32_t)(end - cur);
         int64_t f = kv_find(&o->index, dig + k * H);
         meta_process(&cm[k], f >= 0 ? o->index.vals + f * 11 : NULL);
@@ -446,6 +482,78 @@ int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, in
     if (store_size_out) *store_size_out = storeSize;
     free(off); free(cm); free(dig); free(setv);
     return n;
+}
+
+/* ---- threaded CPU baseline (bench.py cpu_baseline only; never a checker) ------------------
+ * The reference's concurrency shape: chunking + hashing of a block run before its FIFO turn
+ * (DN/DataDeduplicator.java:122-124), so worker threads chunk and hash blocks ahead while the
+ * ordered part (Redis lookups, checkChunk, storers, storeDB) takes the blocks one at a time in
+ * arrival order (:124-204).  Results are those of hdrf_oracle_reduce called in order. */
+typedef struct {
+    const uint8_t *data;
+    int64_t size;
+    uint32_t *off;
+    uint8_t *dig;
+    int64_t n;
+    int ready;
+} hash_job;
+
+typedef struct {
+    hash_job *jobs;
+    int64_t njobs;
+    int64_t next;          /* next job to take (atomic) */
+    int64_t consumed;      /* jobs the ordered part finished (atomic): bounds the lookahead */
+    int64_t ahead;
+    int hasher, H;
+} hash_pool;
+
+static void *hash_worker(void *arg)
+{
+    hash_pool *p = (hash_pool *)arg;
+    for (;;) {
+        const int64_t i = __atomic_fetch_add(&p->next, 1, __ATOMIC_RELAXED);
+        if (i >= p->njobs) return NULL;
+        while (i - __atomic_load_n(&p->consumed, __ATOMIC_ACQUIRE) > p->ahead) sched_yield();
+        hash_job *j = &p->jobs[i];
+        j->n = chunk_and_hash(p->hasher, p->H, j->data, j->size, &j->off, &j->dig);
+        __atomic_store_n(&j->ready, 1, __ATOMIC_RELEASE);
+    }
+}
+
+int64_t hdrf_oracle_reduce_many(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
+                                const int64_t *ids, int64_t nblocks, int nthreads, int64_t *store_sizes)
+{
+    if (nthreads < 1) nthreads = 1;
+    hash_pool p;
+    memset(&p, 0, sizeof p);
+    p.jobs = (hash_job *)calloc((size_t)(nblocks > 0 ? nblocks : 1), sizeof(hash_job));
+    if (!p.jobs) return -2;
+    p.njobs = nblocks; p.ahead = 2 * nthreads; p.hasher = o->hasher; p.H = o->H;
+    for (int64_t i = 0; i < nblocks; i++) { p.jobs[i].data = blocks[i]; p.jobs[i].size = sizes[i]; }
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    int started = 0;
+    for (int t = 0; t < nthreads; t++)
+        if (pthread_create(&th[t], NULL, hash_worker, &p) == 0) started++;
+    int64_t rc = 0;
+    if (!started) rc = -2;
+    for (int64_t i = 0; i < nblocks && rc >= 0; i++) {
+        hash_job *j = &p.jobs[i];
+        while (!__atomic_load_n(&j->ready, __ATOMIC_ACQUIRE)) sched_yield();
+        if (j->n < 0) { rc = j->n; break; }
+        int64_t ss = 0;
+        const int64_t n = reduce_hashed(o, j->data, j->size, ids[i], j->off, j->n, j->dig, NULL, NULL, NULL, NULL, &ss);
+        j->off = NULL; j->dig = NULL;
+        if (n < 0) { rc = n; break; }
+        if (store_sizes) store_sizes[i] = ss;
+        __atomic_store_n(&p.consumed, i + 1, __ATOMIC_RELEASE);
+    }
+    __atomic_store_n(&p.consumed, nblocks + p.ahead + 1, __ATOMIC_RELEASE);   /* release waiting workers */
+    for (int t = 0; t < nthreads; t++)
+        if (t < started) pthread_join(th[t], NULL);
+    for (int64_t i = 0; i < nblocks; i++) { free(p.jobs[i].off); free(p.jobs[i].dig); }
+    free(th);
+    free(p.jobs);
+    return rc < 0 ? rc : nblocks;
 }
 
 int hdrf_oracle_index_get(const hdrf_oracle *o, const uint8_t *digest, uint8_t out11[11])

@@ -65,6 +65,10 @@ def lib():
         for name in ("hdrf_oracle_lz4_compress", "hdrf_oracle_hadoop_lz4_frame"):
             getattr(L, name).argtypes = [_u8p, ctypes.c_int64, _u8p]
             getattr(L, name).restype = ctypes.c_int64
+        L.hdrf_oracle_reduce_many.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                              ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                              ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        L.hdrf_oracle_reduce_many.restype = ctypes.c_int64
         L.hdrf_oracle_hadoop_lz4_stream_bound.argtypes = [ctypes.c_int64, ctypes.c_int64]
         L.hdrf_oracle_hadoop_lz4_stream_bound.restype = ctypes.c_int64
         L.hdrf_oracle_hadoop_lz4_stream.argtypes = [_u8p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, _u8p]
@@ -196,6 +200,23 @@ class Oracle:
         if h:
             lib().hdrf_oracle_free(h)
             self._h = None
+
+    def reduce_many(self, blocks, block_ids, nthreads):
+        """Threaded CPU baseline: chunk+hash on nthreads workers ahead of the ordered index/store
+        part; same state as reduce() called in order.  Returns per-block storeSize."""
+        arrs = [_as_u8(b) for b in blocks]
+        n = len(arrs)
+        keep = [a if a.size else np.zeros(1, np.uint8) for a in arrs]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in keep])
+        sizes = np.array([a.size for a in arrs], np.int64)
+        ids = np.ascontiguousarray(block_ids, np.int64)
+        ss = np.zeros(max(n, 1), np.int64)
+        p64 = ctypes.POINTER(ctypes.c_int64)
+        rc = lib().hdrf_oracle_reduce_many(self._h, ptrs, sizes.ctypes.data_as(p64), ids.ctypes.data_as(p64), n,
+                                           int(nthreads), ss.ctypes.data_as(p64))
+        if rc < 0:
+            raise RuntimeError(f"hdrf_oracle_reduce_many: {rc}")
+        return ss[:n]
 
     def reduce(self, data, block_id):
         a = _as_u8(data)
