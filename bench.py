@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="one batch at a time (no stream overlap): clean per-kernel stage times")
+    ap.add_argument("--read-blocks", type=int, default=0,
+                    help="read side: blocks reduced into a separate context and rebuilt on the GPU (default 0: "
+                         "off, so a rocprof summary of the default bench holds only the timed pipeline's kernels)")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight (1..3, pipelined mode)")
     ap.add_argument("--alone", action="store_true",
                     help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
@@ -300,6 +303,9 @@ def main():
                        "lz4_ratio_closed": round(st["closed_raw_bytes"] / max(st["closed_file_bytes"], 1), 6),
                        "node_ratio": round(st["logical_bytes"] / max(stored, 1), 6),
                        "node_ratio_def": "logical / (closed Lz4Codec files + open raw containers)"}
+    read_side = None
+    if rank == 0 and world == 1 and a.read_blocks > 0 and not host:
+        read_side = read_bench(ctx, dev, S, min(a.read_blocks, nb), a.hasher, compressor)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu and a.cpu_sample_blocks > 0:
         cpu = cpu_baseline(ctx, dev, S, min(a.cpu_sample_blocks, nb), store, a.hasher, compressor)
@@ -321,6 +327,8 @@ def main():
                 "roofline": roofline, "cpu_baseline": cpu, "dedup": dedup, "stages": stages}
         if compression:
             line["compression"] = compression
+        if read_side:
+            line["read_side"] = read_side
         if host:
             line["config"]["workload"] = ("config5: %d x %d MiB host-resident (pinned) blocks, %d%% dup, streamed "
                                           "H2D on a side stream overlapped with the reduction (hdrf_submit_host), "
@@ -335,6 +343,33 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def read_bench(ctx, dev, S, m, hasher, compressor):
+    """Read side (DataConstructor, hdrf_reconstruct): m blocks of the same corpus reduced into a
+    separate context that keeps recipes, then every block rebuilt into HBM from its recipe (index
+    lookups + chunk gather from the container arena); checked byte for byte on the first block."""
+    import numpy as np
+    from hdrf_amd.lib import Context
+    B = 8
+    v = Context(device=int(ctx.cfg.device), hasher=hasher, compressor=compressor, max_block_bytes=S,
+                max_batch_blocks=B, index_log2=24, arena_slots=512, keep_recipes=1)
+    for b0 in range(0, m, B):
+        k = min(B, m - b0)
+        v.reduce_batch([dev + (b0 + i) * S for i in range(k)], [S] * k, [S + 4096] * k, list(range(b0, b0 + k)))
+    recipes = [v.recipe(b) for b in range(m)]
+    out = v.dev_alloc(S + 4096)
+    v.reconstruct(recipes[0], out, S)                    # warm-up
+    ok = bool(np.array_equal(v.d2h(out, S), ctx.d2h(dev, S)))
+    t0 = time.perf_counter()
+    for r in recipes:
+        v.reconstruct(r, out, S)
+    t = time.perf_counter() - t0
+    v.dev_free(out)
+    v.close()
+    return {"GB_s": round(m * S / t / 1e9, 2), "blocks": m, "seconds": round(t, 4), "first_block_identical": ok,
+            "path": "hdrf_reconstruct: recipe digests -> index lookup -> offsets scan -> arena gather, output in HBM, "
+                    "one block per call (host round trip each)"}
 
 
 def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1):

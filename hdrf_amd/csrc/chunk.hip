@@ -262,12 +262,19 @@ __device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const 
                 const int pe = min(T + 1024, c.size - c.w);            // window complete & inside the view
                 const int hiv = min(T + 2047, c.size - 1);
                 const int cut_thr = stop.cut_thr(), cnt_thr = min(stop.cnt_thr(), sink.cap);
-                bool pushed = false;
+                bool pushed = false, resume = false;
+                int lim_r = 0;
                 while (p < pe && cnt < cnt_thr) {
                     const int e = p + c.w;
                     if (next_ff(fA, fB, bA, bB, T, p) > e) break;      // no 0x7F in the window
                     const int f2 = next_ff(fA, fB, bA, bB, T, e + 1);
-                    if (f2 > min(p + c.maxlen, hiv)) break;
+                    if (f2 > min(p + c.maxlen, hiv)) {
+                        // no 0x7F in [e+1, view end]: unless lim or the data end is inside the
+                        // view, the search simply continues in the next view (no generic step)
+                        lim_r = min(p + c.maxlen, c.size - 1);
+                        resume = lim_r > T + 2047;
+                        break;
+                    }
                     p = f2 + 1;                                        // :276-283
                     if (lane_id() == (cnt & 63)) stage = (uint32_t)p;
                     cnt++;
@@ -281,6 +288,13 @@ __device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const 
                     ch.p = p;
                     ch.first = false;
                     if (stop(p, cnt)) return false;
+                }
+                if (resume) {
+                    ch.p = p;
+                    ch.lim = lim_r;
+                    ch.q = T + 2048;
+                    ch.state = kSearchFF;
+                    return true;
                 }
             }
             if (ch.p >= T + 1024) return true;
