@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--read-blocks", type=int, default=0,
                     help="read side: blocks reduced into a separate context and rebuilt on the GPU (default 0: "
                          "off, so a rocprof summary of the default bench holds only the timed pipeline's kernels)")
+    ap.add_argument("--keep-recipes", type=int, default=1,
+                    help="storeDB's recipe SET per block into the device recipe store (default 1, as the reference)")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight (1..3, pipelined mode)")
     ap.add_argument("--alone", action="store_true",
                     help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
@@ -116,7 +118,7 @@ def main():
         nb = 128                                         # 16 GiB of pinned host memory
     compressor = 2 if mixed else 1
     ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
-                  arena_slots=a.arena_slots, keep_recipes=0, timing=1, n_ranks=world, rank=rank, compressor=compressor)
+                  arena_slots=a.arena_slots, keep_recipes=a.keep_recipes, timing=1, n_ranks=world, rank=rank, compressor=compressor)
     node = None
     if world > 1:
         from hdrf_amd.node import NodeRank, global_block
@@ -315,12 +317,13 @@ def main():
                 "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
                 "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                 "config": {"workload": "config%d: %d x %d MiB %sblocks per GPU, %d%% dup (%d MiB segments), "
-                                       "chunk+SHA-%s+%s index+container store%s, fresh index per step"
+                                       "chunk+SHA-%s+%s index+container store%s%s, fresh index per step"
                                        % (4 if mixed else (2 if world == 1 else 3), nb, a.block_mib,
                                           "mixed-entropy (random/text/binary) " if mixed else "",
                                           a.dup_ppm // 10000, a.seg_mib, "1" if a.hasher == 0 else "224",
                                           "local" if world == 1 else "node-global (RCCL all-to-all)",
-                                          " + Lz4Codec on closed containers" if mixed else ""),
+                                          " + Lz4Codec on closed containers" if mixed else "",
+                                          " + recipes (device store)" if a.keep_recipes else ", no recipes"),
                            "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks_per_gpu": B,
                            "parallelism": "dp%d: blocks sharded by rank; one index partitioned by digest prefix"
                                           % world},

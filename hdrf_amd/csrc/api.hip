@@ -74,6 +74,9 @@ struct Slot {
     int nblocks = 0;
     bool pending = false;
     uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
+    RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
+    hipEvent_t recipe_done = nullptr;         // the copies read d_dig: the slot's next SHA waits
+    bool recipe_pending = false;
     hipEvent_t walk_done = nullptr, front_done = nullptr, back_done = nullptr;
     hipEvent_t copy_done = nullptr;          // host path: the batch's H2D copies landed
     uint8_t *d_hstage = nullptr;              // host path: device copies of the batch's blocks
@@ -111,7 +114,13 @@ struct hdrf_ctx {
     AllocState h_alloc{};
     std::map<uint32_t, ContainerInfo> containers;   // container id -> arena slot
     std::map<uint32_t, uint32_t> slot_owner;         // arena slot -> container id
-    std::map<uint32_t, std::vector<uint8_t>> recipes; // longToBytes(blockId,4) -> recipe
+    // recipes (SET longToBytes(blockId,4) -> BE32 size | digests) live in HBM: digests in an
+    // append-only store of 256 MiB chunks, the host keeps only where each one is
+    struct RecipeLoc { uint32_t chunk; uint64_t off; uint32_t n; };
+    std::vector<uint8_t *> rchunks;
+    uint32_t rcur = 0;                                // chunk being filled
+    uint64_t rhead = 0;                               // bytes used in it
+    std::map<uint32_t, RecipeLoc> recipes;
     std::map<uint32_t, int64_t> lengths;              // block length (recipe head)
     struct Loaded { uint8_t *ptr; uint64_t len; };
     std::map<uint32_t, Loaded> loaded;               // containers loaded back from files (read side)
@@ -224,7 +233,9 @@ static void free_slot(Slot &S)
     void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_closed, S.h_filelen, S.h_desc};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
-    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done};
+    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done};
+    if (S.d_rjobs) (void)hipFree(S.d_rjobs);
+    if (S.h_rjobs) (void)hipHostFree(S.h_rjobs);
     if (S.d_hstage) (void)hipFree(S.d_hstage);
     for (auto e : evs)
         if (e) (void)hipEventDestroy(e);
@@ -241,6 +252,8 @@ static void free_all(hdrf_ctx *ctx)
     for (auto &S : ctx->sl) free_slot(S);
     for (auto &kv : ctx->loaded) (void)hipFree(kv.second.ptr);
     ctx->loaded.clear();
+    for (auto p : ctx->rchunks) (void)hipFree(p);
+    ctx->rchunks.clear();
     void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch[0],
                     ctx->d_scratch[1], ctx->d_gxe[0], ctx->d_gxe[1], ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot,
                     ctx->d_oflags, ctx->d_carena};
@@ -281,8 +294,10 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
     if (c.compressor == 2 && ((rc = dalloc(ctx, &S.d_segclen, (size_t)ctx->closed_cap * nseg_lz)) ||
                               (rc = dalloc(ctx, &S.d_filelen, (size_t)ctx->closed_cap))))
         return rc;
+    if ((rc = dalloc(ctx, &S.d_rjobs, B)) || (rc = halloc(ctx, &S.h_rjobs, B))) return rc;
     if (hipEventCreateWithFlags(&S.walk_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.copy_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.recipe_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.front_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
@@ -333,6 +348,9 @@ static int init_state(hdrf_ctx *ctx)
     for (auto &kv : ctx->loaded) (void)hipFree(kv.second.ptr);
     ctx->loaded.clear();
     ctx->recipes.clear();
+    ctx->rcur = 0;
+    ctx->rhead = 0;
+    for (auto &S : ctx->sl) S.recipe_pending = false;
     ctx->lengths.clear();
     ctx->last_nblocks = 0;
     ctx->gx_nfront = ctx->gx_nfwait = ctx->gx_nback = 0;
@@ -534,8 +552,9 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
                           S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, W, &mw));
     mw.mark(W);
     HIPCK(hipEventRecord(S.walk_done, W));
-    // ---- fingerprints on A
+    // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig)
     HIPCK(hipStreamWaitEvent(A, S.walk_done, 0));
+    if (S.recipe_pending) HIPCK(hipStreamWaitEvent(A, S.recipe_done, 0));
     Marker ma;
     ma.ev = ctx->timing ? S.evA : nullptr;
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig, S.d_queue, A,
@@ -579,6 +598,41 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
 }
 
 static int complete_state(hdrf_ctx *ctx, Slot &S);
+
+// space for one recipe's digests in the device recipe store (4-B aligned words; entries start
+// on 16 B)
+static int recipe_alloc(hdrf_ctx *ctx, uint64_t bytes, uint32_t key, uint32_t n, uint8_t **dst)
+{
+    constexpr uint64_t kChunk = 256ull << 20;
+    if (bytes > kChunk) return set_err(ctx, HDRF_E_CAPACITY, "recipe larger than a recipe-store chunk");
+    if (ctx->rcur < ctx->rchunks.size() && ctx->rhead + bytes > kChunk) { ctx->rcur++; ctx->rhead = 0; }
+    if (ctx->rcur >= ctx->rchunks.size()) {
+        uint8_t *p = nullptr;
+        HIPCK(hipMalloc((void **)&p, kChunk));
+        ctx->rchunks.push_back(p);
+        ctx->rcur = (uint32_t)ctx->rchunks.size() - 1;
+        ctx->rhead = 0;
+    }
+    *dst = ctx->rchunks[ctx->rcur] + ctx->rhead;
+    ctx->recipes[key] = hdrf_ctx::RecipeLoc{ctx->rcur, ctx->rhead, n};
+    ctx->rhead += (bytes + 15) & ~15ull;
+    return 0;
+}
+
+// GET longToBytes(id,4): [BE32 size | digests] out of the device store; the caller drained.
+// 1 found, 0 absent, < 0 error
+static int fetch_recipe(hdrf_ctx *ctx, uint32_t key, std::vector<uint8_t> &r)
+{
+    auto it = ctx->recipes.find(key);
+    if (it == ctx->recipes.end()) return 0;
+    const int64_t ln = ctx->lengths[key];
+    r.resize(4 + (size_t)it->second.n * ctx->H);
+    r[0] = (uint8_t)(ln >> 24); r[1] = (uint8_t)(ln >> 16); r[2] = (uint8_t)(ln >> 8); r[3] = (uint8_t)ln;
+    if (it->second.n)
+        HIPCK(hipMemcpy(r.data() + 4, ctx->rchunks[it->second.chunk] + it->second.off, (size_t)it->second.n * ctx->H,
+                        hipMemcpyDeviceToHost));
+    return 1;
+}
 
 // After a batch's read-back landed: container / recipe / allocator bookkeeping.
 static int complete_slot(hdrf_ctx *ctx, int si, bool timed)
@@ -630,22 +684,25 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
     ctx->stats.open_bytes = 0;
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) ctx->stats.open_bytes += ctx->h_alloc.cur[t];
-    // recipes (SET longToBytes(id,4) -> BE32 size | digests); the slot is not reused before
-    // this returns (submit waits for it), so its digests are still intact
+    // recipes (SET longToBytes(id,4) -> BE32 size | digests): the block's digests are copied on
+    // the device into the recipe store (stream B); the slot's next SHA waits for the copies
+    int nj = 0;
     for (int b = 0; b < nblocks; b++) {
         const uint32_t key = (uint32_t)S.ids[b];
-        const uint64_t ln = S.lens[b];
-        ctx->lengths[key] = (int64_t)ln;
+        ctx->lengths[key] = (int64_t)S.lens[b];
         if (c.keep_recipes) {
-            const int64_t n = S.h_bst[b].n_chunks;
-            std::vector<uint8_t> r(4 + n * ctx->H);
-            r[0] = (uint8_t)(ln >> 24); r[1] = (uint8_t)(ln >> 16); r[2] = (uint8_t)(ln >> 8); r[3] = (uint8_t)ln;
-            std::vector<uint32_t> dw((size_t)n * ctx->HW);
-            HIPCK(hipMemcpy(dw.data(), S.d_dig + (size_t)b * ctx->cap_blk * ctx->HW, dw.size() * 4,
-                            hipMemcpyDeviceToHost));
-            std::memcpy(r.data() + 4, dw.data(), (size_t)n * ctx->H);
-            ctx->recipes[key] = std::move(r);
+            const uint32_t n = (uint32_t)S.h_bst[b].n_chunks;
+            uint8_t *dst = nullptr;
+            if (int rc = recipe_alloc(ctx, (uint64_t)n * ctx->H, key, n, &dst)) return rc;
+            S.h_rjobs[nj++] = RecipeCopy{(uint64_t)(uintptr_t)(S.d_dig + (size_t)b * ctx->cap_blk * ctx->HW),
+                                         (uint64_t)(uintptr_t)dst, n * (uint32_t)ctx->HW, 0};
         }
+    }
+    if (nj) {
+        HIPCK(hipMemcpyAsync(S.d_rjobs, S.h_rjobs, sizeof(RecipeCopy) * nj, hipMemcpyHostToDevice, ctx->stB));
+        HIPCK(launch_recipe_copy(S.d_rjobs, nj, ctx->stB));
+        HIPCK(hipEventRecord(S.recipe_done, ctx->stB));
+        S.recipe_pending = true;
     }
     return 0;
 }
@@ -967,6 +1024,7 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     mk.ev = ctx->timing ? S.evB : nullptr;             // 8 markers: walk .. slow+decide, end
     HIPCK(launch_chunking(S.d_blocks, nblocks, max_nseg, c.window, c.max_chunk, S.d_spec, ctx->spec_cap,
                           S.d_meta, S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, st, &mk));
+    if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
                      S.d_queue, st, &mk));
     // local aggregation: a fresh scratch table, every entry "created" in batch 1
@@ -1406,7 +1464,11 @@ extern "C" int hdrf_recipe_load(hdrf_ctx *ctx, uint64_t block_id, const uint8_t 
 {
     if (!ctx || !recipe || len < 4 || (len - 4) % ctx->H) return HDRF_E_INVAL;
     const uint32_t key = (uint32_t)block_id;
-    ctx->recipes[key].assign(recipe, recipe + len);
+    if (int rc = drain(ctx)) return rc;
+    const uint32_t n = (uint32_t)((len - 4) / ctx->H);
+    uint8_t *dst = nullptr;
+    if (int rc = recipe_alloc(ctx, (uint64_t)n * ctx->H, key, n, &dst)) return rc;
+    if (n) HIPCK(hipMemcpy(dst, recipe + 4, (size_t)n * ctx->H, hipMemcpyHostToDevice));
     ctx->lengths[key] = ((int64_t)recipe[0] << 24) | (recipe[1] << 16) | (recipe[2] << 8) | recipe[3];
     return 0;
 }
@@ -1416,9 +1478,13 @@ extern "C" int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *ou
     if (!ctx) return HDRF_E_INVAL;
     auto it = ctx->recipes.find((uint32_t)block_id);
     if (it == ctx->recipes.end()) return 0;
-    const int64_t n = (int64_t)it->second.size();
+    const int64_t n = 4 + (int64_t)it->second.n * ctx->H;
     if (!out || cap < n) return set_err(ctx, HDRF_E_CAPACITY, "recipe needs " + std::to_string(n) + " bytes");
-    std::memcpy(out, it->second.data(), n);
+    if (int rc = drain(ctx)) return rc;
+    std::vector<uint8_t> r;
+    const int fr = fetch_recipe(ctx, (uint32_t)block_id, r);
+    if (fr < 0) return fr;
+    std::memcpy(out, r.data(), (size_t)n);
     return n;
 }
 
@@ -1510,9 +1576,10 @@ extern "C" int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint
 {
     if (!ctx) return HDRF_E_INVAL;
     if (int rc = drain(ctx)) return rc;
-    auto it = ctx->recipes.find((uint32_t)block_id);     // GET longToBytes(blockId,4) (DN/BlockSender.java:292-328)
-    if (it == ctx->recipes.end()) return set_err(ctx, HDRF_E_NOTFOUND, "no recipe for this block (keep_recipes?)");
-    const std::vector<uint8_t> &rec = it->second;
+    std::vector<uint8_t> rec;                            // GET longToBytes(blockId,4) (DN/BlockSender.java:292-328)
+    const int fr = fetch_recipe(ctx, (uint32_t)block_id, rec);
+    if (fr < 0) return fr;
+    if (!fr) return set_err(ctx, HDRF_E_NOTFOUND, "no recipe for this block (keep_recipes?)");
     const int64_t size = ((int64_t)rec[0] << 24) | (rec[1] << 16) | (rec[2] << 8) | rec[3];
     if (!out || cap < size) return set_err(ctx, HDRF_E_CAPACITY, "needs " + std::to_string(size) + " bytes");
     if (int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, (uint64_t)size + 4096)) return rc;

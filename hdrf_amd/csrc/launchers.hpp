@@ -81,6 +81,12 @@ hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int
                             uint32_t *tilesum, hipStream_t st);
 hipError_t launch_gx_commit(const uint32_t *x3, const int64_t *counts, int64_t max_count, int64_t cap, int G,
                             IndexEntry *tab, hipStream_t st);
+// recipes (storeDB): a batch's digests copied into the device recipe store
+struct RecipeCopy {
+    uint64_t src, dst;       // device addresses (4-B aligned)
+    uint32_t words, pad;
+};
+hipError_t launch_recipe_copy(const RecipeCopy *jobs, int n, hipStream_t st);
 // stream mode (compressor 4): pieces of one block -> LZ4 blocks (stage) -> framed file
 struct LzPiece {
     uint64_t src;            // offset in the block

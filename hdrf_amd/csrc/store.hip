@@ -370,4 +370,21 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
     return e;
 }
 
+// storeDB's recipe SET (DN/DataDeduplicator.java:372-392): copy each block's digests (already
+// contiguous in the batch slot) into the device recipe store; grid (n, 8) x 256
+__global__ void __launch_bounds__(256) recipe_copy_kernel(const RecipeCopy *__restrict__ jobs, int n)
+{
+    if ((int)blockIdx.x >= n) return;
+    const RecipeCopy j = jobs[blockIdx.x];
+    const uint32_t *src = (const uint32_t *)(uintptr_t)j.src;
+    uint32_t *dst = (uint32_t *)(uintptr_t)j.dst;
+    for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < j.words; i += gridDim.y * 256) dst[i] = src[i];
+}
+
+hipError_t launch_recipe_copy(const RecipeCopy *jobs, int n, hipStream_t st)
+{
+    if (n > 0) hipLaunchKernelGGL(recipe_copy_kernel, dim3(n, 8), dim3(256), 0, st, jobs, n);
+    return hipGetLastError();
+}
+
 }  // namespace hdrf
