@@ -769,15 +769,23 @@ static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need);
 // BlockCompressorStream decisions (hadoop-common 3.1.0) depend only on the write sizes, so the
 // host plans the pieces (groups of buffered packets, or <= MAX_INPUT slices of one large write)
 // and the GPU compresses all pieces of the block at once (one wave per piece), then frames them.
+// BlockCompressorStream MAX_INPUT = bufferSize - compressionOverhead (256 KiB buffers): Lz4Codec
+// overhead bufferSize/255 + 16, SnappyCodec bufferSize/6 + 32 (hadoop-common 3.1.0)
+static int64_t stream_max_input(int codec)
+{
+    return codec == 0 ? 262144 - (262144 / 6 + 32) : 262144 - (262144 / 255 + 16);
+}
+
 extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data,
                                      uint64_t len, uint64_t readable, const uint64_t *writes, int32_t nwrites,
                                      uint8_t *out, int64_t cap)
 {
     if (!ctx) return HDRF_E_INVAL;
-    if (codec != 4) return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: only 4 (Lz4Codec) is implemented");
+    if (codec != 4 && codec != 0)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec) and 4 (Lz4Codec) are implemented");
     if (nwrites < 0 || (nwrites && !writes) || (len && !dev_data) || readable < len + kSlack)
         return set_err(ctx, HDRF_E_INVAL, "bad stream arguments (readable must be >= len + 64)");
-    constexpr int64_t kMaxIn = 261100;                  // BlockCompressorStream MAX_INPUT_SIZE
+    const int64_t kMaxIn = stream_max_input(codec);     // BlockCompressorStream MAX_INPUT_SIZE
     std::vector<LzPiece> pieces;
     std::vector<LzOut> outs;
     uint64_t off = 0, gs = 0, lim = 0;
@@ -806,8 +814,20 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
     const uint64_t a_pieces = 0, a_outs = ((uint64_t)n * sizeof(LzPiece) + 255) & ~255ull;
     const uint64_t a_clen = a_outs + (((uint64_t)n * sizeof(LzOut) + 255) & ~255ull);
     const uint64_t a_stage = a_clen + (((uint64_t)n * 4 + 255) & ~255ull);
-    const uint64_t a_file = a_stage + (uint64_t)n * stride;
-    const uint64_t need = a_file + (uint64_t)n * (stride + 8) + 16;
+    const uint64_t a_file = a_stage + (((uint64_t)n * stride + 255) & ~255ull);   // keeps later arrays aligned
+    // snappy: every group split into independent 64 KiB fragments (pieces[i].pad = first one)
+    std::vector<LzPiece> frags;
+    if (codec == 0)
+        for (int i = 0; i < n; i++) {
+            pieces[i].pad = (uint32_t)frags.size();
+            for (uint64_t o = 0; o < pieces[i].len; o += 65536)
+                frags.push_back(LzPiece{pieces[i].src + o, (uint32_t)std::min<uint64_t>(65536, pieces[i].len - o), 0});
+        }
+    const int nf = (int)frags.size();
+    const uint64_t a_frags = a_file + (((uint64_t)n * (stride + 8) + 16 + 255) & ~255ull);
+    const uint64_t a_fclen = a_frags + (((uint64_t)nf * sizeof(LzPiece) + 255) & ~255ull);
+    const uint64_t a_fscr = a_fclen + (((uint64_t)nf * 4 + 255) & ~255ull);
+    const uint64_t need = a_fscr + (uint64_t)nf * snappy_frag_stride() + 16;
     if (int rc = drain(ctx)) return rc;
     if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, need)) return rc;
     uint8_t *R = ctx->d_rd;
@@ -815,7 +835,14 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
     std::vector<uint32_t> clen(n);
     if (n) {
         HIPCK(hipMemcpyAsync(R + a_pieces, pieces.data(), n * sizeof(LzPiece), hipMemcpyHostToDevice, st));
-        HIPCK(launch_lz4_stream((const LzPiece *)(R + a_pieces), n, dev_data, R + a_stage, (uint32_t *)(R + a_clen), st));
+        if (codec == 4) {
+            HIPCK(launch_lz4_stream((const LzPiece *)(R + a_pieces), n, dev_data, R + a_stage, (uint32_t *)(R + a_clen), st));
+        } else {
+            if (nf) HIPCK(hipMemcpyAsync(R + a_frags, frags.data(), nf * sizeof(LzPiece), hipMemcpyHostToDevice, st));
+            HIPCK(launch_snappy_stream((const LzPiece *)(R + a_pieces), n, (const LzPiece *)(R + a_frags), nf, dev_data,
+                                       R + a_fscr, (uint32_t *)(R + a_fclen), R + a_stage, stride,
+                                       (uint32_t *)(R + a_clen), st));
+        }
         HIPCK(hipMemcpyAsync(clen.data(), R + a_clen, n * 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
     }
@@ -837,12 +864,13 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
     return total;
 }
 
-// Hadoop Lz4Codec file (BlockCompressorStream framing: [BE32 raw] ([BE32 clen] block)* groups)
-// -> the LZ4 blocks it holds.  A group's raw length is sliced at MAX_INPUT (261,100), exactly as
-// the stream wrote it; returns false on a malformed frame.
-static bool plan_lz4_frame(const uint8_t *f, int64_t n, std::vector<LzDec> &items, uint64_t *raw_total)
+// Hadoop codec file (BlockCompressorStream framing: [BE32 raw] ([BE32 clen] block)* groups)
+// -> the compressed blocks it holds.  A group's raw length is sliced at the codec's MAX_INPUT
+// (Lz4Codec 261,100, SnappyCodec 218,422), exactly as the stream wrote it; false if malformed.
+static bool plan_lz4_frame(const uint8_t *f, int64_t n, std::vector<LzDec> &items, uint64_t *raw_total,
+                           int codec = 4)
 {
-    constexpr uint64_t kMaxIn = 261100;
+    const uint64_t kMaxIn = (uint64_t)stream_max_input(codec);
     auto be32 = [&](int64_t i) { return ((uint64_t)f[i] << 24) | ((uint64_t)f[i + 1] << 16) | ((uint64_t)f[i + 2] << 8) | f[i + 3]; };
     int64_t i = 0;
     uint64_t o = 0;
@@ -868,12 +896,13 @@ static bool plan_lz4_frame(const uint8_t *f, int64_t n, std::vector<LzDec> &item
 }
 
 // decode a host-resident Lz4Codec file into device memory (dev_out, cap bytes); returns raw length
-static int64_t decode_file(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap)
+static int64_t decode_file(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap,
+                           int codec = 4)
 {
     std::vector<LzDec> items;
     uint64_t raw = 0;
-    if (flen < 0 || (flen && !file) || !plan_lz4_frame(file, flen, items, &raw))
-        return set_err(ctx, HDRF_E_INVAL, "malformed Lz4Codec frame");
+    if (flen < 0 || (flen && !file) || !plan_lz4_frame(file, flen, items, &raw, codec))
+        return set_err(ctx, HDRF_E_INVAL, codec == 4 ? "malformed Lz4Codec frame" : "malformed SnappyCodec frame");
     if ((int64_t)raw > cap || (raw && !dev_out)) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
     if (items.empty()) return (int64_t)raw;
     const int n = (int)items.size();
@@ -885,11 +914,13 @@ static int64_t decode_file(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uin
     HIPCK(hipMemcpyAsync(R + o_file, file, (size_t)flen, hipMemcpyHostToDevice, st));
     HIPCK(hipMemcpyAsync(R + o_items, items.data(), (size_t)n * sizeof(LzDec), hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(R + o_err, 0, 4, st));
-    HIPCK(launch_lz4_decode((const LzDec *)(R + o_items), n, R + o_file, dev_out, (int *)(R + o_err), st));
+    if (codec == 4) HIPCK(launch_lz4_decode((const LzDec *)(R + o_items), n, R + o_file, dev_out, (int *)(R + o_err), st));
+    else HIPCK(launch_snappy_decode((const LzDec *)(R + o_items), n, R + o_file, dev_out, (int *)(R + o_err), st));
     int err = 0;
     HIPCK(hipMemcpyAsync(&err, R + o_err, 4, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    if (err) return set_err(ctx, HDRF_E_INVAL, "corrupt LZ4 block in the Lz4Codec file");
+    if (err) return set_err(ctx, HDRF_E_INVAL, codec == 4 ? "corrupt LZ4 block in the Lz4Codec file"
+                                                          : "corrupt snappy block in the SnappyCodec file");
     return (int64_t)raw;
 }
 
@@ -899,6 +930,17 @@ extern "C" int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int6
 {
     if (!ctx) return HDRF_E_INVAL;
     return decode_file(ctx, file, flen, dev_out, cap);
+}
+
+// The same for a stream-mode block file of codec 0 (SnappyCodec) or 4 (Lz4Codec): DataConstructor's
+// compression-only decoders (DN/DataConstructor.java:102-220)
+extern "C" int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const uint8_t *file, int64_t flen,
+                                           uint8_t *dev_out, int64_t cap)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (codec != 0 && codec != 4)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec) and 4 (Lz4Codec) are implemented");
+    return decode_file(ctx, file, flen, dev_out, cap, codec);
 }
 
 // Make container `id` readable for reconstruction from its chunkDir file (raw, or a closed

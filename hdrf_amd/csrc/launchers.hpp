@@ -108,6 +108,13 @@ struct LzDec {               // one LZ4 block of a Lz4Codec file -> raw bytes
     uint32_t clen, rawlen;
 };
 hipError_t launch_lz4_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
+// stream mode compressor 0 (snappy.hip): pieces (pad = first fragment) split into 64 KiB
+// fragments -> raw snappy groups at stage + i * stride; decoder for SnappyCodec files
+hipError_t launch_snappy_stream(const LzPiece *pieces, int n, const LzPiece *frags, int nf, const uint8_t *base,
+                                uint8_t *scratch, uint32_t *fclen, uint8_t *stage, uint64_t stride, uint32_t *clen,
+                                hipStream_t st);
+uint64_t snappy_frag_stride();
+hipError_t launch_snappy_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
 // compression stage (lz4.hip): closed containers -> Lz4Codec files in the compressed arena
 uint64_t lz4_slot_bytes(uint32_t cmax);
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,

@@ -28,7 +28,7 @@ EXPORTS = [
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_front_launch", "hdrf_gx_front_wait", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
-    "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_lz4_file_decode", "hdrf_container_load",
+    "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_lz4_file_decode", "hdrf_stream_file_decode", "hdrf_container_load",
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
 ]
 
@@ -118,6 +118,7 @@ def load():
         "hdrf_host_alloc": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(_vp)]),
         "hdrf_host_free": (ctypes.c_int, [_vp, _vp]),
         "hdrf_lz4_file_decode": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
+        "hdrf_stream_file_decode": (ctypes.c_int64, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_container_load": (ctypes.c_int, [_vp, ctypes.c_uint32, _u8p, ctypes.c_int64, ctypes.c_int32]),
         "hdrf_container_unload": (ctypes.c_int, [_vp, ctypes.c_uint32]),
         "hdrf_index_load": (ctypes.c_int, [_vp, _u8p, _u8p, ctypes.c_int64]),
@@ -300,6 +301,17 @@ class Context:
         finally:
             self.dev_free(dev)
 
+    def stream_file_decode(self, codec, file, raw_cap):
+        """Decode a stream-mode block file (codec 0 SnappyCodec, 4 Lz4Codec) on the GPU -> raw bytes."""
+        f = _u8(file)
+        dev = self.dev_alloc(raw_cap + 64)
+        try:
+            n = self._ck(self.L.hdrf_stream_file_decode(self._h, codec, _p(f if f.size else np.zeros(1, np.uint8)),
+                                                        f.size, dev, raw_cap))
+            return self.d2h(dev, n).tobytes() if n else b""
+        finally:
+            self.dev_free(dev)
+
     def container_load(self, cid, file, lz4):
         f = _u8(file)
         self._ck(self.L.hdrf_container_load(self._h, cid, _p(f if f.size else np.zeros(1, np.uint8)), f.size,
@@ -329,11 +341,11 @@ class Context:
         self._ck(self.L.hdrf_recipe_load(self._h, block_id, _p(r), r.size))
 
     def stream_block(self, codec, block_id, dev, nbytes, readable, writes):
-        """Stream-mode scheme (compressor 4 = Lz4Codec): the file the reference writes for a block
-        received as write()s of the given sizes -> bytes."""
+        """Stream-mode scheme (compressor 4 = Lz4Codec, 0 = SnappyCodec): the file the reference
+        writes for a block received as write()s of the given sizes -> bytes."""
         w = np.ascontiguousarray(writes, np.uint64)
         wp = _p(w if w.size else np.zeros(1, np.uint64), _u64p)
-        cap = 16 + nbytes + nbytes // 200 + 16 * (len(w) + nbytes // 261100 + 2)
+        cap = 16 + nbytes + nbytes // 6 + 48 * (len(w) + nbytes // 218422 + 2)
         out = np.zeros(cap, np.uint8)
         n = self._ck(self.L.hdrf_stream_block(self._h, codec, block_id, dev, nbytes, readable, wp, len(w), _p(out),
                                               cap))

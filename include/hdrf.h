@@ -106,10 +106,11 @@ int hdrf_wait_batch(hdrf_ctx *ctx);
 int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
                      const uint64_t *block_ids);
 /* Stream-mode schemes (DataNode.compressor 0/3/4/5: the whole block through a Hadoop codec,
- * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec: the file the reference writes to
- * chunkDir+id when the block arrives as write()s of the given sizes (one per packet, summing to
- * len) followed by close().  dev_data needs len + 64 readable bytes.  Returns the file length
- * (written to out), HDRF_E_CAPACITY if cap is too small, HDRF_E_UNSUPPORTED for codecs 0/3/5.
+ * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec, codec 0 = SnappyCodec: the file
+ * the reference writes to chunkDir+id when the block arrives as write()s of the given sizes (one
+ * per packet, summing to len) followed by close().  dev_data needs len + 64 readable bytes.
+ * Returns the file length (written to out), HDRF_E_CAPACITY if cap is too small,
+ * HDRF_E_UNSUPPORTED for codecs 3/5 (LZOP, Gzip).
  * Records the block length (SET id -> BE32(len)) for hdrf_block_length. */
 int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data, uint64_t len,
                           uint64_t readable, const uint64_t *writes, int32_t nwrites, uint8_t *out, int64_t cap);
@@ -121,6 +122,10 @@ int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const
  * file (lz4 = 1 for a closed container's Lz4Codec file, 0 for raw bytes) after its arena slot was
  * reused or the DataNode restarted; hdrf_container_unload frees that copy. */
 int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap);
+/* The same for a stream-mode block file of codec 0 (SnappyCodec) or 4 (Lz4Codec): the
+ * compression-only decoders of DataConstructor (DN/DataConstructor.java:102-220). */
+int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const uint8_t *file, int64_t flen, uint8_t *dev_out,
+                                int64_t cap);
 int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4);
 int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id);
 /* Restore a DataNode from its persisted state (the Redis keys + chunkDir files), on a fresh or

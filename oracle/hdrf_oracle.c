@@ -904,6 +904,241 @@ int64_t hdrf_oracle_hadoop_lz4_stream(const uint8_t *src, const int64_t *writes,
     return p - dst;
 }
 
+/* ---- Snappy (stream mode compressor == 0, DN/BlockReceiver.java:826-873,887-894) ----------
+ * Hadoop SnappyCodec (hadoop-common 3.1.0): BlockCompressorStream with a 256 KiB buffer and
+ * compressionOverhead = bufferSize / 6 + 32, so MAX_INPUT = 218,422; each group is one
+ * snappy::RawCompress call made by the native SnappyCompressor (snappy-c snappy_compress).
+ * Third-party and not in the reference tree.  Restated from google/snappy's published
+ * compressor (default level 1): varint(n), then independent fragments of 64 KiB, each with a
+ * fresh hash table of max(256, next pow2 >= fragment) u16 entries capped at 2^15, hash
+ * ((v * 0x1e35a7bd) >> 17) & mask, the skip heuristic (step = skip++ >> 5 from 32), greedy copies
+ * with the ip-1 / ip table refresh, 64-byte copy splitting (>= 68: 64, > 64: 60).  Pinned byte
+ * for byte against the snappy bundled in pyarrow (tests/test_snappy.py); vs Hadoop's own
+ * libsnappy UNPINNED (its version is the host's). */
+#define SNAPPY_FRAG 65536
+#define HADOOP_SNAPPY_MAX_INPUT 218422
+
+static uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+
+static uint8_t *sn_literal(uint8_t *op, const uint8_t *lit, int64_t len)
+{
+    const uint32_t n = (uint32_t)(len - 1);
+    if (n < 60) {
+        *op++ = (uint8_t)(n << 2);
+    } else {
+        int cnt = 0;
+        for (uint32_t t = n; t; t >>= 8) cnt++;
+        *op++ = (uint8_t)((59 + cnt) << 2);
+        for (int k = 0; k < cnt; k++) *op++ = (uint8_t)(n >> (8 * k));
+    }
+    memcpy(op, lit, (size_t)len);
+    return op + len;
+}
+
+static uint8_t *sn_copy64(uint8_t *op, uint32_t off, uint32_t len)
+{
+    if (len < 12 && off < 2048) {
+        *op++ = (uint8_t)(1 | ((len - 4) << 2) | ((off >> 8) << 5));
+        *op++ = (uint8_t)off;
+    } else {
+        *op++ = (uint8_t)(2 | ((len - 1) << 2));
+        *op++ = (uint8_t)off;
+        *op++ = (uint8_t)(off >> 8);
+    }
+    return op;
+}
+
+static uint8_t *sn_copy(uint8_t *op, uint32_t off, int64_t len)
+{
+    while (len >= 68) { op = sn_copy64(op, off, 64); len -= 64; }
+    if (len > 64) { op = sn_copy64(op, off, 60); len -= 60; }
+    return sn_copy64(op, off, (uint32_t)len);
+}
+
+static uint8_t *sn_fragment(const uint8_t *src, int64_t n, uint8_t *op, uint16_t *tab)
+{
+    uint32_t ts = 256;
+    while (ts < (1u << 15) && ts < n) ts <<= 1;
+    const uint32_t mask = ts - 1;
+    memset(tab, 0, ts * sizeof(uint16_t));
+#define SNH(v) ((((uint32_t)(v) * 0x1e35a7bdu) >> 17) & mask)
+    int64_t ip = 0;
+    if (n >= 15) {
+        const int64_t lim = n - 15;
+        for (;;) {
+            const int64_t next_emit = ip++;
+            uint32_t skip = 32;
+            int64_t cand;
+            for (;;) {                                         /* search with growing strides */
+                const uint32_t h = SNH(ld32(src + ip));
+                const uint32_t step = skip >> 5;
+                skip += step;
+                if (ip + step > lim) { ip = next_emit; goto remainder; }
+                cand = tab[h];
+                tab[h] = (uint16_t)ip;
+                if (ld32(src + ip) == ld32(src + cand)) break;
+                ip += step;
+            }
+            op = sn_literal(op, src + next_emit, ip - next_emit);
+            for (;;) {                                         /* copies back to back */
+                const int64_t base = ip;
+                int64_t m = 4;
+                while (ip + m < n && src[cand + m] == src[ip + m]) m++;
+                ip += m;
+                op = sn_copy(op, (uint32_t)(base - cand), m);
+                if (ip >= lim) goto remainder;
+                tab[SNH(ld32(src + ip - 1))] = (uint16_t)(ip - 1);
+                const uint32_t h = SNH(ld32(src + ip));
+                cand = tab[h];
+                tab[h] = (uint16_t)ip;
+                if (ld32(src + ip) != ld32(src + cand)) break;
+            }
+        }
+    }
+remainder:
+    if (ip < n) op = sn_literal(op, src + ip, n - ip);
+#undef SNH
+    return op;
+}
+
+int64_t hdrf_oracle_snappy_bound(int64_t n) { return 32 + n + n / 6; }
+
+int64_t hdrf_oracle_snappy_compress(const uint8_t *src, int64_t n, uint8_t *dst)
+{
+    static __thread uint16_t tab[1 << 15];
+    uint8_t *op = dst;
+    for (uint64_t v = (uint64_t)n; ; v >>= 7) {             /* varint32 of the raw length */
+        if (v < 0x80) { *op++ = (uint8_t)v; break; }
+        *op++ = (uint8_t)(v | 0x80);
+    }
+    for (int64_t o = 0; o < n; o += SNAPPY_FRAG)
+        op = sn_fragment(src + o, n - o < SNAPPY_FRAG ? n - o : SNAPPY_FRAG, op, tab);
+    return op - dst;
+}
+
+/* snappy::RawUncompress; returns the decoded length or -1 on malformed input */
+int64_t hdrf_oracle_snappy_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap)
+{
+    int64_t i = 0, o = 0;
+    uint64_t raw = 0;
+    for (int sh = 0;; sh += 7) {
+        if (i >= n || sh > 28) return -1;
+        const uint8_t b = src[i++];
+        raw |= (uint64_t)(b & 0x7f) << sh;
+        if (!(b & 0x80)) break;
+    }
+    if ((int64_t)raw > cap) return -1;
+    while (i < n) {
+        const uint8_t tag = src[i++];
+        int64_t len, off;
+        if ((tag & 3) == 0) {
+            len = (tag >> 2) + 1;
+            if (len > 60) {
+                const int cnt = (int)len - 60;
+                if (i + cnt > n) return -1;
+                len = 0;
+                for (int k = 0; k < cnt; k++) len |= (int64_t)src[i + k] << (8 * k);
+                len += 1;
+                i += cnt;
+            }
+            if (i + len > n || o + len > (int64_t)raw) return -1;
+            memcpy(dst + o, src + i, (size_t)len);
+            i += len; o += len;
+            continue;
+        }
+        if ((tag & 3) == 1) {
+            if (i + 1 > n) return -1;
+            len = 4 + ((tag >> 2) & 7);
+            off = ((int64_t)(tag >> 5) << 8) | src[i];
+            i += 1;
+        } else if ((tag & 3) == 2) {
+            if (i + 2 > n) return -1;
+            len = (tag >> 2) + 1;
+            off = src[i] | ((int64_t)src[i + 1] << 8);
+            i += 2;
+        } else {
+            if (i + 4 > n) return -1;
+            len = (tag >> 2) + 1;
+            off = (int64_t)ld32(src + i);
+            i += 4;
+        }
+        if (off == 0 || off > o || o + len > (int64_t)raw) return -1;
+        for (int64_t k = 0; k < len; k++) dst[o + k] = dst[o - off + k];
+        o += len;
+    }
+    return o == (int64_t)raw ? o : -1;
+}
+
+/* Stream mode through a Hadoop BlockCompressorStream codec: 0 SnappyCodec, 4 Lz4Codec */
+typedef int64_t (*raw_codec)(const uint8_t *, int64_t, uint8_t *);
+
+static uint8_t *codec_group(uint8_t *p, const uint8_t *src, int64_t n, raw_codec f)
+{
+    p = put_be32(p, (uint32_t)n);
+    const int64_t c = f(src, n, p + 4);
+    put_be32(p, (uint32_t)c);
+    return p + 4 + c;
+}
+
+int64_t hdrf_oracle_hadoop_stream_bound(int codec, int64_t n, int64_t nwrites)
+{
+    return codec == 0 ? hdrf_oracle_snappy_bound(n) + 24 * (nwrites + 1) + 48 * (n / HADOOP_SNAPPY_MAX_INPUT + 1)
+                      : hdrf_oracle_hadoop_lz4_stream_bound(n, nwrites);
+}
+
+int64_t hdrf_oracle_hadoop_stream(int codec, const uint8_t *src, const int64_t *writes, int64_t nwrites, uint8_t *dst)
+{
+    if (codec == 4) return hdrf_oracle_hadoop_lz4_stream(src, writes, nwrites, dst);
+    if (codec != 0) return -1;
+    const raw_codec f = hdrf_oracle_snappy_compress;
+    const int64_t MAX = HADOOP_SNAPPY_MAX_INPUT;
+    uint8_t *p = dst;
+    int64_t off = 0, gs = 0, lim = 0;
+    for (int64_t w = 0; w < nwrites; w++) {
+        const int64_t len = writes[w];
+        if (lim > 0 && len + lim > MAX) { p = codec_group(p, src + gs, lim, f); lim = 0; }
+        if (len > MAX) {
+            p = put_be32(p, (uint32_t)len);
+            for (int64_t o = 0; o < len; o += MAX) {
+                const int64_t m = len - o < MAX ? len - o : MAX;
+                const int64_t c = f(src + off + o, m, p + 4);
+                put_be32(p, (uint32_t)c);
+                p += 4 + c;
+            }
+            off += len;
+            continue;
+        }
+        if (lim == 0) gs = off;
+        lim += len;
+        off += len;
+    }
+    p = lim > 0 ? codec_group(p, src + gs, lim, f) : put_be32(p, 0);
+    return p - dst;
+}
+
+/* BlockDecompressorStream for codec 0 (snappy) or 4 (lz4); decoded length or -1 */
+int64_t hdrf_oracle_hadoop_unframe(int codec, const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap)
+{
+    if (codec == 4) return hdrf_oracle_hadoop_lz4_unframe(src, n, dst, cap);
+    if (codec != 0) return -1;
+    int64_t o = 0, i = 0;
+    while (i + 4 <= n) {
+        const int64_t total = ((int64_t)src[i] << 24) | (src[i + 1] << 16) | (src[i + 2] << 8) | src[i + 3];
+        i += 4;
+        int64_t got = 0;
+        while (got < total) {
+            if (i + 4 > n) return -1;
+            const int64_t c = ((int64_t)src[i] << 24) | (src[i + 1] << 16) | (src[i + 2] << 8) | src[i + 3];
+            i += 4;
+            if (i + c > n) return -1;
+            const int64_t d = hdrf_oracle_snappy_decompress(src + i, c, dst + o, cap - o);
+            if (d < 0) return -1;
+            i += c; o += d; got += d;
+        }
+    }
+    return i == n ? o : -1;
+}
+
 /* BlockDecompressorStream over the frame above; returns the decoded length or -1 */
 int64_t hdrf_oracle_hadoop_lz4_unframe(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap)
 {

@@ -79,6 +79,16 @@ int64_t hdrf_oracle_hadoop_lz4_unframe(const uint8_t *src, int64_t n, uint8_t *d
 int64_t hdrf_oracle_hadoop_lz4_stream_bound(int64_t n, int64_t nwrites);
 int64_t hdrf_oracle_hadoop_lz4_stream(const uint8_t *src, const int64_t *writes, int64_t nwrites, uint8_t *dst);
 
+/* Stream mode compressor == 0 (Hadoop SnappyCodec, MAX_INPUT 218,422): snappy raw format
+ * restated from google/snappy; pinned against pyarrow's bundled snappy, vs Hadoop UNPINNED. */
+int64_t hdrf_oracle_snappy_bound(int64_t n);
+int64_t hdrf_oracle_snappy_compress(const uint8_t *src, int64_t n, uint8_t *dst);
+int64_t hdrf_oracle_snappy_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+/* codec 0 (SnappyCodec) or 4 (Lz4Codec) stream file / its decoding */
+int64_t hdrf_oracle_hadoop_stream_bound(int codec, int64_t n, int64_t nwrites);
+int64_t hdrf_oracle_hadoop_stream(int codec, const uint8_t *src, const int64_t *writes, int64_t nwrites, uint8_t *dst);
+int64_t hdrf_oracle_hadoop_unframe(int codec, const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+
 /* Synthetic corpus (shared spec with hdrf_amd corpus generator). */
 uint64_t hdrf_oracle_mix64(uint64_t z);
 void hdrf_oracle_corpus_roots(uint64_t seed, uint32_t dup_ppm, int64_t nblocks, int64_t segs_per_block,

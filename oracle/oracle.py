@@ -76,6 +76,19 @@ def lib():
         for name in ("hdrf_oracle_lz4_decompress", "hdrf_oracle_hadoop_lz4_unframe"):
             getattr(L, name).argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
             getattr(L, name).restype = ctypes.c_int64
+        L.hdrf_oracle_snappy_bound.argtypes = [ctypes.c_int64]
+        L.hdrf_oracle_snappy_bound.restype = ctypes.c_int64
+        L.hdrf_oracle_snappy_compress.argtypes = [_u8p, ctypes.c_int64, _u8p]
+        L.hdrf_oracle_snappy_compress.restype = ctypes.c_int64
+        L.hdrf_oracle_snappy_decompress.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
+        L.hdrf_oracle_snappy_decompress.restype = ctypes.c_int64
+        L.hdrf_oracle_hadoop_stream_bound.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int64]
+        L.hdrf_oracle_hadoop_stream_bound.restype = ctypes.c_int64
+        L.hdrf_oracle_hadoop_stream.argtypes = [ctypes.c_int, _u8p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64,
+                                                _u8p]
+        L.hdrf_oracle_hadoop_stream.restype = ctypes.c_int64
+        L.hdrf_oracle_hadoop_unframe.argtypes = [ctypes.c_int, _u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
+        L.hdrf_oracle_hadoop_unframe.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -272,3 +285,41 @@ class Oracle:
         out = np.zeros(max(need, 1), np.uint8)
         m = lib().hdrf_oracle_container(self._h, cid, _p(out), need, ctypes.byref(closed))
         return out[:m].tobytes(), bool(closed.value)
+
+
+def snappy_raw(data):
+    """snappy::RawCompress (google/snappy level 1) -> raw snappy bytes (oracle restatement)."""
+    a = _as_u8(data)
+    out = np.zeros(lib().hdrf_oracle_snappy_bound(a.size) + 8, np.uint8)
+    n = lib().hdrf_oracle_snappy_compress(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out))
+    return out[:n].tobytes()
+
+
+def snappy_raw_decode(data, cap):
+    a = _as_u8(data)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = lib().hdrf_oracle_snappy_decompress(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), cap)
+    return None if n < 0 else out[:n].tobytes()
+
+
+def hadoop_stream(codec, data, writes):
+    """Stream mode through a Hadoop codec output stream (codec 0 SnappyCodec, 4 Lz4Codec): one
+    write() per packet of the given sizes, then close() -> file bytes
+    (DN/BlockReceiver.java:826-873,887-894,1238-1256)."""
+    a = _as_u8(data)
+    w = np.ascontiguousarray(writes, np.int64)
+    assert int(w.sum()) == a.size
+    buf = a if a.size else np.zeros(1, np.uint8)
+    out = np.zeros(lib().hdrf_oracle_hadoop_stream_bound(codec, a.size, w.size), np.uint8)
+    n = lib().hdrf_oracle_hadoop_stream(codec, _p(buf), w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), w.size,
+                                        _p(out))
+    if n < 0:
+        raise ValueError("unsupported stream codec %d" % codec)
+    return out[:n].tobytes()
+
+
+def hadoop_stream_decode(codec, data, cap):
+    a = _as_u8(data)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = lib().hdrf_oracle_hadoop_unframe(codec, _p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), cap)
+    return None if n < 0 else out[:n].tobytes()

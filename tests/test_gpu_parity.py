@@ -414,6 +414,58 @@ def test_lz4_file_decode_round_trip(kind):
     ctx.close()
 
 
+@pytest.mark.parametrize("case", ["packets", "ragged", "single", "empty", "tail_large", "kinds"])
+def test_stream_mode_snappy_file_matches_oracle(case):
+    """Stream-mode scheme compressor 0 (SnappyCodec, DN/BlockReceiver.java:826-873,887-894): the
+    GPU writes the oracle's SnappyCodec file byte for byte (MAX_INPUT 218,422 groups of
+    independent 64 KiB snappy fragments) for every write pattern; codecs 3/5 stay unsupported."""
+    from oracle.oracle import hadoop_stream
+    n = {"packets": 3_000_000, "ragged": 1_200_000, "single": 700_000, "empty": 0, "tail_large": 900_000,
+         "kinds": 8 * 70_001}[case]
+    kinds = ["text", "random", "binary", "zeros"] if case != "kinds" else \
+        ["random", "zeros", "ff", "text", "lowent", "periodic", "sparse", "binary"]
+    parts = [make_block(k, 90 + i, n // len(kinds) + 1) for i, k in enumerate(kinds)]
+    d = np.concatenate(parts)[:n]
+    writes = {"packets": [64_512] * (n // 64_512) + [n % 64_512],
+              "ragged": [1000, 0, 50_000, 600_000, 249_000, 300_000], "single": [n], "empty": [],
+              "tail_large": [1000, 899_000], "kinds": [70_001] * 8}[case]
+    ctx = Context(**SMALL)
+    dev = ctx.dev_alloc(n + 4096)
+    if n:
+        ctx.h2d(dev, d)
+    f = ctx.stream_block(0, 79, dev, n, n + 4096, writes)
+    assert f == hadoop_stream(0, d, writes)
+    assert ctx.block_length(79) == n
+    assert ctx.stream_file_decode(0, f, n) == d.tobytes()
+    for codec in (3, 5):
+        with pytest.raises(HdrfError):
+            ctx.stream_block(codec, 78, dev, n, n + 4096, writes)
+    ctx.dev_free(dev)
+    ctx.close()
+
+
+@pytest.mark.parametrize("kind", ["random", "text", "zeros", "lowent", "periodic", "sparse"])
+def test_snappy_file_decode_round_trip(kind):
+    """GPU SnappyCodec decoder (DataConstructor's compression-only read, DN/DataConstructor.java:
+    102-220): oracle files of several write patterns decode to the raw bytes; corrupt files are
+    rejected."""
+    from oracle.oracle import hadoop_stream
+    n = 1_100_000
+    d = make_block(kind, 33, n).tobytes()
+    ctx = Context(**SMALL)
+    for w in ([n], [64_512] * (n // 64_512) + [n % 64_512], [1000, 700_000, n - 701_000]):
+        assert ctx.stream_file_decode(0, hadoop_stream(0, d, w), n) == d
+    assert ctx.stream_file_decode(0, hadoop_stream(0, d[:5000], [5000]), n) == d[:5000]
+    assert ctx.stream_file_decode(0, hadoop_stream(0, b"", []), n) == b""
+    good = hadoop_stream(0, d[:100_000], [100_000])
+    for bad in (good[:-1],
+                good[:4] + (int.from_bytes(good[4:8], "big") - 1).to_bytes(4, "big") + good[8:-1],
+                good[:8] + b"\x00" + good[9:]):                     # varint length 0 != raw length
+        with pytest.raises(HdrfError):
+            ctx.stream_file_decode(0, bad, n)
+    ctx.close()
+
+
 def test_reconstruct_from_loaded_container_files():
     """A context whose arena slots were reused (small arena) cannot rebuild early blocks from
     device memory; after loading the chunkDir files of the missing containers (closed ones as
