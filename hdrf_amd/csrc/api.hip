@@ -764,8 +764,8 @@ extern "C" int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *c
 
 static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need);
 
-// Stream mode (compressor 4, DN/BlockReceiver.java:846-855,887-894,1238-1256): the block as
-// Lz4Codec.createOutputStream(file).write(packet) per received packet, then close().  The
+// Stream mode (compressor 4 / 0, DN/BlockReceiver.java:826-873,887-894,1238-1256): the block as
+// codec.createOutputStream(file).write(packet) per received packet, then close().  The
 // BlockCompressorStream decisions (hadoop-common 3.1.0) depend only on the write sizes, so the
 // host plans the pieces (groups of buffered packets, or <= MAX_INPUT slices of one large write)
 // and the GPU compresses all pieces of the block at once (one wave per piece), then frames them.
@@ -862,6 +862,20 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
     if (trailer) std::memset(out + pos, 0, 4);
     ctx->lengths[(uint32_t)block_id] = (int64_t)len;   // SET id -> BE32(len) (:1238-1256)
     return total;
+}
+
+// The same for a host-resident block (the DataNode's received bytes): staged H2D, then streamed
+extern "C" int64_t hdrf_stream_block_host(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *data,
+                                          uint64_t len, const uint64_t *writes, int32_t nwrites, uint8_t *out,
+                                          int64_t cap)
+{
+    if (!ctx || (len && !data)) return HDRF_E_INVAL;
+    if (codec != 4 && codec != 0)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec) and 4 (Lz4Codec) are implemented");
+    if (int rc = drain(ctx)) return rc;
+    if (int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, len + kSlack)) return rc;
+    if (len) HIPCK(hipMemcpy(ctx->d_stage, data, len, hipMemcpyHostToDevice));
+    return hdrf_stream_block(ctx, codec, block_id, ctx->d_stage, len, len + kSlack, writes, nwrites, out, cap);
 }
 
 // Hadoop codec file (BlockCompressorStream framing: [BE32 raw] ([BE32 clen] block)* groups)

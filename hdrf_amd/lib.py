@@ -28,7 +28,8 @@ EXPORTS = [
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_front_launch", "hdrf_gx_front_wait", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
-    "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_lz4_file_decode", "hdrf_stream_file_decode", "hdrf_container_load",
+    "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_stream_block_host", "hdrf_lz4_file_decode",
+    "hdrf_stream_file_decode", "hdrf_container_load",
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
 ]
 
@@ -126,6 +127,8 @@ def load():
         "hdrf_recipe_load": (ctypes.c_int, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
         "hdrf_stream_block": (ctypes.c_int64, [_vp, ctypes.c_int32, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                                ctypes.c_uint64, _u64p, ctypes.c_int32, _u8p, ctypes.c_int64]),
+        "hdrf_stream_block_host": (ctypes.c_int64, [_vp, ctypes.c_int32, ctypes.c_uint64, _u8p, ctypes.c_uint64,
+                                                    _u64p, ctypes.c_int32, _u8p, ctypes.c_int64]),
         "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
         "hdrf_reconstruct": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_reconstruct_block": (ctypes.c_int64, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
@@ -349,6 +352,17 @@ class Context:
         out = np.zeros(cap, np.uint8)
         n = self._ck(self.L.hdrf_stream_block(self._h, codec, block_id, dev, nbytes, readable, wp, len(w), _p(out),
                                               cap))
+        return out[:n].tobytes()
+
+    def stream_block_host(self, codec, block_id, data, writes):
+        """hdrf_stream_block for host bytes (staged H2D by the library)."""
+        d = _u8(data)
+        w = np.ascontiguousarray(writes, np.uint64)
+        wp = _p(w if w.size else np.zeros(1, np.uint64), _u64p)
+        cap = 16 + d.size + d.size // 6 + 48 * (len(w) + d.size // 218422 + 2)
+        out = np.zeros(cap, np.uint8)
+        n = self._ck(self.L.hdrf_stream_block_host(self._h, codec, block_id, _p(d if d.size else np.zeros(1, np.uint8)),
+                                                   d.size, wp, len(w), _p(out), cap))
         return out[:n].tobytes()
 
     def last_nblocks(self):

@@ -114,6 +114,9 @@ int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_
  * Records the block length (SET id -> BE32(len)) for hdrf_block_length. */
 int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data, uint64_t len,
                           uint64_t readable, const uint64_t *writes, int32_t nwrites, uint8_t *out, int64_t cap);
+/* hdrf_stream_block for a host-resident block (copied H2D first; no alignment or slack needed). */
+int64_t hdrf_stream_block_host(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *data, uint64_t len,
+                               const uint64_t *writes, int32_t nwrites, uint8_t *out, int64_t cap);
 /* Read side for container / block FILES (DataConstructor's Lz4Codec input stream,
  * DN/DataConstructor.java:171-176,495-500): hdrf_lz4_file_decode decodes a Hadoop Lz4Codec file
  * (BlockCompressorStream framing, as written by compressor 2 containers and compressor 4 blocks)

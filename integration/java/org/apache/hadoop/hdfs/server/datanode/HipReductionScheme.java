@@ -41,6 +41,17 @@ public final class HipReductionScheme extends ReductionScheme {
     wait0(ctx);
   }
 
+  /**
+   * Stream-mode schemes (DataNode.compressor 0 SnappyCodec, 4 Lz4Codec; BlockReceiver.java:
+   * 826-873,887-894,1238-1256): the file the reference writes to chunkDir + blockId when the block
+   * arrives as write()s of the given packet sizes followed by close().  The caller stores it and
+   * the library records SET blockId -> BE32(length).
+   */
+  public byte[] streamBlock(int codec, ByteBuffer block, long blockId, long[] packetSizes) throws IOException {
+    if (!block.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
+    return stream0(ctx, codec, block, block.position(), blockId, packetSizes);
+  }
+
   @Override
   public byte[] reconstruct(long blockId) throws IOException {
     return reconstruct0(ctx, blockId);          // DataConstructor(blkID, recipe).data
@@ -68,5 +79,7 @@ public final class HipReductionScheme extends ReductionScheme {
   private static native void wait0(long ctx) throws IOException;
   private static native long length0(long ctx, long blockId) throws IOException;
   private static native byte[] recipe0(long ctx, long blockId) throws IOException;
+  private static native byte[] stream0(long ctx, int codec, ByteBuffer direct, int len, long blockId, long[] writes)
+      throws IOException;
   private static native void close0(long ctx);
 }

@@ -5,6 +5,7 @@
  * Errors become IOException; DDRunner-style callers may log and continue (DDRunner.java:27-31). */
 #include <jni.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include "hdrf.h"
@@ -105,6 +106,30 @@ JNIEXPORT jbyteArray JNICALL JFN(reconstruct0)(JNIEnv *env, jclass cls, jlong h,
     (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);
     free(tmp);
     return out;
+}
+
+/* stream mode (compressor 0 SnappyCodec / 4 Lz4Codec): the block's chunkDir file for packet writes */
+JNIEXPORT jbyteArray JNICALL JFN(stream0)(JNIEnv *env, jclass cls, jlong h, jint codec, jobject buf, jint len,
+                                          jlong id, jlongArray writes)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
+    const jsize nw = (*env)->GetArrayLength(env, writes);
+    if (!p && len) { throw_io(env, ctx, HDRF_E_INVAL); return NULL; }
+    jlong *w = (*env)->GetLongArrayElements(env, writes, NULL);
+    const int64_t cap = 64 + (int64_t)len + len / 6 + 48 * ((int64_t)nw + len / 218422 + 2);
+    uint8_t *out = (uint8_t *)malloc((size_t)cap);
+    int64_t n = out ? hdrf_stream_block_host(ctx, codec, (uint64_t)id, p, (uint64_t)len, (const uint64_t *)w, nw, out,
+                                             cap)
+                    : HDRF_E_INVAL;
+    (*env)->ReleaseLongArrayElements(env, writes, w, JNI_ABORT);
+    jbyteArray r = NULL;
+    if (n < 0) throw_io(env, ctx, (int)n);
+    else if ((r = (*env)->NewByteArray(env, (jsize)n)) != NULL)
+        (*env)->SetByteArrayRegion(env, r, 0, (jsize)n, (const jbyte *)out);
+    free(out);
+    return r;
 }
 
 JNIEXPORT void JNICALL JFN(close0)(JNIEnv *env, jclass cls, jlong h)

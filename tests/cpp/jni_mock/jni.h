@@ -1,0 +1,32 @@
+/* Minimal stand-in for a JDK's jni.h, for a compile-only check of integration/jni/hdrf_jni.c in
+ * this JDK-less image (tests/test_cpp_scheme.py).  Only the types and the JNIEnv functions the
+ * shim calls, with the JNI specification's signatures; nothing is linked or run. */
+#pragma once
+#include <stdint.h>
+
+#define JNIEXPORT __attribute__((visibility("default")))
+#define JNICALL
+#define JNI_ABORT 2
+
+typedef int32_t jint;
+typedef int64_t jlong;
+typedef int8_t jbyte;
+typedef jint jsize;
+typedef struct _jobject *jobject;
+typedef jobject jclass;
+typedef jobject jarray;
+typedef jarray jbyteArray;
+typedef jarray jlongArray;
+
+struct JNINativeInterface_;
+typedef const struct JNINativeInterface_ *JNIEnv;
+struct JNINativeInterface_ {
+    jclass (*FindClass)(JNIEnv *env, const char *name);
+    jint (*ThrowNew)(JNIEnv *env, jclass clazz, const char *msg);
+    void *(*GetDirectBufferAddress)(JNIEnv *env, jobject buf);
+    jsize (*GetArrayLength)(JNIEnv *env, jarray array);
+    jlong *(*GetLongArrayElements)(JNIEnv *env, jlongArray array, unsigned char *isCopy);
+    void (*ReleaseLongArrayElements)(JNIEnv *env, jlongArray array, jlong *elems, jint mode);
+    jbyteArray (*NewByteArray)(JNIEnv *env, jsize len);
+    void (*SetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, const jbyte *buf);
+};

@@ -33,3 +33,11 @@ def test_cpp_scheme_matches_oracle_on_gpu(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
     assert r.returncode == 0 and "PASS" in r.stdout
+
+
+def test_jni_shim_compiles():
+    """integration/jni/hdrf_jni.c (the binding a maintainer adds to the DataNode) compiles against
+    include/hdrf.h; the JDK is absent here, so a minimal jni.h with the spec's signatures stands in."""
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-fsyntax-only", "-I", os.path.join(ROOT, "include"),
+                    "-I", os.path.join(ROOT, "tests", "cpp", "jni_mock"),
+                    os.path.join(ROOT, "integration", "jni", "hdrf_jni.c")], check=True)

@@ -435,6 +435,7 @@ def test_stream_mode_snappy_file_matches_oracle(case):
         ctx.h2d(dev, d)
     f = ctx.stream_block(0, 79, dev, n, n + 4096, writes)
     assert f == hadoop_stream(0, d, writes)
+    assert ctx.stream_block_host(0, 80, d, writes) == f
     assert ctx.block_length(79) == n
     assert ctx.stream_file_decode(0, f, n) == d.tobytes()
     for codec in (3, 5):
