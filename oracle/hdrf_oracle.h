@@ -84,6 +84,12 @@ int64_t hdrf_oracle_hadoop_lz4_stream(const uint8_t *src, const int64_t *writes,
 int64_t hdrf_oracle_snappy_bound(int64_t n);
 int64_t hdrf_oracle_snappy_compress(const uint8_t *src, int64_t n, uint8_t *dst);
 int64_t hdrf_oracle_snappy_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+/* Stream mode compressor == 5 (Hadoop GzipCodec over native zlib, level 6): zlib 1.2.11
+ * deflate_slow + trees restated (hdrf_gzip.c); pinned byte for byte against this image's
+ * zlib 1.2.11.  The file is one gzip member (header OS byte 3, CRC-32 + ISIZE trailer). */
+int64_t hdrf_oracle_gzip_bound(int64_t n);
+int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst);
+uint32_t hdrf_oracle_crc32(const uint8_t *p, int64_t n);
 /* codec 0 (SnappyCodec) or 4 (Lz4Codec) stream file / its decoding */
 int64_t hdrf_oracle_hadoop_stream_bound(int codec, int64_t n, int64_t nwrites);
 int64_t hdrf_oracle_hadoop_stream(int codec, const uint8_t *src, const int64_t *writes, int64_t nwrites, uint8_t *dst);

@@ -89,6 +89,12 @@ def lib():
         L.hdrf_oracle_hadoop_stream.restype = ctypes.c_int64
         L.hdrf_oracle_hadoop_unframe.argtypes = [ctypes.c_int, _u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
         L.hdrf_oracle_hadoop_unframe.restype = ctypes.c_int64
+        L.hdrf_oracle_gzip_bound.argtypes = [ctypes.c_int64]
+        L.hdrf_oracle_gzip_bound.restype = ctypes.c_int64
+        L.hdrf_oracle_gzip_compress.argtypes = [_u8p, ctypes.c_int64, _u8p]
+        L.hdrf_oracle_gzip_compress.restype = ctypes.c_int64
+        L.hdrf_oracle_crc32.argtypes = [_u8p, ctypes.c_int64]
+        L.hdrf_oracle_crc32.restype = ctypes.c_uint32
         _lib = L
     return _lib
 
@@ -315,6 +321,17 @@ def hadoop_stream(codec, data, writes):
                                         _p(out))
     if n < 0:
         raise ValueError("unsupported stream codec %d" % codec)
+    return out[:n].tobytes()
+
+
+def gzip_stream(data):
+    """Stream mode compressor 5 (Hadoop GzipCodec, native zlib level 6): the block file
+    (DN/BlockReceiver.java:858-873); any packet-write pattern gives the same bytes."""
+    a = _as_u8(data)
+    out = np.zeros(lib().hdrf_oracle_gzip_bound(a.size), np.uint8)
+    n = lib().hdrf_oracle_gzip_compress(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out))
+    if n < 0:
+        raise MemoryError("gzip oracle state")
     return out[:n].tobytes()
 
 
