@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--blocks", type=int, default=512)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--block-mib", type=int, default=128)
     ap.add_argument("--seg-mib", type=int, default=1)
     ap.add_argument("--dup-ppm", type=int, default=500000)
