@@ -957,6 +957,19 @@ extern "C" int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const u
     return decode_file(ctx, file, flen, dev_out, cap, codec);
 }
 
+// Compressor 5 stage 1 (gzip.hip): per-position longest_match answers for both chain limits.
+extern "C" int hdrf_gzip_match_pass(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t len, uint32_t *dev_prev,
+                                    uint32_t *dev_out128, uint32_t *dev_out32)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (len && (!dev_data || !dev_prev || !dev_out128 || !dev_out32)) return set_err(ctx, HDRF_E_INVAL, "null buffer");
+    if (len >= (1ull << 31)) return set_err(ctx, HDRF_E_INVAL, "gzip match pass: len must be < 2^31");
+    if (int rc = drain(ctx)) return rc;
+    HIPCK(launch_gzip_match(dev_data, (int64_t)len, dev_prev, dev_out128, dev_out32, ctx->st));
+    HIPCK(hipStreamSynchronize(ctx->st));
+    return 0;
+}
+
 // Make container `id` readable for reconstruction from its chunkDir file (raw, or a closed
 // container's Lz4Codec file): a DataNode that restarted, or whose arena slot was reused.
 extern "C" int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4)

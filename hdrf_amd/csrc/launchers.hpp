@@ -114,6 +114,10 @@ hipError_t launch_snappy_stream(const LzPiece *pieces, int n, const LzPiece *fra
                                 uint8_t *scratch, uint32_t *fclen, uint8_t *stage, uint64_t stride, uint32_t *clen,
                                 hipStream_t st);
 uint64_t snappy_frag_stride();
+// stream mode compressor 5 (gzip.hip), stage 1 of the GPU deflate: per-position chain-128 /
+// chain-32 longest_match answers ((len << 16) | dist); prev = n u32 scratch
+hipError_t launch_gzip_match(const uint8_t *src, int64_t n, uint32_t *prev, uint32_t *out128, uint32_t *out32,
+                             hipStream_t st);
 hipError_t launch_snappy_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
 // compression stage (lz4.hip): closed containers -> Lz4Codec files in the compressed arena
 uint64_t lz4_slot_bytes(uint32_t cmax);

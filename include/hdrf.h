@@ -129,6 +129,14 @@ int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, u
  * compression-only decoders of DataConstructor (DN/DataConstructor.java:102-220). */
 int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const uint8_t *file, int64_t flen, uint8_t *dev_out,
                                 int64_t cap);
+/* Stage 1 of the GPU compressor 5 (GzipCodec = zlib level 6 deflate_slow, DN/BlockReceiver.java:
+ * 858-873): for every position p of the len device bytes, the answer zlib's
+ * longest_match gives at p with a 128-candidate chain (out128, prev_length < 8) and a 32-candidate
+ * chain (out32, prev_length 8..15): (len << 16) | distance, 0 when no match of >= 3 bytes, bit 31
+ * when the head candidate is a window-base position at distance exactly MAX_DIST.  dev_prev is
+ * len u32 of scratch (the hash-chain predecessor + 1).  Synchronous on the context's stream. */
+int hdrf_gzip_match_pass(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t len, uint32_t *dev_prev,
+                         uint32_t *dev_out128, uint32_t *dev_out32);
 int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4);
 int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id);
 /* Restore a DataNode from its persisted state (the Redis keys + chunkDir files), on a fresh or

@@ -139,6 +139,7 @@ typedef struct {
     const uint8_t *src;
     int64_t n, base, strstart, block_start, match_start, prev_match;
     uint32_t lookahead, match_length, prev_length, match_available;
+    int64_t *trace, ntrace, tcap;   /* optional longest_match call log (hdrf_oracle_gzip_trace) */
     uint16_t head[WSIZE], prev[WSIZE];
     uint16_t dbuf[LITBUF];
     uint8_t lbuf[LITBUF];
@@ -434,6 +435,10 @@ static void deflate_slow(gz_state *s)
         s->match_length = 2;
         if (hash_head != 0 && s->prev_length < LAZY && s->strstart - s->base - hash_head <= MAX_DIST) {
             s->match_length = longest_match(s, hash_head);
+            if (s->trace && s->ntrace < s->tcap) {
+                int64_t *t = s->trace + 4 * s->ntrace++;
+                t[0] = s->strstart; t[1] = s->prev_length; t[2] = s->match_length; t[3] = s->match_start;
+            }
             if (s->match_length == 3 && s->strstart - s->match_start > TOO_FAR) s->match_length = 2;
         }
         if (s->prev_length >= 3 && s->match_length <= s->prev_length) {
@@ -475,7 +480,24 @@ uint32_t hdrf_oracle_crc32(const uint8_t *p, int64_t n)
     return c ^ 0xffffffffu;
 }
 
+static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap, int64_t *ntrace);
+
 int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst)
+{
+    return gzip_run(src, n, dst, NULL, 0, NULL);
+}
+
+/* The same compression, logging every longest_match call as (strstart, prev_length, returned
+ * length, match_start) into trace[4*k..] (at most tcap calls; *ntrace = calls logged).  Checker
+ * for the GPU match pass (hdrf_gzip_match_pass): the answer a call returns is a function of the
+ * position and of prev_length only. */
+int64_t hdrf_oracle_gzip_trace(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap,
+                               int64_t *ntrace)
+{
+    return gzip_run(src, n, dst, trace, tcap, ntrace);
+}
+
+static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap, int64_t *ntrace)
 {
     init_tables();
     gz_state *s = (gz_state *)calloc(1, sizeof(gz_state));
@@ -484,6 +506,8 @@ int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst)
     memcpy(dst, hdr, 10);
     s->src = src;
     s->n = n;
+    s->trace = trace;
+    s->tcap = tcap;
     s->match_length = s->prev_length = 2;
     s->w.out = dst;
     s->w.pos = 10;
@@ -496,6 +520,7 @@ int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst)
     int64_t p = s->w.pos;
     for (int k = 0; k < 4; k++) dst[p++] = (uint8_t)(crc >> (8 * k));
     for (int k = 0; k < 4; k++) dst[p++] = (uint8_t)(isize >> (8 * k));
+    if (ntrace) *ntrace = s->ntrace;
     free(s);
     return p;
 }

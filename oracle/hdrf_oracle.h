@@ -89,6 +89,9 @@ int64_t hdrf_oracle_snappy_decompress(const uint8_t *src, int64_t n, uint8_t *ds
  * zlib 1.2.11.  The file is one gzip member (header OS byte 3, CRC-32 + ISIZE trailer). */
 int64_t hdrf_oracle_gzip_bound(int64_t n);
 int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst);
+/* the same, logging every longest_match call as (strstart, prev_length, length, match_start) */
+int64_t hdrf_oracle_gzip_trace(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap,
+                               int64_t *ntrace);
 uint32_t hdrf_oracle_crc32(const uint8_t *p, int64_t n);
 /* codec 0 (SnappyCodec) or 4 (Lz4Codec) stream file / its decoding */
 int64_t hdrf_oracle_hadoop_stream_bound(int codec, int64_t n, int64_t nwrites);

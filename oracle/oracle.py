@@ -93,6 +93,9 @@ def lib():
         L.hdrf_oracle_gzip_bound.restype = ctypes.c_int64
         L.hdrf_oracle_gzip_compress.argtypes = [_u8p, ctypes.c_int64, _u8p]
         L.hdrf_oracle_gzip_compress.restype = ctypes.c_int64
+        L.hdrf_oracle_gzip_trace.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_void_p, ctypes.c_int64,
+                                             ctypes.c_void_p]
+        L.hdrf_oracle_gzip_trace.restype = ctypes.c_int64
         L.hdrf_oracle_crc32.argtypes = [_u8p, ctypes.c_int64]
         L.hdrf_oracle_crc32.restype = ctypes.c_uint32
         _lib = L
@@ -333,6 +336,21 @@ def gzip_stream(data):
     if n < 0:
         raise MemoryError("gzip oracle state")
     return out[:n].tobytes()
+
+
+def gzip_trace(data):
+    """The longest_match calls of gzip_stream(data) as an int64 array of rows (strstart,
+    prev_length, returned length, match_start): the checker of the GPU match pass."""
+    a = _as_u8(data)
+    out = np.zeros(lib().hdrf_oracle_gzip_bound(a.size), np.uint8)
+    cap = max(a.size, 1)
+    tr = np.zeros((cap, 4), np.int64)
+    nt = ctypes.c_int64(0)
+    n = lib().hdrf_oracle_gzip_trace(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), tr.ctypes.data,
+                                     cap, ctypes.byref(nt))
+    if n < 0:
+        raise MemoryError("gzip oracle state")
+    return out[:n].tobytes(), tr[:nt.value]
 
 
 def hadoop_stream_decode(codec, data, cap):

@@ -57,3 +57,99 @@ def test_gzip_member_framing():
     assert c[:10] == bytes([0x1F, 0x8B, 8, 0, 0, 0, 0, 0, 0, 3])    # zlib's gzip header (OS_CODE 3)
     assert int.from_bytes(c[-8:-4], "little") == zlib.crc32(d)
     assert int.from_bytes(c[-4:], "little") == len(d)
+
+
+# ---- stage 1 of the GPU compressor 5: per-position longest_match answers ----
+MAX_DIST = 32768 - 262
+
+
+def _prev_py(a):
+    """1 + nearest earlier inserted position with the same 15-bit hash (position 0 is zlib's NIL)."""
+    n = a.size
+    h = np.zeros(max(n - 2, 0), np.int64)
+    if n >= 3:
+        h = ((a[:-2].astype(np.int64) << 10) ^ (a[1:-1].astype(np.int64) << 5) ^ a[2:]) & 0x7FFF
+    prev = np.zeros(n, np.int64)
+    last = {}
+    for p in range(h.size):
+        prev[p] = last.get(h[p], 0)
+        if p >= 1:
+            last[h[p]] = p + 1
+    return prev
+
+
+def _match_py(a, prev, p, chain):
+    """The rule gz_match_kernel computes: (len, dist) of the first candidate reaching nice, else the
+    earliest longest, over `chain` chain candidates (head <= MAX_DIST, the rest < MAX_DIST)."""
+    n = a.size
+    if p >= n - 2 or prev[p] == 0 or p - (prev[p] - 1) > MAX_DIST:
+        return 0, 0
+    maxlen, nice = min(n - p, 258), min(n - p, 128)
+    best, bq, q = 2, 0, prev[p] - 1
+    for _ in range(chain):
+        eq = a[q:q + maxlen] == a[p:p + maxlen]
+        ln = maxlen if eq.all() else int(np.argmin(eq))
+        if ln > best:
+            best, bq = ln, q
+            if ln >= nice:
+                break
+        nx = prev[q]
+        if nx == 0 or p - (nx - 1) >= MAX_DIST:
+            break
+        q = nx - 1
+    return (best, p - bq) if best >= 3 else (0, 0)
+
+
+def _check_trace(tr, answer):
+    """Every longest_match call the oracle made is answered by the per-position table."""
+    for s, L, ret, ms in tr:
+        ln, dist = answer(int(s), 128 if L < 8 else 32)
+        if ln > L:
+            assert (ret, s - ms) == (ln, dist), (s, L, ret, ms, ln, dist)
+        else:
+            assert ret <= L, (s, L, ret, ln)
+
+
+@pytest.mark.parametrize("kind", ["text", "lowent", "periodic", "zeros", "binary"])
+def test_match_rule_explains_every_longest_match_call(kind):
+    """CPU check of the stage-1 derivation: the position-only rule reproduces all of the
+    oracle's (zlib-pinned) longest_match answers, across a window slide (n > 65,274)."""
+    from oracle.oracle import gzip_trace
+    a = make_block(kind, 5, 90_000)
+    f, tr = gzip_trace(a)
+    assert f == gzip_stream(a)
+    assert len(tr) > 0
+    prev = _prev_py(a)
+    sel = tr[np.unique(np.concatenate([np.arange(0, len(tr), max(1, len(tr) // 1500)),
+                                       np.nonzero(np.abs(tr[:, 0] - 65_274) < 300)[0]]))]
+    _check_trace(sel, lambda p, c: _match_py(a, prev, p, c))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [("text", 300_000), ("lowent", 200_000), ("random", 150_000),
+                                    ("periodic", 140_000), ("zeros", 100_000), ("binary", 250_000),
+                                    ("sparse", 70_000), ("text", 3), ("text", 2), ("lowent", 4097)])
+def test_gpu_match_pass_matches_oracle_calls(kind, n):
+    """hdrf_gzip_match_pass answers every longest_match call of the zlib-pinned oracle exactly
+    (all calls checked), and equals the position rule on a sample of all positions."""
+    from hdrf_amd.lib import Context
+    from oracle.oracle import gzip_trace
+    a = make_block(kind, 9, n)
+    _, tr = gzip_trace(a)
+    ctx = Context(max_block_bytes=16 << 20, max_batch_blocks=8, index_log2=20, arena_slots=64)
+    dev = ctx.dev_alloc(n + 64)
+    ctx.h2d(dev, a)
+    m128, m32 = ctx.gzip_match_pass(dev, n)
+    ctx.dev_free(dev)
+    ctx.close()
+
+    def answer(p, chain):
+        v = int((m128 if chain == 128 else m32)[p])
+        assert not (v >> 31), "window-base candidate at MAX_DIST (stage 2 re-checks it)"
+        return (v >> 16) & 0x7FFF, v & 0xFFFF
+    _check_trace(tr, answer)
+    prev = _prev_py(a)
+    for p in np.linspace(0, max(n - 1, 0), num=min(n, 400)).astype(np.int64):
+        for chain in (128, 32):
+            v = int((m128 if chain == 128 else m32)[p]) & 0x7FFFFFFF
+            assert ((v >> 16), v & 0xFFFF) == _match_py(a, prev, int(p), chain), (p, chain)
