@@ -970,6 +970,20 @@ extern "C" int hdrf_gzip_match_pass(hdrf_ctx *ctx, const uint8_t *dev_data, uint
     return 0;
 }
 
+// Compressor 5 stage 2 (gzip.hip): the lazy parse over stage 1's answers.
+extern "C" int hdrf_gzip_parse(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t len, const uint32_t *dev_m128,
+                               const uint32_t *dev_m32, uint32_t *dev_syms, int64_t *dev_blks, int64_t *dev_cnt)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    if (!dev_syms || !dev_blks || !dev_cnt || (len && (!dev_data || !dev_m128 || !dev_m32)))
+        return set_err(ctx, HDRF_E_INVAL, "null buffer");
+    if (len >= (1ull << 31)) return set_err(ctx, HDRF_E_INVAL, "gzip parse: len must be < 2^31");
+    if (int rc = drain(ctx)) return rc;
+    HIPCK(launch_gzip_parse(dev_data, (int64_t)len, dev_m128, dev_m32, dev_syms, dev_blks, dev_cnt, ctx->st));
+    HIPCK(hipStreamSynchronize(ctx->st));
+    return 0;
+}
+
 // Make container `id` readable for reconstruction from its chunkDir file (raw, or a closed
 // container's Lz4Codec file): a DataNode that restarted, or whose arena slot was reused.
 extern "C" int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4)

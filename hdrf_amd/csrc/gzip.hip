@@ -115,6 +115,79 @@ __global__ void __launch_bounds__(256) gz_match_kernel(const uint8_t *__restrict
     out32[p] = r32;
 }
 
+// ---- stage 2: zlib's lazy parse (deflate_slow) over the stage-1 answers, one lane per stream.
+// The window base advances by WSIZE exactly when zlib's fill_window slides (strstart - base >=
+// WSIZE + MAX_DIST once the lookahead is under MIN_LOOKAHEAD); it decides the window-base NIL
+// corner flagged by stage 1 and the stored-block eligibility (block_start >= base) of stage 3.
+// syms: (dist << 8) | lc per symbol; blks: per flushed block (symbol end, block_start, strstart,
+// base, last); cnt = {symbols, blocks}.
+__global__ void gz_parse_kernel(const uint8_t *__restrict__ src, int64_t n, const uint32_t *__restrict__ m128,
+                                const uint32_t *__restrict__ m32, uint32_t *__restrict__ syms, int64_t *__restrict__ blks,
+                                int64_t *__restrict__ cnt)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    constexpr int64_t kLook = 262, kLitbuf = 16384;
+    int64_t strstart = 0, base = 0, end = 0, block_start = 0, match_start = 0, prev_match = 0;
+    int64_t nsym = 0, nblk = 0, blk_sym = 0;
+    uint32_t match_length = 2, prev_length = 2;
+    bool match_available = false;
+    auto flush = [&](int last) {
+        int64_t *b = blks + 5 * nblk++;
+        b[0] = nsym; b[1] = block_start; b[2] = strstart; b[3] = base; b[4] = last;
+        blk_sym = nsym;
+        block_start = strstart;
+    };
+    auto tally = [&](uint32_t dist, uint32_t lc) {
+        syms[nsym++] = (dist << 8) | lc;
+        return nsym - blk_sym == kLitbuf - 1;
+    };
+    for (;;) {
+        if (end - strstart < kLook) {
+            if (strstart - base >= kGzWsize + kGzMaxDist) base += kGzWsize;
+            end = base + 2 * kGzWsize < n ? base + 2 * kGzWsize : n;
+            if (end - strstart == 0) break;
+        }
+        prev_length = match_length;
+        prev_match = match_start;
+        match_length = 2;
+        if (end - strstart >= 3 && prev_length < 16) {
+            const uint32_t v = (prev_length >= 8 ? m32 : m128)[strstart];
+            const int64_t dist = v & 0xffff;
+            const uint32_t len = (v >> 16) & 0x7fff;
+            const bool nil = (v >> 31) && strstart - dist == base;
+            if (v && !nil && len > prev_length) {
+                match_length = len;
+                match_start = strstart - dist;
+                if (len == 3 && dist > 4096) match_length = 2;
+            }
+        }
+        if (prev_length >= 3 && match_length <= prev_length) {
+            const bool bf = tally((uint32_t)(strstart - 1 - prev_match), prev_length - 3);
+            strstart += prev_length - 1;
+            match_available = false;
+            match_length = 2;
+            if (bf) flush(0);
+        } else if (match_available) {
+            if (tally(0, src[strstart - 1])) flush(0);
+            strstart++;
+        } else {
+            match_available = true;
+            strstart++;
+        }
+    }
+    if (match_available) tally(0, src[strstart - 1]);
+    flush(1);
+    cnt[0] = nsym;
+    cnt[1] = nblk;
+}
+
+hipError_t launch_gzip_parse(const uint8_t *src, int64_t n, const uint32_t *m128, const uint32_t *m32, uint32_t *syms,
+                             int64_t *blks, int64_t *cnt, hipStream_t st)
+{
+    hipLaunchKernelGGL(gz_parse_kernel, dim3(1), dim3(64), 0, st, src, n, m128, m32, syms, blks, cnt);
+    return hipGetLastError();
+}
+
 size_t gzip_match_lds() { return sizeof(uint32_t) * kGzHash; }
 
 hipError_t launch_gzip_match(const uint8_t *src, int64_t n, uint32_t *prev, uint32_t *out128, uint32_t *out32,

@@ -118,6 +118,8 @@ uint64_t snappy_frag_stride();
 // chain-32 longest_match answers ((len << 16) | dist); prev = n u32 scratch
 hipError_t launch_gzip_match(const uint8_t *src, int64_t n, uint32_t *prev, uint32_t *out128, uint32_t *out32,
                              hipStream_t st);
+hipError_t launch_gzip_parse(const uint8_t *src, int64_t n, const uint32_t *m128, const uint32_t *m32, uint32_t *syms,
+                             int64_t *blks, int64_t *cnt, hipStream_t st);
 hipError_t launch_snappy_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
 // compression stage (lz4.hip): closed containers -> Lz4Codec files in the compressed arena
 uint64_t lz4_slot_bytes(uint32_t cmax);

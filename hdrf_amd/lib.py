@@ -29,7 +29,7 @@ EXPORTS = [
     "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
     "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_stream_block_host", "hdrf_lz4_file_decode",
-    "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_container_load",
+    "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
 ]
 
@@ -120,6 +120,7 @@ def load():
         "hdrf_host_free": (ctypes.c_int, [_vp, _vp]),
         "hdrf_lz4_file_decode": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_gzip_match_pass": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
+        "hdrf_gzip_parse": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
         "hdrf_stream_file_decode": (ctypes.c_int64, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_container_load": (ctypes.c_int, [_vp, ctypes.c_uint32, _u8p, ctypes.c_int64, ctypes.c_int32]),
         "hdrf_container_unload": (ctypes.c_int, [_vp, ctypes.c_uint32]),
@@ -462,16 +463,25 @@ class Context:
         self._ck(self.L.hdrf_memcpy_d2h(self._h, out.ctypes.data, dev, nbytes))
         return out
 
-    def gzip_match_pass(self, dev, nbytes):
+    def gzip_match_pass(self, dev, nbytes, parse=False):
         """Compressor 5 stage 1 (hdrf_gzip_match_pass): per-position chain-128 and chain-32
-        longest_match answers, (len << 16) | dist, for the nbytes device bytes at dev."""
-        if nbytes == 0:
+        longest_match answers, (len << 16) | dist, for the nbytes device bytes at dev.  With
+        parse=True also stage 2 (hdrf_gzip_parse): returns (m128, m32, symbols, blocks)."""
+        if nbytes == 0 and not parse:
             return np.zeros(0, np.uint32), np.zeros(0, np.uint32)
-        bufs = [self.dev_alloc(4 * nbytes + 64) for _ in range(3)]
+        nb = nbytes // 16383 + 2
+        bufs = [self.dev_alloc(4 * nbytes + 64) for _ in range(4)] + [self.dev_alloc(40 * nb + 64)]
         try:
             self._ck(self.L.hdrf_gzip_match_pass(self._h, dev, nbytes, bufs[0], bufs[1], bufs[2]))
-            return (self.d2h(bufs[1], 4 * nbytes).view(np.uint32).copy(),
-                    self.d2h(bufs[2], 4 * nbytes).view(np.uint32).copy())
+            m128 = self.d2h(bufs[1], 4 * nbytes).view(np.uint32).copy()
+            m32 = self.d2h(bufs[2], 4 * nbytes).view(np.uint32).copy()
+            if not parse:
+                return m128, m32
+            self._ck(self.L.hdrf_gzip_parse(self._h, dev, nbytes, bufs[1], bufs[2], bufs[3], bufs[4], bufs[0]))
+            ns, nblk = (int(x) for x in self.d2h(bufs[0], 16).view(np.int64))
+            syms = self.d2h(bufs[3], 4 * ns).view(np.uint32).copy()
+            blks = self.d2h(bufs[4], 40 * nblk).view(np.int64).reshape(nblk, 5).copy()
+            return m128, m32, syms, blks
         finally:
             for b in bufs:
                 self.dev_free(b)

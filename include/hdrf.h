@@ -137,6 +137,12 @@ int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const uint8_t *fil
  * len u32 of scratch (the hash-chain predecessor + 1).  Synchronous on the context's stream. */
 int hdrf_gzip_match_pass(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t len, uint32_t *dev_prev,
                          uint32_t *dev_out128, uint32_t *dev_out32);
+/* Stage 2 of the GPU compressor 5: zlib's lazy parse (deflate_slow) over stage 1's answers.
+ * dev_syms (len + 1 u32) receives (dist << 8) | lc per symbol (dist 0: literal lc; else lc =
+ * length - 3); dev_blks (5 * (len / 16383 + 2) int64) one row per deflate block (symbol end,
+ * block_start, strstart, window base, last); dev_cnt (2 int64) = {symbols, blocks}. */
+int hdrf_gzip_parse(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t len, const uint32_t *dev_m128,
+                    const uint32_t *dev_m32, uint32_t *dev_syms, int64_t *dev_blks, int64_t *dev_cnt);
 int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4);
 int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id);
 /* Restore a DataNode from its persisted state (the Redis keys + chunkDir files), on a fresh or

@@ -140,6 +140,8 @@ typedef struct {
     int64_t n, base, strstart, block_start, match_start, prev_match;
     uint32_t lookahead, match_length, prev_length, match_available;
     int64_t *trace, ntrace, tcap;   /* optional longest_match call log (hdrf_oracle_gzip_trace) */
+    uint32_t *syms;                 /* optional symbol log: (dist << 8) | lc per tally */
+    int64_t *blks, nsyms, nblks;    /* optional block log: sym_end, block_start, strstart, base, last */
     uint16_t head[WSIZE], prev[WSIZE];
     uint16_t dbuf[LITBUF];
     uint8_t lbuf[LITBUF];
@@ -314,6 +316,10 @@ static void emit_symbols(gz_state *s, const uint16_t *lc_code, const uint16_t *l
 static void flush_block(gz_state *s, int last)
 {
     const int64_t stored_len = s->strstart - s->block_start;
+    if (s->blks) {
+        int64_t *b = s->blks + 5 * s->nblks++;
+        b[0] = s->nsyms; b[1] = s->block_start; b[2] = s->strstart; b[3] = s->base; b[4] = last;
+    }
     const int have_buf = s->block_start >= s->base;           /* zlib: block_start >= 0 (window-relative) */
     make_tree(s, &s->lt);
     make_tree(s, &s->dt);
@@ -358,6 +364,7 @@ static void flush_block(gz_state *s, int last)
 
 static int tally(gz_state *s, unsigned dist, unsigned lc)
 {
+    if (s->syms) s->syms[s->nsyms++] = (dist << 8) | lc;
     s->dbuf[s->last_lit] = (uint16_t)dist;
     s->lbuf[s->last_lit++] = (uint8_t)lc;
     if (dist == 0) s->lfc[lc]++;
@@ -480,11 +487,22 @@ uint32_t hdrf_oracle_crc32(const uint8_t *p, int64_t n)
     return c ^ 0xffffffffu;
 }
 
-static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap, int64_t *ntrace);
+static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap, int64_t *ntrace,
+                        uint32_t *syms, int64_t *nsyms, int64_t *blks, int64_t *nblks);
+
+/* The same compression, logging the lazy parse: syms (room for n + 1) receives (dist << 8) | lc
+ * of every tallied symbol (dist 0 = literal lc, else lc = length - 3), blks (room for
+ * 5 * (n / 16383 + 2)) one row per flushed block (symbol end, block_start, strstart, window base,
+ * last).  Checker for the GPU parse (gz_parse_kernel). */
+int64_t hdrf_oracle_gzip_symbols(const uint8_t *src, int64_t n, uint8_t *dst, uint32_t *syms, int64_t *nsyms,
+                                 int64_t *blks, int64_t *nblks)
+{
+    return gzip_run(src, n, dst, NULL, 0, NULL, syms, nsyms, blks, nblks);
+}
 
 int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst)
 {
-    return gzip_run(src, n, dst, NULL, 0, NULL);
+    return gzip_run(src, n, dst, NULL, 0, NULL, NULL, NULL, NULL, NULL);
 }
 
 /* The same compression, logging every longest_match call as (strstart, prev_length, returned
@@ -494,10 +512,11 @@ int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst)
 int64_t hdrf_oracle_gzip_trace(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap,
                                int64_t *ntrace)
 {
-    return gzip_run(src, n, dst, trace, tcap, ntrace);
+    return gzip_run(src, n, dst, trace, tcap, ntrace, NULL, NULL, NULL, NULL);
 }
 
-static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap, int64_t *ntrace)
+static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap, int64_t *ntrace,
+                        uint32_t *syms, int64_t *nsyms, int64_t *blks, int64_t *nblks)
 {
     init_tables();
     gz_state *s = (gz_state *)calloc(1, sizeof(gz_state));
@@ -507,6 +526,8 @@ static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *tr
     s->src = src;
     s->n = n;
     s->trace = trace;
+    s->syms = syms;
+    s->blks = blks;
     s->tcap = tcap;
     s->match_length = s->prev_length = 2;
     s->w.out = dst;
@@ -521,6 +542,8 @@ static int64_t gzip_run(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *tr
     for (int k = 0; k < 4; k++) dst[p++] = (uint8_t)(crc >> (8 * k));
     for (int k = 0; k < 4; k++) dst[p++] = (uint8_t)(isize >> (8 * k));
     if (ntrace) *ntrace = s->ntrace;
+    if (nsyms) *nsyms = s->nsyms;
+    if (nblks) *nblks = s->nblks;
     free(s);
     return p;
 }

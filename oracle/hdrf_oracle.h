@@ -92,6 +92,9 @@ int64_t hdrf_oracle_gzip_compress(const uint8_t *src, int64_t n, uint8_t *dst);
 /* the same, logging every longest_match call as (strstart, prev_length, length, match_start) */
 int64_t hdrf_oracle_gzip_trace(const uint8_t *src, int64_t n, uint8_t *dst, int64_t *trace, int64_t tcap,
                                int64_t *ntrace);
+/* the same, logging the parse: symbols ((dist << 8) | lc) and flushed blocks (5 int64 each) */
+int64_t hdrf_oracle_gzip_symbols(const uint8_t *src, int64_t n, uint8_t *dst, uint32_t *syms, int64_t *nsyms,
+                                 int64_t *blks, int64_t *nblks);
 uint32_t hdrf_oracle_crc32(const uint8_t *p, int64_t n);
 /* codec 0 (SnappyCodec) or 4 (Lz4Codec) stream file / its decoding */
 int64_t hdrf_oracle_hadoop_stream_bound(int codec, int64_t n, int64_t nwrites);

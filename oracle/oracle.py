@@ -96,6 +96,9 @@ def lib():
         L.hdrf_oracle_gzip_trace.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p]
         L.hdrf_oracle_gzip_trace.restype = ctypes.c_int64
+        L.hdrf_oracle_gzip_symbols.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p]
+        L.hdrf_oracle_gzip_symbols.restype = ctypes.c_int64
         L.hdrf_oracle_crc32.argtypes = [_u8p, ctypes.c_int64]
         L.hdrf_oracle_crc32.restype = ctypes.c_uint32
         _lib = L
@@ -351,6 +354,21 @@ def gzip_trace(data):
     if n < 0:
         raise MemoryError("gzip oracle state")
     return out[:n].tobytes(), tr[:nt.value]
+
+
+def gzip_symbols(data):
+    """The lazy parse of gzip_stream(data): (file, symbols u32 (dist << 8) | lc, blocks int64 rows
+    (symbol end, block_start, strstart, window base, last))."""
+    a = _as_u8(data)
+    out = np.zeros(lib().hdrf_oracle_gzip_bound(a.size), np.uint8)
+    syms = np.zeros(a.size + 1, np.uint32)
+    blks = np.zeros((a.size // 16383 + 2, 5), np.int64)
+    ns, nb = ctypes.c_int64(0), ctypes.c_int64(0)
+    n = lib().hdrf_oracle_gzip_symbols(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), syms.ctypes.data,
+                                       ctypes.byref(ns), blks.ctypes.data, ctypes.byref(nb))
+    if n < 0:
+        raise MemoryError("gzip oracle state")
+    return out[:n].tobytes(), syms[:ns.value], blks[:nb.value]
 
 
 def hadoop_stream_decode(codec, data, cap):

@@ -153,3 +153,27 @@ def test_gpu_match_pass_matches_oracle_calls(kind, n):
         for chain in (128, 32):
             v = int((m128 if chain == 128 else m32)[p]) & 0x7FFFFFFF
             assert ((v >> 16), v & 0xFFFF) == _match_py(a, prev, int(p), chain), (p, chain)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [("text", 300_000), ("lowent", 200_000), ("random", 150_000),
+                                    ("periodic", 140_000), ("zeros", 100_000), ("binary", 250_000),
+                                    ("sparse", 70_000), ("ff", 65_274), ("text", 65_537), ("text", 3),
+                                    ("text", 2), ("text", 0)])
+def test_gpu_parse_matches_oracle_symbols(kind, n):
+    """hdrf_gzip_parse (stage 2: deflate_slow's lazy parse over stage 1) tallies exactly the
+    oracle's symbols and flushes exactly its deflate blocks (symbol ranges, block_start, strstart,
+    window base), across window slides and the 16,383-symbol block cuts."""
+    from hdrf_amd.lib import Context
+    from oracle.oracle import gzip_symbols
+    a = make_block(kind, 11, n) if n else np.zeros(0, np.uint8)
+    _, syms, blks = gzip_symbols(a)
+    ctx = Context(max_block_bytes=16 << 20, max_batch_blocks=8, index_log2=20, arena_slots=64)
+    dev = ctx.dev_alloc(n + 64)
+    if n:
+        ctx.h2d(dev, a)
+    _, _, gs, gb = ctx.gzip_match_pass(dev, n, parse=True)
+    ctx.dev_free(dev)
+    ctx.close()
+    assert gs.size == syms.size and np.array_equal(gs, syms)
+    assert np.array_equal(gb, blks)
