@@ -776,15 +776,68 @@ static int64_t stream_max_input(int codec)
     return codec == 0 ? 262144 - (262144 / 6 + 32) : 262144 - (262144 / 255 + 16);
 }
 
+// Stream-mode compressor 5 (GzipCodec, zlib level 6; DN/BlockReceiver.java:858-873,887-894): the
+// file does not depend on the packet writes.  Stage 1 match pass, stage 2 lazy
+// parse, stage 3 per-deflate-block trees + bits, stage 4 offsets / placement / CRC-32 trailer.
+static int64_t stream_gzip(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *dev_data, uint64_t len, uint8_t *out,
+                           int64_t cap)
+{
+    if (len >= (1ull << 31)) return set_err(ctx, HDRF_E_INVAL, "gzip stream: len must be < 2^31");
+    if (int rc = drain(ctx)) return rc;
+    hipStream_t st = ctx->st;
+    const int64_t n = (int64_t)len, maxblk = n / 16383 + 2, slot = 16384 * 6 + 2048;
+    const int64_t bound = n + (n >> 3) + 1024;
+    const size_t sz[] = {(size_t)(4 * n + 64), (size_t)(4 * n + 64), (size_t)(4 * n + 64), (size_t)(4 * n + 68),
+                         (size_t)(40 * maxblk + 64), 64, gzip_tab_bytes(), gzip_block_state_bytes() * (size_t)maxblk,
+                         (size_t)(slot * maxblk), (size_t)(24 * maxblk + 64), (size_t)(8 * maxblk + 72),
+                         (size_t)(4 * ((n >> 16) + 2)), (size_t)(bound + 64)};
+    constexpr int kBufs = 13;
+    uint8_t *B[kBufs] = {};
+    auto release = [&] { for (auto p : B) if (p) (void)hipFree(p); };
+    for (int i = 0; i < kBufs; i++)
+        if (hipMalloc((void **)&B[i], sz[i]) != hipSuccess) { release(); return set_err(ctx, HDRF_E_HIP, "gzip scratch"); }
+    std::vector<uint8_t> tab(gzip_tab_bytes());
+    gzip_host_tab(tab.data());
+    int64_t cnt[2] = {0, 0}, flen = 0;
+    hipError_t e = hipMemcpyAsync(B[6], tab.data(), tab.size(), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemsetAsync(B[12], 0, sz[12], st);
+    if (e == hipSuccess) e = launch_gzip_match(dev_data, n, (uint32_t *)B[0], (uint32_t *)B[1], (uint32_t *)B[2], st);
+    if (e == hipSuccess)
+        e = launch_gzip_parse(dev_data, n, (const uint32_t *)B[1], (const uint32_t *)B[2], (uint32_t *)B[3],
+                              (int64_t *)B[4], (int64_t *)B[5], st);
+    if (e == hipSuccess) e = hipMemcpyAsync(cnt, B[5], 16, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && (cnt[1] < 1 || cnt[1] > maxblk)) { release(); return set_err(ctx, HDRF_E_DEVICE, "gzip parse block count"); }
+    if (e == hipSuccess)
+        e = launch_gzip_encode(dev_data, n, B[6], (const uint32_t *)B[3], (const int64_t *)B[4], (int)cnt[1], B[7], B[8],
+                               slot, (int64_t *)B[9], (int64_t *)B[10], (uint32_t *)B[11], B[12], (int64_t *)B[5], st);
+    if (e == hipSuccess) e = hipMemcpyAsync(&flen, B[5], 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { release(); return set_err(ctx, HDRF_E_HIP, std::string("gzip stream: ") + hipGetErrorString(e)); }
+    if (flen > bound) { release(); return set_err(ctx, HDRF_E_DEVICE, "gzip stream exceeded its bound"); }
+    if (!out || cap < flen) { release(); return set_err(ctx, HDRF_E_CAPACITY, "stream file needs " + std::to_string(flen) + " bytes"); }
+    e = hipMemcpy(out, B[12], (size_t)flen, hipMemcpyDeviceToHost);
+    release();
+    if (e != hipSuccess) return set_err(ctx, HDRF_E_HIP, "gzip D2H");
+    ctx->lengths[(uint32_t)block_id] = (int64_t)len;   // SET id -> BE32(len) (:1238-1256)
+    return flen;
+}
+
 extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data,
                                      uint64_t len, uint64_t readable, const uint64_t *writes, int32_t nwrites,
                                      uint8_t *out, int64_t cap)
 {
     if (!ctx) return HDRF_E_INVAL;
-    if (codec != 4 && codec != 0)
-        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec) and 4 (Lz4Codec) are implemented");
+    if (codec != 4 && codec != 0 && codec != 5)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec) are implemented");
     if (nwrites < 0 || (nwrites && !writes) || (len && !dev_data) || readable < len + kSlack)
         return set_err(ctx, HDRF_E_INVAL, "bad stream arguments (readable must be >= len + 64)");
+    if (codec == 5) {
+        uint64_t sum = 0;
+        for (int w = 0; w < nwrites; w++) sum += writes[w];
+        if (sum != len) return set_err(ctx, HDRF_E_INVAL, "write sizes do not add up to the block length");
+        return stream_gzip(ctx, block_id, dev_data, len, out, cap);
+    }
     const int64_t kMaxIn = stream_max_input(codec);     // BlockCompressorStream MAX_INPUT_SIZE
     std::vector<LzPiece> pieces;
     std::vector<LzOut> outs;
@@ -870,8 +923,8 @@ extern "C" int64_t hdrf_stream_block_host(hdrf_ctx *ctx, int32_t codec, uint64_t
                                           int64_t cap)
 {
     if (!ctx || (len && !data)) return HDRF_E_INVAL;
-    if (codec != 4 && codec != 0)
-        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec) and 4 (Lz4Codec) are implemented");
+    if (codec != 4 && codec != 0 && codec != 5)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec) are implemented");
     if (int rc = drain(ctx)) return rc;
     if (int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, len + kSlack)) return rc;
     if (len) HIPCK(hipMemcpy(ctx->d_stage, data, len, hipMemcpyHostToDevice));

@@ -188,6 +188,447 @@ hipError_t launch_gzip_parse(const uint8_t *src, int64_t n, const uint32_t *m128
     return hipGetLastError();
 }
 
+// ---- stage 3: one lane per deflate block builds zlib's trees (heap build_tree with the depth
+// tie-break, gen_bitlen's overflow repair, scan_tree/bl_tree), makes the stored/static/dynamic
+// choice of _tr_flush_block and writes the block's bits from bit 0 of its own scratch slot
+// (stored blocks only record their length: their bits depend on the byte phase).
+struct GzTab {
+    uint8_t len_code[256], dist_code[512];
+    int base_len[29], base_dist[30];
+    uint16_t slcode[288], sllen[288], sdcode[30], sdlen[30];
+};
+struct GzBlk {
+    uint16_t lfc[573], ldl[573], dfc[61], ddl[61], bfc[39], bdl[39];
+    int heap[573];
+    uint8_t depth[573];
+    uint16_t bl_count[16];
+    int heap_len, heap_max;
+    int64_t opt_len, static_len;
+};
+struct GzTree { uint16_t *fc, *dl; const uint16_t *slen; const uint8_t *extra; int extra_base, elems, max_length, max_code; };
+struct GzBits { uint8_t *out; int64_t pos; uint64_t bb; int nb; };
+
+__constant__ uint8_t kGzXL[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint8_t kGzXD[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+__constant__ uint8_t kGzXB[19] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 3, 7};
+__constant__ uint8_t kGzBlOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+__device__ __forceinline__ void gz_put(GzBits &w, unsigned v, int n)
+{
+    w.bb |= (uint64_t)v << w.nb;
+    w.nb += n;
+    while (w.nb >= 8) { w.out[w.pos++] = (uint8_t)w.bb; w.bb >>= 8; w.nb -= 8; }
+}
+
+__device__ unsigned gz_rev(unsigned c, int n)
+{
+    unsigned r = 0;
+    while (n-- > 0) { r = (r << 1) | (c & 1); c >>= 1; }
+    return r;
+}
+
+__device__ bool gz_smaller(const GzTree &t, const GzBlk &s, int a, int b)
+{
+    return t.fc[a] < t.fc[b] || (t.fc[a] == t.fc[b] && s.depth[a] <= s.depth[b]);
+}
+
+__device__ void gz_sift(GzBlk &s, const GzTree &t, int k)
+{
+    const int v = s.heap[k];
+    int j = k << 1;
+    while (j <= s.heap_len) {
+        if (j < s.heap_len && gz_smaller(t, s, s.heap[j + 1], s.heap[j])) j++;
+        if (gz_smaller(t, s, v, s.heap[j])) break;
+        s.heap[k] = s.heap[j];
+        k = j;
+        j <<= 1;
+    }
+    s.heap[k] = v;
+}
+
+__device__ void gz_bitlen(GzBlk &s, GzTree &t)
+{
+    int overflow = 0, h;
+    for (int b = 0; b <= 15; b++) s.bl_count[b] = 0;
+    t.dl[s.heap[s.heap_max]] = 0;
+    for (h = s.heap_max + 1; h < 573; h++) {
+        const int n = s.heap[h];
+        int bits = t.dl[t.dl[n]] + 1;
+        if (bits > t.max_length) { bits = t.max_length; overflow++; }
+        t.dl[n] = (uint16_t)bits;
+        if (n > t.max_code) continue;
+        s.bl_count[bits]++;
+        const int xb = n >= t.extra_base ? t.extra[n - t.extra_base] : 0;
+        const int64_t f = t.fc[n];
+        s.opt_len += f * (bits + xb);
+        if (t.slen) s.static_len += f * (t.slen[n] + xb);
+    }
+    if (overflow == 0) return;
+    do {
+        int b = t.max_length - 1;
+        while (s.bl_count[b] == 0) b--;
+        s.bl_count[b]--;
+        s.bl_count[b + 1] += 2;
+        s.bl_count[t.max_length]--;
+        overflow -= 2;
+    } while (overflow > 0);
+    for (int b = t.max_length; b != 0; b--) {
+        int n = s.bl_count[b];
+        while (n != 0) {
+            const int m = s.heap[--h];
+            if (m > t.max_code) continue;
+            if (t.dl[m] != b) {
+                s.opt_len += ((int64_t)b - t.dl[m]) * t.fc[m];
+                t.dl[m] = (uint16_t)b;
+            }
+            n--;
+        }
+    }
+}
+
+__device__ void gz_tree(GzBlk &s, GzTree &t)
+{
+    int max_code = -1, node;
+    s.heap_len = 0;
+    s.heap_max = 573;
+    for (int n = 0; n < t.elems; n++) {
+        if (t.fc[n] != 0) { s.heap[++s.heap_len] = max_code = n; s.depth[n] = 0; }
+        else t.dl[n] = 0;
+    }
+    while (s.heap_len < 2) {
+        node = s.heap[++s.heap_len] = max_code < 2 ? ++max_code : 0;
+        t.fc[node] = 1;
+        s.depth[node] = 0;
+        s.opt_len--;
+        if (t.slen) s.static_len -= t.slen[node];
+    }
+    t.max_code = max_code;
+    for (int n = s.heap_len / 2; n >= 1; n--) gz_sift(s, t, n);
+    node = t.elems;
+    do {
+        const int n = s.heap[1];
+        s.heap[1] = s.heap[s.heap_len--];
+        gz_sift(s, t, 1);
+        const int m = s.heap[1];
+        s.heap[--s.heap_max] = n;
+        s.heap[--s.heap_max] = m;
+        t.fc[node] = (uint16_t)(t.fc[n] + t.fc[m]);
+        s.depth[node] = (uint8_t)((s.depth[n] >= s.depth[m] ? s.depth[n] : s.depth[m]) + 1);
+        t.dl[n] = t.dl[m] = (uint16_t)node;
+        s.heap[1] = node++;
+        gz_sift(s, t, 1);
+    } while (s.heap_len >= 2);
+    s.heap[--s.heap_max] = s.heap[1];
+    gz_bitlen(s, t);
+    uint16_t next[16];
+    unsigned c = 0;
+    for (int b = 1; b <= 15; b++) { c = (c + s.bl_count[b - 1]) << 1; next[b] = (uint16_t)c; }
+    for (int n = 0; n <= max_code; n++)
+        if (t.dl[n]) t.fc[n] = (uint16_t)gz_rev(next[t.dl[n]]++, t.dl[n]);
+}
+
+__device__ void gz_rle(GzBlk &s, GzTree &t, int max_code, GzBits *w)
+{
+    int prevlen = -1, nextlen = t.dl[0], count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    if (!w) t.dl[max_code + 1] = 0xffff;
+    for (int n = 0; n <= max_code; n++) {
+        const int curlen = nextlen;
+        nextlen = t.dl[n + 1];
+        if (++count < max_count && curlen == nextlen) continue;
+        if (count < min_count) {
+            if (w) do gz_put(*w, s.bfc[curlen], s.bdl[curlen]); while (--count != 0);
+            else s.bfc[curlen] = (uint16_t)(s.bfc[curlen] + count);
+        } else if (curlen != 0) {
+            if (w) {
+                if (curlen != prevlen) { gz_put(*w, s.bfc[curlen], s.bdl[curlen]); count--; }
+                gz_put(*w, s.bfc[16], s.bdl[16]);
+                gz_put(*w, (unsigned)(count - 3), 2);
+            } else {
+                if (curlen != prevlen) s.bfc[curlen]++;
+                s.bfc[16]++;
+            }
+        } else if (count <= 10) {
+            if (w) { gz_put(*w, s.bfc[17], s.bdl[17]); gz_put(*w, (unsigned)(count - 3), 3); }
+            else s.bfc[17]++;
+        } else {
+            if (w) { gz_put(*w, s.bfc[18], s.bdl[18]); gz_put(*w, (unsigned)(count - 11), 7); }
+            else s.bfc[18]++;
+        }
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+__device__ __forceinline__ int gz_dcode(const GzTab &T, unsigned d) { return d < 256 ? T.dist_code[d] : T.dist_code[256 + (d >> 7)]; }
+
+__device__ void gz_emit(GzBits &w, const GzTab &T, const uint32_t *sy, int64_t ns, const uint16_t *lcode,
+                        const uint16_t *llen, const uint16_t *dcode, const uint16_t *dlen)
+{
+    for (int64_t i = 0; i < ns; i++) {
+        unsigned dist = sy[i] >> 8, lc = sy[i] & 0xff;
+        if (dist == 0) { gz_put(w, lcode[lc], llen[lc]); continue; }
+        int code = T.len_code[lc];
+        gz_put(w, lcode[code + 257], llen[code + 257]);
+        if (kGzXL[code]) gz_put(w, lc - (unsigned)T.base_len[code], kGzXL[code]);
+        dist--;
+        code = gz_dcode(T, dist);
+        gz_put(w, dcode[code], dlen[code]);
+        if (kGzXD[code]) gz_put(w, dist - (unsigned)T.base_dist[code], kGzXD[code]);
+    }
+    gz_put(w, lcode[256], llen[256]);
+}
+
+// info[b] = {kind (0 stored, 1 static, 2 dynamic), bits (non-stored), stored_len}
+__global__ void __launch_bounds__(64) gz_block_kernel(const GzTab *__restrict__ tab, const uint32_t *__restrict__ syms,
+                                                      const int64_t *__restrict__ blks, int nblk, GzBlk *__restrict__ st,
+                                                      uint8_t *__restrict__ scratch, int64_t slot, int64_t *__restrict__ info)
+{
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= nblk) return;
+    const GzTab &T = *tab;
+    GzBlk &s = st[b];
+    const int64_t *r = blks + 5 * b;
+    const int64_t s0 = b ? blks[5 * (b - 1)] : 0, s1 = r[0];
+    const int last = (int)r[4];
+    const int64_t stored_len = r[2] - r[1];
+    const bool have_buf = r[1] >= r[3];
+    for (int n = 0; n < 286; n++) s.lfc[n] = 0;
+    for (int n = 0; n < 30; n++) s.dfc[n] = 0;
+    for (int n = 0; n < 19; n++) s.bfc[n] = 0;
+    s.lfc[256] = 1;
+    s.opt_len = s.static_len = 0;
+    for (int64_t i = s0; i < s1; i++) {
+        const unsigned dist = syms[i] >> 8, lc = syms[i] & 0xff;
+        if (dist == 0) s.lfc[lc]++;
+        else { s.lfc[T.len_code[lc] + 257]++; s.dfc[gz_dcode(T, dist - 1)]++; }
+    }
+    GzTree lt{s.lfc, s.ldl, T.sllen, kGzXL, 257, 286, 15, 0};
+    GzTree dt{s.dfc, s.ddl, T.sdlen, kGzXD, 0, 30, 15, 0};
+    GzTree bt{s.bfc, s.bdl, nullptr, kGzXB, 0, 19, 7, 0};
+    gz_tree(s, lt);
+    gz_tree(s, dt);
+    gz_rle(s, lt, lt.max_code, nullptr);
+    gz_rle(s, dt, dt.max_code, nullptr);
+    gz_tree(s, bt);
+    int max_blindex;
+    for (max_blindex = 18; max_blindex >= 3; max_blindex--)
+        if (s.bdl[kGzBlOrder[max_blindex]] != 0) break;
+    s.opt_len += 3 * ((int64_t)max_blindex + 1) + 14;
+    int64_t opt_lenb = (s.opt_len + 10) >> 3;
+    const int64_t static_lenb = (s.static_len + 10) >> 3;
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    int64_t *inf = info + 3 * b;
+    inf[2] = stored_len;
+    if (stored_len + 4 <= opt_lenb && have_buf) { inf[0] = 0; inf[1] = 0; return; }
+    GzBits w{scratch + (int64_t)b * slot, 0, 0, 0};
+    if (static_lenb == opt_lenb) {
+        gz_put(w, 2u + (unsigned)last, 3);
+        gz_emit(w, T, syms + s0, s1 - s0, T.slcode, T.sllen, T.sdcode, T.sdlen);
+        inf[0] = 1;
+    } else {
+        gz_put(w, 4u + (unsigned)last, 3);
+        const int lcodes = lt.max_code + 1, dcodes = dt.max_code + 1, blcodes = max_blindex + 1;
+        gz_put(w, (unsigned)(lcodes - 257), 5);
+        gz_put(w, (unsigned)(dcodes - 1), 5);
+        gz_put(w, (unsigned)(blcodes - 4), 4);
+        for (int k = 0; k < blcodes; k++) gz_put(w, s.bdl[kGzBlOrder[k]], 3);
+        gz_rle(s, lt, lcodes - 1, &w);
+        gz_rle(s, dt, dcodes - 1, &w);
+        gz_emit(w, T, syms + s0, s1 - s0, s.lfc, s.ldl, s.dfc, s.ddl);
+        inf[0] = 2;
+    }
+    inf[1] = w.pos * 8 + w.nb;
+    if (w.nb) w.out[w.pos] = (uint8_t)w.bb;
+}
+
+// ---- stage 4: bit offsets (one lane: the stored blocks' padding depends on the byte phase), then
+// one workgroup per block ORs its bits into the file at its offset (32-bit atomics at the seams).
+__global__ void gz_offsets_kernel(const int64_t *__restrict__ info, int nblk, int64_t *__restrict__ off)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t bit = 80;                                              // the 10-byte gzip header
+    for (int b = 0; b < nblk; b++) {
+        off[b] = bit;
+        const int64_t *inf = info + 3 * b;
+        if (inf[0] == 0) bit = ((bit + 3 + 7) & ~7ll) + 32 + 8 * inf[2];
+        else bit += inf[1];
+    }
+    off[nblk] = (bit + 7) & ~7ll;                                  // last block: align_byte
+}
+
+__device__ __forceinline__ void gz_or_byte(uint8_t *out, int64_t byte, uint32_t v)
+{
+    if (!v) return;
+    uint32_t *w = (uint32_t *)(out + (byte & ~3ll));
+    atomicOr(w, v << (8 * (byte & 3)));
+}
+
+__global__ void __launch_bounds__(256) gz_place_kernel(const uint8_t *__restrict__ src, const int64_t *__restrict__ blks,
+                                                       const int64_t *__restrict__ info, const int64_t *__restrict__ off,
+                                                       const uint8_t *__restrict__ scratch, int64_t slot,
+                                                       uint8_t *__restrict__ out)
+{
+    const int b = blockIdx.x;
+    const int64_t *inf = info + 3 * b;
+    const int64_t bit0 = off[b];
+    if (inf[0] == 0) {
+        const int last = (int)blks[5 * b + 4];
+        const int64_t start = blks[5 * b + 1], len = inf[2];
+        if (threadIdx.x == 0) {
+            gz_or_byte(out, bit0 >> 3, (uint32_t)last << (bit0 & 7));   // 3 header bits (type 0)
+            const int64_t pos = (bit0 + 3 + 7) >> 3;
+            const unsigned L = (unsigned)len & 0xffff;
+            gz_or_byte(out, pos, L & 0xff);
+            gz_or_byte(out, pos + 1, L >> 8);
+            gz_or_byte(out, pos + 2, (~L) & 0xff);
+            gz_or_byte(out, pos + 3, (~L >> 8) & 0xff);
+        }
+        const int64_t pos = ((bit0 + 3 + 7) >> 3) + 4;
+        for (int64_t i = threadIdx.x; i < len; i += 256) gz_or_byte(out, pos + i, src[start + i]);
+        return;
+    }
+    const int64_t nbits = inf[1];
+    const int64_t nbytes = (nbits + 7) >> 3;
+    const int sh = (int)(bit0 & 7);
+    const int64_t byte0 = bit0 >> 3;
+    const uint8_t *in = scratch + (int64_t)b * slot;
+    for (int64_t i = threadIdx.x; i < nbytes; i += 256) {
+        uint32_t v = in[i];
+        if (8 * (i + 1) > nbits) v &= (1u << (nbits - 8 * i)) - 1u;  // bits past the block end
+        v <<= sh;
+        gz_or_byte(out, byte0 + i, v & 0xff);
+        gz_or_byte(out, byte0 + i + 1, v >> 8);
+    }
+}
+
+// CRC-32 (gzip trailer): per-64 KiB piece in parallel, then combined in order with zlib's
+// crc32_combine (GF(2) matrix powers of the zero-byte operator) by one lane.
+__device__ uint32_t gz_crc_table(int i)
+{
+    uint32_t c = (uint32_t)i;
+    for (int k = 0; k < 8; k++) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    return c;
+}
+
+__global__ void __launch_bounds__(256) gz_crc_piece_kernel(const uint8_t *__restrict__ src, int64_t n,
+                                                           uint32_t *__restrict__ pcrc)
+{
+    __shared__ uint32_t tab[256];
+    tab[threadIdx.x] = gz_crc_table(threadIdx.x);
+    __syncthreads();
+    const int64_t pc = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t a = pc << 16, e = a + 65536 < n ? a + 65536 : n;
+    if (a >= n) return;
+    uint32_t c = 0xffffffffu;
+    for (int64_t i = a; i < e; i++) c = tab[(c ^ src[i]) & 0xff] ^ (c >> 8);
+    pcrc[pc] = c ^ 0xffffffffu;
+}
+
+__device__ uint32_t gz_mtimes(const uint32_t *m, uint32_t v)
+{
+    uint32_t s = 0;
+    for (int i = 0; v; i++, v >>= 1) if (v & 1) s ^= m[i];
+    return s;
+}
+
+__device__ void gz_msquare(uint32_t *sq, const uint32_t *m)
+{
+    for (int i = 0; i < 32; i++) sq[i] = gz_mtimes(m, m[i]);
+}
+
+__device__ uint32_t gz_crc_combine(uint32_t c1, uint32_t c2, int64_t len2)
+{
+    uint32_t even[32], odd[32];
+    if (len2 <= 0) return c1;
+    odd[0] = 0xedb88320u;
+    uint32_t row = 1;
+    for (int i = 1; i < 32; i++) { odd[i] = row; row <<= 1; }
+    gz_msquare(even, odd);
+    gz_msquare(odd, even);
+    do {
+        gz_msquare(even, odd);
+        if (len2 & 1) c1 = gz_mtimes(even, c1);
+        len2 >>= 1;
+        if (len2 == 0) break;
+        gz_msquare(odd, even);
+        if (len2 & 1) c1 = gz_mtimes(odd, c1);
+        len2 >>= 1;
+    } while (len2 != 0);
+    return c1 ^ c2;
+}
+
+__global__ void gz_trailer_kernel(const uint32_t *__restrict__ pcrc, int64_t n, const int64_t *__restrict__ off,
+                                  int nblk, uint8_t *__restrict__ out, int64_t *__restrict__ flen)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t c = 0;
+    for (int64_t a = 0, k = 0; a < n; a += 65536, k++) {
+        const int64_t l = n - a < 65536 ? n - a : 65536;
+        c = gz_crc_combine(c, pcrc[k], l);
+    }
+    const int64_t p = off[nblk] >> 3;
+    const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 3};
+    for (int k = 0; k < 10; k++) gz_or_byte(out, k, hdr[k]);
+    for (int k = 0; k < 4; k++) gz_or_byte(out, p + k, (c >> (8 * k)) & 0xff);
+    for (int k = 0; k < 4; k++) gz_or_byte(out, p + 4 + k, ((uint32_t)n >> (8 * k)) & 0xff);
+    *flen = p + 8;
+}
+
+size_t gzip_block_state_bytes() { return sizeof(GzBlk); }
+size_t gzip_tab_bytes() { return sizeof(GzTab); }
+
+void gzip_host_tab(void *dst)
+{
+    GzTab &T = *(GzTab *)dst;
+    static const uint8_t XL[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+    static const uint8_t XD[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+    int l = 0, code;
+    for (code = 0; code < 28; code++) {
+        T.base_len[code] = l;
+        for (int k = 0; k < (1 << XL[code]); k++) T.len_code[l++] = (uint8_t)code;
+    }
+    T.len_code[l - 1] = (uint8_t)code;
+    T.base_len[28] = 0;
+    int d = 0;
+    for (code = 0; code < 16; code++) {
+        T.base_dist[code] = d;
+        for (int k = 0; k < (1 << XD[code]); k++) T.dist_code[d++] = (uint8_t)code;
+    }
+    d >>= 7;
+    for (; code < 30; code++) {
+        T.base_dist[code] = d << 7;
+        for (int k = 0; k < (1 << (XD[code] - 7)); k++) T.dist_code[256 + d++] = (uint8_t)code;
+    }
+    uint16_t cnt[16] = {0}, next[16];
+    for (int n = 0; n < 288; n++) {
+        T.sllen[n] = n <= 143 ? 8 : n <= 255 ? 9 : n <= 279 ? 7 : 8;
+        cnt[T.sllen[n]]++;
+    }
+    auto rev = [](unsigned c, int n) { unsigned r = 0; while (n-- > 0) { r = (r << 1) | (c & 1); c >>= 1; } return r; };
+    unsigned c = 0;
+    for (int b = 1; b <= 15; b++) { c = (c + cnt[b - 1]) << 1; next[b] = (uint16_t)c; }
+    for (int n = 0; n < 288; n++) T.slcode[n] = (uint16_t)rev(next[T.sllen[n]]++, T.sllen[n]);
+    for (int n = 0; n < 30; n++) { T.sdlen[n] = 5; T.sdcode[n] = (uint16_t)rev((unsigned)n, 5); }
+}
+
+hipError_t launch_gzip_encode(const uint8_t *src, int64_t n, const void *tab, const uint32_t *syms, const int64_t *blks,
+                              int nblk, void *state, uint8_t *scratch, int64_t slot, int64_t *info, int64_t *off,
+                              uint32_t *pcrc, uint8_t *out, int64_t *flen, hipStream_t st)
+{
+    hipLaunchKernelGGL(gz_block_kernel, dim3((nblk + 63) / 64), dim3(64), 0, st, (const GzTab *)tab, syms, blks, nblk,
+                       (GzBlk *)state, scratch, slot, info);
+    hipLaunchKernelGGL(gz_offsets_kernel, dim3(1), dim3(64), 0, st, info, nblk, off);
+    hipLaunchKernelGGL(gz_place_kernel, dim3(nblk), dim3(256), 0, st, src, blks, info, off, scratch, slot, out);
+    const int64_t pieces = (n + 65535) >> 16;
+    if (pieces) hipLaunchKernelGGL(gz_crc_piece_kernel, dim3((unsigned)((pieces + 255) / 256)), dim3(256), 0, st, src, n, pcrc);
+    hipLaunchKernelGGL(gz_trailer_kernel, dim3(1), dim3(64), 0, st, pcrc, n, off, nblk, out, flen);
+    return hipGetLastError();
+}
+
 size_t gzip_match_lds() { return sizeof(uint32_t) * kGzHash; }
 
 hipError_t launch_gzip_match(const uint8_t *src, int64_t n, uint32_t *prev, uint32_t *out128, uint32_t *out32,

@@ -120,6 +120,12 @@ hipError_t launch_gzip_match(const uint8_t *src, int64_t n, uint32_t *prev, uint
                              hipStream_t st);
 hipError_t launch_gzip_parse(const uint8_t *src, int64_t n, const uint32_t *m128, const uint32_t *m32, uint32_t *syms,
                              int64_t *blks, int64_t *cnt, hipStream_t st);
+size_t gzip_block_state_bytes();
+size_t gzip_tab_bytes();
+void gzip_host_tab(void *dst);
+hipError_t launch_gzip_encode(const uint8_t *src, int64_t n, const void *tab, const uint32_t *syms, const int64_t *blks,
+                              int nblk, void *state, uint8_t *scratch, int64_t slot, int64_t *info, int64_t *off,
+                              uint32_t *pcrc, uint8_t *out, int64_t *flen, hipStream_t st);
 hipError_t launch_snappy_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
 // compression stage (lz4.hip): closed containers -> Lz4Codec files in the compressed arena
 uint64_t lz4_slot_bytes(uint32_t cmax);

@@ -386,7 +386,7 @@ def test_stream_mode_lz4_file_matches_oracle(case):
     assert f == hadoop_lz4_stream(d, writes)
     assert ctx.block_length(77) == n
     with pytest.raises(HdrfError):
-        ctx.stream_block(5, 78, dev, n, n + 4096, writes)          # gzip: not built
+        ctx.stream_block(3, 78, dev, n, n + 4096, writes)          # LZOP: not built
     ctx.dev_free(dev)
     ctx.close()
 
