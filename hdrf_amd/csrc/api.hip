@@ -790,8 +790,8 @@ static int64_t stream_gzip(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *dev_
     const size_t sz[] = {(size_t)(4 * n + 64), (size_t)(4 * n + 64), (size_t)(4 * n + 64), (size_t)(4 * n + 68),
                          (size_t)(40 * maxblk + 64), 64, gzip_tab_bytes(), gzip_block_state_bytes() * (size_t)maxblk,
                          (size_t)(slot * maxblk), (size_t)(24 * maxblk + 64), (size_t)(8 * maxblk + 72),
-                         (size_t)(4 * ((n >> 16) + 2)), (size_t)(bound + 64)};
-    constexpr int kBufs = 13;
+                         (size_t)(4 * ((n >> 16) + 2)), (size_t)(bound + 64), gzip_parse_scratch(n)};
+    constexpr int kBufs = 14;
     uint8_t *B[kBufs] = {};
     auto release = [&] { for (auto p : B) if (p) (void)hipFree(p); };
     for (int i = 0; i < kBufs; i++)
@@ -804,7 +804,7 @@ static int64_t stream_gzip(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *dev_
     if (e == hipSuccess) e = launch_gzip_match(dev_data, n, (uint32_t *)B[0], (uint32_t *)B[1], (uint32_t *)B[2], st);
     if (e == hipSuccess)
         e = launch_gzip_parse(dev_data, n, (const uint32_t *)B[1], (const uint32_t *)B[2], (uint32_t *)B[3],
-                              (int64_t *)B[4], (int64_t *)B[5], st);
+                              (int64_t *)B[4], (int64_t *)B[5], B[13], st);
     if (e == hipSuccess) e = hipMemcpyAsync(cnt, B[5], 16, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     if (e == hipSuccess && (cnt[1] < 1 || cnt[1] > maxblk)) { release(); return set_err(ctx, HDRF_E_DEVICE, "gzip parse block count"); }
@@ -1032,8 +1032,12 @@ extern "C" int hdrf_gzip_parse(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t 
         return set_err(ctx, HDRF_E_INVAL, "null buffer");
     if (len >= (1ull << 31)) return set_err(ctx, HDRF_E_INVAL, "gzip parse: len must be < 2^31");
     if (int rc = drain(ctx)) return rc;
-    HIPCK(launch_gzip_parse(dev_data, (int64_t)len, dev_m128, dev_m32, dev_syms, dev_blks, dev_cnt, ctx->st));
-    HIPCK(hipStreamSynchronize(ctx->st));
+    void *scr = nullptr;
+    HIPCK(hipMalloc(&scr, gzip_parse_scratch((int64_t)len)));
+    hipError_t e = launch_gzip_parse(dev_data, (int64_t)len, dev_m128, dev_m32, dev_syms, dev_blks, dev_cnt, scr, ctx->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->st);
+    (void)hipFree(scr);
+    if (e != hipSuccess) return set_err(ctx, HDRF_E_HIP, std::string("gzip parse: ") + hipGetErrorString(e));
     return 0;
 }
 

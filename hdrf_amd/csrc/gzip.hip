@@ -115,76 +115,219 @@ __global__ void __launch_bounds__(256) gz_match_kernel(const uint8_t *__restrict
     out32[p] = r32;
 }
 
-// ---- stage 2: zlib's lazy parse (deflate_slow) over the stage-1 answers, one lane per stream.
-// The window base advances by WSIZE exactly when zlib's fill_window slides (strstart - base >=
-// WSIZE + MAX_DIST once the lookahead is under MIN_LOOKAHEAD); it decides the window-base NIL
-// corner flagged by stage 1 and the stored-block eligibility (block_start >= base) of stage 3.
-// syms: (dist << 8) | lc per symbol; blks: per flushed block (symbol end, block_start, strstart,
-// base, last); cnt = {symbols, blocks}.
-__global__ void gz_parse_kernel(const uint8_t *__restrict__ src, int64_t n, const uint32_t *__restrict__ m128,
-                                const uint32_t *__restrict__ m32, uint32_t *__restrict__ syms, int64_t *__restrict__ blks,
-                                int64_t *__restrict__ cnt)
+// ---- stage 2: zlib's lazy parse (deflate_slow) over the stage-1 answers, made segment-parallel.
+// Everything a parse step reads besides its state is a function of the position: the window base
+// (zlib slides at the first visited s > k*WSIZE + MAX_DIST, or at s == that threshold when fewer
+// than 262 bytes remain — steps never jump 262 B), the "lookahead >= 3" test (n - s >= 3) and the
+// stage-1 answers.  The state at the top of a step is (s, match_length, match_start,
+// match_available).  So (a) one lane per 4096-position segment parses speculatively from a fresh
+// state, recording the state and its symbol count at every position it visits; (b) one lane
+// replays the true parse and, at the first position where its state equals the recorded one,
+// jumps to that segment's exit (paths that meet stay together); (c) the segments' symbols
+// (true-lane prefix + speculative rest) are concatenated, and the deflate blocks follow from
+// the symbol count (a cut every 16,383 in-loop symbols) and the symbols' end positions.
+constexpr int kGzSeg = 4096, kGzSegCap = kGzSeg + 2;
+
+struct GzPs { uint32_t ml, ms, avail; };                 // match_length, match_start, match_available
+
+__device__ __forceinline__ int64_t gz_base_at(int64_t s, int64_t n)
 {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    constexpr int64_t kLook = 262, kLitbuf = 16384;
-    int64_t strstart = 0, base = 0, end = 0, block_start = 0, match_start = 0, prev_match = 0;
-    int64_t nsym = 0, nblk = 0, blk_sym = 0;
-    uint32_t match_length = 2, prev_length = 2;
-    bool match_available = false;
-    auto flush = [&](int last) {
-        int64_t *b = blks + 5 * nblk++;
-        b[0] = nsym; b[1] = block_start; b[2] = strstart; b[3] = base; b[4] = last;
-        blk_sym = nsym;
-        block_start = strstart;
-    };
-    auto tally = [&](uint32_t dist, uint32_t lc) {
-        syms[nsym++] = (dist << 8) | lc;
-        return nsym - blk_sym == kLitbuf - 1;
-    };
+    int64_t k = 0;
     for (;;) {
-        if (end - strstart < kLook) {
-            if (strstart - base >= kGzWsize + kGzMaxDist) base += kGzWsize;
-            end = base + 2 * kGzWsize < n ? base + 2 * kGzWsize : n;
-            if (end - strstart == 0) break;
-        }
-        prev_length = match_length;
-        prev_match = match_start;
-        match_length = 2;
-        if (end - strstart >= 3 && prev_length < 16) {
-            const uint32_t v = (prev_length >= 8 ? m32 : m128)[strstart];
-            const int64_t dist = v & 0xffff;
-            const uint32_t len = (v >> 16) & 0x7fff;
-            const bool nil = (v >> 31) && strstart - dist == base;
-            if (v && !nil && len > prev_length) {
-                match_length = len;
-                match_start = strstart - dist;
-                if (len == 3 && dist > 4096) match_length = 2;
-            }
-        }
-        if (prev_length >= 3 && match_length <= prev_length) {
-            const bool bf = tally((uint32_t)(strstart - 1 - prev_match), prev_length - 3);
-            strstart += prev_length - 1;
-            match_available = false;
-            match_length = 2;
-            if (bf) flush(0);
-        } else if (match_available) {
-            if (tally(0, src[strstart - 1])) flush(0);
-            strstart++;
-        } else {
-            match_available = true;
-            strstart++;
+        const int64_t T = (k + 1) * kGzWsize + kGzMaxDist;
+        if (s > T || (s == T && n - s < 262)) k++;
+        else break;
+    }
+    return k * kGzWsize;
+}
+
+__device__ __forceinline__ uint32_t gz_enc(const GzPs &q, int64_t s)
+{
+    const uint32_t d = q.ml >= 3 ? (uint32_t)(s - (int64_t)q.ms) & 0xffffu : 0u;
+    return 0x80000000u | (q.avail << 30) | (q.ml << 16) | d;
+}
+
+// one step of deflate_slow at s (the top-of-loop fill already reflected in gz_base_at); emits
+// at most one symbol via out(sym, end); returns the next s
+template <class Out>
+__device__ __forceinline__ int64_t gz_step(const uint8_t *src, int64_t n, const uint32_t *m128, const uint32_t *m32,
+                                           int64_t s, GzPs &q, Out out)
+{
+    const uint32_t prev_length = q.ml, prev_match = q.ms;
+    uint32_t ml = 2;
+    if (n - s >= 3 && prev_length < 16) {
+        const uint32_t v = (prev_length >= 8 ? m32 : m128)[s];
+        const int64_t dist = v & 0xffff;
+        const uint32_t len = (v >> 16) & 0x7fff;
+        const bool nil = (v >> 31) && s - dist == gz_base_at(s, n);
+        if (v && !nil && len > prev_length) {
+            ml = len;
+            q.ms = (uint32_t)(s - dist);
+            if (len == 3 && dist > 4096) ml = 2;
         }
     }
-    if (match_available) tally(0, src[strstart - 1]);
-    flush(1);
-    cnt[0] = nsym;
-    cnt[1] = nblk;
+    if (prev_length >= 3 && ml <= prev_length) {
+        out(((uint32_t)(s - 1 - prev_match) << 8) | (prev_length - 3), (uint32_t)(s - 1 + prev_length));
+        q.avail = 0;
+        q.ml = 2;
+        return s + prev_length - 1;
+    }
+    q.ml = ml;
+    if (q.avail) out((uint32_t)src[s - 1], (uint32_t)s);
+    q.avail = 1;
+    return s + 1;
+}
+
+// (a) speculative lanes: st[s] / cn[s] = state and symbol count on arrival at s; ex[k] = exit
+__global__ void __launch_bounds__(64) gz_spec_kernel(const uint8_t *__restrict__ src, int64_t n,
+                                                     const uint32_t *__restrict__ m128, const uint32_t *__restrict__ m32,
+                                                     uint32_t *__restrict__ st, uint32_t *__restrict__ cn,
+                                                     uint32_t *__restrict__ ssym, uint32_t *__restrict__ send,
+                                                     uint32_t *__restrict__ ex, int nseg)
+{
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= nseg) return;
+    const int64_t p0 = (int64_t)k * kGzSeg, e = p0 + kGzSeg < n ? p0 + kGzSeg : n;
+    GzPs q{2, 0, 0};
+    uint32_t c = 0;
+    uint32_t *ys = ssym + (int64_t)k * kGzSegCap, *ye = send + (int64_t)k * kGzSegCap;
+    int64_t s = p0;
+    while (s < e) {
+        st[s] = gz_enc(q, s);
+        cn[s] = c;
+        s = gz_step(src, n, m128, m32, s, q, [&](uint32_t y, uint32_t end) { ys[c] = y; ye[c] = end; c++; });
+    }
+    uint32_t *x = ex + 4 * (int64_t)k;
+    x[0] = (uint32_t)s; x[1] = q.ml; x[2] = q.ms | (q.avail << 31); x[3] = c;
+}
+
+// (b) the true lane: fx* = its own symbols per segment, take[k] = {own count, first speculative
+// symbol used}; tail = {after-loop literal?, symbol, end, in-loop symbol count}
+__global__ void gz_fix_kernel(const uint8_t *__restrict__ src, int64_t n, const uint32_t *__restrict__ m128,
+                              const uint32_t *__restrict__ m32, const uint32_t *__restrict__ st,
+                              const uint32_t *__restrict__ cn, const uint32_t *__restrict__ ex,
+                              uint32_t *__restrict__ fsym, uint32_t *__restrict__ fend, uint32_t *__restrict__ take,
+                              uint32_t *__restrict__ tail, int nseg)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int k = 0; k < nseg; k++) { take[2 * k] = 0; take[2 * k + 1] = ex[4 * k + 3]; }
+    GzPs q{2, 0, 0};
+    int64_t s = 0;
+    uint32_t total = 0;
+    while (s < n) {
+        const int k = (int)(s / kGzSeg);
+        if (st[s] == gz_enc(q, s)) {                       // met the speculative path: jump to its exit
+            take[2 * k + 1] = cn[s];
+            const uint32_t *x = ex + 4 * (int64_t)k;
+            total += x[3] - cn[s];
+            s = x[0];
+            q.ml = x[1]; q.ms = x[2] & 0x7fffffffu; q.avail = x[2] >> 31;
+            continue;
+        }
+        uint32_t *fy = fsym + (int64_t)k * kGzSegCap, *fe = fend + (int64_t)k * kGzSegCap;
+        s = gz_step(src, n, m128, m32, s, q, [&](uint32_t y, uint32_t end) {
+            fy[take[2 * k]] = y; fe[take[2 * k]] = end; take[2 * k]++; total++;
+        });
+    }
+    tail[0] = q.avail;
+    tail[1] = n ? (uint32_t)src[n - 1] : 0u;
+    tail[2] = (uint32_t)n;
+    tail[3] = total;
+}
+
+// (c) segment offsets (one lane), then one workgroup per segment copies its symbols in order
+__global__ void gz_segoff_kernel(const uint32_t *__restrict__ ex, const uint32_t *__restrict__ take, int nseg,
+                                 uint32_t *__restrict__ off)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t o = 0;
+    for (int k = 0; k < nseg; k++) {
+        off[k] = o;
+        o += take[2 * k] + (ex[4 * k + 3] - take[2 * k + 1]);
+    }
+    off[nseg] = o;
+}
+
+__global__ void __launch_bounds__(256) gz_gather_kernel(const uint32_t *__restrict__ ssym, const uint32_t *__restrict__ send,
+                                                        const uint32_t *__restrict__ fsym, const uint32_t *__restrict__ fend,
+                                                        const uint32_t *__restrict__ ex, const uint32_t *__restrict__ take,
+                                                        const uint32_t *__restrict__ off, uint32_t *__restrict__ syms,
+                                                        uint32_t *__restrict__ symend)
+{
+    const int k = blockIdx.x;
+    const int64_t base = (int64_t)k * kGzSegCap;
+    const uint32_t nf = take[2 * k], from = take[2 * k + 1], to = ex[4 * k + 3], o = off[k];
+    for (uint32_t i = threadIdx.x; i < nf; i += 256) { syms[o + i] = fsym[base + i]; symend[o + i] = fend[base + i]; }
+    for (uint32_t i = from + threadIdx.x; i < to; i += 256) {
+        syms[o + nf + i - from] = ssym[base + i];
+        symend[o + nf + i - from] = send[base + i];
+    }
+}
+
+// blocks: a cut after every 16,383rd in-loop symbol, then the last block (strstart = n)
+__global__ void __launch_bounds__(256) gz_blocks_kernel(int64_t n, uint32_t *__restrict__ syms,
+                                                        const uint32_t *__restrict__ symend, const uint32_t *__restrict__ tail,
+                                                        int64_t *__restrict__ blks, int64_t *__restrict__ cnt)
+{
+    const uint32_t inloop = tail[3], total = inloop + tail[0];
+    const int64_t ncut = inloop / 16383;
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b == 0) {
+        if (tail[0]) syms[inloop] = tail[1];
+        cnt[0] = total;
+        cnt[1] = ncut + 1;
+    }
+    if (b > ncut) return;
+    int64_t *r = blks + 5 * b;
+    r[1] = b ? (int64_t)symend[b * 16383 - 1] : 0;
+    if (b < ncut) {
+        const int64_t j = (b + 1) * 16383 - 1;
+        const uint32_t y = syms[j], end = symend[j];
+        const int64_t cover = (y >> 8) ? (int64_t)(y & 0xff) + 3 : 1;
+        r[0] = j + 1; r[2] = end; r[3] = gz_base_at(end - cover + 1, n); r[4] = 0;
+    } else {
+        r[0] = total; r[2] = n; r[3] = gz_base_at(n, n); r[4] = 1;
+    }
+}
+
+size_t gzip_parse_scratch(int64_t n)
+{
+    const int64_t K = (n + kGzSeg - 1) / kGzSeg + 1;
+    return (size_t)(8 * n + 16 * K * kGzSegCap + 16 * K + 8 * K + 16 + 4 * (n + 2) + 4 * (K + 1) + 1024);
 }
 
 hipError_t launch_gzip_parse(const uint8_t *src, int64_t n, const uint32_t *m128, const uint32_t *m32, uint32_t *syms,
-                             int64_t *blks, int64_t *cnt, hipStream_t st)
+                             int64_t *blks, int64_t *cnt, void *scratch, hipStream_t st)
 {
-    hipLaunchKernelGGL(gz_parse_kernel, dim3(1), dim3(64), 0, st, src, n, m128, m32, syms, blks, cnt);
+    const int nseg = (int)((n + kGzSeg - 1) / kGzSeg);
+    const int64_t K = nseg + 1;
+    uint32_t *p = (uint32_t *)scratch;
+    uint32_t *stw = p; p += n;
+    uint32_t *cnw = p; p += n;
+    uint32_t *ssym = p; p += K * kGzSegCap;
+    uint32_t *send = p; p += K * kGzSegCap;
+    uint32_t *fsym = p; p += K * kGzSegCap;
+    uint32_t *fend = p; p += K * kGzSegCap;
+    uint32_t *ex = p; p += 4 * K;
+    uint32_t *take = p; p += 2 * K;
+    uint32_t *tail = p; p += 4;
+    uint32_t *symend = p; p += n + 2;
+    uint32_t *off = p;
+    if (n) (void)hipMemsetAsync(stw, 0, 4 * (size_t)n, st);
+    if (nseg) {
+        hipLaunchKernelGGL(gz_spec_kernel, dim3((nseg + 63) / 64), dim3(64), 0, st, src, n, m128, m32, stw, cnw, ssym,
+                           send, ex, nseg);
+    }
+    hipLaunchKernelGGL(gz_fix_kernel, dim3(1), dim3(64), 0, st, src, n, m128, m32, stw, cnw, ex, fsym, fend, take, tail,
+                       nseg);
+    if (nseg) {
+        hipLaunchKernelGGL(gz_segoff_kernel, dim3(1), dim3(64), 0, st, ex, take, nseg, off);
+        hipLaunchKernelGGL(gz_gather_kernel, dim3(nseg), dim3(256), 0, st, ssym, send, fsym, fend, ex, take, off, syms,
+                           symend);
+    }
+    const int64_t maxcut = n / 16383 + 1;
+    hipLaunchKernelGGL(gz_blocks_kernel, dim3((unsigned)((maxcut + 255) / 256)), dim3(256), 0, st, n, syms, symend, tail,
+                       blks, cnt);
     return hipGetLastError();
 }
 

@@ -118,8 +118,9 @@ uint64_t snappy_frag_stride();
 // chain-32 longest_match answers ((len << 16) | dist); prev = n u32 scratch
 hipError_t launch_gzip_match(const uint8_t *src, int64_t n, uint32_t *prev, uint32_t *out128, uint32_t *out32,
                              hipStream_t st);
+size_t gzip_parse_scratch(int64_t n);
 hipError_t launch_gzip_parse(const uint8_t *src, int64_t n, const uint32_t *m128, const uint32_t *m32, uint32_t *syms,
-                             int64_t *blks, int64_t *cnt, hipStream_t st);
+                             int64_t *blks, int64_t *cnt, void *scratch, hipStream_t st);
 size_t gzip_block_state_bytes();
 size_t gzip_tab_bytes();
 void gzip_host_tab(void *dst);
