@@ -339,6 +339,7 @@ struct GzTab {
     uint8_t len_code[256], dist_code[512];
     int base_len[29], base_dist[30];
     uint16_t slcode[288], sllen[288], sdcode[30], sdlen[30];
+    uint32_t crc64k[32];                               // CRC-32 shift by 64 KiB of zeros (GF(2) matrix)
 };
 struct GzBlk {
     uint16_t lfc[573], ldl[573], dfc[61], ddl[61], bfc[39], bdl[39];
@@ -704,14 +705,17 @@ __device__ uint32_t gz_crc_combine(uint32_t c1, uint32_t c2, int64_t len2)
     return c1 ^ c2;
 }
 
-__global__ void gz_trailer_kernel(const uint32_t *__restrict__ pcrc, int64_t n, const int64_t *__restrict__ off,
-                                  int nblk, uint8_t *__restrict__ out, int64_t *__restrict__ flen)
+__global__ void gz_trailer_kernel(const GzTab *__restrict__ tab, const uint32_t *__restrict__ pcrc, int64_t n,
+                                  const int64_t *__restrict__ off, int nblk, uint8_t *__restrict__ out,
+                                  int64_t *__restrict__ flen)
 {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    __shared__ uint32_t M[32];
+    for (int i = 0; i < 32; i++) M[i] = tab->crc64k[i];
     uint32_t c = 0;
     for (int64_t a = 0, k = 0; a < n; a += 65536, k++) {
         const int64_t l = n - a < 65536 ? n - a : 65536;
-        c = gz_crc_combine(c, pcrc[k], l);
+        c = l == 65536 ? gz_mtimes(M, c) ^ pcrc[k] : gz_crc_combine(c, pcrc[k], l);
     }
     const int64_t p = off[nblk] >> 3;
     const uint8_t hdr[10] = {0x1f, 0x8b, 8, 0, 0, 0, 0, 0, 0, 3};
@@ -756,6 +760,17 @@ void gzip_host_tab(void *dst)
     for (int b = 1; b <= 15; b++) { c = (c + cnt[b - 1]) << 1; next[b] = (uint16_t)c; }
     for (int n = 0; n < 288; n++) T.slcode[n] = (uint16_t)rev(next[T.sllen[n]]++, T.sllen[n]);
     for (int n = 0; n < 30; n++) { T.sdlen[n] = 5; T.sdcode[n] = (uint16_t)rev((unsigned)n, 5); }
+    // zlib crc32_combine's operator for 65,536 zero bytes: odd = one zero bit, squared 3 times
+    // gives one zero byte, then 16 more squarings give 2^16 bytes; column i = image of bit i
+    auto times = [](const uint32_t *m, uint32_t v) { uint32_t r = 0; for (int i = 0; v; i++, v >>= 1) if (v & 1) r ^= m[i]; return r; };
+    uint32_t op[32], sq[32];
+    op[0] = 0xedb88320u;
+    for (int i = 1; i < 32; i++) op[i] = 1u << (i - 1);
+    for (int r = 0; r < 3 + 16; r++) {
+        for (int i = 0; i < 32; i++) sq[i] = times(op, op[i]);
+        for (int i = 0; i < 32; i++) op[i] = sq[i];
+    }
+    for (int i = 0; i < 32; i++) T.crc64k[i] = op[i];
 }
 
 hipError_t launch_gzip_encode(const uint8_t *src, int64_t n, const void *tab, const uint32_t *syms, const int64_t *blks,
@@ -768,7 +783,7 @@ hipError_t launch_gzip_encode(const uint8_t *src, int64_t n, const void *tab, co
     hipLaunchKernelGGL(gz_place_kernel, dim3(nblk), dim3(256), 0, st, src, blks, info, off, scratch, slot, out);
     const int64_t pieces = (n + 65535) >> 16;
     if (pieces) hipLaunchKernelGGL(gz_crc_piece_kernel, dim3((unsigned)((pieces + 255) / 256)), dim3(256), 0, st, src, n, pcrc);
-    hipLaunchKernelGGL(gz_trailer_kernel, dim3(1), dim3(64), 0, st, pcrc, n, off, nblk, out, flen);
+    hipLaunchKernelGGL(gz_trailer_kernel, dim3(1), dim3(64), 0, st, (const GzTab *)tab, pcrc, n, off, nblk, out, flen);
     return hipGetLastError();
 }
 
