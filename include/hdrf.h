@@ -106,11 +106,12 @@ int hdrf_wait_batch(hdrf_ctx *ctx);
 int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
                      const uint64_t *block_ids);
 /* Stream-mode schemes (DataNode.compressor 0/3/4/5: the whole block through a Hadoop codec,
- * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec, codec 0 = SnappyCodec: the file
+ * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec, 0 = SnappyCodec, 5 = GzipCodec: the file
  * the reference writes to chunkDir+id when the block arrives as write()s of the given sizes (one
  * per packet, summing to len) followed by close().  dev_data needs len + 64 readable bytes.
  * Returns the file length (written to out), HDRF_E_CAPACITY if cap is too small,
- * HDRF_E_UNSUPPORTED for codecs 3/5 (LZOP, Gzip).
+ * HDRF_E_UNSUPPORTED for codec 3 (LZOP).  Codec 5's file does not depend on the write sizes
+ * (zlib level 6 fed through Hadoop's ZlibCompressor); they must still add up to len.
  * Records the block length (SET id -> BE32(len)) for hdrf_block_length. */
 int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data, uint64_t len,
                           uint64_t readable, const uint64_t *writes, int32_t nwrites, uint8_t *out, int64_t cap);

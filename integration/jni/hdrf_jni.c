@@ -108,7 +108,7 @@ JNIEXPORT jbyteArray JNICALL JFN(reconstruct0)(JNIEnv *env, jclass cls, jlong h,
     return out;
 }
 
-/* stream mode (compressor 0 SnappyCodec / 4 Lz4Codec): the block's chunkDir file for packet writes */
+/* stream mode (compressor 0 SnappyCodec / 4 Lz4Codec / 5 GzipCodec): the block's chunkDir file for packet writes */
 JNIEXPORT jbyteArray JNICALL JFN(stream0)(JNIEnv *env, jclass cls, jlong h, jint codec, jobject buf, jint len,
                                           jlong id, jlongArray writes)
 {
