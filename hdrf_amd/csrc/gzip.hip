@@ -526,67 +526,127 @@ __device__ void gz_emit(GzBits &w, const GzTab &T, const uint32_t *sy, int64_t n
     gz_put(w, lcode[256], llen[256]);
 }
 
-// info[b] = {kind (0 stored, 1 static, 2 dynamic), bits (non-stored), stored_len}
-__global__ void __launch_bounds__(64) gz_block_kernel(const GzTab *__restrict__ tab, const uint32_t *__restrict__ syms,
-                                                      const int64_t *__restrict__ blks, int nblk, GzBlk *__restrict__ st,
-                                                      uint8_t *__restrict__ scratch, int64_t slot, int64_t *__restrict__ info)
+__device__ __forceinline__ void gz_or_bits(uint8_t *base, int64_t bit, uint64_t v, int n)
 {
-    const int b = blockIdx.x * 64 + threadIdx.x;
-    if (b >= nblk) return;
+    // v holds n <= 48 bits; OR them at bit offset `bit` (LSB-first) with 32-bit atomics
+    while (n > 0) {
+        const int64_t w = bit >> 5;
+        const int sh = (int)(bit & 31);
+        const int take = 32 - sh < n ? 32 - sh : n;
+        const uint32_t part = (uint32_t)(v & ((1ull << take) - 1)) << sh;
+        if (part) atomicOr((uint32_t *)base + w, part);
+        v >>= take;
+        n -= take;
+        bit += take;
+    }
+}
+
+// info[b] = {kind (0 stored, 1 static, 2 dynamic), bits (non-stored), stored_len}.  One workgroup
+// per deflate block: lane 0 builds the trees, makes the choice and writes the block header and
+// code-length codes; then the symbols are coded 256 at a time (bit lengths, a workgroup scan,
+// ORed at their offsets).  The slot must be zero.
+__global__ void __launch_bounds__(256) gz_block_kernel(const GzTab *__restrict__ tab, const uint32_t *__restrict__ syms,
+                                                       const int64_t *__restrict__ blks, int nblk, GzBlk *__restrict__ st,
+                                                       uint8_t *__restrict__ scratch, int64_t slot, int64_t *__restrict__ info)
+{
+    __shared__ int64_t s_bit;
+    __shared__ int s_kind;
+    __shared__ uint32_t s_wsum[4];
+    const int b = blockIdx.x;
     const GzTab &T = *tab;
     GzBlk &s = st[b];
-    const int64_t *r = blks + 5 * b;
-    const int64_t s0 = b ? blks[5 * (b - 1)] : 0, s1 = r[0];
-    const int last = (int)r[4];
-    const int64_t stored_len = r[2] - r[1];
-    const bool have_buf = r[1] >= r[3];
-    for (int n = 0; n < 286; n++) s.lfc[n] = 0;
-    for (int n = 0; n < 30; n++) s.dfc[n] = 0;
-    for (int n = 0; n < 19; n++) s.bfc[n] = 0;
-    s.lfc[256] = 1;
-    s.opt_len = s.static_len = 0;
-    for (int64_t i = s0; i < s1; i++) {
-        const unsigned dist = syms[i] >> 8, lc = syms[i] & 0xff;
-        if (dist == 0) s.lfc[lc]++;
-        else { s.lfc[T.len_code[lc] + 257]++; s.dfc[gz_dcode(T, dist - 1)]++; }
+    const int64_t s0 = b ? blks[5 * (b - 1)] : 0, s1 = blks[5 * b];
+    uint8_t *outp = scratch + (int64_t)b * slot;
+    if (threadIdx.x == 0) {
+        const int64_t *r = blks + 5 * b;
+        const int last = (int)r[4];
+        const int64_t stored_len = r[2] - r[1];
+        const bool have_buf = r[1] >= r[3];
+        for (int n = 0; n < 286; n++) s.lfc[n] = 0;
+        for (int n = 0; n < 30; n++) s.dfc[n] = 0;
+        for (int n = 0; n < 19; n++) s.bfc[n] = 0;
+        s.lfc[256] = 1;
+        s.opt_len = s.static_len = 0;
+        for (int64_t i = s0; i < s1; i++) {
+            const unsigned dist = syms[i] >> 8, lc = syms[i] & 0xff;
+            if (dist == 0) s.lfc[lc]++;
+            else { s.lfc[T.len_code[lc] + 257]++; s.dfc[gz_dcode(T, dist - 1)]++; }
+        }
+        GzTree lt{s.lfc, s.ldl, T.sllen, kGzXL, 257, 286, 15, 0};
+        GzTree dt{s.dfc, s.ddl, T.sdlen, kGzXD, 0, 30, 15, 0};
+        GzTree bt{s.bfc, s.bdl, nullptr, kGzXB, 0, 19, 7, 0};
+        gz_tree(s, lt);
+        gz_tree(s, dt);
+        gz_rle(s, lt, lt.max_code, nullptr);
+        gz_rle(s, dt, dt.max_code, nullptr);
+        gz_tree(s, bt);
+        int max_blindex;
+        for (max_blindex = 18; max_blindex >= 3; max_blindex--)
+            if (s.bdl[kGzBlOrder[max_blindex]] != 0) break;
+        s.opt_len += 3 * ((int64_t)max_blindex + 1) + 14;
+        int64_t opt_lenb = (s.opt_len + 10) >> 3;
+        const int64_t static_lenb = (s.static_len + 10) >> 3;
+        if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+        int64_t *inf = info + 3 * b;
+        inf[2] = stored_len;
+        GzBits w{outp, 0, 0, 0};
+        if (stored_len + 4 <= opt_lenb && have_buf) {
+            s_kind = 0;
+        } else if (static_lenb == opt_lenb) {
+            gz_put(w, 2u + (unsigned)last, 3);
+            s_kind = 1;
+        } else {
+            gz_put(w, 4u + (unsigned)last, 3);
+            const int lcodes = lt.max_code + 1, dcodes = dt.max_code + 1, blcodes = max_blindex + 1;
+            gz_put(w, (unsigned)(lcodes - 257), 5);
+            gz_put(w, (unsigned)(dcodes - 1), 5);
+            gz_put(w, (unsigned)(blcodes - 4), 4);
+            for (int k = 0; k < blcodes; k++) gz_put(w, s.bdl[kGzBlOrder[k]], 3);
+            gz_rle(s, lt, lcodes - 1, &w);
+            gz_rle(s, dt, dcodes - 1, &w);
+            s_kind = 2;
+        }
+        if (w.nb) w.out[w.pos] = (uint8_t)w.bb;
+        s_bit = w.pos * 8 + w.nb;
+        inf[0] = s_kind;
     }
-    GzTree lt{s.lfc, s.ldl, T.sllen, kGzXL, 257, 286, 15, 0};
-    GzTree dt{s.dfc, s.ddl, T.sdlen, kGzXD, 0, 30, 15, 0};
-    GzTree bt{s.bfc, s.bdl, nullptr, kGzXB, 0, 19, 7, 0};
-    gz_tree(s, lt);
-    gz_tree(s, dt);
-    gz_rle(s, lt, lt.max_code, nullptr);
-    gz_rle(s, dt, dt.max_code, nullptr);
-    gz_tree(s, bt);
-    int max_blindex;
-    for (max_blindex = 18; max_blindex >= 3; max_blindex--)
-        if (s.bdl[kGzBlOrder[max_blindex]] != 0) break;
-    s.opt_len += 3 * ((int64_t)max_blindex + 1) + 14;
-    int64_t opt_lenb = (s.opt_len + 10) >> 3;
-    const int64_t static_lenb = (s.static_len + 10) >> 3;
-    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
-    int64_t *inf = info + 3 * b;
-    inf[2] = stored_len;
-    if (stored_len + 4 <= opt_lenb && have_buf) { inf[0] = 0; inf[1] = 0; return; }
-    GzBits w{scratch + (int64_t)b * slot, 0, 0, 0};
-    if (static_lenb == opt_lenb) {
-        gz_put(w, 2u + (unsigned)last, 3);
-        gz_emit(w, T, syms + s0, s1 - s0, T.slcode, T.sllen, T.sdcode, T.sdlen);
-        inf[0] = 1;
-    } else {
-        gz_put(w, 4u + (unsigned)last, 3);
-        const int lcodes = lt.max_code + 1, dcodes = dt.max_code + 1, blcodes = max_blindex + 1;
-        gz_put(w, (unsigned)(lcodes - 257), 5);
-        gz_put(w, (unsigned)(dcodes - 1), 5);
-        gz_put(w, (unsigned)(blcodes - 4), 4);
-        for (int k = 0; k < blcodes; k++) gz_put(w, s.bdl[kGzBlOrder[k]], 3);
-        gz_rle(s, lt, lcodes - 1, &w);
-        gz_rle(s, dt, dcodes - 1, &w);
-        gz_emit(w, T, syms + s0, s1 - s0, s.lfc, s.ldl, s.dfc, s.ddl);
-        inf[0] = 2;
+    __syncthreads();
+    const int kind = s_kind;
+    if (kind == 0) return;
+    __threadfence_block();
+    const uint16_t *lcode = kind == 1 ? T.slcode : s.lfc, *llen = kind == 1 ? T.sllen : s.ldl;
+    const uint16_t *dcode = kind == 1 ? T.sdcode : s.dfc, *dlen = kind == 1 ? T.sdlen : s.ddl;
+    int64_t bit = s_bit;
+    for (int64_t c0 = s0; c0 < s1; c0 += 256) {
+        const int64_t i = c0 + threadIdx.x;
+        uint64_t v = 0;
+        int nb = 0;
+        if (i < s1) {
+            unsigned dist = syms[i] >> 8, lc = syms[i] & 0xff;
+            if (dist == 0) { v = lcode[lc]; nb = llen[lc]; }
+            else {
+                int code = T.len_code[lc];
+                v = lcode[code + 257]; nb = llen[code + 257];
+                if (kGzXL[code]) { v |= (uint64_t)(lc - (unsigned)T.base_len[code]) << nb; nb += kGzXL[code]; }
+                dist--;
+                code = gz_dcode(T, dist);
+                v |= (uint64_t)dcode[code] << nb; nb += dlen[code];
+                if (kGzXD[code]) { v |= (uint64_t)(dist - (unsigned)T.base_dist[code]) << nb; nb += kGzXD[code]; }
+            }
+        }
+        const uint32_t incl = wave_incl_scan((uint32_t)nb);
+        if (lane_id() == 63) s_wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (int k = 0; k < 4; k++) { if (k < (int)(threadIdx.x >> 6)) pre += s_wsum[k]; tot += s_wsum[k]; }
+        if (nb) gz_or_bits(outp, bit + pre + incl - nb, v, nb);
+        bit += tot;
+        __syncthreads();
     }
-    inf[1] = w.pos * 8 + w.nb;
-    if (w.nb) w.out[w.pos] = (uint8_t)w.bb;
+    if (threadIdx.x == 0) {
+        gz_or_bits(outp, bit, lcode[256], llen[256]);
+        info[3 * b + 1] = bit + llen[256];
+    }
 }
 
 // ---- stage 4: bit offsets (one lane: the stored blocks' padding depends on the byte phase), then
@@ -777,7 +837,8 @@ hipError_t launch_gzip_encode(const uint8_t *src, int64_t n, const void *tab, co
                               int nblk, void *state, uint8_t *scratch, int64_t slot, int64_t *info, int64_t *off,
                               uint32_t *pcrc, uint8_t *out, int64_t *flen, hipStream_t st)
 {
-    hipLaunchKernelGGL(gz_block_kernel, dim3((nblk + 63) / 64), dim3(64), 0, st, (const GzTab *)tab, syms, blks, nblk,
+    (void)hipMemsetAsync(scratch, 0, (size_t)slot * (size_t)nblk, st);
+    hipLaunchKernelGGL(gz_block_kernel, dim3(nblk), dim3(256), 0, st, (const GzTab *)tab, syms, blks, nblk,
                        (GzBlk *)state, scratch, slot, info);
     hipLaunchKernelGGL(gz_offsets_kernel, dim3(1), dim3(64), 0, st, info, nblk, off);
     hipLaunchKernelGGL(gz_place_kernel, dim3(nblk), dim3(256), 0, st, src, blks, info, off, scratch, slot, out);
