@@ -15,7 +15,8 @@
 //   MAX_DIST).  One workgroup per 4096-position tile: a 32768-entry "last position" table in LDS
 //   (128 KiB) is seeded from the MAX_DIST positions before the tile (atomicMax, order-free), then
 //   the tile runs in rounds of 256 positions (nearest equal hash earlier in the round, else the
-//   table; the round's positions are then max-inserted).
+//   table; the round's positions are then max-inserted).  Within a wave the nearest equal hash
+//   comes from 16 ballots; the round's 4 waves read and insert in position order.
 // gz_match_kernel: one lane per position walks prev[] and compares bytes; out128[p] / out32[p] =
 //   (len << 16) | dist of the chain-128 / chain-32 answer (0 if no match of >= 3 bytes), bit 31
 //   set when the head candidate sits at distance exactly MAX_DIST on a 32 KiB boundary — zlib's
@@ -38,7 +39,6 @@ __global__ void __launch_bounds__(256) gz_prev_kernel(const uint8_t *__restrict_
                                                       uint32_t *__restrict__ prev)
 {
     extern __shared__ uint32_t last[];             // kGzHash entries: 1 + latest position (0 none)
-    __shared__ uint32_t sh[256];
     const int tid = threadIdx.x;
     const int64_t t0 = (int64_t)blockIdx.x * kGzTile;
     const int64_t nins = n - 2;                    // positions p <= n-3 are hashed/inserted
@@ -48,22 +48,26 @@ __global__ void __launch_bounds__(256) gz_prev_kernel(const uint8_t *__restrict_
     if (w0 < 1) w0 = 1;
     for (int64_t q = w0 + tid; q < t0 && q < nins; q += 256) atomicMax(&last[gz_hash(src + q)], (uint32_t)q + 1u);
     __syncthreads();
+    const int lane = lane_id(), wave = tid >> 6;
     for (int r = 0; r < kGzTile; r += 256) {
         const int64_t p = t0 + r + tid;
         const bool valid = p < nins;
-        const uint32_t h = valid ? gz_hash(src + p) : 0xffffffffu;
-        sh[tid] = (valid && p >= 1) ? h : 0xfffffffeu;
-        __syncthreads();
-        uint32_t pr = 0;
-        if (valid) {
-            int j = tid - 1;
-            while (j >= 0 && sh[j] != h) j--;
-            pr = j >= 0 ? (uint32_t)(t0 + r + j) + 1u : last[h];
-            prev[p] = pr;
+        const uint32_t h = valid ? gz_hash(src + p) : 0u;
+        // lanes of this wave holding the same key (16 ballots); key bit 15 = not a candidate
+        const uint32_t key = (valid && p >= 1) ? h : 0x8000u;
+        uint64_t m = ~0ull;
+        for (int bt = 0; bt < 16; bt++) {
+            const uint64_t bal = __ballot((key >> bt) & 1u);
+            m &= ((key >> bt) & 1u) ? bal : ~bal;
         }
-        __syncthreads();
-        if (valid && p >= 1) atomicMax(&last[h], (uint32_t)p + 1u);
-        __syncthreads();
+        const uint64_t lower = lane ? m & ((1ull << lane) - 1ull) : 0ull;
+        for (int w = 0; w < 4; w++) {                  // waves in position order: table, then insert
+            if (wave == w && valid) {
+                prev[p] = lower ? (uint32_t)(p - lane + (63 - __builtin_clzll(lower))) + 1u : last[h];
+                if (p >= 1) atomicMax(&last[h], (uint32_t)p + 1u);
+            }
+            __syncthreads();
+        }
     }
 }
 
