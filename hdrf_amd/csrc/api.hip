@@ -45,8 +45,9 @@ struct Slot {
     BlockDesc *d_blocks = nullptr;
     uint32_t *d_spec = nullptr;
     SegMeta *d_meta = nullptr;
-    int32_t *d_sync = nullptr;
-    SegPlan *d_plan = nullptr;
+    int *d_rq = nullptr, *d_rq_count = nullptr;   // failed speculative boundaries (repair queue), meta_cap entries
+    size_t spec_words = 0, meta_cap = 0;      // capacity of d_spec (u32) / d_meta (segments), grown on demand
+    int total_waves = 0, total_segs = 0, spec_cap = 0;   // lane walk of the batch in this slot
     BlockState *d_bst = nullptr;
     uint32_t *d_off = nullptr, *d_dig = nullptr, *d_mid = nullptr, *d_slot = nullptr, *d_pre = nullptr;
     uint8_t *d_flags = nullptr;
@@ -93,7 +94,7 @@ struct hdrf_ctx {
     hipStream_t stB = nullptr;   // stream B: back stage (index + store)
     hipStream_t stW = nullptr;   // stream W: chunking stage
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
-    int max_batch = 0, cap_blk = 0, ntiles = 0, spec_cap = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
+    int max_batch = 0, cap_blk = 0, ntiles = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
     Slot sl[kSlots];
     uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
     int res = 0;                   // slot of the last completed batch (hdrf_batch_* views)
@@ -172,6 +173,8 @@ static int device_error(hdrf_ctx *ctx, int herr)
     std::string m = "device reported error flags " + std::to_string(herr);
     if (herr & 32) m += " (arena_slots too small: a storer range closed more containers in one batch than its ring holds)";
     if (herr & 2) m += " (index table full)";
+    if (herr & 1) m += " (chunking: offsets capacity or an unterminated fallback walk)";
+    if (herr & 192) m += " (chunking: speculative list overflow / inconsistent stitch)";
     return set_err(ctx, (herr & kErrCapacity) ? HDRF_E_CAPACITY : HDRF_E_DEVICE, m);
 }
 
@@ -225,7 +228,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
 
 static void free_slot(Slot &S)
 {
-    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_sync, S.d_plan, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
+    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
                    S.d_pre, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
                    S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err};
     for (void *p : dev)
@@ -270,12 +273,17 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
     const hdrf_cfg &c = ctx->cfg;
     const int B = ctx->max_batch;
     const size_t nchunk = (size_t)B * ctx->cap_blk;
-    const size_t nseg = (size_t)B * kMaxSegs;
     const int nseg_lz = (int)((c.container_max + 261099) / 261100);
     int rc = 0;
-    if ((rc = dalloc(ctx, &S.d_blocks, B)) || (rc = dalloc(ctx, &S.d_spec, nseg * ctx->spec_cap)) ||
-        (rc = dalloc(ctx, &S.d_meta, nseg)) || (rc = dalloc(ctx, &S.d_sync, nseg)) ||
-        (rc = dalloc(ctx, &S.d_plan, nseg)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
+    // speculative lists: sized for one wave of lane segments per 1 MiB of the largest batch, grown
+    // on demand when a batch cuts finer (prepare_blocks)
+    const int seg_len0 = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / (c.window + 2)))) *
+                         (c.window + 2);
+    S.meta_cap = (size_t)B * (size_t)(c.max_block_bytes / seg_len0 + 2);
+    S.spec_words = S.meta_cap * (size_t)lane_spec_cap(seg_len0, c.window);
+    if ((rc = dalloc(ctx, &S.d_blocks, B)) || (rc = dalloc(ctx, &S.d_spec, S.spec_words)) ||
+        (rc = dalloc(ctx, &S.d_meta, S.meta_cap)) || (rc = dalloc(ctx, &S.d_rq, S.meta_cap)) ||
+        (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
         (rc = dalloc(ctx, &S.d_off, nchunk)) || (rc = dalloc(ctx, &S.d_dig, nchunk * ctx->HW)) ||
         (rc = dalloc(ctx, &S.d_mid, nchunk * 8)) || (rc = dalloc(ctx, &S.d_slot, nchunk)) ||
         (rc = dalloc(ctx, &S.d_pre, nchunk)) || (rc = dalloc(ctx, &S.d_flags, nchunk)) ||
@@ -404,7 +412,6 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     // minimum chunk is window+2 bytes; +2 for the drop-last/append rule and rounding
     ctx->cap_blk = (int)(c.max_block_bytes / (c.window + 2) + 2);
     ctx->ntiles = (ctx->cap_blk + 255) / 256;
-    ctx->spec_cap = (int)((2ll * c.segment_bytes) / (c.window + 2) + 4 + kOverrun);
     ctx->ev_cap = (int)(B * (c.max_block_bytes / ((int64_t)c.container_max - c.max_chunk) + 2) + 16);
     ctx->closed_cap = 3 * ctx->ev_cap;
     ctx->coll_cap = 1 << 16;
@@ -476,35 +483,62 @@ static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t l
     ctx->containers[id] = ContainerInfo{slot, len, closed, clen};
 }
 
-// Validate a batch and fill the slot's (pinned) descriptors; returns the largest segment count.
+// Validate a batch and fill the slot's (pinned) descriptors: the lane segmentation of the chunking
+// pass (chunk.hip).  seg_len = segment_bytes / 63 rounded to a multiple of window + 2, within
+// [4, 24] x 702 B, and shortened (down to 6 x 702 B) while the batch would give the lane walk fewer
+// than 1024 waves (one-block calls).  Grows the slot's speculative lists when needed (the slot's
+// previous batch has completed).
 static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t *const *dev_data,
-                          const uint64_t *len, const uint64_t *readable, int *max_nseg_out)
+                          const uint64_t *len, const uint64_t *readable)
 {
     if (nblocks < 1 || nblocks > ctx->max_batch || !dev_data || !len || !readable)
         return set_err(ctx, HDRF_E_INVAL, "bad batch arguments");
     const hdrf_cfg &c = ctx->cfg;
-    int max_nseg = 1;
+    int64_t total = 0;
     for (int b = 0; b < nblocks; b++) {
         if ((int64_t)len[b] > c.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
         if (readable[b] < len[b] + kSlack) return set_err(ctx, HDRF_E_INVAL, "readable must be >= len + 64");
         if (((uintptr_t)dev_data[b] & 15) != 0) return set_err(ctx, HDRF_E_INVAL, "block data must be 16-B aligned");
+        total += (int64_t)len[b];
     }
+    const int unit = c.window + 2;
+    int wins = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / unit)));
+    while (wins > 6 && total / ((int64_t)wins * unit * kWaveSegs) < 1024) wins--;
+    const int seg_len = wins * unit;
+    int seg0 = 0, wave0 = 0;
     for (int b = 0; b < nblocks; b++) {
         BlockDesc &d = S.h_desc[b];
         d.data = dev_data[b];
         d.len = len[b];
         d.readable = readable[b];
-        int nseg = (int)std::min<int64_t>(kMaxSegs, std::max<int64_t>(1, (int64_t)len[b] / c.segment_bytes));
-        int seg_len = (int)len[b];
-        if (nseg > 1) {
-            seg_len = (int)(((int64_t)len[b] / nseg) / (c.window + 2) * (c.window + 2));
-            if (seg_len < 4 * (c.window + 2)) { nseg = 1; seg_len = (int)len[b]; }
-        }
-        d.nseg = nseg;
+        d.nseg = (int)std::max<int64_t>(1, ((int64_t)len[b] + seg_len - 1) / seg_len);
         d.seg_len = seg_len;
-        max_nseg = std::max(max_nseg, nseg);
+        d.seg0 = seg0;
+        d.wave0 = wave0;
+        seg0 += d.nseg;
+        wave0 += (d.nseg + kWaveSegs - 1) / kWaveSegs;
     }
-    *max_nseg_out = max_nseg;
+    S.total_waves = wave0;
+    S.total_segs = seg0;
+    S.spec_cap = lane_spec_cap(seg_len, c.window);
+    const size_t words = (size_t)seg0 * S.spec_cap;
+    if ((size_t)seg0 > S.meta_cap) {
+        (void)hipFree(S.d_meta);
+        (void)hipFree(S.d_rq);
+        S.d_meta = nullptr;
+        S.d_rq = nullptr;
+        S.meta_cap = 0;
+        if (int rc = dalloc(ctx, &S.d_meta, (size_t)seg0)) return rc;
+        if (int rc = dalloc(ctx, &S.d_rq, (size_t)seg0)) return rc;
+        S.meta_cap = (size_t)seg0;
+    }
+    if (words > S.spec_words) {
+        (void)hipFree(S.d_spec);
+        S.d_spec = nullptr;
+        S.spec_words = 0;
+        if (int rc = dalloc(ctx, &S.d_spec, words)) return rc;
+        S.spec_words = words;
+    }
     return 0;
 }
 
@@ -532,8 +566,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         if (int rc = wait_one(ctx)) return rc;
     Slot &S = ctx->sl[ctx->nsub % kSlots];
     const hdrf_cfg &c = ctx->cfg;
-    int max_nseg = 1;
-    if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable, &max_nseg)) return rc;
+    if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable)) return rc;
     S.ids.assign(nblocks, 0);
     if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
     S.lens.assign(len, len + nblocks);
@@ -548,8 +581,8 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, W));
     Marker mw;
     mw.ev = ctx->timing ? S.evW : nullptr;
-    HIPCK(launch_chunking(S.d_blocks, nblocks, max_nseg, c.window, c.max_chunk, S.d_spec, ctx->spec_cap, S.d_meta,
-                          S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, W, &mw));
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.total_waves, S.total_segs, c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta,
+                          S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, W, &mw));
     mw.mark(W);
     HIPCK(hipEventRecord(S.walk_done, W));
     // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig)
@@ -1155,15 +1188,15 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     const int si = (int)(ctx->gx_nfront % 2);
     Slot &S = ctx->sl[si];
     const hdrf_cfg &c = ctx->cfg;
-    int max_nseg = 1;
-    if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable, &max_nseg)) return rc;
+    if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable)) return rc;
     S.gx_batch = ++ctx->batch;
     hipStream_t st = ctx->st;
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
     Marker mk;
     mk.ev = ctx->timing ? S.evB : nullptr;             // 8 markers: walk .. slow+decide, end
-    HIPCK(launch_chunking(S.d_blocks, nblocks, max_nseg, c.window, c.max_chunk, S.d_spec, ctx->spec_cap,
-                          S.d_meta, S.d_sync, S.d_plan, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, st, &mk));
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.total_waves, S.total_segs, c.window, c.max_chunk, S.d_spec, S.spec_cap,
+                          S.d_meta, S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, st,
+                          &mk));
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
                      S.d_queue, st, &mk));

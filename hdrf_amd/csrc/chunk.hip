@@ -278,7 +278,7 @@ __device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const 
                     p = f2 + 1;                                        // :276-283
                     if (lane_id() == (cnt & 63)) stage = (uint32_t)p;
                     cnt++;
-                    if ((cnt & 63) == 0) sink.out[cnt - 64 + lane_id()] = stage;
+                    if ((cnt & 63) == 0) sink.store64(cnt, stage);
                     pushed = true;
                     if (p >= cut_thr) break;
                 }
@@ -345,12 +345,13 @@ struct ListSink {
     int cap;
     int cnt;
     uint32_t stage;
+    __device__ __forceinline__ void store64(int c, uint32_t st) { out[c - 64 + lane_id()] = st; }
     __device__ __forceinline__ bool push(uint32_t cut)
     {
         if (cnt >= cap) return false;
         if (lane_id() == (cnt & 63)) stage = cut;
         cnt++;
-        if ((cnt & 63) == 0) out[cnt - 64 + lane_id()] = stage;
+        if ((cnt & 63) == 0) store64(cnt, stage);
         return true;
     }
     __device__ __forceinline__ void flush()
@@ -360,19 +361,22 @@ struct ListSink {
     }
 };
 
-// Stop predicates: operator() is evaluated after every cut; cut_thr/cnt_thr tell the fast path the
-// first cut position / count at which the predicate can change, so it only asks then.
-struct SpecStop {          // segment walk: cuts past s_next are overrun; stop after kOverrun of them
-    int s_next;
-    int n_main;
-    __device__ __forceinline__ bool operator()(int cut, int cnt)
+// Cut sink that only counts (the repair pass finds where a chain merges before anything is written).
+struct CountSink {
+    int cap;
+    int cnt;
+    uint32_t stage;
+    __device__ __forceinline__ void store64(int, uint32_t) {}
+    __device__ __forceinline__ bool push(uint32_t)
     {
-        if (n_main < 0 && cut >= s_next) n_main = cnt - 1;
-        return n_main >= 0 && cnt - n_main >= kOverrun;
+        if (cnt >= cap) return false;
+        cnt++;
+        return true;
     }
-    __device__ __forceinline__ int cut_thr() const { return n_main < 0 ? s_next : 0x7fffffff; }
-    __device__ __forceinline__ int cnt_thr() const { return n_main < 0 ? 0x7fffffff : n_main + kOverrun; }
 };
+
+// Stop predicate of the sequential fallback walk: never stops (operator() is evaluated after every
+// cut; cut_thr/cnt_thr tell the fast path the first cut position / count at which it could change).
 struct NoStop {
     __device__ __forceinline__ bool operator()(int, int) { return false; }
     __device__ __forceinline__ int cut_thr() const { return 0x7fffffff; }
@@ -381,8 +385,8 @@ struct NoStop {
 
 // Walk the chain from p (a cut, or the block start when first) calling sink.push(cut) for
 // every cut until the data ends (returns true) or the sink/stop predicate says stop (false).
-template <class Stop>
-__device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, ListSink &sink, Stop &stop)
+template <class Sink, class Stop>
+__device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, Sink &sink, Stop &stop)
 {
     Chain ch;
     ch.p = p; ch.state = kWindow; ch.q = 0; ch.lim = 0; ch.m = 0; ch.first = first; ch.ended = false;
@@ -403,152 +407,475 @@ __device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, 
     return ch.ended;
 }
 
+
 // ------------------------------------------------------------------------------------------
-// 1. speculative walk: a pool of waves (HDRF_WALK_WAVES per SIMD, default 8 = one segment per
-//    wave for a 64 x 128 MiB batch) strides over the (block, segment) pairs.  The walk is bound
-//    by the scalar unit (one SALU issue per SIMD per 4 cycles), so it wants every wave slot.
-__global__ void __launch_bounds__(256) spec_walk_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
-                                                        int max_nseg, int w, int maxlen,
-                                                        uint32_t *__restrict__ spec, int spec_cap,
-                                                        SegMeta *__restrict__ meta)
-{
-    const int total = nblocks * max_nseg;
-    const int nw = gridDim.x * 4;
-    for (int t = blockIdx.x * 4 + wave_id(); t < total; t += nw) {
-        const int b = t / max_nseg;
-        const int k = t - b * max_nseg;
-        const BlockDesc bd = blocks[b];
-        if (k >= bd.nseg) continue;
-        const int size = (int)bd.len;
-        const int s_k = k * bd.seg_len;
-        const int s_next = (k + 1 == bd.nseg) ? 0x7fffffff : (k + 1) * bd.seg_len;  // last: every cut is main
-        WalkCfg W;
-        W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = size;
-        W.w = w; W.maxlen = maxlen;
-        ListSink sink;
-        const int idx = b * kMaxSegs + k;
-        sink.out = spec + (size_t)idx * spec_cap; sink.cap = spec_cap; sink.cnt = 0; sink.stage = 0;
-        SpecStop stop{s_next, -1};
-        bool ended = walk_chain(W, s_k, k == 0, sink, stop);
-        sink.flush();
-        const int n_main = stop.n_main < 0 ? sink.cnt : stop.n_main;
-        if (lane_id() == 0) {
-            SegMeta m;
-            m.n_main = n_main; m.n_over = sink.cnt - n_main; m.ended = ended ? 1 : 0; m.pad = 0;
-            meta[idx] = m;
-        }
-    }
-}
+// 1. lane walk (the speculative pass).  Every block is cut into segments of seg_len bytes (a
+//    multiple of 702); lane l of a wave walks the chain from the start of segment k = 63*wl + l
+//    as if a cut were there, one 32-B unit at a time, entirely in VALU:
+//      window part   M = max(M, unit max) while the unit lies inside [p, p+700]; the unit
+//                    holding p (a cut, or the segment start) is folded in later from a saved
+//                    copy (every 8 units, always before the window can end); the unit holding
+//                    p+700 needs its exact prefix only when its max exceeds M
+//      search part   the 32-bit mask of bytes >= M (SWAR carry test + v_dot4 bit gather), cut to
+//                    [p+701, min(p+maxlen, size-1)], plus the forced position p+maxlen; the first
+//                    set bit j gives the cut j+1 (DN/DataDeduplicator.java:276-294)
+//    Its cuts go to an LDS list (u16 offsets from the segment start; written to the segment's
+//    global list when the lane stops).  Past its segment end (overrun) a lane compares each cut
+//    with the next lane's list (the next segment's chain, walked concurrently and seg_len bytes
+//    ahead): the first shared cut proves the chains equal from there on, the lane records (i, j)
+//    and stops.  Lane 63 walks the NEXT wave's first segment (a helper: LDS only), so every
+//    boundary is settled inside one wave.  A lane that meets no shared cut within kLaneOver cuts
+//    or ~seg_len bytes reports kSyncFail and queues its boundary for the repair pass.
+//    Bytes move HBM -> VGPR -> LDS in 4 KiB steps (each lane fetches 16 B of four segments, so a
+//    wave-instruction reads 16 x 64 contiguous bytes), prefetched two steps ahead, and every lane
+//    reads its own 64 B back with conflict-free ds_read_b128 (XOR-swizzled 16-B slots).
 
-// 2. sync: one wave per (block, boundary k -> k+1).  sync[idx] = i | j<<16, or -1 END, -2 FAIL.
-//    Lane i holds overrun cut O_k[i]; lane j holds segment k+1's cut M_{k+1}[j] (first 64);
-//    a lower_bound through ds_bpermute finds whether O_k[i] is one of them.
-__global__ void __launch_bounds__(256) spec_sync_kernel(const BlockDesc *__restrict__ blocks,
-                                                        const uint32_t *__restrict__ spec, int spec_cap,
-                                                        const SegMeta *__restrict__ meta, int32_t *__restrict__ sync)
+// A unit is 32 bytes (two granules, 8 dwords) of one lane's segment.  Biasing (XOR 0x80, signed
+// order == unsigned order) is folded into the masks below.
+struct Unit {
+    uint32_t d[8];
+};
+
+// max over the 32 biased bytes: even bytes and odd bytes as u16 lanes (odd ones scaled by 256,
+// which keeps their order), v_pk_max_u16 trees, then the two halves
+__device__ __forceinline__ uint32_t unit_max(const Unit &u)
 {
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * 4 + wave_id();
-    const int l = lane_id();
-    const BlockDesc bd = blocks[b];
-    if (k + 1 >= bd.nseg) return;
-    const int idx = b * kMaxSegs + k;
-    const SegMeta m0 = meta[idx], m1 = meta[idx + 1];
-    const uint32_t *L0 = spec + (size_t)idx * spec_cap;
-    const uint32_t *L1 = spec + (size_t)(idx + 1) * spec_cap;
-    const int n1 = min(m1.n_main, 64);
-    const uint32_t mv = l < n1 ? L1[l] : 0xffffffffu;
-    const uint32_t o = l < m0.n_over ? L0[m0.n_main + l] : 0xfffffffeu;
-    int pos = 0;
+    uint32_t e = 0, o = 0;
 #pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {
-        const uint32_t v = (uint32_t)__shfl((int)mv, pos + step - 1, 64);
-        if (v < o) pos += step;
+    for (int i = 0; i < 8; i++) {
+        e = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(as_us2(e), as_us2((u.d[i] ^ 0x80808080u) & 0x00ff00ffu)));
+        o = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(as_us2(o), as_us2((u.d[i] ^ 0x80808080u) & 0xff00ff00u)));
     }
-    const uint32_t v = (uint32_t)__shfl((int)mv, pos, 64);
-    const bool found = (l < m0.n_over) && pos < n1 && v == o;
-    const unsigned long long bal = ballot64(found);
-    const int i = bal ? __builtin_ctzll(bal) : 0;
-    const int jsel = __shfl(pos, i, 64);
-    if (l == 0) sync[idx] = bal ? (i | (jsel << 16)) : (m0.ended ? -1 : -2);
+    const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(as_us2(e), as_us2(o >> 8)));
+    return max(m & 0xffffu, m >> 16);
 }
 
-// 3a. plan: one 256-thread workgroup per block; thread k handles segment k.
-__global__ void __launch_bounds__(256) spec_plan_kernel(const BlockDesc *__restrict__ blocks,
-                                                        const uint32_t *__restrict__ spec, int spec_cap,
-                                                        const SegMeta *__restrict__ meta, const int32_t *__restrict__ sync,
-                                                        SegPlan *__restrict__ plan, BlockState *__restrict__ bst)
+// max over the biased bytes whose unit index is in [lo, hi] (0 <= lo, hi <= 31)
+__device__ __forceinline__ uint32_t unit_range_max(const Unit &u, int lo, int hi)
 {
-    __shared__ int s_bad;
-    __shared__ uint32_t s_cnt[256];
-    const int b = blockIdx.x;
-    const int k = threadIdx.x;
-    const BlockDesc bd = blocks[b];
-    const int nseg = bd.nseg;
-    if (k == 0) s_bad = nseg;          // first boundary whose status is not "found"
-    __syncthreads();
-    const int idx = b * kMaxSegs + k;
-    int st = 0;
-    if (k + 1 < nseg) {
-        st = sync[idx];
-        if (st < 0) atomicMin(&s_bad, k);
+    Unit m;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int a = min(max(lo - 4 * i, 0), 4), b = min(max(hi - 4 * i + 1, 0), 4);   // keep bytes [a, b)
+        const uint32_t keep = (a >= b) ? 0u : ((b == 4 ? ~0u : ((1u << (8 * b)) - 1u)) & (~0u << (8 * a)));
+        m.d[i] = ((u.d[i] ^ 0x80808080u) & keep) ^ 0x80808080u;     // dropped bytes read as biased 0
     }
-    __syncthreads();
-    const int bad = s_bad;
-    int main_begin = 0, main_count = 0, over_count = 0;
-    if (k < nseg && k <= bad) {
-        const SegMeta m = meta[idx];
-        main_begin = (k == 0) ? 0 : ((sync[idx - 1] >> 16) & 0xffff);
-        main_count = m.n_main - main_begin;
-        if (k + 1 < nseg) over_count = (k == bad) ? m.n_over : (st & 0xffff);
+    return unit_max(m);
+}
+
+// 32-bit mask of the biased bytes >= m (1 <= m <= 255): SWAR carry-out of byte + (256 - m), the
+// bit-7 flags gathered with v_dot4_u32_u8 (weights 1..128 per dword pair)
+// bit 7 of each byte of raw dword d where the biased byte (d ^ 0x80) >= m: the carry out of the
+// byte sum (d ^ 0x80) + (256 - m) = maj(NOT d7, C7, s7) with s = low-7-bit sum; 4 VALU (and, add,
+// bitop3, and)
+__device__ __forceinline__ uint32_t ge_flags(uint32_t d, uint32_t C, uint32_t Cm)
+{
+    const uint32_t s = (d & 0x7f7f7f7fu) + Cm;
+    return __builtin_amdgcn_bitop3_b32(d, C, s, 0x8e) & 0x80808080u;   // 0x8e: maj(NOT d, C, s)
+}
+__device__ __forceinline__ uint32_t unit_ge(const Unit &u, uint32_t m)
+{
+    const uint32_t C = __builtin_amdgcn_perm(256u - m, 256u - m, 0u), Cm = C & 0x7f7f7f7fu;
+    uint32_t x[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const uint32_t f0 = ge_flags(u.d[2 * p], C, Cm), f1 = ge_flags(u.d[2 * p + 1], C, Cm);
+        x[p] = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
     }
-    uint32_t c = (uint32_t)(main_count + over_count);
-    s_cnt[k] = c;
-    __syncthreads();
-    // exclusive scan over 256 entries (Hillis-Steele in LDS)
-    for (int d = 1; d < 256; d <<= 1) {
-        uint32_t t = k >= d ? s_cnt[k - d] : 0u;
-        __syncthreads();
-        s_cnt[k] += t;
-        __syncthreads();
+    return (x[0] >> 7) | (x[1] << 1) | (x[2] << 9) | (x[3] << 17);
+}
+
+constexpr int kNegPos = -(1 << 30);      // "no forced cut possible" relative position
+
+// LDS of one wave (one array for the whole workgroup: a second __shared__ object beside LDS-DMA
+// staging makes hipcc drain vmcnt before LDS reads): a ring of 3 step images of 2 KiB (lane l's
+// 32 B at 16-B slots 2l + (c ^ ((l >> 3) & 1)), filled by LDS-DMA), each lane's cuts as u16 offsets
+// from its segment start, and their counts.
+constexpr int kRingSlot = 2048;
+constexpr int kWaveLds = 3 * kRingSlot + 64 * kLdsCuts * 2 + 64;
+typedef __attribute__((address_space(3))) u32x4v lds_u4;
+typedef __attribute__((address_space(3))) volatile uint16_t lds_u16v;
+typedef __attribute__((address_space(3))) volatile uint8_t lds_u8v;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+
+__global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
+                                                        int total_waves, int w, int maxlen,
+                                                        uint32_t *__restrict__ spec, int cap,
+                                                        SegMeta *__restrict__ meta, int *__restrict__ rq,
+                                                        int *__restrict__ rq_count, int rq_cap,
+                                                        int *__restrict__ err)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[4 * kWaveLds];
+    const int wv = blockIdx.x * 4 + wave_id();
+    if (wv >= total_waves) return;
+    lds_u8 *wl_lds = (lds_u8 *)s_lds + kWaveLds * wave_id();
+    lds_u16v *vcuts = (lds_u16v *)(wl_lds + 3 * kRingSlot);          // read by the neighbouring lane:
+    lds_u8v *vcnt = (lds_u8v *)(wl_lds + 3 * kRingSlot + 64 * kLdsCuts * 2);   // volatile, never cached
+    int bi = 0;
+    for (int i = 1; i < nblocks; i++)
+        if (blocks[i].wave0 <= wv) bi = i;
+    const BlockDesc bd = blocks[bi];
+    const int l = lane_id();
+    const int wl = wv - bd.wave0;
+    const int nseg = bd.nseg, Ls = bd.seg_len, size = (int)bd.len;
+    const int avail = (int)min(bd.readable, (uint64_t)0x7fffffff);
+    const uint8_t *base = bd.data;
+    const int k = wl * kWaveSegs + l;                 // lane 63: the next wave's first segment
+    const bool exists = k < nseg;
+    const bool real = exists && l < kWaveSegs;
+    const int s = k * Ls;
+    const int e = (real && k + 1 < nseg) ? (k + 1) * Ls : 0x7fffffff;   // the next segment's start
+    const int over_lim = (e == 0x7fffffff) ? 0x7fffffff : e + Ls - 64;  // overrun byte cap (unit start)
+    const int ncap = min(cap, kLdsCuts);
+
+    // loader: per step (one 32-B unit per segment) two LDS-DMA wave-instructions; in instruction i
+    // this lane moves 16 B of segment lane j = 32 i + l/2 (chunk c) into ring slot 2j + (l & 1), as
+    // long as that lane is active and the bytes are readable
+    uint32_t ld_off[2];
+    int ld_last[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+        const int j = 32 * i + (l >> 1);
+        const int kj = wl * kWaveSegs + j;
+        const int c = (l & 1) ^ ((j >> 3) & 1);
+        const int off = ((kj * Ls) & ~15) + 16 * c;
+        ld_off[i] = (uint32_t)off;
+        ld_last[i] = kj < nseg && off + 16 <= avail ? (avail - 16 - off) >> 5 : -1;
     }
-    const uint32_t incl = s_cnt[k];
-    if (k < kMaxSegs) {
-        SegPlan p;
-        p.main_begin = main_begin; p.main_count = main_count; p.over_count = over_count; p.dst = (int)(incl - c);
-        plan[idx] = p;
-    }
-    if (k == 255) {
-        BlockState s;
-        s.n_cuts = (int)incl;
-        s.fail_dst = -1; s.fail_p0 = 0; s.n_chunks = 0;
-        if (bad < nseg - 1 && sync[b * kMaxSegs + bad] == -2) {
-            const SegMeta m = meta[b * kMaxSegs + bad];
-            s.fail_dst = (int)incl;
-            s.fail_p0 = spec[(size_t)(b * kMaxSegs + bad) * spec_cap + m.n_main + m.n_over - 1];
+    const int jsh = l >> 1;
+    const uint32_t rd0 = 32u * (uint32_t)l + 16u * (uint32_t)((l >> 3) & 1);   // this lane's chunk 0 / 1
+    const uint32_t rd1 = 32u * (uint32_t)l + 16u * (uint32_t)(((l >> 3) & 1) ^ 1);
+
+    // chain state (positions relative to the current unit start g)
+    int g = s & ~15;
+    int rb = s + w - g;                                           // window end p + w
+    int rL = min(s + maxlen, size - 1) - g;                       // search limit
+    int rf = (s + maxlen <= size - 1) ? s + maxlen - g : kNegPos; // forced-cut position
+    uint32_t M = (s == 0) ? 0u : 0x80u;                           // biased; 0x80 = the 0 floor (:281)
+    bool pend = false;
+    int pend_lo = 0;
+    Unit pend_u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) pend_u.d[i] = 0;
+    int n = 0, n_main = -1, ptr = 0, sync = kSyncEnd;
+    bool active = exists && g <= size - 1, overflow = false;
+    vcnt[l] = 0;
+
+    // step t's two LDS-DMAs into ring slot t % 3 (vmcnt counted by hand: exactly 2 per step, no other
+    // vector-memory instruction in the loop)
+    auto issue = [&](int t, unsigned long long am) {
+        const unsigned long long amj = am >> jsh;                // bit 32 i = segment lane j_i
+        lds_u8 *slot = wl_lds + kRingSlot * (t % 3);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const bool ok = t <= ld_last[i] && ((amj >> (32 * i)) & 1ull);
+            const uint32_t off = ok ? ld_off[i] + 32u * (uint32_t)t : 0u;     // finished: re-read byte 0
+            __builtin_amdgcn_global_load_lds((const HDRF_GLOBAL void *)(base + off),
+                                             (__attribute__((address_space(3))) void *)(slot + 1024 * i), 16, 0, 0);
         }
+    };
+    auto unit = [&](const Unit &u) {
+        const uint32_t um = unit_max(u);
+        M = (unsigned)(rb - 31) <= (unsigned)(w - 31) ? max(M, um) : M;                 // inside the window
+        if ((unsigned)rb <= 30u && um > M) M = max(M, unit_range_max(u, 0, rb));        // window ends here (rare)
+        const int lo = min(max(rb + 1, 0), 32), hi = min(max(rL, -1), 31);
+        const uint32_t smask = (lo > 31 ? 0u : (~0u << lo)) & (hi < 0 ? 0u : (~0u >> (31 - hi)));
+        const uint32_t V = M == 0 ? ~0u : unit_ge(u, max(M, 1u));
+        const uint32_t F = (unsigned)rf <= 31u ? (1u << rf) : 0u;
+        const uint32_t H = (V | F) & smask;
+        if (H) {
+            const int h = __builtin_ctz(H);
+            const int cut = g + h + 1;
+            const int ci = min(n, ncap - 1);                  // n < ncap always (the caps bound it)
+            overflow |= n >= ncap;
+            vcuts[l * kLdsCuts + ci] = (uint16_t)min(cut - s, 0xffff);
+            vcnt[l] = (uint8_t)(ci + 1);
+            n = ci + 1;
+            if (cut >= e) {                                   // overrun: look for a shared cut
+                if (n_main < 0) n_main = ci;
+                const int sc = vcnt[l + 1];
+                const int rel = cut - e;
+                lds_u16v *sl = vcuts + (l + 1) * kLdsCuts;
+                while (ptr < sc && (int)sl[ptr] < rel) ptr++;
+                if (ptr < sc && (int)sl[ptr] == rel) { sync = (ci - n_main) | (ptr << 16); active = false; }
+                else if (n - n_main >= kLaneOver) { sync = kSyncFail; active = false; }
+            }
+            M = 0x80u;
+            rb = h + 1 + w;
+            rL = min(h + 1 + maxlen, size - 1 - g);
+            rf = (cut + maxlen <= size - 1) ? h + 1 + maxlen : kNegPos;
+        }
+        if ((unsigned)(rb - w - 1) <= 30u) { pend = true; pend_u = u; pend_lo = rb - w; }   // window starts here
+        rb -= 32; rL -= 32; rf -= 32; g += 32;
+        const bool capped = active && g >= over_lim && g <= size - 1;    // overrun byte cap
+        sync = capped ? kSyncFail : sync;
+        active = active && g <= size - 1 && !capped && !overflow;        // data end: no more cuts
+    };
+    unsigned long long am = ballot64(active);
+    issue(0, am);
+    issue(1, am);
+    for (int t = 0;; t++) {
+        if ((t & 7) == 0 && ballot64(pend)) {                 // fold in the window-start units
+            if (pend) { M = max(M, unit_range_max(pend_u, pend_lo, 31)); pend = false; }
+        }
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");     // step t landed (step t + 1 may be in flight)
+        const lds_u8 *slot = wl_lds + kRingSlot * (t % 3);
+        const u32x4v x0 = *(const lds_u4 *)(slot + rd0), x1 = *(const lds_u4 *)(slot + rd1);
+        Unit U;
+        U.d[0] = x0.x; U.d[1] = x0.y; U.d[2] = x0.z; U.d[3] = x0.w;
+        U.d[4] = x1.x; U.d[5] = x1.y; U.d[6] = x1.z; U.d[7] = x1.w;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slot t % 3 read before step t + 3 refills it
+        issue(t + 2, am);
+        if (active) unit(U);
+        am = ballot64(active);
+        if (!ballot64(active && l < kWaveSegs)) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // no LDS-DMA lands after the wave is gone
+    if (overflow && real) atomicOr(err, 64);
+    if (real) {
+        const int G = bd.seg0 + k;
+        uint32_t *list = spec + (size_t)G * cap;
+        for (int i = 0; i < n; i++) list[i] = (uint32_t)s + (uint32_t)vcuts[l * kLdsCuts + i];
+        if (n_main < 0) n_main = n;
+        SegMeta m;
+        m.n_main = n_main; m.n_over = n - n_main; m.sync = sync; m.jmp = 0; m.jj = 0; m.n_ext = 0; m.ext_dst = -1;
+        m.cp_from = 0; m.cp_n = 0; m.cp_dst = 0; m.pad[0] = m.pad[1] = m.pad[2] = 0;
+        meta[G] = m;
+        if (sync == kSyncFail) {
+            const int q = atomicAdd(rq_count, 1);
+            if (q < rq_cap) rq[q] = G;                        // beyond rq_cap: no repair, stitch falls back
+        }
+    }
+}
+
+// 2. repair: one wave per failed boundary k (queued by the lane walk), the exact sequential walker
+//    continues segment k's chain from its last cut.  find: every new cut c is looked up in the list
+//    of the segment m = c / seg_len holding it (m > k); once found at index j, segment k's chain
+//    continues as segment m's from there (kSyncJump, k + jmp = m, jj = j, n_ext cuts walked); no
+//    shared cut within kRepairCuts cuts / kRepairBytes bytes, or the block end: kSyncGiveUp.
+//    emit (after the stitch placed it): the same walk writes its n_ext - 1 cuts before the shared
+//    one into the block's offsets, for repairs on the block's path.
+struct MergeStop {
+    const uint32_t *spec;
+    const SegMeta *meta;
+    int cap, seg0, k, nseg, Ls, lim_cut;
+    int m_cached = -1;
+    uint32_t lane_val = 0xffffffffu;
+    int status = 0, res_m = 0, res_j = 0;             // status 1 merged, 2 gave up
+    __device__ __forceinline__ bool operator()(int cut, int)
+    {
+        if (cut > lim_cut) { status = 2; return true; }
+        const int m = cut / Ls;
+        if (m <= k || m >= nseg) return false;
+        if (m != m_cached) {
+            m_cached = m;
+            const int nm = min(meta[seg0 + m].n_main, 64);
+            lane_val = lane_id() < nm ? spec[(size_t)(seg0 + m) * cap + lane_id()] : 0xffffffffu;
+        }
+        const unsigned long long hit = ballot64(lane_val == (uint32_t)cut);
+        if (hit) { status = 1; res_m = m; res_j = __builtin_ctzll(hit); return true; }
+        return false;
+    }
+    __device__ __forceinline__ int cut_thr() const { return 0; }      // every cut is looked up
+    __device__ __forceinline__ int cnt_thr() const { return 0x7fffffff; }
+};
+
+__global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
+                                                          const int *__restrict__ rq, const int *__restrict__ rq_count,
+                                                          int rq_cap, int w, int maxlen,
+                                                          const uint32_t *__restrict__ spec, int cap,
+                                                          SegMeta *__restrict__ meta, uint32_t *__restrict__ offsets,
+                                                          int cap_blk, int emit)
+{
+    const int nw = gridDim.x * 4;
+    const int cnt = min(*rq_count, rq_cap);
+    for (int q = blockIdx.x * 4 + wave_id(); q < cnt; q += nw) {
+        const int G = __builtin_amdgcn_readfirstlane(rq[q]);
+        int bi = 0;
+        for (int i = 1; i < nblocks; i++)
+            if (blocks[i].seg0 <= G) bi = i;
+        const BlockDesc bd = blocks[bi];
+        const int k = G - bd.seg0;
+        const SegMeta m = meta[G];
+        if (emit && (m.sync != kSyncJump || m.ext_dst < 0 || m.n_ext <= 1)) continue;
+        const int n = m.n_main + m.n_over;
+        const int s_k = k * bd.seg_len;
+        const int p0 = n > 0 ? (int)spec[(size_t)G * cap + n - 1] : s_k;
+        const bool first = n == 0 && s_k == 0;
+        WalkCfg W;
+        W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
+        W.w = w; W.maxlen = maxlen;
+        if (!emit) {
+            CountSink sink;
+            sink.cap = kRepairCuts; sink.cnt = 0; sink.stage = 0;
+            MergeStop st;
+            st.spec = spec; st.meta = meta; st.cap = cap; st.seg0 = bd.seg0; st.k = k; st.nseg = bd.nseg;
+            st.Ls = bd.seg_len; st.lim_cut = p0 + kRepairBytes;
+            (void)walk_chain(W, p0, first, sink, st);
+            if (lane_id() == 0) {
+                if (st.status == 1) {
+                    meta[G].jmp = st.res_m - k;
+                    meta[G].jj = st.res_j;
+                    meta[G].n_ext = sink.cnt;
+                    meta[G].sync = kSyncJump;
+                } else {
+                    meta[G].sync = kSyncGiveUp;
+                }
+            }
+        } else {
+            ListSink sink;
+            sink.out = offsets + (size_t)bi * cap_blk + m.ext_dst; sink.cap = m.n_ext - 1; sink.cnt = 0; sink.stage = 0;
+            NoStop ns;
+            (void)walk_chain(W, p0, first, sink, ns);
+            sink.flush();
+        }
+    }
+}
+
+// 3. stitch: one 1024-thread workgroup per block.  The block's chain is segment 0's list, then,
+//    boundary by boundary, the next segment's list from the shared cut: synced boundaries go to
+//    k + 1 (seg k keeps its overrun cuts [0, i)), repaired ones jump to k + jmp (seg k keeps all
+//    its cuts and the repair's n_ext - 1 cuts; the segments jumped over are off the path); the
+//    path ends at the last segment, at a chain that ran to the block end, or at a failed boundary
+//    (seg k keeps all its cuts and the sequential fallback continues from the last one).  The
+//    nodes that are not "synced to k + 1" are compacted (prefix over the threads' segment runs)
+//    and thread 0 follows the path through them; then each thread sizes its segments' pieces, a
+//    prefix places them and each thread copies its pieces.
+constexpr int kStitchNodes = 4096;       // compacted irregular boundaries per block (more: fallback)
+__global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__restrict__ blocks,
+                                                           const uint32_t *__restrict__ spec, int cap,
+                                                           SegMeta *__restrict__ meta,
+                                                           uint32_t *__restrict__ offsets, int cap_blk,
+                                                           BlockState *__restrict__ bst, int *__restrict__ err)
+{
+    __shared__ uint32_t s_sum[1024];
+    __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes (ascending)
+    __shared__ int s_jx[kStitchNodes];       // on-path jumps: source node, target, shared-cut index
+    __shared__ int s_jm[kStitchNodes];
+    __shared__ int s_jj[kStitchNodes];
+    __shared__ int s_nj, s_term, s_fb;
+    const int b = blockIdx.x;
+    const BlockDesc bd = blocks[b];
+    const int nseg = bd.nseg, t = threadIdx.x;
+    SegMeta *mt = meta + bd.seg0;
+    const int per = (nseg + 1023) / 1024;
+    const int k0 = min(nseg, t * per), k1 = min(nseg, k0 + per);
+    auto scan = [&](uint32_t v) -> uint32_t {           // exclusive prefix over the threads; s_sum[1023] = total
+        s_sum[t] = v;
+        __syncthreads();
+        for (int d = 1; d < 1024; d <<= 1) {
+            const uint32_t x = t >= d ? s_sum[t - d] : 0u;
+            __syncthreads();
+            s_sum[t] += x;
+            __syncthreads();
+        }
+        return s_sum[t] - v;
+    };
+    // (a) compact the irregular boundaries (sync < 0), k < nseg - 1
+    uint32_t nirr = 0;
+    for (int k = k0; k < k1; k++) nirr += (k < nseg - 1 && mt[k].sync < 0);
+    uint32_t pos = scan(nirr);
+    const int tot_irr = (int)s_sum[1023];
+    for (int k = k0; k < k1; k++)
+        if (k < nseg - 1 && mt[k].sync < 0) {
+            if (pos < (uint32_t)kStitchNodes) s_nx[pos] = k;
+            pos++;
+        }
+    __syncthreads();
+    // (b) thread 0 follows the path through the irregular nodes
+    if (t == 0) {
+        const int nnx = min(tot_irr, kStitchNodes);
+        int cur = 0, i = 0, nj = 0, term = nseg - 1, fb = 0;
+        for (;;) {
+            while (i < nnx && s_nx[i] < cur) i++;
+            if (i >= nnx) {
+                if (tot_irr > kStitchNodes) { term = cur; fb = 1; }   // uncompacted nodes ahead: fall back here
+                break;
+            }
+            const int x = s_nx[i];
+            const int sy = mt[x].sync;
+            if (sy == kSyncJump && nj < kStitchNodes) {
+                s_jx[nj] = x; s_jm[nj] = x + mt[x].jmp; s_jj[nj] = mt[x].jj; nj++;
+                cur = x + mt[x].jmp;
+                continue;
+            }
+            term = x;
+            fb = sy != kSyncEnd;
+            break;
+        }
+        s_nj = nj; s_term = term; s_fb = fb;
+    }
+    __syncthreads();
+    const int nj = s_nj, term = s_term;
+    // (c) the piece of every segment on the path
+    auto piece = [&](int k, int &from, int &cnt, int &ext) {
+        from = 0; cnt = 0; ext = -1;
+        if (k > term) return;
+        int lo = 0, hi = nj;                               // last jump with source < k
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_jx[mid] < k) lo = mid + 1; else hi = mid; }
+        const int ji = lo - 1;
+        bool target = false;
+        if (ji >= 0) {
+            if (s_jm[ji] > k) return;                      // jumped over
+            target = s_jm[ji] == k;
+        }
+        const SegMeta m = mt[k];
+        if (k == 0) from = 0;
+        else if (target) from = s_jj[ji];
+        else from = (mt[k - 1].sync >> 16) & 0xffff;
+        if (from > m.n_main) { atomicOr(err, 128); from = m.n_main; }   // never: a shared cut is a main cut
+        cnt = m.n_main - from;
+        if (k == term) cnt += m.n_over;
+        else if (m.sync == kSyncJump) { cnt += m.n_over; ext = cnt; cnt += m.n_ext - 1; }
+        else cnt += m.sync & 0xffff;
+    };
+    uint32_t local = 0;
+    for (int k = k0; k < k1; k++) {
+        int from, cnt, ext;
+        piece(k, from, cnt, ext);
+        local += (uint32_t)cnt;
+    }
+    uint32_t dst = scan(local);
+    const uint32_t total = s_sum[1023];
+    if (total > (uint32_t)cap_blk) {
+        if (t == 0) atomicOr(err, 1);
+        for (int k = k0; k < k1; k++) mt[k].cp_n = 0;
+        return;
+    }
+    for (int k = k0; k < k1; k++) {                        // the plan; lane_copy_kernel moves the cuts
+        int from, cnt, ext;
+        piece(k, from, cnt, ext);
+        if (ext >= 0) mt[k].ext_dst = (int)dst + ext;      // the repair's cuts (emit pass)
+        mt[k].cp_from = from;
+        mt[k].cp_n = ext >= 0 ? ext : cnt;
+        mt[k].cp_dst = b * cap_blk + (int)dst;
+        dst += (uint32_t)cnt;
+    }
+    if (t == 0) {
+        BlockState s;
+        s.n_cuts = (int)total;
+        s.fail_dst = s_fb ? (int)total : -1;
+        s.fail_p0 = 0; s.n_chunks = 0;
         bst[b] = s;
     }
 }
 
-// 3b. copy: one wave per (block, segment): plan piece -> offsets.
-__global__ void __launch_bounds__(256) spec_copy_kernel(const BlockDesc *__restrict__ blocks,
-                                                        const uint32_t *__restrict__ spec, int spec_cap,
-                                                        const SegPlan *__restrict__ plan,
-                                                        uint32_t *__restrict__ offsets, int cap_blk)
+// 3b. copy: 32 lanes per segment move its planned piece of the speculative list into the offsets
+__global__ void __launch_bounds__(256) lane_copy_kernel(const uint32_t *__restrict__ spec, int cap,
+                                                        const SegMeta *__restrict__ meta, int nsegs,
+                                                        uint32_t *__restrict__ offsets)
 {
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * 4 + wave_id();
-    if (k >= blocks[b].nseg) return;
-    const int idx = b * kMaxSegs + k;
-    const SegPlan p = plan[idx];
-    const uint32_t *src = spec + (size_t)idx * spec_cap + p.main_begin;
-    uint32_t *dst = offsets + (size_t)b * cap_blk + p.dst;
-    const int n = p.main_count + p.over_count;
-    for (int i = lane_id(); i < n; i += 64) dst[i] = src[i];
+    const int G = blockIdx.x * 8 + (threadIdx.x >> 5);
+    const int i = threadIdx.x & 31;
+    if (G >= nsegs) return;
+    const int n = meta[G].cp_n;
+    if (i < n) offsets[meta[G].cp_dst + i] = spec[(size_t)G * cap + meta[G].cp_from + i];
 }
 
-// 4. fallback + drop-last/append-size: one wave per block.
+// 4. fallback + drop-last/append-size: one wave per block.  A block whose path ends at a failed
+//    boundary continues with the exact sequential walk from the last proven cut (or from the
+//    block start under the first-chunk rule); then :300-304 — the last detected cut is dropped and
+//    the block size appended.
 __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__restrict__ blocks, int w, int maxlen,
                                                            uint32_t *__restrict__ offsets, int cap_blk,
                                                            BlockState *__restrict__ bst, int *__restrict__ err)
@@ -561,15 +888,16 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
         WalkCfg W;
         W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
         W.w = w; W.maxlen = maxlen;
+        const bool first = s.fail_dst == 0;
+        const int p0 = first ? 0 : (int)off[s.fail_dst - 1];
         ListSink sink;
         sink.out = off + s.fail_dst; sink.cap = cap_blk - s.fail_dst; sink.cnt = 0; sink.stage = 0;
         NoStop nostop;
-        bool ok = walk_chain(W, (int)s.fail_p0, false, sink, nostop);
+        bool ok = walk_chain(W, p0, first, sink, nostop);
         sink.flush();
         if (!ok && lane_id() == 0) atomicOr(err, 1);
         s.n_cuts = s.fail_dst + sink.cnt;
     }
-    // :300-304 — drop the last detected cut, append size
     const int c = s.n_cuts;
     const int n = c > 0 ? c : 1;
     __builtin_amdgcn_s_waitcnt(0);
@@ -582,24 +910,28 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
 
 }  // namespace hdrf
 
-// ---- host-side launchers (called from api.cpp) -------------------------------------------
+// ---- host-side launchers (called from api.hip) -------------------------------------------
 namespace hdrf {
-hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg, int w, int maxlen,
-                           uint32_t *spec, int spec_cap, SegMeta *meta, int32_t *sync, SegPlan *plan,
+int lane_spec_cap(int seg_len, int w) { return seg_len / (w + 2) + 2 + kLaneOver; }
+
+hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int total_waves, int nsegs, int w, int maxlen,
+                           uint32_t *spec, int spec_cap, SegMeta *meta, int *rq, int *rq_count, int rq_cap,
                            BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk)
 {
     mk->mark(st);
-    dim3 g((max_nseg + 3) / 4, nblocks);
-    static const int per_simd = [] { const char *e = getenv("HDRF_WALK_WAVES"); return e ? atoi(e) : 8; }();
-    const int total = nblocks * max_nseg;
-    const int nwg = std::max(1, std::min((total + 3) / 4, per_simd * 1024 / 4));
-    hipLaunchKernelGGL(spec_walk_kernel, dim3(nwg), dim3(256), 0, st, d_blocks, nblocks, max_nseg, w, maxlen, spec,
-                       spec_cap, meta);
+    hipError_t e = hipMemsetAsync(rq_count, 0, sizeof(int), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), 0, st, d_blocks, nblocks, total_waves,
+                       w, maxlen, spec, spec_cap, meta, rq, rq_count, rq_cap, err);
     mk->mark(st);
-    hipLaunchKernelGGL(spec_sync_kernel, g, dim3(256), 0, st, d_blocks, spec, spec_cap, meta, sync);
-    hipLaunchKernelGGL(spec_plan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, spec, spec_cap, meta, sync,
-                       plan, bst);
-    hipLaunchKernelGGL(spec_copy_kernel, g, dim3(256), 0, st, d_blocks, spec, spec_cap, plan, offsets, cap_blk);
+    const int rgrid = 512;                             // 2048 repair waves loop over the queue
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, rq, rq_count, rq_cap, w,
+                       maxlen, spec, spec_cap, meta, offsets, cap_blk, 0);
+    hipLaunchKernelGGL(lane_stitch_kernel, dim3(nblocks), dim3(1024), 0, st, d_blocks, spec, spec_cap, meta, offsets,
+                       cap_blk, bst, err);
+    hipLaunchKernelGGL(lane_copy_kernel, dim3((nsegs + 7) / 8), dim3(256), 0, st, spec, spec_cap, meta, nsegs, offsets);
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, rq, rq_count, rq_cap, w,
+                       maxlen, spec, spec_cap, meta, offsets, cap_blk, 1);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
                        cap_blk, bst, err);
     return hipGetLastError();

@@ -16,8 +16,15 @@ namespace hdrf {
 
 constexpr int kWave = 64;
 constexpr int kMaxBatch = 64;        // one bit per block of the batch in IndexEntry::mask
-constexpr int kMaxSegs = 256;        // speculative chunking segments per block
-constexpr int kOverrun = 64;         // overrun cuts recorded past a segment end (one per lane)
+// Lane walker (chunk.hip): one lane walks one speculative segment of seg_len bytes; a wave holds
+// kWaveSegs segments plus a helper lane that walks the next wave's first segment.
+constexpr int kWaveSegs = 63;
+constexpr int kLaneOver = 8;         // overrun cuts a lane may record past its segment end
+constexpr int kLdsCuts = 30;         // LDS list of every lane (u16 offsets from its segment start)
+constexpr int kRepairCuts = 4096;    // a repair walk gives up after this many cuts ...
+constexpr int kRepairBytes = 2 << 20;  // ... or this many bytes past its start
+constexpr int kSegMinWin = 4;        // seg_len bounds, in units of window + 2 (702 B)
+constexpr int kSegMaxWin = 20;        // seg_len / 702 + 2 + kLaneOver <= kLdsCuts
 constexpr uint64_t kEmptyTag = 0;
 
 // Index entry: 64 B.  tag = first 8 digest bytes (0 remapped to 1 with flag bit 31 of `batch`);
@@ -42,31 +49,37 @@ struct BlockDesc {
     const uint8_t *data;
     uint64_t len;
     uint64_t readable;       // bytes readable from data (>= len)
-    int32_t nseg;
+    int32_t nseg;            // speculative lane segments [k*seg_len, min((k+1)*seg_len, len))
     int32_t seg_len;         // multiple of 702 (window + 2) so all-zero data syncs at once
+    int32_t seg0;            // the block's first segment in the batch's flat spec / meta arrays
+    int32_t wave0;           // the block's first lane-walker wave
 };
 
-// Speculative segment walk result.
+// Speculative segment walk result (one per lane segment).
+constexpr int kSyncEnd = -1;         // the chain ran to the block end without meeting the next one
+constexpr int kSyncFail = -2;        // no shared cut within the overrun caps (no repair record)
+constexpr int kSyncJump = -3;        // repaired: the chain continued and met segment k + jmp at its cut jj
+constexpr int kSyncGiveUp = -4;      // repair found no shared cut within kRepairCuts / kRepairBytes
 struct SegMeta {
     int32_t n_main;          // cuts < next segment start
-    int32_t n_over;          // cuts >= next segment start (<= kOverrun)
-    int32_t ended;           // chain ended at block end
-    int32_t pad;
-};
-
-// Stitch plan per segment.
-struct SegPlan {
-    int32_t main_begin;      // first main index taken
-    int32_t main_count;
-    int32_t over_count;      // overrun entries taken
-    int32_t dst;             // destination index in the block's offsets
+    int32_t n_over;          // cuts >= next segment start (<= kLaneOver)
+    int32_t sync;            // i | j << 16: overrun cut i == the next segment's cut j; or a kSync* status
+    int32_t jmp;             // kSyncJump: target segment - this segment
+    int32_t jj;              // kSyncJump: index of the shared cut in the target's list
+    int32_t n_ext;           // kSyncJump: cuts of the repair walk, the shared cut included
+    int32_t ext_dst;         // the repair's cuts go to offsets[ext_dst..] (-1: not on the block's path)
+    int32_t cp_from;         // stitch plan: copy list[cp_from, cp_from + cp_n) to the batch's offsets
+    int32_t cp_n;            //   array at cp_dst (absolute: block * cap_blk + position)
+    int32_t cp_dst;
+    int32_t pad[3];
 };
 
 // Per-block state after chunking/stitching.
 struct BlockState {
     int32_t n_cuts;          // true boundaries before the drop-last rule (stitched + fallback)
-    int32_t fail_dst;        // fallback writes from here (-1 = none)
-    uint32_t fail_p0;        // last true boundary before fallback
+    int32_t fail_dst;        // fallback writes from here (-1 = none); it starts at offsets[fail_dst - 1]
+                             // (or at the block start, first-chunk rule, when fail_dst == 0)
+    uint32_t fail_p0;        // unused (kept for the layout)
     int32_t n_chunks;        // final chunk count (offsets list length)
 };
 

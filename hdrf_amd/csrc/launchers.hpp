@@ -27,8 +27,10 @@ struct StoreParams {
     int place_lds = 0;         // dynamic LDS per place workgroup (occupancy throttle, 0 = none)
 };
 
-hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int max_nseg, int w, int maxlen,
-                           uint32_t *spec, int spec_cap, SegMeta *meta, int32_t *sync, SegPlan *plan,
+// chunking: lane walk (total_waves waves over the batch's segments) -> stitch -> fallback
+int lane_spec_cap(int seg_len, int w);
+hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int total_waves, int nsegs, int w, int maxlen,
+                           uint32_t *spec, int spec_cap, SegMeta *meta, int *rq, int *rq_count, int rq_cap,
                            BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
