@@ -45,6 +45,9 @@ struct Slot {
     BlockDesc *d_blocks = nullptr;
     uint32_t *d_spec = nullptr;
     SegMeta *d_meta = nullptr;
+    uint8_t *d_gm = nullptr;                  // granule maxima [B][gstride] (chunking pass 1)
+    int gstride = 0;
+    int64_t max_len = 0;                      // longest block of the batch in this slot
     int *d_rq = nullptr, *d_rq_count = nullptr;   // failed speculative boundaries (repair queue), meta_cap entries
     size_t spec_words = 0, meta_cap = 0;      // capacity of d_spec (u32) / d_meta (segments), grown on demand
     int total_waves = 0, total_segs = 0, spec_cap = 0;   // lane walk of the batch in this slot
@@ -82,7 +85,7 @@ struct Slot {
     hipEvent_t copy_done = nullptr;          // host path: the batch's H2D copies landed
     uint8_t *d_hstage = nullptr;              // host path: device copies of the batch's blocks
     uint64_t hstage_stride = 0;
-    hipEvent_t evW[3] = {}, evA[3] = {}, evB[9] = {};   // stage markers (timing)
+    hipEvent_t evW[4] = {}, evA[3] = {}, evB[10] = {};   // stage markers (timing)
 };
 
 }  // namespace
@@ -228,7 +231,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
 
 static void free_slot(Slot &S)
 {
-    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
+    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
                    S.d_pre, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
                    S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err};
     for (void *p : dev)
@@ -281,7 +284,9 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
                          (c.window + 2);
     S.meta_cap = (size_t)B * (size_t)(c.max_block_bytes / seg_len0 + 2);
     S.spec_words = S.meta_cap * (size_t)lane_spec_cap(seg_len0, c.window);
+    S.gstride = (int)(((c.max_block_bytes + 15) / 16 + 1024 + 255) & ~(int64_t)255);
     if ((rc = dalloc(ctx, &S.d_blocks, B)) || (rc = dalloc(ctx, &S.d_spec, S.spec_words)) ||
+        (rc = dalloc(ctx, &S.d_gm, (size_t)B * S.gstride)) ||
         (rc = dalloc(ctx, &S.d_meta, S.meta_cap)) || (rc = dalloc(ctx, &S.d_rq, S.meta_cap)) ||
         (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
         (rc = dalloc(ctx, &S.d_off, nchunk)) || (rc = dalloc(ctx, &S.d_dig, nchunk * ctx->HW)) ||
@@ -494,13 +499,15 @@ static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t
     if (nblocks < 1 || nblocks > ctx->max_batch || !dev_data || !len || !readable)
         return set_err(ctx, HDRF_E_INVAL, "bad batch arguments");
     const hdrf_cfg &c = ctx->cfg;
-    int64_t total = 0;
+    int64_t total = 0, max_len = 0;
     for (int b = 0; b < nblocks; b++) {
         if ((int64_t)len[b] > c.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
         if (readable[b] < len[b] + kSlack) return set_err(ctx, HDRF_E_INVAL, "readable must be >= len + 64");
         if (((uintptr_t)dev_data[b] & 15) != 0) return set_err(ctx, HDRF_E_INVAL, "block data must be 16-B aligned");
         total += (int64_t)len[b];
+        max_len = std::max(max_len, (int64_t)len[b]);
     }
+    S.max_len = max_len;
     const int unit = c.window + 2;
     int wins = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / unit)));
     while (wins > 6 && total / ((int64_t)wins * unit * kWaveSegs) < 1024) wins--;
@@ -581,8 +588,8 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, W));
     Marker mw;
     mw.ev = ctx->timing ? S.evW : nullptr;
-    HIPCK(launch_chunking(S.d_blocks, nblocks, S.total_waves, S.total_segs, c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta,
-                          S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, W, &mw));
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.total_waves, S.total_segs, S.d_gm, S.gstride, c.window,
+                          c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, W, &mw));
     mw.mark(W);
     HIPCK(hipEventRecord(S.walk_done, W));
     // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig)
@@ -673,7 +680,8 @@ static int complete_slot(hdrf_ctx *ctx, int si, bool timed)
     Slot &S = ctx->sl[si];
     const int nblocks = S.nblocks;
     if (ctx->timing && timed) {
-        for (int i = 0; i < 2; i++) ctx->stage_ms[i] += elapsed(S.evW[i], S.evW[i + 1]);
+        ctx->stage_ms[11] += elapsed(S.evW[0], S.evW[1]);
+        for (int i = 0; i < 2; i++) ctx->stage_ms[i] += elapsed(S.evW[i + 1], S.evW[i + 2]);
         for (int i = 0; i < 2; i++) ctx->stage_ms[2 + i] += elapsed(S.evA[i], S.evA[i + 1]);
         for (int i = 0; i < 6; i++) ctx->stage_ms[4 + i] += elapsed(S.evB[i], S.evB[i + 1]);
         ctx->stage_ms[10] += elapsed(S.evB[7], S.evB[8]);
@@ -1193,9 +1201,9 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     hipStream_t st = ctx->st;
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
     Marker mk;
-    mk.ev = ctx->timing ? S.evB : nullptr;             // 8 markers: walk .. slow+decide, end
-    HIPCK(launch_chunking(S.d_blocks, nblocks, S.total_waves, S.total_segs, c.window, c.max_chunk, S.d_spec, S.spec_cap,
-                          S.d_meta, S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, st,
+    mk.ev = ctx->timing ? S.evB : nullptr;             // 9 markers: gmax, walk .. slow+decide, end
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.total_waves, S.total_segs, S.d_gm, S.gstride, c.window,
+                          c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, st,
                           &mk));
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
@@ -1233,7 +1241,9 @@ extern "C" int hdrf_gx_front_wait(hdrf_ctx *ctx, int64_t *send_counts)
     HIPCK(hipStreamSynchronize(st));
     ctx->gx_nfwait++;
     if (ctx->timing)
-        for (int i = 0; i < 7; i++) ctx->stage_ms[i] += elapsed(S.evB[i], S.evB[i + 1]);
+        ctx->stage_ms[11] += elapsed(S.evB[0], S.evB[1]);
+    if (ctx->timing)
+        for (int i = 0; i < 7; i++) ctx->stage_ms[i] += elapsed(S.evB[i + 1], S.evB[i + 2]);
     if (herr) {
         HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
         HIPCK(hipStreamSynchronize(st));

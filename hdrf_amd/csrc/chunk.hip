@@ -409,108 +409,172 @@ __device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, 
 
 
 // ------------------------------------------------------------------------------------------
-// 1. lane walk (the speculative pass).  Every block is cut into segments of seg_len bytes (a
-//    multiple of 702); lane l of a wave walks the chain from the start of segment k = 63*wl + l
-//    as if a cut were there, one 32-B unit at a time, entirely in VALU:
-//      window part   M = max(M, unit max) while the unit lies inside [p, p+700]; the unit
-//                    holding p (a cut, or the segment start) is folded in later from a saved
-//                    copy (every 8 units, always before the window can end); the unit holding
-//                    p+700 needs its exact prefix only when its max exceeds M
-//      search part   the 32-bit mask of bytes >= M (SWAR carry test + v_dot4 bit gather), cut to
-//                    [p+701, min(p+maxlen, size-1)], plus the forced position p+maxlen; the first
-//                    set bit j gives the cut j+1 (DN/DataDeduplicator.java:276-294)
-//    Its cuts go to an LDS list (u16 offsets from the segment start; written to the segment's
-//    global list when the lane stops).  Past its segment end (overrun) a lane compares each cut
-//    with the next lane's list (the next segment's chain, walked concurrently and seg_len bytes
-//    ahead): the first shared cut proves the chains equal from there on, the lane records (i, j)
-//    and stops.  Lane 63 walks the NEXT wave's first segment (a helper: LDS only), so every
-//    boundary is settled inside one wave.  A lane that meets no shared cut within kLaneOver cuts
-//    or ~seg_len bytes reports kSyncFail and queues its boundary for the repair pass.
-//    Bytes move HBM -> VGPR -> LDS in 4 KiB steps (each lane fetches 16 B of four segments, so a
-//    wave-instruction reads 16 x 64 contiguous bytes), prefetched two steps ahead, and every lane
-//    reads its own 64 B back with conflict-free ds_read_b128 (XOR-swizzled 16-B slots).
+// 1a. granule maxima: gm[b][g] = max of the biased bytes of granule g (bytes [16g, 16g + 16)) of
+//     block b.  One coalesced streaming pass (16 B in, 1 B out per granule) — the only pass of the
+//     speculative walk that reads every byte; it is HBM-bound.
+constexpr int kGmPerWg = 4096;           // granules per workgroup (64 KiB of data, 16 per thread)
 
-// A unit is 32 bytes (two granules, 8 dwords) of one lane's segment.  Biasing (XOR 0x80, signed
-// order == unsigned order) is folded into the masks below.
-struct Unit {
-    uint32_t d[8];
-};
-
-// max over the 32 biased bytes: even bytes and odd bytes as u16 lanes (odd ones scaled by 256,
-// which keeps their order), v_pk_max_u16 trees, then the two halves
-__device__ __forceinline__ uint32_t unit_max(const Unit &u)
+__global__ void __launch_bounds__(256) gmax_kernel(const BlockDesc *__restrict__ blocks, uint8_t *__restrict__ gm,
+                                                   int gstride)
 {
+    const BlockDesc bd = blocks[blockIdx.y];
+    const int64_t ngran = (int64_t)((bd.len + 15) >> 4);
+    const int64_t g0 = (int64_t)blockIdx.x * kGmPerWg;
+    if (g0 >= ngran) return;
+    const uint8_t *base = bd.data;
+    HDRF_GLOBAL uint8_t *out = gptr_w<uint8_t>(gm + (size_t)blockIdx.y * gstride);
+    const int t = threadIdx.x;
+    uint4 v[16];
+    if ((g0 + kGmPerWg) * 16 <= (int64_t)bd.readable) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = ld16(base + (g0 + 256 * i + t) * 16);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int64_t g = g0 + 256 * i + t;
+            v[i] = g < ngran ? load16_guard(base, g * 16, (int64_t)bd.readable) : make_uint4(0, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const int64_t g = g0 + 256 * i + t;
+        if (g < ngran) out[g] = (uint8_t)gmax16(bias(v[i]));
+    }
+}
+
+// 1b. lane walk (the speculative pass).  Every block is cut into segments of seg_len bytes (a
+//     multiple of 702); lane l of a wave walks the chain from the start of segment k = 63*wl + l as
+//     if a cut were there, one CHUNK per loop iteration, in VALU, from the granule maxima:
+//       window   M(p) = max over the granule maxima of the 42-44 granules inside [p, p+700] plus
+//                the exact partial maxima of the two edge granules (raw 16-B loads)
+//       search   the first granule after p+700 whose maximum is >= M (SWAR carry test on the
+//                maxima, v_dot4 bit gather, 64-bit bit scan), then its first byte >= M (raw load);
+//                none up to min(p+maxlen, size-1): the forced cut p+maxlen
+//                (DN/DataDeduplicator.java:276-294)
+//     A lane's working set per chunk is 128 granule maxima (8 x 16-B loads, 2 KiB of data) and two
+//     or three raw granules, so a chunk costs two dependent memory round trips and ~400 VALU instead
+//     of re-reading its ~950 bytes.  Its cuts go to an LDS list (u16 offsets from the segment start;
+//     written to the segment's global list when the lane stops).  Past its segment end (overrun) a
+//     lane compares each cut with the next lane's list (the next segment's chain, walked
+//     concurrently and seg_len bytes ahead): the first shared cut proves the chains equal from there
+//     on, the lane records (i, j) and stops.  Lane 63 walks the NEXT wave's first segment (a helper:
+//     LDS only), so every boundary is settled inside one wave.  A lane that meets no shared cut
+//     within kLaneOver cuts or ~seg_len bytes reports kSyncFail and queues its boundary for the
+//     repair pass.
+constexpr int kGmWin = 32;               // dwords of granule maxima a lane holds (128 granules)
+
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(as_us2(a), as_us2(b)));
+}
+// bytes [lo, hi) of a dword (lo, hi clamped to [0, 4])
+__device__ __forceinline__ uint32_t keep_bytes(int lo, int hi)
+{
+    lo = min(max(lo, 0), 4);
+    hi = min(max(hi, 0), 4);
+    return (uint32_t)(~0ull << (8 * lo)) & (uint32_t)((1ull << (8 * hi)) - 1ull);
+}
+struct BMax {                             // running max of biased bytes: even / odd bytes as u16 lanes
     uint32_t e = 0, o = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        e = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(as_us2(e), as_us2((u.d[i] ^ 0x80808080u) & 0x00ff00ffu)));
-        o = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(as_us2(o), as_us2((u.d[i] ^ 0x80808080u) & 0xff00ff00u)));
+    __device__ __forceinline__ void add(uint32_t x)
+    {
+        e = pk_max(e, x & 0x00ff00ffu);
+        o = pk_max(o, x & 0xff00ff00u);
     }
-    const uint32_t m = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(as_us2(e), as_us2(o >> 8)));
-    return max(m & 0xffffu, m >> 16);
-}
-
-// max over the biased bytes whose unit index is in [lo, hi] (0 <= lo, hi <= 31)
-__device__ __forceinline__ uint32_t unit_range_max(const Unit &u, int lo, int hi)
+    __device__ __forceinline__ uint32_t get() const
+    {
+        const uint32_t m = pk_max(e, o >> 8);
+        return max(m & 0xffffu, m >> 16);
+    }
+};
+// biased max over bytes [lo, hi] of a raw granule
+__device__ __forceinline__ uint32_t gran_max(uint4 v, int lo, int hi)
 {
-    Unit m;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const int a = min(max(lo - 4 * i, 0), 4), b = min(max(hi - 4 * i + 1, 0), 4);   // keep bytes [a, b)
-        const uint32_t keep = (a >= b) ? 0u : ((b == 4 ? ~0u : ((1u << (8 * b)) - 1u)) & (~0u << (8 * a)));
-        m.d[i] = ((u.d[i] ^ 0x80808080u) & keep) ^ 0x80808080u;     // dropped bytes read as biased 0
-    }
-    return unit_max(m);
+    BMax m;
+    m.add((v.x ^ 0x80808080u) & keep_bytes(lo, hi + 1));
+    m.add((v.y ^ 0x80808080u) & keep_bytes(lo - 4, hi - 3));
+    m.add((v.z ^ 0x80808080u) & keep_bytes(lo - 8, hi - 7));
+    m.add((v.w ^ 0x80808080u) & keep_bytes(lo - 12, hi - 11));
+    return m.get();
 }
-
-// 32-bit mask of the biased bytes >= m (1 <= m <= 255): SWAR carry-out of byte + (256 - m), the
-// bit-7 flags gathered with v_dot4_u32_u8 (weights 1..128 per dword pair)
-// bit 7 of each byte of raw dword d where the biased byte (d ^ 0x80) >= m: the carry out of the
-// byte sum (d ^ 0x80) + (256 - m) = maj(NOT d7, C7, s7) with s = low-7-bit sum; 4 VALU (and, add,
-// bitop3, and)
+// bit 7 of each byte of raw dword d whose biased value (d ^ 0x80) is >= m, with C = (256 - m) in
+// every byte and Cm = C & 0x7f7f7f7f: the carry out of the byte sum = maj(NOT d7, C7, s7), s the
+// low-7-bit sum (and, add, bitop3, and)
 __device__ __forceinline__ uint32_t ge_flags(uint32_t d, uint32_t C, uint32_t Cm)
 {
     const uint32_t s = (d & 0x7f7f7f7fu) + Cm;
     return __builtin_amdgcn_bitop3_b32(d, C, s, 0x8e) & 0x80808080u;   // 0x8e: maj(NOT d, C, s)
 }
-__device__ __forceinline__ uint32_t unit_ge(const Unit &u, uint32_t m)
+// the same for a dword of already biased bytes: maj(x7, C7, s7)
+__device__ __forceinline__ uint32_t ge_flags_b(uint32_t x, uint32_t C, uint32_t Cm)
 {
-    const uint32_t C = __builtin_amdgcn_perm(256u - m, 256u - m, 0u), Cm = C & 0x7f7f7f7fu;
-    uint32_t x[4];
+    const uint32_t s = (x & 0x7f7f7f7fu) + Cm;
+    return __builtin_amdgcn_bitop3_b32(x, C, s, 0xe8) & 0x80808080u;   // 0xe8: maj(x, C, s)
+}
+// gather the bit-7 flags of four dwords into 16 bits (v_dot4_u32_u8, weights 1..128 per pair)
+__device__ __forceinline__ uint32_t gather16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3)
+{
+    const uint32_t lo = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(f3, 0x80402010u, __builtin_amdgcn_udot4(f2, 0x08040201u, 0u, false), false);
+    return (lo | (hi << 8)) >> 7;
+}
+// 16-bit mask of the bytes of a raw granule whose biased value is >= m (m >= 1)
+__device__ __forceinline__ uint32_t gran_ge(uint4 v, uint32_t C, uint32_t Cm)
+{
+    return gather16(ge_flags(v.x, C, Cm), ge_flags(v.y, C, Cm), ge_flags(v.z, C, Cm), ge_flags(v.w, C, Cm));
+}
+// 64-bit mask of the granule maxima d[16 h .. 16 h + 16) that are >= m
+__device__ __forceinline__ unsigned long long gm_ge64(const uint32_t (&d)[kGmWin], int h, uint32_t C, uint32_t Cm)
+{
+    uint32_t q[4];
 #pragma unroll
-    for (int p = 0; p < 4; p++) {
-        const uint32_t f0 = ge_flags(u.d[2 * p], C, Cm), f1 = ge_flags(u.d[2 * p + 1], C, Cm);
-        x[p] = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
+    for (int i = 0; i < 4; i++) {
+        const int o = 16 * h + 4 * i;
+        q[i] = gather16(ge_flags_b(d[o], C, Cm), ge_flags_b(d[o + 1], C, Cm), ge_flags_b(d[o + 2], C, Cm),
+                        ge_flags_b(d[o + 3], C, Cm));
     }
-    return (x[0] >> 7) | (x[1] << 1) | (x[2] << 9) | (x[3] << 17);
+    return (unsigned long long)(q[0] | (q[1] << 16)) | ((unsigned long long)(q[2] | (q[3] << 16)) << 32);
+}
+__device__ __forceinline__ unsigned long long bits_from(int x)
+{
+    return x <= 0 ? ~0ull : (x >= 64 ? 0ull : (~0ull << x));
+}
+__device__ __forceinline__ unsigned long long bits_to(int y)     // bits 0..y
+{
+    return y < 0 ? 0ull : (y >= 63 ? ~0ull : ((2ull << y) - 1ull));
+}
+__device__ __forceinline__ uint32_t range16(int lo, int hi)      // bits lo..hi of 16
+{
+    const uint32_t a = lo >= 16 ? 0u : (0xffffu << max(lo, 0));
+    const uint32_t b = hi < 0 ? 0u : (hi >= 15 ? 0xffffu : ((2u << hi) - 1u));
+    return a & b;
+}
+__device__ __forceinline__ void load_gm(uint32_t (&d)[kGmWin], const uint8_t *p)
+{
+#pragma unroll
+    for (int i = 0; i < kGmWin / 4; i++) {
+        const uint4 v = ld16(p + 16 * i);
+        d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+    }
 }
 
-constexpr int kNegPos = -(1 << 30);      // "no forced cut possible" relative position
-
-// LDS of one wave (one array for the whole workgroup: a second __shared__ object beside LDS-DMA
-// staging makes hipcc drain vmcnt before LDS reads): a ring of 3 step images of 2 KiB (lane l's
-// 32 B at 16-B slots 2l + (c ^ ((l >> 3) & 1)), filled by LDS-DMA), each lane's cuts as u16 offsets
-// from its segment start, and their counts.
-constexpr int kRingSlot = 2048;
-constexpr int kWaveLds = 3 * kRingSlot + 64 * kLdsCuts * 2 + 64;
-typedef __attribute__((address_space(3))) u32x4v lds_u4;
 typedef __attribute__((address_space(3))) volatile uint16_t lds_u16v;
 typedef __attribute__((address_space(3))) volatile uint8_t lds_u8v;
-typedef __attribute__((address_space(3))) uint8_t lds_u8;
 
 __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
-                                                        int total_waves, int w, int maxlen,
+                                                        int total_waves, const uint8_t *__restrict__ gm,
+                                                        int gstride, int w, int maxlen,
                                                         uint32_t *__restrict__ spec, int cap,
                                                         SegMeta *__restrict__ meta, int *__restrict__ rq,
                                                         int *__restrict__ rq_count, int rq_cap,
                                                         int *__restrict__ err)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t s_lds[4 * kWaveLds];
+    __shared__ uint16_t s_cuts[4][64 * kLdsCuts];
+    __shared__ uint8_t s_cnt[4][64];
     const int wv = blockIdx.x * 4 + wave_id();
     if (wv >= total_waves) return;
-    lds_u8 *wl_lds = (lds_u8 *)s_lds + kWaveLds * wave_id();
-    lds_u16v *vcuts = (lds_u16v *)(wl_lds + 3 * kRingSlot);          // read by the neighbouring lane:
-    lds_u8v *vcnt = (lds_u8v *)(wl_lds + 3 * kRingSlot + 64 * kLdsCuts * 2);   // volatile, never cached
+    lds_u16v *vcuts = (lds_u16v *)s_cuts[wave_id()];      // read by the neighbouring lane:
+    lds_u8v *vcnt = (lds_u8v *)s_cnt[wave_id()];          // volatile, never cached
     int bi = 0;
     for (int i = 1; i < nblocks; i++)
         if (blocks[i].wave0 <= wv) bi = i;
@@ -518,119 +582,98 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
     const int l = lane_id();
     const int wl = wv - bd.wave0;
     const int nseg = bd.nseg, Ls = bd.seg_len, size = (int)bd.len;
-    const int avail = (int)min(bd.readable, (uint64_t)0x7fffffff);
-    const uint8_t *base = bd.data;
-    const int k = wl * kWaveSegs + l;                 // lane 63: the next wave's first segment
+    const uint8_t *base = bd.data;                        // raw loads stay < size + 16 <= readable
+    const uint8_t *gmb = gm + (size_t)bi * gstride;
+    const int k = wl * kWaveSegs + l;                     // lane 63: the next wave's first segment
     const bool exists = k < nseg;
     const bool real = exists && l < kWaveSegs;
     const int s = k * Ls;
-    const int e = (real && k + 1 < nseg) ? (k + 1) * Ls : 0x7fffffff;   // the next segment's start
-    const int over_lim = (e == 0x7fffffff) ? 0x7fffffff : e + Ls - 64;  // overrun byte cap (unit start)
+    const bool has_next = exists && k + 1 < nseg;
+    const int e = (real && has_next) ? (k + 1) * Ls : 0x7fffffff;     // overrun (sync) threshold
+    const int over_lim = has_next ? (k + 1) * Ls + Ls - 64 : 0x7fffffff;   // byte cap (helper too)
     const int ncap = min(cap, kLdsCuts);
 
-    // loader: per step (one 32-B unit per segment) two LDS-DMA wave-instructions; in instruction i
-    // this lane moves 16 B of segment lane j = 32 i + l/2 (chunk c) into ring slot 2j + (l & 1), as
-    // long as that lane is active and the bytes are readable
-    uint32_t ld_off[2];
-    int ld_last[2];
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const int j = 32 * i + (l >> 1);
-        const int kj = wl * kWaveSegs + j;
-        const int c = (l & 1) ^ ((j >> 3) & 1);
-        const int off = ((kj * Ls) & ~15) + 16 * c;
-        ld_off[i] = (uint32_t)off;
-        ld_last[i] = kj < nseg && off + 16 <= avail ? (avail - 16 - off) >> 5 : -1;
-    }
-    const int jsh = l >> 1;
-    const uint32_t rd0 = 32u * (uint32_t)l + 16u * (uint32_t)((l >> 3) & 1);   // this lane's chunk 0 / 1
-    const uint32_t rd1 = 32u * (uint32_t)l + 16u * (uint32_t)(((l >> 3) & 1) ^ 1);
-
-    // chain state (positions relative to the current unit start g)
-    int g = s & ~15;
-    int rb = s + w - g;                                           // window end p + w
-    int rL = min(s + maxlen, size - 1) - g;                       // search limit
-    int rf = (s + maxlen <= size - 1) ? s + maxlen - g : kNegPos; // forced-cut position
-    uint32_t M = (s == 0) ? 0u : 0x80u;                           // biased; 0x80 = the 0 floor (:281)
-    bool pend = false;
-    int pend_lo = 0;
-    Unit pend_u;
-#pragma unroll
-    for (int i = 0; i < 8; i++) pend_u.d[i] = 0;
+    int p = s;
+    bool first = s == 0;                                  // the block's first chunk: no 0 floor (:281)
     int n = 0, n_main = -1, ptr = 0, sync = kSyncEnd;
-    bool active = exists && g <= size - 1, overflow = false;
+    bool active = exists, overflow = false;
     vcnt[l] = 0;
-
-    // step t's two LDS-DMAs into ring slot t % 3 (vmcnt counted by hand: exactly 2 per step, no other
-    // vector-memory instruction in the loop)
-    auto issue = [&](int t, unsigned long long am) {
-        const unsigned long long amj = am >> jsh;                // bit 32 i = segment lane j_i
-        lds_u8 *slot = wl_lds + kRingSlot * (t % 3);
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const bool ok = t <= ld_last[i] && ((amj >> (32 * i)) & 1ull);
-            const uint32_t off = ok ? ld_off[i] + 32u * (uint32_t)t : 0u;     // finished: re-read byte 0
-            __builtin_amdgcn_global_load_lds((const HDRF_GLOBAL void *)(base + off),
-                                             (__attribute__((address_space(3))) void *)(slot + 1024 * i), 16, 0, 0);
-        }
-    };
-    auto unit = [&](const Unit &u) {
-        const uint32_t um = unit_max(u);
-        M = (unsigned)(rb - 31) <= (unsigned)(w - 31) ? max(M, um) : M;                 // inside the window
-        if ((unsigned)rb <= 30u && um > M) M = max(M, unit_range_max(u, 0, rb));        // window ends here (rare)
-        const int lo = min(max(rb + 1, 0), 32), hi = min(max(rL, -1), 31);
-        const uint32_t smask = (lo > 31 ? 0u : (~0u << lo)) & (hi < 0 ? 0u : (~0u >> (31 - hi)));
-        const uint32_t V = M == 0 ? ~0u : unit_ge(u, max(M, 1u));
-        const uint32_t F = (unsigned)rf <= 31u ? (1u << rf) : 0u;
-        const uint32_t H = (V | F) & smask;
-        if (H) {
-            const int h = __builtin_ctz(H);
-            const int cut = g + h + 1;
-            const int ci = min(n, ncap - 1);                  // n < ncap always (the caps bound it)
-            overflow |= n >= ncap;
-            vcuts[l * kLdsCuts + ci] = (uint16_t)min(cut - s, 0xffff);
-            vcnt[l] = (uint8_t)(ci + 1);
-            n = ci + 1;
-            if (cut >= e) {                                   // overrun: look for a shared cut
-                if (n_main < 0) n_main = ci;
-                const int sc = vcnt[l + 1];
-                const int rel = cut - e;
-                lds_u16v *sl = vcuts + (l + 1) * kLdsCuts;
-                while (ptr < sc && (int)sl[ptr] < rel) ptr++;
-                if (ptr < sc && (int)sl[ptr] == rel) { sync = (ci - n_main) | (ptr << 16); active = false; }
-                else if (n - n_main >= kLaneOver) { sync = kSyncFail; active = false; }
-            }
-            M = 0x80u;
-            rb = h + 1 + w;
-            rL = min(h + 1 + maxlen, size - 1 - g);
-            rf = (cut + maxlen <= size - 1) ? h + 1 + maxlen : kNegPos;
-        }
-        if ((unsigned)(rb - w - 1) <= 30u) { pend = true; pend_u = u; pend_lo = rb - w; }   // window starts here
-        rb -= 32; rL -= 32; rf -= 32; g += 32;
-        const bool capped = active && g >= over_lim && g <= size - 1;    // overrun byte cap
-        sync = capped ? kSyncFail : sync;
-        active = active && g <= size - 1 && !capped && !overflow;        // data end: no more cuts
-    };
-    unsigned long long am = ballot64(active);
-    issue(0, am);
-    issue(1, am);
-    for (int t = 0;; t++) {
-        if ((t & 7) == 0 && ballot64(pend)) {                 // fold in the window-start units
-            if (pend) { M = max(M, unit_range_max(pend_u, pend_lo, 31)); pend = false; }
-        }
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");     // step t landed (step t + 1 may be in flight)
-        const lds_u8 *slot = wl_lds + kRingSlot * (t % 3);
-        const u32x4v x0 = *(const lds_u4 *)(slot + rd0), x1 = *(const lds_u4 *)(slot + rd1);
-        Unit U;
-        U.d[0] = x0.x; U.d[1] = x0.y; U.d[2] = x0.z; U.d[3] = x0.w;
-        U.d[4] = x1.x; U.d[5] = x1.y; U.d[6] = x1.z; U.d[7] = x1.w;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slot t % 3 read before step t + 3 refills it
-        issue(t + 2, am);
-        if (active) unit(U);
-        am = ballot64(active);
+    uint32_t d[kGmWin];
+    for (;;) {
         if (!ballot64(active && l < kWaveSegs)) break;
+        if (!active) continue;
+        const int wend = p + w;
+        if (wend > size - 1) { active = false; continue; }     // window incomplete: no more cuts
+        const int lim = min(p + maxlen, size - 1);
+        const int G0 = p >> 4, G1 = wend >> 4;
+        int W0 = G0 & ~3;
+        load_gm(d, gmb + W0);
+        const uint4 r0 = ld16(base + 16 * G0), r1 = ld16(base + 16 * G1);
+        // M(p): granules G0+1 .. G1-1 are whole (bytes [a, b] of d, 1 <= a <= 4, 42 <= b <= 46)
+        const int a = G0 + 1 - W0, b = G1 - 1 - W0;
+        BMax mx;
+        mx.add(d[0] & keep_bytes(a, b + 1));
+#pragma unroll
+        for (int i = 1; i < 10; i++) mx.add(d[i]);
+        mx.add(d[10] & keep_bytes(a - 40, b - 39));
+        mx.add(d[11] & keep_bytes(a - 44, b - 43));
+        uint32_t M = max(mx.get(), max(gran_max(r0, p & 15, 15), gran_max(r1, 0, wend & 15)));
+        if (!first) M = max(M, 0x80u);                    // mValue reset to 0 after a cut (:281)
+        int j = -1;
+        bool capped = false;
+        if (M == 0) {
+            j = wend + 1 <= lim ? wend + 1 : -1;          // every byte qualifies
+        } else {
+            const uint32_t C = __builtin_amdgcn_perm(256u - M, 256u - M, 0u), Cm = C & 0x7f7f7f7fu;
+            const uint32_t h1 = gran_ge(r1, C, Cm) & range16((wend & 15) + 1, lim - 16 * G1);
+            if (h1) {
+                j = 16 * G1 + __builtin_ctz(h1);
+            } else {
+                const int Glim = lim >> 4;
+                int Gs = G1 + 1;
+                while (Gs <= Glim) {
+                    if (Gs >= W0 + 4 * kGmWin) {
+                        if (16 * Gs > over_lim) { capped = true; break; }
+                        W0 = Gs & ~3;
+                        load_gm(d, gmb + W0);
+                    }
+                    const unsigned long long m0 = gm_ge64(d, 0, C, Cm) & bits_from(Gs - W0) & bits_to(Glim - W0);
+                    const unsigned long long m1 =
+                        gm_ge64(d, 1, C, Cm) & bits_from(Gs - W0 - 64) & bits_to(Glim - W0 - 64);
+                    if (m0 | m1) {
+                        const int g = W0 + (m0 ? __builtin_ctzll(m0) : 64 + __builtin_ctzll(m1));
+                        const uint32_t h = gran_ge(ld16(base + 16 * g), C, Cm) & range16(0, lim - 16 * g);
+                        if (h) j = 16 * g + __builtin_ctz(h);
+                        break;                            // h == 0 only in the last granule (g == Glim)
+                    }
+                    Gs = W0 + 4 * kGmWin;
+                }
+            }
+            if (j < 0 && !capped && p + maxlen <= size - 1) j = p + maxlen;   // forced cut (:288-294)
+        }
+        if (capped) { sync = kSyncFail; active = false; continue; }
+        if (j < 0) { active = false; continue; }          // the data ended
+        const int cut = j + 1;                            // :276-283
+        const int ci = min(n, ncap - 1);                  // n < ncap always (the caps bound it)
+        overflow |= n >= ncap;
+        vcuts[l * kLdsCuts + ci] = (uint16_t)min(cut - s, 0xffff);
+        vcnt[l] = (uint8_t)(ci + 1);
+        n = ci + 1;
+        if (cut >= e) {                                   // overrun: look for a shared cut
+            if (n_main < 0) n_main = ci;
+            const int sc = vcnt[l + 1];
+            const int rel = cut - e;
+            lds_u16v *sl = vcuts + (l + 1) * kLdsCuts;
+            while (ptr < sc && (int)sl[ptr] < rel) ptr++;
+            if (rel >= Ls) { sync = kSyncFail; active = false; }       // past the next segment's own cuts
+            else if (ptr < sc && (int)sl[ptr] == rel) { sync = (ci - n_main) | (ptr << 16); active = false; }
+            else if (n - n_main >= kLaneOver) { sync = kSyncFail; active = false; }
+        }
+        p = cut;
+        first = false;
+        if (active && p >= over_lim && p + w <= size - 1) { sync = kSyncFail; active = false; }   // byte cap
+        if (overflow) active = false;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // no LDS-DMA lands after the wave is gone
     if (overflow && real) atomicOr(err, 64);
     if (real) {
         const int G = bd.seg0 + k;
@@ -741,7 +784,7 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
 //    nodes that are not "synced to k + 1" are compacted (prefix over the threads' segment runs)
 //    and thread 0 follows the path through them; then each thread sizes its segments' pieces, a
 //    prefix places them and each thread copies its pieces.
-constexpr int kStitchNodes = 4096;       // compacted irregular boundaries per block (more: fallback)
+constexpr int kStitchNodes = 2048;       // compacted irregular boundaries per block (more: fallback)
 __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__restrict__ blocks,
                                                            const uint32_t *__restrict__ spec, int cap,
                                                            SegMeta *__restrict__ meta,
@@ -749,10 +792,13 @@ __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__re
                                                            BlockState *__restrict__ bst, int *__restrict__ err)
 {
     __shared__ uint32_t s_sum[1024];
+    // 32 KiB of LDS in all: a 1024-thread workgroup must find a CU with that much free beside the
+    // co-running walk / SHA / place workgroups
     __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes (ascending)
-    __shared__ int s_jx[kStitchNodes];       // on-path jumps: source node, target, shared-cut index
-    __shared__ int s_jm[kStitchNodes];
-    __shared__ int s_jj[kStitchNodes];
+    __shared__ uint32_t s_nv[kStitchNodes];  // their status: bit 31 jump (jmp in bits 0..23, jj in 24..29),
+                                             // bit 30 chain end (loaded in parallel: thread 0's walk reads LDS)
+    __shared__ int s_jx[kStitchNodes];       // on-path jumps: source node ...
+    __shared__ uint32_t s_jt[kStitchNodes];  // ... target segment (bits 0..23) | shared-cut index << 24
     __shared__ int s_nj, s_term, s_fb;
     const int b = blockIdx.x;
     const BlockDesc bd = blocks[b];
@@ -778,7 +824,12 @@ __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__re
     const int tot_irr = (int)s_sum[1023];
     for (int k = k0; k < k1; k++)
         if (k < nseg - 1 && mt[k].sync < 0) {
-            if (pos < (uint32_t)kStitchNodes) s_nx[pos] = k;
+            if (pos < (uint32_t)kStitchNodes) {
+                s_nx[pos] = k;
+                const int sy = mt[k].sync;
+                s_nv[pos] = sy == kSyncJump ? (0x80000000u | ((uint32_t)mt[k].jj << 24) | (uint32_t)mt[k].jmp)
+                                            : (sy == kSyncEnd ? 0x40000000u : 0u);
+            }
             pos++;
         }
     __syncthreads();
@@ -793,14 +844,15 @@ __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__re
                 break;
             }
             const int x = s_nx[i];
-            const int sy = mt[x].sync;
-            if (sy == kSyncJump && nj < kStitchNodes) {
-                s_jx[nj] = x; s_jm[nj] = x + mt[x].jmp; s_jj[nj] = mt[x].jj; nj++;
-                cur = x + mt[x].jmp;
+            const uint32_t v = s_nv[i];
+            if ((v & 0x80000000u) && nj < kStitchNodes) {
+                const int tgt = x + (int)(v & 0xffffffu);
+                s_jx[nj] = x; s_jt[nj] = (uint32_t)tgt | (v & 0x3f000000u); nj++;
+                cur = tgt;
                 continue;
             }
             term = x;
-            fb = sy != kSyncEnd;
+            fb = (v & 0x40000000u) == 0;
             break;
         }
         s_nj = nj; s_term = term; s_fb = fb;
@@ -816,12 +868,13 @@ __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__re
         const int ji = lo - 1;
         bool target = false;
         if (ji >= 0) {
-            if (s_jm[ji] > k) return;                      // jumped over
-            target = s_jm[ji] == k;
+            const int tgt = (int)(s_jt[ji] & 0xffffffu);
+            if (tgt > k) return;                           // jumped over
+            target = tgt == k;
         }
         const SegMeta m = mt[k];
         if (k == 0) from = 0;
-        else if (target) from = s_jj[ji];
+        else if (target) from = (int)(s_jt[ji] >> 24);
         else from = (mt[k - 1].sync >> 16) & 0xffff;
         if (from > m.n_main) { atomicOr(err, 128); from = m.n_main; }   // never: a shared cut is a main cut
         cnt = m.n_main - from;
@@ -860,16 +913,16 @@ __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__re
     }
 }
 
-// 3b. copy: 32 lanes per segment move its planned piece of the speculative list into the offsets
+// 3b. copy: one thread per segment moves its planned piece of the speculative list into the offsets
 __global__ void __launch_bounds__(256) lane_copy_kernel(const uint32_t *__restrict__ spec, int cap,
                                                         const SegMeta *__restrict__ meta, int nsegs,
                                                         uint32_t *__restrict__ offsets)
 {
-    const int G = blockIdx.x * 8 + (threadIdx.x >> 5);
-    const int i = threadIdx.x & 31;
+    const int G = blockIdx.x * 256 + threadIdx.x;
     if (G >= nsegs) return;
-    const int n = meta[G].cp_n;
-    if (i < n) offsets[meta[G].cp_dst + i] = spec[(size_t)G * cap + meta[G].cp_from + i];
+    const int n = meta[G].cp_n, from = meta[G].cp_from, dst = meta[G].cp_dst;
+    const uint32_t *src = spec + (size_t)G * cap + from;
+    for (int i = 0; i < n; i++) offsets[dst + i] = src[i];
 }
 
 // 4. fallback + drop-last/append-size: one wave per block.  A block whose path ends at a failed
@@ -914,22 +967,27 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
 namespace hdrf {
 int lane_spec_cap(int seg_len, int w) { return seg_len / (w + 2) + 2 + kLaneOver; }
 
-hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int total_waves, int nsegs, int w, int maxlen,
-                           uint32_t *spec, int spec_cap, SegMeta *meta, int *rq, int *rq_count, int rq_cap,
-                           BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk)
+hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int total_waves, int nsegs,
+                           uint8_t *gm, int gstride, int w, int maxlen, uint32_t *spec, int spec_cap, SegMeta *meta,
+                           int *rq, int *rq_count, int rq_cap, BlockState *bst, uint32_t *offsets, int cap_blk,
+                           int *err, hipStream_t st, Marker *mk)
 {
+    if ((max_len + 15) / 16 + 4 * kGmWin > gstride) return hipErrorInvalidValue;
     mk->mark(st);
     hipError_t e = hipMemsetAsync(rq_count, 0, sizeof(int), st);
     if (e != hipSuccess) return e;
+    const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
+    hipLaunchKernelGGL(gmax_kernel, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, gm, gstride);
+    mk->mark(st);
     hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), 0, st, d_blocks, nblocks, total_waves,
-                       w, maxlen, spec, spec_cap, meta, rq, rq_count, rq_cap, err);
+                       gm, gstride, w, maxlen, spec, spec_cap, meta, rq, rq_count, rq_cap, err);
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, rq, rq_count, rq_cap, w,
                        maxlen, spec, spec_cap, meta, offsets, cap_blk, 0);
     hipLaunchKernelGGL(lane_stitch_kernel, dim3(nblocks), dim3(1024), 0, st, d_blocks, spec, spec_cap, meta, offsets,
                        cap_blk, bst, err);
-    hipLaunchKernelGGL(lane_copy_kernel, dim3((nsegs + 7) / 8), dim3(256), 0, st, spec, spec_cap, meta, nsegs, offsets);
+    hipLaunchKernelGGL(lane_copy_kernel, dim3((nsegs + 255) / 256), dim3(256), 0, st, spec, spec_cap, meta, nsegs, offsets);
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, rq, rq_count, rq_cap, w,
                        maxlen, spec, spec_cap, meta, offsets, cap_blk, 1);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,

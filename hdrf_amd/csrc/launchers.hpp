@@ -6,7 +6,7 @@ namespace hdrf {
 
 // Stage markers: when timing is on, a HIP event is recorded on the launch stream at every
 // stage boundary (kernels of one stream run in order, so event deltas are kernel times).
-constexpr int kNumStages = 11;  // walk, stitch, sha_full, sha_tail, claim, apply, slow+decide, scan, flush, place, (spare)
+constexpr int kNumStages = 12;  // walk, stitch, sha_full, sha_tail, claim, apply, slow+decide, scan, flush, place, compress, gmax
 struct Marker {
     hipEvent_t *ev = nullptr;   // kNumStages + 1 events
     int next = 0;
@@ -27,10 +27,11 @@ struct StoreParams {
     int place_lds = 0;         // dynamic LDS per place workgroup (occupancy throttle, 0 = none)
 };
 
-// chunking: lane walk (total_waves waves over the batch's segments) -> stitch -> fallback
+// chunking: granule maxima -> lane walk (total_waves waves over the batch's segments) -> repair ->
+// stitch -> fallback.  gm: [nblocks][gstride] bytes, gstride >= max_len / 16 + 4 * 128.
 int lane_spec_cap(int seg_len, int w);
-hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int total_waves, int nsegs, int w, int maxlen,
-                           uint32_t *spec, int spec_cap, SegMeta *meta, int *rq, int *rq_count, int rq_cap,
+hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int total_waves, int nsegs,
+                           uint8_t *gm, int gstride, int w, int maxlen, uint32_t *spec, int spec_cap, SegMeta *meta, int *rq, int *rq_count, int rq_cap,
                            BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,

@@ -41,7 +41,7 @@ PIPELINE_DEPTH = 3          # HDRF_PIPELINE_DEPTH: batches in flight
 STAGES = ["walk(spec_walk_kernel)", "stitch(spec_sync/plan/copy/fallback)", "sha_full(sha_full_kernel)",
           "sha_tail(sha_tail_kernel)", "index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
           "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
-          "place(place_kernel)", "compress(lz4_seg/lz4_pack)"]
+          "place(place_kernel)", "compress(lz4_seg/lz4_pack)", "gmax(gmax_kernel)"]
 
 
 class HdrfError(RuntimeError):
