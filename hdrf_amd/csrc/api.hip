@@ -48,6 +48,13 @@ struct Slot {
     uint8_t *d_gm = nullptr;                  // granule maxima [B][gstride] (chunking pass 1)
     int gstride = 0;
     int64_t max_len = 0;                      // longest block of the batch in this slot
+    int max_nseg = 0;                         // most segments of one block of the batch
+    uint32_t *d_irr = nullptr;                // irregular-boundary bitmask (meta_cap / 32 + 2 words)
+    PathInfo *d_path = nullptr;               // [B]
+    int *d_jx = nullptr;                      // [B][2048]
+    uint32_t *d_jt = nullptr;                 // [B][2048]
+    uint32_t *d_wgsum = nullptr;              // [B][maxw_cap]
+    int maxw_cap = 0;
     int *d_rq = nullptr, *d_rq_count = nullptr;   // failed speculative boundaries (repair queue), meta_cap entries
     size_t spec_words = 0, meta_cap = 0;      // capacity of d_spec (u32) / d_meta (segments), grown on demand
     int total_waves = 0, total_segs = 0, spec_cap = 0;   // lane walk of the batch in this slot
@@ -231,7 +238,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
 
 static void free_slot(Slot &S)
 {
-    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
+    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
                    S.d_pre, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
                    S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err};
     for (void *p : dev)
@@ -286,7 +293,9 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
     S.spec_words = S.meta_cap * (size_t)lane_spec_cap(seg_len0, c.window);
     S.gstride = (int)(((c.max_block_bytes + 15) / 16 + 1024 + 255) & ~(int64_t)255);
     if ((rc = dalloc(ctx, &S.d_blocks, B)) || (rc = dalloc(ctx, &S.d_spec, S.spec_words)) ||
-        (rc = dalloc(ctx, &S.d_gm, (size_t)B * S.gstride)) ||
+        (rc = dalloc(ctx, &S.d_gm, (size_t)B * S.gstride)) || (rc = dalloc(ctx, &S.d_path, B)) ||
+        (rc = dalloc(ctx, &S.d_jx, (size_t)B * 2048)) || (rc = dalloc(ctx, &S.d_jt, (size_t)B * 2048)) ||
+        (rc = dalloc(ctx, &S.d_irr, S.meta_cap / 32 + 2)) ||
         (rc = dalloc(ctx, &S.d_meta, S.meta_cap)) || (rc = dalloc(ctx, &S.d_rq, S.meta_cap)) ||
         (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
         (rc = dalloc(ctx, &S.d_off, nchunk)) || (rc = dalloc(ctx, &S.d_dig, nchunk * ctx->HW)) ||
@@ -493,6 +502,14 @@ static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t l
 // [4, 24] x 702 B, and shortened (down to 6 x 702 B) while the batch would give the lane walk fewer
 // than 1024 waves (one-block calls).  Grows the slot's speculative lists when needed (the slot's
 // previous batch has completed).
+static ChunkScratch chunk_scratch(Slot &S)
+{
+    ChunkScratch X;
+    X.gm = S.d_gm; X.gstride = S.gstride; X.rq = S.d_rq; X.rq_count = S.d_rq_count; X.rq_cap = (int)S.meta_cap;
+    X.irr = S.d_irr; X.path = S.d_path; X.jx = S.d_jx; X.jt = S.d_jt; X.wgsum = S.d_wgsum; X.maxw = S.maxw_cap;
+    return X;
+}
+
 static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t *const *dev_data,
                           const uint64_t *len, const uint64_t *readable)
 {
@@ -527,6 +544,17 @@ static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t
     }
     S.total_waves = wave0;
     S.total_segs = seg0;
+    int max_nseg = 1;
+    for (int b = 0; b < nblocks; b++) max_nseg = std::max(max_nseg, S.h_desc[b].nseg);
+    S.max_nseg = max_nseg;
+    const int maxw = (max_nseg + 255) / 256;
+    if (maxw > S.maxw_cap) {
+        (void)hipFree(S.d_wgsum);
+        S.d_wgsum = nullptr;
+        S.maxw_cap = 0;
+        if (int rc = dalloc(ctx, &S.d_wgsum, (size_t)ctx->max_batch * maxw)) return rc;
+        S.maxw_cap = maxw;
+    }
     S.spec_cap = lane_spec_cap(seg_len, c.window);
     const size_t words = (size_t)seg0 * S.spec_cap;
     if ((size_t)seg0 > S.meta_cap) {
@@ -537,6 +565,9 @@ static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t
         S.meta_cap = 0;
         if (int rc = dalloc(ctx, &S.d_meta, (size_t)seg0)) return rc;
         if (int rc = dalloc(ctx, &S.d_rq, (size_t)seg0)) return rc;
+        (void)hipFree(S.d_irr);
+        S.d_irr = nullptr;
+        if (int rc = dalloc(ctx, &S.d_irr, (size_t)seg0 / 32 + 2)) return rc;
         S.meta_cap = (size_t)seg0;
     }
     if (words > S.spec_words) {
@@ -588,8 +619,9 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, W));
     Marker mw;
     mw.ev = ctx->timing ? S.evW : nullptr;
-    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.total_waves, S.total_segs, S.d_gm, S.gstride, c.window,
-                          c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, W, &mw));
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs, chunk_scratch(S),
+                          c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst, S.d_off, ctx->cap_blk, S.d_err,
+                          W, &mw));
     mw.mark(W);
     HIPCK(hipEventRecord(S.walk_done, W));
     // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig)
@@ -1202,9 +1234,9 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
     Marker mk;
     mk.ev = ctx->timing ? S.evB : nullptr;             // 9 markers: gmax, walk .. slow+decide, end
-    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.total_waves, S.total_segs, S.d_gm, S.gstride, c.window,
-                          c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_rq, S.d_rq_count, (int)S.meta_cap, S.d_bst, S.d_off, ctx->cap_blk, S.d_err, st,
-                          &mk));
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs, chunk_scratch(S),
+                          c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst, S.d_off, ctx->cap_blk, S.d_err,
+                          st, &mk));
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
                      S.d_queue, st, &mk));

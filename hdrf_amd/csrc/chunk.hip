@@ -8,19 +8,21 @@
 // block size appended (:300-304).
 //
 // GPU formulation:
-//   1. spec_walk  — each block is cut into segments; one wave walks the chain from each
-//                   segment start as if a cut were there, recording its cuts plus up to
-//                   64 "overrun" cuts past the segment end.  Bytes are streamed as 1 KiB
-//                   tiles (64 lanes x 16 B, coalesced) with two tiles of prefetch; the
-//                   window max is a per-granule max + DPP reduction, the search is a
-//                   ballot over granules >= M followed by a scalar SWAR byte test.
-//   2. spec_sync  — chains are deterministic in p, so the true chain (from segment k's
-//                   overrun) and segment k+1's speculative chain agree from the first cut
-//                   they share.  One wave per segment boundary finds that cut.
-//   3. spec_plan / spec_copy — prefix-sum the pieces and compact them into offsets[].
-//   4. spec_fallback — blocks whose chains did not meet (periodic data) are finished by a
-//                   sequential exact walk from the last proven cut; every block then gets
-//                   the reference's drop-last/append-size rule.
+//   1a. gmax        — one coalesced pass: the biased maximum of every 16-B granule (1 B each).
+//   1b. lane walk   — each block is cut into speculative segments of seg_len bytes; one LANE
+//                     walks the chain from each segment start as if a cut were there, one chunk
+//                     per step from the granule maxima (window max = 42-44 maxima + two exact
+//                     edge granules; search = first granule max >= M, then its first byte).
+//                     Past its segment end it compares its cuts with the next lane's list (LDS):
+//                     the first shared cut proves the chains equal from there on.
+//   2.  repair      — boundaries whose chains did not meet within the lane's caps: the exact
+//                     wave walker (walk_chain below) continues the chain until it meets ANY
+//                     later segment's list (or gives up).
+//   3.  stitch/copy — follow the path through synced / repaired boundaries, prefix-sum the pieces,
+//                     compact them into offsets[].
+//   4.  fallback    — blocks whose path ends at an unrepaired boundary (periodic data) are finished
+//                     by the sequential exact walk from the last proven cut; every block then gets
+//                     the reference's drop-last/append-size rule.
 #include "launchers.hpp"
 
 namespace hdrf {
@@ -567,7 +569,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
                                                         uint32_t *__restrict__ spec, int cap,
                                                         SegMeta *__restrict__ meta, int *__restrict__ rq,
                                                         int *__restrict__ rq_count, int rq_cap,
-                                                        int *__restrict__ err)
+                                                        uint32_t *__restrict__ irr, int *__restrict__ err)
 {
     __shared__ uint16_t s_cuts[4][64 * kLdsCuts];
     __shared__ uint8_t s_cnt[4][64];
@@ -599,6 +601,8 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
     bool active = exists, overflow = false;
     vcnt[l] = 0;
     uint32_t d[kGmWin];
+    uint4 rh = make_uint4(0, 0, 0, 0);                    // raw bytes of the last hit granule gh
+    int gh = -1;
     for (;;) {
         if (!ballot64(active && l < kWaveSegs)) break;
         if (!active) continue;
@@ -608,8 +612,9 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
         const int G0 = p >> 4, G1 = wend >> 4;
         int W0 = G0 & ~3;
         load_gm(d, gmb + W0);
-        const uint4 r0 = ld16(base + 16 * G0), r1 = ld16(base + 16 * G1);
-        // M(p): granules G0+1 .. G1-1 are whole (bytes [a, b] of d, 1 <= a <= 4, 42 <= b <= 46)
+        // M(p): granules G0+1 .. G1-1 are whole (bytes [a, b] of d, 1 <= a <= 4, 42 <= b <= 46); the
+        // two edge granules need their raw bytes only when their maximum exceeds the rest (rare:
+        // ~6 % of random-data windows), so most chunks touch no raw byte before the hit granule
         const int a = G0 + 1 - W0, b = G1 - 1 - W0;
         BMax mx;
         mx.add(d[0] & keep_bytes(a, b + 1));
@@ -617,15 +622,39 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
         for (int i = 1; i < 10; i++) mx.add(d[i]);
         mx.add(d[10] & keep_bytes(a - 40, b - 39));
         mx.add(d[11] & keep_bytes(a - 44, b - 43));
-        uint32_t M = max(mx.get(), max(gran_max(r0, p & 15, 15), gran_max(r1, 0, wend & 15)));
+        uint32_t M = mx.get();
         if (!first) M = max(M, 0x80u);                    // mValue reset to 0 after a cut (:281)
+        const uint32_t e0 = (d[0] >> (8 * (G0 - W0))) & 0xffu;
+        const int i1 = G1 - W0;
+        const uint32_t e1 = (((i1 >> 2) == 10 ? d[10] : d[11]) >> (8 * (i1 & 3))) & 0xffu;
+        if (e0 > M) {
+            if ((p & 15) == 0) M = e0;
+            else {
+                const uint4 r0 = G0 == gh ? rh : ld16(base + 16 * G0);   // usually the last hit granule
+                M = max(M, gran_max(r0, p & 15, 15));
+            }
+        }
+        uint4 r1 = make_uint4(0, 0, 0, 0);
+        bool have1 = false;
+        if (e1 > M) {
+            if ((wend & 15) == 15) M = e1;
+            else {
+                r1 = ld16(base + 16 * G1);
+                have1 = true;
+                M = max(M, gran_max(r1, 0, wend & 15));
+            }
+        }
         int j = -1;
         bool capped = false;
         if (M == 0) {
             j = wend + 1 <= lim ? wend + 1 : -1;          // every byte qualifies
         } else {
             const uint32_t C = __builtin_amdgcn_perm(256u - M, 256u - M, 0u), Cm = C & 0x7f7f7f7fu;
-            const uint32_t h1 = gran_ge(r1, C, Cm) & range16((wend & 15) + 1, lim - 16 * G1);
+            uint32_t h1 = 0;
+            if (e1 >= M && (wend & 15) != 15) {           // bytes of G1 after the window may qualify
+                if (!have1) r1 = ld16(base + 16 * G1);
+                h1 = gran_ge(r1, C, Cm) & range16((wend & 15) + 1, lim - 16 * G1);
+            }
             if (h1) {
                 j = 16 * G1 + __builtin_ctz(h1);
             } else {
@@ -642,7 +671,9 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
                         gm_ge64(d, 1, C, Cm) & bits_from(Gs - W0 - 64) & bits_to(Glim - W0 - 64);
                     if (m0 | m1) {
                         const int g = W0 + (m0 ? __builtin_ctzll(m0) : 64 + __builtin_ctzll(m1));
-                        const uint32_t h = gran_ge(ld16(base + 16 * g), C, Cm) & range16(0, lim - 16 * g);
+                        rh = ld16(base + 16 * g);
+                        gh = g;
+                        const uint32_t h = gran_ge(rh, C, Cm) & range16(0, lim - 16 * g);
                         if (h) j = 16 * g + __builtin_ctz(h);
                         break;                            // h == 0 only in the last granule (g == Glim)
                     }
@@ -684,6 +715,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
         m.n_main = n_main; m.n_over = n - n_main; m.sync = sync; m.jmp = 0; m.jj = 0; m.n_ext = 0; m.ext_dst = -1;
         m.cp_from = 0; m.cp_n = 0; m.cp_dst = 0; m.pad[0] = m.pad[1] = m.pad[2] = 0;
         meta[G] = m;
+        if (k < nseg - 1 && sync < 0) atomicOr(irr + (G >> 5), 1u << (G & 31));   // irregular boundary
         if (sync == kSyncFail) {
             const int q = atomicAdd(rq_count, 1);
             if (q < rq_cap) rq[q] = G;                        // beyond rq_cap: no repair, stitch falls back
@@ -775,55 +807,59 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
     }
 }
 
-// 3. stitch: one 1024-thread workgroup per block.  The block's chain is segment 0's list, then,
-//    boundary by boundary, the next segment's list from the shared cut: synced boundaries go to
-//    k + 1 (seg k keeps its overrun cuts [0, i)), repaired ones jump to k + jmp (seg k keeps all
-//    its cuts and the repair's n_ext - 1 cuts; the segments jumped over are off the path); the
-//    path ends at the last segment, at a chain that ran to the block end, or at a failed boundary
-//    (seg k keeps all its cuts and the sequential fallback continues from the last one).  The
-//    nodes that are not "synced to k + 1" are compacted (prefix over the threads' segment runs)
-//    and thread 0 follows the path through them; then each thread sizes its segments' pieces, a
-//    prefix places them and each thread copies its pieces.
-constexpr int kStitchNodes = 2048;       // compacted irregular boundaries per block (more: fallback)
-__global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__restrict__ blocks,
-                                                           const uint32_t *__restrict__ spec, int cap,
-                                                           SegMeta *__restrict__ meta,
-                                                           uint32_t *__restrict__ offsets, int cap_blk,
-                                                           BlockState *__restrict__ bst, int *__restrict__ err)
+// 3. stitch.  The block's chain is segment 0's list, then, boundary by boundary, the next
+//    segment's list from the shared cut: synced boundaries go to k + 1 (seg k keeps its overrun
+//    cuts [0, i)), repaired ones jump to k + jmp (seg k keeps all its cuts and the repair's n_ext - 1
+//    cuts; the segments jumped over are off the path); the path ends at the last segment, at a chain
+//    that ran to the block end, or at a failed boundary (seg k keeps all its cuts and the sequential
+//    fallback continues from the last one).  Four wide kernels:
+//      path   one workgroup per block: the irregular boundaries (not "synced to k + 1"; a bitmask the
+//             lane walk wrote) are compacted in order with their status, thread 0 follows the path
+//             through them (LDS only) and writes the on-path jumps, the terminal and the fallback flag
+//      count  one thread per segment: its piece (first list index, cuts, repair cuts) + workgroup sums
+//      scan   one workgroup per block: prefix over the workgroup sums; n_cuts / fail_dst
+//      copy   one thread per segment: workgroup prefix -> destination; the piece is copied
+constexpr int kStitchNodes = 2048;       // irregular boundaries per block followed (more: fallback there)
+
+__global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__restrict__ blocks,
+                                                          const uint32_t *__restrict__ irr,
+                                                          const SegMeta *__restrict__ meta,
+                                                          PathInfo *__restrict__ path, int *__restrict__ jx_all,
+                                                          uint32_t *__restrict__ jt_all)
 {
-    __shared__ uint32_t s_sum[1024];
-    // 32 KiB of LDS in all: a 1024-thread workgroup must find a CU with that much free beside the
-    // co-running walk / SHA / place workgroups
     __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes (ascending)
-    __shared__ uint32_t s_nv[kStitchNodes];  // their status: bit 31 jump (jmp in bits 0..23, jj in 24..29),
-                                             // bit 30 chain end (loaded in parallel: thread 0's walk reads LDS)
-    __shared__ int s_jx[kStitchNodes];       // on-path jumps: source node ...
-    __shared__ uint32_t s_jt[kStitchNodes];  // ... target segment (bits 0..23) | shared-cut index << 24
-    __shared__ int s_nj, s_term, s_fb;
-    const int b = blockIdx.x;
+    __shared__ uint32_t s_nv[kStitchNodes];  // status: bit 31 jump (jmp in bits 0..23, jj in 24..29), bit 30 end
+    __shared__ uint32_t s_sum[256];
+    const int b = blockIdx.x, t = threadIdx.x;
     const BlockDesc bd = blocks[b];
-    const int nseg = bd.nseg, t = threadIdx.x;
-    SegMeta *mt = meta + bd.seg0;
-    const int per = (nseg + 1023) / 1024;
-    const int k0 = min(nseg, t * per), k1 = min(nseg, k0 + per);
-    auto scan = [&](uint32_t v) -> uint32_t {           // exclusive prefix over the threads; s_sum[1023] = total
-        s_sum[t] = v;
-        __syncthreads();
-        for (int d = 1; d < 1024; d <<= 1) {
-            const uint32_t x = t >= d ? s_sum[t - d] : 0u;
-            __syncthreads();
-            s_sum[t] += x;
-            __syncthreads();
-        }
-        return s_sum[t] - v;
+    const int nseg = bd.nseg, s0 = bd.seg0;
+    const SegMeta *mt = meta + s0;
+    const int nb = nseg - 1;                 // boundaries 0 .. nseg - 2
+    const int nwords = (nb + 31) >> 5;
+    auto word = [&](int i) -> uint32_t {     // boundaries 32 i .. 32 i + 31 of this block
+        const int gbit = s0 + 32 * i, wi = gbit >> 5, sh = gbit & 31;
+        uint32_t v = irr[wi] >> sh;
+        if (sh) v |= irr[wi + 1] << (32 - sh);
+        const int rem = nb - 32 * i;
+        return rem >= 32 ? v : (v & ((1u << rem) - 1u));
     };
-    // (a) compact the irregular boundaries (sync < 0), k < nseg - 1
-    uint32_t nirr = 0;
-    for (int k = k0; k < k1; k++) nirr += (k < nseg - 1 && mt[k].sync < 0);
-    uint32_t pos = scan(nirr);
-    const int tot_irr = (int)s_sum[1023];
-    for (int k = k0; k < k1; k++)
-        if (k < nseg - 1 && mt[k].sync < 0) {
+    const int per = (nwords + 255) >> 8;
+    const int w0 = min(nwords, t * per), w1 = min(nwords, w0 + per);
+    uint32_t cnt = 0;
+    for (int i = w0; i < w1; i++) cnt += (uint32_t)__popc(word(i));
+    s_sum[t] = cnt;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+        const uint32_t x = t >= d ? s_sum[t - d] : 0u;
+        __syncthreads();
+        s_sum[t] += x;
+        __syncthreads();
+    }
+    uint32_t pos = s_sum[t] - cnt;
+    const int tot = (int)s_sum[255];
+    for (int i = w0; i < w1; i++)
+        for (uint32_t v = word(i); v; v &= v - 1) {
+            const int k = 32 * i + __builtin_ctz(v);
             if (pos < (uint32_t)kStitchNodes) {
                 s_nx[pos] = k;
                 const int sy = mt[k].sync;
@@ -833,21 +869,22 @@ __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__re
             pos++;
         }
     __syncthreads();
-    // (b) thread 0 follows the path through the irregular nodes
     if (t == 0) {
-        const int nnx = min(tot_irr, kStitchNodes);
+        const int nnx = min(tot, kStitchNodes);
+        int *jx = jx_all + (size_t)b * kStitchNodes;
+        uint32_t *jt = jt_all + (size_t)b * kStitchNodes;
         int cur = 0, i = 0, nj = 0, term = nseg - 1, fb = 0;
         for (;;) {
             while (i < nnx && s_nx[i] < cur) i++;
             if (i >= nnx) {
-                if (tot_irr > kStitchNodes) { term = cur; fb = 1; }   // uncompacted nodes ahead: fall back here
+                if (tot > kStitchNodes) { term = cur; fb = 1; }   // uncompacted nodes ahead: fall back here
                 break;
             }
             const int x = s_nx[i];
             const uint32_t v = s_nv[i];
             if ((v & 0x80000000u) && nj < kStitchNodes) {
                 const int tgt = x + (int)(v & 0xffffffu);
-                s_jx[nj] = x; s_jt[nj] = (uint32_t)tgt | (v & 0x3f000000u); nj++;
+                jx[nj] = x; jt[nj] = (uint32_t)tgt | (v & 0x3f000000u); nj++;
                 cur = tgt;
                 continue;
             }
@@ -855,74 +892,137 @@ __global__ void __launch_bounds__(1024) lane_stitch_kernel(const BlockDesc *__re
             fb = (v & 0x40000000u) == 0;
             break;
         }
-        s_nj = nj; s_term = term; s_fb = fb;
+        PathInfo pi;
+        pi.nj = nj; pi.term = term; pi.fb = fb; pi.pad = 0;
+        path[b] = pi;
+    }
+}
+
+// block-wide (256 threads) sum / exclusive prefix through 4 wave partials
+__device__ __forceinline__ uint32_t wg_excl_scan(uint32_t v, uint32_t *s_w, uint32_t &total)
+{
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane_id() == 63) s_w[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (int i = 0; i < (int)(threadIdx.x >> 6); i++) base += s_w[i];
+    total = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    return base + incl - v;
+}
+
+__global__ void __launch_bounds__(256) stitch_count_kernel(const BlockDesc *__restrict__ blocks,
+                                                           SegMeta *__restrict__ meta,
+                                                           const PathInfo *__restrict__ path,
+                                                           const int *__restrict__ jx_all,
+                                                           const uint32_t *__restrict__ jt_all,
+                                                           uint32_t *__restrict__ wgsum, int maxw,
+                                                           int *__restrict__ err)
+{
+    __shared__ int s_jx[kStitchNodes];
+    __shared__ uint32_t s_jt[kStitchNodes];
+    __shared__ uint32_t s_w[4];
+    const int b = blockIdx.y, t = threadIdx.x;
+    const BlockDesc bd = blocks[b];
+    const int nseg = bd.nseg;
+    if ((int)blockIdx.x * 256 >= nseg) return;            // whole workgroup
+    const int k = blockIdx.x * 256 + t;
+    const PathInfo pi = path[b];
+    const int nj = pi.nj, term = pi.term;
+    for (int i = t; i < nj; i += 256) {
+        s_jx[i] = jx_all[(size_t)b * kStitchNodes + i];
+        s_jt[i] = jt_all[(size_t)b * kStitchNodes + i];
     }
     __syncthreads();
-    const int nj = s_nj, term = s_term;
-    // (c) the piece of every segment on the path
-    auto piece = [&](int k, int &from, int &cnt, int &ext) {
-        from = 0; cnt = 0; ext = -1;
-        if (k > term) return;
+    SegMeta *mt = meta + bd.seg0;
+    int from = 0, cnt = 0, ext = -1;
+    if (k < nseg && k <= term) {
         int lo = 0, hi = nj;                               // last jump with source < k
         while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_jx[mid] < k) lo = mid + 1; else hi = mid; }
         const int ji = lo - 1;
-        bool target = false;
+        bool target = false, over = false;
         if (ji >= 0) {
             const int tgt = (int)(s_jt[ji] & 0xffffffu);
-            if (tgt > k) return;                           // jumped over
+            over = tgt > k;                                // jumped over
             target = tgt == k;
         }
-        const SegMeta m = mt[k];
-        if (k == 0) from = 0;
-        else if (target) from = (int)(s_jt[ji] >> 24);
-        else from = (mt[k - 1].sync >> 16) & 0xffff;
-        if (from > m.n_main) { atomicOr(err, 128); from = m.n_main; }   // never: a shared cut is a main cut
-        cnt = m.n_main - from;
-        if (k == term) cnt += m.n_over;
-        else if (m.sync == kSyncJump) { cnt += m.n_over; ext = cnt; cnt += m.n_ext - 1; }
-        else cnt += m.sync & 0xffff;
-    };
-    uint32_t local = 0;
-    for (int k = k0; k < k1; k++) {
-        int from, cnt, ext;
-        piece(k, from, cnt, ext);
-        local += (uint32_t)cnt;
+        if (!over) {
+            const SegMeta m = mt[k];
+            if (k == 0) from = 0;
+            else if (target) from = (int)(s_jt[ji] >> 24);
+            else from = (mt[k - 1].sync >> 16) & 0xffff;
+            if (from > m.n_main) { atomicOr(err, 128); from = m.n_main; }   // never: a shared cut is a main cut
+            cnt = m.n_main - from;
+            if (k == term) cnt += m.n_over;
+            else if (m.sync == kSyncJump) { cnt += m.n_over; ext = cnt; cnt += m.n_ext - 1; }
+            else cnt += m.sync & 0xffff;
+        }
     }
-    uint32_t dst = scan(local);
-    const uint32_t total = s_sum[1023];
-    if (total > (uint32_t)cap_blk) {
-        if (t == 0) atomicOr(err, 1);
-        for (int k = k0; k < k1; k++) mt[k].cp_n = 0;
-        return;
-    }
-    for (int k = k0; k < k1; k++) {                        // the plan; lane_copy_kernel moves the cuts
-        int from, cnt, ext;
-        piece(k, from, cnt, ext);
-        if (ext >= 0) mt[k].ext_dst = (int)dst + ext;      // the repair's cuts (emit pass)
+    if (k < nseg) {
         mt[k].cp_from = from;
-        mt[k].cp_n = ext >= 0 ? ext : cnt;
-        mt[k].cp_dst = b * cap_blk + (int)dst;
-        dst += (uint32_t)cnt;
+        mt[k].cp_n = ext >= 0 ? ext : cnt;                 // list cuts; the repair's cuts follow (emit)
+        mt[k].pad[0] = cnt;
+        mt[k].pad[1] = ext;
+    }
+    uint32_t total;
+    (void)wg_excl_scan((uint32_t)cnt, s_w, total);
+    if (t == 0) wgsum[(size_t)b * maxw + blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(256) stitch_scan_kernel(const BlockDesc *__restrict__ blocks,
+                                                          const PathInfo *__restrict__ path,
+                                                          uint32_t *__restrict__ wgsum, int maxw,
+                                                          BlockState *__restrict__ bst, int cap_blk,
+                                                          int *__restrict__ err)
+{
+    __shared__ uint32_t s_w[4];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const int nw = (blocks[b].nseg + 255) >> 8;
+    uint32_t run = 0;
+    for (int i0 = 0; i0 < nw; i0 += 256) {
+        const int i = i0 + t;
+        const uint32_t v = i < nw ? wgsum[(size_t)b * maxw + i] : 0u;
+        uint32_t total;
+        const uint32_t ex = wg_excl_scan(v, s_w, total);
+        if (i < nw) wgsum[(size_t)b * maxw + i] = run + ex;
+        run += total;
+        __syncthreads();
     }
     if (t == 0) {
         BlockState s;
-        s.n_cuts = (int)total;
-        s.fail_dst = s_fb ? (int)total : -1;
+        s.n_cuts = (int)run;
+        s.fail_dst = path[b].fb ? (int)run : -1;
         s.fail_p0 = 0; s.n_chunks = 0;
+        if (run > (uint32_t)cap_blk) { atomicOr(err, 1); s.n_cuts = 0; s.fail_dst = -1; }
         bst[b] = s;
     }
 }
 
-// 3b. copy: one thread per segment moves its planned piece of the speculative list into the offsets
-__global__ void __launch_bounds__(256) lane_copy_kernel(const uint32_t *__restrict__ spec, int cap,
-                                                        const SegMeta *__restrict__ meta, int nsegs,
-                                                        uint32_t *__restrict__ offsets)
+__global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__restrict__ blocks,
+                                                          SegMeta *__restrict__ meta,
+                                                          const uint32_t *__restrict__ spec, int cap,
+                                                          const uint32_t *__restrict__ wgsum, int maxw,
+                                                          const BlockState *__restrict__ bst,
+                                                          uint32_t *__restrict__ offsets, int cap_blk)
 {
-    const int G = blockIdx.x * 256 + threadIdx.x;
-    if (G >= nsegs) return;
-    const int n = meta[G].cp_n, from = meta[G].cp_from, dst = meta[G].cp_dst;
-    const uint32_t *src = spec + (size_t)G * cap + from;
-    for (int i = 0; i < n; i++) offsets[dst + i] = src[i];
+    __shared__ uint32_t s_w[4];
+    const int b = blockIdx.y, t = threadIdx.x;
+    const BlockDesc bd = blocks[b];
+    const int nseg = bd.nseg;
+    if ((int)blockIdx.x * 256 >= nseg) return;
+    if (bst[b].n_cuts == 0) return;                       // nothing on the path (or capacity error)
+    const int k = blockIdx.x * 256 + t;
+    const int G = bd.seg0 + k;
+    const int cnt = k < nseg ? meta[G].pad[0] : 0;
+    uint32_t total;
+    const uint32_t dst = wgsum[(size_t)b * maxw + blockIdx.x] + wg_excl_scan((uint32_t)cnt, s_w, total);
+    if (k < nseg && cnt > 0) {
+        const int ext = meta[G].pad[1];
+        if (ext >= 0) meta[G].ext_dst = (int)dst + ext;  // the repair's cuts (emit pass)
+        const int n = meta[G].cp_n, from = meta[G].cp_from;
+        const uint32_t *src = spec + (size_t)G * cap + from;
+        uint32_t *out = offsets + (size_t)b * cap_blk + dst;
+        for (int i = 0; i < n; i++) out[i] = src[i];
+    }
 }
 
 // 4. fallback + drop-last/append-size: one wave per block.  A block whose path ends at a failed
@@ -967,29 +1067,36 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
 namespace hdrf {
 int lane_spec_cap(int seg_len, int w) { return seg_len / (w + 2) + 2 + kLaneOver; }
 
-hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int total_waves, int nsegs,
-                           uint8_t *gm, int gstride, int w, int maxlen, uint32_t *spec, int spec_cap, SegMeta *meta,
-                           int *rq, int *rq_count, int rq_cap, BlockState *bst, uint32_t *offsets, int cap_blk,
-                           int *err, hipStream_t st, Marker *mk)
+hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
+                           int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
+                           SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
+                           Marker *mk)
 {
-    if ((max_len + 15) / 16 + 4 * kGmWin > gstride) return hipErrorInvalidValue;
+    if ((max_len + 15) / 16 + 4 * kGmWin > X.gstride) return hipErrorInvalidValue;
+    const int maxw = (max_nseg + 255) / 256;
+    if (maxw > X.maxw) return hipErrorInvalidValue;
     mk->mark(st);
-    hipError_t e = hipMemsetAsync(rq_count, 0, sizeof(int), st);
+    hipError_t e = hipMemsetAsync(X.rq_count, 0, sizeof(int), st);
+    if (e == hipSuccess) e = hipMemsetAsync(X.irr, 0, sizeof(uint32_t) * (size_t)(nsegs / 32 + 2), st);
     if (e != hipSuccess) return e;
     const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
-    hipLaunchKernelGGL(gmax_kernel, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, gm, gstride);
+    hipLaunchKernelGGL(gmax_kernel, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm, X.gstride);
     mk->mark(st);
     hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), 0, st, d_blocks, nblocks, total_waves,
-                       gm, gstride, w, maxlen, spec, spec_cap, meta, rq, rq_count, rq_cap, err);
+                       X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err);
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue
-    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, rq, rq_count, rq_cap, w,
-                       maxlen, spec, spec_cap, meta, offsets, cap_blk, 0);
-    hipLaunchKernelGGL(lane_stitch_kernel, dim3(nblocks), dim3(1024), 0, st, d_blocks, spec, spec_cap, meta, offsets,
-                       cap_blk, bst, err);
-    hipLaunchKernelGGL(lane_copy_kernel, dim3((nsegs + 255) / 256), dim3(256), 0, st, spec, spec_cap, meta, nsegs, offsets);
-    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, rq, rq_count, rq_cap, w,
-                       maxlen, spec, spec_cap, meta, offsets, cap_blk, 1);
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, 0);
+    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt);
+    hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt,
+                       X.wgsum, maxw, err);
+    hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
+                       cap_blk, err);
+    hipLaunchKernelGGL(stitch_copy_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, spec, spec_cap,
+                       X.wgsum, maxw, bst, offsets, cap_blk);
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, 1);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
                        cap_blk, bst, err);
     return hipGetLastError();

@@ -68,10 +68,15 @@ struct SegMeta {
     int32_t jj;              // kSyncJump: index of the shared cut in the target's list
     int32_t n_ext;           // kSyncJump: cuts of the repair walk, the shared cut included
     int32_t ext_dst;         // the repair's cuts go to offsets[ext_dst..] (-1: not on the block's path)
-    int32_t cp_from;         // stitch plan: copy list[cp_from, cp_from + cp_n) to the batch's offsets
-    int32_t cp_n;            //   array at cp_dst (absolute: block * cap_blk + position)
-    int32_t cp_dst;
-    int32_t pad[3];
+    int32_t cp_from;         // stitch plan: copy list[cp_from, cp_from + cp_n) to the block's offsets
+    int32_t cp_n;
+    int32_t cp_dst;          // unused
+    int32_t pad[3];          // stitch scratch: piece size, repair-cut position in the piece
+};
+
+// Stitch path of one block (stitch_path_kernel): on-path jumps, the terminal segment, fallback flag.
+struct PathInfo {
+    int32_t nj, term, fb, pad;
 };
 
 // Per-block state after chunking/stitching.

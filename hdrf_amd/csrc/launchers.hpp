@@ -30,9 +30,23 @@ struct StoreParams {
 // chunking: granule maxima -> lane walk (total_waves waves over the batch's segments) -> repair ->
 // stitch -> fallback.  gm: [nblocks][gstride] bytes, gstride >= max_len / 16 + 4 * 128.
 int lane_spec_cap(int seg_len, int w);
-hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int total_waves, int nsegs,
-                           uint8_t *gm, int gstride, int w, int maxlen, uint32_t *spec, int spec_cap, SegMeta *meta, int *rq, int *rq_count, int rq_cap,
-                           BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st, Marker *mk);
+// scratch of one batch's chunking (api.hip slot buffers)
+struct ChunkScratch {
+    uint8_t *gm;             // granule maxima [nblocks][gstride]
+    int gstride;
+    int *rq, *rq_count;      // repair queue (rq_cap entries)
+    int rq_cap;
+    uint32_t *irr;           // irregular-boundary bitmask over the batch's segments (+2 words)
+    PathInfo *path;          // [nblocks]
+    int *jx;                 // [nblocks][2048] on-path jump sources
+    uint32_t *jt;            // [nblocks][2048] targets | shared-cut index << 24
+    uint32_t *wgsum;         // [nblocks][maxw] piece sums per 256 segments
+    int maxw;
+};
+hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
+                           int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
+                           SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
+                           Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
                       hipStream_t st, Marker *mk);
