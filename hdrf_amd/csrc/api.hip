@@ -610,9 +610,10 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     S.lens.assign(len, len + nblocks);
     S.nblocks = nblocks;
     const uint32_t cur = ++ctx->batch;
-    // chunking shares stream A with SHA unless HDRF_STREAMS=3 (measured: co-running the walk's
-    // readlane/scalar chains with SHA's VALU stream slows both; two stages are faster)
-    static const int nstreams = [] { const char *e = getenv("HDRF_STREAMS"); return e ? atoi(e) : 2; }();
+    // chunking runs on its own stream W (HDRF_STREAMS=2: shares stream A with SHA).  Measured with
+    // the two-pass lane walker (r02): three streams 992 GB/s vs two 919 — the walk's latency-bound
+    // kernels and the HBM-bound granule pass overlap SHA's VALU stream of the previous batch
+    static const int nstreams = [] { const char *e = getenv("HDRF_STREAMS"); return e ? atoi(e) : 3; }();
     hipStream_t W = nstreams == 3 ? ctx->stW : ctx->st, A = ctx->st, Bst = ctx->stB;
     // ---- chunking on W: the slot's previous batch has completed (wait_one ran), so W may overwrite it
     if (after_copy) HIPCK(hipStreamWaitEvent(W, S.copy_done, 0));

@@ -320,10 +320,11 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
 {
     (void)hipMemsetAsync(queue, 0, sizeof(uint32_t) * nblocks, st);
     mk->mark(st);
-    // 4 waves per SIMD measured faster than 8 (fewer concurrent per-lane streams: less L2
-    // thrashing of the 128-B lines two consecutive compressions of a lane share); env knobs for
+    // 2 waves per SIMD (r02, pipelined with chunking on its own stream: 992 GB/s vs 940 at 3 and
+    // 919 at 4) — fewer concurrent per-lane streams thrash L2 less and leave CUs to the
+    // co-running place / granule passes; env knobs for
     // experiments: HDRF_SHA_WAVES (waves per SIMD over 1024 SIMDs), HDRF_SHA_LDS (bytes per WG)
-    static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : 4; }();
+    static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : 2; }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     const int wpb = std::max(4, (per_simd * 1024 / nblocks) & ~3);
     dim3 gf(wpb / 4, nblocks);
