@@ -32,8 +32,15 @@ sys.path.insert(0, ROOT)
 METRIC = "logical GB/s reduced per node (1/2/4/8 GPUs) at 50% dup, bit-exact dedup ratio"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_WI_NS = 1033.0       # v_add_u32 wave-instructions/ns, chip-wide (tools/valu_peak.hip)
-KERNEL_OF = {"walk(spec_walk_kernel)": "spec_walk_kernel", "sha_full(sha_full_kernel)": "sha_full_kernel",
-             "place(place_kernel)": "place_kernel"}
+KERNEL_OF = {"gmax(gmax_kernel)": "gmax_kernel", "walk(lane_walk_kernel)": "lane_walk_kernel",
+             "sha_full(sha_full_kernel)": "sha_full_kernel", "place(place_kernel)": "place_kernel"}
+# stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index + store
+CHAINS = {"W: chunking": ["gmax(gmax_kernel)", "walk(lane_walk_kernel)", "stitch(repair/path/count/scan/copy/fallback)"],
+          "A: SHA": ["sha_full(sha_full_kernel)", "sha_tail(sha_tail_kernel)"],
+          "B: index+store": ["index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
+                             "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
+                             "place(place_kernel)", "compress(lz4_seg/lz4_pack)"]}
+SHA_MIX_CEILING_WI_NS = 425.0  # tools/sha_peak.hip: the SHA-1 instruction mix on register-resident data
 
 
 def load_pmc():
@@ -230,35 +237,66 @@ def main():
     logical = nb * S * world
     value = logical / (el / a.steps) / 1e9
 
-    # ---- roofline of the dominant kernel (algorithmic bytes / HIP-event time) -----------------
+    # ---- rooflines (algorithmic bytes / HIP-event time on the library's streams) ---------------
     nbatch = len(batches)
     chunks_step = int(n_chunks.sum())
     new_bytes = int(store.sum())
+    S_batch = nb * S / nbatch
     per_launch = {   # algorithmic HBM bytes per launch
-        STAGES[0]: (nb * S + 4 * chunks_step) / nbatch,                 # read block bytes, write cuts
-        STAGES[2]: (nb * S + 40 * chunks_step) / nbatch,                # read chunk bytes + offsets, write mid-state
-        STAGES[9]: (2 * new_bytes + 16 * chunks_step) / nbatch,         # read+write new bytes, chunk metadata
+        "gmax(gmax_kernel)": S_batch * (1 + 1 / 16),                      # read block bytes, write granule maxima
+        "walk(lane_walk_kernel)": S_batch / 16 + 4 * chunks_step / nbatch,  # read maxima, write cuts
+        STAGES[2]: S_batch + 40 * chunks_step / nbatch,                   # read chunk bytes + offsets, write mid-state
+        STAGES[9]: (2 * new_bytes + 16 * chunks_step) / nbatch,           # read+write new bytes, chunk metadata
     }
+    avg = {name: ms / a.steps / nbatch for name, ms in zip(STAGES, stage_ms)}
     stages = {}
     for name, ms in zip(STAGES, stage_ms):
-        avg_ms = ms / a.steps / nbatch
-        d = {"ms_per_step": round(ms / a.steps, 3), "avg_launch_ms": round(avg_ms, 4)}
-        if name in per_launch and avg_ms > 0:
-            d["GB_s"] = round(per_launch[name] / (avg_ms * 1e-3) / 1e9, 1)
+        d = {"ms_per_step": round(ms / a.steps, 3), "avg_launch_ms": round(avg[name], 4)}
+        if name in per_launch and avg[name] > 0:
+            d["GB_s"] = round(per_launch[name] / (avg[name] * 1e-3) / 1e9, 1)
         stages[name] = d
-    dom = max(per_launch, key=lambda s: stage_ms[STAGES.index(s)])
-    dom_ms = stage_ms[STAGES.index(dom)] / a.steps / nbatch
-    achieved = per_launch[dom] / (dom_ms * 1e-3) / 1e9
     pmc, pmc_src = load_pmc()
     want = {"blocks": nb, "block_mib": a.block_mib, "batch": B, "n_gpus": world, "hasher": a.hasher}
     if any(pmc.get("_config", {}).get(k) != v for k, v in want.items()):
         pmc, pmc_src = {}, None                        # profiled on another workload: not this one's traffic
-    kname = KERNEL_OF[dom] + ("<5>" if a.hasher == 0 else "<7>") * (dom in (STAGES[2],))
-    prof = pmc.get(kname, {})
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": prof.get("hbm_bytes_per_launch"), "traffic_source": pmc_src,
-                "avg_launch_ms": round(dom_ms, 4), "algorithmic_bytes_per_launch": int(per_launch[dom])}
+    sha_k = "sha_full_kernel" + ("<5>" if a.hasher == 0 else "<7>")
+
+    def hbm_entry(name):
+        ms = avg[name]
+        ach = per_launch[name] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+        return {"bound": "hbm", "kernel": KERNEL_OF[name], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms, 4),
+                "algorithmic_bytes_per_launch": int(per_launch[name]),
+                "traffic": pmc.get(KERNEL_OF[name], {}).get("hbm_bytes_per_launch")}
+
+    # per-stream chains: the batch period is set by the longest one (the critical path)
+    chains = {c: round(sum(avg[s] for s in st), 4) for c, st in CHAINS.items()}
+    crit = max(chains, key=chains.get)
+    chunk_ms = chains["W: chunking"]
+    chunking = {"kernels": "gmax + lane walk + stitch (one batch, in pipeline)", "avg_batch_ms": chunk_ms,
+                "achieved": round(S_batch / (chunk_ms * 1e-3) / 1e9, 1) if chunk_ms > 0 else None,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s (block bytes chunked)",
+                "frac": round(S_batch / (chunk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if chunk_ms > 0 else None,
+                "gmax": hbm_entry("gmax(gmax_kernel)"), "walk": hbm_entry("walk(lane_walk_kernel)")}
+    sha = hbm_entry(STAGES[2])
+    sha_prof = pmc.get(sha_k, {})
+    if sha_prof.get("sq_insts_valu") and avg[STAGES[2]] > 0:
+        # SHA is integer-VALU bound: wave-instructions per launch (PMC SQ_INSTS_VALU) over the
+        # measured launch time, against the full-rate v_add_u32 peak (profiles/r01_valu_peak.txt)
+        # and the SHA-1 instruction mix's own ceiling (tools/sha_peak.hip)
+        wi_ns = sha_prof["sq_insts_valu"] / (avg[STAGES[2]] * 1e6)
+        sha["limiter"] = "int-VALU"
+        sha["valu"] = {"wave_instr_per_ns": round(wi_ns, 1), "peak": VALU_PEAK_WI_NS,
+                       "frac": round(wi_ns / VALU_PEAK_WI_NS, 4), "mix_ceiling": SHA_MIX_CEILING_WI_NS,
+                       "frac_of_mix_ceiling": round(wi_ns / SHA_MIX_CEILING_WI_NS, 4),
+                       "sq_insts_valu_per_launch": int(sha_prof["sq_insts_valu"])}
+    place = hbm_entry(STAGES[9])
+    # the line's roofline: the dominant kernel of the critical chain
+    top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place}[crit]
+    roofline = dict(top)
+    roofline.update({"traffic_source": pmc_src, "critical_path": crit, "chains_ms_per_batch": chains,
+                     "batch_period_ms": round(el / a.steps / nbatch * 1e3, 4),
+                     "chunking": chunking, "sha": sha, "place": place})
     if alone_ms is not None:
         # per-kernel figures of the untimed serial pass (not part of `value`)
         ra = {}
@@ -268,21 +306,12 @@ def main():
                 ach = per_launch[name] / (ms * 1e-3) / 1e9
                 ra[name] = {"avg_launch_ms": round(ms, 4), "achieved_GB_s": round(ach, 1),
                             "frac_hbm": round(ach / HBM_PEAK_GBS, 4)}
-                sha_prof = pmc.get(KERNEL_OF[name] + ("<5>" if a.hasher == 0 else "<7>"), {})
-                if name == STAGES[2] and sha_prof.get("sq_insts_valu"):
-                    wi_ns = sha_prof["sq_insts_valu"] / (ms * 1e6)
-                    ra[name]["valu_frac"] = round(wi_ns / VALU_PEAK_WI_NS, 4)
+        if ra.get(STAGES[2]) and sha_prof.get("sq_insts_valu"):
+            ra[STAGES[2]]["valu_frac"] = round(sha_prof["sq_insts_valu"] / (ra[STAGES[2]]["avg_launch_ms"] * 1e6)
+                                              / VALU_PEAK_WI_NS, 4)
         roofline["alone"] = ra
         roofline["alone_note"] = ("same kernels in one untimed serial pass (one batch at a time); the "
                                   "in-pipeline figures above include co-running batches")
-    if dom == STAGES[2] and prof.get("sq_insts_valu"):
-        # SHA is integer-VALU bound: wave-instructions per launch (PMC SQ_INSTS_VALU) over the
-        # measured launch time, against the full-rate v_add_u32 peak (profiles/r01_valu_peak.txt)
-        wi_ns = prof["sq_insts_valu"] / (dom_ms * 1e6)
-        roofline["limiter"] = "int-VALU"
-        roofline["valu"] = {"wave_instr_per_ns": round(wi_ns, 1), "peak": VALU_PEAK_WI_NS,
-                            "frac": round(wi_ns / VALU_PEAK_WI_NS, 4),
-                            "sq_insts_valu_per_launch": int(prof["sq_insts_valu"])}
 
     node_new, node_chunks = new_bytes, chunks_step
     if dist is not None:
@@ -377,36 +406,48 @@ def read_bench(ctx, dev, S, m, hasher, compressor):
 
 def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1):
     """CPU oracle (C restatement of the reference) on the first m blocks of the same corpus, timed
-    two ways: one thread, and the reference's concurrency shape (chunk + hash of later blocks on
-    worker threads ahead of the ordered index/store part, DN/DataDeduplicator.java:122-204) with
-    the GPU box's CPU share of threads.  Both check per-block storeSize == the GPU's (bit-exact
-    dedup ratio); for the compression stage a fresh GPU context reducing the same m blocks must
-    write byte-identical container files (closed Lz4Codec files and open raw containers)."""
+    in BASELINE.md's two shapes plus one thread:
+      reference  the reference's own concurrency, blocks serialised: per block 1 chunking thread,
+                 3 threadedHasher threads over the chunk ranges, then the ordered index/store part
+                 (DN/DataDeduplicator.java:122-204, :578-641)
+      all_cores  every usable core (sched_getaffinity): chunk + hash of later blocks on N-1 worker
+                 threads ahead of 1 ordered index/store thread
+    All check per-block storeSize == the GPU's (bit-exact dedup ratio); for the compression stage a
+    fresh GPU context reducing the same m blocks must write byte-identical container files."""
     from oracle.oracle import Oracle
+    blks = [ctx.d2h(dev + b * S, S) for b in range(m)]
+    ids = list(range(m))
+    usable = len(os.sched_getaffinity(0))
     ora = Oracle(hasher=hasher, compressor=compressor)
-    t = 0.0
-    mism = 0
-    blks = []
-    for b in range(m):
-        blk = ctx.d2h(dev + b * S, S)
-        blks.append(blk)
-        t0 = time.perf_counter()
-        r = ora.reduce(blk, b)
-        t += time.perf_counter() - t0
-        mism += int(r["store_size"] != gpu_store[b])
-    nthr = max(1, min(16, (os.cpu_count() or 2) - 1))
+    t0 = time.perf_counter()
+    ss1 = [ora.reduce(blk, b)["store_size"] for b, blk in enumerate(blks)]
+    t1 = time.perf_counter() - t0
+    ref = Oracle(hasher=hasher, compressor=compressor)
+    t0 = time.perf_counter()
+    ssr = ref.reduce_ref_shape(blks, ids, 3)
+    tr = time.perf_counter() - t0
+    nthr = max(1, usable - 1)
     par = Oracle(hasher=hasher, compressor=compressor)
     t0 = time.perf_counter()
-    ss = par.reduce_many(blks, list(range(m)), nthr)
+    ssp = par.reduce_many(blks, ids, nthr)
     tp = time.perf_counter() - t0
-    mism_p = int(sum(int(ss[b] != gpu_store[b]) for b in range(m)))
+
+    def mism(ss):
+        return int(sum(int(ss[b] != gpu_store[b]) for b in range(m)))
+
     sample = "first %d of the same blocks (%.1f GiB), oracle/hdrf_oracle.c%s" % (
         m, m * S / 2**30, " with lz4 r123 containers" if compressor == 2 else "")
     out = {"value": round(m * S / tp / 1e9, 4), "unit": "GB/s", "cores": nthr + 1, "kind": "port",
-           "sample": sample + ", %d chunk+hash worker threads + 1 ordered index/store thread, %.1f s" % (nthr, tp),
-           "store_size_mismatches": mism_p, "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
-           "single_thread": {"value": round(m * S / t / 1e9, 4), "unit": "GB/s", "cores": 1,
-                             "seconds": round(t, 2), "store_size_mismatches": mism}}
+           "sample": sample + ", all usable cores: %d chunk+hash worker threads + 1 ordered index/store thread, %.1f s"
+                     % (nthr, tp),
+           "store_size_mismatches": mism(ssp), "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+           "usable_cores": usable,
+           "reference_shape": {"value": round(m * S / tr / 1e9, 4), "unit": "GB/s", "cores": 4,
+                               "threads": "per block 1 chunking + 3 hasher threads, then the ordered part; "
+                                          "blocks serialised", "seconds": round(tr, 2),
+                               "store_size_mismatches": mism(ssr)},
+           "single_thread": {"value": round(m * S / t1 / 1e9, 4), "unit": "GB/s", "cores": 1,
+                             "seconds": round(t1, 2), "store_size_mismatches": mism(ss1)}}
     if compressor == 2:
         out["container_file_mismatches"], out["containers_checked"] = _check_containers(ctx, dev, S, m, ora, hasher)
     return out

@@ -497,11 +497,6 @@ static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t l
     ctx->containers[id] = ContainerInfo{slot, len, closed, clen};
 }
 
-// Validate a batch and fill the slot's (pinned) descriptors: the lane segmentation of the chunking
-// pass (chunk.hip).  seg_len = segment_bytes / 63 rounded to a multiple of window + 2, within
-// [4, 24] x 702 B, and shortened (down to 6 x 702 B) while the batch would give the lane walk fewer
-// than 1024 waves (one-block calls).  Grows the slot's speculative lists when needed (the slot's
-// previous batch has completed).
 static ChunkScratch chunk_scratch(Slot &S)
 {
     ChunkScratch X;
@@ -510,6 +505,10 @@ static ChunkScratch chunk_scratch(Slot &S)
     return X;
 }
 
+// Validate a batch and fill the slot's (pinned) descriptors: the lane segmentation of the chunking
+// pass (chunk.hip).  seg_len = segment_bytes / 63 rounded down to a multiple of window + 2, within
+// [4, 20] x 702 B.  Grows the slot's speculative lists when needed (the slot's previous batch has
+// completed).
 static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t *const *dev_data,
                           const uint64_t *len, const uint64_t *readable)
 {
@@ -526,8 +525,11 @@ static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t
     }
     S.max_len = max_len;
     const int unit = c.window + 2;
-    int wins = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / unit)));
-    while (wins > 6 && total / ((int64_t)wins * unit * kWaveSegs) < 1024) wins--;
+    // one lane per segment: a block of any size has thousands of lanes, so the segment length
+    // follows segment_bytes alone (shorter segments only raise the share of boundaries whose
+    // chains have not met within the next segment, which then take the repair pass)
+    const int wins = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / unit)));
+    (void)total;
     const int seg_len = wins * unit;
     int seg0 = 0, wave0 = 0;
     for (int b = 0; b < nblocks; b++) {

@@ -90,6 +90,7 @@ struct WalkCfg {
     int size;      // block length
     int w;         // window (700)
     int maxlen;    // forced-cut length (1,000,000)
+    const uint8_t *gm;   // the block's granule maxima (gmax_kernel), for long searches
 };
 
 enum : int { kWindow = 0, kSearchFF = 1, kSearchGen = 2 };
@@ -101,6 +102,7 @@ struct Chain {
     uint32_t m;    // threshold (biased) of a general search
     bool first;    // the very first chunk of a block: M has no 0 floor
     bool ended;    // chain ended because the data ended
+    bool jump;     // the search skipped ahead (granule maxima): re-seed the view at q
 };
 
 __device__ __forceinline__ uint4 tile_raw(const WalkCfg &c, int X)
@@ -243,6 +245,47 @@ __device__ __forceinline__ int next_ff(uint32_t fA, uint32_t fB, unsigned long l
     return 0x7fffffff;
 }
 
+// the same for a dword of already biased bytes: maj(x7, C7, s7)
+__device__ __forceinline__ uint32_t ge_flags_b(uint32_t x, uint32_t C, uint32_t Cm)
+{
+    const uint32_t s = (x & 0x7f7f7f7fu) + Cm;
+    return __builtin_amdgcn_bitop3_b32(x, C, s, 0xe8) & 0x80808080u;   // 0xe8: maj(x, C, s)
+}
+// gather the bit-7 flags of four dwords into 16 bits (v_dot4_u32_u8, weights 1..128 per pair)
+__device__ __forceinline__ uint32_t gather16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3)
+{
+    const uint32_t lo = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(f3, 0x80402010u, __builtin_amdgcn_udot4(f2, 0x08040201u, 0u, false), false);
+    return (lo | (hi << 8)) >> 7;
+}
+// First position >= q (inside a granule whose maximum is >= m, biased) up to lim, or lim + 1: the
+// wave scans the granule maxima 1,024 at a time (16 per lane, one 16-B load), so a long search
+// (the forced-cut regime, text windows with high maxima) costs a load per 16 KiB instead of a pass
+// over every tile.
+__device__ int gm_skip(const uint8_t *gm, int q, int lim, uint32_t m)
+{
+    if (m == 0) return q;
+    const uint32_t C = __builtin_amdgcn_perm(256u - m, 256u - m, 0u), Cm = C & 0x7f7f7f7fu;
+    const int gq = q >> 4, gl = lim >> 4;
+    for (int g0 = gq & ~15; g0 <= gl; g0 += 1024) {
+        const int gb = g0 + 16 * lane_id();
+        uint32_t h = 0;
+        if (gb <= gl) {
+            const uint4 v = ld16(gm + gb);
+            h = gather16(ge_flags_b(v.x, C, Cm), ge_flags_b(v.y, C, Cm), ge_flags_b(v.z, C, Cm), ge_flags_b(v.w, C, Cm));
+            if (gb < gq) h &= gq - gb >= 16 ? 0u : (0xffffu << (gq - gb));
+            if (gl - gb < 15) h &= 0xffffu >> (15 - (gl - gb));
+        }
+        const unsigned long long bal = ballot64(h != 0);
+        if (bal) {
+            const int L = __builtin_ctzll(bal);
+            const int g = g0 + 16 * L + __builtin_ctz(rdlane(h, L));
+            return max(16 * g, q);
+        }
+    }
+    return lim + 1;
+}
+
 struct ListSink;
 
 // Advance the chain as far as the view [T, T+2048) allows.  Returns true when the view must
@@ -330,6 +373,11 @@ __device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const 
             else { ch.ended = true; return false; }
         } else {
             ch.q = max(ch.q, T + 2048);                                // continue after the advance
+            if (ch.lim > T + 4096) {
+                // long search: the granule maxima say where the next candidate byte can be
+                const int q2 = gm_skip(c.gm, ch.q, ch.lim, ch.state == kSearchFF ? 0xffu : ch.m);
+                if (q2 >= T + 4096) { ch.q = min(q2, ch.lim); ch.jump = true; }
+            }
             return true;
         }
         cut = __builtin_amdgcn_readfirstlane(cut);
@@ -392,19 +440,26 @@ __device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, 
 {
     Chain ch;
     ch.p = p; ch.state = kWindow; ch.q = 0; ch.lim = 0; ch.m = 0; ch.first = first; ch.ended = false;
+    ch.jump = false;
     int T = p & ~1023;
-    uint4 R0 = tile_raw(c, T), R1 = tile_raw(c, T + 1024), R2 = tile_raw(c, T + 2048), R3 = tile_raw(c, T + 3072);
-    uint32_t f0 = ffmask16(R0), f1 = ffmask16(R1), f2 = 0, f3 = 0;
-    unsigned long long b0 = ballot64(f0 != 0), b1 = ballot64(f1 != 0), b2 = 0, b3 = 0;
-    for (;;) {
-        if (!process_view(c, ch, R0, R1, f0, f1, b0, b1, T, sink, stop)) break;
-        T += 1024; f2 = ffmask16(R2); b2 = ballot64(f2 != 0); R0 = tile_raw(c, T + 3072);
-        if (!process_view(c, ch, R1, R2, f1, f2, b1, b2, T, sink, stop)) break;
-        T += 1024; f3 = ffmask16(R3); b3 = ballot64(f3 != 0); R1 = tile_raw(c, T + 3072);
-        if (!process_view(c, ch, R2, R3, f2, f3, b2, b3, T, sink, stop)) break;
-        T += 1024; f0 = ffmask16(R0); b0 = ballot64(f0 != 0); R2 = tile_raw(c, T + 3072);
-        if (!process_view(c, ch, R3, R0, f3, f0, b3, b0, T, sink, stop)) break;
-        T += 1024; f1 = ffmask16(R1); b1 = ballot64(f1 != 0); R3 = tile_raw(c, T + 3072);
+    for (;;) {                                    // (re)seed the view at T
+        uint4 R0 = tile_raw(c, T), R1 = tile_raw(c, T + 1024), R2 = tile_raw(c, T + 2048), R3 = tile_raw(c, T + 3072);
+        uint32_t f0 = ffmask16(R0), f1 = ffmask16(R1), f2 = 0, f3 = 0;
+        unsigned long long b0 = ballot64(f0 != 0), b1 = ballot64(f1 != 0), b2 = 0, b3 = 0;
+        bool go;
+        for (;;) {
+            if (!(go = process_view(c, ch, R0, R1, f0, f1, b0, b1, T, sink, stop)) || ch.jump) break;
+            T += 1024; f2 = ffmask16(R2); b2 = ballot64(f2 != 0); R0 = tile_raw(c, T + 3072);
+            if (!(go = process_view(c, ch, R1, R2, f1, f2, b1, b2, T, sink, stop)) || ch.jump) break;
+            T += 1024; f3 = ffmask16(R3); b3 = ballot64(f3 != 0); R1 = tile_raw(c, T + 3072);
+            if (!(go = process_view(c, ch, R2, R3, f2, f3, b2, b3, T, sink, stop)) || ch.jump) break;
+            T += 1024; f0 = ffmask16(R0); b0 = ballot64(f0 != 0); R2 = tile_raw(c, T + 3072);
+            if (!(go = process_view(c, ch, R3, R0, f3, f0, b3, b0, T, sink, stop)) || ch.jump) break;
+            T += 1024; f1 = ffmask16(R1); b1 = ballot64(f1 != 0); R3 = tile_raw(c, T + 3072);
+        }
+        if (!go) break;
+        ch.jump = false;
+        T = ch.q & ~1023;
     }
     return ch.ended;
 }
@@ -506,19 +561,6 @@ __device__ __forceinline__ uint32_t ge_flags(uint32_t d, uint32_t C, uint32_t Cm
 {
     const uint32_t s = (d & 0x7f7f7f7fu) + Cm;
     return __builtin_amdgcn_bitop3_b32(d, C, s, 0x8e) & 0x80808080u;   // 0x8e: maj(NOT d, C, s)
-}
-// the same for a dword of already biased bytes: maj(x7, C7, s7)
-__device__ __forceinline__ uint32_t ge_flags_b(uint32_t x, uint32_t C, uint32_t Cm)
-{
-    const uint32_t s = (x & 0x7f7f7f7fu) + Cm;
-    return __builtin_amdgcn_bitop3_b32(x, C, s, 0xe8) & 0x80808080u;   // 0xe8: maj(x, C, s)
-}
-// gather the bit-7 flags of four dwords into 16 bits (v_dot4_u32_u8, weights 1..128 per pair)
-__device__ __forceinline__ uint32_t gather16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3)
-{
-    const uint32_t lo = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
-    const uint32_t hi = __builtin_amdgcn_udot4(f3, 0x80402010u, __builtin_amdgcn_udot4(f2, 0x08040201u, 0u, false), false);
-    return (lo | (hi << 8)) >> 7;
 }
 // 16-bit mask of the bytes of a raw granule whose biased value is >= m (m >= 1)
 __device__ __forceinline__ uint32_t gran_ge(uint4 v, uint32_t C, uint32_t Cm)
@@ -760,7 +802,8 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
                                                           int rq_cap, int w, int maxlen,
                                                           const uint32_t *__restrict__ spec, int cap,
                                                           SegMeta *__restrict__ meta, uint32_t *__restrict__ offsets,
-                                                          int cap_blk, int emit)
+                                                          int cap_blk, const uint8_t *__restrict__ gm, int gstride,
+                                                          int emit)
 {
     const int nw = gridDim.x * 4;
     const int cnt = min(*rq_count, rq_cap);
@@ -779,7 +822,7 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
         const bool first = n == 0 && s_k == 0;
         WalkCfg W;
         W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
-        W.w = w; W.maxlen = maxlen;
+        W.w = w; W.maxlen = maxlen; W.gm = gm + (size_t)bi * gstride;
         if (!emit) {
             CountSink sink;
             sink.cap = kRepairCuts; sink.cnt = 0; sink.stage = 0;
@@ -1031,7 +1074,8 @@ __global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__res
 //    the block size appended.
 __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__restrict__ blocks, int w, int maxlen,
                                                            uint32_t *__restrict__ offsets, int cap_blk,
-                                                           BlockState *__restrict__ bst, int *__restrict__ err)
+                                                           BlockState *__restrict__ bst, const uint8_t *__restrict__ gm,
+                                                           int gstride, int *__restrict__ err)
 {
     const int b = blockIdx.x;
     const BlockDesc bd = blocks[b];
@@ -1040,7 +1084,7 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
     if (s.fail_dst >= 0) {
         WalkCfg W;
         W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
-        W.w = w; W.maxlen = maxlen;
+        W.w = w; W.maxlen = maxlen; W.gm = gm + (size_t)b * gstride;
         const bool first = s.fail_dst == 0;
         const int p0 = first ? 0 : (int)off[s.fail_dst - 1];
         ListSink sink;
@@ -1087,7 +1131,7 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, 0);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0);
     hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt);
     hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt,
                        X.wgsum, maxw, err);
@@ -1096,9 +1140,9 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     hipLaunchKernelGGL(stitch_copy_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, spec, spec_cap,
                        X.wgsum, maxw, bst, offsets, cap_blk);
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
-                       cap_blk, bst, err);
+                       cap_blk, bst, X.gm, X.gstride, err);
     return hipGetLastError();
 }
 }  // namespace hdrf

@@ -556,6 +556,64 @@ int64_t hdrf_oracle_reduce_many(hdrf_oracle *o, const uint8_t *const *blocks, co
     return rc < 0 ? rc : nblocks;
 }
 
+/* The reference's own concurrency shape, blocks serialised (BASELINE.md CPU plan 1): per block
+ * chunking on one thread (DN/DataDeduplicator.java:122), then nhash threadedHasher threads over
+ * the chunk ranges [n*t/nhash, n*(t+1)/nhash) (:168-185, :578-641), then the ordered part on the
+ * calling thread (Redis lookups, checkChunk, storers, storeDB).  The reference's 3 storer threads
+ * copy into 3 different containers; here those appends run on the calling thread (a memcpy share
+ * of the block's time well under its hashing).  Results equal hdrf_oracle_reduce in order. */
+typedef struct {
+    int hasher, H;
+    const uint8_t *data;
+    const uint32_t *off;
+    uint8_t *dig;
+    int64_t k0, k1;
+} hash_range;
+
+static void *hash_range_worker(void *arg)
+{
+    hash_range *r = (hash_range *)arg;
+    int64_t cur = r->k0 ? r->off[r->k0 - 1] : 0;
+    for (int64_t k = r->k0; k < r->k1; k++) {
+        if (r->hasher == 0) hdrf_oracle_sha1(r->data + cur, (uint64_t)(r->off[k] - cur), r->dig + k * r->H);
+        else hdrf_oracle_sha224(r->data + cur, (uint64_t)(r->off[k] - cur), r->dig + k * r->H);
+        cur = r->off[k];
+    }
+    return NULL;
+}
+
+int64_t hdrf_oracle_reduce_ref_shape(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
+                                     const int64_t *ids, int64_t nblocks, int nhash, int64_t *store_sizes)
+{
+    if (nhash < 1) nhash = 1;
+    if (nhash > 64) nhash = 64;
+    for (int64_t i = 0; i < nblocks; i++) {
+        const int64_t ocap = sizes[i] / 700 + 2;
+        uint32_t *off = (uint32_t *)malloc((size_t)ocap * sizeof(uint32_t));
+        if (!off) return -2;
+        const int64_t n = hdrf_oracle_chunk(blocks[i], sizes[i], off, ocap);
+        if (n < 0) { free(off); return -1; }
+        uint8_t *dig = (uint8_t *)malloc((size_t)n * o->H + 1);
+        if (!dig) { free(off); return -2; }
+        pthread_t th[64];
+        hash_range rg[64];
+        int started[64] = {0};
+        for (int t = 0; t < nhash; t++) {
+            rg[t].hasher = o->hasher; rg[t].H = o->H; rg[t].data = blocks[i]; rg[t].off = off; rg[t].dig = dig;
+            rg[t].k0 = n * t / nhash; rg[t].k1 = n * (t + 1) / nhash;
+            started[t] = pthread_create(&th[t], NULL, hash_range_worker, &rg[t]) == 0;
+            if (!started[t]) hash_range_worker(&rg[t]);
+        }
+        for (int t = 0; t < nhash; t++)
+            if (started[t]) pthread_join(th[t], NULL);
+        int64_t ss = 0;
+        const int64_t r = reduce_hashed(o, blocks[i], sizes[i], ids[i], off, n, dig, NULL, NULL, NULL, NULL, &ss);
+        if (r < 0) return r;
+        if (store_sizes) store_sizes[i] = ss;
+    }
+    return nblocks;
+}
+
 int hdrf_oracle_index_get(const hdrf_oracle *o, const uint8_t *digest, uint8_t out11[11])
 {
     int64_t f = kv_find(&o->index, digest);

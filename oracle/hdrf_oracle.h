@@ -51,6 +51,10 @@ int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, in
  * the ordered part handles them in arrival order; same results as hdrf_oracle_reduce in order. */
 int64_t hdrf_oracle_reduce_many(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
                                 const int64_t *ids, int64_t nblocks, int nthreads, int64_t *store_sizes);
+/* The reference's concurrency shape, blocks serialised: per block 1 chunking thread + nhash hasher
+ * threads over chunk ranges, then the ordered part (BASELINE.md CPU plan 1). */
+int64_t hdrf_oracle_reduce_ref_shape(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
+                                     const int64_t *ids, int64_t nblocks, int nhash, int64_t *store_sizes);
 int hdrf_oracle_index_get(const hdrf_oracle *o, const uint8_t *digest, uint8_t out11[11]);
 int64_t hdrf_oracle_index_count(const hdrf_oracle *o);
 /* Dump every (digest, value) pair, sorted by digest bytes. Returns count (or -needed if cap small). */

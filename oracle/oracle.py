@@ -69,6 +69,8 @@ def lib():
                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                               ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
         L.hdrf_oracle_reduce_many.restype = ctypes.c_int64
+        L.hdrf_oracle_reduce_ref_shape.argtypes = L.hdrf_oracle_reduce_many.argtypes
+        L.hdrf_oracle_reduce_ref_shape.restype = ctypes.c_int64
         L.hdrf_oracle_hadoop_lz4_stream_bound.argtypes = [ctypes.c_int64, ctypes.c_int64]
         L.hdrf_oracle_hadoop_lz4_stream_bound.restype = ctypes.c_int64
         L.hdrf_oracle_hadoop_lz4_stream.argtypes = [_u8p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, _u8p]
@@ -241,6 +243,23 @@ class Oracle:
                                            int(nthreads), ss.ctypes.data_as(p64))
         if rc < 0:
             raise RuntimeError(f"hdrf_oracle_reduce_many: {rc}")
+        return ss[:n]
+
+    def reduce_ref_shape(self, blocks, block_ids, nhash=3):
+        """The reference's concurrency shape, blocks serialised: per block 1 chunking thread, nhash
+        hasher threads over chunk ranges, then the ordered part.  Returns per-block storeSize."""
+        arrs = [_as_u8(b) for b in blocks]
+        n = len(arrs)
+        keep = [a if a.size else np.zeros(1, np.uint8) for a in arrs]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in keep])
+        sizes = np.array([a.size for a in arrs], np.int64)
+        ids = np.ascontiguousarray(block_ids, np.int64)
+        ss = np.zeros(max(n, 1), np.int64)
+        p64 = ctypes.POINTER(ctypes.c_int64)
+        rc = lib().hdrf_oracle_reduce_ref_shape(self._h, ptrs, sizes.ctypes.data_as(p64), ids.ctypes.data_as(p64),
+                                                n, int(nhash), ss.ctypes.data_as(p64))
+        if rc < 0:
+            raise RuntimeError(f"hdrf_oracle_reduce_ref_shape: {rc}")
         return ss[:n]
 
     def reduce(self, data, block_id):
