@@ -13,6 +13,9 @@
 // So while batch k is being indexed and stored, batch k+1 is already being chunked and hashed.
 // hdrf_submit_batch enqueues; hdrf_wait_batch completes the oldest batch (host bookkeeping);
 // hdrf_reduce_batch does both.
+#include <condition_variable>
+#include <mutex>
+#include <set>
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -84,6 +87,7 @@ struct Slot {
     std::vector<uint64_t> ids, lens;
     int nblocks = 0;
     bool pending = false;
+    uint32_t close_bound = 0;                 // durable containers: closes this batch may make per range
     uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
     RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
     hipEvent_t recipe_done = nullptr;         // the copies read d_dig: the slot's next SHA waits
@@ -151,6 +155,19 @@ struct hdrf_ctx {
     uint64_t gx_nfront = 0, gx_nfwait = 0, gx_nback = 0;   // fronts launched / waited, batches committed
     int gx_bphase = 0;                           // back batch: 0 owner next, 1 decide, 2 flush, 3 place, 4 commit
     hdrf_stats stats{};                          // cumulative since the last reset
+    // concurrency: every entry point holds mu; ticketed reductions also wait for their turn
+    // (AIWriteQueue order, DN/DataDeduplicator.java:124-158, DN/DDRunner.java:20-36)
+    std::recursive_mutex mu;
+    std::condition_variable_any turn;
+    uint64_t next_ticket = 0, serving = 0;
+    std::set<uint64_t> cancelled;
+    // durable containers (cfg.retain_containers): closed containers stay in their arena slot until
+    // drained; open containers' bytes already handed out
+    std::vector<uint32_t> pend_closed;
+    uint32_t undrained[4] = {0, 0, 0, 0};
+    uint32_t inflight_bound = 0;
+    std::map<uint32_t, int64_t> handed;
+    bool lost = false;
     // timing
     bool timing = false;
     double stage_ms[kStages] = {};
@@ -165,6 +182,11 @@ struct hdrf_ctx {
             return HDRF_E_HIP;                                                         \
         }                                                                              \
     } while (0)
+
+// every entry point: one caller at a time (a null context is checked by the function itself)
+#define HDRF_LOCK(c)                                                                                 \
+    std::unique_lock<std::recursive_mutex> lk_ =                                                     \
+        (c) ? std::unique_lock<std::recursive_mutex>((c)->mu) : std::unique_lock<std::recursive_mutex>()
 
 static unsigned long long tag_mask(const hdrf_ctx *ctx)
 {
@@ -226,6 +248,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
     cfg->device = 0;
     cfg->max_block_bytes = 128ll << 20;
     cfg->max_batch_blocks = 8;
+    cfg->retain_containers = 0;
     cfg->index_log2 = 22;
     cfg->arena_slots = 16;
     cfg->segment_bytes = 1 << 20;
@@ -378,6 +401,11 @@ static int init_state(hdrf_ctx *ctx)
     ctx->gx_nfront = ctx->gx_nfwait = ctx->gx_nback = 0;
     ctx->gx_bphase = 0;
     ctx->stats = hdrf_stats{};
+    ctx->pend_closed.clear();
+    for (auto &u : ctx->undrained) u = 0;
+    ctx->inflight_bound = 0;
+    ctx->handed.clear();
+    ctx->lost = false;
     return 0;
 }
 
@@ -484,6 +512,7 @@ extern "C" int hdrf_digest_len(const hdrf_ctx *ctx) { return ctx ? ctx->H : HDRF
 
 extern "C" int hdrf_reset(hdrf_ctx *ctx)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     return init_state(ctx);
 }
@@ -492,7 +521,13 @@ extern "C" int hdrf_reset(hdrf_ctx *ctx)
 static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t len, int closed, uint32_t clen = 0)
 {
     auto so = ctx->slot_owner.find(slot);
-    if (so != ctx->slot_owner.end() && so->second != id) ctx->containers.erase(so->second);
+    if (so != ctx->slot_owner.end() && so->second != id) {
+        // durable mode: the ring check in submit() keeps undrained closed containers out of reach
+        if (ctx->cfg.retain_containers)
+            for (uint32_t u : ctx->pend_closed)
+                if (u == so->second) ctx->lost = true;
+        ctx->containers.erase(so->second);
+    }
     ctx->slot_owner[slot] = id;
     ctx->containers[id] = ContainerInfo{slot, len, closed, clen};
 }
@@ -598,6 +633,17 @@ static float elapsed(hipEvent_t a, hipEvent_t b)
     return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.f;
 }
 
+// Upper bound on the containers one storer range can close in a batch of `bytes` new bytes: a
+// container closes when its length plus the next chunk exceeds container_max, so it holds more
+// than container_max - max_chunk - 1 bytes, and two consecutive closes hold more than
+// container_max between them (DN/DataDeduplicator.java:748-796).
+static uint32_t close_bound(const hdrf_cfg &c, uint64_t bytes)
+{
+    const uint64_t a = bytes / std::max<uint64_t>(1, (uint64_t)c.container_max - (uint64_t)c.max_chunk - 1);
+    const uint64_t b = 2 * bytes / c.container_max;
+    return (uint32_t)std::min<uint64_t>(std::min(a, b), 1u << 30) + 1;
+}
+
 // Enqueue one batch: front on stream A, back on stream B (see the file comment).
 static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                   const uint64_t *readable, const uint64_t *block_ids, bool after_copy = false)
@@ -607,6 +653,22 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     Slot &S = ctx->sl[ctx->nsub % kSlots];
     const hdrf_cfg &c = ctx->cfg;
     if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable)) return rc;
+    S.close_bound = 0;
+    if (c.retain_containers) {
+        // durable containers: the ring of every storer range (arena_slots / 4 slots, its open
+        // container included) must keep room for the closes this batch and the batches in flight
+        // can make without reaching an undrained closed container
+        uint64_t bytes = 0;
+        for (int b = 0; b < nblocks; b++) bytes += len[b];
+        const uint32_t bound = close_bound(c, bytes), per = (uint32_t)(c.arena_slots / 4);
+        for (int t = 0; t < c.n_thread; t++)
+            if ((uint64_t)ctx->undrained[t] + ctx->inflight_bound + bound > per - 1)
+                return set_err(ctx, HDRF_E_CAPACITY, "container arena: undrained closed containers fill the ring of "
+                                                     "storer range " + std::to_string(t) +
+                                                     " (hdrf_drain_containers first)");
+        S.close_bound = bound;
+        ctx->inflight_bound += bound;
+    }
     S.ids.assign(nblocks, 0);
     if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
     S.lens.assign(len, len + nblocks);
@@ -739,16 +801,23 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
     const int nblocks = S.nblocks;
     const uint32_t nclosed = *S.h_nclosed;
     if ((int)nclosed > ctx->closed_cap) return set_err(ctx, HDRF_E_CAPACITY, "closed-container list overflow");
+    ctx->inflight_bound -= std::min(ctx->inflight_bound, S.close_bound);
+    S.close_bound = 0;
     for (uint32_t i = 0; i < nclosed; i++) {
         const ClosedRec &r = S.h_closed[i];
         const uint32_t flen = c.compressor == 2 ? S.h_filelen[i] : r.len;
         note_container(ctx, r.id, r.slot, r.len, 1, flen);
+        if (c.retain_containers) {
+            ctx->pend_closed.push_back(r.id);
+            ctx->undrained[std::min<uint32_t>(r.id >> 22, 3)]++;
+        }
         ctx->stats.closed_containers++;
         ctx->stats.closed_raw_bytes += r.len;
         ctx->stats.closed_file_bytes += flen;
     }
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) note_container(ctx, ctx->h_alloc.id[t], ctx->h_alloc.slot[t], ctx->h_alloc.cur[t], 0);
+    if (ctx->lost) return set_err(ctx, HDRF_E_CAPACITY, "an undrained closed container's arena slot was reused");
     ctx->have_alloc = 1;                              // storeDB always SETs "blockID" (:389)
     for (int b = 0; b < nblocks; b++) {
         ctx->stats.blocks++;
@@ -799,8 +868,11 @@ static int wait_one(hdrf_ctx *ctx)
 extern "C" int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                                  const uint64_t *readable, const uint64_t *block_ids)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
+    if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)     // every submit pairs with one hdrf_wait_batch
+        return set_err(ctx, HDRF_E_CAPACITY, "pipeline full: hdrf_wait_batch first");
     return submit(ctx, nblocks, dev_data, len, readable, block_ids);
 }
 
@@ -810,6 +882,7 @@ extern "C" int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *
 extern "C" int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
                                 const uint64_t *block_ids)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
     if (nblocks < 1 || nblocks > ctx->max_batch || !host_data || !len) return set_err(ctx, HDRF_E_INVAL, "bad batch arguments");
@@ -817,8 +890,8 @@ extern "C" int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *c
         if ((int64_t)len[b] > ctx->cfg.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
         if (len[b] && !host_data[b]) return set_err(ctx, HDRF_E_INVAL, "null block data");
     }
-    if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)
-        if (int rc = wait_one(ctx)) return rc;
+    if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)     // every submit pairs with one hdrf_wait_batch
+        return set_err(ctx, HDRF_E_CAPACITY, "pipeline full: hdrf_wait_batch first");
     Slot &S = ctx->sl[ctx->nsub % kSlots];
     const uint64_t stride = ((uint64_t)ctx->cfg.max_block_bytes + kSlack + 255) & ~(uint64_t)255;
     if (!S.d_hstage) {                                 // first host batch of this slot
@@ -903,6 +976,7 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
                                      uint64_t len, uint64_t readable, const uint64_t *writes, int32_t nwrites,
                                      uint8_t *out, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (codec != 4 && codec != 0 && codec != 5)
         return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec) are implemented");
@@ -998,6 +1072,7 @@ extern "C" int64_t hdrf_stream_block_host(hdrf_ctx *ctx, int32_t codec, uint64_t
                                           uint64_t len, const uint64_t *writes, int32_t nwrites, uint8_t *out,
                                           int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || (len && !data)) return HDRF_E_INVAL;
     if (codec != 4 && codec != 0 && codec != 5)
         return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec) are implemented");
@@ -1071,6 +1146,7 @@ static int64_t decode_file(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uin
 // compressor 2 (DN/DataConstructor.java:495-500) and for stream-mode blocks (:171-176).
 extern "C" int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     return decode_file(ctx, file, flen, dev_out, cap);
 }
@@ -1080,6 +1156,7 @@ extern "C" int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int6
 extern "C" int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const uint8_t *file, int64_t flen,
                                            uint8_t *dev_out, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (codec != 0 && codec != 4)
         return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec) and 4 (Lz4Codec) are implemented");
@@ -1090,6 +1167,7 @@ extern "C" int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const u
 extern "C" int hdrf_gzip_match_pass(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t len, uint32_t *dev_prev,
                                     uint32_t *dev_out128, uint32_t *dev_out32)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (len && (!dev_data || !dev_prev || !dev_out128 || !dev_out32)) return set_err(ctx, HDRF_E_INVAL, "null buffer");
     if (len >= (1ull << 31)) return set_err(ctx, HDRF_E_INVAL, "gzip match pass: len must be < 2^31");
@@ -1103,6 +1181,7 @@ extern "C" int hdrf_gzip_match_pass(hdrf_ctx *ctx, const uint8_t *dev_data, uint
 extern "C" int hdrf_gzip_parse(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t len, const uint32_t *dev_m128,
                                const uint32_t *dev_m32, uint32_t *dev_syms, int64_t *dev_blks, int64_t *dev_cnt)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (!dev_syms || !dev_blks || !dev_cnt || (len && (!dev_data || !dev_m128 || !dev_m32)))
         return set_err(ctx, HDRF_E_INVAL, "null buffer");
@@ -1121,6 +1200,7 @@ extern "C" int hdrf_gzip_parse(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t 
 // container's Lz4Codec file): a DataNode that restarted, or whose arena slot was reused.
 extern "C" int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *file, int64_t flen, int32_t lz4)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || flen < 0 || (flen && !file)) return HDRF_E_INVAL;
     uint64_t raw = (uint64_t)flen;
     if (lz4) {
@@ -1145,6 +1225,7 @@ extern "C" int hdrf_container_load(hdrf_ctx *ctx, uint32_t id, const uint8_t *fi
 
 extern "C" int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (int rc = drain(ctx)) return rc;
     auto it = ctx->loaded.find(id);
@@ -1156,6 +1237,7 @@ extern "C" int hdrf_container_unload(hdrf_ctx *ctx, uint32_t id)
 
 extern "C" int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !out) return HDRF_E_INVAL;
     HIPCK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
     return 0;
@@ -1163,6 +1245,7 @@ extern "C" int hdrf_host_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
 
 extern "C" int hdrf_host_free(hdrf_ctx *ctx, void *p)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (p) HIPCK(hipHostFree(p));
     return 0;
@@ -1170,15 +1253,21 @@ extern "C" int hdrf_host_free(hdrf_ctx *ctx, void *p)
 
 extern "C" int hdrf_wait_batch(hdrf_ctx *ctx)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     return wait_one(ctx);
 }
 
-extern "C" int hdrf_batch_nblocks(hdrf_ctx *ctx) { return ctx ? ctx->last_nblocks : HDRF_E_INVAL; }
+extern "C" int hdrf_batch_nblocks(hdrf_ctx *ctx)
+{
+    HDRF_LOCK(ctx);
+    return ctx ? ctx->last_nblocks : HDRF_E_INVAL;
+}
 
 extern "C" int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                                  const uint64_t *readable, const uint64_t *block_ids)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
     if (int rc = drain(ctx)) return rc;
@@ -1209,6 +1298,7 @@ static int64_t max_count(const int64_t *counts, int G)
 
 extern "C" int hdrf_gx_layout_get(hdrf_ctx *ctx, hdrf_gx_layout *out)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !out) return HDRF_E_INVAL;
     out->cap = ctx->gx_cap;
     out->x1_words = ctx->HW + 2;
@@ -1223,6 +1313,7 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
                                     const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase,
                                     uint32_t *x1_send)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
     if (ctx->gx_nfront != ctx->gx_nfwait || ctx->gx_nfront - ctx->gx_nback >= 2)
@@ -1263,6 +1354,7 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
 // Wait for the launched front; its per-peer X1 record counts -> send_counts[G].
 extern "C" int hdrf_gx_front_wait(hdrf_ctx *ctx, int64_t *send_counts)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->gx_nfront != ctx->gx_nfwait + 1) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front_wait: no front pending");
     if (!send_counts) return set_err(ctx, HDRF_E_INVAL, "null counts");
@@ -1292,6 +1384,7 @@ extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *cons
                              const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send,
                              int64_t *send_counts)
 {
+    HDRF_LOCK(ctx);
     if (!send_counts) return ctx ? set_err(ctx, HDRF_E_INVAL, "null counts") : HDRF_E_INVAL;
     if (int rc = hdrf_gx_front_launch(ctx, nblocks, dev_data, len, readable, block_ids, gbase, x1_send)) return rc;
     return hdrf_gx_front_wait(ctx, send_counts);
@@ -1299,6 +1392,7 @@ extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *cons
 
 extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send)
 {
+    HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 0)) return rc;
     Slot &S = ctx->sl[ctx->gx_nback % 2];
     if (!x1_recv || !recv_counts || !x2_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
@@ -1323,6 +1417,7 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
 
 extern "C" int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv)
 {
+    HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 1)) return rc;
     const int si = (int)(ctx->gx_nback % 2);
     Slot &S = ctx->sl[si];
@@ -1341,6 +1436,7 @@ extern "C" int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv)
 
 extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out)
 {
+    HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 2)) return rc;
     Slot &S = ctx->sl[ctx->gx_nback % 2];
     hipStream_t st = ctx->stB;
@@ -1362,6 +1458,7 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
 
 extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts)
 {
+    HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 3)) return rc;
     const int si = (int)(ctx->gx_nback % 2);
     Slot &S = ctx->sl[si];
@@ -1392,6 +1489,7 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
 
 extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts)
 {
+    HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 4)) return rc;
     if (!x3_recv || !recv_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     for (int s = 0; s < ctx->G; s++)
@@ -1414,6 +1512,7 @@ static int check_b(hdrf_ctx *ctx, int32_t b)
 
 extern "C" int hdrf_batch_info(hdrf_ctx *ctx, int32_t b, int64_t *n_chunks, int64_t *store_size)
 {
+    HDRF_LOCK(ctx);
     if (int rc = check_b(ctx, b)) return rc;
     const Slot &R = ctx->sl[ctx->res];
     if (n_chunks) *n_chunks = R.h_bst[b].n_chunks;
@@ -1423,6 +1522,7 @@ extern "C" int hdrf_batch_info(hdrf_ctx *ctx, int32_t b, int64_t *n_chunks, int6
 
 extern "C" int hdrf_batch_offsets(hdrf_ctx *ctx, int32_t b, uint32_t *out, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (int rc = check_b(ctx, b)) return rc;
     const Slot &R = ctx->sl[ctx->res];
     const int64_t n = R.h_bst[b].n_chunks;
@@ -1433,6 +1533,7 @@ extern "C" int hdrf_batch_offsets(hdrf_ctx *ctx, int32_t b, uint32_t *out, int64
 
 extern "C" int hdrf_batch_digests(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap_bytes)
 {
+    HDRF_LOCK(ctx);
     if (int rc = check_b(ctx, b)) return rc;
     const Slot &R = ctx->sl[ctx->res];
     const int64_t n = R.h_bst[b].n_chunks;
@@ -1443,6 +1544,7 @@ extern "C" int hdrf_batch_digests(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_
 
 extern "C" int hdrf_batch_is_new(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (int rc = check_b(ctx, b)) return rc;
     const Slot &R = ctx->sl[ctx->res];
     const int64_t n = R.h_bst[b].n_chunks;
@@ -1454,6 +1556,7 @@ extern "C" int hdrf_batch_is_new(hdrf_ctx *ctx, int32_t b, uint8_t *out, int64_t
 
 extern "C" int hdrf_batch_placement(hdrf_ctx *ctx, int32_t b, uint32_t *cid, uint32_t *pos, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (int rc = check_b(ctx, b)) return rc;
     const Slot &R = ctx->sl[ctx->res];
     const int64_t n = R.h_bst[b].n_chunks;
@@ -1473,6 +1576,7 @@ extern "C" int hdrf_batch_placement(hdrf_ctx *ctx, int32_t b, uint32_t *cid, uin
 extern "C" int hdrf_reduce_block(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *data, uint64_t len,
                                  hdrf_block_result *out)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
     if ((int64_t)len > ctx->cfg.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
@@ -1533,6 +1637,7 @@ static void entry_digest(const IndexEntry &e, int H, uint8_t *out)
 
 extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out11[11])
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !digest) return HDRF_E_INVAL;
     unsigned long long tag;
     std::memcpy(&tag, digest, 8);
@@ -1567,6 +1672,7 @@ static int fetch_table(hdrf_ctx *ctx, std::vector<IndexEntry> &tab)
 
 extern "C" int64_t hdrf_index_count(hdrf_ctx *ctx)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     std::vector<IndexEntry> tab;
     if (int rc = fetch_table(ctx, tab)) return rc;
@@ -1577,6 +1683,7 @@ extern "C" int64_t hdrf_index_count(hdrf_ctx *ctx)
 
 extern "C" int64_t hdrf_index_dump(hdrf_ctx *ctx, uint8_t *keys, uint8_t *vals, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     std::vector<IndexEntry> tab;
     if (int rc = fetch_table(ctx, tab)) return rc;
@@ -1601,6 +1708,7 @@ extern "C" int64_t hdrf_index_dump(hdrf_ctx *ctx, uint8_t *keys, uint8_t *vals, 
 
 extern "C" int hdrf_allocator(hdrf_ctx *ctx, uint8_t out24[24])
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !out24) return HDRF_E_INVAL;
     if (!ctx->have_alloc) return 0;
     uint32_t v[8];
@@ -1621,6 +1729,7 @@ extern "C" int hdrf_allocator(hdrf_ctx *ctx, uint8_t out24[24])
 // not hold these digests yet (a fresh or reset context).
 extern "C" int hdrf_index_load(hdrf_ctx *ctx, const uint8_t *keys, const uint8_t *vals, int64_t n)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || n < 0 || (n && (!keys || !vals))) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "restore on node-global contexts: not yet");
     if (int rc = drain(ctx)) return rc;
@@ -1650,6 +1759,7 @@ extern "C" int hdrf_index_load(hdrf_ctx *ctx, const uint8_t *keys, const uint8_t
 extern "C" int hdrf_allocator_load(hdrf_ctx *ctx, const uint8_t alloc24[24], const uint8_t *const *open_files,
                                    const int64_t *open_len)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !alloc24 || !open_len) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "restore on node-global contexts: not yet");
     if (int rc = drain(ctx)) return rc;
@@ -1680,6 +1790,7 @@ extern "C" int hdrf_allocator_load(hdrf_ctx *ctx, const uint8_t alloc24[24], con
 // SET longToBytes(blockId,4) -> recipe (storeDB, DN/DataDeduplicator.java:372-392)
 extern "C" int hdrf_recipe_load(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *recipe, int64_t len)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !recipe || len < 4 || (len - 4) % ctx->H) return HDRF_E_INVAL;
     const uint32_t key = (uint32_t)block_id;
     if (int rc = drain(ctx)) return rc;
@@ -1693,12 +1804,13 @@ extern "C" int hdrf_recipe_load(hdrf_ctx *ctx, uint64_t block_id, const uint8_t 
 
 extern "C" int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
+    if (int rc = drain(ctx)) return rc;                 // blocks in flight first: their recipes are SET
     auto it = ctx->recipes.find((uint32_t)block_id);
     if (it == ctx->recipes.end()) return 0;
     const int64_t n = 4 + (int64_t)it->second.n * ctx->H;
     if (!out || cap < n) return set_err(ctx, HDRF_E_CAPACITY, "recipe needs " + std::to_string(n) + " bytes");
-    if (int rc = drain(ctx)) return rc;
     std::vector<uint8_t> r;
     const int fr = fetch_recipe(ctx, (uint32_t)block_id, r);
     if (fr < 0) return fr;
@@ -1708,6 +1820,7 @@ extern "C" int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *ou
 
 extern "C" int64_t hdrf_block_length(hdrf_ctx *ctx, uint64_t block_id)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     auto it = ctx->lengths.find((uint32_t)block_id);
     return it == ctx->lengths.end() ? HDRF_E_NOTFOUND : it->second;
@@ -1715,7 +1828,9 @@ extern "C" int64_t hdrf_block_length(hdrf_ctx *ctx, uint64_t block_id)
 
 extern "C" int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t cap, int32_t *closed)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
+    if (int rc = drain(ctx)) return rc;                 // batches in flight may append, close or recycle it
     auto it = ctx->containers.find(id);
     if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_NOTFOUND, "container not resident");
     if (closed) *closed = it->second.closed;
@@ -1723,11 +1838,109 @@ extern "C" int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out,
     const int64_t n = lz ? it->second.clen : it->second.len;
     if (!out) return n;
     if (cap < n) return set_err(ctx, HDRF_E_CAPACITY, "container capacity");
-    if (int rc = drain(ctx)) return rc;
     const uint8_t *src = lz ? ctx->d_carena + (size_t)it->second.slot * ctx->cslot
                             : ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max;
     if (n) HIPCK(hipMemcpy(out, src, n, hipMemcpyDeviceToHost));
     return n;
+}
+
+// ---- durable containers: the chunkDir files of the storers (DN/DataDeduplicator.java:748-818) ----
+// Since the last drain: every container that closed (the whole file: raw bytes, or the Lz4Codec
+// stream under compressor 2, rewritten at :748-786) in close order, then every open container's
+// bytes appended since (:806-818).  Events are emitted whole, in order, while they fit.
+extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev, int64_t ev_cap, uint8_t *out,
+                                         int64_t out_cap, int64_t *need)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx) return HDRF_E_INVAL;
+    if (need) *need = 0;
+    if (!ctx->cfg.retain_containers) return set_err(ctx, HDRF_E_INVAL, "hdrf_drain_containers needs cfg.retain_containers");
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "container drain on node-global contexts");
+    if (ev_cap < 0 || out_cap < 0 || (ev_cap && !ev) || (out_cap && !out)) return set_err(ctx, HDRF_E_INVAL, "bad buffers");
+    if (int rc = drain(ctx)) return rc;
+    const hdrf_cfg &c = ctx->cfg;
+    struct Pend { uint32_t id; int closed; int64_t off, n; ContainerInfo ci; };
+    std::vector<Pend> todo;
+    for (uint32_t id : ctx->pend_closed) {
+        auto it = ctx->containers.find(id);
+        if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_DEVICE, "undrained container missing");
+        const bool lz = c.compressor == 2;
+        todo.push_back(Pend{id, 1, 0, lz ? (int64_t)it->second.clen : (int64_t)it->second.len, it->second});
+    }
+    const size_t nclosed = todo.size();
+    for (int t = 0; t < c.n_thread; t++) {
+        if (!ctx->h_alloc.exists[t]) continue;
+        const uint32_t id = ctx->h_alloc.id[t];
+        auto it = ctx->containers.find(id);
+        if (it == ctx->containers.end()) continue;
+        const int64_t done = ctx->handed.count(id) ? ctx->handed[id] : 0;
+        if ((int64_t)it->second.len > done) todo.push_back(Pend{id, 0, done, (int64_t)it->second.len - done, it->second});
+    }
+    int64_t k = 0, used = 0;
+    for (const Pend &e : todo) {
+        if (k >= ev_cap || used + e.n > out_cap) {
+            if (need) *need = e.n;
+            break;
+        }
+        const uint8_t *src = (e.closed && c.compressor == 2) ? ctx->d_carena + (size_t)e.ci.slot * ctx->cslot
+                                                             : ctx->d_arena + (size_t)e.ci.slot * c.container_max;
+        if (e.n) HIPCK(hipMemcpy(out + used, src + e.off, (size_t)e.n, hipMemcpyDeviceToHost));
+        ev[k] = hdrf_container_event{e.id, e.closed, e.off, e.n, used};
+        used += e.n;
+        k++;
+    }
+    // the emitted ones are handed over
+    const size_t kc = std::min<size_t>((size_t)k, nclosed);
+    for (size_t i = 0; i < kc; i++) {
+        const uint32_t id = ctx->pend_closed[i];
+        ctx->undrained[std::min<uint32_t>(id >> 22, 3)]--;
+        ctx->handed.erase(id);
+    }
+    ctx->pend_closed.erase(ctx->pend_closed.begin(), ctx->pend_closed.begin() + kc);
+    for (size_t i = nclosed; i < (size_t)k; i++) ctx->handed[todo[i].id] = todo[i].off + todo[i].n;
+    if (k == 0 && !todo.empty()) return set_err(ctx, HDRF_E_CAPACITY, "drain buffer too small for the next event");
+    return k;
+}
+
+// ---- arrival tickets: the FIFO of DN/DataDeduplicator.java:124-158 (DN/DDRunner.java:20-36) ------
+extern "C" int hdrf_ticket_take(hdrf_ctx *ctx, uint64_t *ticket)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || !ticket) return HDRF_E_INVAL;
+    *ticket = ctx->next_ticket++;
+    return 0;
+}
+
+static void ticket_done(hdrf_ctx *ctx, uint64_t ticket)
+{
+    if (ctx->serving == ticket) {
+        ctx->serving++;
+        while (ctx->cancelled.count(ctx->serving)) ctx->cancelled.erase(ctx->serving++);
+    } else if (ticket > ctx->serving) {
+        ctx->cancelled.insert(ticket);
+    }
+    ctx->turn.notify_all();
+}
+
+extern "C" int hdrf_ticket_cancel(hdrf_ctx *ctx, uint64_t ticket)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || ticket >= ctx->next_ticket) return HDRF_E_INVAL;
+    ticket_done(ctx, ticket);
+    return 0;
+}
+
+extern "C" int hdrf_reduce_block_ticketed(hdrf_ctx *ctx, uint64_t ticket, uint64_t block_id, const uint8_t *data,
+                                          uint64_t len, hdrf_block_result *out)
+{
+    if (!ctx) return HDRF_E_INVAL;
+    std::unique_lock<std::recursive_mutex> lk(ctx->mu);
+    if (ticket >= ctx->next_ticket || ticket < ctx->serving || ctx->cancelled.count(ticket))
+        return set_err(ctx, HDRF_E_INVAL, "unknown or finished ticket");
+    ctx->turn.wait(lk, [&] { return ctx->serving == ticket; });
+    const int rc = hdrf_reduce_block(ctx, block_id, data, len, out);
+    ticket_done(ctx, ticket);
+    return rc;
 }
 
 // ---- read side: DataConstructor (DN/DataConstructor.java:73-250, 360-531) --------------------
@@ -1745,6 +1958,7 @@ static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need)
 extern "C" int64_t hdrf_reconstruct(hdrf_ctx *ctx, const uint8_t *recipe, int64_t recipe_len, uint8_t *dev_out,
                                     int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !recipe || recipe_len < 4) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "reconstruction on node-global contexts: not yet");
     if (int rc = drain(ctx)) return rc;
@@ -1792,6 +2006,7 @@ extern "C" int64_t hdrf_reconstruct(hdrf_ctx *ctx, const uint8_t *recipe, int64_
 
 extern "C" int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (int rc = drain(ctx)) return rc;
     std::vector<uint8_t> rec;                            // GET longToBytes(blockId,4) (DN/BlockSender.java:292-328)
@@ -1810,6 +2025,7 @@ extern "C" int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint
 // ---- memory helpers, corpus, timing ------------------------------------------------------
 extern "C" int hdrf_dev_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !out) return HDRF_E_INVAL;
     HIPCK(hipMalloc(out, bytes));
     return 0;
@@ -1817,6 +2033,7 @@ extern "C" int hdrf_dev_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out)
 
 extern "C" int hdrf_dev_free(hdrf_ctx *ctx, void *p)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (int rc = drain(ctx)) return rc;
     HIPCK(hipFree(p));
@@ -1825,6 +2042,7 @@ extern "C" int hdrf_dev_free(hdrf_ctx *ctx, void *p)
 
 extern "C" int hdrf_memcpy_h2d(hdrf_ctx *ctx, void *dst, const void *src, uint64_t bytes)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     HIPCK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
@@ -1833,6 +2051,7 @@ extern "C" int hdrf_memcpy_h2d(hdrf_ctx *ctx, void *dst, const void *src, uint64
 
 extern "C" int hdrf_memcpy_d2h(hdrf_ctx *ctx, void *dst, const void *src, uint64_t bytes)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
@@ -1842,6 +2061,7 @@ extern "C" int hdrf_memcpy_d2h(hdrf_ctx *ctx, void *dst, const void *src, uint64
 
 extern "C" int hdrf_synchronize(hdrf_ctx *ctx)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     return drain(ctx);                                 // completes every batch in flight
 }
@@ -1849,12 +2069,14 @@ extern "C" int hdrf_synchronize(hdrf_ctx *ctx)
 extern "C" int hdrf_corpus_fill(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
                                 int64_t segs_per_block, int64_t seg_bytes, uint64_t seed)
 {
+    HDRF_LOCK(ctx);
     return hdrf_corpus_fill_kind(ctx, dev, roots_host, nblocks, segs_per_block, seg_bytes, seed, 0);
 }
 
 extern "C" int hdrf_corpus_fill_kind(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_host, int64_t nblocks,
                                      int64_t segs_per_block, int64_t seg_bytes, uint64_t seed, int32_t mixed)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !dev || !roots_host || seg_bytes % 16 != 0) return HDRF_E_INVAL;
     uint32_t *d_roots = nullptr;
     const size_t n = (size_t)nblocks * segs_per_block;
@@ -1868,6 +2090,7 @@ extern "C" int hdrf_corpus_fill_kind(hdrf_ctx *ctx, uint8_t *dev, const uint32_t
 
 extern "C" int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out)
 {
+    HDRF_LOCK(ctx);
     if (!ctx || !out) return HDRF_E_INVAL;
     *out = ctx->stats;
     return 0;
@@ -1875,6 +2098,7 @@ extern "C" int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out)
 
 extern "C" int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset)
 {
+    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     for (int i = 0; i < n && i < kStages; i++) ms[i] = ctx->stage_ms[i];
     if (reset)

@@ -31,6 +31,7 @@ EXPORTS = [
     "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_stream_block_host", "hdrf_lz4_file_decode",
     "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
+    "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -58,7 +59,13 @@ class Config(ctypes.Structure):
         ("max_batch_blocks", ctypes.c_int32), ("index_log2", ctypes.c_int32), ("arena_slots", ctypes.c_int64),
         ("segment_bytes", ctypes.c_int32), ("keep_recipes", ctypes.c_int32), ("timing", ctypes.c_int32),
         ("debug_tag_bits", ctypes.c_int32), ("n_ranks", ctypes.c_int32), ("rank", ctypes.c_int32),
+        ("retain_containers", ctypes.c_int32),
     ]
+
+
+class ContainerEvent(ctypes.Structure):
+    _fields_ = [("id", ctypes.c_uint32), ("closed", ctypes.c_int32), ("file_off", ctypes.c_int64),
+                ("nbytes", ctypes.c_int64), ("data_off", ctypes.c_int64)]
 
 
 class Stats(ctypes.Structure):
@@ -112,6 +119,12 @@ def load():
         "hdrf_last_error": (ctypes.c_char_p, [_vp]),
         "hdrf_digest_len": (ctypes.c_int, [_vp]),
         "hdrf_reduce_block": (ctypes.c_int, [_vp, ctypes.c_uint64, _u8p, ctypes.c_uint64, ctypes.POINTER(BlockResult)]),
+        "hdrf_reduce_block_ticketed": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _u8p, ctypes.c_uint64,
+                                                      ctypes.POINTER(BlockResult)]),
+        "hdrf_ticket_take": (ctypes.c_int, [_vp, _u64p]),
+        "hdrf_ticket_cancel": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+        "hdrf_drain_containers": (ctypes.c_int64, [_vp, ctypes.POINTER(ContainerEvent), ctypes.c_int64, _u8p,
+                                                   ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
         "hdrf_reduce_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
         "hdrf_submit_batch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p]),
         "hdrf_wait_batch": (ctypes.c_int, [_vp]),
@@ -236,7 +249,9 @@ class Context:
         self.close()
 
     # ---- write path ---------------------------------------------------------------------
-    def reduce_block(self, data, block_id):
+    def reduce_block(self, data, block_id, ticket=None):
+        """hdrf_reduce_block (or hdrf_reduce_block_ticketed with an arrival ticket from
+        ticket_take(): waits for every earlier ticket; safe to call from any thread)."""
         a = _u8(data)
         buf = a if a.size else np.zeros(1, np.uint8)
         cap = a.size // (self.cfg.window + 2) + 2
@@ -246,11 +261,40 @@ class Context:
         cid = np.zeros(cap, np.uint32)
         pos = np.zeros(cap, np.uint32)
         r = BlockResult(0, 0, cap, _p(offs, _u32p), _p(digs), _p(isnew), _p(cid, _u32p), _p(pos, _u32p))
-        self._ck(self.L.hdrf_reduce_block(self._h, block_id, _p(buf), a.size, ctypes.byref(r)))
+        if ticket is None:
+            self._ck(self.L.hdrf_reduce_block(self._h, block_id, _p(buf), a.size, ctypes.byref(r)))
+        else:
+            self._ck(self.L.hdrf_reduce_block_ticketed(self._h, ticket, block_id, _p(buf), a.size, ctypes.byref(r)))
         n = r.n_chunks
         return {"offsets": offs[:n].copy(), "digests": digs[:n * self.H].reshape(n, self.H).copy(),
                 "is_new": isnew[:n].copy(), "container_id": cid[:n].copy(), "container_pos": pos[:n].copy(),
                 "store_size": r.store_size}
+
+    def ticket_take(self):
+        t = ctypes.c_uint64()
+        self._ck(self.L.hdrf_ticket_take(self._h, ctypes.byref(t)))
+        return t.value
+
+    def ticket_cancel(self, ticket):
+        self._ck(self.L.hdrf_ticket_cancel(self._h, ticket))
+
+    def drain_containers(self, buf_bytes=64 << 20, max_events=4096):
+        """hdrf_drain_containers until nothing is pending: [(id, closed, file_off, bytes)] in order."""
+        out = []
+        ev = (ContainerEvent * max_events)()
+        need = ctypes.c_int64()
+        cap = buf_bytes
+        while True:
+            buf = np.zeros(max(cap, 1), np.uint8)
+            n = self.L.hdrf_drain_containers(self._h, ev, max_events, _p(buf), cap, ctypes.byref(need))
+            if n == -4 and need.value > cap:                 # HDRF_E_CAPACITY: the next event alone
+                cap = int(need.value)
+                continue
+            self._ck(n)
+            if n == 0:
+                return out
+            for e in ev[:n]:
+                out.append((e.id, e.closed, e.file_off, buf[e.data_off:e.data_off + e.nbytes].tobytes()))
 
     def reduce_batch(self, dev_ptrs, lens, readable, block_ids):
         n = len(dev_ptrs)

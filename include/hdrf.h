@@ -8,9 +8,13 @@
  *
  * Conventions: plain pointers and sizes only; every function returns 0 on success or a
  * negative HDRF_E* code; hdrf_last_error() describes the last failure of a context; no C++
- * exception crosses this ABI.  A context is bound to one GPU and is NOT thread-safe: the
- * reference serialises reductions through its FIFO (DN/DataDeduplicator.java:124-158,
- * 197-204) and callers do the same (one context per DataNode, calls in block order).
+ * exception crosses this ABI.  A context is bound to one GPU.  Threads: every entry point takes
+ * the context's lock, so any number of threads (one DataXceiver / DDRunner thread per block) may
+ * call it concurrently (hdrf_close excepted: no call may be in progress or follow).  Block ORDER is
+ * the call order unless the caller uses arrival tickets (hdrf_ticket_take at block arrival,
+ * hdrf_reduce_block_ticketed later from any thread), which reproduce the reference's FIFO
+ * (DN/DataDeduplicator.java:124-158, 197-204; DN/DDRunner.java:20-36).  hdrf_last_error() is the
+ * context's last error, whichever thread caused it.
  */
 #ifndef HDRF_H
 #define HDRF_H
@@ -52,6 +56,10 @@ typedef struct {
                                 tag collisions through the exact slow path; 0 = full 64-bit tag */
     int32_t n_ranks;         /* GPUs sharing ONE node-global index (1 = this GPU is the whole node) */
     int32_t rank;            /* this GPU's rank in [0, n_ranks) = index partition it owns */
+    int32_t retain_containers; /* 1: durable containers (a DataNode): a closed container keeps its arena
+                                  slot until hdrf_drain_containers has handed it out, and a submit that
+                                  could need such a slot returns HDRF_E_CAPACITY; 0 (default): the
+                                  arena is a ring cache of the newest containers (benchmarks, tests) */
 } hdrf_cfg;
 
 /* Per-block result of hdrf_reduce_block (caller-owned host arrays; NULL to skip). */
@@ -89,10 +97,12 @@ int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_
 /* Pipelined form of hdrf_reduce_batch: hdrf_submit_batch enqueues the batch (chunking, SHA and
  * index + store on three HIP streams, in block order) and returns; hdrf_wait_batch completes the
  * OLDEST submitted batch and makes it the one hdrf_batch_* report.  At most HDRF_PIPELINE_DEPTH
- * batches are in flight (one more submit first completes the oldest); the device buffers of a
- * batch must stay valid until it is completed.  Chunking of batch k+2, hashing of batch k+1 and
- * the index/store stage of batch k run concurrently (scalar units, vector units and memory).
- * Views (index, containers, allocator) complete all batches first. */
+ * batches are in flight: a submit beyond that returns HDRF_E_CAPACITY (call hdrf_wait_batch
+ * first), so every submit pairs with exactly one wait.  The device buffers of a batch must stay
+ * valid until it is completed.  Chunking of batch k+1 overlaps hashing of batch k and the
+ * index/store stage of batch k-1 (latency-bound walk, VALU-bound SHA, HBM-bound store); the
+ * bench keeps two batches in flight.  Views (index, containers, allocator) complete all batches
+ * first. */
 #define HDRF_PIPELINE_DEPTH 3
 int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                       const uint64_t *readable, const uint64_t *block_ids);
@@ -182,10 +192,42 @@ int hdrf_allocator(hdrf_ctx *ctx, uint8_t out24[24]);
 int64_t hdrf_recipe_get(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap);
 /* FsDatasetImpl.getLength for 0-byte replicas (DN/fsdataset/impl/FsDatasetImpl.java:736-763). */
 int64_t hdrf_block_length(hdrf_ctx *ctx, uint64_t block_id);
-/* Container file chunkDir+id.  Returns length; *closed = 1 once it overflowed.  Raw bytes, except
- * closed containers under compressor 2: the Lz4Codec file the storer rewrote (:770-779).
- * HDRF_E_NOTFOUND if it never existed or its arena slot was recycled. */
+/* Container file chunkDir+id as it is now (the batches in flight complete first).  Returns length;
+ * *closed = 1 once it overflowed.  Raw bytes, except closed containers under compressor 2: the
+ * Lz4Codec file the storer rewrote (:770-779).  HDRF_E_NOTFOUND if it never existed or its arena
+ * slot was recycled (cfg.retain_containers = 0), or after a drain handed it out and its slot was
+ * reused (retain_containers = 1: the file is the caller's then). */
 int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t cap, int32_t *closed);
+
+/* Durable containers (cfg.retain_containers = 1): what the storers wrote to chunkDir since the
+ * last drain (DN/DataDeduplicator.java:748-818).  Each event is one file operation:
+ *   closed = 1   the container closed: (re)write the whole file chunkDir+id with nbytes bytes (raw,
+ *                or the Lz4Codec stream under compressor 2; :748-786)
+ *   closed = 0   the open container grew: write nbytes bytes at file_off (= the file's length so
+ *                far) of chunkDir+id, creating it when file_off == 0 (:806-818)
+ * The bytes of event i are out[data_off, data_off + nbytes).  Events come in order (closes in
+ * close order, then the open containers) and whole; returns the number written, 0 when nothing is
+ * pending, HDRF_E_CAPACITY (and *need = the next event's bytes) when not even one fits.  Call again
+ * until it returns 0.  Completes the batches in flight first.  A drained closed container's slot
+ * may then be reused; read it back with hdrf_container_load. */
+typedef struct {
+    uint32_t id;             /* container id (utilities.bytesToBlockID ranges, DN/utilities.java:36-75) */
+    int32_t closed;
+    int64_t file_off;
+    int64_t nbytes;
+    int64_t data_off;
+} hdrf_container_event;
+int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev, int64_t ev_cap, uint8_t *out, int64_t out_cap,
+                              int64_t *need);
+
+/* Arrival tickets (AIWriteQueue, DN/DataDeduplicator.java:124-158): take one when a block arrives
+ * (BlockReceiver, before its DDRunner starts), reduce with it from any thread: a ticketed call waits
+ * until every earlier ticket has been reduced or cancelled, so the index / containers / recipes
+ * are those of the arrival order.  A ticket that will never be used must be cancelled. */
+int hdrf_ticket_take(hdrf_ctx *ctx, uint64_t *ticket);
+int hdrf_ticket_cancel(hdrf_ctx *ctx, uint64_t ticket);
+int hdrf_reduce_block_ticketed(hdrf_ctx *ctx, uint64_t ticket, uint64_t block_id, const uint8_t *data, uint64_t len,
+                               hdrf_block_result *out);
 
 /* Read side: DataConstructor(blkID, recipe).data (DN/DataConstructor.java:73-250, 360-531), the
  * rebuild BlockSender serves on READ_BLOCK (DN/BlockSender.java:612-619).  Every recipe digest
@@ -212,9 +254,10 @@ int hdrf_corpus_fill_kind(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_hos
                           int64_t segs_per_block, int64_t seg_bytes, uint64_t seed, int32_t mixed);
 
 /* Per-stage device time (ms) accumulated since the last reset, measured with HIP events on
- * the context's stream (cfg.timing = 1): [0] spec_walk_kernel, [1] stitch (sync/plan/copy/
- * fallback), [2] sha_full_kernel, [3] sha_tail_kernel, [4] idx_claim_kernel, [5] idx_apply_kernel,
- * [6] idx_slow+decide, [7] new-byte scans, [8] flush_kernel, [9] place_kernel, [10] lz4 (compressor 2). */
+ * the streams the stages run on (cfg.timing = 1): [0] lane_walk_kernel, [1] stitch (repair / path /
+ * count / scan / copy / fallback), [2] sha_full_kernel, [3] sha_tail_kernel, [4] idx_claim_kernel,
+ * [5] idx_apply_kernel, [6] idx_slow+decide, [7] new-byte scans, [8] flush_kernel, [9] place_kernel,
+ * [10] lz4 (compressor 2), [11] gmax_kernel (granule maxima). */
 int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
 /* Reduction totals since the last reset (this context's blocks): the dedup / compression ratio
  * of the node is logical_bytes / (closed_file_bytes + open_bytes [+ recipe_bytes]). */

@@ -6,7 +6,16 @@ import java.nio.ByteBuffer;
 /**
  * MI355X backend: JNI over libhdrf.so (include/hdrf.h).  Selected where DataNode.compressor is
  * tested (DataNode.java:438, BlockReceiver.java:822-879) in place of `new DDRunner(bf1, id)`.
- * bf1 must be a direct ByteBuffer (BlockReceiver.java:877 allocates it with allocateDirect).
+ * bf1 must be a direct ByteBuffer (BlockReceiver.java:877 allocates it with allocateDirect, or
+ * allocPinned() for an overlapped H2D).
+ *
+ * Threads: every method may be called from any thread (the native context serialises calls).
+ * Block order: reduce() reduces in call order; for the reference's FIFO (AIWriteQueue,
+ * DataDeduplicator.java:124-158) take arrive() when the block is received and pass the ticket to
+ * reduce(ticket, ...) from the block's own DDRunner-style thread.
+ * Durability: containers are kept in HBM until drainContainers(chunkDir) has written them; call it
+ * after reductions (a reduction that could overwrite an undrained container fails with
+ * IOException "drain ... first": drain and retry).
  */
 public final class HipReductionScheme extends ReductionScheme {
   static { System.loadLibrary("hdrf_jni"); }   // libhdrf_jni.so -> libhdrf.so
@@ -24,12 +33,48 @@ public final class HipReductionScheme extends ReductionScheme {
     reduce0(ctx, block, block.position(), blockId);   // H2D copy happens before return
   }
 
+  /** The block's place in the FIFO, taken when it is received (before its reducing thread starts). */
+  public long arrive() throws IOException {
+    return arrive0(ctx);
+  }
+
+  /** reduce() in arrival-ticket order: waits until every earlier ticket was reduced or cancelled. */
+  public void reduce(long ticket, ByteBuffer block, long blockId) throws IOException {
+    if (!block.isDirect()) { cancel0(ctx, ticket); throw new IOException("HipReductionScheme needs a direct ByteBuffer"); }
+    reduceTicket0(ctx, ticket, block, block.position(), blockId);
+  }
+
+  /** A ticket whose block will not be reduced (the receive failed). */
+  public void cancel(long ticket) throws IOException {
+    cancel0(ctx, ticket);
+  }
+
+  /**
+   * The storers' chunkDir writes since the last call (DataDeduplicator.java:748-818): closed
+   * containers rewritten whole (Lz4Codec files under compressor 2), open containers appended.
+   * Returns the number of file operations.
+   */
+  public int drainContainers(String chunkDir) throws IOException {
+    return drain0(ctx, chunkDir);
+  }
+
+  /** Page-locked direct buffer for received blocks (reduceAsync copies it H2D on a side stream). */
+  public ByteBuffer allocPinned(long bytes) throws IOException {
+    return allocPinned0(ctx, bytes);
+  }
+
+  public void freePinned(ByteBuffer buf) throws IOException {
+    freePinned0(ctx, buf);
+  }
+
   /**
    * Streaming write path (BASELINE config 5): enqueue the received block and return at once; its
    * H2D copy runs on a side stream overlapped with the blocks already in flight.  `block` must
    * stay untouched until awaitOldest() has returned for it (keep a reference; BlockReceiver
    * allocates a fresh bf1 per block).  Completion is in submission order, like the FIFO
-   * (DataDeduplicator.java:124-158).
+   * (DataDeduplicator.java:124-158).  At most 3 blocks are in flight: a fourth reduceAsync throws
+   * IOException ("pipeline full") until awaitOldest() completed one, so every reduceAsync pairs
+   * with exactly one awaitOldest.
    */
   public void reduceAsync(ByteBuffer block, long blockId) throws IOException {
     if (!block.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
@@ -82,4 +127,11 @@ public final class HipReductionScheme extends ReductionScheme {
   private static native byte[] stream0(long ctx, int codec, ByteBuffer direct, int len, long blockId, long[] writes)
       throws IOException;
   private static native void close0(long ctx);
+  private static native long arrive0(long ctx) throws IOException;
+  private static native void reduceTicket0(long ctx, long ticket, ByteBuffer direct, int len, long blockId)
+      throws IOException;
+  private static native void cancel0(long ctx, long ticket) throws IOException;
+  private static native int drain0(long ctx, String chunkDir) throws IOException;
+  private static native ByteBuffer allocPinned0(long ctx, long bytes) throws IOException;
+  private static native void freePinned0(long ctx, ByteBuffer buf) throws IOException;
 }

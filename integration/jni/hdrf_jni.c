@@ -3,10 +3,14 @@
  *   cc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
  *      integration/jni/hdrf_jni.c -Lhdrf_amd/_build -lhdrf -o libhdrf_jni.so
  * Errors become IOException; DDRunner-style callers may log and continue (DDRunner.java:27-31). */
+#define _FILE_OFFSET_BITS 64
+#define _POSIX_C_SOURCE 200809L
 #include <jni.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <sys/types.h>
 
 #include "hdrf.h"
 
@@ -28,7 +32,8 @@ JNIEXPORT jlong JNICALL JFN(open0)(JNIEnv *env, jclass cls, jint hasher, jint co
     hdrf_default_cfg(&cfg);
     cfg.hasher = hasher;              /* DataNode.hasher  (DataNode.java:446) */
     cfg.compressor = compressor;      /* 1 dedup, 2 dedup + Lz4Codec (DataNode.java:438) */
-    cfg.arena_slots = 64;             /* resident containers for the read side */
+    cfg.arena_slots = 256;            /* 64 containers per storer range resident (8 GiB of HBM) */
+    cfg.retain_containers = 1;        /* durable: nothing leaves HBM before drain0 wrote its file */
     cfg.device = device;
     cfg.max_block_bytes = max_block;  /* dfs.blocksize */
     cfg.max_batch_blocks = 1;
@@ -45,6 +50,107 @@ JNIEXPORT void JNICALL JFN(reduce0)(JNIEnv *env, jclass cls, jlong h, jobject bu
     const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
     if (!p) { throw_io(env, ctx, HDRF_E_INVAL); return; }
     int rc = hdrf_reduce_block(ctx, (uint64_t)id, p, (uint64_t)len, NULL);
+    if (rc) throw_io(env, ctx, rc);
+}
+
+/* BlockReceiver, at block arrival: the block's place in the FIFO (AIWriteQueue,
+ * DataDeduplicator.java:124-158) */
+JNIEXPORT jlong JNICALL JFN(arrive0)(JNIEnv *env, jclass cls, jlong h)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    uint64_t t = 0;
+    int rc = hdrf_ticket_take(ctx, &t);
+    if (rc) throw_io(env, ctx, rc);
+    return (jlong)t;
+}
+
+/* DDRunner.run on any thread: waits for the earlier tickets, then reduces */
+JNIEXPORT void JNICALL JFN(reduceTicket0)(JNIEnv *env, jclass cls, jlong h, jlong ticket, jobject buf, jint len,
+                                          jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
+    if (!p && len) {
+        hdrf_ticket_cancel(ctx, (uint64_t)ticket);
+        throw_io(env, ctx, HDRF_E_INVAL);
+        return;
+    }
+    int rc = hdrf_reduce_block_ticketed(ctx, (uint64_t)ticket, (uint64_t)id, p, (uint64_t)len, NULL);
+    if (rc) throw_io(env, ctx, rc);
+}
+
+JNIEXPORT void JNICALL JFN(cancel0)(JNIEnv *env, jclass cls, jlong h, jlong ticket)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int rc = hdrf_ticket_cancel(ctx, (uint64_t)ticket);
+    if (rc) throw_io(env, ctx, rc);
+}
+
+/* The storers' chunkDir writes (DataDeduplicator.java:748-818): every container closed since the
+ * last call is (re)written whole to chunkDir + id, every open container's new bytes are written at
+ * the file's end.  Returns the number of file operations. */
+static int write_event(const char *dir, const hdrf_container_event *e, const uint8_t *data)
+{
+    char path[4096];
+    snprintf(path, sizeof path, "%s%u", dir, e->id);   /* DataNode.chunkDir + id (:754, :811) */
+    FILE *f = fopen(path, (e->closed || e->file_off == 0) ? "wb" : "r+b");
+    if (!f) return -1;
+    int ok = fseeko(f, (off_t)e->file_off, SEEK_SET) == 0 &&
+             fwrite(data, 1, (size_t)e->nbytes, f) == (size_t)e->nbytes;
+    ok = (fclose(f) == 0) && ok;
+    return ok ? 0 : -1;
+}
+
+JNIEXPORT jint JNICALL JFN(drain0)(JNIEnv *env, jclass cls, jlong h, jstring chunkDir)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    const char *dir = (*env)->GetStringUTFChars(env, chunkDir, NULL);
+    int64_t cap = 64ll << 20, need = 0, total = 0;
+    uint8_t *buf = (uint8_t *)malloc((size_t)cap);
+    hdrf_container_event ev[256];
+    int rc = buf ? 0 : HDRF_E_NOMEM;
+    while (!rc) {
+        int64_t n = hdrf_drain_containers(ctx, ev, 256, buf, cap, &need);
+        if (n == HDRF_E_CAPACITY && need > cap) {          /* one event larger than the buffer */
+            uint8_t *nb = (uint8_t *)realloc(buf, (size_t)need);
+            if (!nb) { rc = HDRF_E_NOMEM; break; }
+            buf = nb;
+            cap = need;
+            continue;
+        }
+        if (n < 0) { rc = (int)n; break; }
+        if (n == 0) break;
+        for (int64_t i = 0; i < n && !rc; i++)
+            if (write_event(dir, &ev[i], buf + ev[i].data_off)) rc = HDRF_E_INVAL;
+        total += n;
+    }
+    free(buf);
+    (*env)->ReleaseStringUTFChars(env, chunkDir, dir);
+    if (rc) { throw_io(env, ctx, rc); return -1; }
+    return (jint)total;
+}
+
+/* page-locked receive buffers: hdrf_submit_host copies from them on a side stream */
+JNIEXPORT jobject JNICALL JFN(allocPinned0)(JNIEnv *env, jclass cls, jlong h, jlong bytes)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    void *p = NULL;
+    int rc = hdrf_host_alloc(ctx, (uint64_t)bytes, &p);
+    if (rc) { throw_io(env, ctx, rc); return NULL; }
+    return (*env)->NewDirectByteBuffer(env, p, bytes);
+}
+
+JNIEXPORT void JNICALL JFN(freePinned0)(JNIEnv *env, jclass cls, jlong h, jobject buf)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    void *p = (*env)->GetDirectBufferAddress(env, buf);
+    int rc = p ? hdrf_host_free(ctx, p) : HDRF_E_INVAL;
     if (rc) throw_io(env, ctx, rc);
 }
 

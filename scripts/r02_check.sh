@@ -5,7 +5,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 mkdir -p gpurun_out
 T=${TESTS:-tests/test_gpu_parity.py tests/test_config2_shape.py}
-timeout -k 10 900 python -u -m pytest $T -x -v --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1
+timeout -k 10 900 python -u -m pytest $T -x -v --timeout 150 --timeout-method thread > gpurun_out/t.log 2>&1
 rc=$?
 tail -25 gpurun_out/t.log
 [ $rc -eq 0 ] || exit $rc

@@ -17,6 +17,8 @@ typedef jobject jclass;
 typedef jobject jarray;
 typedef jarray jbyteArray;
 typedef jarray jlongArray;
+typedef jobject jstring;
+typedef uint8_t jboolean;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_ *JNIEnv;
@@ -29,4 +31,7 @@ struct JNINativeInterface_ {
     void (*ReleaseLongArrayElements)(JNIEnv *env, jlongArray array, jlong *elems, jint mode);
     jbyteArray (*NewByteArray)(JNIEnv *env, jsize len);
     void (*SetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, const jbyte *buf);
+    const char *(*GetStringUTFChars)(JNIEnv *env, jstring string, jboolean *isCopy);
+    void (*ReleaseStringUTFChars)(JNIEnv *env, jstring string, const char *utf);
+    jobject (*NewDirectByteBuffer)(JNIEnv *env, void *address, jlong capacity);
 };

@@ -57,7 +57,7 @@ def compare_block(g, o, tag=""):
         assert np.array_equal(g["container_pos"][m], start[m]), f"{tag}: container positions differ"
 
 
-def compare_state(ctx, ora, block_ids, tag=""):
+def compare_state(ctx, ora, block_ids, tag="", containers=True):
     gk, gv = ctx.index_dump()
     ok, ov = ora.index_dump()
     assert gk.shape == ok.shape, f"{tag}: index size {gk.shape[0]} vs {ok.shape[0]}"
@@ -70,7 +70,7 @@ def compare_state(ctx, ora, block_ids, tag=""):
         assert ctx.block_length(bid) == int.from_bytes(ora.recipe(bid)[:4], "big")
     # every container the oracle wrote
     alloc = ora.allocator()
-    if alloc:
+    if alloc and containers:
         ids = [int.from_bytes(alloc[3 * t:3 * t + 3], "big") for t in range(3)]
         for t in range(3):
             base = t << 22

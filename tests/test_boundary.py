@@ -1,0 +1,192 @@
+"""The drop-in boundary's contract: concurrent callers with
+arrival tickets, and durable containers handed out as chunkDir file operations.
+
+- Tickets: DataXceiver threads take a ticket when their block arrives and reduce later from their
+  own thread in any order; the result is the reference's FIFO order (AIWriteQueue,
+  DN/DataDeduplicator.java:124-158; DN/DDRunner.java:20-36).
+- Durable containers (cfg.retain_containers): every closed container and every open-container
+  append is drained as the file operation the storer performs on chunkDir + id
+  (DN/DataDeduplicator.java:748-818); the files equal the oracle's containers, the arena ring wraps
+  without losing anything, a submit that could overwrite an undrained container is refused, and
+  every block rebuilds from the drained files alone.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import compare_block, compare_state, make_block
+from hdrf_amd.lib import Context, HdrfError
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _blocks(seed, n, size, dup_div=3):
+    """n blocks: two pieces of size // dup_div from a shared base (cross-block duplicates) + new random bytes."""
+    rng = np.random.default_rng(seed)
+    base = [make_block(k, seed + i, 600_000) for i, k in enumerate(["random", "text", "binary"])]
+    out = []
+    d = size // dup_div
+    for i in range(n):
+        parts = [base[int(rng.integers(3))][int(rng.integers(0, 200_000)):][:d] for _ in range(2)]
+        out.append(np.concatenate(parts + [make_block("random", seed + 100 + i, size - 2 * d)]))
+    return out
+
+
+def test_ticketed_threads_reduce_in_arrival_order():
+    """One thread per block (the DDRunner shape, DN/BlockReceiver.java:1261), tickets taken in
+    arrival order, threads started in REVERSE order so later blocks reach the native call first:
+    every result and the final index / containers / recipes / allocator equal the sequential
+    oracle run in ticket (arrival) order."""
+    import time
+    blocks = _blocks(31, 6, 700_000)
+    ids = [4000 + i for i in range(6)]
+    ctx = Context(container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64)
+    tickets = [ctx.ticket_take() for _ in blocks]          # arrival order 0..5
+    assert tickets == sorted(tickets)
+    results, errors = {}, []
+
+    def worker(b):
+        try:
+            results[b] = ctx.reduce_block(blocks[b], ids[b], ticket=tickets[b])
+        except Exception as e:                             # noqa: BLE001 - surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(b,)) for b in range(6)]
+    for b in reversed(range(6)):
+        th[b].start()
+        time.sleep(0.05)
+    for t in th:
+        t.join(60)
+    assert not any(t.is_alive() for t in th), "ticketed reductions did not finish"
+    assert not errors, errors
+    ora = Oracle(max_size=1 << 20)
+    for b in range(6):
+        compare_block(results[b], ora.reduce(blocks[b], ids[b]), tag=f"ticket {b}")
+    compare_state(ctx, ora, ids, tag="tickets")
+    # a cancelled ticket does not hold up the ones after it
+    t0, t1 = ctx.ticket_take(), ctx.ticket_take()
+    ctx.ticket_cancel(t0)
+    extra = make_block("random", 77, 50_000)
+    compare_block(ctx.reduce_block(extra, 4100, ticket=t1), ora.reduce(extra, 4100), tag="after cancel")
+    ctx.close()
+
+
+def test_threads_with_racing_views_are_serialised():
+    """Threads taking tickets as their blocks "arrive" (order recorded), reducing with them and
+    reading views (index count) while the other threads reduce: the state is the oracle's for the
+    recorded arrival order, so the context lock serialised every call."""
+    blocks = _blocks(41, 6, 300_000)
+    ids = [5000 + i for i in range(6)]
+    ctx = Context(container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64)
+    order, lock, errors = [], threading.Lock(), []
+
+    def worker(t):
+        try:
+            for b in (t, t + 3):
+                tk = None
+                with lock:                                   # arrival = this thread's turn at the lock
+                    tk = ctx.ticket_take()
+                    order.append(b)
+                ctx.reduce_block(blocks[b], ids[b], ticket=tk)
+                ctx.index_count()                            # a view racing the other threads' reductions
+        except Exception as e:                               # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors
+    ora = Oracle(max_size=1 << 20)
+    for b in order:
+        ora.reduce(blocks[b], ids[b])
+    compare_state(ctx, ora, ids, tag="serialised")
+    ctx.close()
+
+
+def _apply(disk, events):
+    """The storer's file operations on a dict chunkDir: closed -> rewrite, open -> write at offset."""
+    for cid, closed, off, data in events:
+        if closed:
+            disk[cid] = (bytearray(data), True)
+        else:
+            f = disk.get(cid, (bytearray(), False))[0]
+            assert len(f) == off, f"append to {cid} at {off}, file has {len(f)}"
+            f[off:] = data
+            disk[cid] = (f, False)
+
+
+@pytest.mark.parametrize("compressor", [1, 2])
+def test_durable_containers_drain_wrap_and_rebuild(compressor):
+    cmax = 1 << 20
+    blocks = _blocks(51 + compressor, 22, 2 << 20, dup_div=8)   # ~1.5 MiB new per block: the 8-slot rings wrap
+    ids = [6000 + i for i in range(len(blocks))]
+    kw = dict(compressor=compressor, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20,
+              arena_slots=32, retain_containers=1)
+    # without drains the ring fills: the submit is refused BEFORE anything changes
+    ctx0 = Context(**kw)
+    with pytest.raises(HdrfError) as ei:
+        for b, i in zip(blocks, ids):
+            ctx0.reduce_block(b, i)
+    assert ei.value.code == -4 and "drain" in str(ei.value)
+    ctx0.close()
+
+    ctx = Context(**kw)
+    ora = Oracle(compressor=compressor, max_size=cmax)
+    disk = {}
+    for b, i in zip(blocks, ids):
+        compare_block(ctx.reduce_block(b, i), ora.reduce(b, i), tag=f"durable block {i}")
+        _apply(disk, ctx.drain_containers(buf_bytes=1 << 20))     # small buffer: several drain calls
+    assert ctx.drain_containers() == []
+    # the files are the oracle's containers, byte for byte (closed: raw or Lz4Codec; open: raw)
+    alloc = ora.allocator()
+    n_cont = 0
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, oc = ora.container(cid)
+            if od is None:
+                continue
+            n_cont += 1
+            assert cid in disk, f"container {cid} never drained"
+            assert bytes(disk[cid][0]) == bytes(od) and disk[cid][1] == oc, f"container {cid} file differs"
+    assert n_cont == len(disk) and n_cont > 8 * 3, "the ring of 8 slots per range must have wrapped"
+    wrapped = sum(ctx.container(cid)[0] is None for cid in disk)
+    assert wrapped > 0
+    compare_state(ctx, ora, ids, tag=f"durable c{compressor}", containers=False)   # files compared above
+    # a restarted DataNode with nothing but the Redis state and the drained files rebuilds every block
+    keys, vals = ctx.index_dump()
+    recipes = {i: ctx.recipe(i) for i in ids}
+    ctx.close()
+    ctx2 = Context(**kw)
+    ctx2.index_load(keys, vals)
+    for i, r in recipes.items():
+        ctx2.recipe_load(i, r)
+    for cid, (data, closed) in disk.items():
+        ctx2.container_load(cid, bytes(data), closed and compressor == 2)
+    for b, i in zip(blocks, ids):
+        assert np.array_equal(ctx2.reconstruct_block(i), b), f"block {i} not rebuilt from drained files"
+    ctx2.close()
+
+
+def test_pipeline_depth_is_refused_not_waited():
+    """A submit beyond HDRF_PIPELINE_DEPTH returns HDRF_E_CAPACITY (the caller's awaitOldest pairs
+    one to one with its submits) and leaves the batches in flight untouched."""
+    from hdrf_amd.lib import PIPELINE_DEPTH as D
+    blocks = _blocks(61, D + 1, 200_000)
+    ctx = Context(container_max=1 << 20, max_block_bytes=1 << 20, max_batch_blocks=1, index_log2=18, arena_slots=16)
+    ora = Oracle(max_size=1 << 20)
+    for i in range(D):
+        ctx.submit_host([blocks[i].ctypes.data], [len(blocks[i])], [7000 + i])
+    with pytest.raises(HdrfError) as ei:
+        ctx.submit_host([blocks[D].ctypes.data], [len(blocks[D])], [7000 + D])
+    assert ei.value.code == -4
+    for i in range(D):
+        ctx.wait_batch()
+        compare_block(ctx.batch_result(0), ora.reduce(blocks[i], 7000 + i), tag=f"depth {i}")
+    with pytest.raises(HdrfError):
+        ctx.wait_batch()                                     # nothing left in flight
+    ctx.close()

@@ -218,9 +218,10 @@ def test_device_corpus_matches_host_and_reduces(mixed):
 
 
 def test_pipelined_submit_wait_matches_sequential_oracle():
-    """hdrf_submit_batch / hdrf_wait_batch: up to PIPELINE_DEPTH batches in flight (chunking of
-    batch k+2, SHA of k+1 and index/store of k on three streams) give the same results as the
-    sequential oracle, including when a submit beyond the depth completes the oldest batch."""
+    """hdrf_submit_batch / hdrf_wait_batch: up to PIPELINE_DEPTH batches in flight (chunking, SHA
+    and index/store on three streams) give the same results as the sequential oracle; a submit
+    beyond the depth is refused with HDRF_E_CAPACITY (every submit pairs with one wait) and changes
+    nothing."""
     from hdrf_amd.lib import PIPELINE_DEPTH as D
     nb, spb, seg = 14, 8, 1 << 18
     roots = corpus_roots(77, 500000, nb, spb)
@@ -240,11 +241,14 @@ def test_pipelined_submit_wait_matches_sequential_oracle():
 
     pending = []
     for gi, g in enumerate(groups):
-        if len(pending) == D:                # this submit completes the oldest batch itself
-            for b in pending.pop(0):
-                ora.reduce(blocks[b], ids[b])
-        ctx.submit_batch([dev + b * size for b in g], [size] * len(g), [size * (nb - b) + 4096 for b in g],
-                         [ids[b] for b in g])
+        args = ([dev + b * size for b in g], [size] * len(g), [size * (nb - b) + 4096 for b in g], [ids[b] for b in g])
+        if len(pending) == D:                # pipeline full: refused, the caller waits first
+            with pytest.raises(HdrfError) as ei:
+                ctx.submit_batch(*args)
+            assert ei.value.code == -4
+            ctx.wait_batch()
+            check(pending.pop(0))
+        ctx.submit_batch(*args)
         pending.append(g)
         if gi % 4 != 3:                      # mostly keep the pipeline full
             continue
