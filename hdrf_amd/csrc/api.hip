@@ -108,6 +108,8 @@ struct hdrf_ctx {
     hipStream_t stB = nullptr;   // stream B: back stage (index + store)
     hipStream_t stW = nullptr;   // stream W: chunking stage
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
+    hipStream_t stL = nullptr;   // LZ4 side stream (short last segments beside the main kernel)
+    hipEvent_t lz_fork = nullptr, lz_join = nullptr;
     int max_batch = 0, cap_blk = 0, ntiles = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
     Slot sl[kSlots];
     uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
@@ -299,6 +301,9 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
     if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
+    if (ctx->stL) (void)hipStreamDestroy(ctx->stL);
+    if (ctx->lz_fork) (void)hipEventDestroy(ctx->lz_fork);
+    if (ctx->lz_join) (void)hipEventDestroy(ctx->lz_join);
 }
 
 static int alloc_slot(hdrf_ctx *ctx, Slot &S)
@@ -365,6 +370,7 @@ static int drain(hdrf_ctx *ctx)
     while (ctx->nwait < ctx->nsub)
         if (int r = wait_one(ctx)) rc = rc ? rc : r;
     HIPCK(hipStreamSynchronize(ctx->stC));
+    HIPCK(hipStreamSynchronize(ctx->stL));
     HIPCK(hipStreamSynchronize(ctx->stW));
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
@@ -444,7 +450,10 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, pa) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stB, hipStreamNonBlocking, pb) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pa) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stL, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->lz_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->lz_join, hipEventDisableTiming) != hipSuccess) {
         free_all(ctx);
         delete ctx;
         return HDRF_E_HIP;
@@ -718,7 +727,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
                        S.d_pcid, S.d_ppos, S.d_err, Bst, &mb));
     if (c.compressor == 2)      // compression stage: closed containers -> Lz4Codec files (:770-779)
         HIPCK(launch_lz4(S.d_closed, S.d_nclosed, ctx->closed_cap, c.container_max, ctx->d_arena, ctx->d_carena,
-                         ctx->cslot, S.d_segclen, S.d_filelen, Bst));
+                         ctx->cslot, S.d_segclen, S.d_filelen, Bst, ctx->stL, ctx->lz_fork, ctx->lz_join));
     mb.mark(Bst);
     HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nblocks, hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nblocks, hipMemcpyDeviceToHost, Bst));

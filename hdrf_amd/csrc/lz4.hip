@@ -37,19 +37,41 @@ __device__ __forceinline__ int put_len(uint8_t *out, int op, int len)
     return op + n255 + 1;
 }
 
+// LDS of one wave's hash table.  byU16 (blocks < 64 KiB + 11): 8192 u16 entries, 16 KiB.  byU32
+// (larger blocks, <= 262,144 B): 4096 positions < 2^18 kept as a u16 low half + a 2-bit high part
+// (16 per dword, updated with LDS atomics), 9 KiB, so a CU holds 17 compressing waves instead of
+// 10 with u32 entries (the kernel is bound by waves in flight: each match waits on one read at
+// its candidate position).
+constexpr int kLzTabU16 = 16384;
+constexpr int kLzTabU32 = 9216;
+
 // One LZ4 block (lz4 r123 LZ4_compress, noDict): returns the compressed size.  Uniform control
-// flow; `tab` is this wave's LDS hash table (u32 entries, byU32, or u16 entries, byU16).
-__device__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint32_t *tab)
+// flow; `tabmem` is this wave's LDS hash table (layout above).
+__device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint8_t *tabmem)
 {
     const int l = lane_id();
     const bool u16 = n < k64KLimit;
     const int hshift = u16 ? 32 - 13 : 32 - 12;
-    unsigned short *tab16 = (unsigned short *)tab;
-    for (int i = l; i < 4096; i += 64) tab[i] = 0;
+    unsigned short *tab16 = (unsigned short *)tabmem;   // byU16 entries, or the byU32 low halves
+    uint32_t *tabhi = (uint32_t *)(tabmem + 8192);      // byU32 bits 16-17, entry h at word h/16
+    {
+        uint32_t *t32 = (uint32_t *)tabmem;
+        const int nw = (u16 ? kLzTabU16 : kLzTabU32) / 4;
+        for (int i = l; i < nw; i += 64) t32[i] = 0;
+    }
     __builtin_amdgcn_s_waitcnt(0);
     asm volatile("" ::: "memory");
-    auto tget = [&](uint32_t h) -> int { return u16 ? (int)tab16[h] : (int)tab[h]; };
-    auto tput = [&](uint32_t h, int p) { if (u16) tab16[h] = (unsigned short)p; else tab[h] = (uint32_t)p; };
+    auto tget = [&](uint32_t h) -> int {
+        return u16 ? (int)tab16[h] : (int)tab16[h] | (int)(((tabhi[h >> 4] >> (2 * (h & 15))) & 3u) << 16);
+    };
+    auto tput = [&](uint32_t h, int p) {
+        tab16[h] = (unsigned short)p;
+        if (!u16) {
+            const uint32_t sh = 2 * (h & 15);
+            const uint32_t cur = (tabhi[h >> 4] >> sh) & 3u, want = ((uint32_t)p >> 16) & 3u;
+            if (cur != want) atomicXor(&tabhi[h >> 4], (cur ^ want) << sh);   // lanes share words
+        }
+    };
     auto hash = [&](uint32_t v) -> uint32_t { return (v * 2654435761u) >> hshift; };
 
     const int mflimit = n - kMfLimit, matchlimit = n - kLastLit;
@@ -79,14 +101,15 @@ __device__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint32_t *tab)
             // restored and the replay runs lane by lane.
             bool slow = u16;
             if (!u16) {
-                if (valid) old = (int)tab[h];
+                // distinct hashes: scatter lane tags into the low halves and read them back
+                if (valid) old = tget(h);
                 asm volatile("" ::: "memory");
-                if (valid) tab[h] = 0x80000000u | (uint32_t)l;
+                if (valid) tab16[h] = (unsigned short)l;
                 asm volatile("" ::: "memory");
-                const uint32_t t = valid ? tab[h] : 0u;
-                slow = ballot64(valid && t != (0x80000000u | (uint32_t)l)) != 0;
+                const uint32_t t = valid ? (uint32_t)tab16[h] : 0u;
+                slow = ballot64(valid && t != (uint32_t)l) != 0;
                 asm volatile("" ::: "memory");
-                if (slow && valid) tab[h] = (uint32_t)old;         // equal hashes carry equal olds
+                if (slow && valid) tab16[h] = (unsigned short)old;   // equal hashes carry equal olds
                 ref = old;
             }
             asm volatile("" ::: "memory");
@@ -102,7 +125,7 @@ __device__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint32_t *tab)
             const unsigned long long okm = ballot64(ok);
             if (!slow) {                                  // commit: attempts up to the first match
                 const int last = okm ? __builtin_ctzll(okm) : 63;
-                if (valid) tab[h] = l <= last ? (uint32_t)ipl : (uint32_t)old;
+                if (valid) tput(h, l <= last ? ipl : old);
                 asm volatile("" ::: "memory");
             }
             if (okm) {
@@ -217,26 +240,33 @@ last_literals:
     return op;
 }
 
-// grid (nseg_max, nclosed) x 64 threads: segment s of closed container c
+// grid (nseg_max, nclosed) x 64 threads: segment s of closed container c.  Two instances: byU32
+// segments with a 12 KiB table (every 261,100-B segment), byU16 ones (a container's short last
+// segment) with 16 KiB; each returns at once for the other kind.
+template <bool kSmall>
 __global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed,
                                                      const uint32_t *__restrict__ nclosed, const uint8_t *__restrict__ arena,
                                                      uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
                                                      uint32_t *__restrict__ seg_clen, int nseg_max)
 {
-    __shared__ uint32_t tab[4096];
+    __shared__ __attribute__((aligned(16))) uint8_t tabmem[kSmall ? kLzTabU16 : kLzTabU32];
     const int c = blockIdx.y, s = blockIdx.x;
     if ((uint32_t)c >= *nclosed) return;                   // grid sized for closed_cap
     const ClosedRec r = closed[c];
     const int64_t off = (int64_t)s * kLzMaxIn;
     if (off >= (int64_t)r.len) return;
     const int n = (int)min((int64_t)kLzMaxIn, (int64_t)r.len - off);
+    if ((n < k64KLimit) != kSmall) return;
     const uint8_t *src = arena + (size_t)r.slot * cmax + off;
     uint8_t *out = carena + (size_t)r.slot * cslot + 8 + (size_t)s * kLzSegStride;
-    const int cl = lz4_block(src, n, out, tab);
+    const int cl = lz4_block(src, n, out, tabmem);
     if (lane_id() == 0) seg_clen[(size_t)c * nseg_max + s] = (uint32_t)cl;
 }
 
-// grid nclosed x 256 threads: frame the segments in place, [BE32 len] ([BE32 clen] block)* [BE32 0]
+// grid nclosed x 256 threads: frame the segments in place, [BE32 len] ([BE32 clen] block)* [BE32 0].
+// Every segment moves to a lower (or equal) offset, so tiles copied in order — all loads of a tile
+// before any of its stores — never overwrite bytes not yet read.  A tile is 16 KiB (four 16-B
+// words per thread, source realigned with load16_shift, destination 16-B aligned after a head).
 __global__ void __launch_bounds__(256) lz4_pack_kernel(const ClosedRec *__restrict__ closed,
                                                        const uint32_t *__restrict__ nclosed, uint8_t *__restrict__ carena,
                                                        uint64_t cslot, const uint32_t *__restrict__ seg_clen, int nseg_max,
@@ -253,18 +283,38 @@ __global__ void __launch_bounds__(256) lz4_pack_kernel(const ClosedRec *__restri
         const uint32_t cl = seg_clen[(size_t)c * nseg_max + s];
         const uint32_t from = 8 + (uint32_t)s * kLzSegStride;
         const uint32_t to = pos + 4;
-        if (to != from) {                                  // to < from: forward tiles, load then store
-            for (uint32_t o = 0; o < cl; o += 256 * 16) {
-                uint8_t v[16];
-                const uint32_t q = o + 16 * t;
+        if (to != from && cl) {
+            uint8_t *dst = base + to;
+            const uint8_t *src = base + from;
+            uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
+            if (head > cl) head = cl;
+            const uint8_t hb = (uint32_t)t < head ? src[t] : 0;
+            __syncthreads();
+            if ((uint32_t)t < head) dst[t] = hb;
+            const uint32_t n16 = (cl - head) >> 4;
+            const uint8_t *sp = src + head;
+            const int sh = (int)((uintptr_t)sp & 15);
+            const uint8_t *sa = sp - sh;
+            uint8_t *d = dst + head;
+            for (uint32_t w0 = 0; w0 < n16; w0 += 1024) {
+                uint4 v[4];
 #pragma unroll
-                for (int k = 0; k < 16; k++) v[k] = (q + k < cl) ? base[from + q + k] : 0;
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t w = w0 + 256 * k + t;
+                    v[k] = w < n16 ? load16_shift(sa + 16 * (size_t)w, sh) : make_uint4(0, 0, 0, 0);
+                }
                 __syncthreads();
 #pragma unroll
-                for (int k = 0; k < 16; k++)
-                    if (q + k < cl) base[to + q + k] = v[k];
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t w = w0 + 256 * k + t;
+                    if (w < n16) st16(d + 16 * (size_t)w, v[k]);
+                }
                 __syncthreads();
             }
+            const uint32_t tb = head + 16 * n16;
+            const uint8_t tv = tb + t < cl ? src[tb + t] : 0;
+            __syncthreads();
+            if (tb + t < cl) dst[tb + t] = tv;
         }
         if (t == 0) put_be32(base + pos, cl);
         __syncthreads();
@@ -290,11 +340,11 @@ __global__ void __launch_bounds__(64) lz4_list_kernel(const LzPiece *__restrict_
                                                       const uint8_t *__restrict__ base, uint8_t *__restrict__ stage,
                                                       uint32_t *__restrict__ clen)
 {
-    __shared__ uint32_t tab[4096];
+    __shared__ __attribute__((aligned(16))) uint8_t tabmem[kLzTabU16];
     const int i = blockIdx.x;
     if (i >= n) return;
     const LzPiece pc = pieces[i];
-    const int c = lz4_block(base + pc.src, (int)pc.len, stage + (size_t)i * kLzSegStride, tab);
+    const int c = lz4_block(base + pc.src, (int)pc.len, stage + (size_t)i * kLzSegStride, tabmem);
     if (lane_id() == 0) clen[i] = (uint32_t)c;
 }
 
@@ -423,13 +473,21 @@ uint64_t lz4_piece_stride() { return kLzSegStride; }
 
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
                       const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
-                      hipStream_t st)
+                      hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join)
 {
     // grid covers closed_cap containers; workgroups past the device-side count exit at once, so
-    // the compression stays in stream order with the batch (no host round trip)
+    // the compression stays in stream order with the batch (no host round trip).  The short last
+    // segments (16 KiB tables, a few dozen waves) run on the side stream beside the main kernel.
     const int nseg_max = (int)((cmax + kLzMaxIn - 1) / kLzMaxIn);
-    hipLaunchKernelGGL(lz4_seg_kernel, dim3(nseg_max, closed_cap), dim3(64), 0, st, closed, nclosed, arena,
+    hipError_t e = hipEventRecord(fork, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(lz4_seg_kernel<true>, dim3(nseg_max, closed_cap), dim3(64), 0, side, closed, nclosed, arena,
                        (uint64_t)cmax, carena, cslot, seg_clen, nseg_max);
+    if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
+    hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(nseg_max, closed_cap), dim3(64), 0, st, closed, nclosed, arena,
+                       (uint64_t)cmax, carena, cslot, seg_clen, nseg_max);
+    if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(lz4_pack_kernel, dim3(closed_cap), dim3(256), 0, st, closed, nclosed, carena, cslot, seg_clen,
                        nseg_max, file_len);
     return hipGetLastError();
