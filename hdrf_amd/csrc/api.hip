@@ -1679,6 +1679,33 @@ static int fetch_table(hdrf_ctx *ctx, std::vector<IndexEntry> &tab)
     return 0;
 }
 
+// Probe lengths of the last completed batch (linear probing from each chunk's home slot to the
+// entry it resolved to): sum, max and the number of chunks.  Steady-state index measurement.
+extern "C" int hdrf_probe_stats(hdrf_ctx *ctx, int64_t *probe_sum, int64_t *probe_max, int64_t *chunks)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || !probe_sum || !probe_max || !chunks) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "probe stats on node-global contexts");
+    if (int rc = drain(ctx)) return rc;
+    Slot &S = ctx->sl[ctx->res];
+    if (ctx->last_nblocks < 1) return set_err(ctx, HDRF_E_INVAL, "no completed batch");
+    unsigned long long *d = nullptr;
+    HIPCK(hipMalloc((void **)&d, 3 * sizeof(unsigned long long)));
+    unsigned long long h[3] = {0, 0, 0};
+    hipError_t e = hipMemsetAsync(d, 0, sizeof h, ctx->st);
+    if (e == hipSuccess)
+        e = launch_index_probe(ctx->cfg.hasher, S.d_bst, ctx->last_nblocks, ctx->cap_blk, S.d_dig, S.d_slot,
+                               ctx->cfg.index_log2, tag_mask(ctx), d, ctx->st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, ctx->st);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->st);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_err(ctx, HDRF_E_HIP, hipGetErrorString(e));
+    *probe_sum = (int64_t)h[0];
+    *probe_max = (int64_t)h[1];
+    *chunks = (int64_t)h[2];
+    return 0;
+}
+
 extern "C" int64_t hdrf_index_count(hdrf_ctx *ctx)
 {
     HDRF_LOCK(ctx);

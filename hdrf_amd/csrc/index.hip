@@ -303,6 +303,52 @@ hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals
     return hipGetLastError();
 }
 
+// Probe lengths of a completed batch (steady-state measurement): each chunk's final slot minus its
+// home slot, summed / maxed into stats[0] (sum), stats[1] (max), stats[2] (chunks)
+template <int HW>
+__global__ void __launch_bounds__(256) idx_probe_kernel(const BlockState *__restrict__ bst, int cap_blk,
+                                                        const uint32_t *__restrict__ digests, const uint32_t *__restrict__ slot,
+                                                        int log2cap, unsigned long long tag_mask,
+                                                        unsigned long long *__restrict__ stats)
+{
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const bool on = k < bst[b].n_chunks;
+    unsigned long long d = 0;
+    if (on) {
+        const size_t c = (size_t)b * cap_blk + k;
+        uint32_t dw[HW];
+#pragma unroll
+        for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
+        uint32_t z;
+        const unsigned long long tag = make_tag(dw, z, tag_mask);
+        const uint64_t mask = (1ull << log2cap) - 1;
+        d = ((uint64_t)slot[c] - home_slot(tag, log2cap)) & mask;
+    }
+    // wave reductions, one atomic per wave
+    unsigned long long s = d, m = d, n = on ? 1ull : 0ull;
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
+        n += __shfl_xor(n, o, 64);
+    }
+    if (lane_id() == 0 && n) {
+        atomicAdd(&stats[0], s);
+        atomicMax(&stats[1], m);
+        atomicAdd(&stats[2], n);
+    }
+}
+
+hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *digests,
+                              const uint32_t *slot, int log2cap, unsigned long long tag_mask,
+                              unsigned long long *stats, hipStream_t st)
+{
+    dim3 g((cap_blk + 255) / 256, nblocks);
+    if (hasher == 0) hipLaunchKernelGGL(idx_probe_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, slot, log2cap, tag_mask, stats);
+    else hipLaunchKernelGGL(idx_probe_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, slot, log2cap, tag_mask, stats);
+    return hipGetLastError();
+}
+
 hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st)
 {
     const uint64_t n16 = (sizeof(IndexEntry) << log2cap) / 16;

@@ -52,6 +52,9 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
                       hipStream_t st, Marker *mk);
 hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals, int n, IndexEntry *tab, int log2cap,
                              unsigned long long tag_mask, int *err, hipStream_t st);
+hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *digests,
+                              const uint32_t *slot, int log2cap, unsigned long long tag_mask,
+                              unsigned long long *stats, hipStream_t st);
 hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st);
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,

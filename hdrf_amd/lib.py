@@ -32,6 +32,7 @@ EXPORTS = [
     "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
     "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
+    "hdrf_probe_stats",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -122,6 +123,8 @@ def load():
         "hdrf_reduce_block_ticketed": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _u8p, ctypes.c_uint64,
                                                       ctypes.POINTER(BlockResult)]),
         "hdrf_ticket_take": (ctypes.c_int, [_vp, _u64p]),
+        "hdrf_probe_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                            ctypes.POINTER(ctypes.c_int64)]),
         "hdrf_ticket_cancel": (ctypes.c_int, [_vp, ctypes.c_uint64]),
         "hdrf_drain_containers": (ctypes.c_int64, [_vp, ctypes.POINTER(ContainerEvent), ctypes.c_int64, _u8p,
                                                    ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]),
@@ -269,6 +272,12 @@ class Context:
         return {"offsets": offs[:n].copy(), "digests": digs[:n * self.H].reshape(n, self.H).copy(),
                 "is_new": isnew[:n].copy(), "container_id": cid[:n].copy(), "container_pos": pos[:n].copy(),
                 "store_size": r.store_size}
+
+    def probe_stats(self):
+        """(probe_sum, probe_max, chunks) of the last completed batch."""
+        a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self._ck(self.L.hdrf_probe_stats(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
 
     def ticket_take(self):
         t = ctypes.c_uint64()

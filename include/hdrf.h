@@ -182,6 +182,9 @@ int hdrf_batch_placement(hdrf_ctx *ctx, int32_t b, uint32_t *cid, uint32_t *pos,
  * Returns 1 if found, 0 if absent, <0 on error. */
 int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out11[11]);
 int64_t hdrf_index_count(hdrf_ctx *ctx);
+/* Probe lengths of the last completed batch: each chunk's distance (entries) from its home slot to
+ * the entry its digest resolved to (linear probing); sum, max and chunk count.  Measurement only. */
+int hdrf_probe_stats(hdrf_ctx *ctx, int64_t *probe_sum, int64_t *probe_max, int64_t *chunks);
 /* All (digest, value) pairs sorted by digest; returns count (or HDRF_E_CAPACITY). */
 int64_t hdrf_index_dump(hdrf_ctx *ctx, uint8_t *keys, uint8_t *vals, int64_t cap);
 /* GET "blockID": 24-byte allocator (utilities.blockIDtoBytes, DN/utilities.java:66-75).

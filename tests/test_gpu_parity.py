@@ -564,3 +564,28 @@ def test_restart_from_persisted_state(hasher, compressor):
     for i, b in zip(ids, blocks):
         assert np.array_equal(ctx2.reconstruct_block(i), b), f"block {i}"
     ctx2.close()
+
+
+def test_probe_stats_count_every_chunk():
+    """hdrf_probe_stats (steady-state index measurement) covers every chunk of the last batch; on a
+    nearly full small table the probes get longer than on an empty one."""
+    blocks = [make_block("random", 910 + i, 1_000_000) for i in range(4)]
+    lens = []
+    for log2 in (20, 13):
+        ctx = Context(max_block_bytes=4 << 20, max_batch_blocks=4, index_log2=log2, arena_slots=16,
+                      container_max=1 << 21)
+        pinned = ctx.host_alloc(sum(len(b) for b in blocks))
+        o, ptrs = 0, []
+        for b in blocks:
+            pinned[o:o + len(b)] = b
+            ptrs.append(pinned.ctypes.data + o)
+            o += len(b)
+        ctx.submit_host(ptrs, [len(b) for b in blocks], [1, 2, 3, 4])
+        ctx.wait_batch()
+        n = sum(ctx.batch_info(i)[0] for i in range(4))
+        s, m, c = ctx.probe_stats()
+        assert c == n and m >= 0 and s >= 0
+        lens.append(s / c)
+        ctx.host_free(pinned)
+        ctx.close()
+    assert lens[1] > lens[0]
