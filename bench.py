@@ -81,6 +81,10 @@ def parse():
                          "batches (off by default so a rocprof summary of the bench matches its in-pipeline averages)")
     ap.add_argument("--arena-slots", type=int, default=512,
                     help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers")
+    ap.add_argument("--packet-kib", type=int, default=0,
+                    help="config5: deliver every block as packets of this many KiB (hdrf_rx_begin / "
+                         "hdrf_append_packet / hdrf_submit_slot, one block per submit: the JNI shape); "
+                         "0 = whole blocks through hdrf_submit_host")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
                     help="config4: mixed-entropy blocks (random/text/binary), dedup + Lz4Codec containers; "
                          "config5: host-resident (pinned) blocks streamed H2D on a side stream (PCIe-inclusive)")
@@ -172,6 +176,25 @@ def main():
         if node is None and a.serial:
             for ptrs, lens, rd, ids in batches:
                 ctx.reduce_batch(ptrs, lens, rd, ids)
+                collect()
+        elif host and a.packet_kib:
+            # packet-granular receive, one block per submit (the JNI shape): each block's packets are
+            # appended as they "arrive" (chunk H2D on the copy stream) while earlier blocks reduce
+            P = a.packet_kib << 10
+            pend = 0
+            for b in range(nb):
+                rx = ctx.rx_begin(b)
+                base = hbuf.ctypes.data + b * S
+                for o in range(0, S, P):
+                    ctx.append_packet(rx, base + o, min(P, S - o))
+                if pend == 3:
+                    ctx.wait_batch()
+                    collect()
+                    pend -= 1
+                ctx.submit_slot(rx)
+                pend += 1
+            for _ in range(pend):
+                ctx.wait_batch()
                 collect()
         elif host:
             # streaming: the H2D copies of batch k+1 (side stream) overlap the reduction of batch k
@@ -363,9 +386,12 @@ def main():
             line["read_side"] = read_side
         if host:
             line["config"]["workload"] = ("config5: %d x %d MiB host-resident (pinned) blocks, %d%% dup, streamed "
-                                          "H2D on a side stream overlapped with the reduction (hdrf_submit_host), "
+                                          "H2D on a side stream overlapped with the reduction (%s), "
                                           "chunk+SHA-1+local index+container store, fresh index per step"
-                                          % (nb, a.block_mib, a.dup_ppm // 10000))
+                                          % (nb, a.block_mib, a.dup_ppm // 10000,
+                                             ("%d KiB packets, hdrf_append_packet + hdrf_submit_slot, one block "
+                                              "per submit" % a.packet_kib) if a.packet_kib else
+                                             "whole blocks, hdrf_submit_host"))
             line["pcie"] = {"h2d_GB_s_raw_copy": round(h2d_gbs, 2), "value_over_raw_copy": round(value / h2d_gbs, 4),
                             "note": "value is PCIe-inclusive: host buffers -> HBM -> reduced"}
         print(json.dumps(line), flush=True)

@@ -88,6 +88,7 @@ struct Slot {
     int nblocks = 0;
     bool pending = false;
     uint32_t close_bound = 0;                 // durable containers: closes this batch may make per range
+    int rx_release = -1;                      // packet path: receive buffer to free when the batch completes
     uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
     RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
     hipEvent_t recipe_done = nullptr;         // the copies read d_dig: the slot's next SHA waits
@@ -170,6 +171,18 @@ struct hdrf_ctx {
     uint32_t inflight_bound = 0;
     std::map<uint32_t, int64_t> handed;
     bool lost = false;
+    // packet-granular receive (hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot): device
+    // receive buffers, and a pinned chunk ring the packets are copied into before their H2D
+    static constexpr int kRx = 8;
+    static constexpr int kRingChunks = 8;
+    static constexpr uint64_t kRingChunk = 4ull << 20;
+    struct Rx { uint8_t *d = nullptr; uint64_t len = 0; uint64_t id = 0; int state = 0; };   // 0 free 1 receiving 2 submitted
+    Rx rx[kRx];
+    uint8_t *h_ring = nullptr;
+    hipEvent_t ring_ev[kRingChunks] = {};
+    bool ring_busy[kRingChunks] = {};
+    int ring_cur = 0, ring_rx = -1;
+    uint64_t ring_fill = 0, ring_dst = 0;
     // timing
     bool timing = false;
     double stage_ms[kStages] = {};
@@ -302,6 +315,11 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
     if (ctx->stL) (void)hipStreamDestroy(ctx->stL);
+    for (auto &r : ctx->rx)
+        if (r.d) (void)hipFree(r.d);
+    if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
+    for (auto &e : ctx->ring_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->lz_fork) (void)hipEventDestroy(ctx->lz_fork);
     if (ctx->lz_join) (void)hipEventDestroy(ctx->lz_join);
 }
@@ -412,6 +430,10 @@ static int init_state(hdrf_ctx *ctx)
     ctx->inflight_bound = 0;
     ctx->handed.clear();
     ctx->lost = false;
+    for (auto &r : ctx->rx) { r.state = 0; r.len = 0; }
+    for (auto &S : ctx->sl) S.rx_release = -1;
+    ctx->ring_rx = -1;
+    ctx->ring_fill = 0;
     return 0;
 }
 
@@ -871,7 +893,102 @@ static int wait_one(hdrf_ctx *ctx)
     ctx->nwait++;
     S.pending = false;
     HIPCK(hipEventSynchronize(S.back_done));
+    if (S.rx_release >= 0) {                           // its receive buffer is free again
+        ctx->rx[S.rx_release].state = 0;
+        ctx->rx[S.rx_release].len = 0;
+        S.rx_release = -1;
+    }
     return complete_slot(ctx, si, true);
+}
+
+// ---- packet-granular receive (DN/BlockReceiver.java:877-896: each packet appended to bf1 as it
+// arrives; :1258-1261 the finished block handed to the reducer) ------------------------------
+// A packet is copied into a pinned 4 MiB chunk of a ring (the caller may reuse it when the call
+// returns); every full chunk goes H2D on stream C into the block's receive buffer, overlapping the
+// next packets and the kernels of the blocks in flight.  The ring's chunks are reused in order,
+// waiting (host side) for a chunk's copy only when the ring wraps.
+static int ring_flush(hdrf_ctx *ctx)
+{
+    if (ctx->ring_fill == 0) return 0;
+    const int c = ctx->ring_cur;
+    hdrf_ctx::Rx &r = ctx->rx[ctx->ring_rx];
+    HIPCK(hipMemcpyAsync(r.d + ctx->ring_dst, ctx->h_ring + (uint64_t)c * hdrf_ctx::kRingChunk, ctx->ring_fill,
+                         hipMemcpyHostToDevice, ctx->stC));
+    HIPCK(hipEventRecord(ctx->ring_ev[c], ctx->stC));
+    ctx->ring_busy[c] = true;
+    ctx->ring_cur = (c + 1) % hdrf_ctx::kRingChunks;
+    ctx->ring_fill = 0;
+    if (ctx->ring_busy[ctx->ring_cur]) {               // ring wrapped: that chunk's copy must have landed
+        HIPCK(hipEventSynchronize(ctx->ring_ev[ctx->ring_cur]));
+        ctx->ring_busy[ctx->ring_cur] = false;
+    }
+    return 0;
+}
+
+extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || !rx) return HDRF_E_INVAL;
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
+    if (!ctx->h_ring) {
+        HIPCK(hipHostMalloc((void **)&ctx->h_ring, hdrf_ctx::kRingChunks * hdrf_ctx::kRingChunk));
+        for (auto &e : ctx->ring_ev) HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    for (int i = 0; i < hdrf_ctx::kRx; i++) {
+        hdrf_ctx::Rx &r = ctx->rx[i];
+        if (r.state != 0) continue;
+        if (!r.d) HIPCK(hipMalloc((void **)&r.d, (uint64_t)ctx->cfg.max_block_bytes + kSlack + 256));
+        r.state = 1;
+        r.len = 0;
+        r.id = block_id;
+        *rx = i;
+        return 0;
+    }
+    return set_err(ctx, HDRF_E_CAPACITY, "every receive buffer holds a block being received or reduced (hdrf_wait_batch)");
+}
+
+extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data, uint64_t len)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state != 1 || (len && !data))
+        return ctx ? set_err(ctx, HDRF_E_INVAL, "bad receive buffer or packet") : HDRF_E_INVAL;
+    hdrf_ctx::Rx &r = ctx->rx[rx];
+    if (r.len + len > (uint64_t)ctx->cfg.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
+    while (len) {
+        if (ctx->ring_fill && ctx->ring_rx != rx)
+            if (int rc = ring_flush(ctx)) return rc;   // the chunk holds another block's packets
+        if (ctx->ring_fill == 0) { ctx->ring_rx = rx; ctx->ring_dst = r.len; }
+        const uint64_t n = std::min(len, hdrf_ctx::kRingChunk - ctx->ring_fill);
+        std::memcpy(ctx->h_ring + (uint64_t)ctx->ring_cur * hdrf_ctx::kRingChunk + ctx->ring_fill, data, n);
+        ctx->ring_fill += n;
+        r.len += n;
+        data += n;
+        len -= n;
+        if (ctx->ring_fill == hdrf_ctx::kRingChunk)
+            if (int rc = ring_flush(ctx)) return rc;
+    }
+    return 0;
+}
+
+extern "C" int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state != 1)
+        return ctx ? set_err(ctx, HDRF_E_INVAL, "bad receive buffer") : HDRF_E_INVAL;
+    if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)     // every submit pairs with one hdrf_wait_batch
+        return set_err(ctx, HDRF_E_CAPACITY, "pipeline full: hdrf_wait_batch first");
+    hdrf_ctx::Rx &r = ctx->rx[rx];
+    if (ctx->ring_rx == rx)
+        if (int rc = ring_flush(ctx)) return rc;
+    HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, ctx->stC));
+    Slot &S = ctx->sl[ctx->nsub % kSlots];
+    HIPCK(hipEventRecord(S.copy_done, ctx->stC));
+    const uint8_t *p = r.d;
+    const uint64_t len = r.len, readable = (uint64_t)ctx->cfg.max_block_bytes + kSlack + 256, id = r.id;
+    if (int rc = submit(ctx, 1, &p, &len, &readable, &id, true)) return rc;
+    S.rx_release = rx;
+    r.state = 2;
+    return 0;
 }
 
 extern "C" int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,

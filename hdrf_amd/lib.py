@@ -32,7 +32,7 @@ EXPORTS = [
     "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
     "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
-    "hdrf_probe_stats",
+    "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -123,6 +123,9 @@ def load():
         "hdrf_reduce_block_ticketed": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint64, _u8p, ctypes.c_uint64,
                                                       ctypes.POINTER(BlockResult)]),
         "hdrf_ticket_take": (ctypes.c_int, [_vp, _u64p]),
+        "hdrf_rx_begin": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32)]),
+        "hdrf_append_packet": (ctypes.c_int, [_vp, ctypes.c_int32, _vp, ctypes.c_uint64]),
+        "hdrf_submit_slot": (ctypes.c_int, [_vp, ctypes.c_int32]),
         "hdrf_probe_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                             ctypes.POINTER(ctypes.c_int64)]),
         "hdrf_ticket_cancel": (ctypes.c_int, [_vp, ctypes.c_uint64]),
@@ -272,6 +275,18 @@ class Context:
         return {"offsets": offs[:n].copy(), "digests": digs[:n * self.H].reshape(n, self.H).copy(),
                 "is_new": isnew[:n].copy(), "container_id": cid[:n].copy(), "container_pos": pos[:n].copy(),
                 "store_size": r.store_size}
+
+    def rx_begin(self, block_id):
+        r = ctypes.c_int32()
+        self._ck(self.L.hdrf_rx_begin(self._h, block_id, ctypes.byref(r)))
+        return r.value
+
+    def append_packet(self, rx, ptr, nbytes):
+        """Host address + length of one received packet (copied before the call returns)."""
+        self._ck(self.L.hdrf_append_packet(self._h, rx, ptr, nbytes))
+
+    def submit_slot(self, rx):
+        self._ck(self.L.hdrf_submit_slot(self._h, rx))
 
     def probe_stats(self):
         """(probe_sum, probe_max, chunks) of the last completed batch."""

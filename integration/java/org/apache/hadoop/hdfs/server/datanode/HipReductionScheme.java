@@ -81,6 +81,24 @@ public final class HipReductionScheme extends ReductionScheme {
     submit0(ctx, block, block.position(), blockId);
   }
 
+  /**
+   * Packet-granular receive (BlockReceiver.java:877-896): begin a block, hand every packet over as
+   * it arrives (copied before the call returns; its H2D overlaps the next packets and the blocks in
+   * flight), then submit it.  Pair every submitBlock with one awaitOldest, like reduceAsync.
+   */
+  public int beginBlock(long blockId) throws IOException {
+    return rxBegin0(ctx, blockId);
+  }
+
+  public void packet(int rx, ByteBuffer pkt, int off, int len) throws IOException {
+    if (!pkt.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
+    packet0(ctx, rx, pkt, off, len);
+  }
+
+  public void submitBlock(int rx) throws IOException {
+    submitSlot0(ctx, rx);
+  }
+
   /** Complete the oldest block submitted with reduceAsync (its index/containers/recipe are final). */
   public void awaitOldest() throws IOException {
     wait0(ctx);
@@ -134,4 +152,7 @@ public final class HipReductionScheme extends ReductionScheme {
   private static native int drain0(long ctx, String chunkDir) throws IOException;
   private static native ByteBuffer allocPinned0(long ctx, long bytes) throws IOException;
   private static native void freePinned0(long ctx, ByteBuffer buf) throws IOException;
+  private static native int rxBegin0(long ctx, long blockId) throws IOException;
+  private static native void packet0(long ctx, int rx, ByteBuffer pkt, int off, int len) throws IOException;
+  private static native void submitSlot0(long ctx, int rx) throws IOException;
 }

@@ -154,6 +154,36 @@ JNIEXPORT void JNICALL JFN(freePinned0)(JNIEnv *env, jclass cls, jlong h, jobjec
     if (rc) throw_io(env, ctx, rc);
 }
 
+/* Packet-granular receive (BlockReceiver.java:877-896): each received packet goes to the GPU as it
+ * arrives; submitSlot hands the finished block to the pipeline (pair with wait0). */
+JNIEXPORT jint JNICALL JFN(rxBegin0)(JNIEnv *env, jclass cls, jlong h, jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int32_t rx = -1;
+    int rc = hdrf_rx_begin(ctx, (uint64_t)id, &rx);
+    if (rc) throw_io(env, ctx, rc);
+    return rx;
+}
+
+JNIEXPORT void JNICALL JFN(packet0)(JNIEnv *env, jclass cls, jlong h, jint rx, jobject buf, jint off, jint len)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
+    if (!p && len) { throw_io(env, ctx, HDRF_E_INVAL); return; }
+    int rc = hdrf_append_packet(ctx, rx, p + off, (uint64_t)len);   /* copied before return */
+    if (rc) throw_io(env, ctx, rc);
+}
+
+JNIEXPORT void JNICALL JFN(submitSlot0)(JNIEnv *env, jclass cls, jlong h, jint rx)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int rc = hdrf_submit_slot(ctx, rx);
+    if (rc) throw_io(env, ctx, rc);
+}
+
 /* reduceAsync: hdrf_submit_host on the direct buffer (copied H2D on a side stream) */
 JNIEXPORT void JNICALL JFN(submit0)(JNIEnv *env, jclass cls, jlong h, jobject buf, jint len, jlong id)
 {

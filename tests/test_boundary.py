@@ -190,3 +190,52 @@ def test_pipeline_depth_is_refused_not_waited():
     with pytest.raises(HdrfError):
         ctx.wait_batch()                                     # nothing left in flight
     ctx.close()
+
+
+def test_packet_receive_matches_oracle():
+    """hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot (DN/BlockReceiver.java:877-896): blocks
+    arrive as ragged packets, two blocks' packets interleaved, packet buffers overwritten right
+    after each call; every block is reduced exactly like the sequential oracle in submit order."""
+    rng = np.random.default_rng(71)
+    blocks = _blocks(71, 6, 900_000)
+    blocks[2] = blocks[2][:3]                                  # a 3-byte block
+    blocks[4] = np.zeros(0, np.uint8)                          # an empty block
+    ids = [8000 + i for i in range(len(blocks))]
+    ctx = Context(container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64)
+    ora = Oracle(max_size=1 << 20)
+    scratch = np.zeros(1 << 21, np.uint8)                      # the "network buffer", reused per packet
+
+    def packets(b):
+        o, out = 0, []
+        while o < len(b):
+            n = int(rng.choice([1, 700, 65536, 100_003, 1 << 20]))
+            out.append(b[o:o + n])
+            o += n
+        return out
+
+    pending = []
+    order = []
+    for pair in ((0, 1), (2, 3), (4, 5)):
+        rxs = {b: ctx.rx_begin(ids[b]) for b in pair}
+        queues = {b: packets(blocks[b]) for b in pair}
+        while any(queues.values()):                            # interleave the two blocks' packets
+            for b in pair:
+                if queues[b]:
+                    p = queues[b].pop(0)
+                    scratch[:len(p)] = p
+                    ctx.append_packet(rxs[b], scratch.ctypes.data, len(p))
+                    scratch[:len(p)] = 0xA5                    # the caller reuses its buffer at once
+        for b in pair:
+            if len(pending) == 3:
+                ctx.wait_batch()
+                g = pending.pop(0)
+                compare_block(ctx.batch_result(0), ora.reduce(blocks[g], ids[g]), tag=f"packet block {g}")
+            ctx.submit_slot(rxs[b])
+            pending.append(b)
+            order.append(b)
+    while pending:
+        ctx.wait_batch()
+        g = pending.pop(0)
+        compare_block(ctx.batch_result(0), ora.reduce(blocks[g], ids[g]), tag=f"packet block {g}")
+    compare_state(ctx, ora, ids, tag="packets")
+    ctx.close()
