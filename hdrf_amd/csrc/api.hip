@@ -1268,6 +1268,113 @@ static int64_t decode_file(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uin
     return (int64_t)raw;
 }
 
+// ---- GzipCodec read side (DN/DataConstructor.java:194-218) -----------------------------------
+// CRC-32 combination over GF(2) (zlib's crc32_combine: the CRC of A||B from crc(A), crc(B), |B|)
+static uint32_t gf2_times(const uint32_t *mat, uint32_t vec)
+{
+    uint32_t sum = 0;
+    for (int i = 0; vec; vec >>= 1, i++)
+        if (vec & 1) sum ^= mat[i];
+    return sum;
+}
+static void gf2_square(uint32_t *sq, const uint32_t *mat)
+{
+    for (int n = 0; n < 32; n++) sq[n] = gf2_times(mat, mat[n]);
+}
+// the operator "append len2 zero bytes" as a 32x32 matrix (columns)
+static void crc_shift_op(uint32_t *op, int64_t len2)
+{
+    uint32_t odd[32], even[32];
+    odd[0] = 0xEDB88320u;                     // x^1 (one zero bit)
+    uint32_t row = 1;
+    for (int n = 1; n < 32; n++) { odd[n] = row; row <<= 1; }
+    gf2_square(even, odd);                    // 2 bits
+    gf2_square(odd, even);                    // 4 bits
+    for (int n = 0; n < 32; n++) op[n] = 1u << n;     // identity
+    uint32_t *cur = odd, *nxt = even;         // cur: the operator for 8 * 2^k bits as k grows
+    // start at one byte: square twice more (8 bits)
+    gf2_square(nxt, cur);                     // 8 bits in nxt
+    std::swap(cur, nxt);
+    while (len2) {
+        if (len2 & 1) {
+            uint32_t t[32];
+            for (int n = 0; n < 32; n++) t[n] = gf2_times(cur, op[n]);
+            std::memcpy(op, t, sizeof t);
+        }
+        len2 >>= 1;
+        if (!len2) break;
+        gf2_square(nxt, cur);
+        std::swap(cur, nxt);
+    }
+}
+static uint32_t crc_combine_op(const uint32_t *op, uint32_t crc1, uint32_t crc2) { return gf2_times(op, crc1) ^ crc2; }
+
+static int64_t decode_gzip(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap)
+{
+    if (flen < 0 || (flen && !file) || cap < 0 || (cap && !dev_out)) return set_err(ctx, HDRF_E_INVAL, "bad buffers");
+    if (flen == 0) return 0;                  // an empty file decodes to nothing
+    if (int rc = drain(ctx)) return rc;
+    constexpr int64_t kPiece = 1 << 16;
+    const uint64_t o_res = 0, o_crc = 256, pieces_cap = (uint64_t)(cap / kPiece + 2);
+    const uint64_t o_file = (o_crc + 4 * pieces_cap + 255) & ~255ull;
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_file + (uint64_t)flen + 64)) return rc;
+    uint8_t *R = ctx->d_rd;
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(R + o_file, file, (size_t)flen, hipMemcpyHostToDevice, st));
+    uint32_t piece_op[32];
+    crc_shift_op(piece_op, kPiece);
+    int64_t at = 0, out = 0;
+    std::vector<uint32_t> crcs;
+    while (at < flen) {
+        // gzip member header (RFC 1952): ID1 ID2 CM FLG MTIME(4) XFL OS [XLEN extra] [name\0] [comment\0] [CRC16]
+        if (flen - at < 18 || file[at] != 0x1f || file[at + 1] != 0x8b || file[at + 2] != 8)
+            return set_err(ctx, HDRF_E_INVAL, "not a gzip member at offset " + std::to_string(at));
+        const uint8_t flg = file[at + 3];
+        int64_t h = at + 10;
+        if (flg & 4) { if (h + 2 > flen) return set_err(ctx, HDRF_E_INVAL, "gzip header"); h += 2 + (file[h] | (file[h + 1] << 8)); }
+        if (flg & 8) { while (h < flen && file[h]) h++; h++; }
+        if (flg & 16) { while (h < flen && file[h]) h++; h++; }
+        if (flg & 2) h += 2;
+        if (h > flen) return set_err(ctx, HDRF_E_INVAL, "gzip header");
+        HIPCK(launch_inflate(R + o_file + h, flen - h, dev_out + out, cap - out, (int64_t *)(R + o_res), st));
+        int64_t res[2] = {0, 0};
+        HIPCK(hipMemcpyAsync(res, R + o_res, sizeof res, hipMemcpyDeviceToHost, st));
+        HIPCK(hipStreamSynchronize(st));
+        if (res[0] == -12) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
+        if (res[0] < 0) return set_err(ctx, HDRF_E_INVAL, "corrupt deflate stream (inflate error " + std::to_string(res[0]) + ")");
+        const int64_t n = res[0], end = h + res[1];
+        if (end + 8 > flen) return set_err(ctx, HDRF_E_INVAL, "gzip trailer missing");
+        const uint32_t want_crc = (uint32_t)file[end] | ((uint32_t)file[end + 1] << 8) | ((uint32_t)file[end + 2] << 16) |
+                                  ((uint32_t)file[end + 3] << 24);
+        const uint32_t isize = (uint32_t)file[end + 4] | ((uint32_t)file[end + 5] << 8) | ((uint32_t)file[end + 6] << 16) |
+                               ((uint32_t)file[end + 7] << 24);
+        if (isize != (uint32_t)n) return set_err(ctx, HDRF_E_INVAL, "gzip ISIZE mismatch");
+        // CRC-32 of this member's output: 64 KiB pieces on the GPU, combined here
+        const int64_t np = (n + kPiece - 1) / kPiece;
+        uint32_t crc = 0;
+        if (np) {
+            HIPCK(launch_crc32_pieces(dev_out + out, n, kPiece, (uint32_t *)(R + o_crc), st));
+            crcs.resize((size_t)np);
+            HIPCK(hipMemcpyAsync(crcs.data(), R + o_crc, 4 * (size_t)np, hipMemcpyDeviceToHost, st));
+            HIPCK(hipStreamSynchronize(st));
+            crc = crcs[0];
+            for (int64_t i = 1; i < np; i++) {
+                const int64_t len2 = std::min(kPiece, n - i * kPiece);
+                if (len2 == kPiece) crc = crc_combine_op(piece_op, crc, crcs[(size_t)i]);
+                else {
+                    uint32_t op[32];
+                    crc_shift_op(op, len2);
+                    crc = crc_combine_op(op, crc, crcs[(size_t)i]);
+                }
+            }
+        }
+        if (crc != want_crc) return set_err(ctx, HDRF_E_INVAL, "gzip CRC-32 mismatch");
+        out += n;
+        at = end + 8;
+    }
+    return out;
+}
+
 // Read side for files: the Lz4Codec input stream DataConstructor opens for closed containers under
 // compressor 2 (DN/DataConstructor.java:495-500) and for stream-mode blocks (:171-176).
 extern "C" int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap)
@@ -1284,8 +1391,9 @@ extern "C" int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const u
 {
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
+    if (codec == 5) return decode_gzip(ctx, file, flen, dev_out, cap);
     if (codec != 0 && codec != 4)
-        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec) and 4 (Lz4Codec) are implemented");
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec)");
     return decode_file(ctx, file, flen, dev_out, cap, codec);
 }
 

@@ -52,6 +52,10 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
                       hipStream_t st, Marker *mk);
 hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals, int n, IndexEntry *tab, int log2cap,
                              unsigned long long tag_mask, int *err, hipStream_t st);
+// GzipCodec read side (inflate.hip): one raw deflate stream -> dst; res[0] = length or < 0, res[1] =
+// bytes consumed.  CRC-32 of fixed-size pieces of a buffer.
+hipError_t launch_inflate(const uint8_t *src, int64_t slen, uint8_t *dst, int64_t cap, int64_t *res, hipStream_t st);
+hipError_t launch_crc32_pieces(const uint8_t *data, int64_t n, int64_t piece, uint32_t *crc, hipStream_t st);
 hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *digests,
                               const uint32_t *slot, int log2cap, unsigned long long tag_mask,
                               unsigned long long *stats, hipStream_t st);

@@ -375,7 +375,7 @@ class Context:
             self.dev_free(dev)
 
     def stream_file_decode(self, codec, file, raw_cap):
-        """Decode a stream-mode block file (codec 0 SnappyCodec, 4 Lz4Codec) on the GPU -> raw bytes."""
+        """Decode a stream-mode block file (codec 0 SnappyCodec, 4 Lz4Codec, 5 GzipCodec) on the GPU -> raw bytes."""
         f = _u8(file)
         dev = self.dev_alloc(raw_cap + 64)
         try:

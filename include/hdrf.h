@@ -147,8 +147,9 @@ int64_t hdrf_stream_block_host(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, 
  * file (lz4 = 1 for a closed container's Lz4Codec file, 0 for raw bytes) after its arena slot was
  * reused or the DataNode restarted; hdrf_container_unload frees that copy. */
 int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap);
-/* The same for a stream-mode block file of codec 0 (SnappyCodec) or 4 (Lz4Codec): the
- * compression-only decoders of DataConstructor (DN/DataConstructor.java:102-220). */
+/* The same for a stream-mode block file of codec 0 (SnappyCodec), 4 (Lz4Codec) or 5 (GzipCodec:
+ * gzip members, inflated on the GPU, CRC-32 and ISIZE checked): the compression-only decoders of
+ * DataConstructor (DN/DataConstructor.java:102-220).  HDRF_E_INVAL on a malformed file. */
 int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const uint8_t *file, int64_t flen, uint8_t *dev_out,
                                 int64_t cap);
 /* Stage 1 of the GPU compressor 5 (GzipCodec = zlib level 6 deflate_slow, DN/BlockReceiver.java:

@@ -105,7 +105,7 @@ public final class HipReductionScheme extends ReductionScheme {
   }
 
   /**
-   * Stream-mode schemes (DataNode.compressor 0 SnappyCodec, 4 Lz4Codec; BlockReceiver.java:
+   * Stream-mode schemes (DataNode.compressor 0 SnappyCodec, 4 Lz4Codec, 5 GzipCodec; BlockReceiver.java:
    * 826-873,887-894,1238-1256): the file the reference writes to chunkDir + blockId when the block
    * arrives as write()s of the given packet sizes followed by close().  The caller stores it and
    * the library records SET blockId -> BE32(length).
@@ -113,6 +113,15 @@ public final class HipReductionScheme extends ReductionScheme {
   public byte[] streamBlock(int codec, ByteBuffer block, long blockId, long[] packetSizes) throws IOException {
     if (!block.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
     return stream0(ctx, codec, block, block.position(), blockId, packetSizes);
+  }
+
+  /**
+   * Stream-mode read (DataConstructor.java:102-220): the chunkDir + blockId file written by
+   * streamBlock, decoded on the GPU through the codec (0 Snappy, 4 Lz4, 5 Gzip with CRC-32/ISIZE
+   * checks); IOException on a malformed file or one whose length differs from the recorded one.
+   */
+  public byte[] streamDecode(int codec, byte[] file, long blockId) throws IOException {
+    return streamDecode0(ctx, codec, file, blockId);
   }
 
   @Override
@@ -155,4 +164,5 @@ public final class HipReductionScheme extends ReductionScheme {
   private static native int rxBegin0(long ctx, long blockId) throws IOException;
   private static native void packet0(long ctx, int rx, ByteBuffer pkt, int off, int len) throws IOException;
   private static native void submitSlot0(long ctx, int rx) throws IOException;
+  private static native byte[] streamDecode0(long ctx, int codec, byte[] file, long blockId) throws IOException;
 }

@@ -273,3 +273,34 @@ JNIEXPORT void JNICALL JFN(close0)(JNIEnv *env, jclass cls, jlong h)
     (void)env; (void)cls;
     hdrf_close((hdrf_ctx *)(intptr_t)h);
 }
+
+/* stream-mode read (DataConstructor's codec input stream over chunkDir + blkID,
+ * DN/DataConstructor.java:102-220): the block file decoded on the GPU (codec 0 SnappyCodec,
+ * 4 Lz4Codec, 5 GzipCodec); the raw length is the one streamBlock recorded for blockId. */
+JNIEXPORT jbyteArray JNICALL JFN(streamDecode0)(JNIEnv *env, jclass cls, jlong h, jint codec, jbyteArray file,
+                                                jlong id)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int64_t len = hdrf_block_length(ctx, (uint64_t)id);
+    if (len < 0) { throw_io(env, ctx, (int)len); return NULL; }
+    const jsize flen = (*env)->GetArrayLength(env, file);
+    void *dev = NULL;
+    uint8_t *tmp = (uint8_t *)malloc((size_t)(len ? len : 1));
+    int rc = tmp ? hdrf_dev_alloc(ctx, (uint64_t)(len ? len : 1), &dev) : HDRF_E_NOMEM;
+    int64_t n = rc;
+    if (!rc) {
+        jbyte *f = (*env)->GetByteArrayElements(env, file, NULL);
+        n = f ? hdrf_stream_file_decode(ctx, codec, (const uint8_t *)f, flen, (uint8_t *)dev, len) : HDRF_E_INVAL;
+        if (f) (*env)->ReleaseByteArrayElements(env, file, f, JNI_ABORT);
+        if (n >= 0 && n != len) n = HDRF_E_INVAL;          /* the file must hold the recorded length */
+        if (n > 0 && (rc = hdrf_memcpy_d2h(ctx, tmp, dev, (uint64_t)n)) != 0) n = rc;
+        hdrf_dev_free(ctx, dev);
+    }
+    jbyteArray r = NULL;
+    if (n < 0) throw_io(env, ctx, (int)n);
+    else if ((r = (*env)->NewByteArray(env, (jsize)n)) != NULL)
+        (*env)->SetByteArrayRegion(env, r, 0, (jsize)n, (const jbyte *)tmp);
+    free(tmp);
+    return r;
+}

@@ -34,4 +34,6 @@ struct JNINativeInterface_ {
     const char *(*GetStringUTFChars)(JNIEnv *env, jstring string, jboolean *isCopy);
     void (*ReleaseStringUTFChars)(JNIEnv *env, jstring string, const char *utf);
     jobject (*NewDirectByteBuffer)(JNIEnv *env, void *address, jlong capacity);
+    jbyte *(*GetByteArrayElements)(JNIEnv *env, jbyteArray array, jboolean *isCopy);
+    void (*ReleaseByteArrayElements)(JNIEnv *env, jbyteArray array, jbyte *elems, jint mode);
 };

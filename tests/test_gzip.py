@@ -208,3 +208,63 @@ def test_gpu_stream_gzip_file_matches_oracle(kind, n):
     want = gzip_stream(a)
     assert f == want
     assert zlib.decompress(f, 31) == a.tobytes()
+    # read side (DN/DataConstructor.java:194-218): the GPU inflates its own file back
+    ctx = Context(max_block_bytes=16 << 20, max_batch_blocks=8, index_log2=20, arena_slots=64)
+    assert ctx.stream_file_decode(5, np.frombuffer(f, np.uint8), max(n, 1)) == a.tobytes()
+    ctx.close()
+
+
+def _gpu_inflate(f, cap):
+    from hdrf_amd.lib import Context
+    ctx = Context(max_block_bytes=16 << 20, max_batch_blocks=8, index_log2=20, arena_slots=64)
+    try:
+        return ctx.stream_file_decode(5, np.frombuffer(f, np.uint8), cap)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("level,kind,n", [(0, "text", 200_000), (1, "text", 300_000), (9, "lowent", 250_000),
+                                          (6, "random", 140_000), (6, "periodic", 100_000), (1, "zeros", 1_000_000),
+                                          (6, "binary", 70_000), (6, "text", 5), (6, "text", 0), (2, "sparse", 300_000)])
+def test_gpu_inflate_matches_zlib(level, kind, n):
+    """GzipCodec read side on the GPU (hdrf_stream_file_decode codec 5) on files written by this
+    image's zlib at several levels: stored blocks (level 0), fixed and dynamic Huffman blocks,
+    long runs (level 1 zeros: distance-1 overlapping copies), window-edge distances."""
+    a = (make_block(kind, 31, n) if n else np.zeros(0, np.uint8)).tobytes()
+    c = zlib.compressobj(level, zlib.DEFLATED, 31, 9 if level == 9 else 8, zlib.Z_DEFAULT_STRATEGY)
+    f = c.compress(a) + c.flush()
+    assert _gpu_inflate(f, max(n, 1)) == a
+
+
+@pytest.mark.gpu
+def test_gpu_inflate_members_header_flags_and_errors():
+    """Concatenated members (each with its own trailer), an FNAME/FCOMMENT/FEXTRA/FHCRC header,
+    and rejection of a flipped CRC byte, a truncated stream and a too-small output buffer."""
+    import gzip
+    import io
+    from hdrf_amd.lib import HdrfError
+    a = make_block("text", 41, 120_000).tobytes()
+    b = make_block("binary", 42, 90_000).tobytes()
+    buf = io.BytesIO()
+    with gzip.GzipFile(filename="block_1073741825", mode="wb", fileobj=buf, mtime=7) as g:   # FNAME
+        g.write(a)
+    m1 = buf.getvalue()
+    m2 = zlib_gzip(b)
+    # a hand-made member with FEXTRA + FCOMMENT + FHCRC around zlib's raw deflate of b
+    co = zlib.compressobj(6, zlib.DEFLATED, -15)
+    raw = co.compress(b) + co.flush()
+    hdr = bytes([0x1f, 0x8b, 8, 4 | 16 | 2, 0, 0, 0, 0, 0, 3]) + (5).to_bytes(2, "little") + b"xtra!" + b"note\0"
+    hdr += (zlib.crc32(hdr) & 0xffff).to_bytes(2, "little")
+    m3 = hdr + raw + zlib.crc32(b).to_bytes(4, "little") + len(b).to_bytes(4, "little")
+    f = m1 + m2 + m3
+    assert _gpu_inflate(f, len(a) + 2 * len(b)) == a + b + b
+    bad = bytearray(m2)
+    bad[-6] ^= 0xff                                            # CRC-32 byte
+    with pytest.raises(HdrfError):
+        _gpu_inflate(bytes(bad), len(b))
+    with pytest.raises(HdrfError):
+        _gpu_inflate(m2[: len(m2) // 2], len(b))               # truncated
+    with pytest.raises(HdrfError) as ei:
+        _gpu_inflate(m2, len(b) - 1)                           # output capacity
+    assert ei.value.code == -4
