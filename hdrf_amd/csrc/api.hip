@@ -155,6 +155,7 @@ struct hdrf_ctx {
     uint32_t *d_oslot = nullptr;
     uint8_t *d_oflags = nullptr;
     const uint32_t *gx_x2 = nullptr;             // responses of the back batch (caller's buffer)
+    AllocState gx_ain{}, gx_aout{};              // allocator before / after this rank's flush walk
     uint64_t gx_nfront = 0, gx_nfwait = 0, gx_nback = 0;   // fronts launched / waited, batches committed
     int gx_bphase = 0;                           // back batch: 0 owner next, 1 decide, 2 flush, 3 place, 4 commit
     hdrf_stats stats{};                          // cumulative since the last reset
@@ -1054,6 +1055,7 @@ static int64_t stream_max_input(int codec)
 // Stream-mode compressor 5 (GzipCodec, zlib level 6; DN/BlockReceiver.java:858-873,887-894): the
 // file does not depend on the packet writes.  Stage 1 match pass, stage 2 lazy
 // parse, stage 3 per-deflate-block trees + bits, stage 4 offsets / placement / CRC-32 trailer.
+static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need);
 static int64_t stream_gzip(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *dev_data, uint64_t len, uint8_t *out,
                            int64_t cap)
 {
@@ -1067,10 +1069,11 @@ static int64_t stream_gzip(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *dev_
                          (size_t)(slot * maxblk), (size_t)(24 * maxblk + 64), (size_t)(8 * maxblk + 72),
                          (size_t)(4 * ((n >> 16) + 2)), (size_t)(bound + 64), gzip_parse_scratch(n)};
     constexpr int kBufs = 14;
-    uint8_t *B[kBufs] = {};
-    auto release = [&] { for (auto p : B) if (p) (void)hipFree(p); };
-    for (int i = 0; i < kBufs; i++)
-        if (hipMalloc((void **)&B[i], sz[i]) != hipSuccess) { release(); return set_err(ctx, HDRF_E_HIP, "gzip scratch"); }
+    uint64_t at[kBufs + 1] = {0};                      // one grown scratch (ctx->d_rd), 256-B aligned parts
+    for (int i = 0; i < kBufs; i++) at[i + 1] = at[i] + ((sz[i] + 255) & ~(size_t)255);
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, at[kBufs])) return rc;
+    uint8_t *B[kBufs];
+    for (int i = 0; i < kBufs; i++) B[i] = ctx->d_rd + at[i];
     std::vector<uint8_t> tab(gzip_tab_bytes());
     gzip_host_tab(tab.data());
     int64_t cnt[2] = {0, 0}, flen = 0;
@@ -1082,17 +1085,16 @@ static int64_t stream_gzip(hdrf_ctx *ctx, uint64_t block_id, const uint8_t *dev_
                               (int64_t *)B[4], (int64_t *)B[5], B[13], st);
     if (e == hipSuccess) e = hipMemcpyAsync(cnt, B[5], 16, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e == hipSuccess && (cnt[1] < 1 || cnt[1] > maxblk)) { release(); return set_err(ctx, HDRF_E_DEVICE, "gzip parse block count"); }
+    if (e == hipSuccess && (cnt[1] < 1 || cnt[1] > maxblk)) { return set_err(ctx, HDRF_E_DEVICE, "gzip parse block count"); }
     if (e == hipSuccess)
         e = launch_gzip_encode(dev_data, n, B[6], (const uint32_t *)B[3], (const int64_t *)B[4], (int)cnt[1], B[7], B[8],
                                slot, (int64_t *)B[9], (int64_t *)B[10], (uint32_t *)B[11], B[12], (int64_t *)B[5], st);
     if (e == hipSuccess) e = hipMemcpyAsync(&flen, B[5], 8, hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) { release(); return set_err(ctx, HDRF_E_HIP, std::string("gzip stream: ") + hipGetErrorString(e)); }
-    if (flen > bound) { release(); return set_err(ctx, HDRF_E_DEVICE, "gzip stream exceeded its bound"); }
-    if (!out || cap < flen) { release(); return set_err(ctx, HDRF_E_CAPACITY, "stream file needs " + std::to_string(flen) + " bytes"); }
+    if (e != hipSuccess) { return set_err(ctx, HDRF_E_HIP, std::string("gzip stream: ") + hipGetErrorString(e)); }
+    if (flen > bound) { return set_err(ctx, HDRF_E_DEVICE, "gzip stream exceeded its bound"); }
+    if (!out || cap < flen) { return set_err(ctx, HDRF_E_CAPACITY, "stream file needs " + std::to_string(flen) + " bytes"); }
     e = hipMemcpy(out, B[12], (size_t)flen, hipMemcpyDeviceToHost);
-    release();
     if (e != hipSuccess) return set_err(ctx, HDRF_E_HIP, "gzip D2H");
     ctx->lengths[(uint32_t)block_id] = (int64_t)len;   // SET id -> BE32(len) (:1238-1256)
     return flen;
@@ -1421,11 +1423,10 @@ extern "C" int hdrf_gzip_parse(hdrf_ctx *ctx, const uint8_t *dev_data, uint64_t 
         return set_err(ctx, HDRF_E_INVAL, "null buffer");
     if (len >= (1ull << 31)) return set_err(ctx, HDRF_E_INVAL, "gzip parse: len must be < 2^31");
     if (int rc = drain(ctx)) return rc;
-    void *scr = nullptr;
-    HIPCK(hipMalloc(&scr, gzip_parse_scratch((int64_t)len)));
-    hipError_t e = launch_gzip_parse(dev_data, (int64_t)len, dev_m128, dev_m32, dev_syms, dev_blks, dev_cnt, scr, ctx->st);
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, gzip_parse_scratch((int64_t)len))) return rc;
+    hipError_t e = launch_gzip_parse(dev_data, (int64_t)len, dev_m128, dev_m32, dev_syms, dev_blks, dev_cnt, ctx->d_rd,
+                                     ctx->st);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->st);
-    (void)hipFree(scr);
     if (e != hipSuccess) return set_err(ctx, HDRF_E_HIP, std::string("gzip parse: ") + hipGetErrorString(e));
     return 0;
 }
@@ -1674,7 +1675,12 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
     if (int rc = gx_check(ctx, 2)) return rc;
     Slot &S = ctx->sl[ctx->gx_nback % 2];
     hipStream_t st = ctx->stB;
-    if (alloc_in) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_in, sizeof(AllocState), hipMemcpyHostToDevice, st));
+    if (alloc_in) {
+        std::memcpy(&ctx->gx_ain, alloc_in, sizeof(AllocState));
+        HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_in, sizeof(AllocState), hipMemcpyHostToDevice, st));
+    } else {
+        HIPCK(hipMemcpyAsync(&ctx->gx_ain, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
+    }
     HIPCK(hipMemsetAsync(S.d_nclosed, 0, sizeof(uint32_t), st));
     const StoreParams P = store_params(ctx, S.nblocks);
     HIPCK(launch_store_flush(P, S.d_bst, S.d_store, S.d_pre, ctx->d_alloc, S.d_rstate, S.d_ev,
@@ -1682,6 +1688,7 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
     AllocState a{};
     HIPCK(hipMemcpyAsync(&a, ctx->d_alloc, sizeof a, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    ctx->gx_aout = a;
     if (alloc_out) {
         std::memset(alloc_out, 0, HDRF_ALLOC_STATE_BYTES);
         std::memcpy(alloc_out, &a, sizeof a);
@@ -1715,6 +1722,11 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    // the open containers this rank's flush walk started and ended in hold its placed chunks even
+    // when another rank closes them (the node read, hdrf_gx_read_fill, gathers from them)
+    for (const AllocState *a : {&ctx->gx_ain, &ctx->gx_aout})
+        for (int t = 0; t < ctx->cfg.n_thread; t++)
+            if (a->exists[t] && !ctx->containers.count(a->id[t])) note_container(ctx, a->id[t], a->slot[t], a->cur[t], 0);
     if (int rc = complete_slot(ctx, si, false)) return rc;
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
     ctx->gx_bphase = 4;
@@ -2221,7 +2233,8 @@ extern "C" int64_t hdrf_reconstruct(hdrf_ctx *ctx, const uint8_t *recipe, int64_
 {
     HDRF_LOCK(ctx);
     if (!ctx || !recipe || recipe_len < 4) return HDRF_E_INVAL;
-    if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "reconstruction on node-global contexts: not yet");
+    if (ctx->G > 1)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "node-global contexts read through hdrf_gx_read_locate / _fill (every rank)");
     if (int rc = drain(ctx)) return rc;
     const int64_t size = ((int64_t)recipe[0] << 24) | (recipe[1] << 16) | (recipe[2] << 8) | recipe[3];
     const int64_t n = recipe_len / ctx->H;             // t1data.length / hash_length (:223)
@@ -2281,6 +2294,82 @@ extern "C" int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint
     if (got < 0) return got;
     if (got) HIPCK(hipMemcpy(out, ctx->d_stage, got, hipMemcpyDeviceToHost));
     return got;
+}
+
+// ---- node-global read (G > 1): DataConstructor over the node's one index ------------------
+// Every rank takes part (include/hdrf.h): the owners locate the digests they own, the locations
+// are combined (sum of disjoint rows), and every rank gathers the chunks it placed; the partial
+// blocks are disjoint, so their byte sum on the reading rank is the block (hdrf_amd/node.py).
+extern "C" int64_t hdrf_gx_read_locate(hdrf_ctx *ctx, const uint8_t *digests, int64_t n, uint32_t *loc)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_read_* needs cfg.n_ranks > 1");
+    if (n < 0 || (n && (!digests || !loc))) return set_err(ctx, HDRF_E_INVAL, "bad locate arguments");
+    if (n == 0) return 0;
+    if (ctx->gx_nfront != ctx->gx_nback) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_read_locate: a batch is in flight");
+    const uint64_t o_loc = (((uint64_t)n * ctx->H) + 255) & ~255ull, o_err = o_loc + (((uint64_t)n * 16 + 255) & ~255ull);
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_err + 256)) return rc;
+    uint8_t *R = ctx->d_rd;
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(R, digests, (size_t)n * ctx->H, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(R + o_err, 0, 4, st));
+    HIPCK(launch_gx_locate(ctx->cfg.hasher, (const uint32_t *)R, (int)n, ctx->d_tab, ctx->cfg.index_log2, tag_mask(ctx),
+                           ctx->G, ctx->cfg.rank, (uint32_t *)(R + o_loc), (int *)(R + o_err), st));
+    int herr = 0;
+    HIPCK(hipMemcpyAsync(loc, R + o_loc, (size_t)n * 16, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&herr, R + o_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (herr) return set_err(ctx, HDRF_E_NOTFOUND, "a recipe digest owned by this rank is not in its index partition");
+    int64_t mine = 0;
+    for (int64_t k = 0; k < n; k++) mine += loc[4 * k + 3] != 0;
+    return mine;
+}
+
+extern "C" int64_t hdrf_gx_read_fill(hdrf_ctx *ctx, const uint32_t *loc, int64_t n, uint8_t *dev_out, int64_t cap)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_read_* needs cfg.n_ranks > 1");
+    if (n < 0 || (n && !loc)) return set_err(ctx, HDRF_E_INVAL, "bad fill arguments");
+    if (ctx->gx_nfront != ctx->gx_nback) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_read_fill: a batch is in flight");
+    struct RdChunkH { uint32_t slot, start, len, off; };
+    static_assert(sizeof(RdChunkH) == 16, "RdChunk layout");
+    if (rd_chunk_bytes() != sizeof(RdChunkH)) return set_err(ctx, HDRF_E_DEVICE, "RdChunk layout");
+    std::vector<RdChunkH> mine;
+    std::vector<uint64_t> bases;
+    std::map<uint32_t, uint32_t> base_of;               // container id -> index in bases
+    uint64_t off = 0, filled = 0;
+    for (int64_t k = 0; k < n; k++) {
+        const uint32_t *r = loc + 4 * k;
+        if (r[3] == 0 || r[2] < r[1]) return set_err(ctx, HDRF_E_INVAL, "location without its placing rank");
+        const uint32_t len = r[2] - r[1];
+        if ((int)r[3] - 1 == ctx->cfg.rank && len) {
+            auto it = ctx->containers.find(r[0]);
+            if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_NOTFOUND, "container of a placed chunk is not resident");
+            auto b = base_of.find(r[0]);
+            if (b == base_of.end()) {
+                b = base_of.emplace(r[0], (uint32_t)bases.size()).first;
+                bases.push_back((uint64_t)(uintptr_t)(ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max));
+            }
+            if ((uint64_t)r[2] > ctx->cfg.container_max) return set_err(ctx, HDRF_E_DEVICE, "chunk beyond its container");
+            mine.push_back(RdChunkH{b->second, r[1], len, (uint32_t)off});
+            filled += len;
+        }
+        off += len;
+    }
+    if ((int64_t)off > cap || (off && !dev_out)) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
+    if (!mine.empty()) {
+        const uint64_t o_b = ((mine.size() * sizeof(RdChunkH)) + 255) & ~255ull;
+        if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_b + bases.size() * 8 + 256)) return rc;
+        uint8_t *R = ctx->d_rd;
+        hipStream_t st = ctx->st;
+        HIPCK(hipMemcpyAsync(R, mine.data(), mine.size() * sizeof(RdChunkH), hipMemcpyHostToDevice, st));
+        HIPCK(hipMemcpyAsync(R + o_b, bases.data(), bases.size() * 8, hipMemcpyHostToDevice, st));
+        HIPCK(launch_rd_gather(R, (int)mine.size(), (const uint64_t *)(R + o_b), dev_out, st));
+        HIPCK(hipStreamSynchronize(st));
+    }
+    return (int64_t)filled;
 }
 
 // ---- memory helpers, corpus, timing ------------------------------------------------------

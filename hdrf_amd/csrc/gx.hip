@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(256) own_commit_kernel(const uint32_t *__restr
     if (i >= counts[s]) return;
     const uint32_t *rec = x3 + ((size_t)s * cap + i) * 4;
     IndexEntry *e = tab + rec[0];
-    e->cid = rec[1];
+    e->cid = rec[1] | ((uint32_t)(s + 1) << 24);          // ids are < 2^24: bits 24-31 = placing rank + 1
     e->start = rec[2];
     e->stop = rec[3];
 }

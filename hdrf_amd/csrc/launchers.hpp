@@ -159,6 +159,9 @@ hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int clos
                       hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join);
 // read side (read.hip): lookup + scan (gather = false), then the copy (gather = true)
 size_t rd_chunk_bytes();
+hipError_t launch_gx_locate(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
+                            unsigned long long tag_mask, int G, int rank, uint32_t *loc, int *err, hipStream_t st);
+hipError_t launch_rd_gather(const void *chunks, int n, const uint64_t *bases, uint8_t *out, hipStream_t st);
 hipError_t launch_reconstruct(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
                               unsigned long long tag_mask, const uint32_t *cids, const uint64_t *bases, int ncont,
                               void *chunks, uint64_t *total, uint8_t *out, int *err, hipStream_t st, bool gather);

@@ -12,6 +12,8 @@
 //               slot, or a container loaded back from its file with hdrf_container_load)
 //   rd_scan   — one workgroup: exclusive prefix of the chunk lengths (block offsets) + total
 //   rd_gather — one wave per chunk: 16-B-per-lane copy arena -> output block
+//   gx_locate — node-global contexts: the owner's lookup of the digests it owns (location +
+//               placing rank); each rank then gathers the chunks it placed (hdrf_gx_read_*)
 #include "launchers.hpp"
 
 namespace hdrf {
@@ -21,6 +23,29 @@ struct RdChunk {
     uint32_t start, len;
     uint32_t off;        // offset in the rebuilt block
 };
+
+// probe the index for one digest (the open addressing of index.hip); nullptr when absent
+template <int HW>
+__device__ const IndexEntry *rd_probe(const uint32_t *dw, const IndexEntry *__restrict__ tab, int log2cap,
+                                      unsigned long long tag_mask)
+{
+    unsigned long long tag = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
+    const uint32_t z = tag == 0 ? 0x80000000u : 0u;
+    if (tag == 0) tag = 1;
+    const uint64_t mask = (1ull << log2cap) - 1;
+    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
+    for (uint64_t probe = 0; probe <= mask; probe++) {
+        const IndexEntry &e = tab[h];
+        if (e.tag == kEmptyTag) return nullptr;
+        bool match = e.tag == tag && (e.batch & 0x80000000u) == z;
+#pragma unroll
+        for (int i = 2; i < HW; i++) match = match && e.dig[i - 2] == dw[i];
+        if (HW == 5) match = match && e.dig[3] == dw[0] && e.dig[4] == dw[1];
+        if (match) return &e;
+        h = (h + 1) & mask;
+    }
+    return nullptr;
+}
 
 template <int HW>
 __global__ void __launch_bounds__(256) rd_lookup_kernel(const uint32_t *__restrict__ dig, int n,
@@ -33,37 +58,45 @@ __global__ void __launch_bounds__(256) rd_lookup_kernel(const uint32_t *__restri
     uint32_t dw[HW];
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = dig[(size_t)k * HW + i];
-    unsigned long long tag = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
-    const uint32_t z = tag == 0 ? 0x80000000u : 0u;
-    if (tag == 0) tag = 1;
-    const uint64_t mask = (1ull << log2cap) - 1;
-    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
     RdChunk r;
     r.slot = 0xffffffffu; r.start = 0; r.len = 0; r.off = 0;
-    bool found = false;
-    for (uint64_t probe = 0; probe <= mask; probe++) {
-        const IndexEntry &e = tab[h];
-        if (e.tag == kEmptyTag) break;
-        bool match = e.tag == tag && (e.batch & 0x80000000u) == z;
-#pragma unroll
-        for (int i = 2; i < HW; i++) match = match && e.dig[i - 2] == dw[i];
-        if (HW == 5) match = match && e.dig[3] == dw[0] && e.dig[4] == dw[1];
-        if (match) {
-            found = true;
-            r.start = e.start;
-            r.len = e.stop - e.start;                  // chunkMeta.length = blockStop - blockStart
-            int lo = 0, hi = ncont;                   // readable container list, sorted by id
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (cids[mid] < e.cid) lo = mid + 1; else hi = mid;
-            }
-            if (lo < ncont && cids[lo] == e.cid) r.slot = (uint32_t)lo;
-            break;
+    const IndexEntry *e = rd_probe<HW>(dw, tab, log2cap, tag_mask);
+    if (e) {
+        r.start = e->start;
+        r.len = e->stop - e->start;                    // chunkMeta.length = blockStop - blockStart
+        int lo = 0, hi = ncont;                        // readable container list, sorted by id
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (cids[mid] < e->cid) lo = mid + 1; else hi = mid;
         }
-        h = (h + 1) & mask;
+        if (lo < ncont && cids[lo] == e->cid) r.slot = (uint32_t)lo;
     }
-    if (!found || (r.slot == 0xffffffffu && r.len != 0)) atomicOr(err, 1);   // empty chunks need no container
+    if (!e || (r.slot == 0xffffffffu && r.len != 0)) atomicOr(err, 1);   // empty chunks need no container
     out[k] = r;
+}
+
+// Node-global read (G > 1): the owner's lookup of the recipe digests it owns (first digest word
+// mod G == rank).  loc[k] = {container id, start, stop, placing rank + 1} for an owned digest,
+// zeros for the others; an owned digest that is absent sets *err.  The placing rank is the X3
+// source own_commit_kernel recorded in bits 24-31 of the entry's container id.
+template <int HW>
+__global__ void __launch_bounds__(256) gx_locate_kernel(const uint32_t *__restrict__ dig, int n,
+                                                        const IndexEntry *__restrict__ tab, int log2cap,
+                                                        unsigned long long tag_mask, int G, int rank,
+                                                        uint32_t *__restrict__ loc, int *__restrict__ err)
+{
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    uint32_t dw[HW];
+#pragma unroll
+    for (int i = 0; i < HW; i++) dw[i] = dig[(size_t)k * HW + i];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if ((int)(dw[0] % (uint32_t)G) == rank) {
+        const IndexEntry *e = rd_probe<HW>(dw, tab, log2cap, tag_mask);
+        if (e) v = make_uint4(e->cid & 0xffffffu, e->start, e->stop, e->cid >> 24);
+        if (!e || v.w == 0u) atomicOr(err, 1);        // missing, or a location without its placer
+    }
+    *(uint4 *)(loc + 4 * (size_t)k) = v;
 }
 
 // one workgroup of 1024 threads: off[k] = sum of len[0..k), total -> *total
@@ -141,5 +174,25 @@ hipError_t launch_reconstruct(int hasher, const uint32_t *dig, int n, const Inde
 }
 
 size_t rd_chunk_bytes() { return sizeof(RdChunk); }
+
+hipError_t launch_gx_locate(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
+                            unsigned long long tag_mask, int G, int rank, uint32_t *loc, int *err, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    const dim3 g((n + 255) / 256);
+    if (hasher == 0)
+        hipLaunchKernelGGL(gx_locate_kernel<5>, g, dim3(256), 0, st, dig, n, tab, log2cap, tag_mask, G, rank, loc, err);
+    else
+        hipLaunchKernelGGL(gx_locate_kernel<7>, g, dim3(256), 0, st, dig, n, tab, log2cap, tag_mask, G, rank, loc, err);
+    return hipGetLastError();
+}
+
+// gather a host-built chunk list (RdChunk {base index, start, len, off}) into out
+hipError_t launch_rd_gather(const void *chunks, int n, const uint64_t *bases, uint8_t *out, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rd_gather_kernel, dim3((n + 3) / 4), dim3(256), 0, st, (const RdChunk *)chunks, n, bases, out);
+    return hipGetLastError();
+}
 
 }  // namespace hdrf

@@ -33,6 +33,7 @@ EXPORTS = [
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
     "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
     "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot",
+    "hdrf_gx_read_locate", "hdrf_gx_read_fill",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -153,6 +154,8 @@ def load():
         "hdrf_batch_nblocks": (ctypes.c_int, [_vp]),
         "hdrf_reconstruct": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_reconstruct_block": (ctypes.c_int64, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
+        "hdrf_gx_read_locate": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp]),
+        "hdrf_gx_read_fill": (ctypes.c_int64, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_batch_info": (ctypes.c_int, [_vp, ctypes.c_int32, _i64p, _i64p]),
         "hdrf_batch_offsets": (ctypes.c_int, [_vp, ctypes.c_int32, _u32p, ctypes.c_int64]),
         "hdrf_batch_digests": (ctypes.c_int, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64]),
@@ -626,6 +629,21 @@ class Context:
         af = None if alloc_final is None else _p(np.ascontiguousarray(alloc_final, np.uint8))
         self._ck(self.L.hdrf_gx_place(self._h, af, x3_send, _p(cnt, _i64p)))
         return cnt
+
+    def gx_read_locate(self, digests):
+        """Node-global read, step 1: locations {cid, start, stop, placing rank + 1} of the recipe
+        digests this rank owns (uint32 [n, 4], zero rows for the others) and how many it owns."""
+        d = np.frombuffer(bytes(digests), np.uint8).copy()
+        n = d.size // self.H
+        loc = np.zeros((max(n, 1), 4), np.uint32)
+        m = self._ck(self.L.hdrf_gx_read_locate(self._h, _p(d) if d.size else None, n, loc.ctypes.data))
+        return loc[:n], m
+
+    def gx_read_fill(self, loc, dev_out, cap):
+        """Node-global read, step 3: write the chunks this rank placed at their block offsets."""
+        loc = np.ascontiguousarray(loc, np.uint32)
+        return self._ck(self.L.hdrf_gx_read_fill(self._h, loc.ctypes.data if loc.size else None, loc.shape[0],
+                                                 dev_out, cap))
 
     def gx_commit(self, x3_recv, recv_counts):
         rc = np.ascontiguousarray(recv_counts, np.int64)

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .lib import ALLOC_STATE_BYTES
+from .lib import ALLOC_STATE_BYTES, HdrfError
 
 
 class Exchange:
@@ -148,6 +148,52 @@ class NodeRank:
                 done(k)
             if k + 1 < len(batches):
                 c1 = ctx.gx_front_wait()
+
+    def reconstruct_block(self, block_id, reader):
+        """DataConstructor(blkID, recipe).data on the node (DN/DataConstructor.java:73-250,360-417):
+        a collective of every rank; the reading rank (the one that reduced the block and keeps
+        its recipe) gets the block as a numpy uint8 array, the others None.  The owners locate
+        the digests (hdrf_gx_read_locate), the disjoint locations are summed, each rank gathers
+        the chunks it placed (hdrf_gx_read_fill) and the disjoint partial blocks are summed on
+        the reader."""
+        ctx, dev = self.ctx, (self.device if self.xc.nccl else None)
+        rec = np.frombuffer(ctx.recipe(block_id), np.uint8) if self.rank == reader else np.zeros(0, np.uint8)
+        n = torch.tensor([rec.size], dtype=torch.int64, device=dev)
+        dist.broadcast(n, src=reader)
+        t = torch.zeros(int(n.item()), dtype=torch.uint8, device=dev)
+        if self.rank == reader:
+            t.copy_(torch.from_numpy(rec.copy()))
+        dist.broadcast(t, src=reader)
+        rec = t.cpu().numpy()
+        size = int.from_bytes(rec[:4].tobytes(), "big")
+        nd = (rec.size - 4) // ctx.H
+        err = 0
+        try:
+            loc, _ = ctx.gx_read_locate(rec[4:].tobytes())
+        except HdrfError:
+            loc, err = np.zeros((nd, 4), np.uint32), 1
+        # the disjoint rows summed, plus an error row: every rank fails together, none blocks
+        lt = torch.as_tensor(np.vstack([loc.astype(np.int64), [[err, 0, 0, 0]]]), device=dev)
+        dist.all_reduce(lt)
+        lt = lt.cpu().numpy()
+        if lt[-1, 0]:
+            raise HdrfError(-5, f"node read of block {block_id}: a digest is missing from its owner's partition")
+        loc = lt[:-1].astype(np.uint32)
+        self.last_loc = loc
+        part = torch.zeros(max(size, 1), dtype=torch.uint8, device=self.device)
+        torch.cuda.synchronize(self.device)            # the zero fill (torch's stream) lands before the gather
+        try:
+            filled, err = ctx.gx_read_fill(loc, part.data_ptr(), size), 0
+        except HdrfError:
+            filled, err = 0, 1
+        torch.cuda.synchronize(self.device)
+        tot = torch.tensor([filled, err], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        if int(tot[1].item()) or int(tot[0].item()) != size:
+            raise HdrfError(-5, f"node read of block {block_id}: {int(tot[0].item())} of {size} bytes readable")
+        buf = part if self.xc.nccl else part.cpu()
+        dist.reduce(buf, dst=reader)
+        return buf[:size].cpu().numpy() if self.rank == reader else None
 
     def batch_base(self, nblocks):
         """Rank-major batch positions: gbase of this rank given every rank's block count."""

@@ -253,6 +253,24 @@ int hdrf_reduce_block_ticketed(hdrf_ctx *ctx, uint64_t ticket, uint64_t block_id
 int64_t hdrf_reconstruct(hdrf_ctx *ctx, const uint8_t *recipe, int64_t recipe_len, uint8_t *dev_out, int64_t cap);
 int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, int64_t cap);
 
+/* The same read on a node-global context (cfg.n_ranks = G > 1): the node's ONE index is
+ * partitioned over the ranks, and a container's bytes are spread over the ranks that placed
+ * chunks into it, so every rank takes part (hdrf_amd/node.py NodeRank.reconstruct_block; the
+ * shared Redis of DN/DataConstructor.java:360-417 serves any DataNode):
+ *   1. every rank gets the block's n recipe digests (n * digest_len bytes, host);
+ *      hdrf_gx_read_locate fills loc[4k..4k+3] = {container id, start, stop, placing rank + 1}
+ *      for the digests it owns (first digest word mod G == rank) and zeros for the others;
+ *      returns how many it owns, HDRF_E_NOTFOUND if an owned digest is absent;
+ *   2. the G loc arrays are summed (the rows are disjoint);
+ *   3. hdrf_gx_read_fill writes, at each chunk's block offset (running sum of stop - start) of
+ *      dev_out (zeroed by the caller), the chunks this rank placed; returns the bytes written
+ *      (HDRF_E_NOTFOUND when such a chunk's container left the arena ring);
+ *   4. the G partial blocks summed byte-wise (disjoint) on the reading rank are the block; the
+ *      returned counts sum to the recipe size.
+ * Call between batches (no hdrf_gx_* batch in flight). */
+int64_t hdrf_gx_read_locate(hdrf_ctx *ctx, const uint8_t *digests, int64_t n, uint32_t *loc);
+int64_t hdrf_gx_read_fill(hdrf_ctx *ctx, const uint32_t *loc, int64_t n, uint8_t *dev_out, int64_t cap);
+
 /* Device memory helpers for callers without their own allocator (bench, tests). */
 int hdrf_dev_alloc(hdrf_ctx *ctx, uint64_t bytes, void **out);
 int hdrf_dev_free(hdrf_ctx *ctx, void *p);

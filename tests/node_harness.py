@@ -102,6 +102,26 @@ class Loopback:
                 c1 = [ctxs[r].gx_front_wait() for r in range(G)]
 
 
+def loopback_read(ctxs, reader, block_id):
+    """The node read (hdrf_gx_read_locate / _fill on every rank, summed) in one process."""
+    rec = ctxs[reader].recipe(block_id)
+    size = int.from_bytes(rec[:4], "big")
+    locs = [c.gx_read_locate(rec[4:])[0].astype(np.int64) for c in ctxs]
+    loc = np.sum(locs, axis=0).astype(np.uint32)
+    dev = torch.device("cuda", int(ctxs[0].cfg.device))
+    total = torch.zeros(max(size, 1), dtype=torch.int32, device=dev)
+    filled = 0
+    for c in ctxs:
+        part = torch.zeros(max(size, 1), dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()                    # zero fill on torch's stream before the gather
+        filled += c.gx_read_fill(loc, part.data_ptr(), size)
+        torch.cuda.synchronize()
+        total += part.to(torch.int32)
+    assert filled == size, f"{filled} of {size} bytes placed"
+    assert int(total.max()) <= 255
+    return total[:size].to(torch.uint8).cpu().numpy()
+
+
 def merged_index(ctxs):
     """Union of the ranks' index partitions, sorted by digest (the node's Redis)."""
     ks, vs = zip(*[c.index_dump() for c in ctxs])

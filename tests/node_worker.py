@@ -50,6 +50,13 @@ def main(out):
             res[f"b{gi}_store"] = np.array([b["store_size"]])
             res[f"b{gi}_recipe"] = np.frombuffer(ctx.recipe(0x900 + gi), np.uint8)
     node.reduce_batches(batches, done)
+    # the node read (DataConstructor over the node's one index): every rank takes part in every
+    # read, the rank that reduced the block receives it
+    for gi, (_, rr, _) in enumerate(seq):
+        got = node.reconstruct_block(0x900 + gi, rr)
+        if rr == r:
+            res[f"b{gi}_read"] = got
+        res[f"b{gi}_loc"] = node.last_loc
     for p in allp:
         ctx.dev_free(p)
     k, v = ctx.index_dump()
@@ -73,6 +80,17 @@ def check_outputs(out, G):
         g["store_size"] = int(z[f"b{gi}_store"][0])
         compare_block(g, o, tag=f"global block {gi} on rank {r}")
         assert z[f"b{gi}_recipe"].tobytes() == ora.recipe(0x900 + gi)
+        rd = z[f"b{gi}_read"]
+        loc = z[f"b{gi}_loc"]
+        offs = np.concatenate([[0], np.cumsum(loc[:, 2].astype(np.int64) - loc[:, 1])])
+        badk = [k for k in range(len(loc)) if not np.array_equal(rd[offs[k]:offs[k + 1]], blks[gi][offs[k]:offs[k + 1]])]
+        if badk:
+            print("BAD chunks", gi, [(k, loc[k].tolist(), int(offs[k])) for k in badk[:10]])
+            print("placers", np.bincount(loc[:, 3]))
+        bad = np.nonzero(rd != blks[gi])[0] if rd.shape == blks[gi].shape else np.arange(1)
+        assert bad.size == 0, (f"node read of global block {gi} on rank {r}: {bad.size} bytes differ, first at "
+                               f"{bad[:8]}, len {rd.shape} vs {blks[gi].shape}, got {rd[bad[:8]] if rd.shape == blks[gi].shape else ''} "
+                               f"want {blks[gi][bad[:8]]}")
     k = np.concatenate([z["index_keys"] for z in ranks])
     v = np.concatenate([z["index_vals"] for z in ranks])
     order = np.lexsort(k.T[::-1])

@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ])
 def test_node_loopback_matches_single_sequence(G, hasher, sched):
     import torch  # noqa: F401
-    from node_harness import Loopback, assemble_containers, merged_index, open_ranks
+    from node_harness import Loopback, assemble_containers, loopback_read, merged_index, open_ranks
     from oracle.oracle import Oracle
 
     cmax = 1 << 20                                   # small containers: many flushes across ranks
@@ -86,6 +86,13 @@ def test_node_loopback_matches_single_sequence(G, hasher, sched):
             od, _ = ora.container(cid)
             if od:
                 assert cid in conts, f"container {cid:#x} missing"
+    # the node read: every block rebuilt from the partitioned index and the ranks' arenas
+    for gi in range(len(seq)):
+        got = loopback_read(ctxs, seq[gi][1], 0x500 + 3 * gi)
+        assert np.array_equal(got, blocks[gi]), f"node read of global block {gi}"
+    from hdrf_amd.lib import HdrfError
+    with pytest.raises(HdrfError):
+        ctxs[0].reconstruct_block(0x500)                  # single-node read refused on G > 1
     for c, p in devs:
         c.dev_free(p)
     for c in ctxs:
@@ -132,6 +139,12 @@ def test_node_loopback_pipelined_matches_single_sequence(G, hasher):
             compare_block(ctxs[r].batch_result(i), ora.reduce(blocks[gi], 0x700 + gi),
                           tag=f"pipelined G={G} batch {j} rank {r} block {i}")
     lb.batches_pipelined(per_batch, done)
+    from node_harness import loopback_read
+    for wj in where:
+        for r, i, gi in wj:
+            got = loopback_read(ctxs, r, 0x700 + gi)
+            bad = np.nonzero(got != blocks[gi])[0]
+            assert bad.size == 0, f"pipelined node read of block {gi}: {bad.size} bytes differ, first {bad[:8]}"
     gk, gv = merged_index(ctxs)
     ok, ov = ora.index_dump()
     assert np.array_equal(gk, ok) and np.array_equal(gv, ov), "node index differs"
