@@ -11,7 +11,7 @@ blocks.  value = logical bytes reduced per second over all ranks (GB = 1e9 B).
 Multi-GPU (`torch.distributed.run`, BASELINE config 3): the GPUs of the node are ranks of ONE
 reduction, as the DataNodes of one host share one Redis, allocator and chunkDir in the reference
 (DN/DataDeduplicator.java:119,165-172): a global corpus of N x 512 blocks sharded by block, each
-global batch takes 64 blocks from every rank, and the fingerprint index is partitioned by digest
+global batch takes --batch (32) blocks from every rank, and the fingerprint index is partitioned by digest
 prefix with three RCCL all-to-alls per batch over xGMI (hdrf_amd/node.py).  Work per GPU is
 fixed as N grows: scaling is weak.  (HDRF_BENCH_SAME_DEVICE=1 puts every rank on cuda:0 over gloo:
 a one-GPU rehearsal of the multi-rank path, not a measurement.)
@@ -233,6 +233,8 @@ def main():
     for _ in range(a.warmup):
         step()
     ctx.stage_times(reset=True)
+    if node is not None:
+        node.phase_ms = {}
     barrier()
     torch.cuda.synchronize()
     ctx.synchronize()
@@ -394,6 +396,10 @@ def main():
                                              "whole blocks, hdrf_submit_host"))
             line["pcie"] = {"h2d_GB_s_raw_copy": round(h2d_gbs, 2), "value_over_raw_copy": round(value / h2d_gbs, 4),
                             "note": "value is PCIe-inclusive: host buffers -> HBM -> reduced"}
+        if node is not None and node.phase_ms.get("batches"):
+            nbt = node.phase_ms["batches"]
+            line["node_back_ms_per_batch"] = {k: round(v / nbt, 3) for k, v in node.phase_ms.items() if k != "batches"}
+            line["node_back_ms_per_batch"]["note"] = "rank 0 host wall time per back phase (allocator: scan, no chain)"
         print(json.dumps(line), flush=True)
     ctx.dev_free(dev)
     if hbuf is not None:

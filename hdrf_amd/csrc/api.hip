@@ -156,6 +156,10 @@ struct hdrf_ctx {
     uint8_t *d_oflags = nullptr;
     const uint32_t *gx_x2 = nullptr;             // responses of the back batch (caller's buffer)
     AllocState gx_ain{}, gx_aout{};              // allocator before / after this rank's flush walk
+    AllocState gx_expect{};                      // this rank's flush result predicted by hdrf_gx_alloc_scan
+    int gx_scanned = 0;                          // the back batch's allocator came from the scan
+    uint8_t *d_fn = nullptr;                     // flush-function scratch (hdrf_gx_flush_fn)
+    uint64_t fn_cap = 0;
     uint64_t gx_nfront = 0, gx_nfwait = 0, gx_nback = 0;   // fronts launched / waited, batches committed
     int gx_bphase = 0;                           // back batch: 0 owner next, 1 decide, 2 flush, 3 place, 4 commit
     hdrf_stats stats{};                          // cumulative since the last reset
@@ -308,7 +312,7 @@ static void free_all(hdrf_ctx *ctx)
     ctx->rchunks.clear();
     void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch[0],
                     ctx->d_scratch[1], ctx->d_gxe[0], ctx->d_gxe[1], ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot,
-                    ctx->d_oflags, ctx->d_carena};
+                    ctx->d_oflags, ctx->d_carena, ctx->d_fn};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -1685,15 +1689,142 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
     const StoreParams P = store_params(ctx, S.nblocks);
     HIPCK(launch_store_flush(P, S.d_bst, S.d_store, S.d_pre, ctx->d_alloc, S.d_rstate, S.d_ev,
                              S.d_closed, S.d_nclosed, S.d_err, st));
+    if (!alloc_out && ctx->gx_scanned) {                // the scan knows the result: no host round trip
+        ctx->gx_aout = ctx->gx_expect;
+        ctx->gx_bphase = 3;
+        return 0;
+    }
     AllocState a{};
     HIPCK(hipMemcpyAsync(&a, ctx->d_alloc, sizeof a, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     ctx->gx_aout = a;
+    if (ctx->gx_scanned && std::memcmp(&a, &ctx->gx_expect, sizeof a) != 0)
+        return set_err(ctx, HDRF_E_DEVICE, "allocator scan disagrees with the flush walk");
     if (alloc_out) {
         std::memset(alloc_out, 0, HDRF_ALLOC_STATE_BYTES);
         std::memcpy(alloc_out, &a, sizeof a);
     }
     ctx->gx_bphase = 3;
+    return 0;
+}
+
+// ---- allocator scan: every rank's flush walk as a function of the incoming allocator ------
+// (store.hip fn_info / fn_chain).  Descriptor, int64 words: n_thread, then per range t
+// {any, S, base_last, S_last, m, m x (v, final container start, closes after the first)}.
+static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need);
+
+extern "C" int64_t hdrf_gx_flush_fn(hdrf_ctx *ctx, int64_t *desc, int64_t cap)
+{
+    HDRF_LOCK(ctx);
+    if (int rc = gx_check(ctx, 2)) return rc;
+    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    hipStream_t st = ctx->stB;
+    const StoreParams P = store_params(ctx, S.nblocks);
+    const int nt = P.n_thread;
+    const int64_t kcap = (int64_t)ctx->max_batch * ctx->cap_blk + 1;
+    const uint64_t o_fr = 64 * 4 * sizeof(FnBlock), o_k = o_fr + 256, o_err = o_k + 64, o_out = o_err + 192;
+    if (int rc = grow(ctx, &ctx->d_fn, &ctx->fn_cap, o_out + (uint64_t)nt * kcap * 24)) return rc;
+    uint8_t *F = ctx->d_fn;
+    HIPCK(hipMemsetAsync(F + o_k, 0, 64 + 4, st));
+    HIPCK(launch_flush_fn(P, S.d_bst, S.d_store, S.d_pre, (FnBlock *)F, (FnRange *)(F + o_fr), (uint64_t *)(F + o_out),
+                          kcap, (unsigned long long *)(F + o_k), (int *)(F + o_err), st));
+    FnRange fr[4];
+    unsigned long long K[4];
+    int herr = 0;
+    HIPCK(hipMemcpyAsync(fr, F + o_fr, sizeof(FnRange) * nt, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(K, F + o_k, 8 * nt, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&herr, F + o_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (herr) return set_err(ctx, HDRF_E_DEVICE, "flush function: candidate table overflow or runaway chain");
+    std::vector<uint64_t> rows[4];
+    for (int t = 0; t < nt; t++) {
+        rows[t].resize(3 * K[t]);
+        if (K[t]) HIPCK(hipMemcpyAsync(rows[t].data(), F + o_out + (uint64_t)t * kcap * 24, 24 * K[t], hipMemcpyDeviceToHost, st));
+    }
+    HIPCK(hipStreamSynchronize(st));
+    std::vector<int64_t> d{nt};
+    for (int t = 0; t < nt; t++) {
+        const size_t h = d.size();
+        d.insert(d.end(), {(int64_t)fr[t].any, (int64_t)fr[t].S, (int64_t)fr[t].base_last, (int64_t)fr[t].S_last, 0});
+        int64_t m = 0;
+        for (uint64_t i = 0; i < K[t]; i++) {
+            const uint64_t *r = &rows[t][3 * i];
+            if (r[2] >> 63) continue;                      // repeats the previous prefix
+            d.insert(d.end(), {(int64_t)r[0], (int64_t)r[1], (int64_t)r[2]});
+            m++;
+        }
+        if (fr[t].any && (m == 0 || d[h + 5] != 0)) return set_err(ctx, HDRF_E_DEVICE, "flush function: no start candidate");
+        d[h + 4] = m;
+    }
+    if (!desc || cap < (int64_t)d.size()) {
+        if (cap >= 0) set_err(ctx, HDRF_E_CAPACITY, "flush descriptor needs " + std::to_string(d.size()) + " words");
+        return -(int64_t)d.size() - 1000;           // callers size with the returned -(n + 1000)
+    }
+    std::copy(d.begin(), d.end(), desc);
+    return (int64_t)d.size();
+}
+
+// one rank's flush function applied to the allocator A (the walk of store.hip flush_kernel)
+static bool gx_apply_fn(const hdrf_ctx *ctx, const int64_t *d, int64_t len, AllocState &A)
+{
+    if (len < 1) return false;
+    const int nt = (int)d[0];
+    if (nt != ctx->cfg.n_thread) return false;
+    const int64_t cmax = (int64_t)ctx->cfg.container_max;
+    const uint32_t per = (uint32_t)(ctx->cfg.arena_slots / 4);
+    int64_t p = 1;
+    for (int t = 0; t < nt; t++) {
+        if (p + 5 > len) return false;
+        const int64_t any = d[p], S = d[p + 1], bl = d[p + 2], Sl = d[p + 3], m = d[p + 4];
+        const int64_t *v = d + p + 5;
+        p += 5 + 3 * m;
+        if (m < 0 || p > len) return false;
+        if (!any) continue;
+        const int64_t x = A.exists[t] ? (int64_t)A.cur[t] : 0;
+        int64_t cs = -x, n = 0;
+        if (x + S > cmax) {
+            const int64_t thr = cmax - x;              // first close after the last prefix <= thr
+            int64_t lo = 0, hi = m;                    // largest v <= thr (v_0 = 0 <= thr)
+            while (hi - lo > 1) {
+                const int64_t mid = (lo + hi) / 2;
+                if (v[3 * mid] <= thr) lo = mid; else hi = mid;
+            }
+            cs = v[3 * lo + 1];
+            n = 1 + v[3 * lo + 2];
+        }
+        const uint32_t base = (uint32_t)t * per;
+        A.id[t] += (uint32_t)n;
+        A.slot[t] = base + (uint32_t)(((int64_t)(A.slot[t] - base) + n) % per);
+        A.cur[t] = (uint32_t)(S - cs);
+        A.exists[t] = 1;
+        A.pos[t] = (uint32_t)(Sl - std::max<int64_t>(cs - bl, 0));
+    }
+    return p == len;
+}
+
+// The node's allocator for this batch from every rank's flush function (rank order): the state
+// this rank's flush walk starts from (the exclusive scan) and the state after the last rank.
+extern "C" int hdrf_gx_alloc_scan(hdrf_ctx *ctx, const int64_t *descs, const int64_t *lens, uint8_t *alloc_in,
+                                  uint8_t *alloc_final)
+{
+    HDRF_LOCK(ctx);
+    if (int rc = gx_check(ctx, 2)) return rc;
+    if (!descs || !lens || !alloc_in || !alloc_final) return set_err(ctx, HDRF_E_INVAL, "null scan argument");
+    AllocState A = ctx->h_alloc;
+    int64_t off = 0;
+    for (int r = 0; r < ctx->G; r++) {
+        if (r == ctx->cfg.rank) {
+            std::memset(alloc_in, 0, HDRF_ALLOC_STATE_BYTES);
+            std::memcpy(alloc_in, &A, sizeof A);
+        }
+        if (lens[r] < 1 || !gx_apply_fn(ctx, descs + off, lens[r], A))
+            return set_err(ctx, HDRF_E_INVAL, "malformed flush descriptor of rank " + std::to_string(r));
+        if (r == ctx->cfg.rank) ctx->gx_expect = A;
+        off += lens[r];
+    }
+    std::memset(alloc_final, 0, HDRF_ALLOC_STATE_BYTES);
+    std::memcpy(alloc_final, &A, sizeof A);
+    ctx->gx_scanned = 1;
     return 0;
 }
 
@@ -1711,6 +1842,9 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     gx.x2 = ctx->gx_x2; gx.x3 = x3_send; gx.cap = ctx->gx_cap; gx.counts = ctx->d_gx_counts; gx.G = ctx->G;
     HIPCK(launch_store_place(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_pre, S.d_rstate, S.d_ev, S.d_slot,
                              ctx->d_scratch[si], ctx->d_arena, S.d_pcid, S.d_ppos, gx, st));
+    // the flush walk's own result, checked against the scan's prediction after the sync below
+    AllocState got{};
+    if (ctx->gx_scanned) HIPCK(hipMemcpyAsync(&got, ctx->d_alloc, sizeof got, hipMemcpyDeviceToHost, st));
     // the node's allocator after the last rank (the next batch and the "blockID" view start here)
     if (alloc_final) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_final, sizeof(AllocState), hipMemcpyHostToDevice, st));
     std::vector<unsigned long long> cnt(ctx->G);
@@ -1722,6 +1856,11 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    if (ctx->gx_scanned) {
+        ctx->gx_scanned = 0;
+        if (std::memcmp(&got, &ctx->gx_expect, sizeof got) != 0)
+            return set_err(ctx, HDRF_E_DEVICE, "allocator scan disagrees with this rank's flush walk");
+    }
     // the open containers this rank's flush walk started and ended in hold its placed chunks even
     // when another rank closes them (the node read, hdrf_gx_read_fill, gathers from them)
     for (const AllocState *a : {&ctx->gx_ain, &ctx->gx_aout})

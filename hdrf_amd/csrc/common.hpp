@@ -118,6 +118,18 @@ struct RangeState {          // per (block, range t)
     int32_t active;              // storer t runs (storeSize != 0 and t < nThread)
 };
 
+// Node-global allocator scan (gx.hip / api.hip hdrf_gx_flush_fn): one range's flush walk over
+// a batch as a function of the open container's fill, with the batch's active blocks of range t
+// laid end to end as one stream of new bytes.
+struct FnBlock {             // per (range t, block b)
+    uint32_t act, c0, c1, base;   // active (storeSize != 0 and t < nT), chunk range, pre[c0 - 1]
+    uint64_t off, S;              // stream offset of the block's first new byte, new bytes
+    uint32_t coff, pad;           // stream index of the block's first chunk
+};
+struct FnRange {             // per range t
+    uint64_t any, S, base_last, S_last, nstream;
+};
+
 struct ClosedRec {           // a container closed during a batch
     uint32_t id, slot, len, range;
 };

@@ -84,6 +84,9 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
 hipError_t launch_store_scan(const StoreParams &P, const BlockState *bst, const uint32_t *offsets, const uint8_t *flags,
                              const uint32_t *tilesum, uint32_t *tilepre, uint64_t *store_size, uint32_t *pre,
                              hipStream_t st);
+hipError_t launch_flush_fn(const StoreParams &P, const BlockState *bst, const uint64_t *store_size, const uint32_t *pre,
+                           FnBlock *fb, FnRange *fr, uint64_t *out, int64_t kcap, unsigned long long *K, int *err,
+                           hipStream_t st);
 hipError_t launch_store_flush(const StoreParams &P, const BlockState *bst, const uint64_t *store_size, const uint32_t *pre,
                               AllocState *alloc, RangeState *rstate, FlushEv *events, ClosedRec *closed,
                               uint32_t *nclosed, int *err, hipStream_t st);

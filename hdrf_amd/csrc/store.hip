@@ -184,6 +184,121 @@ __global__ void __launch_bounds__(256) flush_kernel(StoreParams P, const BlockSt
     }
 }
 
+// ---- node-global allocator scan: the flush walk as a function of the incoming fill -------
+// Range t's closes depend on the batch-start state only through the open container's fill x:
+// the first close falls after the last chunk whose stream prefix is <= cmax - x, and from
+// there on every close is fixed by the data.  fn_chain tabulates, for every distinct stream
+// prefix v <= cmax (the possible first-close points), the final container start and the number
+// of closes; the host (api.hip gx_apply_fn) evaluates the function for any x, so the ranks'
+// allocator states come from one all-gather instead of a rank-to-rank chain.
+// grid n_thread x 64: one wave per range, lane = block
+__global__ void __launch_bounds__(64) fn_info_kernel(StoreParams P, const BlockState *__restrict__ bst,
+                                                     const uint64_t *__restrict__ store_size,
+                                                     const uint32_t *__restrict__ pre, FnBlock *__restrict__ fb,
+                                                     FnRange *__restrict__ fr)
+{
+    __shared__ uint64_t sS[64];
+    __shared__ uint32_t sN[64], sA[64];
+    const int t = blockIdx.x, l = lane_id();
+    FnBlock f{};
+    if (l < P.nblocks) {
+        const int n = bst[l].n_chunks;
+        int c0, c1, nT;
+        range_bounds(n, t, P.n_thread, P.min_mt, c0, c1, nT);
+        f.act = (store_size[l] != 0 && t < nT) ? 1u : 0u;
+        const uint32_t *pb = pre + (size_t)l * P.cap_blk;
+        f.base = c0 > 0 ? pb[c0 - 1] : 0u;
+        f.c0 = (uint32_t)c0;
+        f.c1 = (uint32_t)c1;
+        f.S = (f.act && c1 > c0) ? (uint64_t)(pb[c1 - 1] - f.base) : 0ull;
+    }
+    sS[l] = f.S;
+    sN[l] = f.act ? f.c1 - f.c0 : 0u;
+    sA[l] = f.act;
+    __syncthreads();
+    if (l == 0) {                                      // <= 64 blocks: serial exclusive offsets
+        uint64_t off = 0;
+        uint32_t coff = 0;
+        FnRange r{};
+        for (int b = 0; b < P.nblocks; b++) {
+            const uint64_t Sb = sS[b];
+            const uint32_t nb = sN[b];
+            if (sA[b]) { r.any = 1; r.base_last = off; r.S_last = Sb; }
+            sS[b] = off;
+            sN[b] = coff;
+            off += Sb;
+            coff += nb;
+        }
+        r.S = off;
+        r.nstream = coff;
+        fr[t] = r;
+    }
+    __syncthreads();
+    if (l < P.nblocks) {
+        f.off = sS[l];
+        f.coff = sN[l];
+        fb[(size_t)t * 64 + l] = f;
+    }
+}
+
+// grid (ceil((max stream chunks + 1) / 256), n_thread) x 256: candidate i of range t is the
+// stream prefix v_i before stream chunk i (v_0 = 0).  Candidates with v_i <= cmax whose chunk
+// i - 1 added bytes (the distinct prefixes) run the close chain from a container starting at
+// v_i; out[i] = {v_i, final container start, closes | repeat flag}; K[t] = candidates with
+// v_i <= cmax (a prefix, v is nondecreasing).
+__global__ void __launch_bounds__(256) fn_chain_kernel(StoreParams P, const uint32_t *__restrict__ pre,
+                                                       const FnBlock *__restrict__ fb, const FnRange *__restrict__ fr,
+                                                       uint64_t *__restrict__ out, int64_t kcap,
+                                                       unsigned long long *__restrict__ K, int *__restrict__ err)
+{
+    __shared__ FnBlock sb[64];
+    const int t = blockIdx.y;
+    const int nb = P.nblocks;
+    if ((int)threadIdx.x < nb) sb[threadIdx.x] = fb[(size_t)t * 64 + threadIdx.x];
+    __syncthreads();
+    const FnRange R = fr[t];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i > (int64_t)R.nstream) return;
+    // stream chunk j = i - 1 -> (block, chunk); v_i = prefix after it, w = prefix before it
+    uint64_t v = 0, w = 0;
+    if (i > 0) {
+        const uint32_t j = (uint32_t)(i - 1);
+        int b = 0;
+        for (int q = 0; q < nb; q++)
+            if (sb[q].act && sb[q].c1 > sb[q].c0 && sb[q].coff <= j) b = q;
+        const uint32_t *pb = pre + (size_t)b * P.cap_blk;
+        const uint32_t c = sb[b].c0 + (j - sb[b].coff);
+        v = sb[b].off + (uint64_t)(pb[c] - sb[b].base);
+        w = sb[b].off + (c > sb[b].c0 ? (uint64_t)(pb[c - 1] - sb[b].base) : 0ull);
+    }
+    if (v > (uint64_t)P.cmax) return;
+    if (i >= kcap) { atomicOr(err, 64); return; }
+    atomicMax(K + t, (unsigned long long)(i + 1));
+    uint64_t *o = out + ((size_t)t * kcap + i) * 3;
+    o[0] = v;
+    if (i > 0 && v == w) { o[1] = 0; o[2] = 1ull << 63; return; }   // same prefix as candidate i - 1
+    int64_t cs = (int64_t)v;
+    uint64_t n = 0;
+    while ((int64_t)R.S - cs > (int64_t)P.cmax) {
+        const int64_t thr = cs + (int64_t)P.cmax;
+        int b = -1;                                    // first active block ending past thr
+        for (int q = 0; q < nb && b < 0; q++)
+            if (sb[q].act && (int64_t)(sb[q].off + sb[q].S) > thr) b = q;
+        if (b < 0 || n > (uint64_t)P.ev_cap * 64) { atomicOr(err, 64); return; }
+        const uint32_t *pb = pre + (size_t)b * P.cap_blk;
+        const uint64_t lim = (uint64_t)(thr - (int64_t)sb[b].off) + sb[b].base;   // first pb[c] > lim
+        uint32_t lo = sb[b].c0, hi = sb[b].c1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((uint64_t)pb[mid] > lim) hi = mid; else lo = mid + 1;
+        }
+        cs = (int64_t)sb[b].off + (lo > sb[b].c0 ? (int64_t)(pb[lo - 1] - sb[b].base) : 0);
+        n++;
+    }
+    o[1] = (uint64_t)cs;
+    o[2] = n;
+}
+
 // workgroup-cooperative copy of one contiguous run (16-B aligned destination stores)
 __device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32_t len)
 {
@@ -334,6 +449,17 @@ hipError_t launch_store_flush(const StoreParams &P, const BlockState *bst, const
 {
     hipLaunchKernelGGL(flush_kernel, dim3(1), dim3(256), 0, st, P, bst, store_size, pre, alloc, rstate, events, closed,
                        nclosed, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_flush_fn(const StoreParams &P, const BlockState *bst, const uint64_t *store_size, const uint32_t *pre,
+                           FnBlock *fb, FnRange *fr, uint64_t *out, int64_t kcap, unsigned long long *K, int *err,
+                           hipStream_t st)
+{
+    hipLaunchKernelGGL(fn_info_kernel, dim3(P.n_thread), dim3(64), 0, st, P, bst, store_size, pre, fb, fr);
+    const int64_t nmax = (int64_t)P.nblocks * P.cap_blk + 1;
+    hipLaunchKernelGGL(fn_chain_kernel, dim3((unsigned)((nmax + 255) / 256), P.n_thread), dim3(256), 0, st, P, pre, fb, fr,
+                       out, kcap, K, err);
     return hipGetLastError();
 }
 

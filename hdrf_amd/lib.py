@@ -33,7 +33,7 @@ EXPORTS = [
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
     "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
     "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot",
-    "hdrf_gx_read_locate", "hdrf_gx_read_fill",
+    "hdrf_gx_read_locate", "hdrf_gx_read_fill", "hdrf_gx_flush_fn", "hdrf_gx_alloc_scan",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -155,6 +155,8 @@ def load():
         "hdrf_reconstruct": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_reconstruct_block": (ctypes.c_int64, [_vp, ctypes.c_uint64, _u8p, ctypes.c_int64]),
         "hdrf_gx_read_locate": (ctypes.c_int64, [_vp, _u8p, ctypes.c_int64, _vp]),
+        "hdrf_gx_flush_fn": (ctypes.c_int64, [_vp, _vp, ctypes.c_int64]),
+        "hdrf_gx_alloc_scan": (ctypes.c_int32, [_vp, _vp, _vp, _u8p, _u8p]),
         "hdrf_gx_read_fill": (ctypes.c_int64, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_int64]),
         "hdrf_batch_info": (ctypes.c_int, [_vp, ctypes.c_int32, _i64p, _i64p]),
         "hdrf_batch_offsets": (ctypes.c_int, [_vp, ctypes.c_int32, _u32p, ctypes.c_int64]),
@@ -618,11 +620,31 @@ class Context:
     def gx_decide(self, x2_recv):
         self._ck(self.L.hdrf_gx_decide(self._h, x2_recv))
 
-    def gx_flush(self, alloc_in=None):
+    def gx_flush(self, alloc_in=None, want_out=True):
         out = np.zeros(ALLOC_STATE_BYTES, np.uint8)
-        ain = None if alloc_in is None else _p(np.ascontiguousarray(alloc_in, np.uint8))
-        self._ck(self.L.hdrf_gx_flush(self._h, ain, _p(out)))
-        return out
+        a = None if alloc_in is None else np.ascontiguousarray(alloc_in, np.uint8)
+        self._ck(self.L.hdrf_gx_flush(self._h, None if a is None else _p(a), _p(out) if want_out else None))
+        return out if want_out else None
+
+    def gx_flush_fn(self):
+        """This rank's flush function (int64 descriptor) for the allocator scan."""
+        cap = 1 << 16
+        while True:
+            d = np.zeros(cap, np.int64)
+            n = self.L.hdrf_gx_flush_fn(self._h, d.ctypes.data, cap)
+            if n <= -1000:
+                cap = int(-n - 1000)
+                continue
+            return d[:self._ck(n)]
+
+    def gx_alloc_scan(self, descs):
+        """Every rank's descriptor (rank order) -> (this rank's allocator in, the node's after the batch)."""
+        lens = np.array([len(d) for d in descs], np.int64)
+        cat = np.ascontiguousarray(np.concatenate(descs), np.int64)
+        ain = np.zeros(ALLOC_STATE_BYTES, np.uint8)
+        afin = np.zeros(ALLOC_STATE_BYTES, np.uint8)
+        self._ck(self.L.hdrf_gx_alloc_scan(self._h, cat.ctypes.data, lens.ctypes.data, _p(ain), _p(afin)))
+        return ain, afin
 
     def gx_place(self, alloc_final, x3_send):
         cnt = np.zeros(self.cfg.n_ranks, np.int64)

@@ -13,6 +13,9 @@ global batch), which is what tests/test_node.py checks against the oracle.
 The phases themselves are C-ABI calls into libhdrf (include/hdrf.h, hdrf_gx_*); this module
 only moves bytes between ranks.
 """
+import os
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -62,6 +65,20 @@ class Exchange:
         if recv.is_cuda:
             torch.cuda.current_stream(recv.device).synchronize()
 
+    def all_gather_i64(self, arr):
+        """Every rank's int64 array (lengths may differ) -> list in rank order."""
+        dev = self.device if self.nccl else None
+        n = torch.tensor([len(arr)], dtype=torch.int64, device=dev)
+        ns = [torch.empty_like(n) for _ in range(self.G)]
+        dist.all_gather(ns, n)
+        ns = [int(x.item()) for x in ns]
+        m = max(ns)
+        t = torch.zeros(m, dtype=torch.int64, device=dev)
+        t[:len(arr)] = torch.as_tensor(np.asarray(arr, np.int64), device=dev)
+        out = [torch.empty_like(t) for _ in range(self.G)]
+        dist.all_gather(out, t)
+        return [o[:k].cpu().numpy() for o, k in zip(out, ns)]
+
     def chain_alloc(self, alloc_prev_batch, flush):
         """Rank r flushes after rank r-1 (rank 0 starts from the node's state); returns the node's
         allocator state after the last rank, known to every rank."""
@@ -103,6 +120,8 @@ class NodeRank:
         self.x2s, self.x2r = mk(self.w[1]), mk(self.w[1])
         self.x3s, self.x3r = mk(self.w[2]), mk(self.w[2])
         self.alloc = None          # node allocator after the last batch (None: initial state)
+        self.phase_ms = {}         # host wall time per back phase, summed over batches
+        self.chain = os.environ.get("HDRF_NODE_CHAIN") == "1"   # A/B: the old rank-to-rank chain
 
     def reset(self):
         self.ctx.reset()
@@ -117,16 +136,41 @@ class NodeRank:
     def _back(self, c1, x1s):
         """Exchanges and back phases of the batch whose front was waited (X1 counts c1)."""
         ctx, xc, cap, (w1, w2, w3) = self.ctx, self.xc, self.cap, self.w
+        tm = self.phase_ms
+        t0 = time.perf_counter()
         r1 = xc.counts(c1)
         xc.records(x1s, self.x1r, c1, r1, cap, w1)
+        t1 = time.perf_counter()
         ctx.gx_owner(self.x1r.data_ptr(), r1, self.x2s.data_ptr())
+        t2 = time.perf_counter()
         xc.records(self.x2s, self.x2r, r1, c1, cap, w2)           # responses retrace X1
+        t3 = time.perf_counter()
         ctx.gx_decide(self.x2r.data_ptr())
-        self.alloc = xc.chain_alloc(self.alloc, ctx.gx_flush)
+        if self.chain:                                   # the rank-to-rank allocator chain
+            self.alloc = xc.chain_alloc(self.alloc, ctx.gx_flush)
+            ta = tb = time.perf_counter()
+        else:
+            # the allocator as an exclusive scan of the ranks' flush functions: one all-gather
+            # instead of a rank-to-rank chain (hdrf_gx_flush_fn / hdrf_gx_alloc_scan)
+            desc = ctx.gx_flush_fn()
+            ta = time.perf_counter()
+            descs = xc.all_gather_i64(desc)
+            tb = time.perf_counter()
+            a_in, self.alloc = ctx.gx_alloc_scan(descs)
+            ctx.gx_flush(a_in, want_out=False)
+        t4 = time.perf_counter()
         c3 = ctx.gx_place(self.alloc, self.x3s.data_ptr())
+        t5 = time.perf_counter()
         r3 = xc.counts(c3)
         xc.records(self.x3s, self.x3r, c3, r3, cap, w3)
+        t6 = time.perf_counter()
         ctx.gx_commit(self.x3r.data_ptr(), r3)
+        t7 = time.perf_counter()
+        for k, (a, b) in zip(("x1", "owner", "x2", "decide+flush_fn" if not self.chain else "decide+flush chain",
+                              "fn all_gather", "scan+flush", "place", "x3", "commit"),
+                             ((t0, t1), (t1, t2), (t2, t3), (t3, ta), (ta, tb), (tb, t4), (t4, t5), (t5, t6), (t6, t7))):
+            tm[k] = tm.get(k, 0.0) + 1e3 * (b - a)
+        tm["batches"] = tm.get("batches", 0) + 1
 
     def reduce_batches(self, batches, done=None):
         """Pipelined node-global reduction of a sequence of this rank's batches

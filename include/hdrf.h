@@ -322,7 +322,10 @@ int hdrf_reset(hdrf_ctx *ctx);
  *   hdrf_gx_front  -> X1 send (records for each owner)      all-to-all X1
  *   hdrf_gx_owner  <- X1 recv, -> X2 send (responses)        all-to-all X2 (reverse counts)
  *   hdrf_gx_decide <- X2 recv
- *   hdrf_gx_flush  (rank order: rank r gets rank r-1's allocator state, rank 0 the node's)
+ *   hdrf_gx_flush_fn -> this rank's flush descriptor             all-gather of the descriptors
+ *   hdrf_gx_alloc_scan <- every rank's descriptor: its allocator in + the node's after the batch
+ *   hdrf_gx_flush  <- alloc_in (from the scan; or, without the scan, rank r gets rank r-1's
+ *                     state over a rank-to-rank chain, rank 0 the node's)
  *   hdrf_gx_place  -> X3 send (locations of new entries)     all-to-all X3
  *   hdrf_gx_commit <- X3 recv
  * hdrf_reduce_block / hdrf_reduce_batch return HDRF_E_INVAL on such a context. */
@@ -345,8 +348,20 @@ int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *d
 int hdrf_gx_front_wait(hdrf_ctx *ctx, int64_t *send_counts);
 int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send);
 int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv);
-/* alloc_in: HDRF_ALLOC_STATE_BYTES from the previous rank (NULL: this context's own state);
- * alloc_out receives the state after this rank's blocks. */
+/* The container allocator of a node-global batch without a rank-to-rank chain.  Each storer
+ * range's flush walk (DN/DataDeduplicator.java:702-818: close when curPos + len > maxSize) depends
+ * on the allocator a rank receives only through the open container's fill; hdrf_gx_flush_fn
+ * (after hdrf_gx_decide) tabulates that function on the GPU into desc (int64 words; returns the
+ * count, or -(count + 1000) when cap is too small).  With every rank's descriptor (rank order,
+ * concatenated, lens[n_ranks]) hdrf_gx_alloc_scan computes this rank's incoming allocator
+ * (alloc_in, the exclusive scan from the state after the previous batch) and the node's state
+ * after the batch (alloc_final); hdrf_gx_place verifies the prediction against the flush walk. */
+int64_t hdrf_gx_flush_fn(hdrf_ctx *ctx, int64_t *desc, int64_t cap);
+int hdrf_gx_alloc_scan(hdrf_ctx *ctx, const int64_t *descs, const int64_t *lens, uint8_t *alloc_in,
+                       uint8_t *alloc_final);
+/* alloc_in: HDRF_ALLOC_STATE_BYTES from the previous rank or the scan (NULL: this context's own
+ * state); alloc_out receives the state after this rank's blocks (NULL after a scan: no host
+ * round trip). */
 int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out);
 /* alloc_final: the node's state after the last rank's flush (becomes this context's state). */
 int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts);

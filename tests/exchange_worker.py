@@ -41,6 +41,9 @@ def main():
         return a
     fin = xc.chain_alloc(start, flush)
     assert int(fin[0]) == G * (G + 1) // 2 and all(int(fin[1 + q]) == 0xA0 + q for q in range(G)), fin[:4]
+    # descriptors of different lengths for the allocator scan
+    got = xc.all_gather_i64(np.arange(3 + 5 * r, dtype=np.int64) * (r + 1))
+    assert [g.tolist() for g in got] == [(np.arange(3 + 5 * q) * (q + 1)).tolist() for q in range(G)], got
     print("exchange ok", r, flush=True)
     dist.destroy_process_group()
 

@@ -88,10 +88,15 @@ class Loopback:
             self._a2a(self.x2s, self.x2r, r1, self.w[1])
             for r in range(G):
                 ctxs[r].gx_decide(self.x2r[r].data_ptr())
-            a = self.alloc
+            # allocator scan (NodeRank's path): every rank's flush function, no chain
+            descs = [ctxs[r].gx_flush_fn() for r in range(G)]
+            fin = None
             for r in range(G):
-                a = ctxs[r].gx_flush(a)
-            self.alloc = a
+                a_in, a_fin = ctxs[r].gx_alloc_scan(descs)
+                assert fin is None or np.array_equal(fin, a_fin), "ranks disagree on the node allocator"
+                fin = a_fin
+                ctxs[r].gx_flush(a_in, want_out=(r % 2 == 0))   # both the checked and the async form
+            a = self.alloc = fin
             c3 = [ctxs[r].gx_place(a, self.x3s[r].data_ptr()) for r in range(G)]
             r3 = self._a2a(self.x3s, self.x3r, c3, self.w[2])
             for d in range(G):
