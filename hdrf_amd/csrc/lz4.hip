@@ -156,29 +156,35 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 else tok = (uint32_t)lit << 4;
                 wave_copy(out + op, src + anchor, lit);
                 op += lit;
+                // Windows: lane l holds the 4 bytes at wb + 4l (forward) and at wb + dr + 4l (the
+                // reference, dr = mref - ip during a match).  A verified candidate arrives with both
+                // windows already loaded (its check loaded them), so a match chain costs one global
+                // round trip per sequence: the candidate bytes and the next forward bytes together.
+                uint32_t Fw = 0, Rw = 0;
+                bool have = false;
+                auto wload = [&](int at) -> uint32_t {    // guarded lane word at src + at + 4l
+                    const int q = at + 4 * l;
+                    return (q >= 0 && q + 4 <= n) ? rd32u(src + q) : 0u;
+                };
                 for (;;) {                                 // _next_match
                     if (l == 0) { wr8(out + op, (uint32_t)(ip - mref)); wr8(out + op + 1, (uint32_t)(ip - mref) >> 8); }
                     op += 2;
-                    ip += 4; mref += 4;
-                    anchor = ip;
+                    const int dr = mref - ip;
+                    if (!have) { Fw = wload(ip); Rw = wload(mref); }
+                    int wb = ip, l0 = 1;                   // lane 0 of the first window: the minmatch
+                    anchor = ip + 4;
                     for (;;) {                             // match extension
-                        const int p = ip + 4 * l;
-                        uint32_t x = 0;
+                        const int p = wb + 4 * l;
+                        uint32_t x = Fw ^ Rw;
                         bool stop = p + 4 > matchlimit;
-                        if (!stop) x = rd32u(src + p) ^ rd32u(src + mref + 4 * l);
-                        else if (p < matchlimit) {
-                            x = rd32u(src + p) ^ rd32u(src + mref + 4 * l);
-                            x |= 0xffffffffu << (8 * (matchlimit - p));   // bytes past matchlimit differ
-                        } else {
-                            x = 0xffffffffu;
-                        }
+                        if (stop) x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
+                        if (l < l0) { x = 0u; stop = false; }
                         const unsigned long long mm = ballot64(x != 0u || stop);
-                        if (!mm) { ip += 256; mref += 256; continue; }
+                        if (!mm) { wb += 256; l0 = 0; Fw = wload(wb); Rw = wload(wb + dr); continue; }
                         const int L = __builtin_ctzll(mm);
                         const uint32_t xl = rdlane(x, L);
-                        const int eq = xl ? (__builtin_ctz(xl) >> 3) : 4;
-                        ip += 4 * L + eq;
-                        mref += 4 * L + eq;
+                        ip = wb + 4 * L + (xl ? (__builtin_ctz(xl) >> 3) : 4);
+                        mref = ip + dr;
                         break;
                     }
                     int ml = ip - anchor;
@@ -197,18 +203,32 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     }
                     if (l == 0) wr8(out + tpos, tok);
                     if (ip > mflimit) { anchor = ip; goto last_literals; }
-                    // fill table; test next position
-                    const uint32_t v2 = rd32u(src + ip - 2), v0 = rd32u(src + ip);
+                    // fill table; test next position (its bytes are in the forward window unless
+                    // the match ended right at a window start)
+                    const int o2 = ip - 2 - wb;
+                    uint32_t v2, v0;
+                    if (o2 >= 0 && ((o2 + 2) >> 2) + 1 <= 63) {
+                        const int a2 = o2 >> 2, a0 = (o2 + 2) >> 2;
+                        v2 = __builtin_amdgcn_alignbyte(rdlane(Fw, a2 + 1), rdlane(Fw, a2), (uint32_t)(o2 & 3));
+                        v0 = __builtin_amdgcn_alignbyte(rdlane(Fw, a0 + 1), rdlane(Fw, a0), (uint32_t)((o2 + 2) & 3));
+                    } else {
+                        v2 = rd32u(src + ip - 2);
+                        v0 = rd32u(src + ip);
+                    }
                     int r = 0;
                     asm volatile("" ::: "memory");
                     if (l == 0) { tput(hash(v2), ip - 2); r = tget(hash(v0)); tput(hash(v0), ip); }
                     asm volatile("" ::: "memory");
                     r = (int)rdlane((uint32_t)r, 0);
-                    if (r + kMaxDist >= ip && rd32u(src + r) == v0) {
-                        mref = r;
-                        tpos = op++;
-                        tok = 0;
-                        continue;
+                    if (r + kMaxDist >= ip) {
+                        const uint32_t Cw = wload(r), Nw = wload(ip);   // one round trip
+                        if (rdlane(Cw, 0) == v0) {
+                            mref = r;
+                            tpos = op++;
+                            tok = 0;
+                            Fw = Nw; Rw = Cw; have = true;
+                            continue;
+                        }
                     }
                     break;
                 }
@@ -239,6 +259,7 @@ last_literals:
     }
     return op;
 }
+
 
 // grid (nseg_max, nclosed) x 64 threads: segment s of closed container c.  Two instances: byU32
 // segments with a 12 KiB table (every 261,100-B segment), byU16 ones (a container's short last
