@@ -80,6 +80,27 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         if (l == 0) tput(hash(rd32u(src)), 0);        // first byte
         ip = 1;
         int fip = ip, attempts = (1 << 6) + 3, m = kLzFirstBatch;
+        // Windows: lane l holds the 4 bytes at wb + 4l (forward) and at wb + dr + 4l (the
+        // reference, dr = mref - ip during a match).  A verified candidate arrives with both
+        // windows already loaded (its check loaded them), so a match chain costs one global round
+        // trip per sequence: the candidate bytes and the next forward bytes together.  The search
+        // takes its attempt words from a forward window (Sw at sb) when the batch fits in it, and a
+        // match found by the search loads one window pair 64 bytes before the match that serves
+        // the catch-up, the literals (<= 64 bytes) and the first extension step at once.
+        auto wload = [&](int at) -> uint32_t {        // guarded lane word at src + at + 4l
+            const int q = at + 4 * l;
+            if (q >= 0 && q + 4 <= n) return rd32u(src + q);
+            if (q < 0 && q > -4) return rd32u(src) << (8 * (-q));   // straddles the start: its real bytes
+            return 0u;
+        };
+        auto lane_word = [&](uint32_t w, int o) -> uint32_t {   // bytes [o, o + 4) of a window
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((o >> 2) << 2, (int)w);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) + 1) << 2, (int)w);
+            return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
+        };
+        uint32_t Fw = 0, Rw = 0, Sw = 0;
+        bool have = false, swok = false;
+        int hwb = 0, sb = 0;
         for (;;) {
             // ---- match search: a batch of m attempts at once ------------------------------
             // attempt l advances by step_l = (a0 + l) >> 6, which takes only the values q and
@@ -89,89 +110,120 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             const int step = q + (l >= 64 - rr ? 1 : 0);
             const int ipl = fip + l * q + max(0, l - (64 - rr));       // this lane's attempt
             const bool valid = l < m && ipl + step <= mflimit;
-            const uint32_t v = valid ? rd32u(src + ipl) : 0u;
+            const int last_at = fip + (m - 1) * q + max(0, m - 1 - (64 - rr));   // lane m-1's attempt
+            bool inwin = swok && fip >= sb && last_at - sb <= 251;
+            if (!inwin && last_at - fip <= 251) { Sw = wload(fip); sb = fip; swok = true; inwin = true; }
+            const uint32_t vw = lane_word(Sw, (valid && inwin) ? ipl - sb : 0);
+            const uint32_t v = !valid ? 0u : inwin ? vw : rd32u(src + ipl);
             const uint32_t h = hash(v);
             const unsigned long long vmask = ballot64(valid);
             const int nv = vmask == ~0ull ? 64 : __builtin_ctzll(~vmask);   // valid lanes are a prefix
-            int ref = 0, old = 0;
-            // Table replay in attempt order.  Fast path (u32 table): if the batch's hashes are
-            // pairwise distinct, every attempt reads the pre-batch entry and the writes commute,
-            // so one gather + one scatter do it.  Distinctness is checked by scattering lane tags
-            // (positions never have bit 31 set) and reading them back; otherwise the entries are
-            // restored and the replay runs lane by lane.
-            bool slow = u16;
-            if (!u16) {
-                // distinct hashes: scatter lane tags into the low halves and read them back
-                if (valid) old = tget(h);
-                asm volatile("" ::: "memory");
-                if (valid) tab16[h] = (unsigned short)l;
-                asm volatile("" ::: "memory");
-                const uint32_t t = valid ? (uint32_t)tab16[h] : 0u;
-                slow = ballot64(valid && t != (uint32_t)l) != 0;
-                asm volatile("" ::: "memory");
-                if (slow && valid) tab16[h] = (unsigned short)old;   // equal hashes carry equal olds
-                ref = old;
-            }
+            // Table replay in attempt order, in parallel.  Distinct hashes (the common case): every
+            // attempt reads the pre-batch entry and the writes commute — checked by scattering lane
+            // tags into the entries and reading them back.  Equal hashes: attempt i reads the
+            // position of the last earlier attempt with its hash (else the pre-batch entry), found
+            // with one ballot per hash bit; each hash keeps its last attempt up to the first match.
+            int old = 0;
+            if (valid) old = tget(h);
             asm volatile("" ::: "memory");
-            if (slow) {
-                for (int i = 0; i < nv; i++) {            // sequential replay
-                    if (l == i) { ref = tget(h); tput(h, ipl); }
-                    asm volatile("" ::: "memory");        // keep the LDS ops in program order
+            if (valid) tab16[h] = (unsigned short)l;
+            asm volatile("" ::: "memory");
+            const uint32_t tg = valid ? (uint32_t)tab16[h] : 0u;
+            const bool collide = ballot64(valid && tg != (uint32_t)l) != 0;
+            asm volatile("" ::: "memory");
+            if (valid) tab16[h] = (unsigned short)old;     // (the high parts were not touched)
+            asm volatile("" ::: "memory");
+            unsigned long long eq = 0;
+            int ref = old;
+            if (collide) {
+                eq = vmask;
+#pragma unroll
+                for (int b = 0; b < 13; b++) {
+                    if (b == 12 && !u16) break;            // byU32: 12-bit hashes, byU16: 13
+                    const bool hb = (h >> b) & 1u;
+                    const unsigned long long mb = ballot64(valid && hb);
+                    eq &= hb ? mb : ~mb;
                 }
+                const unsigned long long below = eq & ((1ull << l) - 1ull);
+                const int prev = below ? 63 - __builtin_clzll(below) : l;
+                const int pipl = __builtin_amdgcn_ds_bpermute(prev << 2, ipl);
+                if (below) ref = pipl;
             }
-            asm volatile("" ::: "memory");
             bool ok = false;
             if (valid && ref + kMaxDist >= ipl) ok = rd32u(src + ref) == v;
             const unsigned long long okm = ballot64(ok);
-            if (!slow) {                                  // commit: attempts up to the first match
+            {                                             // commit: attempts up to the first match
                 const int last = okm ? __builtin_ctzll(okm) : 63;
-                if (valid) tput(h, l <= last ? ipl : old);
+                const unsigned long long upto = last == 63 ? ~0ull : ((2ull << last) - 1ull);
+                const unsigned long long later = (l == 63 || !collide) ? 0ull : (eq & upto & (~0ull << (l + 1)));
+                if (valid && l <= last && !later) tput(h, ipl);
                 asm volatile("" ::: "memory");
             }
             if (okm) {
                 const int istar = __builtin_ctzll(okm);
-                if (slow) {
-                    for (int i = nv - 1; i > istar; i--) {    // undo the attempts after the match
-                        if (l == i) tput(h, ref);
-                        asm volatile("" ::: "memory");
-                    }
-                }
                 asm volatile("" ::: "memory");
                 ip = (int)rdlane((uint32_t)ipl, istar);
                 int mref = (int)rdlane((uint32_t)ref, istar);
-                // ---- catch up ----------------------------------------------------------
-                for (;;) {
-                    const int k = l + 1;
-                    const bool c = ip - k >= anchor && mref - k >= 0 && rd8(src + ip - k) == rd8(src + mref - k);
-                    const unsigned long long bad = ballot64(!c);
-                    const int back = bad ? __builtin_ctzll(bad) : 64;
-                    ip -= back; mref -= back;
-                    if (back < 64) break;
-                }
-                // ---- literals ----------------------------------------------------------
-                int tpos = op++;
-                const int lit = ip - anchor;
+                int tpos;
                 uint32_t tok;
-                if (lit >= 15) { tok = 15u << 4; op = put_len(out, op, lit - 15); }
-                else tok = (uint32_t)lit << 4;
-                wave_copy(out + op, src + anchor, lit);
-                op += lit;
-                // Windows: lane l holds the 4 bytes at wb + 4l (forward) and at wb + dr + 4l (the
-                // reference, dr = mref - ip during a match).  A verified candidate arrives with both
-                // windows already loaded (its check loaded them), so a match chain costs one global
-                // round trip per sequence: the candidate bytes and the next forward bytes together.
-                uint32_t Fw = 0, Rw = 0;
-                bool have = false;
-                auto wload = [&](int at) -> uint32_t {    // guarded lane word at src + at + 4l
-                    const int q = at + 4 * l;
-                    return (q >= 0 && q + 4 <= n) ? rd32u(src + q) : 0u;
-                };
+                bool fast = ip - anchor <= 64;
+                if (fast) {
+                    // one window pair at ip - 64: catch-up, literals and the first extension step
+                    const int wb0 = ip - 64, d0 = mref - ip;
+                    Fw = wload(wb0);
+                    Rw = wload(wb0 + d0);
+                    const uint32_t x = Fw ^ Rw;
+                    int hstop = -1;                        // highest stop byte in [wb0, ip)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int pos = wb0 + 4 * l + j;
+                        const bool st = l < 16 && (pos < anchor || pos + d0 < 0 || ((x >> (8 * j)) & 0xffu) != 0u);
+                        const unsigned long long bm = ballot64(st);
+                        if (bm) hstop = max(hstop, 4 * (63 - __builtin_clzll(bm)) + j);
+                    }
+                    if (hstop < 0) {
+                        fast = false;                      // 64 equal bytes: the general catch-up
+                    } else {
+                        const int back = 63 - hstop;
+                        ip -= back; mref -= back;
+                        tpos = op++;
+                        const int lit = ip - anchor;
+                        if (lit >= 15) { tok = 15u << 4; op = put_len(out, op, lit - 15); }
+                        else tok = (uint32_t)lit << 4;
+                        const int o = anchor + l - wb0;    // literal byte l from the window
+                        const uint32_t wv = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) & 63) << 2, (int)Fw);
+                        if (l < lit) wr8(out + op + l, wv >> (8 * (o & 3)));
+                        op += lit;
+                        have = true;
+                        hwb = wb0;
+                    }
+                }
+                if (!fast) {
+                    // ---- catch up ------------------------------------------------------
+                    for (;;) {
+                        const int k = l + 1;
+                        const bool c = ip - k >= anchor && mref - k >= 0 && rd8(src + ip - k) == rd8(src + mref - k);
+                        const unsigned long long bad = ballot64(!c);
+                        const int back = bad ? __builtin_ctzll(bad) : 64;
+                        ip -= back; mref -= back;
+                        if (back < 64) break;
+                    }
+                    // ---- literals ------------------------------------------------------
+                    tpos = op++;
+                    const int lit = ip - anchor;
+                    if (lit >= 15) { tok = 15u << 4; op = put_len(out, op, lit - 15); }
+                    else tok = (uint32_t)lit << 4;
+                    wave_copy(out + op, src + anchor, lit);
+                    op += lit;
+                    have = false;
+                }
                 for (;;) {                                 // _next_match
                     if (l == 0) { wr8(out + op, (uint32_t)(ip - mref)); wr8(out + op + 1, (uint32_t)(ip - mref) >> 8); }
                     op += 2;
                     const int dr = mref - ip;
-                    if (!have) { Fw = wload(ip); Rw = wload(mref); }
-                    int wb = ip, l0 = 1;                   // lane 0 of the first window: the minmatch
+                    int wb, l0;                            // lanes below l0: the minmatch (and before)
+                    if (!have) { Fw = wload(ip); Rw = wload(mref); wb = ip; l0 = 1; }
+                    else { wb = hwb; l0 = (ip + 4 - hwb) >> 2; }
                     anchor = ip + 4;
                     for (;;) {                             // match extension
                         const int p = wb + 4 * l;
@@ -226,9 +278,10 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                             mref = r;
                             tpos = op++;
                             tok = 0;
-                            Fw = Nw; Rw = Cw; have = true;
+                            Fw = Nw; Rw = Cw; have = true; hwb = ip;
                             continue;
                         }
+                        Sw = Nw; sb = ip; swok = true;     // the search after the break starts in it
                     }
                     break;
                 }

@@ -160,3 +160,19 @@ def test_stream_ragged_writes_with_large_write():
     assert f[:4] == (51_000).to_bytes(4, "big")                 # first group: 1000 + 0 + 50,000
     f2 = hadoop_lz4_stream(d, [1000, 899_000])
     assert f2.endswith(b"\0\0\0\0") and hadoop_lz4_decode(f2, len(d)) == d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", KINDS)
+def test_gpu_lz4_blocks_match_oracle(kind):
+    """The GPU lz4_block (stream-mode Lz4Codec, one write) byte for byte against the oracle's r123
+    restatement: table sizes byU16 (< 64 KiB + 11) and byU32, equal-hash batches (lowent, zeros,
+    binary), catch-up across the segment start, multi-segment blocks."""
+    from hdrf_amd.lib import Context
+    from oracle.oracle import hadoop_lz4_stream
+    ctx = Context(max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=16, arena_slots=16)
+    for n in [13, 100, 4176, 65546, 65547, 70000, 261_100, 600_000]:
+        for seed in (3, 4):
+            d = make_block(kind, seed + n, n)
+            assert ctx.stream_block_host(4, 1, d, [n]) == hadoop_lz4_stream(d, [n]), f"{kind} n={n} seed={seed}"
+    ctx.close()
