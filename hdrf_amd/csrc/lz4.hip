@@ -73,6 +73,15 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         }
     };
     auto hash = [&](uint32_t v) -> uint32_t { return (v * 2654435761u) >> hshift; };
+    auto tswap = [&](uint32_t h, int p) -> int {    // old entry, then p (one read of each word)
+        const int lo = (int)tab16[h];
+        tab16[h] = (unsigned short)p;
+        if (u16) return lo;
+        const uint32_t sh = 2 * (h & 15);
+        const uint32_t cur = (tabhi[h >> 4] >> sh) & 3u, want = ((uint32_t)p >> 16) & 3u;
+        if (cur != want) atomicXor(&tabhi[h >> 4], (cur ^ want) << sh);   // lanes share words
+        return lo | (int)(cur << 16);
+    };
 
     const int mflimit = n - kMfLimit, matchlimit = n - kLastLit;
     int op = 0, anchor = 0, ip = 0;
@@ -138,8 +147,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             if (collide) {
                 eq = vmask;
 #pragma unroll
-                for (int b = 0; b < 13; b++) {
-                    if (b == 12 && !u16) break;            // byU32: 12-bit hashes, byU16: 13
+                for (int b = 0; b < 13; b++) {             // byU32: 12-bit hashes (bit 12 is 0)
                     const bool hb = (h >> b) & 1u;
                     const unsigned long long mb = ballot64(valid && hb);
                     eq &= hb ? mb : ~mb;
@@ -267,13 +275,22 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         v2 = rd32u(src + ip - 2);
                         v0 = rd32u(src + ip);
                     }
+                    // table: [h2] = ip - 2, r = [h0], [h0] = ip.  Distinct hashes: lanes 0 and 1
+                    // do the two slots in one pass; equal hashes: r is ip - 2.
+                    const uint32_t Nw = wload(ip);        // in flight under the table update
+                    const uint32_t h2 = hash(v2), h0 = hash(v0);
                     int r = 0;
                     asm volatile("" ::: "memory");
-                    if (l == 0) { tput(hash(v2), ip - 2); r = tget(hash(v0)); tput(hash(v0), ip); }
+                    if (h2 == h0) {
+                        if (l == 0) tput(h0, ip);
+                        r = ip - 2;
+                    } else {
+                        if (l < 2) r = tswap(l == 0 ? h2 : h0, l == 0 ? ip - 2 : ip);
+                        r = (int)rdlane((uint32_t)r, 1);
+                    }
                     asm volatile("" ::: "memory");
-                    r = (int)rdlane((uint32_t)r, 0);
                     if (r + kMaxDist >= ip) {
-                        const uint32_t Cw = wload(r), Nw = wload(ip);   // one round trip
+                        const uint32_t Cw = wload(r);      // one round trip
                         if (rdlane(Cw, 0) == v0) {
                             mref = r;
                             tpos = op++;
