@@ -25,7 +25,7 @@ constexpr int kLzMaxIn = 261100;                 // BlockCompressorStream MAX_IN
 constexpr int kLzSegBound = kLzMaxIn + kLzMaxIn / 255 + 16;
 constexpr int kLzSegStride = kLzSegBound + 4;    // per-segment stride of the unpacked layout
 constexpr int kMfLimit = 12, kLastLit = 5, kMaxDist = 65535, k64KLimit = 65536 + kMfLimit - 1;
-constexpr int kLzFirstBatch = 16;                // attempts per batch after a match (then 32, 64)
+constexpr int kLzFirstBatch = 8;                 // attempts per batch after a match (then 16, 32, 64)
 
 // length >= 15 continuation bytes (255 ... rest); returns the new output offset
 __device__ __forceinline__ int put_len(uint8_t *out, int op, int len)
