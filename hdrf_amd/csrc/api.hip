@@ -1320,15 +1320,12 @@ static int64_t decode_gzip(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uin
     if (flen < 0 || (flen && !file) || cap < 0 || (cap && !dev_out)) return set_err(ctx, HDRF_E_INVAL, "bad buffers");
     if (flen == 0) return 0;                  // an empty file decodes to nothing
     if (int rc = drain(ctx)) return rc;
-    constexpr int64_t kPiece = 1 << 16;
-    const uint64_t o_res = 0, o_crc = 256, pieces_cap = (uint64_t)(cap / kPiece + 2);
-    const uint64_t o_file = (o_crc + 4 * pieces_cap + 255) & ~255ull;
-    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_file + (uint64_t)flen + 64)) return rc;
-    uint8_t *R = ctx->d_rd;
+    constexpr int64_t kPiece = 1 << 16;       // crc32_piece_kernel's piece
     hipStream_t st = ctx->st;
-    HIPCK(hipMemcpyAsync(R + o_file, file, (size_t)flen, hipMemcpyHostToDevice, st));
     uint32_t piece_op[32];
     crc_shift_op(piece_op, kPiece);
+    CrcOp op1k;
+    crc_shift_op(op1k.m, 1024);
     int64_t at = 0, out = 0;
     std::vector<uint32_t> crcs;
     while (at < flen) {
@@ -1342,24 +1339,75 @@ static int64_t decode_gzip(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uin
         if (flg & 16) { while (h < flen && file[h]) h++; h++; }
         if (flg & 2) h += 2;
         if (h > flen) return set_err(ctx, HDRF_E_INVAL, "gzip header");
-        HIPCK(launch_inflate(R + o_file + h, flen - h, dev_out + out, cap - out, (int64_t *)(R + o_res), st));
-        int64_t res[2] = {0, 0};
-        HIPCK(hipMemcpyAsync(res, R + o_res, sizeof res, hipMemcpyDeviceToHost, st));
+        // ---- 1. speculative chunk starts + per-chunk decode counts (inflate.hip) ----------------
+        const int64_t slen = flen - h, nch = inflate_chunks(slen);
+        const uint64_t o_file = 0, o_st = (o_file + (uint64_t)slen + 64 + 255) & ~255ull;
+        const uint64_t o_info = o_st + (((uint64_t)nch * 8 + 255) & ~255ull);
+        const uint64_t o_job = o_info + (((uint64_t)nch * 32 + 255) & ~255ull);
+        const uint64_t o_misc = o_job + (((uint64_t)nch * 40 + 255) & ~255ull);
+        const uint64_t o_crc = o_misc + 256, o_scr = (o_crc + 4 * ((uint64_t)(cap - out) / kPiece + 2) + 255) & ~255ull;
+        if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_scr + 256)) return rc;
+        uint8_t *R = ctx->d_rd;
+        HIPCK(hipMemcpyAsync(R + o_file, file + h, (size_t)slen, hipMemcpyHostToDevice, st));
+        HIPCK(launch_inflate_find(R + o_file, slen, (int64_t *)(R + o_st), (int64_t *)(R + o_info), st));
+        std::vector<int64_t> starts((size_t)nch), info((size_t)nch * 4);
+        HIPCK(hipMemcpyAsync(starts.data(), R + o_st, 8 * (size_t)nch, hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(info.data(), R + o_info, 32 * (size_t)nch, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
-        if (res[0] == -12) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
-        if (res[0] < 0) return set_err(ctx, HDRF_E_INVAL, "corrupt deflate stream (inflate error " + std::to_string(res[0]) + ")");
-        const int64_t n = res[0], end = h + res[1];
+        // ---- 2. the chain of real block boundaries from chunk 0; output offsets ----------------
+        std::vector<int64_t> jobs;
+        int64_t n = 0, end_bit = -1;
+        for (int64_t c = 0; c < nch;) {
+            const int64_t *f = &info[(size_t)c * 4];
+            if (f[2] < 0 || (f[2] <= c && !f[3])) return set_err(ctx, HDRF_E_INVAL, "corrupt deflate stream");
+            jobs.insert(jobs.end(), {starts[(size_t)c], f[1], n, f[0], c});
+            n += f[0];
+            if (f[3]) { end_bit = f[1]; break; }
+            c = f[2];
+        }
+        if (end_bit < 0) return set_err(ctx, HDRF_E_INVAL, "deflate stream without a final block");
+        if (n > cap - out) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
+        const int64_t end = h + (end_bit + 7) / 8;
         if (end + 8 > flen) return set_err(ctx, HDRF_E_INVAL, "gzip trailer missing");
         const uint32_t want_crc = (uint32_t)file[end] | ((uint32_t)file[end + 1] << 8) | ((uint32_t)file[end + 2] << 16) |
                                   ((uint32_t)file[end + 3] << 24);
         const uint32_t isize = (uint32_t)file[end + 4] | ((uint32_t)file[end + 5] << 8) | ((uint32_t)file[end + 6] << 16) |
                                ((uint32_t)file[end + 7] << 24);
         if (isize != (uint32_t)n) return set_err(ctx, HDRF_E_INVAL, "gzip ISIZE mismatch");
+        // ---- 3. decode the chain's chunks in parallel, resolve cross-chunk window bytes --------
+        if (n > 0) {
+            const int nj = (int)(jobs.size() / 5);
+            if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_scr + 4 * (uint64_t)n + 256)) return rc;
+            if (ctx->d_rd != R) {                      // regrown: the file copy moves with it
+                R = ctx->d_rd;
+                HIPCK(hipMemcpyAsync(R + o_file, file + h, (size_t)slen, hipMemcpyHostToDevice, st));
+            }
+            uint32_t *scr = (uint32_t *)(R + o_scr);
+            int *d_err = (int *)(R + o_misc);
+            unsigned int *d_left = (unsigned int *)(R + o_misc + 8);
+            HIPCK(hipMemcpyAsync(R + o_job, jobs.data(), 8 * jobs.size(), hipMemcpyHostToDevice, st));
+            HIPCK(hipMemsetAsync(R + o_misc, 0, 16, st));
+            HIPCK(launch_inflate_write(R + o_file, slen, (const int64_t *)(R + o_job), nj, scr, cap - out, d_err, st));
+            int herr = 0;
+            HIPCK(hipMemcpyAsync(&herr, d_err, 4, hipMemcpyDeviceToHost, st));
+            HIPCK(hipStreamSynchronize(st));
+            if (herr) return set_err(ctx, HDRF_E_INVAL, "corrupt deflate stream (chunk decode)");
+            for (int pass = 0; nj > 1; pass++) {       // pointer jumping: chains halve every pass
+                if (pass > 64) return set_err(ctx, HDRF_E_DEVICE, "window markers did not resolve");
+                unsigned int left = 0;
+                HIPCK(hipMemsetAsync(d_left, 0, 4, st));
+                HIPCK(launch_inflate_resolve(scr, n, d_left, st));
+                HIPCK(hipMemcpyAsync(&left, d_left, 4, hipMemcpyDeviceToHost, st));
+                HIPCK(hipStreamSynchronize(st));
+                if (!left) break;
+            }
+            HIPCK(launch_inflate_pack(scr, n, dev_out + out, st));
+        }
         // CRC-32 of this member's output: 64 KiB pieces on the GPU, combined here
         const int64_t np = (n + kPiece - 1) / kPiece;
         uint32_t crc = 0;
         if (np) {
-            HIPCK(launch_crc32_pieces(dev_out + out, n, kPiece, (uint32_t *)(R + o_crc), st));
+            HIPCK(launch_crc32_pieces(dev_out + out, n, op1k, (uint32_t *)(R + o_crc), st));
             crcs.resize((size_t)np);
             HIPCK(hipMemcpyAsync(crcs.data(), R + o_crc, 4 * (size_t)np, hipMemcpyDeviceToHost, st));
             HIPCK(hipStreamSynchronize(st));

@@ -5,28 +5,42 @@
 // GzipCodec.createInputStream (Hadoop's DecompressorStream over zlib inflate, hadoop-common 3.1.0);
 // tests check the output byte for byte against Python's zlib.decompress of the same file.
 //
-// A deflate stream is one sequential bit stream (each block's start is known only once the one
-// before it is decoded), so one wave decodes one member, with everything it touches per symbol in
-// LDS: the compressed input staged 4 KiB at a time, the Huffman tables (10-bit direct lookup +
-// canonical slow path for longer codes), and a 64 KiB output ring holding the 32 KiB window.
-// Literals are single LDS stores; a match is copied by the whole wave (lane i writes byte i of
-// each 64-B step from ring[pos - dist + (i mod dist)], which is exact for overlapping copies);
-// the ring is flushed to HBM in 16 KiB pieces of 16-B stores.  The CRC-32 runs afterwards, one
-// thread per 64 KiB piece (byte table in LDS); the host combines the piece CRCs
-// (crc32_combine, zlib's published GF(2) method).
+// A deflate stream is one sequential bit stream: a block's start is known only once the block
+// before it is decoded.  A block file is one gzip member of up to 128 MiB, so one sequential
+// decoder would serve a whole block at the speed of one wave.  Instead the member is cut into
+// chunks of compressed bits and decoded speculatively, the way block-parallel CPU decompressors
+// (pugz / rapidgzip, published) do it:
+//   gz_find   one wave per chunk: the first bit offset in the chunk where a dynamic-Huffman block
+//             header is valid (BTYPE 2, HLIT/HDIST in range, complete code-length code, the
+//             code lengths decode within their counts, complete literal/length and distance
+//             codes, a code for end-of-block) — a candidate block start.  Chunk 0 starts at bit 0.
+//   gz_count  one wave per candidate: decode from the candidate, counting output, until a block
+//             ends exactly at a later candidate (or the final block ends).  The host follows the
+//             chain from chunk 0 (each link is a real block boundary, so false candidates are
+//             never on it) and prefix-sums the counts.
+//   gz_write  one wave per chunk on the chain: decode again into an LDS ring of 16-bit values —
+//             bytes, or markers 256 + w for bytes of the 32 KiB window before the chunk that the
+//             chunk cannot see yet — flushed to a u32 scratch at the chunk's output offset, the
+//             markers as 256 + absolute source position.
+//   gz_resolve  pointer jumping over the scratch until no marker is left (each pass replaces a
+//             marker by what its source holds), then gz_pack narrows to bytes.
+// The CRC-32 runs afterwards, one thread per 64 KiB piece (byte table in LDS); the host combines
+// the piece CRCs (crc32_combine, zlib's published GF(2) method).
+#include "bytes.hpp"
 #include "launchers.hpp"
 
 namespace hdrf {
 
-constexpr int kInRing = 4096;                // staged input bytes
-constexpr int kOutRing = 65536;              // output ring (>= 32 KiB window + unflushed)
-constexpr int kFlushStep = 16384;
+constexpr int kInStage = 4096;               // staged compressed bytes (LDS)
+constexpr int kRing = 32768;                 // u16 output ring = the deflate window
+constexpr int kFlushAt = 16384;              // flush the ring every 16 Ki values
 constexpr int kFastBits = 10;
+constexpr int64_t kChunkBits = 8 * 32768;    // compressed bits per speculative chunk
 
 struct HuffTab {
     uint16_t fast[1 << kFastBits];            // (len << 9) | symbol for codes <= 10 bits, 0 = slow path
     uint16_t count[16];                       // codes per length
-    uint16_t sym[320];                        // symbols in canonical order
+    uint16_t sym[288];                        // symbols in canonical order
 };
 
 __constant__ uint16_t kLenBase[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31,
@@ -40,114 +54,143 @@ __constant__ uint8_t kDistExtra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5,
                                        7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-typedef __attribute__((address_space(3))) volatile uint8_t lds_vu8;
+// Kraft check of n code lengths: 0 = complete, 1 = incomplete, -1 = over-subscribed
+__device__ int kraft(const uint16_t *len, int n)
+{
+    int cnt[16] = {0};
+    for (int s = 0; s < n; s++) cnt[len[s] & 15]++;
+    int left = 1;
+    for (int b = 1; b < 16; b++) {
+        left = (left << 1) - cnt[b];
+        if (left < 0) return -1;
+    }
+    return left > 0 ? 1 : 0;
+}
 
-// Build the decode tables from n code lengths (wave-cooperative).  Returns false on an
-// over-subscribed set (an incomplete set is legal for the distance codes).
-__device__ bool huff_build(HuffTab *t, const uint16_t *len, int n)
+// Decode tables from n code lengths (wave-cooperative).  false: not a code zlib's inflate accepts
+// (over-subscribed, or incomplete with more than one code).
+__device__ bool huff_build(HuffTab *t, const uint16_t *len, int n, bool dist)
 {
     const int l = lane_id();
+    __shared__ uint16_t offs_s[16];
     for (int i = l; i < (1 << kFastBits); i += 64) t->fast[i] = 0;
     if (l < 16) t->count[l] = 0;
     __syncthreads();
+    bool ok = true;
     if (l == 0) {
         for (int s = 0; s < n; s++) t->count[len[s]]++;
         t->count[0] = 0;
-    }
-    __syncthreads();
-    uint16_t offs[16];
-    int left = 1;
-    bool ok = true;
-    for (int b = 1; b < 16; b++) {
-        left = (left << 1) - t->count[b];
-        if (left < 0) ok = false;
-    }
-    offs[1] = 0;
-    for (int b = 1; b < 15; b++) offs[b + 1] = offs[b] + t->count[b];
-    if (l == 0)
-        for (int s = 0; s < n; s++)
-            if (len[s]) t->sym[offs[len[s]]++] = (uint16_t)s;
-    __syncthreads();
-    // direct table: canonical code of each symbol (codes of one length are consecutive), bit-reversed
-    if (l == 0) {
-        int code = 0, k = 0;
-        for (int b = 1; b <= kFastBits; b++) {
-            for (int c = 0; c < t->count[b]; c++, k++, code++) {
-                int r = 0;
-                for (int i = 0; i < b; i++) r |= ((code >> i) & 1) << (b - 1 - i);
-                for (int f = r; f < (1 << kFastBits); f += 1 << b) t->fast[f] = (uint16_t)((b << 9) | t->sym[k]);
-            }
-            code <<= 1;
+        int left = 1, nz = 0;
+        for (int b = 1; b < 16; b++) {
+            left = (left << 1) - t->count[b];
+            if (left < 0) ok = false;
+            nz += t->count[b];
         }
+        int maxl = 0;
+        for (int b = 1; b < 16; b++)
+            if (t->count[b]) maxl = b;
+        if (ok && left > 0 && !(maxl == 1 || (dist && nz == 0))) ok = false;   // incomplete
+        uint16_t o = 0;
+        for (int b = 1; b < 16; b++) { offs_s[b] = o; o += t->count[b]; }
+        for (int s = 0; s < n; s++)
+            if (len[s]) t->sym[offs_s[len[s]]++] = (uint16_t)s;
+        o = 0;
+        for (int b = 1; b < 16; b++) { offs_s[b] = o; o += t->count[b]; }   // first sorted index per length
+    }
+    ok = __builtin_amdgcn_readfirstlane(ok ? 1 : 0) != 0;
+    __syncthreads();
+    // direct table: sorted symbol k of length b has canonical code first[b] + (k - offs[b]),
+    // bit-reversed; it fills 2^(10-b) entries.  Lanes take sorted symbols.
+    int first[16];
+    {
+        int code = 0;
+        first[0] = 0;
+        for (int b = 1; b < 16; b++) {
+            code = (code + (b > 1 ? t->count[b - 1] : 0)) << 1;
+            first[b] = code;
+        }
+    }
+    int total = 0;
+    for (int b = 1; b <= kFastBits; b++) total += t->count[b];
+    for (int k = l; k < total; k += 64) {
+        int b = 1;
+        while (b < kFastBits && k >= offs_s[b] + t->count[b]) b++;
+        const int code = first[b] + (k - offs_s[b]);
+        const int r = (int)(__builtin_bitreverse32((uint32_t)code) >> (32 - b));
+        const uint16_t e = (uint16_t)((b << 9) | t->sym[k]);
+        for (int f = r; f < (1 << kFastBits); f += 1 << b) t->fast[f] = e;
     }
     __syncthreads();
     return ok;
 }
 
-// grid 1 x 64: inflate one raw deflate stream src[0, slen) into dst[0, cap).
-// res[0] = output length (or < 0: error), res[1] = input bytes consumed (byte-aligned end)
-__global__ void __launch_bounds__(64) gz_inflate_kernel(const uint8_t *__restrict__ src, int64_t slen,
-                                                        uint8_t *__restrict__ dst, int64_t cap,
-                                                        int64_t *__restrict__ res)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t ring[kOutRing];
-    __shared__ __attribute__((aligned(16))) uint8_t inb[kInRing + 16];
-    __shared__ HuffTab hl, hd;
-    __shared__ uint16_t lens[320];
-    const int l = lane_id();
-    lds_vu8 *vring = (lds_vu8 *)ring;
-    // ---- bit reader over the staged input ---------------------------------------------------
-    int64_t ibase = -(int64_t)kInRing;        // input staged: src[ibase, ibase + kInRing)
-    int64_t ip = 0;                           // next byte to take into the bit buffer
-    uint64_t bb = 0;
-    int bn = 0;
-    int err = 0;
-    auto stage = [&](int64_t at) {            // stage src[at & ~15, +4096) (zero past slen)
-        ibase = at & ~(int64_t)15;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int64_t o = ibase + 16 * (l + 64 * k);
+// Bit reader over the compressed stream, staged in LDS; uniform state (scalar registers).
+struct BitIn {
+    const uint8_t *src;
+    int64_t slen;
+    uint32_t *stage;          // kInStage / 4 words of src[sbase, sbase + kInStage)
+    int64_t sbase;
+    int64_t nb;               // next (4-aligned) byte to pull
+    uint64_t bb;
+    int bn;
+
+    __device__ void restage(int64_t at)
+    {
+        const int l = lane_id();
+        sbase = at & ~(int64_t)15;
+        for (int k = 0; k < kInStage / 1024; k++) {
+            const int64_t o = sbase + 16 * (l + 64 * k);
             uint4 v;
             if (o + 16 <= slen) v = ld16(src + o);
             else {
                 uint32_t w[4] = {0, 0, 0, 0};
                 for (int i = 0; i < 16; i++)
-                    if (o + i < slen) w[i >> 2] |= (uint32_t)src[o + i] << (8 * (i & 3));
+                    if (o + i >= 0 && o + i < slen) w[i >> 2] |= (uint32_t)src[o + i] << (8 * (i & 3));
                 v = make_uint4(w[0], w[1], w[2], w[3]);
             }
-            *(uint4 *)(inb + 16 * (l + 64 * k)) = v;
+            *(uint4 *)(stage + 4 * (l + 64 * k)) = v;
         }
         __syncthreads();
-    };
-    auto byte_at = [&](int64_t p) -> uint32_t {
-        if (p < ibase || p >= ibase + kInRing) stage(p);
-        return inb[p - ibase];
-    };
-    auto refill = [&]() {
-        while (bn <= 56) {
-            if (ip >= slen + 8) { err = -1; return; }            // ran past the stream
-            bb |= (uint64_t)byte_at(ip) << bn;
-            ip++;
-            bn += 8;
-        }
-    };
-    auto bits = [&](int n) -> uint32_t {      // n <= 32
-        if (bn < n) refill();
-        const uint32_t v = (uint32_t)(bb & ((n == 32) ? 0xffffffffull : ((1ull << n) - 1)));
+    }
+    __device__ uint32_t word(int64_t at)     // 4 bytes at a 4-aligned offset
+    {
+        if (at < sbase || at + 4 > sbase + kInStage) restage(at);
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[(at - sbase) >> 2]);
+    }
+    __device__ void start(int64_t bit)
+    {
+        nb = (bit >> 3) & ~(int64_t)3;
+        const int drop = (int)(bit - 8 * nb);
+        bb = (uint64_t)word(nb) >> drop;
+        bn = 32 - drop;
+        nb += 4;
+    }
+    __device__ void pull()
+    {
+        bb |= (uint64_t)word(nb) << bn;
+        bn += 32;
+        nb += 4;
+    }
+    __device__ bool over() const { return nb > slen + 16; }   // decoding the zeros past the stream
+    __device__ uint32_t bits(int n)          // n <= 32
+    {
+        if (bn < n) pull();
+        const uint32_t v = (uint32_t)(bb & ((n >= 32) ? 0xffffffffull : ((1ull << n) - 1)));
         bb >>= n;
         bn -= n;
         return v;
-    };
-    auto decode = [&](const HuffTab *t) -> int {
-        if (bn < 15) refill();
-        const uint32_t e = t->fast[bb & ((1u << kFastBits) - 1)];
+    }
+    __device__ int64_t pos() const { return 8 * nb - bn; }
+    __device__ int decode(const HuffTab *t)
+    {
+        if (bn < 32) pull();
+        const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)t->fast[bb & ((1u << kFastBits) - 1)]);
         if (e) {
-            const int n = e >> 9;
+            const int n = (int)(e >> 9);
             bb >>= n;
             bn -= n;
-            return e & 511;
+            return (int)(e & 511);
         }
-        // canonical decode, one bit at a time (codes longer than 10 bits)
         int code = 0, first = 0, index = 0;
         for (int b = 1; b < 16; b++) {
             code |= (int)(bb & 1);
@@ -161,180 +204,392 @@ __global__ void __launch_bounds__(64) gz_inflate_kernel(const uint8_t *__restric
             code <<= 1;
         }
         return -1;
-    };
-    int64_t pos = 0, flushed = 0;
-    auto flush = [&](int64_t upto) {          // ring bytes [flushed, upto) -> dst (upto - flushed <= 16 KiB)
+    }
+};
+
+// Dynamic block header after BFINAL/BTYPE: the code lengths -> tables.  0 or < 0 (error)
+__device__ int read_dynamic(BitIn &in, uint16_t *lens, HuffTab *hl, HuffTab *hd)
+{
+    const int l = lane_id();
+    const int nlit = (int)in.bits(5) + 257, ndist = (int)in.bits(5) + 1, ncl = (int)in.bits(4) + 4;
+    if (nlit > 286 || ndist > 30) return -4;
+    for (int s = l; s < 19; s += 64) lens[s] = 0;
+    __syncthreads();
+    for (int i = 0; i < ncl; i++) {
+        const uint32_t v = in.bits(3);
+        if (l == 0) lens[kClOrder[i]] = (uint16_t)v;
+    }
+    __syncthreads();
+    if (kraft(lens, 19) != 0) return -5;                 // the code-length code must be complete
+    if (!huff_build(hl, lens, 19, false)) return -5;
+    int i = 0;
+    uint16_t prev = 0;
+    while (i < nlit + ndist) {
+        const int sym = in.decode(hl);
+        if (sym < 0) return -6;
+        int rep = 1;
+        uint16_t v = (uint16_t)sym;
+        if (sym == 16) { if (i == 0) return -7; v = prev; rep = 3 + (int)in.bits(2); }
+        else if (sym == 17) { v = 0; rep = 3 + (int)in.bits(3); }
+        else if (sym == 18) { v = 0; rep = 11 + (int)in.bits(7); }
+        if (i + rep > nlit + ndist) return -8;
         __syncthreads();
-        const int64_t n = upto - flushed;
-        const int off = (int)(flushed & (kOutRing - 1));        // multiple of 16 except the final piece
-        const int nw = ((uintptr_t)dst & 15) ? 0 : (int)(n >> 4);   // 16-B stores need an aligned dst
-        for (int w = l; w < nw; w += 64) {
-            const uint4 v = *(const uint4 *)(ring + off + 16 * w);
-            st16(dst + flushed + 16 * w, v);
+        for (int k = l; k < rep; k += 64) lens[i + k] = v;
+        __syncthreads();
+        i += rep;
+        prev = v;
+    }
+    if (lens[256] == 0) return -9;
+    __syncthreads();
+    const uint16_t dv = l < ndist ? lens[nlit + l] : 0;
+    __syncthreads();
+    if (l < 30) lens[288 + l] = l < ndist ? dv : 0;
+    for (int s = nlit + l; s < 288; s += 64) lens[s] = 0;
+    __syncthreads();
+    if (!huff_build(hl, lens, 288, false)) return -10;
+    if (!huff_build(hd, lens + 288, 30, true)) return -10;
+    return 0;
+}
+
+__device__ void fixed_tables(uint16_t *lens, HuffTab *hl, HuffTab *hd)
+{
+    const int l = lane_id();
+    for (int s = l; s < 288; s += 64) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+    for (int s = l; s < 30; s += 64) lens[288 + s] = 5;
+    __syncthreads();
+    huff_build(hl, lens, 288, false);
+    huff_build(hd, lens + 288, 30, true);
+}
+
+// ---- gz_find: grid nchunks x 64 ---------------------------------------------------------------
+// start[c] = first bit offset in [c * kChunkBits, (c + 1) * kChunkBits) where a dynamic block header
+// validates (chunk 0: bit 0), else -1.
+__global__ void __launch_bounds__(64) gz_find_kernel(const uint8_t *__restrict__ src, int64_t slen, int64_t *__restrict__ start)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kInStage / 4];
+    __shared__ HuffTab hl, hd;
+    __shared__ uint16_t lens[320];
+    const int c = blockIdx.x, l = lane_id();
+    if (c == 0) { if (l == 0) start[0] = 0; return; }
+    const int64_t lo = (int64_t)c * kChunkBits, hi = min(lo + kChunkBits, 8 * slen);
+    BitIn in{src, slen, stage, -(int64_t)kInStage, 0, 0, 0};
+    for (int64_t b0 = lo; b0 < hi; b0 += 64) {
+        // cheap per-lane checks on 96 bits at offset b: BTYPE = 2, HLIT/HDIST ranges, complete CL code
+        const int64_t b = b0 + l;
+        bool cand = b < hi;
+        if (cand) {
+            const int64_t by = b >> 3;
+            uint64_t w = 0;
+            uint32_t w2 = 0;
+            for (int i = 0; i < 12; i++) {
+                const uint32_t x = by + i < slen ? src[by + i] : 0u;
+                if (i < 8) w |= (uint64_t)x << (8 * i); else w2 |= x << (8 * (i - 8));
+            }
+            const int sh = (int)(b & 7);
+            const uint64_t lo64 = (w >> sh) | (sh ? ((uint64_t)w2 << (64 - sh)) : 0ull);
+            const uint32_t hi32 = w2 >> sh;
+            cand = ((lo64 >> 1) & 3) == 2;
+            const int nlit = (int)((lo64 >> 3) & 31), ndist = (int)((lo64 >> 8) & 31), ncl = (int)((lo64 >> 13) & 15) + 4;
+            cand = cand && nlit <= 29 && ndist <= 29;
+            if (cand) {
+                int left = 1 << 7, used = 0;
+                for (int i = 0; i < ncl; i++) {
+                    const int at = 17 + 3 * i;
+                    const uint32_t v = at >= 64 ? (hi32 >> (at - 64)) & 7u
+                                     : at + 3 <= 64 ? (uint32_t)(lo64 >> at) & 7u
+                                                    : (uint32_t)(((lo64 >> at) | ((uint64_t)hi32 << (64 - at))) & 7u);
+                    if (v) { left -= 1 << (7 - v); used++; }
+                }
+                cand = left == 0 && used > 0;
+            }
         }
-        for (int64_t i = 16 * (int64_t)nw + l; i < n; i += 64) dst[flushed + i] = ring[(off + i) & (kOutRing - 1)];
+        unsigned long long m = ballot64(cand);
+        while (m) {                                    // full header decode for each candidate, in order
+            const int k = __builtin_ctzll(m);
+            m &= m - 1;
+            in.start(b0 + k);
+            in.bits(3);
+            if (read_dynamic(in, lens, &hl, &hd) == 0) {
+                if (l == 0) start[c] = b0 + k;
+                return;
+            }
+        }
+    }
+    if (l == 0) start[c] = -1;
+}
+
+// ---- the chunk decoder -----------------------------------------------------------------------
+// Decodes from bit `from` until a block ends at a bit offset equal to a later chunk start
+// (kWrite = false: finds it and counts) or at `stop_bit` (kWrite = true).  Write mode keeps the
+// output in an LDS ring of u16 values (bytes, or 256 + w for window byte w before the chunk) and
+// flushes it to scratch[out0 ..] as u32 (markers as 256 + absolute source position).
+struct ChunkOut {
+    int64_t n;           // output bytes
+    int64_t end_bit;     // bit offset after the last block decoded
+    int end_chunk;       // chunk whose start it reached (nchunks: the final block), -1: error
+    int final_block;
+};
+
+template <bool kWrite>
+__device__ ChunkOut decode_chunk(BitIn &in, int64_t from, const int64_t *starts, int c, int nchunks, int64_t stop_bit,
+                                 uint16_t *lens, HuffTab *hl, HuffTab *hd, uint16_t *ring, uint32_t *scratch,
+                                 int64_t out0, int64_t cap)
+{
+    const int l = lane_id();
+    ChunkOut r{0, 0, -1, 0};
+    in.start(from);
+    int64_t pos = 0, flushed = 0;
+    int j = c + 1;                                     // next candidate chunk start
+    auto flush = [&](int64_t upto) {                   // ring [flushed, upto) -> scratch
+        __syncthreads();
+        for (int64_t i = flushed + l; i < upto; i += 64) {
+            const uint32_t v = ring[i & (kRing - 1)];
+            scratch[out0 + i] = v < 256u ? v : (uint32_t)(256 + (out0 - kRing + (int64_t)(v - 256u)));
+        }
         flushed = upto;
     };
-    bool last = false;
-    while (!last && !err) {
-        last = bits(1);
-        const int type = (int)bits(2);
-        if (type == 0) {                       // stored: byte-align, LEN, NLEN, LEN raw bytes
-            const int drop = bn & 7;
-            bb >>= drop;
-            bn -= drop;
-            ip -= bn >> 3;                     // hand the buffered bytes back to the byte reader
-            bb = 0;
-            bn = 0;
-            const uint32_t len = byte_at(ip) | (byte_at(ip + 1) << 8);
-            const uint32_t nlen = byte_at(ip + 2) | (byte_at(ip + 3) << 8);
-            ip += 4;
-            if ((len ^ 0xffffu) != nlen || ip + len > slen || pos + len > cap) { err = -2; break; }
-            // 4 KiB steps (16 B per lane), flushing between steps so the ring never overruns
-            for (uint32_t o = 0; o < len; o += 1024) {
-                const int64_t q = ip + o + 16 * l;
-                if (o + 16 * l < len) {
-                    const uint32_t nb = min(16u, len - (o + 16 * l));
-                    for (uint32_t j = 0; j < nb; j++)
-                        vring[(pos + o + 16 * l + j) & (kOutRing - 1)] = src[q + j];
-                }
-                if (((o + 1024) & 4095) == 0 || o + 1024 >= len) {
-                    const int64_t at = pos + min(len, o + 1024);
-                    while (at - flushed >= kFlushStep) flush(flushed + kFlushStep);
-                }
-            }
-            ip += len;
-            pos += len;
-            continue;
-        }
-        if (type == 3) { err = -3; break; }
-        // ---- code tables ------------------------------------------------------------------------
-        int nlit = 288, ndist = 30;
-        if (type == 1) {                       // fixed codes
-            for (int s = l; s < 288; s += 64) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-            for (int s = l; s < 30; s += 64) lens[288 + s] = 5;
-            __syncthreads();
-        } else {                               // dynamic codes
-            nlit = (int)bits(5) + 257;
-            ndist = (int)bits(5) + 1;
-            const int ncl = (int)bits(4) + 4;
-            if (nlit > 286 || ndist > 30) { err = -4; break; }
-            for (int s = l; s < 19; s += 64) lens[s] = 0;
-            __syncthreads();
-            for (int i = 0; i < ncl; i++) {
-                const uint32_t v = bits(3);
-                if (l == 0) lens[kClOrder[i]] = (uint16_t)v;
-            }
-            __syncthreads();
-            if (!huff_build(&hl, lens, 19)) { err = -5; break; }
-            int i = 0;
-            uint16_t prev = 0;
-            while (i < nlit + ndist) {
-                const int sym = decode(&hl);
-                if (sym < 0) { err = -6; break; }
-                int rep = 1;
-                uint16_t v = (uint16_t)sym;
-                if (sym == 16) { if (i == 0) { err = -7; break; } v = prev; rep = 3 + (int)bits(2); }
-                else if (sym == 17) { v = 0; rep = 3 + (int)bits(3); }
-                else if (sym == 18) { v = 0; rep = 11 + (int)bits(7); }
-                if (i + rep > nlit + ndist) { err = -8; break; }
-                __syncthreads();
-                for (int k = l; k < rep; k += 64) lens[i + k] = v;
-                __syncthreads();
-                i += rep;
-                prev = v;
-            }
-            if (err) break;
-            if (lens[256] == 0) { err = -9; break; }
-            // the distance lengths follow the literal/length ones: move them to lens[288..]
-            __syncthreads();
-            uint16_t dv = l < ndist ? lens[nlit + l] : 0;
-            __syncthreads();
-            if (l < 30) lens[288 + l] = l < ndist ? dv : 0;
-            for (int s = nlit + l; s < 288; s += 64) lens[s] = 0;
-            __syncthreads();
-        }
-        if (!huff_build(&hl, lens, 288)) { err = -10; break; }
-        {
-            bool ok = huff_build(&hd, lens + 288, 30);
-            (void)ok;                          // an incomplete distance set is legal
-        }
-        // ---- symbols -------------------------------------------------------------------------------
-        for (;;) {
-            const int sym = decode(&hl);
-            if (sym < 0) { err = -11; break; }
-            if (sym < 256) {
-                if (pos >= cap) { err = -12; break; }
-                if (l == 0) vring[pos & (kOutRing - 1)] = (uint8_t)sym;
-                pos++;
-            } else if (sym == 256) {
-                break;
-            } else {
-                const int li = sym - 257;
-                if (li >= 29) { err = -13; break; }
-                const int len = kLenBase[li] + (int)bits(kLenExtra[li]);
-                const int ds = decode(&hd);
-                if (ds < 0 || ds >= 30) { err = -14; break; }
-                const int dist = kDistBase[ds] + (int)bits(kDistExtra[ds]);
-                if (dist > pos) { err = -15; break; }
-                if (pos + len > cap) { err = -12; break; }
-                for (int o = 0; o < len; o += 64) {
-                    const int i = o + l;
-                    if (i < len) {
-                        const int q = dist >= len ? i : i % dist;
-                        const uint8_t b = vring[(pos - dist + q) & (kOutRing - 1)];
-                        vring[(pos + i) & (kOutRing - 1)] = b;
+    for (;;) {
+        const bool last = in.bits(1) != 0;
+        const int type = (int)in.bits(2);
+        if (type == 0) {                               // stored: byte-aligned LEN, NLEN, raw bytes
+            const int drop = in.bn & 7;
+            in.bb >>= drop;
+            in.bn -= drop;
+            const uint32_t len = in.bits(16), nlen = in.bits(16);
+            const int64_t P = in.pos() >> 3;
+            if ((len ^ 0xffffu) != nlen || P + (int64_t)len > in.slen) return r;
+            if (kWrite) {
+                if (pos + (int64_t)len > cap) return r;
+                for (uint32_t o = 0; o < len; o += 1024) {  // 16 bytes per lane per step
+                    const uint32_t q0 = o + 16 * l;
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    if (q0 + 16 <= len) {
+                        const uint8_t *sp = in.src + P + q0;
+                        const uint8_t *sa = (const uint8_t *)((uintptr_t)sp & ~(uintptr_t)3);
+                        const uint32_t sh = (uint32_t)((uintptr_t)sp & 3);
+                        uint32_t a[5];
+#pragma unroll
+                        for (int t = 0; t < 5; t++) a[t] = (t < 4 || sh) ? ld4(sa + 4 * t) : 0u;
+#pragma unroll
+                        for (int t = 0; t < 4; t++) w[t] = __builtin_amdgcn_alignbyte(a[t + 1], a[t], sh);
+                    } else {
+                        for (uint32_t t = 0; t < 16 && q0 + t < len; t++) w[t >> 2] |= (uint32_t)in.src[P + q0 + t] << (8 * (t & 3));
                     }
+#pragma unroll
+                    for (int t = 0; t < 16; t++)
+                        if (q0 + t < len) ring[(pos + q0 + t) & (kRing - 1)] = (uint16_t)((w[t >> 2] >> (8 * (t & 3))) & 0xffu);
+                    const int64_t pw = pos + min(len, o + 1024);
+                    if (pw - flushed >= kFlushAt) flush(flushed + kFlushAt);
                 }
-                pos += len;
             }
-            if (pos - flushed >= kFlushStep) flush(flushed + kFlushStep);
+            pos += len;
+            in.start(8 * (P + (int64_t)len));
+        } else if (type == 3) {
+            return r;
+        } else {
+            if (type == 1) fixed_tables(lens, hl, hd);
+            else if (read_dynamic(in, lens, hl, hd) != 0) return r;
+            for (;;) {
+                const int sym = in.decode(hl);
+                if (sym < 0 || in.over()) return r;
+                if (sym < 256) {
+                    if (kWrite) {
+                        if (pos >= cap) return r;
+                        if (l == 0) ring[pos & (kRing - 1)] = (uint16_t)sym;
+                    }
+                    pos++;
+                } else if (sym == 256) {
+                    break;
+                } else {
+                    const int li = sym - 257;
+                    if (li >= 29) return r;
+                    const int len = kLenBase[li] + (int)in.bits(kLenExtra[li]);
+                    const int ds = in.decode(hd);
+                    if (ds < 0 || ds >= 30) return r;
+                    const int dist = kDistBase[ds] + (int)in.bits(kDistExtra[ds]);
+                    if (kWrite) {
+                        if (pos + len > cap) return r;
+                        if (c == 0 && dist > pos) return r;    // nothing before the first chunk
+                        asm volatile("" ::: "memory");          // ring reads after the earlier writes
+                        for (int o = 0; o < len; o += 64) {
+                            const int i = o + l;
+                            if (i < len) {
+                                int q = i;                         // i mod dist without a division
+                                while (q >= dist) q -= dist;
+                                const int64_t sp = pos - dist + q;
+                                const uint16_t v = sp >= 0 ? ring[sp & (kRing - 1)] : (uint16_t)(256 + (kRing + sp));
+                                ring[(pos + i) & (kRing - 1)] = v;
+                            }
+                        }
+                    } else if (c == 0 && dist > pos) {
+                        return r;
+                    }
+                    pos += len;
+                }
+                if (kWrite && pos - flushed >= kFlushAt) flush(flushed + kFlushAt);
+            }
         }
-    }
-    if (!err) flush(pos);
-    if (l == 0) {
-        res[0] = err ? (int64_t)err : pos;
-        res[1] = ip - (bn >> 3);              // bytes consumed (the unread whole bytes go back)
+        const int64_t e = in.pos();
+        if (kWrite) {
+            if (last || e >= stop_bit) {
+                flush(pos);
+                r.n = pos; r.end_bit = e; r.end_chunk = 0; r.final_block = last;
+                return r;
+            }
+        } else {
+            if (last) {
+                r.n = pos; r.end_bit = e; r.end_chunk = nchunks; r.final_block = 1;
+                return r;
+            }
+            while (j < nchunks && (starts[j] < 0 || starts[j] < e)) j++;
+            if (j < nchunks && starts[j] == e) {
+                r.n = pos; r.end_bit = e; r.end_chunk = j;
+                return r;
+            }
+        }
+        if (e > 8 * in.slen + 64) return r;            // ran past the stream
     }
 }
 
-// grid ceil(pieces / 256) x 256: crc[i] = CRC-32 of dst[i * piece, min((i + 1) * piece, n))
-__global__ void __launch_bounds__(256) crc32_piece_kernel(const uint8_t *__restrict__ data, int64_t n, int64_t piece,
-                                                          uint32_t *__restrict__ crc)
+// grid nchunks x 64: info[c] = {output bytes, end bit, end chunk (-1 error), final}
+__global__ void __launch_bounds__(64) gz_count_kernel(const uint8_t *__restrict__ src, int64_t slen,
+                                                      const int64_t *__restrict__ starts, int nchunks,
+                                                      int64_t *__restrict__ info)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kInStage / 4];
+    __shared__ HuffTab hl, hd;
+    __shared__ uint16_t lens[320];
+    const int c = blockIdx.x;
+    const int64_t s = starts[c];
+    int64_t *o = info + 4 * (size_t)c;
+    if (s < 0) { if (lane_id() == 0) { o[0] = 0; o[1] = 0; o[2] = -1; o[3] = 0; } return; }
+    BitIn in{src, slen, stage, -(int64_t)kInStage, 0, 0, 0};
+    const ChunkOut r = decode_chunk<false>(in, s, starts, c, nchunks, 0, lens, &hl, &hd, nullptr, nullptr, 0, 0);
+    if (lane_id() == 0) { o[0] = r.n; o[1] = r.end_bit; o[2] = r.end_chunk; o[3] = r.final_block; }
+}
+
+// grid nlist x 64: chain chunk k = list[k] -> scratch[out0[k] ..]; ok[k] = 1 on success
+__global__ void __launch_bounds__(64) gz_write_kernel(const uint8_t *__restrict__ src, int64_t slen,
+                                                      const int64_t *__restrict__ job, int njob,
+                                                      uint32_t *__restrict__ scratch, int64_t cap, int *__restrict__ err)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kInStage / 4];
+    __shared__ HuffTab hl, hd;
+    __shared__ uint16_t lens[320];
+    __shared__ uint16_t ring[kRing];
+    const int k = blockIdx.x;
+    const int64_t *jb = job + 5 * (size_t)k;            // {start bit, stop bit, out0, n, chunk index}
+    BitIn in{src, slen, stage, -(int64_t)kInStage, 0, 0, 0};
+    const ChunkOut r = decode_chunk<true>(in, jb[0], nullptr, (int)jb[4], 0, jb[1], lens, &hl, &hd, ring, scratch, jb[2],
+                                          cap - jb[2]);
+    if (lane_id() == 0 && (r.end_chunk != 0 || r.n != jb[3] || r.end_bit != jb[1])) atomicOr(err, 1);
+}
+
+// one pointer-jumping pass: every marker takes what its source holds; *left counts markers seen
+__global__ void __launch_bounds__(256) gz_resolve_kernel(uint32_t *__restrict__ s, int64_t n, unsigned int *__restrict__ left)
+{
+    unsigned int cnt = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const uint32_t v = s[i];
+        if (v >= 256u) {
+            const uint32_t w = s[v - 256u];
+            s[i] = w;
+            cnt += w >= 256u;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (lane_id() == 0 && cnt) atomicAdd(left, cnt);
+}
+
+__global__ void __launch_bounds__(256) gz_pack_kernel(const uint32_t *__restrict__ s, int64_t n, uint8_t *__restrict__ dst)
+{
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) dst[i] = (uint8_t)s[i];
+}
+
+// grid pieces x 64: crc[i] = CRC-32 of data[i * piece, min((i + 1) * piece, n)), piece = 64 KiB.
+// Each lane takes 1 KiB (byte table in LDS); lane 0 folds the lane CRCs with the "append 1 KiB"
+// operator (crc(A||B) = op(crc(A)) ^ crc(B)) and runs the tail bytes itself.
+__global__ void __launch_bounds__(64) crc32_piece_kernel(const uint8_t *__restrict__ data, int64_t n, CrcOp op1k,
+                                                         uint32_t *__restrict__ crc)
 {
     __shared__ uint32_t tab[256];
-    const int t = threadIdx.x;
-    uint32_t c = (uint32_t)t;
-    for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-    tab[t] = c;
-    __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * 256 + t;
-    const int64_t a = i * piece, b = min(n, a + piece);
-    if (a >= n) return;
-    uint32_t r = 0xffffffffu;
-    int64_t p = a;
-    for (; p + 4 <= b && (p & 3); p++) r = tab[(r ^ data[p]) & 0xff] ^ (r >> 8);
-    for (; p + 4 <= b; p += 4) {
-        const uint32_t w = *(const uint32_t *)(data + p);
-        r = tab[(r ^ w) & 0xff] ^ (r >> 8);
-        r = tab[(r ^ (w >> 8)) & 0xff] ^ (r >> 8);
-        r = tab[(r ^ (w >> 16)) & 0xff] ^ (r >> 8);
-        r = tab[(r ^ (w >> 24)) & 0xff] ^ (r >> 8);
+    __shared__ uint32_t lc[64];
+    const int l = lane_id();
+    for (int t = l; t < 256; t += 64) {
+        uint32_t c = (uint32_t)t;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        tab[t] = c;
     }
-    for (; p < b; p++) r = tab[(r ^ data[p]) & 0xff] ^ (r >> 8);
-    crc[i] = r ^ 0xffffffffu;
+    __syncthreads();
+    const int64_t a0 = (int64_t)blockIdx.x * 65536, pl = min((int64_t)65536, n - a0);
+    const int nfull = (int)(pl >> 10);
+    if (l < nfull) {
+        const uint8_t *w = data + a0 + 1024 * l;       // any alignment (members follow each other)
+        uint32_t r = 0xffffffffu;
+        for (int i = 0; i < 256; i++) {
+            // rd32u reads up to 3 bytes past its word: the last word by bytes (the buffer may end there)
+            const uint32_t x = i < 255 ? rd32u(w + 4 * i)
+                                       : (uint32_t)w[1020] | ((uint32_t)w[1021] << 8) | ((uint32_t)w[1022] << 16) |
+                                             ((uint32_t)w[1023] << 24);
+            r = tab[(r ^ x) & 0xff] ^ (r >> 8);
+            r = tab[(r ^ (x >> 8)) & 0xff] ^ (r >> 8);
+            r = tab[(r ^ (x >> 16)) & 0xff] ^ (r >> 8);
+            r = tab[(r ^ (x >> 24)) & 0xff] ^ (r >> 8);
+        }
+        lc[l] = r ^ 0xffffffffu;
+    }
+    __syncthreads();
+    if (l == 0) {
+        uint32_t acc = 0;
+        for (int i = 0; i < nfull; i++) {
+            uint32_t s = 0, v = acc;
+            for (int k = 0; v; v >>= 1, k++)
+                if (v & 1) s ^= op1k.m[k];
+            acc = i ? s ^ lc[i] : lc[0];
+        }
+        uint32_t r = acc ^ 0xffffffffu;                // continue the CRC over the tail bytes
+        for (int64_t p = a0 + 1024 * (int64_t)nfull; p < a0 + pl; p++) r = tab[(r ^ data[p]) & 0xff] ^ (r >> 8);
+        crc[blockIdx.x] = nfull || pl > 0 ? r ^ 0xffffffffu : 0u;
+    }
 }
 
-hipError_t launch_inflate(const uint8_t *src, int64_t slen, uint8_t *dst, int64_t cap, int64_t *res, hipStream_t st)
+int64_t inflate_chunks(int64_t slen) { return (8 * slen + kChunkBits - 1) / kChunkBits; }
+
+hipError_t launch_inflate_find(const uint8_t *src, int64_t slen, int64_t *starts, int64_t *info, hipStream_t st)
 {
-    hipLaunchKernelGGL(gz_inflate_kernel, dim3(1), dim3(64), 0, st, src, slen, dst, cap, res);
+    const int64_t n = inflate_chunks(slen);
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gz_find_kernel, dim3((unsigned)n), dim3(64), 0, st, src, slen, starts);
+    hipLaunchKernelGGL(gz_count_kernel, dim3((unsigned)n), dim3(64), 0, st, src, slen, starts, (int)n, info);
     return hipGetLastError();
 }
 
-hipError_t launch_crc32_pieces(const uint8_t *data, int64_t n, int64_t piece, uint32_t *crc, hipStream_t st)
+hipError_t launch_inflate_write(const uint8_t *src, int64_t slen, const int64_t *jobs, int njobs, uint32_t *scratch,
+                                int64_t cap, int *err, hipStream_t st)
 {
-    const int64_t np = (n + piece - 1) / piece;
-    if (np > 0) hipLaunchKernelGGL(crc32_piece_kernel, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, st, data, n, piece, crc);
+    if (njobs > 0)
+        hipLaunchKernelGGL(gz_write_kernel, dim3((unsigned)njobs), dim3(64), 0, st, src, slen, jobs, njobs, scratch, cap, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_inflate_resolve(uint32_t *scratch, int64_t n, unsigned int *left, hipStream_t st)
+{
+    const unsigned g = (unsigned)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256));
+    hipLaunchKernelGGL(gz_resolve_kernel, dim3(g), dim3(256), 0, st, scratch, n, left);
+    return hipGetLastError();
+}
+
+hipError_t launch_inflate_pack(const uint32_t *scratch, int64_t n, uint8_t *dst, hipStream_t st)
+{
+    const unsigned g = (unsigned)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256));
+    if (n > 0) hipLaunchKernelGGL(gz_pack_kernel, dim3(g), dim3(256), 0, st, scratch, n, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc32_pieces(const uint8_t *data, int64_t n, const CrcOp &op1k, uint32_t *crc, hipStream_t st)
+{
+    const int64_t np = (n + 65535) / 65536;
+    if (np > 0) hipLaunchKernelGGL(crc32_piece_kernel, dim3((unsigned)np), dim3(64), 0, st, data, n, op1k, crc);
     return hipGetLastError();
 }
 

@@ -54,8 +54,14 @@ hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals
                              unsigned long long tag_mask, int *err, hipStream_t st);
 // GzipCodec read side (inflate.hip): one raw deflate stream -> dst; res[0] = length or < 0, res[1] =
 // bytes consumed.  CRC-32 of fixed-size pieces of a buffer.
-hipError_t launch_inflate(const uint8_t *src, int64_t slen, uint8_t *dst, int64_t cap, int64_t *res, hipStream_t st);
-hipError_t launch_crc32_pieces(const uint8_t *data, int64_t n, int64_t piece, uint32_t *crc, hipStream_t st);
+int64_t inflate_chunks(int64_t slen);
+hipError_t launch_inflate_find(const uint8_t *src, int64_t slen, int64_t *starts, int64_t *info, hipStream_t st);
+hipError_t launch_inflate_write(const uint8_t *src, int64_t slen, const int64_t *jobs, int njobs, uint32_t *scratch,
+                                int64_t cap, int *err, hipStream_t st);
+hipError_t launch_inflate_resolve(uint32_t *scratch, int64_t n, unsigned int *left, hipStream_t st);
+hipError_t launch_inflate_pack(const uint32_t *scratch, int64_t n, uint8_t *dst, hipStream_t st);
+struct CrcOp { uint32_t m[32]; };       // GF(2) operator "append k zero bytes" (columns)
+hipError_t launch_crc32_pieces(const uint8_t *data, int64_t n, const CrcOp &op1k, uint32_t *crc, hipStream_t st);
 hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *digests,
                               const uint32_t *slot, int log2cap, unsigned long long tag_mask,
                               unsigned long long *stats, hipStream_t st);

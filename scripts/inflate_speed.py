@@ -7,7 +7,7 @@ import zlib
 
 import numpy as np
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from hdrf_amd.lib import Context  # noqa: E402
 from tests.helpers import make_block  # noqa: E402
 
