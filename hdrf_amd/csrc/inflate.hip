@@ -134,7 +134,7 @@ struct BitIn {
     uint64_t bb;
     int bn;
 
-    __device__ void restage(int64_t at)
+    __device__ __forceinline__ void restage(int64_t at)
     {
         const int l = lane_id();
         sbase = at & ~(int64_t)15;
@@ -152,12 +152,12 @@ struct BitIn {
         }
         __syncthreads();
     }
-    __device__ uint32_t word(int64_t at)     // 4 bytes at a 4-aligned offset
+    __device__ __forceinline__ uint32_t word(int64_t at)     // 4 bytes at a 4-aligned offset
     {
         if (at < sbase || at + 4 > sbase + kInStage) restage(at);
         return (uint32_t)__builtin_amdgcn_readfirstlane((int)stage[(at - sbase) >> 2]);
     }
-    __device__ void start(int64_t bit)
+    __device__ __forceinline__ void start(int64_t bit)
     {
         nb = (bit >> 3) & ~(int64_t)3;
         const int drop = (int)(bit - 8 * nb);
@@ -165,14 +165,14 @@ struct BitIn {
         bn = 32 - drop;
         nb += 4;
     }
-    __device__ void pull()
+    __device__ __forceinline__ void pull()
     {
         bb |= (uint64_t)word(nb) << bn;
         bn += 32;
         nb += 4;
     }
-    __device__ bool over() const { return nb > slen + 16; }   // decoding the zeros past the stream
-    __device__ uint32_t bits(int n)          // n <= 32
+    __device__ __forceinline__ bool over() const { return nb > slen + 16; }   // decoding the zeros past the stream
+    __device__ __forceinline__ uint32_t bits(int n)          // n <= 32
     {
         if (bn < n) pull();
         const uint32_t v = (uint32_t)(bb & ((n >= 32) ? 0xffffffffull : ((1ull << n) - 1)));
@@ -180,8 +180,8 @@ struct BitIn {
         bn -= n;
         return v;
     }
-    __device__ int64_t pos() const { return 8 * nb - bn; }
-    __device__ int decode(const HuffTab *t)
+    __device__ __forceinline__ int64_t pos() const { return 8 * nb - bn; }
+    __device__ __forceinline__ int decode(const HuffTab *t)
     {
         if (bn < 32) pull();
         const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)t->fast[bb & ((1u << kFastBits) - 1)]);
@@ -208,7 +208,7 @@ struct BitIn {
 };
 
 // Dynamic block header after BFINAL/BTYPE: the code lengths -> tables.  0 or < 0 (error)
-__device__ int read_dynamic(BitIn &in, uint16_t *lens, HuffTab *hl, HuffTab *hd)
+__device__ __forceinline__ int read_dynamic(BitIn &in, uint16_t *lens, HuffTab *hl, HuffTab *hd)
 {
     const int l = lane_id();
     const int nlit = (int)in.bits(5) + 257, ndist = (int)in.bits(5) + 1, ncl = (int)in.bits(4) + 4;
@@ -251,7 +251,7 @@ __device__ int read_dynamic(BitIn &in, uint16_t *lens, HuffTab *hl, HuffTab *hd)
     return 0;
 }
 
-__device__ void fixed_tables(uint16_t *lens, HuffTab *hl, HuffTab *hd)
+__device__ __forceinline__ void fixed_tables(uint16_t *lens, HuffTab *hl, HuffTab *hd)
 {
     const int l = lane_id();
     for (int s = l; s < 288; s += 64) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
@@ -331,7 +331,7 @@ struct ChunkOut {
 };
 
 template <bool kWrite>
-__device__ ChunkOut decode_chunk(BitIn &in, int64_t from, const int64_t *starts, int c, int nchunks, int64_t stop_bit,
+__device__ __forceinline__ ChunkOut decode_chunk(BitIn &in, int64_t from, const int64_t *starts, int c, int nchunks, int64_t stop_bit,
                                  uint16_t *lens, HuffTab *hl, HuffTab *hd, uint16_t *ring, uint32_t *scratch,
                                  int64_t out0, int64_t cap)
 {
