@@ -208,6 +208,23 @@ struct BitIn {
 };
 
 // Dynamic block header after BFINAL/BTYPE: the code lengths -> tables.  0 or < 0 (error)
+// Kraft sum of n code lengths over the wave (sum of 2^(15 - len)); codes: number of nonzero lengths
+__device__ __forceinline__ void kraft_wave(const uint16_t *len, int n, int &sum, int &codes, int &maxl)
+{
+    int s = 0, k = 0, m = 0;
+    for (int i = lane_id(); i < n; i += 64) {
+        const int v = len[i];
+        if (v) { s += 1 << (15 - v); k++; m = max(m, v); }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o);
+        k += __shfl_xor(k, o);
+        m = max(m, __shfl_xor(m, o));
+    }
+    sum = s; codes = k; maxl = m;
+}
+
+template <bool kTables = true>
 __device__ __forceinline__ int read_dynamic(BitIn &in, uint16_t *lens, HuffTab *hl, HuffTab *hd)
 {
     const int l = lane_id();
@@ -240,6 +257,14 @@ __device__ __forceinline__ int read_dynamic(BitIn &in, uint16_t *lens, HuffTab *
         prev = v;
     }
     if (lens[256] == 0) return -9;
+    if (!kTables) {                                    // validation only (gz_find): zlib's rules
+        int sum, codes, maxl;
+        kraft_wave(lens, nlit, sum, codes, maxl);
+        if (sum > (1 << 15) || (sum < (1 << 15) && maxl != 1)) return -10;
+        kraft_wave(lens + nlit, ndist, sum, codes, maxl);
+        if (sum > (1 << 15) || (sum < (1 << 15) && codes > 0 && maxl != 1)) return -10;
+        return 0;
+    }
     __syncthreads();
     const uint16_t dv = l < ndist ? lens[nlit + l] : 0;
     __syncthreads();
@@ -264,55 +289,78 @@ __device__ __forceinline__ void fixed_tables(uint16_t *lens, HuffTab *hl, HuffTa
 // ---- gz_find: grid nchunks x 64 ---------------------------------------------------------------
 // start[c] = first bit offset in [c * kChunkBits, (c + 1) * kChunkBits) where a dynamic block header
 // validates (chunk 0: bit 0), else -1.
+__device__ __forceinline__ bool header_cheap(uint64_t lo64, uint32_t hi32)
+{
+    // BTYPE = 2, HLIT / HDIST in range, a complete code-length code; zlib's deflate trims trailing
+    // zero code-length lengths (HCLEN = last nonzero + 1, at least 4) — a heuristic only: a start
+    // it rejects is decoded through by the chunk before
+    if (((lo64 >> 1) & 3) != 2) return false;
+    const int nlit = (int)((lo64 >> 3) & 31), ndist = (int)((lo64 >> 8) & 31), ncl = (int)((lo64 >> 13) & 15) + 4;
+    if (nlit > 29 || ndist > 29) return false;
+    int left = 1 << 7, used = 0;
+    uint32_t lastv = 0;
+    for (int i = 0; i < ncl; i++) {
+        const int at = 17 + 3 * i;
+        const uint32_t v = at >= 64 ? (hi32 >> (at - 64)) & 7u
+                         : at + 3 <= 64 ? (uint32_t)(lo64 >> at) & 7u
+                                        : (uint32_t)(((lo64 >> at) | ((uint64_t)hi32 << (64 - at))) & 7u);
+        if (v) { left -= 1 << (7 - v); used++; }
+        lastv = v;
+    }
+    return left == 0 && used > 0 && (ncl == 4 || lastv != 0);
+}
+
+// grid nchunks x 64: the chunk's bytes staged in LDS; lane = byte, 8 bit offsets per lane
 __global__ void __launch_bounds__(64) gz_find_kernel(const uint8_t *__restrict__ src, int64_t slen, int64_t *__restrict__ start)
 {
+    constexpr int kCB = (int)(kChunkBits / 8);        // chunk bytes
+    __shared__ __attribute__((aligned(16))) uint32_t cb[kCB / 4 + 8];
     __shared__ __attribute__((aligned(16))) uint32_t stage[kInStage / 4];
     __shared__ HuffTab hl, hd;
     __shared__ uint16_t lens[320];
     const int c = blockIdx.x, l = lane_id();
     if (c == 0) { if (l == 0) start[0] = 0; return; }
-    const int64_t lo = (int64_t)c * kChunkBits, hi = min(lo + kChunkBits, 8 * slen);
+    const int64_t B0 = (int64_t)c * kCB, hi = min(8 * (B0 + kCB), 8 * slen);
+    for (int i = l; i < kCB / 4 + 8; i += 64) {        // bytes [B0, B0 + kCB + 32), zeros past the stream
+        const int64_t o = B0 + 4 * i;
+        uint32_t w = 0;
+        if (o + 4 <= slen) w = rd32u(src + o);
+        else for (int k = 0; k < 4; k++) if (o + k < slen) w |= (uint32_t)src[o + k] << (8 * k);
+        cb[i] = w;
+    }
+    __syncthreads();
     BitIn in{src, slen, stage, -(int64_t)kInStage, 0, 0, 0};
-    for (int64_t b0 = lo; b0 < hi; b0 += 64) {
-        // cheap per-lane checks on 96 bits at offset b: BTYPE = 2, HLIT/HDIST ranges, complete CL code
-        const int64_t b = b0 + l;
-        bool cand = b < hi;
-        if (cand) {
-            const int64_t by = b >> 3;
-            uint64_t w = 0;
-            uint32_t w2 = 0;
-            for (int i = 0; i < 12; i++) {
-                const uint32_t x = by + i < slen ? src[by + i] : 0u;
-                if (i < 8) w |= (uint64_t)x << (8 * i); else w2 |= x << (8 * (i - 8));
-            }
-            const int sh = (int)(b & 7);
-            const uint64_t lo64 = (w >> sh) | (sh ? ((uint64_t)w2 << (64 - sh)) : 0ull);
-            const uint32_t hi32 = w2 >> sh;
-            cand = ((lo64 >> 1) & 3) == 2;
-            const int nlit = (int)((lo64 >> 3) & 31), ndist = (int)((lo64 >> 8) & 31), ncl = (int)((lo64 >> 13) & 15) + 4;
-            cand = cand && nlit <= 29 && ndist <= 29;
-            if (cand) {
-                int left = 1 << 7, used = 0;
-                for (int i = 0; i < ncl; i++) {
-                    const int at = 17 + 3 * i;
-                    const uint32_t v = at >= 64 ? (hi32 >> (at - 64)) & 7u
-                                     : at + 3 <= 64 ? (uint32_t)(lo64 >> at) & 7u
-                                                    : (uint32_t)(((lo64 >> at) | ((uint64_t)hi32 << (64 - at))) & 7u);
-                    if (v) { left -= 1 << (7 - v); used++; }
-                }
-                cand = left == 0 && used > 0;
-            }
+    for (int by = 0; by < kCB; by += 64) {
+        const int q = by + l;                          // this lane's byte (chunk-relative)
+        const uint32_t w0 = cb[q >> 2], w1 = cb[(q >> 2) + 1], w2 = cb[(q >> 2) + 2], w3 = cb[(q >> 2) + 3];
+        const uint32_t s8 = 8 * (q & 3);
+        const uint32_t a0 = s8 ? (w0 >> s8) | (w1 << (32 - s8)) : w0;
+        const uint32_t a1 = s8 ? (w1 >> s8) | (w2 << (32 - s8)) : w1;
+        const uint32_t a2 = s8 ? (w2 >> s8) | (w3 << (32 - s8)) : w2;   // bytes q .. q + 11
+        const uint64_t w = (uint64_t)a0 | ((uint64_t)a1 << 32);
+        uint32_t mask = 0;
+#pragma unroll
+        for (int sh = 0; sh < 8; sh++) {
+            const uint64_t lo64 = (w >> sh) | (sh ? ((uint64_t)a2 << (64 - sh)) : 0ull);
+            const int64_t b = 8 * (B0 + q) + sh;
+            if (b < hi && header_cheap(lo64, a2 >> sh)) mask |= 1u << sh;
         }
-        unsigned long long m = ballot64(cand);
-        while (m) {                                    // full header decode for each candidate, in order
+        unsigned long long m = ballot64(mask != 0);
+        while (m) {                                    // full header decode, in bit order
             const int k = __builtin_ctzll(m);
-            m &= m - 1;
-            in.start(b0 + k);
-            in.bits(3);
-            if (read_dynamic(in, lens, &hl, &hd) == 0) {
-                if (l == 0) start[c] = b0 + k;
-                return;
+            uint32_t mk = rdlane(mask, k);
+            while (mk) {
+                const int sh = __builtin_ctz(mk);
+                mk &= mk - 1;
+                const int64_t b = 8 * (B0 + by + k) + sh;
+                in.start(b);
+                in.bits(3);
+                if (read_dynamic<false>(in, lens, &hl, &hd) == 0) {
+                    if (l == 0) start[c] = b;
+                    return;
+                }
             }
+            m &= m - 1;
         }
     }
     if (l == 0) start[c] = -1;
