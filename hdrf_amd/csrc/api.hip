@@ -866,7 +866,8 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) ctx->stats.open_bytes += ctx->h_alloc.cur[t];
     // recipes (SET longToBytes(id,4) -> BE32 size | digests): the block's digests are copied on
-    // the device into the recipe store (stream B); the slot's next SHA waits for the copies
+    // the device into the recipe store on the copy stream (off stream B, the critical chain);
+    // the slot's next SHA waits for the copies
     int nj = 0;
     for (int b = 0; b < nblocks; b++) {
         const uint32_t key = (uint32_t)S.ids[b];
@@ -880,9 +881,9 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
         }
     }
     if (nj) {
-        HIPCK(hipMemcpyAsync(S.d_rjobs, S.h_rjobs, sizeof(RecipeCopy) * nj, hipMemcpyHostToDevice, ctx->stB));
-        HIPCK(launch_recipe_copy(S.d_rjobs, nj, ctx->stB));
-        HIPCK(hipEventRecord(S.recipe_done, ctx->stB));
+        HIPCK(hipMemcpyAsync(S.d_rjobs, S.h_rjobs, sizeof(RecipeCopy) * nj, hipMemcpyHostToDevice, ctx->stC));
+        HIPCK(launch_recipe_copy(S.d_rjobs, nj, ctx->stC));
+        HIPCK(hipEventRecord(S.recipe_done, ctx->stC));
         S.recipe_pending = true;
     }
     return 0;

@@ -307,7 +307,7 @@ hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int ca
                           uint32_t gbase, int G, uint32_t *x1, int64_t cap, unsigned long long *counts, int *err,
                           hipStream_t st)
 {
-    (void)hipMemsetAsync(counts, 0, sizeof(unsigned long long) * G, st);
+    if (hipError_t e = hipMemsetAsync(counts, 0, sizeof(unsigned long long) * G, st)) return e;
     dim3 g(ntiles, nblocks);
     if (hasher == 0)
         hipLaunchKernelGGL(gx_emit_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, scratch, slot, flags, gbase, G,
@@ -325,7 +325,7 @@ hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts
 {
     const int HW = hasher == 0 ? 5 : 7;
     dim3 g(gx_tiles(max_count), G);
-    (void)hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st);
+    if (hipError_t e = hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st)) return e;
     if (hasher == 0) {
         hipLaunchKernelGGL(own_claim_kernel<5>, g, dim3(256), 0, st, x1, counts, cap, tab, log2cap, cur, tag_mask, oslot,
                            oflags, err);

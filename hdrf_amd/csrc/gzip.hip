@@ -317,7 +317,7 @@ hipError_t launch_gzip_parse(const uint8_t *src, int64_t n, const uint32_t *m128
     uint32_t *tail = p; p += 4;
     uint32_t *symend = p; p += n + 2;
     uint32_t *off = p;
-    if (n) (void)hipMemsetAsync(stw, 0, 4 * (size_t)n, st);
+    if (n) if (hipError_t e = hipMemsetAsync(stw, 0, 4 * (size_t)n, st)) return e;
     if (nseg) {
         hipLaunchKernelGGL(gz_spec_kernel, dim3((nseg + 63) / 64), dim3(64), 0, st, src, n, m128, m32, stw, cnw, ssym,
                            send, ex, nseg);
@@ -841,7 +841,7 @@ hipError_t launch_gzip_encode(const uint8_t *src, int64_t n, const void *tab, co
                               int nblk, void *state, uint8_t *scratch, int64_t slot, int64_t *info, int64_t *off,
                               uint32_t *pcrc, uint8_t *out, int64_t *flen, hipStream_t st)
 {
-    (void)hipMemsetAsync(scratch, 0, (size_t)slot * (size_t)nblk, st);
+    if (hipError_t e = hipMemsetAsync(scratch, 0, (size_t)slot * (size_t)nblk, st)) return e;
     hipLaunchKernelGGL(gz_block_kernel, dim3(nblk), dim3(256), 0, st, (const GzTab *)tab, syms, blks, nblk,
                        (GzBlk *)state, scratch, slot, info);
     hipLaunchKernelGGL(gz_offsets_kernel, dim3(1), dim3(64), 0, st, info, nblk, off);

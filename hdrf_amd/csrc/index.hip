@@ -367,7 +367,7 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
     mk->mark(st);
     dim3 g(ntiles, nblocks);
     static const int lds = [] { const char *e = getenv("HDRF_CLAIM_LDS"); return e ? atoi(e) : 0; }();
-    (void)hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st);
+    if (hipError_t e = hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st)) return e;
     if (hasher == 0) {
         hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
                            slot, flags, err);

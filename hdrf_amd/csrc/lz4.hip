@@ -96,11 +96,11 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         // takes its attempt words from a forward window (Sw at sb) when the batch fits in it, and a
         // match found by the search loads one window pair 64 bytes before the match that serves
         // the catch-up, the literals (<= 64 bytes) and the first extension step at once.
-        auto wload = [&](int at) -> uint32_t {        // guarded lane word at src + at + 4l
+        auto wload = [&](int at) -> uint32_t {        // guarded lane word at src + at + 4l (branch-free)
             const int q = at + 4 * l;
-            if (q >= 0 && q + 4 <= n) return rd32u(src + q);
-            if (q < 0 && q > -4) return rd32u(src) << (8 * (-q));   // straddles the start: its real bytes
-            return 0u;
+            const int qc = q < 0 ? 0 : (q + 4 > n ? max(n - 4, 0) : q);
+            const uint32_t raw = rd32u(src + qc);
+            return (q >= 0 && q + 4 <= n) ? raw : (q < 0 && q > -4) ? raw << (8 * (-q)) : 0u;   // straddle: real bytes
         };
         auto lane_word = [&](uint32_t w, int o) -> uint32_t {   // bytes [o, o + 4) of a window
             const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((o >> 2) << 2, (int)w);
@@ -114,6 +114,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             // ---- match search: a batch of m attempts at once ------------------------------
             // attempt l advances by step_l = (a0 + l) >> 6, which takes only the values q and
             // q + 1 inside one batch, so the attempt positions have a closed form (no scan)
+            fip = (int)rdfirst((uint32_t)fip); attempts = (int)rdfirst((uint32_t)attempts); m = (int)rdfirst((uint32_t)m);
+            op = (int)rdfirst((uint32_t)op); anchor = (int)rdfirst((uint32_t)anchor); sb = (int)rdfirst((uint32_t)sb);
             const int a0 = attempts;
             const int q = a0 >> 6, rr = a0 & 63;
             const int step = q + (l >= 64 - rr ? 1 : 0);
@@ -157,8 +159,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 const int pipl = __builtin_amdgcn_ds_bpermute(prev << 2, ipl);
                 if (below) ref = pipl;
             }
-            bool ok = false;
-            if (valid && ref + kMaxDist >= ipl) ok = rd32u(src + ref) == v;
+            const uint32_t cv = rd32u(src + ref);          // ref is a position < n in every lane
+            const bool ok = valid && ref + kMaxDist >= ipl && cv == v;
             const unsigned long long okm = ballot64(ok);
             {                                             // commit: attempts up to the first match
                 const int last = okm ? __builtin_ctzll(okm) : 63;
@@ -226,6 +228,11 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     have = false;
                 }
                 for (;;) {                                 // _next_match
+                    // the parse state is wave-uniform: keep it in scalar registers so the
+                    // branches on it are scalar branches, not exec-mask regions
+                    ip = (int)rdfirst((uint32_t)ip); mref = (int)rdfirst((uint32_t)mref);
+                    op = (int)rdfirst((uint32_t)op); anchor = (int)rdfirst((uint32_t)anchor);
+                    tpos = (int)rdfirst((uint32_t)tpos); tok = rdfirst(tok); hwb = (int)rdfirst((uint32_t)hwb);
                     if (l == 0) { wr8(out + op, (uint32_t)(ip - mref)); wr8(out + op + 1, (uint32_t)(ip - mref) >> 8); }
                     op += 2;
                     const int dr = mref - ip;

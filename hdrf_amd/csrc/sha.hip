@@ -318,7 +318,7 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
                       const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
                       hipStream_t st, Marker *mk)
 {
-    (void)hipMemsetAsync(queue, 0, sizeof(uint32_t) * nblocks, st);
+    if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t) * nblocks, st)) return e;
     mk->mark(st);
     // 2 waves per SIMD (r02, pipelined with chunking on its own stream: 992 GB/s vs 940 at 3 and
     // 919 at 4) — fewer concurrent per-lane streams thrash L2 less and leave CUs to the

@@ -469,7 +469,8 @@ hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, c
                               uint8_t *arena, uint32_t *place_cid, uint32_t *place_pos, const GxPlace &gx,
                               hipStream_t st)
 {
-    if (gx.x3) (void)hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st);
+    if (gx.x3)
+        if (hipError_t e = hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st)) return e;
     hipLaunchKernelGGL(place_kernel, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst, offsets, flags, pre,
                        rstate, events, slot, tab, arena, place_cid, place_pos, gx);
     return hipGetLastError();
