@@ -75,12 +75,16 @@ def parse():
                          "off, so a rocprof summary of the default bench holds only the timed pipeline's kernels)")
     ap.add_argument("--keep-recipes", type=int, default=1,
                     help="storeDB's recipe SET per block into the device recipe store (default 1, as the reference)")
-    ap.add_argument("--depth", type=int, default=2, help="batches in flight (1..3, pipelined mode)")
+    ap.add_argument("--depth", type=int, default=0,
+                    help="batches in flight (1..3, pipelined mode; default 2, config4 3: the LZ4 passes of two "
+                         "batches overlap while the third batch's front half runs)")
     ap.add_argument("--alone", action="store_true",
                     help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
                          "batches (off by default so a rocprof summary of the bench matches its in-pipeline averages)")
-    ap.add_argument("--arena-slots", type=int, default=512,
-                    help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers")
+    ap.add_argument("--arena-slots", type=int, default=0,
+                    help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers "
+                         "(default 512; config4 1280, so a ring also holds the closes of the batch whose LZ4 "
+                         "pass is still running: two batches' LZ4 passes overlap)")
     ap.add_argument("--packet-kib", type=int, default=0,
                     help="config5: deliver every block as packets of this many KiB (hdrf_rx_begin / "
                          "hdrf_append_packet / hdrf_submit_slot, one block per submit: the JNI shape); "
@@ -93,6 +97,14 @@ def parse():
 
 def main():
     a = parse()
+    if not a.depth:
+        a.depth = 3 if a.workload == "config4" else 2
+    if not a.arena_slots:
+        a.arena_slots = 1280 if a.workload == "config4" else 512
+    if a.workload == "config4":
+        # two LZ4 streams beside the four of the batch pipeline: hardware queues for all six (HIP's
+        # default is 4, and streams sharing a queue serialise); read when HIP initialises
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -88,6 +88,9 @@ struct Slot {
     int nblocks = 0;
     bool pending = false;
     uint32_t close_bound = 0;                 // durable containers: closes this batch may make per range
+    uint32_t lz_bound = 0;                    // compressor 2: closes this batch may make per range (LZ4 lag)
+    hipEvent_t placed = nullptr;              // compressor 2: the batch's place kernel finished (stream B)
+    hipEvent_t lz_done = nullptr;             // compressor 2: its closed containers are Lz4Codec files
     int rx_release = -1;                      // packet path: receive buffer to free when the batch completes
     uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
     RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
@@ -109,8 +112,7 @@ struct hdrf_ctx {
     hipStream_t stB = nullptr;   // stream B: back stage (index + store)
     hipStream_t stW = nullptr;   // stream W: chunking stage
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
-    hipStream_t stL = nullptr;   // LZ4 side stream (short last segments beside the main kernel)
-    hipEvent_t lz_fork = nullptr, lz_join = nullptr;
+    hipStream_t stL[2] = {};     // compressor 2: LZ4 streams, alternating by batch (off stream B)
     int max_batch = 0, cap_blk = 0, ntiles = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
     Slot sl[kSlots];
     uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
@@ -289,7 +291,7 @@ static void free_slot(Slot &S)
     void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_closed, S.h_filelen, S.h_desc};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
-    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done};
+    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done, S.placed, S.lz_done};
     if (S.d_rjobs) (void)hipFree(S.d_rjobs);
     if (S.h_rjobs) (void)hipHostFree(S.h_rjobs);
     if (S.d_hstage) (void)hipFree(S.d_hstage);
@@ -319,14 +321,13 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
     if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
-    if (ctx->stL) (void)hipStreamDestroy(ctx->stL);
+    for (auto L : ctx->stL)
+        if (L) (void)hipStreamDestroy(L);
     for (auto &r : ctx->rx)
         if (r.d) (void)hipFree(r.d);
     if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
     for (auto &e : ctx->ring_ev)
         if (e) (void)hipEventDestroy(e);
-    if (ctx->lz_fork) (void)hipEventDestroy(ctx->lz_fork);
-    if (ctx->lz_join) (void)hipEventDestroy(ctx->lz_join);
 }
 
 static int alloc_slot(hdrf_ctx *ctx, Slot &S)
@@ -372,7 +373,9 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         hipEventCreateWithFlags(&S.copy_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.recipe_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.front_done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.placed, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.lz_done, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
     for (auto &e : S.evW)
         if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
@@ -393,7 +396,7 @@ static int drain(hdrf_ctx *ctx)
     while (ctx->nwait < ctx->nsub)
         if (int r = wait_one(ctx)) rc = rc ? rc : r;
     HIPCK(hipStreamSynchronize(ctx->stC));
-    HIPCK(hipStreamSynchronize(ctx->stL));
+    for (auto L : ctx->stL) HIPCK(hipStreamSynchronize(L));
     HIPCK(hipStreamSynchronize(ctx->stW));
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
@@ -478,9 +481,8 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         hipStreamCreateWithPriority(&ctx->stB, hipStreamNonBlocking, pb) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pa) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stL, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->lz_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->lz_join, hipEventDisableTiming) != hipSuccess) {
+        hipStreamCreateWithFlags(&ctx->stL[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stL[1], hipStreamNonBlocking) != hipSuccess) {
         free_all(ctx);
         delete ctx;
         return HDRF_E_HIP;
@@ -749,21 +751,47 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     // place wants full occupancy).  HDRF_PLACE_LDS overrides the reservation (bytes).
     static const int place_lds = [] { const char *e = getenv("HDRF_PLACE_LDS"); return e ? atoi(e) : 40960; }();
     if (ctx->nsub > ctx->nwait) P.place_lds = place_lds;
+    if (c.compressor == 2) {
+        // The compression of earlier batches runs on the LZ4 streams, off stream B, so batch k+1's
+        // index and store overlap batch k's LZ4 and the LZ4 passes of consecutive batches overlap
+        // each other (no per-batch tail on the critical chain).  A place kernel may reopen an arena
+        // slot only after the LZ4 pass reading it finished: a slot closed in batch j is reopened
+        // at the (arena_slots/4)-th open of its ring after it, and a batch opens at most as many
+        // containers per range as it closes (close_bound), so stream B waits for an in-flight
+        // batch's LZ4 only when the closes bound from it up to this batch could wrap the ring.
+        uint64_t bytes = 0;
+        for (int b = 0; b < nblocks; b++) bytes += len[b];
+        S.lz_bound = close_bound(c, bytes);
+        const uint64_t per = (uint64_t)(c.arena_slots / 4);
+        uint64_t sum = S.lz_bound;
+        for (uint64_t j = ctx->nsub - 1; j + 1 > ctx->nwait; j--) {   // in flight, newest first
+            const Slot &Pj = ctx->sl[j % kSlots];
+            sum += Pj.lz_bound;
+            if (sum + 1 >= per) HIPCK(hipStreamWaitEvent(Bst, Pj.lz_done, 0));
+            if (j == 0) break;
+        }
+    }
     HIPCK(launch_store(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_pre,
                        ctx->d_alloc, S.d_rstate, S.d_ev, S.d_closed, S.d_nclosed, S.d_slot, ctx->d_tab, ctx->d_arena,
                        S.d_pcid, S.d_ppos, S.d_err, Bst, &mb));
-    if (c.compressor == 2)      // compression stage: closed containers -> Lz4Codec files (:770-779)
+    if (c.compressor == 2) {    // compression stage: closed containers -> Lz4Codec files (:770-779)
+        hipStream_t L = ctx->stL[cur & 1];
+        HIPCK(hipEventRecord(S.placed, Bst));
+        HIPCK(hipStreamWaitEvent(L, S.placed, 0));
         HIPCK(launch_lz4(S.d_closed, S.d_nclosed, ctx->closed_cap, c.container_max, ctx->d_arena, ctx->d_carena,
-                         ctx->cslot, S.d_segclen, S.d_filelen, Bst, ctx->stL, ctx->lz_fork, ctx->lz_join));
-    mb.mark(Bst);
+                         ctx->cslot, S.d_segclen, S.d_filelen, L));
+        mb.mark(L);
+        HIPCK(hipMemcpyAsync(S.h_filelen, S.d_filelen, sizeof(uint32_t) * ctx->closed_cap, hipMemcpyDeviceToHost, L));
+        HIPCK(hipEventRecord(S.lz_done, L));
+    } else {
+        mb.mark(Bst);
+    }
     HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nblocks, hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nblocks, hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, Bst));
-    if (c.compressor == 2)
-        HIPCK(hipMemcpyAsync(S.h_filelen, S.d_filelen, sizeof(uint32_t) * ctx->closed_cap, hipMemcpyDeviceToHost, Bst));
     HIPCK(hipEventRecord(S.back_done, Bst));
     S.pending = true;
     ctx->nsub++;
@@ -899,6 +927,7 @@ static int wait_one(hdrf_ctx *ctx)
     ctx->nwait++;
     S.pending = false;
     HIPCK(hipEventSynchronize(S.back_done));
+    if (ctx->cfg.compressor == 2) HIPCK(hipEventSynchronize(S.lz_done));
     if (S.rx_release >= 0) {                           // its receive buffer is free again
         ctx->rx[S.rx_release].state = 0;
         ctx->rx[S.rx_release].len = 0;

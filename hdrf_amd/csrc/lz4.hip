@@ -338,9 +338,10 @@ last_literals:
 }
 
 
-// grid (nseg_max, nclosed) x 64 threads: segment s of closed container c.  Two instances: byU32
-// segments with a 12 KiB table (every 261,100-B segment), byU16 ones (a container's short last
-// segment) with 16 KiB; each returns at once for the other kind.
+// 64 threads per segment.  Two instances: byU32 segments with the 9 KiB table (every 261,100-B
+// segment; grid (nseg_max, closed_cap), segment s of closed container c), and byU16 ones with
+// 16 KiB (a container's short last segment; grid (1, closed_cap)); each returns at once for the
+// other kind.
 template <bool kSmall>
 __global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed,
                                                      const uint32_t *__restrict__ nclosed, const uint8_t *__restrict__ arena,
@@ -348,9 +349,10 @@ __global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict
                                                      uint32_t *__restrict__ seg_clen, int nseg_max)
 {
     __shared__ __attribute__((aligned(16))) uint8_t tabmem[kSmall ? kLzTabU16 : kLzTabU32];
-    const int c = blockIdx.y, s = blockIdx.x;
+    const int c = blockIdx.y;
     if ((uint32_t)c >= *nclosed) return;                   // grid sized for closed_cap
     const ClosedRec r = closed[c];
+    const int s = kSmall ? (r.len ? (int)((r.len - 1) / kLzMaxIn) : 0) : (int)blockIdx.x;
     const int64_t off = (int64_t)s * kLzMaxIn;
     if (off >= (int64_t)r.len) return;
     const int n = (int)min((int64_t)kLzMaxIn, (int64_t)r.len - off);
@@ -571,21 +573,17 @@ uint64_t lz4_piece_stride() { return kLzSegStride; }
 
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
                       const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
-                      hipStream_t st, hipStream_t side, hipEvent_t fork, hipEvent_t join)
+                      hipStream_t st)
 {
-    // grid covers closed_cap containers; workgroups past the device-side count exit at once, so
+    // grids cover closed_cap containers; workgroups past the device-side count exit at once, so
     // the compression stays in stream order with the batch (no host round trip).  The short last
-    // segments (16 KiB tables, a few dozen waves) run on the side stream beside the main kernel.
+    // segments (16 KiB tables, at most one per container) go first: the main kernel's tail then
+    // overlaps the next batch's LZ4 pass on the other LZ4 stream instead of this small launch.
     const int nseg_max = (int)((cmax + kLzMaxIn - 1) / kLzMaxIn);
-    hipError_t e = hipEventRecord(fork, st);
-    if (e == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(lz4_seg_kernel<true>, dim3(nseg_max, closed_cap), dim3(64), 0, side, closed, nclosed, arena,
+    hipLaunchKernelGGL(lz4_seg_kernel<true>, dim3(1, closed_cap), dim3(64), 0, st, closed, nclosed, arena,
                        (uint64_t)cmax, carena, cslot, seg_clen, nseg_max);
-    if ((e = hipEventRecord(join, side)) != hipSuccess) return e;
     hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(nseg_max, closed_cap), dim3(64), 0, st, closed, nclosed, arena,
                        (uint64_t)cmax, carena, cslot, seg_clen, nseg_max);
-    if ((e = hipStreamWaitEvent(st, join, 0)) != hipSuccess) return e;
     hipLaunchKernelGGL(lz4_pack_kernel, dim3(closed_cap), dim3(256), 0, st, closed, nclosed, carena, cslot, seg_clen,
                        nseg_max, file_len);
     return hipGetLastError();

@@ -109,3 +109,41 @@ def test_config4_mixed_corpus_full_blocks():
     compare_state(ctx, ora, ids, tag="config4")
     ctx.dev_free(dev)
     ctx.close()
+
+
+@pytest.mark.parametrize("arena_slots", [16, 64])
+def test_config4_lz4_passes_overlap_across_batches(arena_slots):
+    """Compressor 2 with the LZ4 pass of each batch on its own stream (alternating by batch), three
+    batches in flight: batch k+1's place kernel reopens arena slots while batch k's LZ4 pass may
+    still read its closed containers.  With 16 slots (4 per storer ring) the ring can wrap within
+    the batches in flight, so stream B waits for the older LZ4 passes; with 64 it cannot, and the
+    passes run concurrently.  Every container file, index value and recipe matches the oracle."""
+    nb, seg, seed = 9, 1 << 20, 99
+    size = 4 << 20
+    roots = corpus_roots(seed, 400000, nb, size // seg)
+    cmax = 4 << 20
+    ctx = Context(max_block_bytes=size, max_batch_blocks=1, index_log2=20, arena_slots=arena_slots,
+                  container_max=cmax, compressor=2)
+    ora = Oracle(compressor=2, max_size=cmax)
+    total = nb * size + 4096
+    dev = ctx.dev_alloc(total)
+    ctx.corpus_fill(dev, roots, nb, size // seg, seg, seed, mixed=True)
+    blocks = [ctx.d2h(dev + b * size, size) for b in range(nb)]
+    ids = [900 + b for b in range(nb)]
+    pend = []
+    for b in range(nb):
+        ctx.submit_batch([dev + b * size], [size], [total - b * size], [ids[b]])
+        pend.append(b)
+        if len(pend) == 3:
+            ctx.wait_batch()
+            d = pend.pop(0)
+            compare_block(ctx.batch_result(0), ora.reduce(blocks[d], ids[d]), tag=f"lz4 overlap block {d}")
+    while pend:
+        ctx.wait_batch()
+        d = pend.pop(0)
+        compare_block(ctx.batch_result(0), ora.reduce(blocks[d], ids[d]), tag=f"lz4 overlap block {d}")
+    st = ctx.stats()
+    assert st["closed_containers"] >= 3
+    compare_state(ctx, ora, ids, tag=f"lz4 overlap {arena_slots}")
+    ctx.dev_free(dev)
+    ctx.close()
