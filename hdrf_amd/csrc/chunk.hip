@@ -471,6 +471,7 @@ __device__ __forceinline__ bool walk_chain(const WalkCfg &c, int p, bool first, 
 //     speculative walk that reads every byte; it is HBM-bound.
 constexpr int kGmPerWg = 4096;           // granules per workgroup (64 KiB of data, 16 per thread)
 
+template <bool NT>
 __global__ void __launch_bounds__(256) gmax_kernel(const BlockDesc *__restrict__ blocks, uint8_t *__restrict__ gm,
                                                    int gstride)
 {
@@ -484,7 +485,7 @@ __global__ void __launch_bounds__(256) gmax_kernel(const BlockDesc *__restrict__
     uint4 v[16];
     if ((g0 + kGmPerWg) * 16 <= (int64_t)bd.readable) {
 #pragma unroll
-        for (int i = 0; i < 16; i++) v[i] = ld16(base + (g0 + 256 * i + t) * 16);
+        for (int i = 0; i < 16; i++) v[i] = ld16_t<NT>(base + (g0 + 256 * i + t) * 16);
     } else {
 #pragma unroll
         for (int i = 0; i < 16; i++) {
@@ -1124,7 +1125,10 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     if (e == hipSuccess) e = hipMemsetAsync(X.irr, 0, sizeof(uint32_t) * (size_t)(nsegs / 32 + 2), st);
     if (e != hipSuccess) return e;
     const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
-    hipLaunchKernelGGL(gmax_kernel, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm, X.gstride);
+    if (stream_knobs() & 1)
+        hipLaunchKernelGGL(gmax_kernel<true>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm, X.gstride);
+    else
+        hipLaunchKernelGGL(gmax_kernel<false>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm, X.gstride);
     mk->mark(st);
     hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), 0, st, d_blocks, nblocks, total_waves,
                        X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err);

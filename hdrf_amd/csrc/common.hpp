@@ -158,6 +158,15 @@ __device__ __forceinline__ uint4 ld16(const void *p)
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ uint32_t ld4(const void *p) { return *(const HDRF_GLOBAL uint32_t *)(p); }
+// streaming (nontemporal) 16-B load / store: bytes read or written once, kept from displacing
+// the lines other stages re-read in L2 (granule maxima, SHA pairs, index entries, LZ4 windows)
+__device__ __forceinline__ uint4 ld16_nt(const void *p)
+{
+    const u32x4v v = __builtin_nontemporal_load((const HDRF_GLOBAL u32x4v *)(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <bool NT>
+__device__ __forceinline__ uint4 ld16_t(const void *p) { return NT ? ld16_nt(p) : ld16(p); }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // wave index inside the workgroup, as a provably wave-uniform (scalar) value
@@ -220,11 +229,12 @@ __device__ __noinline__ uint32_t load4_guard(const uint8_t *base, int64_t off, i
 
 // 16 output bytes from an arbitrarily aligned source: two aligned 16-B loads + a funnel shift by
 // sh = src & 15 (uniform per run, since destination words are 16-B aligned within a run).
+template <bool NT = false>
 __device__ __forceinline__ uint4 load16_shift(const uint8_t *src_aligned, int sh)
 {
-    const uint4 x = ld16(src_aligned);
+    const uint4 x = ld16_t<NT>(src_aligned);
     if (sh == 0) return x;
-    const uint4 y = ld16(src_aligned + 16);
+    const uint4 y = ld16_t<NT>(src_aligned + 16);
     const uint32_t r = (uint32_t)(sh & 3);
 #define AB(hi, lo) __builtin_amdgcn_alignbyte((hi), (lo), r)
     switch (sh >> 2) {                                   // uniform per run
@@ -241,5 +251,14 @@ __device__ __forceinline__ void st16(void *p, uint4 v)
     u32x4v w = {v.x, v.y, v.z, v.w};
     *(HDRF_GLOBAL u32x4v *)p = w;
 }
+template <bool NT>
+__device__ __forceinline__ void st16_t(void *p, uint4 v)
+{
+    u32x4v w = {v.x, v.y, v.z, v.w};
+    if (NT) __builtin_nontemporal_store(w, (HDRF_GLOBAL u32x4v *)p);
+    else *(HDRF_GLOBAL u32x4v *)p = w;
+}
+// streaming-knob bits (HDRF_NT): 1 = granule-max pass loads, 2 = place copy loads + stores
+int stream_knobs();   // default 3 (measured +1.5 % on the config-2 bench); HDRF_NT=0 turns both off
 
 }  // namespace hdrf

@@ -45,6 +45,21 @@ __device__ __forceinline__ int put_len(uint8_t *out, int op, int len)
 constexpr int kLzTabU16 = 16384;
 constexpr int kLzTabU32 = 9216;
 
+#ifdef HDRF_LZ4_PROF
+// profiling build only (scripts/r02_lzp.sh): shader-clock time per parse phase, summed over waves
+__device__ unsigned long long g_lzprof[16];
+#define LZP_INIT uint64_t lzp_t = __builtin_amdgcn_s_memtime(); uint64_t lzp_a[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint32_t lzp_n[4] = {0, 0, 0, 0};
+#define LZP(i) { const uint64_t t_ = __builtin_amdgcn_s_memtime(); lzp_a[i] += t_ - lzp_t; lzp_t = t_; }
+#define LZN(i) (lzp_n[i]++)
+#define LZP_FLUSH if (lane_id() == 0) { for (int i_ = 0; i_ < 8; i_++) atomicAdd(&g_lzprof[i_], (unsigned long long)lzp_a[i_]); \
+                                        for (int i_ = 0; i_ < 4; i_++) atomicAdd(&g_lzprof[8 + i_], (unsigned long long)lzp_n[i_]); }
+#else
+#define LZP_INIT
+#define LZP(i)
+#define LZN(i)
+#define LZP_FLUSH
+#endif
+
 // One LZ4 block (lz4 r123 LZ4_compress, noDict): returns the compressed size.  Uniform control
 // flow; `tabmem` is this wave's LDS hash table (layout above).
 __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out, uint8_t *tabmem)
@@ -85,6 +100,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
 
     const int mflimit = n - kMfLimit, matchlimit = n - kLastLit;
     int op = 0, anchor = 0, ip = 0;
+    LZP_INIT
     if (n >= kMfLimit + 1) {
         if (l == 0) tput(hash(rd32u(src)), 0);        // first byte
         ip = 1;
@@ -162,6 +178,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             const uint32_t cv = rd32u(src + ref);          // ref is a position < n in every lane
             const bool ok = valid && ref + kMaxDist >= ipl && cv == v;
             const unsigned long long okm = ballot64(ok);
+            LZN(0);
             {                                             // commit: attempts up to the first match
                 const int last = okm ? __builtin_ctzll(okm) : 63;
                 const unsigned long long upto = last == 63 ? ~0ull : ((2ull << last) - 1ull);
@@ -169,7 +186,9 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 if (valid && l <= last && !later) tput(h, ipl);
                 asm volatile("" ::: "memory");
             }
+            LZP(0);
             if (okm) {
+                LZN(1);
                 const int istar = __builtin_ctzll(okm);
                 asm volatile("" ::: "memory");
                 ip = (int)rdlane((uint32_t)ipl, istar);
@@ -227,6 +246,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     op += lit;
                     have = false;
                 }
+                LZP(1);
                 for (;;) {                                 // _next_match
                     // the parse state is wave-uniform: keep it in scalar registers so the
                     // branches on it are scalar branches, not exec-mask regions
@@ -254,6 +274,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         mref = ip + dr;
                         break;
                     }
+                    LZP(2);
                     int ml = ip - anchor;
                     if (ml >= 15) {
                         tok += 15;
@@ -296,9 +317,13 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         r = (int)rdlane((uint32_t)r, 1);
                     }
                     asm volatile("" ::: "memory");
+                    LZP(3);
                     if (r + kMaxDist >= ip) {
                         const uint32_t Cw = wload(r);      // one round trip
-                        if (rdlane(Cw, 0) == v0) {
+                        const bool chain = rdlane(Cw, 0) == v0;
+                        LZP(4);
+                        if (chain) {
+                            LZN(2);
                             mref = r;
                             tpos = op++;
                             tok = 0;
@@ -322,6 +347,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         }
     }
 last_literals:
+    LZP(5);
     {
         int run = n - anchor;
         const int tpos = op++;
@@ -334,6 +360,8 @@ last_literals:
         wave_copy(out + op, src + anchor, run);
         op += run;
     }
+    LZP(6);
+    LZP_FLUSH
     return op;
 }
 
@@ -427,6 +455,18 @@ __global__ void __launch_bounds__(256) lz4_pack_kernel(const ClosedRec *__restri
     if (r.len == 0) pos = 4;
     if (t == 0) file_len[c] = pos;
 }
+
+#ifdef HDRF_LZ4_PROF
+extern "C" int hdrf_debug_lz4_prof(unsigned long long *out16, int reset)
+{
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_lzprof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_lzprof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 uint64_t lz4_slot_bytes(uint32_t cmax)
 {

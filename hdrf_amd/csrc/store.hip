@@ -300,6 +300,7 @@ __global__ void __launch_bounds__(256) fn_chain_kernel(StoreParams P, const uint
 }
 
 // workgroup-cooperative copy of one contiguous run (16-B aligned destination stores)
+template <bool NT>
 __device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32_t len)
 {
     const int t = threadIdx.x;
@@ -313,17 +314,18 @@ __device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32
     const uint8_t *sa = sp - sh;
     uint32_t i = t;
     for (; i + 256 < n16; i += 512) {               // two 16-B words per thread in flight
-        const uint4 v0 = load16_shift(sa + 16 * (size_t)i, sh);
-        const uint4 v1 = load16_shift(sa + 16 * (size_t)(i + 256), sh);
-        st16(d + 16 * (size_t)i, v0);
-        st16(d + 16 * (size_t)(i + 256), v1);
+        const uint4 v0 = load16_shift<NT>(sa + 16 * (size_t)i, sh);
+        const uint4 v1 = load16_shift<NT>(sa + 16 * (size_t)(i + 256), sh);
+        st16_t<NT>(d + 16 * (size_t)i, v0);
+        st16_t<NT>(d + 16 * (size_t)(i + 256), v1);
     }
-    for (; i < n16; i += 256) st16(d + 16 * (size_t)i, load16_shift(sa + 16 * (size_t)i, sh));
+    for (; i < n16; i += 256) st16_t<NT>(d + 16 * (size_t)i, load16_shift<NT>(sa + 16 * (size_t)i, sh));
     const uint32_t tb = head + 16 * n16;
     if ((uint32_t)t < len - tb) dst[tb + t] = src[tb + t];
 }
 
 // ---- place: grid (ntiles, nblocks) ------------------------------------------------------
+template <bool NT>
 __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDesc *__restrict__ blocks,
                                                     const BlockState *__restrict__ bst,
                                                     const uint32_t *__restrict__ offsets,
@@ -428,8 +430,15 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
     __syncthreads();
     for (uint32_t r = 0; r < nruns; r++) {
         const uint64_t dsto = ((uint64_t)r_dst_hi[r] << 32) | r_dst_lo[r];
-        wg_copy(arena + dsto, bd.data + r_src[r], r_end[r] - r_src[r]);
+        wg_copy<NT>(arena + dsto, bd.data + r_src[r], r_end[r] - r_src[r]);
     }
+}
+
+int stream_knobs()
+{
+    // r02 A/B on the config-2 bench (scripts/ab_nt.txt): 973 / 984 GB/s off, 994 / 995 with both
+    static const int k = [] { const char *e = getenv("HDRF_NT"); return e ? atoi(e) : 3; }();
+    return k;
 }
 
 hipError_t launch_store_scan(const StoreParams &P, const BlockState *bst, const uint32_t *offsets, const uint8_t *flags,
@@ -471,8 +480,12 @@ hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, c
 {
     if (gx.x3)
         if (hipError_t e = hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st)) return e;
-    hipLaunchKernelGGL(place_kernel, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst, offsets, flags, pre,
-                       rstate, events, slot, tab, arena, place_cid, place_pos, gx);
+    if (stream_knobs() & 2)
+        hipLaunchKernelGGL(place_kernel<true>, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst,
+                           offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx);
+    else
+        hipLaunchKernelGGL(place_kernel<false>, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst,
+                           offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx);
     return hipGetLastError();
 }
 
