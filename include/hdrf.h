@@ -95,13 +95,15 @@ int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_
                       const uint64_t *readable, const uint64_t *block_ids);
 
 /* Pipelined form of hdrf_reduce_batch: hdrf_submit_batch enqueues the batch (chunking, SHA and
- * index + store on three HIP streams, in block order) and returns; hdrf_wait_batch completes the
+ * index + store on three HIP streams, in block order; under compressor 2 the batch's LZ4 pass runs
+ * on one of two LZ4 streams, so consecutive batches' passes overlap) and returns; hdrf_wait_batch
+ * completes the
  * OLDEST submitted batch and makes it the one hdrf_batch_* report.  At most HDRF_PIPELINE_DEPTH
  * batches are in flight: a submit beyond that returns HDRF_E_CAPACITY (call hdrf_wait_batch
  * first), so every submit pairs with exactly one wait.  The device buffers of a batch must stay
  * valid until it is completed.  Chunking of batch k+1 overlaps hashing of batch k and the
  * index/store stage of batch k-1 (latency-bound walk, VALU-bound SHA, HBM-bound store); the
- * bench keeps two batches in flight.  Views (index, containers, allocator) complete all batches
+ * bench keeps two batches in flight (three under compressor 2).  Views (index, containers, allocator) complete all batches
  * first. */
 #define HDRF_PIPELINE_DEPTH 3
 int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,

@@ -1,4 +1,6 @@
-"""World-size-2 gloo worker for tests/test_node.py::test_exchange_gloo_cpu_world2 (CPU only)."""
+"""Exchange worker for tests/test_node.py: world-size-2 gloo on CPU tensors
+(test_exchange_gloo_cpu_world2), or the RCCL branch on GPU tensors (HDRF_XW_BACKEND=nccl,
+test_exchange_rccl_gpu: list all_to_all, all_gather, send/recv and broadcast over RCCL)."""
 import os
 import sys
 
@@ -12,9 +14,17 @@ from hdrf_amd.node import Exchange  # noqa: E402
 
 
 def main():
-    dist.init_process_group("gloo")
+    nccl = os.environ.get("HDRF_XW_BACKEND") == "nccl"
+    dev = None
+    if nccl:
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
     r, G = dist.get_rank(), dist.get_world_size()
-    xc = Exchange(G, r, None)
+    xc = Exchange(G, r, dev)
+    assert xc.nccl == nccl
     cap, w = 50, 3
     send = torch.full((G * cap * w,), -1, dtype=torch.int32)
     counts = np.array([(r * 7 + d * 3) % 11 + d for d in range(G)], np.int64)
@@ -25,7 +35,10 @@ def main():
     expect_rc = np.array([(s * 7 + r * 3) % 11 + r for s in range(G)], np.int64)
     assert np.array_equal(rc, expect_rc), (rc, expect_rc)
     recv = torch.full((G * cap * w,), -1, dtype=torch.int32)
+    if nccl:
+        send, recv = send.to(dev), recv.to(dev)
     xc.records(send, recv, counts, rc, cap, w)
+    recv = recv.cpu()
     for s in range(G):
         for i in range(int(rc[s])):
             got = recv[(s * cap + i) * w:(s * cap + i + 1) * w].tolist()
@@ -44,7 +57,7 @@ def main():
     # descriptors of different lengths for the allocator scan
     got = xc.all_gather_i64(np.arange(3 + 5 * r, dtype=np.int64) * (r + 1))
     assert [g.tolist() for g in got] == [(np.arange(3 + 5 * q) * (q + 1)).tolist() for q in range(G)], got
-    print("exchange ok", r, flush=True)
+    print("exchange ok", r, "nccl" if nccl else "gloo", flush=True)
     dist.destroy_process_group()
 
 

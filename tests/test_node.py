@@ -190,3 +190,18 @@ def test_exchange_gloo_cpu_world2():
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("exchange ok") == 2, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_exchange_rccl_gpu():
+    """The RCCL branch of hdrf_amd.node.Exchange (backend "nccl" is RCCL on ROCm) on device
+    tensors: counts (all_to_all_single), variable-length record regions (list all_to_all), the
+    allocator hand-off (broadcast; send/recv need a second rank) and the all-gather of scan
+    descriptors.  One GPU here, so world size 1 (every exchange is the rank's own region); the
+    8-GPU node run is the driver's."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+           "--master-port", "29643", os.path.join(ROOT, "tests", "exchange_worker.py")]
+    env = dict(os.environ, PYTHONPATH=ROOT, HDRF_XW_BACKEND="nccl")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("exchange ok 0 nccl") == 1, r.stdout[-2000:]
