@@ -34,12 +34,14 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_WI_NS = 1033.0       # v_add_u32 wave-instructions/ns, chip-wide (tools/valu_peak.hip)
 KERNEL_OF = {"gmax(gmax_kernel)": "gmax_kernel", "walk(lane_walk_kernel)": "lane_walk_kernel",
              "sha_full(sha_full_kernel)": "sha_full_kernel", "place(place_kernel)": "place_kernel"}
-# stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index + store
+# stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index + store,
+# L the LZ4 pass of closed containers (compressor 2; two LZ4 streams alternating by batch)
 CHAINS = {"W: chunking": ["gmax(gmax_kernel)", "walk(lane_walk_kernel)", "stitch(repair/path/count/scan/copy/fallback)"],
           "A: SHA": ["sha_full(sha_full_kernel)", "sha_tail(sha_tail_kernel)"],
           "B: index+store": ["index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
                              "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
-                             "place(place_kernel)", "compress(lz4_seg/lz4_pack)"]}
+                             "place(place_kernel)"],
+          "L: LZ4": ["compress(lz4_seg/lz4_pack)"]}
 SHA_MIX_CEILING_WI_NS = 425.0  # tools/sha_peak.hip: the SHA-1 instruction mix on register-resident data
 
 
@@ -76,8 +78,8 @@ def parse():
     ap.add_argument("--keep-recipes", type=int, default=1,
                     help="storeDB's recipe SET per block into the device recipe store (default 1, as the reference)")
     ap.add_argument("--depth", type=int, default=0,
-                    help="batches in flight (1..3, pipelined mode; default 2, config4 3: the LZ4 passes of two "
-                         "batches overlap while the third batch's front half runs)")
+                    help="batches in flight (1..5, pipelined mode; default 2; config4 5: the LZ4 passes of two "
+                         "batches overlap while the front halves of the next ones run)")
     ap.add_argument("--alone", action="store_true",
                     help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
                          "batches (off by default so a rocprof summary of the bench matches its in-pipeline averages)")
@@ -98,7 +100,7 @@ def parse():
 def main():
     a = parse()
     if not a.depth:
-        a.depth = 3 if a.workload == "config4" else 2
+        a.depth = 5 if a.workload == "config4" else 2
     if not a.arena_slots:
         a.arena_slots = 1280 if a.workload == "config4" else 512
     if a.workload == "config4":
@@ -328,12 +330,28 @@ def main():
                        "frac_of_mix_ceiling": round(wi_ns / SHA_MIX_CEILING_WI_NS, 4),
                        "sq_insts_valu_per_launch": int(sha_prof["sq_insts_valu"])}
     place = hbm_entry(STAGES[9])
+    lz4 = None
+    if mixed:
+        # the LZ4 pass per batch: closed containers read + Lz4Codec files written, over the stage's
+        # average time from the place kernel's end to the pack kernel's end on its LZ4 stream (two
+        # batches' passes overlap, so this is a latency, not an exclusive share of the GPU)
+        st = ctx.stats()
+        lz_ms = avg["compress(lz4_seg/lz4_pack)"]
+        lz_bytes = (st["closed_raw_bytes"] + st["closed_file_bytes"]) / max(1, nbatch)   # stats: since the last reset = one step
+        ach = lz_bytes / (lz_ms * 1e-3) / 1e9 if lz_ms > 0 else 0.0
+        lz4 = {"bound": "hbm", "kernel": "lz4_seg_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+               "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(lz_ms, 4),
+               "algorithmic_bytes_per_launch": int(lz_bytes), "traffic": None,
+               "limiter": "per-sequence dependent instruction chain of the greedy parse (one wave per 261,100-B "
+                          "segment, LDS table caps 17 waves/CU); profiles/r02_lz4_phases.txt"}
     # the line's roofline: the dominant kernel of the critical chain
-    top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place}[crit]
+    top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place, "L: LZ4": lz4}[crit]
     roofline = dict(top)
     roofline.update({"traffic_source": pmc_src, "critical_path": crit, "chains_ms_per_batch": chains,
                      "batch_period_ms": round(el / a.steps / nbatch * 1e3, 4),
                      "chunking": chunking, "sha": sha, "place": place})
+    if lz4:
+        roofline["lz4"] = lz4
     if alone_ms is not None:
         # per-kernel figures of the untimed serial pass (not part of `value`)
         ra = {}

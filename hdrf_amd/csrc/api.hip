@@ -33,7 +33,7 @@ namespace {
 
 constexpr int kStages = hdrf::kNumStages;
 constexpr uint64_t kSlack = 64;   // readable bytes required past each block end
-constexpr int kSlots = 3;         // batches in flight (walk | SHA | index+store)
+constexpr int kSlots = 5;         // batches in flight (walk | SHA | index+store | LZ4 passes)
 constexpr int kErrCapacity = 2 | 4 | 8 | 16 | 32;  // device error bits that mean "a buffer is too small"
 
 struct ContainerInfo {
@@ -73,6 +73,7 @@ struct Slot {
     uint32_t *d_coll = nullptr, *d_ncoll = nullptr;
     uint32_t *d_pcid = nullptr, *d_ppos = nullptr, *d_queue = nullptr;
     uint32_t *d_segclen = nullptr, *d_filelen = nullptr;
+    uint32_t *d_lzwork = nullptr;             // compressor 2: the LZ4 pass's two item counters
     int *d_err = nullptr;
     // pinned read-back, filled by stream B before back_done
     BlockState *h_bst = nullptr;
@@ -285,7 +286,8 @@ static void free_slot(Slot &S)
 {
     void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
                    S.d_pre, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
-                   S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err};
+                   S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err,
+                   S.d_lzwork};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_closed, S.h_filelen, S.h_desc};
@@ -366,7 +368,8 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         (rc = halloc(ctx, &S.h_desc, B)))
         return rc;
     if (c.compressor == 2 && ((rc = dalloc(ctx, &S.d_segclen, (size_t)ctx->closed_cap * nseg_lz)) ||
-                              (rc = dalloc(ctx, &S.d_filelen, (size_t)ctx->closed_cap))))
+                              (rc = dalloc(ctx, &S.d_filelen, (size_t)ctx->closed_cap)) ||
+                              (rc = dalloc(ctx, &S.d_lzwork, 2))))
         return rc;
     if ((rc = dalloc(ctx, &S.d_rjobs, B)) || (rc = halloc(ctx, &S.h_rjobs, B))) return rc;
     if (hipEventCreateWithFlags(&S.walk_done, hipEventDisableTiming) != hipSuccess ||
@@ -779,7 +782,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         HIPCK(hipEventRecord(S.placed, Bst));
         HIPCK(hipStreamWaitEvent(L, S.placed, 0));
         HIPCK(launch_lz4(S.d_closed, S.d_nclosed, ctx->closed_cap, c.container_max, ctx->d_arena, ctx->d_carena,
-                         ctx->cslot, S.d_segclen, S.d_filelen, L));
+                         ctx->cslot, S.d_segclen, S.d_filelen, S.d_lzwork, L));
         mb.mark(L);
         HIPCK(hipMemcpyAsync(S.h_filelen, S.d_filelen, sizeof(uint32_t) * ctx->closed_cap, hipMemcpyDeviceToHost, L));
         HIPCK(hipEventRecord(S.lz_done, L));

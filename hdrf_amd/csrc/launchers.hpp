@@ -165,7 +165,7 @@ hipError_t launch_snappy_decode(const LzDec *items, int n, const uint8_t *src, u
 uint64_t lz4_slot_bytes(uint32_t cmax);
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
                       const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
-                      hipStream_t st);
+                      uint32_t *work, hipStream_t st);
 // read side (read.hip): lookup + scan (gather = false), then the copy (gather = true)
 size_t rd_chunk_bytes();
 hipError_t launch_gx_locate(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,

@@ -17,6 +17,9 @@
 //     writes are replayed lane by lane in attempt order and the writes after the match undone;
 //   * match extension, catch-up and literal copies are 64-lane compares / 16-B-per-lane copies.
 //   lz4_pack then frames the segments ([BE32 len] ([BE32 clen] block)* [BE32 0]) in place.
+#include <algorithm>
+#include <cstdlib>
+
 #include "bytes.hpp"
 
 namespace hdrf {
@@ -367,28 +370,42 @@ last_literals:
 
 
 // 64 threads per segment.  Two instances: byU32 segments with the 9 KiB table (every 261,100-B
-// segment; grid (nseg_max, closed_cap), segment s of closed container c), and byU16 ones with
-// 16 KiB (a container's short last segment; grid (1, closed_cap)); each returns at once for the
-// other kind.
+// segment) and byU16 ones with 16 KiB (a container's short last segment); each skips the other
+// kind.  Persistent: a fixed grid of waves takes (container, segment) items from a per-batch
+// counter (items of the byU16 instance: one per container), so the pass never dispatches the
+// empty workgroups of a (nseg_max, closed_cap) grid, and the grid can leave wave slots free on
+// every CU: with HDRF_LZ4_WAVES = 16 per CU (of the 17 the LDS table allows), the next batch's
+// SHA and chunking kernels get a slot per SIMD while this pass runs, so the next pass is ready
+// when this one drains (otherwise SHA waited for the pass's waves to retire: one pass at a time).
 template <bool kSmall>
 __global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed,
                                                      const uint32_t *__restrict__ nclosed, const uint8_t *__restrict__ arena,
                                                      uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
-                                                     uint32_t *__restrict__ seg_clen, int nseg_max)
+                                                     uint32_t *__restrict__ seg_clen, int nseg_max, uint32_t *__restrict__ work)
 {
     __shared__ __attribute__((aligned(16))) uint8_t tabmem[kSmall ? kLzTabU16 : kLzTabU32];
-    const int c = blockIdx.y;
-    if ((uint32_t)c >= *nclosed) return;                   // grid sized for closed_cap
-    const ClosedRec r = closed[c];
-    const int s = kSmall ? (r.len ? (int)((r.len - 1) / kLzMaxIn) : 0) : (int)blockIdx.x;
-    const int64_t off = (int64_t)s * kLzMaxIn;
-    if (off >= (int64_t)r.len) return;
-    const int n = (int)min((int64_t)kLzMaxIn, (int64_t)r.len - off);
-    if ((n < k64KLimit) != kSmall) return;
-    const uint8_t *src = arena + (size_t)r.slot * cmax + off;
-    uint8_t *out = carena + (size_t)r.slot * cslot + 8 + (size_t)s * kLzSegStride;
-    const int cl = lz4_block(src, n, out, tabmem);
-    if (lane_id() == 0) seg_clen[(size_t)c * nseg_max + s] = (uint32_t)cl;
+    const uint32_t nc = *nclosed;
+    const uint32_t per = kSmall ? 1u : (uint32_t)nseg_max;
+    const uint32_t total = nc * per;
+    for (;;) {
+        uint32_t item = 0;
+        if (lane_id() == 0) item = atomicAdd(work, 1u);
+        item = rdfirst(item);
+        if (item >= total) break;                             // every wave reaches this exit
+        const int c = (int)(item / per);
+        const ClosedRec r = closed[c];
+        const int s = kSmall ? (r.len ? (int)((r.len - 1) / kLzMaxIn) : 0) : (int)(item % per);
+        const int64_t off = (int64_t)s * kLzMaxIn;
+        if (off >= (int64_t)r.len) continue;
+        const int n = (int)min((int64_t)kLzMaxIn, (int64_t)r.len - off);
+        if ((n < k64KLimit) != kSmall) continue;
+        const uint8_t *src = arena + (size_t)r.slot * cmax + off;
+        uint8_t *out = carena + (size_t)r.slot * cslot + 8 + (size_t)s * kLzSegStride;
+        const int cl = lz4_block(src, n, out, tabmem);
+        if (lane_id() == 0) seg_clen[(size_t)c * nseg_max + s] = (uint32_t)cl;
+        __builtin_amdgcn_s_waitcnt(0);                        // the table is reused by the next item
+        asm volatile("" ::: "memory");
+    }
 }
 
 // grid nclosed x 256 threads: frame the segments in place, [BE32 len] ([BE32 clen] block)* [BE32 0].
@@ -613,17 +630,24 @@ uint64_t lz4_piece_stride() { return kLzSegStride; }
 
 hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int closed_cap, uint32_t cmax,
                       const uint8_t *arena, uint8_t *carena, uint64_t cslot, uint32_t *seg_clen, uint32_t *file_len,
-                      hipStream_t st)
+                      uint32_t *work, hipStream_t st)
 {
-    // grids cover closed_cap containers; workgroups past the device-side count exit at once, so
-    // the compression stays in stream order with the batch (no host round trip).  The short last
-    // segments (16 KiB tables, at most one per container) go first: the main kernel's tail then
-    // overlaps the next batch's LZ4 pass on the other LZ4 stream instead of this small launch.
+    // persistent grids (no host round trip for the device-side closed count); the short last
+    // segments (16 KiB tables, at most one per container) go first, the main pass's tail then
+    // overlaps the next batch's pass on the other LZ4 stream
+    static const int ncu = [] {
+        int d = 0, n = 0;
+        if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+            n = 256;
+        return n > 0 ? n : 256;
+    }();
+    static const int wpc = [] { const char *e = getenv("HDRF_LZ4_WAVES"); const int v = e ? atoi(e) : 16; return v > 0 ? v : 16; }();
     const int nseg_max = (int)((cmax + kLzMaxIn - 1) / kLzMaxIn);
-    hipLaunchKernelGGL(lz4_seg_kernel<true>, dim3(1, closed_cap), dim3(64), 0, st, closed, nclosed, arena,
-                       (uint64_t)cmax, carena, cslot, seg_clen, nseg_max);
-    hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(nseg_max, closed_cap), dim3(64), 0, st, closed, nclosed, arena,
-                       (uint64_t)cmax, carena, cslot, seg_clen, nseg_max);
+    if (hipError_t e = hipMemsetAsync(work, 0, 2 * sizeof(uint32_t), st)) return e;
+    hipLaunchKernelGGL(lz4_seg_kernel<true>, dim3(std::min(closed_cap, 4 * ncu)), dim3(64), 0, st, closed, nclosed,
+                       arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work);
+    hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(std::min(closed_cap * nseg_max, wpc * ncu)), dim3(64), 0, st, closed,
+                       nclosed, arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work + 1);
     hipLaunchKernelGGL(lz4_pack_kernel, dim3(closed_cap), dim3(256), 0, st, closed, nclosed, carena, cslot, seg_clen,
                        nseg_max, file_len);
     return hipGetLastError();

@@ -37,7 +37,7 @@ EXPORTS = [
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
-PIPELINE_DEPTH = 3          # HDRF_PIPELINE_DEPTH: batches in flight
+PIPELINE_DEPTH = 5          # HDRF_PIPELINE_DEPTH: batches in flight
 
 
 # per-stage timers of hdrf_stage_times (kernel names in parentheses)

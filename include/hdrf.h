@@ -103,9 +103,10 @@ int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_
  * first), so every submit pairs with exactly one wait.  The device buffers of a batch must stay
  * valid until it is completed.  Chunking of batch k+1 overlaps hashing of batch k and the
  * index/store stage of batch k-1 (latency-bound walk, VALU-bound SHA, HBM-bound store); the
- * bench keeps two batches in flight (three under compressor 2).  Views (index, containers, allocator) complete all batches
+ * bench keeps two batches in flight (five under compressor 2, where a batch's LZ4 pass outlasts
+ * the front halves of the next ones).  Views (index, containers, allocator) complete all batches
  * first. */
-#define HDRF_PIPELINE_DEPTH 3
+#define HDRF_PIPELINE_DEPTH 5
 int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                       const uint64_t *readable, const uint64_t *block_ids);
 int hdrf_wait_batch(hdrf_ctx *ctx);
