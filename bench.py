@@ -306,7 +306,8 @@ def main():
         return {"bound": "hbm", "kernel": KERNEL_OF[name], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms, 4),
                 "algorithmic_bytes_per_launch": int(per_launch[name]),
-                "traffic": (pmc.get(KERNEL_OF[name]) or pmc.get(KERNEL_OF[name] + "<5>") or {}).get("hbm_bytes_per_launch")}
+                "traffic": next((pmc[k] for k in (KERNEL_OF[name] + t for t in ("", "<5>", "<7>", "<true>", "<false>"))
+                                 if k in pmc), {}).get("hbm_bytes_per_launch")}
 
     # per-stream chains: the batch period is set by the longest one (the critical path)
     chains = {c: round(sum(avg[s] for s in st), 4) for c, st in CHAINS.items()}
