@@ -91,6 +91,8 @@ def parse():
                     help="config5: deliver every block as packets of this many KiB (hdrf_rx_begin / "
                          "hdrf_append_packet / hdrf_submit_slot, one block per submit: the JNI shape); "
                          "0 = whole blocks through hdrf_submit_host")
+    ap.add_argument("--packet-threads", type=int, default=4,
+                    help="config5 packets: receiver threads appending different blocks' packets concurrently")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
                     help="config4: mixed-entropy blocks (random/text/binary), dedup + Lz4Codec containers; "
                          "config5: host-resident (pinned) blocks streamed H2D on a side stream (PCIe-inclusive)")
@@ -193,20 +195,36 @@ def main():
                 collect()
         elif host and a.packet_kib:
             # packet-granular receive, one block per submit (the JNI shape): each block's packets are
-            # appended as they "arrive" (chunk H2D on the copy stream) while earlier blocks reduce
-            P = a.packet_kib << 10
+            # appended as they "arrive" (chunk H2D on the copy stream) while earlier blocks reduce;
+            # T receiver threads (one per block, as DataXceiver threads) append concurrently
+            import threading
+            P, T = a.packet_kib << 10, max(1, a.packet_threads)
             pend = 0
-            for b in range(nb):
-                rx = ctx.rx_begin(b)
+
+            def receive(rx, b):
                 base = hbuf.ctypes.data + b * S
                 for o in range(0, S, P):
                     ctx.append_packet(rx, base + o, min(P, S - o))
-                if pend == 3:
+
+            for g in range(0, nb, T):
+                grp = list(range(g, min(nb, g + T)))
+                while pend + len(grp) > 8 or pend >= 5:          # 8 receive buffers, depth 5
                     ctx.wait_batch()
                     collect()
                     pend -= 1
-                ctx.submit_slot(rx)
-                pend += 1
+                rxs = [ctx.rx_begin(b) for b in grp]
+                th = [threading.Thread(target=receive, args=(rx, b)) for rx, b in zip(rxs, grp)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+                for rx in rxs:                             # submitted in arrival (block) order
+                    if pend >= 5:
+                        ctx.wait_batch()
+                        collect()
+                        pend -= 1
+                    ctx.submit_slot(rx)
+                    pend += 1
             for _ in range(pend):
                 ctx.wait_batch()
                 collect()
@@ -422,8 +440,8 @@ def main():
                                           "H2D on a side stream overlapped with the reduction (%s), "
                                           "chunk+SHA-1+local index+container store, fresh index per step"
                                           % (nb, a.block_mib, a.dup_ppm // 10000,
-                                             ("%d KiB packets, hdrf_append_packet + hdrf_submit_slot, one block "
-                                              "per submit" % a.packet_kib) if a.packet_kib else
+                                             ("%d KiB packets, %d receiver threads, hdrf_append_packet + hdrf_submit_slot, "
+                                              "one block per submit" % (a.packet_kib, a.packet_threads)) if a.packet_kib else
                                              "whole blocks, hdrf_submit_host"))
             line["pcie"] = {"h2d_GB_s_raw_copy": round(h2d_gbs, 2), "value_over_raw_copy": round(value / h2d_gbs, 4),
                             "note": "value is PCIe-inclusive: host buffers -> HBM -> reduced"}

@@ -17,6 +17,7 @@
 #include <mutex>
 #include <set>
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -182,15 +183,21 @@ struct hdrf_ctx {
     // packet-granular receive (hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot): device
     // receive buffers, and a pinned chunk ring the packets are copied into before their H2D
     static constexpr int kRx = 8;
-    static constexpr int kRingChunks = 8;
     static constexpr uint64_t kRingChunk = 4ull << 20;
-    struct Rx { uint8_t *d = nullptr; uint64_t len = 0; uint64_t id = 0; int state = 0; };   // 0 free 1 receiving 2 submitted
+    // one receive buffer per block being received: device copy of the block, and two pinned 4 MiB
+    // staging chunks of its own, so receivers of different blocks (one DataXceiver thread each)
+    // copy their packets concurrently, outside the context lock
+    struct Rx {
+        uint8_t *d = nullptr;                   // device buffer (max_block_bytes + slack)
+        uint8_t *h = nullptr;                   // pinned staging, 2 x kRingChunk
+        hipEvent_t ev[2] = {nullptr, nullptr};  // H2D of each staging chunk
+        bool busy[2] = {false, false};
+        int cur = 0;
+        uint64_t fill = 0, dst = 0;             // bytes in the current chunk, their block offset
+        uint64_t len = 0, id = 0;
+        std::atomic<int> state{0};              // 0 free 1 receiving 2 submitted
+    };
     Rx rx[kRx];
-    uint8_t *h_ring = nullptr;
-    hipEvent_t ring_ev[kRingChunks] = {};
-    bool ring_busy[kRingChunks] = {};
-    int ring_cur = 0, ring_rx = -1;
-    uint64_t ring_fill = 0, ring_dst = 0;
     // timing
     bool timing = false;
     double stage_ms[kStages] = {};
@@ -327,9 +334,11 @@ static void free_all(hdrf_ctx *ctx)
         if (L) (void)hipStreamDestroy(L);
     for (auto &r : ctx->rx)
         if (r.d) (void)hipFree(r.d);
-    if (ctx->h_ring) (void)hipHostFree(ctx->h_ring);
-    for (auto &e : ctx->ring_ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto &r : ctx->rx) {
+        if (r.h) (void)hipHostFree(r.h);
+        for (auto e : r.ev)
+            if (e) (void)hipEventDestroy(e);
+    }
 }
 
 static int alloc_slot(hdrf_ctx *ctx, Slot &S)
@@ -441,10 +450,8 @@ static int init_state(hdrf_ctx *ctx)
     ctx->inflight_bound = 0;
     ctx->handed.clear();
     ctx->lost = false;
-    for (auto &r : ctx->rx) { r.state = 0; r.len = 0; }
+    for (auto &r : ctx->rx) { r.state = 0; r.len = 0; r.fill = 0; r.busy[0] = r.busy[1] = false; }
     for (auto &S : ctx->sl) S.rx_release = -1;
-    ctx->ring_rx = -1;
-    ctx->ring_fill = 0;
     return 0;
 }
 
@@ -478,11 +485,13 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     (void)hipDeviceGetStreamPriorityRange(&lo_prio, &hi_prio);
     const char *pe = std::getenv("HDRF_PRIO");
     const int prio_mode = pe ? std::atoi(pe) : 1;
-    const int pa = prio_mode == 1 ? hi_prio : lo_prio, pb = prio_mode == 2 ? hi_prio : lo_prio;
+    // 3 = only A (SHA) high: chunking of a later batch then fills the slots SHA leaves
+    const int pa = (prio_mode == 1 || prio_mode == 3) ? hi_prio : lo_prio, pb = prio_mode == 2 ? hi_prio : lo_prio;
+    const int pw = prio_mode == 1 ? hi_prio : lo_prio;
     if (hipSetDevice(c.device) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, pa) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stB, hipStreamNonBlocking, pb) != hipSuccess ||
-        hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pa) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pw) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[0], hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[1], hipStreamNonBlocking) != hipSuccess) {
@@ -941,24 +950,25 @@ static int wait_one(hdrf_ctx *ctx)
 
 // ---- packet-granular receive (DN/BlockReceiver.java:877-896: each packet appended to bf1 as it
 // arrives; :1258-1261 the finished block handed to the reducer) ------------------------------
-// A packet is copied into a pinned 4 MiB chunk of a ring (the caller may reuse it when the call
-// returns); every full chunk goes H2D on stream C into the block's receive buffer, overlapping the
-// next packets and the kernels of the blocks in flight.  The ring's chunks are reused in order,
-// waiting (host side) for a chunk's copy only when the ring wraps.
-static int ring_flush(hdrf_ctx *ctx)
+// A packet is copied into the receive buffer's current pinned 4 MiB staging chunk (the caller may
+// reuse the packet when the call returns); every full chunk goes H2D on stream C into the block's
+// device buffer, overlapping the next packets and the kernels of the blocks in flight.  The two
+// chunks alternate, waiting (host side) for a chunk's copy only before refilling it.  The packets
+// of one block come from one receiver thread (the reference's BlockReceiver), so appends take
+// only that buffer's state, not the context lock: receivers of different blocks copy in parallel.
+static int rx_flush(hdrf_ctx *ctx, hdrf_ctx::Rx &r)
 {
-    if (ctx->ring_fill == 0) return 0;
-    const int c = ctx->ring_cur;
-    hdrf_ctx::Rx &r = ctx->rx[ctx->ring_rx];
-    HIPCK(hipMemcpyAsync(r.d + ctx->ring_dst, ctx->h_ring + (uint64_t)c * hdrf_ctx::kRingChunk, ctx->ring_fill,
-                         hipMemcpyHostToDevice, ctx->stC));
-    HIPCK(hipEventRecord(ctx->ring_ev[c], ctx->stC));
-    ctx->ring_busy[c] = true;
-    ctx->ring_cur = (c + 1) % hdrf_ctx::kRingChunks;
-    ctx->ring_fill = 0;
-    if (ctx->ring_busy[ctx->ring_cur]) {               // ring wrapped: that chunk's copy must have landed
-        HIPCK(hipEventSynchronize(ctx->ring_ev[ctx->ring_cur]));
-        ctx->ring_busy[ctx->ring_cur] = false;
+    if (r.fill == 0) return 0;
+    const int c = r.cur;
+    HIPCK(hipMemcpyAsync(r.d + r.dst, r.h + (uint64_t)c * hdrf_ctx::kRingChunk, r.fill, hipMemcpyHostToDevice,
+                         ctx->stC));
+    HIPCK(hipEventRecord(r.ev[c], ctx->stC));
+    r.busy[c] = true;
+    r.cur = c ^ 1;
+    r.fill = 0;
+    if (r.busy[r.cur]) {                               // refilling that chunk: its copy must have landed
+        HIPCK(hipEventSynchronize(r.ev[r.cur]));
+        r.busy[r.cur] = false;
     }
     return 0;
 }
@@ -968,17 +978,19 @@ extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
     HDRF_LOCK(ctx);
     if (!ctx || !rx) return HDRF_E_INVAL;
     if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "node-global context: use the hdrf_gx_* phases");
-    if (!ctx->h_ring) {
-        HIPCK(hipHostMalloc((void **)&ctx->h_ring, hdrf_ctx::kRingChunks * hdrf_ctx::kRingChunk));
-        for (auto &e : ctx->ring_ev) HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
     for (int i = 0; i < hdrf_ctx::kRx; i++) {
         hdrf_ctx::Rx &r = ctx->rx[i];
-        if (r.state != 0) continue;
+        if (r.state.load() != 0) continue;
         if (!r.d) HIPCK(hipMalloc((void **)&r.d, (uint64_t)ctx->cfg.max_block_bytes + kSlack + 256));
-        r.state = 1;
+        if (!r.h) {
+            HIPCK(hipHostMalloc((void **)&r.h, 2 * hdrf_ctx::kRingChunk));
+            for (auto &e : r.ev) HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
         r.len = 0;
+        r.fill = 0;
+        r.dst = 0;
         r.id = block_id;
+        r.state.store(1);
         *rx = i;
         return 0;
     }
@@ -987,23 +999,31 @@ extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
 
 extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data, uint64_t len)
 {
-    HDRF_LOCK(ctx);
-    if (!ctx || rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state != 1 || (len && !data))
-        return ctx ? set_err(ctx, HDRF_E_INVAL, "bad receive buffer or packet") : HDRF_E_INVAL;
+    if (!ctx) return HDRF_E_INVAL;
+    if (rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state.load() != 1 || (len && !data)) {
+        HDRF_LOCK(ctx);
+        return set_err(ctx, HDRF_E_INVAL, "bad receive buffer or packet");
+    }
     hdrf_ctx::Rx &r = ctx->rx[rx];
-    if (r.len + len > (uint64_t)ctx->cfg.max_block_bytes) return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
+    if (r.len + len > (uint64_t)ctx->cfg.max_block_bytes) {
+        HDRF_LOCK(ctx);
+        return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
+    }
     while (len) {
-        if (ctx->ring_fill && ctx->ring_rx != rx)
-            if (int rc = ring_flush(ctx)) return rc;   // the chunk holds another block's packets
-        if (ctx->ring_fill == 0) { ctx->ring_rx = rx; ctx->ring_dst = r.len; }
-        const uint64_t n = std::min(len, hdrf_ctx::kRingChunk - ctx->ring_fill);
-        std::memcpy(ctx->h_ring + (uint64_t)ctx->ring_cur * hdrf_ctx::kRingChunk + ctx->ring_fill, data, n);
-        ctx->ring_fill += n;
+        if (r.fill == 0) r.dst = r.len;
+        const uint64_t n = std::min(len, hdrf_ctx::kRingChunk - r.fill);
+        std::memcpy(r.h + (uint64_t)r.cur * hdrf_ctx::kRingChunk + r.fill, data, n);
+        r.fill += n;
         r.len += n;
         data += n;
         len -= n;
-        if (ctx->ring_fill == hdrf_ctx::kRingChunk)
-            if (int rc = ring_flush(ctx)) return rc;
+        if (r.fill == hdrf_ctx::kRingChunk) {
+            const int rc = rx_flush(ctx, r);
+            if (rc) {
+                HDRF_LOCK(ctx);
+                return rc;
+            }
+        }
     }
     return 0;
 }
@@ -1011,13 +1031,12 @@ extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data
 extern "C" int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx)
 {
     HDRF_LOCK(ctx);
-    if (!ctx || rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state != 1)
+    if (!ctx || rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state.load() != 1)
         return ctx ? set_err(ctx, HDRF_E_INVAL, "bad receive buffer") : HDRF_E_INVAL;
     if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)     // every submit pairs with one hdrf_wait_batch
         return set_err(ctx, HDRF_E_CAPACITY, "pipeline full: hdrf_wait_batch first");
     hdrf_ctx::Rx &r = ctx->rx[rx];
-    if (ctx->ring_rx == rx)
-        if (int rc = ring_flush(ctx)) return rc;
+    if (int rc = rx_flush(ctx, r)) return rc;
     HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, ctx->stC));
     Slot &S = ctx->sl[ctx->nsub % kSlots];
     HIPCK(hipEventRecord(S.copy_done, ctx->stC));

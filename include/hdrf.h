@@ -119,13 +119,16 @@ int hdrf_wait_batch(hdrf_ctx *ctx);
 int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
                      const uint64_t *block_ids);
 /* Packet-granular receive (DN/BlockReceiver.java:877-896, 1258-1261): hdrf_rx_begin reserves one of
- * 8 device receive buffers for a block; hdrf_append_packet copies each packet as it arrives into a
- * pinned chunk ring (the packet may be reused when the call returns) and sends every full 4 MiB
- * chunk H2D on a side stream, overlapped with the next packets and with the blocks in flight;
+ * 8 device receive buffers for a block; hdrf_append_packet copies each packet as it arrives into the
+ * buffer's own pair of pinned 4 MiB staging chunks (the packet may be reused when the call returns)
+ * and sends every full chunk H2D on a side stream, overlapped with the next packets and with the
+ * blocks in flight.  The packets of one receive buffer come from one thread at a time (the block's
+ * receiver); hdrf_append_packet does not take the context lock, so receivers of different blocks
+ * copy concurrently;
  * hdrf_submit_slot submits the received block as a one-block batch with no copy left (pair it
  * with hdrf_wait_batch like hdrf_submit_batch; HDRF_E_CAPACITY when the pipeline is full).  The
  * buffer is free again when that batch completes; hdrf_rx_begin returns HDRF_E_CAPACITY while all
- * eight are in use (three blocks in flight leave five for blocks being received). */
+ * eight are in use. */
 int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx);
 int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data, uint64_t len);
 int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx);

@@ -239,3 +239,44 @@ def test_packet_receive_matches_oracle():
         compare_block(ctx.batch_result(0), ora.reduce(blocks[g], ids[g]), tag=f"packet block {g}")
     compare_state(ctx, ora, ids, tag="packets")
     ctx.close()
+
+
+def test_packet_receivers_on_concurrent_threads():
+    """Four receiver threads (one per block, as DataXceiver threads are) append their blocks' ragged
+    packets at the same time (hdrf_append_packet takes no context lock); the blocks are then
+    submitted in arrival order and every one matches the sequential oracle."""
+    import threading
+    blocks = _blocks(93, 4, 3_000_000)
+    ids = [9100 + i for i in range(len(blocks))]
+    ctx = Context(container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64)
+    ora = Oracle(max_size=1 << 20)
+    rxs = [ctx.rx_begin(i) for i in ids]
+    errs = []
+
+    def receive(b):
+        try:
+            rng = np.random.default_rng(200 + b)
+            buf = np.zeros(1 << 20, np.uint8)                  # this receiver's packet buffer, reused
+            o = 0
+            while o < len(blocks[b]):
+                n = int(rng.choice([1, 513, 65536, 200_001, 1 << 20]))
+                p = blocks[b][o:o + n]
+                buf[:len(p)] = p
+                ctx.append_packet(rxs[b], buf.ctypes.data, len(p))
+                buf[:len(p)] = 0x5A
+                o += len(p)
+        except Exception as e:                                  # noqa: BLE001 (reported below)
+            errs.append(e)
+
+    th = [threading.Thread(target=receive, args=(b,)) for b in range(len(blocks))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for b in range(len(blocks)):
+        ctx.submit_slot(rxs[b])
+        ctx.wait_batch()
+        compare_block(ctx.batch_result(0), ora.reduce(blocks[b], ids[b]), tag=f"threaded packets {b}")
+    compare_state(ctx, ora, ids, tag="threaded packets")
+    ctx.close()
