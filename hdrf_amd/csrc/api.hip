@@ -167,6 +167,7 @@ struct hdrf_ctx {
     uint64_t gx_nfront = 0, gx_nfwait = 0, gx_nback = 0;   // fronts launched / waited, batches committed
     int gx_bphase = 0;                           // back batch: 0 owner next, 1 decide, 2 flush, 3 place, 4 commit
     hdrf_stats stats{};                          // cumulative since the last reset
+    uint32_t lzop_mtime = 0;                     // stream codec 3: the lzop header's mtime field
     // concurrency: every entry point holds mu; ticketed reductions also wait for their turn
     // (AIWriteQueue order, DN/DataDeduplicator.java:124-158, DN/DDRunner.java:20-36)
     std::recursive_mutex mu;
@@ -1105,7 +1106,25 @@ static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need);
 // overhead bufferSize/255 + 16, SnappyCodec bufferSize/6 + 32 (hadoop-common 3.1.0)
 static int64_t stream_max_input(int codec)
 {
+    if (codec == 3) return 262144 - ((262144 >> 4) + 64 + 3);    // hadoop-lzo LzopOutputStream (LZO1X)
     return codec == 0 ? 262144 - (262144 / 6 + 32) : 262144 - (262144 / 255 + 16);
+}
+
+// hadoop-lzo LzopOutputStream.writeLzopHeader: magic, {version 0x1010, LZO library version 0x20a0
+// (LZO 2.10), compat 0x0940, LZO1X_1 = method 1 / level 5, flags 0, mode 0x81a4, mtime, gmtdiff 0,
+// no file name} and its Adler-32 (the reference's mtime is the wall clock: hdrf_set_lzop_mtime)
+static size_t lzop_header(uint32_t mtime, uint8_t *dst)
+{
+    static const uint8_t magic[9] = {0x89, 'L', 'Z', 'O', 0x00, 0x0d, 0x0a, 0x1a, 0x0a};
+    uint8_t h[25] = {0x10, 0x10, 0x20, 0xa0, 0x09, 0x40, 1, 5, 0, 0, 0, 0, 0, 0, 0x81, 0xa4,
+                     (uint8_t)(mtime >> 24), (uint8_t)(mtime >> 16), (uint8_t)(mtime >> 8), (uint8_t)mtime, 0, 0, 0, 0, 0};
+    uint32_t a = 1, b = 0;
+    for (uint8_t c : h) { a = (a + c) % 65521u; b = (b + a) % 65521u; }
+    const uint32_t ck = (b << 16) | a;
+    std::memcpy(dst, magic, 9);
+    std::memcpy(dst + 9, h, 25);
+    dst[34] = (uint8_t)(ck >> 24); dst[35] = (uint8_t)(ck >> 16); dst[36] = (uint8_t)(ck >> 8); dst[37] = (uint8_t)ck;
+    return 38;
 }
 
 // Stream-mode compressor 5 (GzipCodec, zlib level 6; DN/BlockReceiver.java:858-873,887-894): the
@@ -1162,8 +1181,8 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
 {
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
-    if (codec != 4 && codec != 0 && codec != 5)
-        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec) are implemented");
+    if (codec != 4 && codec != 0 && codec != 5 && codec != 3)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 3 (LzopCodec), 4 (Lz4Codec) and 5 (GzipCodec)");
     if (nwrites < 0 || (nwrites && !writes) || (len && !dev_data) || readable < len + kSlack)
         return set_err(ctx, HDRF_E_INVAL, "bad stream arguments (readable must be >= len + 64)");
     if (codec == 5) {
@@ -1180,12 +1199,19 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
         pieces.push_back(LzPiece{src, (uint32_t)n, 0});
         outs.push_back(LzOut{0, hval, hlen});
     };
+    const bool lzop = codec == 3;
     for (int w = 0; w < nwrites; w++) {
         const uint64_t n = writes[w];
+        if (lzop && n == 0) continue;
         if (lim > 0 && n + lim > (uint64_t)kMaxIn) { piece(gs, lim, (uint32_t)lim, 4); lim = 0; }   // finish()
         if (n > (uint64_t)kMaxIn) {                                                               // segmented write
-            for (uint64_t o = 0; o < n; o += kMaxIn)
-                piece(off + o, std::min<uint64_t>(kMaxIn, n - o), (uint32_t)n, o == 0 ? 4u : 0u);
+            for (uint64_t o = 0; o < n; o += kMaxIn) {
+                const uint64_t sl = std::min<uint64_t>(kMaxIn, n - o);
+                // Lz4Codec/SnappyCodec: one BE32 raw length for the whole write; LZOP: every slice
+                // is its own block [BE32 raw][BE32 stored]
+                if (lzop) piece(off + o, sl, (uint32_t)sl, 4u);
+                else piece(off + o, sl, (uint32_t)n, o == 0 ? 4u : 0u);
+            }
             off += n;
             continue;
         }
@@ -1194,10 +1220,10 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
         off += n;
     }
     if (off != len) return set_err(ctx, HDRF_E_INVAL, "write sizes do not add up to the block length");
-    const bool trailer = lim == 0;                     // close(): BE32 0 when nothing is buffered
-    if (!trailer) piece(gs, lim, (uint32_t)lim, 4);
+    const bool trailer = lzop || lim == 0;             // close(): BE32 0 when nothing is buffered (LZOP: always)
+    if (lim > 0) piece(gs, lim, (uint32_t)lim, 4);
     const int n = (int)pieces.size();
-    const uint64_t stride = lz4_piece_stride();
+    const uint64_t stride = lzop ? lzo_piece_stride() : lz4_piece_stride();
     const uint64_t a_pieces = 0, a_outs = ((uint64_t)n * sizeof(LzPiece) + 255) & ~255ull;
     const uint64_t a_clen = a_outs + (((uint64_t)n * sizeof(LzOut) + 255) & ~255ull);
     const uint64_t a_stage = a_clen + (((uint64_t)n * 4 + 255) & ~255ull);
@@ -1224,6 +1250,8 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
         HIPCK(hipMemcpyAsync(R + a_pieces, pieces.data(), n * sizeof(LzPiece), hipMemcpyHostToDevice, st));
         if (codec == 4) {
             HIPCK(launch_lz4_stream((const LzPiece *)(R + a_pieces), n, dev_data, R + a_stage, (uint32_t *)(R + a_clen), st));
+        } else if (codec == 3) {
+            HIPCK(launch_lzo_stream((const LzPiece *)(R + a_pieces), n, dev_data, R + a_stage, (uint32_t *)(R + a_clen), st));
         } else {
             if (nf) HIPCK(hipMemcpyAsync(R + a_frags, frags.data(), nf * sizeof(LzPiece), hipMemcpyHostToDevice, st));
             HIPCK(launch_snappy_stream((const LzPiece *)(R + a_pieces), n, (const LzPiece *)(R + a_frags), nf, dev_data,
@@ -1233,17 +1261,20 @@ extern "C" int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t bloc
         HIPCK(hipMemcpyAsync(clen.data(), R + a_clen, n * 4, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
     }
-    uint64_t pos = 0;
+    uint8_t hdr[64];
+    const uint64_t hlen = lzop ? lzop_header(ctx->lzop_mtime, hdr) : 0;
+    uint64_t pos = hlen;
     for (int i = 0; i < n; i++) {
         outs[i].dst = pos;
         pos += outs[i].hlen + 4 + clen[i];
     }
     const int64_t total = (int64_t)pos + (trailer ? 4 : 0);
     if (!out || cap < total) return set_err(ctx, HDRF_E_CAPACITY, "stream file needs " + std::to_string(total) + " bytes");
+    if (hlen) std::memcpy(out, hdr, hlen);
     if (n) {
         HIPCK(hipMemcpyAsync(R + a_outs, outs.data(), n * sizeof(LzOut), hipMemcpyHostToDevice, st));
         HIPCK(launch_lz4_emit((const LzOut *)(R + a_outs), n, R + a_stage, (const uint32_t *)(R + a_clen), R + a_file, st));
-        HIPCK(hipMemcpyAsync(out, R + a_file, pos, hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(out + hlen, R + a_file + hlen, pos - hlen, hipMemcpyDeviceToHost, st));
         HIPCK(hipStreamSynchronize(st));
     }
     if (trailer) std::memset(out + pos, 0, 4);
@@ -1258,8 +1289,8 @@ extern "C" int64_t hdrf_stream_block_host(hdrf_ctx *ctx, int32_t codec, uint64_t
 {
     HDRF_LOCK(ctx);
     if (!ctx || (len && !data)) return HDRF_E_INVAL;
-    if (codec != 4 && codec != 0 && codec != 5)
-        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec) are implemented");
+    if (codec != 4 && codec != 0 && codec != 5 && codec != 3)
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 3 (LzopCodec), 4 (Lz4Codec) and 5 (GzipCodec)");
     if (int rc = drain(ctx)) return rc;
     if (int rc = grow(ctx, &ctx->d_stage, &ctx->stage_cap, len + kSlack)) return rc;
     if (len) HIPCK(hipMemcpy(ctx->d_stage, data, len, hipMemcpyHostToDevice));
@@ -1323,6 +1354,61 @@ static int64_t decode_file(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uin
     HIPCK(hipStreamSynchronize(st));
     if (err) return set_err(ctx, HDRF_E_INVAL, codec == 4 ? "corrupt LZ4 block in the Lz4Codec file"
                                                           : "corrupt snappy block in the SnappyCodec file");
+    return (int64_t)raw;
+}
+
+// ---- LzopCodec read side (DN/DataConstructor.java:140-166): LzopInputStream ----------------
+// header (magic, method LZO1X, Adler-32 / CRC-32 flags, optional file name; the header checksum is
+// checked), then blocks [BE32 raw][BE32 stored][checksums per the flags][bytes] up to BE32 0; one
+// wave per block decodes on the GPU (lzo.hip), stored == raw means the bytes are raw
+static int64_t decode_lzop(hdrf_ctx *ctx, const uint8_t *f, int64_t n, uint8_t *dev_out, int64_t cap)
+{
+    static const uint8_t magic[9] = {0x89, 'L', 'Z', 'O', 0x00, 0x0d, 0x0a, 0x1a, 0x0a};
+    auto be32 = [&](int64_t i) { return ((uint32_t)f[i] << 24) | ((uint32_t)f[i + 1] << 16) | ((uint32_t)f[i + 2] << 8) | f[i + 3]; };
+    if (n < 9 + 29 || !f || std::memcmp(f, magic, 9) != 0) return set_err(ctx, HDRF_E_INVAL, "not an lzop file");
+    const uint8_t *h = f + 9;
+    const uint32_t flags = be32(9 + 8);
+    const int fname = h[24];
+    if ((h[6] != 1 && h[6] != 2 && h[6] != 3) || (flags & 0x40)) return set_err(ctx, HDRF_E_INVAL, "unsupported lzop header");
+    int64_t pos = 9 + 25 + fname;
+    if (pos + 4 > n) return set_err(ctx, HDRF_E_INVAL, "truncated lzop header");
+    uint32_t a = 1, b = 0;
+    for (int i = 0; i < 25 + fname; i++) { a = (a + h[i]) % 65521u; b = (b + a) % 65521u; }
+    if (be32(pos) != ((b << 16) | a)) return set_err(ctx, HDRF_E_INVAL, "lzop header checksum mismatch");
+    pos += 4;
+    const int dck = ((flags & 1) != 0) + ((flags & 0x100) != 0), cck = ((flags & 2) != 0) + ((flags & 0x200) != 0);
+    std::vector<LzDec> items;
+    uint64_t raw = 0;
+    for (;;) {
+        if (pos + 4 > n) return set_err(ctx, HDRF_E_INVAL, "truncated lzop file");
+        const uint32_t ul = be32(pos);
+        pos += 4;
+        if (ul == 0) break;
+        if (pos + 4 > n) return set_err(ctx, HDRF_E_INVAL, "truncated lzop file");
+        const uint32_t cl = be32(pos);
+        pos += 4 + 4 * (int64_t)dck + (cl < ul ? 4 * (int64_t)cck : 0);
+        if (cl > ul || pos + cl > n) return set_err(ctx, HDRF_E_INVAL, "malformed lzop block");
+        items.push_back(LzDec{(uint64_t)pos, raw, cl, ul});
+        pos += cl;
+        raw += ul;
+    }
+    if (pos != n) return set_err(ctx, HDRF_E_INVAL, "bytes after the lzop end marker");
+    if ((int64_t)raw > cap || (raw && !dev_out)) return set_err(ctx, HDRF_E_CAPACITY, "output capacity");
+    if (items.empty()) return 0;
+    const int m = (int)items.size();
+    const uint64_t o_items = 0, o_err = ((uint64_t)m * sizeof(LzDec) + 255) & ~255ull, o_file = o_err + 256;
+    if (int rc = drain(ctx)) return rc;
+    if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_file + (uint64_t)n + 64)) return rc;
+    uint8_t *R = ctx->d_rd;
+    hipStream_t st = ctx->st;
+    HIPCK(hipMemcpyAsync(R + o_file, f, (size_t)n, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(R + o_items, items.data(), (size_t)m * sizeof(LzDec), hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(R + o_err, 0, 4, st));
+    HIPCK(launch_lzo_decode((const LzDec *)(R + o_items), m, R + o_file, dev_out, (int *)(R + o_err), st));
+    int err = 0;
+    HIPCK(hipMemcpyAsync(&err, R + o_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    if (err) return set_err(ctx, HDRF_E_INVAL, "corrupt LZO1X block in the lzop file");
     return (int64_t)raw;
 }
 
@@ -1498,9 +1584,18 @@ extern "C" int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const u
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (codec == 5) return decode_gzip(ctx, file, flen, dev_out, cap);
+    if (codec == 3) return decode_lzop(ctx, file, flen, dev_out, cap);
     if (codec != 0 && codec != 4)
-        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 4 (Lz4Codec) and 5 (GzipCodec)");
+        return set_err(ctx, HDRF_E_UNSUPPORTED, "stream codec: 0 (SnappyCodec), 3 (LzopCodec), 4 (Lz4Codec), 5 (GzipCodec)");
     return decode_file(ctx, file, flen, dev_out, cap, codec);
+}
+
+extern "C" int hdrf_set_lzop_mtime(hdrf_ctx *ctx, uint32_t mtime)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx) return HDRF_E_INVAL;
+    ctx->lzop_mtime = mtime;
+    return 0;
 }
 
 // Compressor 5 stage 1 (gzip.hip): per-position longest_match answers for both chain limits.

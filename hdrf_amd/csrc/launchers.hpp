@@ -141,6 +141,12 @@ struct LzDec {               // one LZ4 block of a Lz4Codec file -> raw bytes
     uint32_t clen, rawlen;
 };
 hipError_t launch_lz4_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
+// stream mode compressor 3 (lzo.hip): LzopCodec blocks (LZO1X-1, raw when not smaller) at stage +
+// i * lzo_piece_stride(); the decoder for LzopCodec files
+hipError_t launch_lzo_stream(const LzPiece *pieces, int n, const uint8_t *base, uint8_t *stage, uint32_t *clen,
+                             hipStream_t st);
+hipError_t launch_lzo_decode(const LzDec *items, int n, const uint8_t *src, uint8_t *dst, int *err, hipStream_t st);
+uint64_t lzo_piece_stride();
 // stream mode compressor 0 (snappy.hip): pieces (pad = first fragment) split into 64 KiB
 // fragments -> raw snappy groups at stage + i * stride; decoder for SnappyCodec files
 hipError_t launch_snappy_stream(const LzPiece *pieces, int n, const LzPiece *frags, int nf, const uint8_t *base,

@@ -34,6 +34,7 @@ EXPORTS = [
     "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
     "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot",
     "hdrf_gx_read_locate", "hdrf_gx_read_fill", "hdrf_gx_flush_fn", "hdrf_gx_alloc_scan",
+    "hdrf_set_lzop_mtime",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -142,6 +143,7 @@ def load():
         "hdrf_gzip_match_pass": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
         "hdrf_gzip_parse": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp]),
         "hdrf_stream_file_decode": (ctypes.c_int64, [_vp, ctypes.c_int32, _u8p, ctypes.c_int64, _vp, ctypes.c_int64]),
+        "hdrf_set_lzop_mtime": (ctypes.c_int, [_vp, ctypes.c_uint32]),
         "hdrf_container_load": (ctypes.c_int, [_vp, ctypes.c_uint32, _u8p, ctypes.c_int64, ctypes.c_int32]),
         "hdrf_container_unload": (ctypes.c_int, [_vp, ctypes.c_uint32]),
         "hdrf_index_load": (ctypes.c_int, [_vp, _u8p, _u8p, ctypes.c_int64]),
@@ -428,6 +430,9 @@ class Context:
         n = self._ck(self.L.hdrf_stream_block(self._h, codec, block_id, dev, nbytes, readable, wp, len(w), _p(out),
                                               cap))
         return out[:n].tobytes()
+
+    def set_lzop_mtime(self, mtime):
+        self._ck(self.L.hdrf_set_lzop_mtime(self._h, mtime))
 
     def stream_block_host(self, codec, block_id, data, writes):
         """hdrf_stream_block for host bytes (staged H2D by the library)."""

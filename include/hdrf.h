@@ -133,11 +133,13 @@ int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx);
 int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data, uint64_t len);
 int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx);
 /* Stream-mode schemes (DataNode.compressor 0/3/4/5: the whole block through a Hadoop codec,
- * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec, 0 = SnappyCodec, 5 = GzipCodec: the file
+ * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec, 0 = SnappyCodec, 3 = LzopCodec
+ * (hadoop-lzo: LZO1X-1 blocks in an lzop file; the header's mtime is hdrf_set_lzop_mtime's value,
+ * default 0, where the reference writes the wall clock), 5 = GzipCodec: the file
  * the reference writes to chunkDir+id when the block arrives as write()s of the given sizes (one
  * per packet, summing to len) followed by close().  dev_data needs len + 64 readable bytes.
  * Returns the file length (written to out), HDRF_E_CAPACITY if cap is too small,
- * HDRF_E_UNSUPPORTED for codec 3 (LZOP).  Codec 5's file does not depend on the write sizes
+ * HDRF_E_UNSUPPORTED for other codecs.  Codec 5's file does not depend on the write sizes
  * (zlib level 6 fed through Hadoop's ZlibCompressor); they must still add up to len.
  * Records the block length (SET id -> BE32(len)) for hdrf_block_length. */
 int64_t hdrf_stream_block(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, const uint8_t *dev_data, uint64_t len,
@@ -153,11 +155,16 @@ int64_t hdrf_stream_block_host(hdrf_ctx *ctx, int32_t codec, uint64_t block_id, 
  * file (lz4 = 1 for a closed container's Lz4Codec file, 0 for raw bytes) after its arena slot was
  * reused or the DataNode restarted; hdrf_container_unload frees that copy. */
 int64_t hdrf_lz4_file_decode(hdrf_ctx *ctx, const uint8_t *file, int64_t flen, uint8_t *dev_out, int64_t cap);
-/* The same for a stream-mode block file of codec 0 (SnappyCodec), 4 (Lz4Codec) or 5 (GzipCodec:
+/* The same for a stream-mode block file of codec 0 (SnappyCodec), 3 (LzopCodec: lzop header and
+ * its checksum checked, LZO1X blocks decoded on the GPU), 4 (Lz4Codec) or 5 (GzipCodec:
  * gzip members, inflated on the GPU, CRC-32 and ISIZE checked): the compression-only decoders of
  * DataConstructor (DN/DataConstructor.java:102-220).  HDRF_E_INVAL on a malformed file. */
 int64_t hdrf_stream_file_decode(hdrf_ctx *ctx, int32_t codec, const uint8_t *file, int64_t flen, uint8_t *dev_out,
                                 int64_t cap);
+/* The mtime field of the lzop headers hdrf_stream_block writes for codec 3 (LzopOutputStream puts
+ * System.currentTimeMillis() / 1000 there, the only bytes of the file that are not a function of
+ * the block). */
+int hdrf_set_lzop_mtime(hdrf_ctx *ctx, uint32_t mtime);
 /* Stage 1 of the GPU compressor 5 (GzipCodec = zlib level 6 deflate_slow, DN/BlockReceiver.java:
  * 858-873): for every position p of the len device bytes, the answer zlib's
  * longest_match gives at p with a 128-candidate chain (out128, prev_length < 8) and a 32-candidate

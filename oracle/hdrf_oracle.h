@@ -119,4 +119,13 @@ void hdrf_oracle_java_random_bytes(int64_t seed, int32_t buffer_len, int64_t tot
 #ifdef __cplusplus
 }
 #endif
+
+/* LZOP stream mode (compressor 3): LZO1X-1 + hadoop-lzo LzopOutputStream framing (hdrf_lzo.c) */
+int64_t hdrf_oracle_lzo1x_1_compress(const uint8_t *in, int64_t in_len, uint8_t *out);
+int64_t hdrf_oracle_lzo1x_decompress(const uint8_t *in, int64_t in_len, uint8_t *out, int64_t cap);
+int64_t hdrf_oracle_lzop_header(uint32_t mtime, uint8_t *dst);
+int64_t hdrf_oracle_lzop_stream_bound(int64_t n, int64_t nwrites);
+int64_t hdrf_oracle_lzop_stream(const uint8_t *src, const int64_t *writes, int64_t nwrites, uint32_t mtime,
+                                uint8_t *dst);
+int64_t hdrf_oracle_lzop_decode(const uint8_t *f, int64_t n, uint8_t *dst, int64_t cap);
 #endif

@@ -101,6 +101,19 @@ def lib():
         L.hdrf_oracle_gzip_symbols.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_void_p]
         L.hdrf_oracle_gzip_symbols.restype = ctypes.c_int64
+        L.hdrf_oracle_lzo1x_1_compress.argtypes = [_u8p, ctypes.c_int64, _u8p]
+        L.hdrf_oracle_lzo1x_1_compress.restype = ctypes.c_int64
+        L.hdrf_oracle_lzo1x_decompress.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
+        L.hdrf_oracle_lzo1x_decompress.restype = ctypes.c_int64
+        L.hdrf_oracle_lzop_header.argtypes = [ctypes.c_uint32, _u8p]
+        L.hdrf_oracle_lzop_header.restype = ctypes.c_int64
+        L.hdrf_oracle_lzop_stream_bound.argtypes = [ctypes.c_int64, ctypes.c_int64]
+        L.hdrf_oracle_lzop_stream_bound.restype = ctypes.c_int64
+        L.hdrf_oracle_lzop_stream.argtypes = [_u8p, ctypes.POINTER(ctypes.c_int64), ctypes.c_int64, ctypes.c_uint32,
+                                              _u8p]
+        L.hdrf_oracle_lzop_stream.restype = ctypes.c_int64
+        L.hdrf_oracle_lzop_decode.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_int64]
+        L.hdrf_oracle_lzop_decode.restype = ctypes.c_int64
         L.hdrf_oracle_crc32.argtypes = [_u8p, ctypes.c_int64]
         L.hdrf_oracle_crc32.restype = ctypes.c_uint32
         _lib = L
@@ -204,6 +217,43 @@ def hadoop_lz4_stream(data, writes):
     n = lib().hdrf_oracle_hadoop_lz4_stream(_p(buf), w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), w.size,
                                             _p(out))
     return out[:n].tobytes()
+
+
+def lzo1x_1(data):
+    """LZO 2.10 lzo1x_1_compress (x86-64 build) -> compressed bytes."""
+    a = _as_u8(data)
+    buf = np.concatenate([a, np.zeros(16, np.uint8)])
+    out = np.zeros(a.size + a.size // 16 + 64 + 3 + 16, np.uint8)
+    n = lib().hdrf_oracle_lzo1x_1_compress(_p(buf), a.size, _p(out))
+    return out[:n].copy()
+
+
+def lzo1x_decode(data, size):
+    a = _as_u8(data)
+    out = np.zeros(max(size, 1), np.uint8)
+    n = lib().hdrf_oracle_lzo1x_decompress(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), size)
+    if n < 0:
+        raise ValueError("malformed LZO1X stream")
+    return out[:n].copy()
+
+
+def lzop_stream(data, writes, mtime=0):
+    """hadoop-lzo LzopCodec output stream of one block: writes (sizes) then close()."""
+    a = _as_u8(data)
+    w = np.ascontiguousarray(writes, np.int64)
+    buf = np.concatenate([a, np.zeros(16, np.uint8)])
+    out = np.zeros(lib().hdrf_oracle_lzop_stream_bound(a.size, w.size), np.uint8)
+    n = lib().hdrf_oracle_lzop_stream(_p(buf), w.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), w.size, mtime, _p(out))
+    return out[:n].copy()
+
+
+def lzop_decode(data, cap):
+    a = _as_u8(data)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = lib().hdrf_oracle_lzop_decode(_p(a if a.size else np.zeros(1, np.uint8)), a.size, _p(out), cap)
+    if n < 0:
+        raise ValueError("malformed LZOP file")
+    return out[:n].copy()
 
 
 def hadoop_lz4_decode(data, cap):
