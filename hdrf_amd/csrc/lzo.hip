@@ -18,7 +18,8 @@
 namespace hdrf {
 
 constexpr int kLzoDBits = 14;
-constexpr int kLzoStride = 262144;                 // stage slot per block (>= 245,693 + n/16 + 67)
+// stage slot per block: the Lz4Codec piece stride (lz4_emit_kernel frames both), >= 245,693 + n/16 + 67
+uint64_t lz4_piece_stride();
 
 __device__ __forceinline__ uint64_t rd64u(const uint8_t *p) { return (uint64_t)rd32u(p) | ((uint64_t)rd32u(p + 4) << 32); }
 
@@ -180,17 +181,17 @@ __device__ int64_t lzo1x_1_block(const uint8_t *in, int64_t in_len, uint8_t *out
     return o.op - out;
 }
 
-// grid n x 64: block i of the stream -> stage + i * kLzoStride; the stored size -> clen[i]
+// grid n x 64: block i of the stream -> stage + i * stride; the stored size -> clen[i]
 // (the raw bytes when LZO does not shrink them, as LzopOutputStream.compress writes them)
 __global__ void __launch_bounds__(64) lzo_list_kernel(const LzPiece *__restrict__ pieces, int n,
                                                       const uint8_t *__restrict__ base, uint8_t *__restrict__ stage,
-                                                      uint32_t *__restrict__ clen)
+                                                      uint64_t stride, uint32_t *__restrict__ clen)
 {
     __shared__ __attribute__((aligned(16))) unsigned short dict[1 << kLzoDBits];
     const int i = blockIdx.x;
     if (i >= n) return;
     const LzPiece pc = pieces[i];
-    uint8_t *out = stage + (size_t)i * kLzoStride;
+    uint8_t *out = stage + (size_t)i * stride;
     int64_t c = lzo1x_1_block(base + pc.src, (int64_t)pc.len, out, dict);
     if (c >= (int64_t)pc.len) {                        // not smaller: store the raw bytes
         __threadfence();
@@ -326,7 +327,8 @@ __global__ void __launch_bounds__(64) lzo_decode_kernel(const LzDec *__restrict_
 hipError_t launch_lzo_stream(const LzPiece *pieces, int n, const uint8_t *base, uint8_t *stage, uint32_t *clen,
                              hipStream_t st)
 {
-    if (n > 0) hipLaunchKernelGGL(lzo_list_kernel, dim3(n), dim3(64), 0, st, pieces, n, base, stage, clen);
+    if (n > 0)
+        hipLaunchKernelGGL(lzo_list_kernel, dim3(n), dim3(64), 0, st, pieces, n, base, stage, lz4_piece_stride(), clen);
     return hipGetLastError();
 }
 
@@ -336,6 +338,6 @@ hipError_t launch_lzo_decode(const LzDec *items, int n, const uint8_t *src, uint
     return hipGetLastError();
 }
 
-uint64_t lzo_piece_stride() { return kLzoStride; }
+uint64_t lzo_piece_stride() { return lz4_piece_stride(); }
 
 }  // namespace hdrf

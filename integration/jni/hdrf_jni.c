@@ -8,6 +8,7 @@
 #include <jni.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/types.h>
@@ -244,7 +245,9 @@ JNIEXPORT jbyteArray JNICALL JFN(reconstruct0)(JNIEnv *env, jclass cls, jlong h,
     return out;
 }
 
-/* stream mode (compressor 0 SnappyCodec / 4 Lz4Codec / 5 GzipCodec): the block's chunkDir file for packet writes */
+/* stream mode (compressor 0 SnappyCodec / 3 LzopCodec / 4 Lz4Codec / 5 GzipCodec): the block's chunkDir
+ * file for packet writes.  LzopCodec headers carry the wall clock, as LzopOutputStream writes
+ * System.currentTimeMillis() / 1000. */
 JNIEXPORT jbyteArray JNICALL JFN(stream0)(JNIEnv *env, jclass cls, jlong h, jint codec, jobject buf, jint len,
                                           jlong id, jlongArray writes)
 {
@@ -254,6 +257,7 @@ JNIEXPORT jbyteArray JNICALL JFN(stream0)(JNIEnv *env, jclass cls, jlong h, jint
     const jsize nw = (*env)->GetArrayLength(env, writes);
     if (!p && len) { throw_io(env, ctx, HDRF_E_INVAL); return NULL; }
     jlong *w = (*env)->GetLongArrayElements(env, writes, NULL);
+    if (codec == 3) hdrf_set_lzop_mtime(ctx, (uint32_t)time(NULL));
     const int64_t cap = 64 + (int64_t)len + len / 6 + 48 * ((int64_t)nw + len / 218422 + 2);
     uint8_t *out = (uint8_t *)malloc((size_t)cap);
     int64_t n = out ? hdrf_stream_block_host(ctx, codec, (uint64_t)id, p, (uint64_t)len, (const uint64_t *)w, nw, out,
@@ -276,7 +280,7 @@ JNIEXPORT void JNICALL JFN(close0)(JNIEnv *env, jclass cls, jlong h)
 
 /* stream-mode read (DataConstructor's codec input stream over chunkDir + blkID,
  * DN/DataConstructor.java:102-220): the block file decoded on the GPU (codec 0 SnappyCodec,
- * 4 Lz4Codec, 5 GzipCodec); the raw length is the one streamBlock recorded for blockId. */
+ * 3 LzopCodec, 4 Lz4Codec, 5 GzipCodec); the raw length is the one streamBlock recorded for blockId. */
 JNIEXPORT jbyteArray JNICALL JFN(streamDecode0)(JNIEnv *env, jclass cls, jlong h, jint codec, jbyteArray file,
                                                 jlong id)
 {
