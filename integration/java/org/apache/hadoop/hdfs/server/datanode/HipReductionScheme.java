@@ -105,7 +105,7 @@ public final class HipReductionScheme extends ReductionScheme {
   }
 
   /**
-   * Stream-mode schemes (DataNode.compressor 0 SnappyCodec, 4 Lz4Codec, 5 GzipCodec; BlockReceiver.java:
+   * Stream-mode schemes (DataNode.compressor 0 SnappyCodec, 3 LzopCodec, 4 Lz4Codec, 5 GzipCodec; BlockReceiver.java:
    * 826-873,887-894,1238-1256): the file the reference writes to chunkDir + blockId when the block
    * arrives as write()s of the given packet sizes followed by close().  The caller stores it and
    * the library records SET blockId -> BE32(length).
@@ -117,8 +117,9 @@ public final class HipReductionScheme extends ReductionScheme {
 
   /**
    * Stream-mode read (DataConstructor.java:102-220): the chunkDir + blockId file written by
-   * streamBlock, decoded on the GPU through the codec (0 Snappy, 4 Lz4, 5 Gzip with CRC-32/ISIZE
-   * checks); IOException on a malformed file or one whose length differs from the recorded one.
+   * streamBlock, decoded on the GPU through the codec (0 Snappy, 3 Lzop with its header checksum,
+   * 4 Lz4, 5 Gzip with CRC-32/ISIZE checks); IOException on a malformed file or one whose length
+   * differs from the recorded one.
    */
   public byte[] streamDecode(int codec, byte[] file, long blockId) throws IOException {
     return streamDecode0(ctx, codec, file, blockId);
