@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--keep-recipes", type=int, default=1,
                     help="storeDB's recipe SET per block into the device recipe store (default 1, as the reference)")
     ap.add_argument("--depth", type=int, default=0,
-                    help="batches in flight (1..5, pipelined mode; default 2; config4 5: the LZ4 passes of two "
+                    help="batches in flight (1..5, pipelined mode; default 3, config4 5: the LZ4 passes of two "
                          "batches overlap while the front halves of the next ones run)")
     ap.add_argument("--alone", action="store_true",
                     help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
@@ -102,7 +102,9 @@ def parse():
 def main():
     a = parse()
     if not a.depth:
-        a.depth = 5 if a.workload == "config4" else 2
+        # config 2: depth 3 984 -> 1004 GB/s (three A/B pairs, scripts/ab_d23.txt): chunking of batch
+        # k+2 starts while batch k+1 hashes instead of after batch k's read-back
+        a.depth = 5 if a.workload == "config4" else 3
     if not a.arena_slots:
         a.arena_slots = 1280 if a.workload == "config4" else 512
     if a.workload == "config4":
