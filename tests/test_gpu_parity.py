@@ -389,8 +389,10 @@ def test_stream_mode_lz4_file_matches_oracle(case):
     f = ctx.stream_block(4, 77, dev, n, n + 4096, writes)
     assert f == hadoop_lz4_stream(d, writes)
     assert ctx.block_length(77) == n
+    from oracle.oracle import lzop_stream
+    assert ctx.stream_block(3, 78, dev, n, n + 4096, writes) == bytes(lzop_stream(d, writes))   # LzopCodec
     with pytest.raises(HdrfError):
-        ctx.stream_block(3, 78, dev, n, n + 4096, writes)          # LZOP: not built
+        ctx.stream_block(7, 79, dev, n, n + 4096, writes)          # no such codec
     ctx.dev_free(dev)
     ctx.close()
 
@@ -442,7 +444,7 @@ def test_stream_mode_snappy_file_matches_oracle(case):
     assert ctx.stream_block_host(0, 80, d, writes) == f
     assert ctx.block_length(79) == n
     assert ctx.stream_file_decode(0, f, n) == d.tobytes()
-    for codec in (3, 7):                                          # LZOP not built; 7 unknown
+    for codec in (1, 7):                                          # not stream codecs
         with pytest.raises(HdrfError):
             ctx.stream_block(codec, 78, dev, n, n + 4096, writes)
     ctx.dev_free(dev)
