@@ -82,7 +82,9 @@ def parse():
                          "batches overlap while the front halves of the next ones run)")
     ap.add_argument("--alone", action="store_true",
                     help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
-                         "batches (off by default so a rocprof summary of the bench matches its in-pipeline averages)")
+                         "batches (on by default for the config-2 line; --no-alone when the bench runs under a "
+                         "profiler whose summary must hold only the timed pipeline's kernels)")
+    ap.add_argument("--no-alone", action="store_true")
     ap.add_argument("--arena-slots", type=int, default=0,
                     help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers "
                          "(default 512; config4 1280, so a ring also holds the closes of the batch whose LZ4 "
@@ -281,7 +283,8 @@ def main():
     el = time.perf_counter() - t0
     stage_ms = ctx.stage_times(reset=True)
     alone_ms = None
-    if a.alone and node is None and not a.serial and not host:
+    alone = (a.alone or (a.workload == "config2" and not a.no_alone)) and not a.no_alone
+    if alone and node is None and not a.serial and not host:
         # one extra, untimed serial pass (one batch at a time): the same kernels without the
         # co-running batch, for the per-kernel "alone" rooflines next to the in-pipeline ones
         ctx.reset()
@@ -385,6 +388,11 @@ def main():
         if ra.get(STAGES[2]) and sha_prof.get("sq_insts_valu"):
             ra[STAGES[2]]["valu_frac"] = round(sha_prof["sq_insts_valu"] / (ra[STAGES[2]]["avg_launch_ms"] * 1e6)
                                               / VALU_PEAK_WI_NS, 4)
+        w_alone = sum(alone_ms[STAGES.index(x)] for x in CHAINS["W: chunking"]) / nbatch
+        if w_alone > 0:
+            ach = S_batch / (w_alone * 1e-3) / 1e9
+            ra["chunking(gmax+walk+stitch)"] = {"avg_batch_ms": round(w_alone, 4), "achieved_GB_s": round(ach, 1),
+                                                "frac_hbm": round(ach / HBM_PEAK_GBS, 4)}
         roofline["alone"] = ra
         roofline["alone_note"] = ("same kernels in one untimed serial pass (one batch at a time); the "
                                   "in-pipeline figures above include co-running batches")

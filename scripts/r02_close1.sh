@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 V=${V:-v3}
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/final_tests_$V.log 2>&1 || { tail -30 gpurun_out/final_tests_$V.log; exit 1; }
 tail -1 gpurun_out/final_tests_$V.log
-TAG=prof_$V BENCH="--steps 2 --warmup 1 --no-cpu" bash scripts/r02_prof.sh > gpurun_out/prof_$V.txt 2>&1 || { tail -20 gpurun_out/prof_$V.txt; exit 1; }
+TAG=prof_$V BENCH="--steps 2 --warmup 1 --no-cpu --no-alone" bash scripts/r02_prof.sh > gpurun_out/prof_$V.txt 2>&1 || { tail -20 gpurun_out/prof_$V.txt; exit 1; }
 head -6 gpurun_out/prof_$V.txt | cut -c1-160
 TAG=r02_$V EXTRA_GROUPS="SQ_INSTS_VALU" bash scripts/r02_traffic.sh > gpurun_out/traffic_$V.txt 2>&1 || { tail -20 gpurun_out/traffic_$V.txt; exit 1; }
 cp gpurun_out/r02_${V}_traffic.json profiles/r02_${V}_traffic.json

@@ -4,7 +4,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${TAG:-r02}
-ARGS=${ARGS:-"--steps 1 --warmup 0 --no-cpu"}
+ARGS=${ARGS:-"--steps 1 --warmup 0 --no-cpu --no-alone"}
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
