@@ -957,21 +957,24 @@ static int wait_one(hdrf_ctx *ctx)
 // chunks alternate, waiting (host side) for a chunk's copy only before refilling it.  The packets
 // of one block come from one receiver thread (the reference's BlockReceiver), so appends take
 // only that buffer's state, not the context lock: receivers of different blocks copy in parallel.
-static int rx_flush(hdrf_ctx *ctx, hdrf_ctx::Rx &r)
+// (touches only the receive buffer and stream C, so it runs without the context lock; the caller
+// records an error under the lock)
+static hipError_t rx_flush(hdrf_ctx *ctx, hdrf_ctx::Rx &r)
 {
-    if (r.fill == 0) return 0;
+    if (r.fill == 0) return hipSuccess;
     const int c = r.cur;
-    HIPCK(hipMemcpyAsync(r.d + r.dst, r.h + (uint64_t)c * hdrf_ctx::kRingChunk, r.fill, hipMemcpyHostToDevice,
-                         ctx->stC));
-    HIPCK(hipEventRecord(r.ev[c], ctx->stC));
+    hipError_t e = hipMemcpyAsync(r.d + r.dst, r.h + (uint64_t)c * hdrf_ctx::kRingChunk, r.fill, hipMemcpyHostToDevice,
+                                  ctx->stC);
+    if (e == hipSuccess) e = hipEventRecord(r.ev[c], ctx->stC);
+    if (e != hipSuccess) return e;
     r.busy[c] = true;
     r.cur = c ^ 1;
     r.fill = 0;
     if (r.busy[r.cur]) {                               // refilling that chunk: its copy must have landed
-        HIPCK(hipEventSynchronize(r.ev[r.cur]));
+        if ((e = hipEventSynchronize(r.ev[r.cur])) != hipSuccess) return e;
         r.busy[r.cur] = false;
     }
-    return 0;
+    return hipSuccess;
 }
 
 extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
@@ -1019,10 +1022,10 @@ extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data
         data += n;
         len -= n;
         if (r.fill == hdrf_ctx::kRingChunk) {
-            const int rc = rx_flush(ctx, r);
-            if (rc) {
+            const hipError_t e = rx_flush(ctx, r);
+            if (e != hipSuccess) {
                 HDRF_LOCK(ctx);
-                return rc;
+                return set_err(ctx, HDRF_E_HIP, std::string("packet copy: ") + hipGetErrorString(e));
             }
         }
     }
@@ -1037,7 +1040,7 @@ extern "C" int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx)
     if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)     // every submit pairs with one hdrf_wait_batch
         return set_err(ctx, HDRF_E_CAPACITY, "pipeline full: hdrf_wait_batch first");
     hdrf_ctx::Rx &r = ctx->rx[rx];
-    if (int rc = rx_flush(ctx, r)) return rc;
+    HIPCK(rx_flush(ctx, r));
     HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, ctx->stC));
     Slot &S = ctx->sl[ctx->nsub % kSlots];
     HIPCK(hipEventRecord(S.copy_done, ctx->stC));
