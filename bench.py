@@ -418,6 +418,12 @@ def main():
                        "lz4_ratio_closed": round(st["closed_raw_bytes"] / max(st["closed_file_bytes"], 1), 6),
                        "node_ratio": round(st["logical_bytes"] / max(stored, 1), 6),
                        "node_ratio_def": "logical / (closed Lz4Codec files + open raw containers)"}
+        # SURVEY §8(d)'s config-4 ratio also counts the metadata the reference keeps in Redis: the
+        # recipes (BE32 size + digests per block) and one index entry (digest key + 11-B value) per
+        # distinct chunk
+        meta = st["recipe_bytes"] + ctx.index_count() * (ctx.H + 11)
+        compression.update({"recipe_bytes": st["recipe_bytes"], "index_bytes": meta - st["recipe_bytes"],
+                            "node_ratio_with_metadata": round(st["logical_bytes"] / max(stored + meta, 1), 6)})
     read_side = None
     if rank == 0 and world == 1 and a.read_blocks > 0 and not host:
         read_side = read_bench(ctx, dev, S, min(a.read_blocks, nb), a.hasher, compressor)

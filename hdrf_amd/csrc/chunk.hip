@@ -863,7 +863,12 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
 //      count  one thread per segment: its piece (first list index, cuts, repair cuts) + workgroup sums
 //      scan   one workgroup per block: prefix over the workgroup sums; n_cuts / fail_dst
 //      copy   one thread per segment: workgroup prefix -> destination; the piece is copied
-constexpr int kStitchNodes = 2048;       // irregular boundaries per block followed (more: fallback there)
+// Irregular boundaries per block followed (more: the fallback takes over there, exact either way).
+// The LDS this sizes (path 17 KiB, count 16.5 KiB) does not fit beside a compressor-2 LZ4 pass at
+// 16 waves per CU (16 KiB left), so in config 4 the stitch kernels of the next batches run in the
+// pass tails; with 1024 nodes they co-run with the pass and config 4 drops from 33 to 27 GB/s
+// (stitch stage 70 -> 115 ms, profiles/r02_c4_stitch1024_ab.txt): kept at 2048.
+constexpr int kStitchNodes = 2048;
 
 __global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__restrict__ blocks,
                                                           const uint32_t *__restrict__ irr,

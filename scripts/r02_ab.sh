@@ -16,6 +16,6 @@ st = d["stages"]
 short = {k.split("(")[0]: v["avg_launch_ms"] for k, v in st.items()}
 print(sys.argv[2], "=>", d["value"], "GB/s", {k: v for k, v in short.items() if v > 0.05})
 if "alone" in d["roofline"]:
-    print("   alone:", {k.split("(")[0]: v["avg_launch_ms"] for k, v in d["roofline"]["alone"].items()})
+    print("   alone:", {k.split("(")[0]: v.get("avg_launch_ms", v.get("avg_batch_ms")) for k, v in d["roofline"]["alone"].items()})
 PY
 done < ${VARIANTS:-/dev/stdin}

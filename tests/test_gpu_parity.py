@@ -47,6 +47,15 @@ def test_many_segments_random_large():
         run_sequence([blk], segment_bytes=seg)
 
 
+@pytest.mark.parametrize("kind", ["periodic", "zeros", "text", "sparse"])
+def test_more_boundaries_than_stitch_nodes(kind):
+    """A 132 MiB block at 64 KiB segments has 2112 segment boundaries, more than the 2048 irregular
+    ones the stitch path follows in LDS (chunk.hip kStitchNodes): past them the fallback walk takes
+    over, with the same cuts."""
+    blk = make_block(kind, 23, 132 * 1024 * 1024 + 77)
+    run_sequence([blk], segment_bytes=1 << 16, max_block_bytes=136 << 20, max_batch_blocks=1)
+
+
 def test_cross_block_dups_and_intra_block_dups():
     a = make_block("random", 1, 600_000)
     b = make_block("random", 2, 400_000)
