@@ -82,6 +82,7 @@ struct Slot {
     AllocState *h_alloc = nullptr;
     int *h_err = nullptr;
     uint32_t *h_nclosed = nullptr;
+    uint32_t *h_long = nullptr;               // the batch held chunks for the long SHA lanes (queue[64])
     ClosedRec *h_closed = nullptr;
     uint32_t *h_filelen = nullptr;
     BlockDesc *h_desc = nullptr;
@@ -115,6 +116,9 @@ struct hdrf_ctx {
     hipStream_t stW = nullptr;   // stream W: chunking stage
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
     hipStream_t stL[2] = {};     // compressor 2: LZ4 streams, alternating by batch (off stream B)
+    // chunks >= 64 KiB were seen in the last completed batch: sha_full hashes them on dedicated
+    // lanes (sha.hip); off otherwise, where the scan for them costs config 2 ~3 %
+    bool sha_long = false;
     int max_batch = 0, cap_blk = 0, ntiles = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
     Slot sl[kSlots];
     uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
@@ -298,7 +302,7 @@ static void free_slot(Slot &S)
                    S.d_lzwork};
     for (void *p : dev)
         if (p) (void)hipFree(p);
-    void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_closed, S.h_filelen, S.h_desc};
+    void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_long, S.h_closed, S.h_filelen, S.h_desc};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
     hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done, S.placed, S.lz_done};
@@ -371,9 +375,9 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         (rc = dalloc(ctx, &S.d_closed, ctx->closed_cap)) || (rc = dalloc(ctx, &S.d_nclosed, 1)) ||
         (rc = dalloc(ctx, &S.d_coll, ctx->coll_cap)) || (rc = dalloc(ctx, &S.d_ncoll, 1)) ||
         (rc = dalloc(ctx, &S.d_pcid, nchunk)) || (rc = dalloc(ctx, &S.d_ppos, nchunk)) ||
-        (rc = dalloc(ctx, &S.d_queue, 64)) || (rc = dalloc(ctx, &S.d_err, 1)) ||
+        (rc = dalloc(ctx, &S.d_queue, 128)) || (rc = dalloc(ctx, &S.d_err, 1)) ||
         (rc = halloc(ctx, &S.h_bst, B)) || (rc = halloc(ctx, &S.h_store, B)) || (rc = halloc(ctx, &S.h_alloc, 1)) ||
-        (rc = halloc(ctx, &S.h_err, 1)) || (rc = halloc(ctx, &S.h_nclosed, 1)) ||
+        (rc = halloc(ctx, &S.h_err, 1)) || (rc = halloc(ctx, &S.h_nclosed, 1)) || (rc = halloc(ctx, &S.h_long, 1)) ||
         (rc = halloc(ctx, &S.h_closed, ctx->closed_cap)) || (rc = halloc(ctx, &S.h_filelen, ctx->closed_cap)) ||
         (rc = halloc(ctx, &S.h_desc, B)))
         return rc;
@@ -745,7 +749,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(A, S.recipe_done, 0));
     Marker ma;
     ma.ev = ctx->timing ? S.evA : nullptr;
-    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig, S.d_queue, A,
+    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig, S.d_queue, ctx->sha_long, A,
                      &ma));
     ma.mark(A);
     HIPCK(hipEventRecord(S.front_done, A));
@@ -804,6 +808,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, Bst));
+    HIPCK(hipMemcpyAsync(S.h_long, S.d_queue + 64, sizeof(uint32_t), hipMemcpyDeviceToHost, Bst));
     HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, Bst));
     HIPCK(hipEventRecord(S.back_done, Bst));
     S.pending = true;
@@ -877,6 +882,7 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
     const hdrf_cfg &c = ctx->cfg;
     const int nblocks = S.nblocks;
     const uint32_t nclosed = *S.h_nclosed;
+    ctx->sha_long = *S.h_long != 0;               // long SHA lanes for the next submissions
     if ((int)nclosed > ctx->closed_cap) return set_err(ctx, HDRF_E_CAPACITY, "closed-container list overflow");
     ctx->inflight_bound -= std::min(ctx->inflight_bound, S.close_bound);
     S.close_bound = 0;
@@ -1770,7 +1776,7 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
                           st, &mk));
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
-                     S.d_queue, st, &mk));
+                     S.d_queue, ctx->sha_long, st, &mk));
     // local aggregation: a fresh scratch table, every entry "created" in batch 1
     HIPCK(hipMemsetAsync(ctx->d_scratch[si], 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_scratch[si],

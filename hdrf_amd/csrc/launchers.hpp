@@ -49,7 +49,7 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
                            Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
-                      hipStream_t st, Marker *mk);
+                      bool long_lanes, hipStream_t st, Marker *mk);   // queue: 65 words; [64] = long chunks seen
 hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals, int n, IndexEntry *tab, int log2cap,
                              unsigned long long tag_mask, int *err, hipStream_t st);
 // GzipCodec read side (inflate.hip): one raw deflate stream -> dst; res[0] = length or < 0, res[1] =

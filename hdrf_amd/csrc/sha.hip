@@ -158,22 +158,140 @@ __device__ __forceinline__ void set_iv(uint32_t st[8])
     }
 }
 
-// grid (waves_per_block/4, nblocks): every wave serves chunks of block b.  A lane owns one chunk's
-// compression chain; chunk offsets come from coalesced per-wave reservations of 64 chunks kept in
-// registers (pool P, with the next reservation Q fetched while P is consumed), so a lane that
-// finishes its chain takes the next chunk with two ds_bpermutes and no memory round trip.
+// One iteration of a lane's compression chain: two consecutive blocks from one 132-B window (one
+// when a single full block is left).  Each 128-B line of the chunk is fetched once per pair instead
+// of by two compressions far apart in time (L2 misses).
 #ifndef HDRF_SHA_PAIRS
 #define HDRF_SHA_PAIRS 1
 #endif
 constexpr bool kPairs = HDRF_SHA_PAIRS != 0;
 
 template <int HW>
+__device__ __forceinline__ void sha_step(const uint8_t *base, uint32_t &pos, uint32_t &r, uint32_t st[8])
+{
+    if (kPairs) {
+        const bool two = r >= 2;
+        const uint32_t apos = pos & ~3u;
+        const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
+        const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
+        uint32_t d[33];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
+            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+        }
+        d[16] = p[16];
+        if (two) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 17 + 4 * q);
+                d[17 + 4 * q] = v.x; d[18 + 4 * q] = v.y; d[19 + 4 * q] = v.z; d[20 + 4 * q] = v.w;
+            }
+        }
+        uint32_t m[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+        if (HW == 5) sha1_compress(st, m);
+        else sha256_compress(st, m);
+        if (two) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 17], d[i + 16], sel);
+            if (HW == 5) sha1_compress(st, m);
+            else sha256_compress(st, m);
+        }
+        pos += two ? 128 : 64;
+        r -= two ? 2 : 1;
+    } else {
+        uint32_t m[16];
+        load_full(base, pos, m);
+        if (HW == 5) sha1_compress(st, m);
+        else sha256_compress(st, m);
+        pos += 64;
+        r--;
+    }
+}
+
+// Long chunks (>= kShaLong bytes: forced cuts of low-entropy runs, up to max_chunk) are hashed by
+// dedicated lanes, packed densely.  A chunk's chain is sequential (Merkle-Damgard), so a 1 MB chunk
+// keeps its lane busy for 15,625 compressions; left in the per-block queue it sits in a wave whose
+// other lanes ran out of chunks, spending a whole SIMD's VALU issue on one lane for tens of
+// milliseconds beside the co-running stages (config 4's mixed-entropy blocks hold ~15 % of their
+// bytes in such chunks: SHA alone 61 -> 26 ms per batch, config 4 33.5 -> 35.8 GB/s).  The scan
+// for them costs config 2 (no long chunks) ~3 %, so the lanes run only while the caller's recent
+// batches held long chunks (queue[64], set by the queue consumers whichever mode ran).  The
+// workgroups at y = 0 of sha_full (dispatched first) scan the offsets of every block (workgroup x
+// takes 1024-chunk tiles x, x + gridDim.x, ...), compact the long chunks into LDS and hash them one
+// lane each; the queue consumers skip them.  A separate list kernel ahead of sha_full cost config 2
+// 4 % (one more dependent launch on the SHA stream).
+constexpr uint32_t kShaLong = 65536;
+constexpr int kShaTile = 1024;                 // chunks per scan tile (4 per thread)
+
+// grid (waves_per_block/4, nblocks): every wave serves chunks of block b.  A lane owns one chunk's
+// compression chain; chunk offsets come from coalesced per-wave reservations of 64 chunks kept in
+// registers (pool P, with the next reservation Q fetched while P is consumed), so a lane that
+// finishes its chain takes the next chunk with two ds_bpermutes and no memory round trip.
+template <int HW>
 __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restrict__ blocks,
                                                        const uint32_t *__restrict__ offsets,
                                                        const BlockState *__restrict__ bst, int cap_blk,
-                                                       uint32_t *__restrict__ mid, uint32_t *__restrict__ queue)
+                                                       uint32_t *__restrict__ mid, uint32_t *__restrict__ queue,
+                                                       uint32_t thr)
 {
-    const int b = blockIdx.y;
+    if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
+        if (thr == 0xffffffffu) return;
+        __shared__ uint32_t s_long[kShaTile + 256];
+        __shared__ uint32_t s_nl;
+        const int t = threadIdx.x;
+        if (t == 0) s_nl = 0;
+        __syncthreads();
+        auto drain = [&]() {                       // every listed chunk: one lane's chain
+            const uint32_t nl = s_nl;
+            for (uint32_t i = t; i < nl; i += 256) {
+                const uint32_t e = s_long[i];
+                const int lb = (int)(e >> 24), lk = (int)(e & 0xffffffu);
+                const uint32_t *lo = offsets + (size_t)lb * cap_blk;
+                uint32_t pos = lk ? lo[lk - 1] : 0u;
+                uint32_t r = (lo[lk] - pos) >> 6;
+                uint32_t st[8];
+                set_iv<HW>(st);
+                const uint8_t *lbase = blocks[lb].data;
+                while (r) sha_step<HW>(lbase, pos, r, st);
+                uint32_t *dst = mid + ((size_t)lb * cap_blk + lk) * 8;
+#pragma unroll
+                for (int j = 0; j < (HW == 5 ? 5 : 8); j++) dst[j] = st[j];
+            }
+            __syncthreads();
+            if (t == 0) s_nl = 0;
+            __syncthreads();
+        };
+        const int nblk = (int)gridDim.y - 1;
+        for (int lb = 0; lb < nblk; lb++) {
+            const int n = bst[lb].n_chunks;
+            const uint32_t *lo = offsets + (size_t)lb * cap_blk;
+            for (int tb = blockIdx.x * kShaTile; tb < n; tb += gridDim.x * kShaTile) {
+                const int k0 = tb + 4 * t;
+                uint32_t o[5];
+#pragma unroll
+                for (int j = 0; j < 5; j++) {
+                    const int k = k0 - 1 + j;
+                    o[j] = (k >= 0 && k < n) ? lo[k] : 0u;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (k0 + j < n && o[j + 1] - o[j] >= thr) s_long[atomicAdd(&s_nl, 1u)] = ((uint32_t)lb << 24) | (uint32_t)(k0 + j);
+                __syncthreads();
+                const uint32_t cnt = s_nl;
+                __syncthreads();
+                if (cnt >= 256) drain();          // <= 255 + kShaTile entries at any time
+            }
+        }
+        __syncthreads();
+        const uint32_t cnt = s_nl;
+        __syncthreads();
+        if (cnt) drain();
+        return;
+    }
+    const int b = blockIdx.y - 1;
     const int n = bst[b].n_chunks;
     const uint8_t *base = blocks[b].data;
     const uint32_t *off = offsets + (size_t)b * cap_blk;
@@ -217,7 +335,10 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
             const int idx = min(head + rank, 63);
             const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), s0 = (uint32_t)__shfl((int)SP, idx, 64);
             bool zero = false;
-            if (!active && rank < avail) {
+            if (ballot64(!active && rank < avail && e - s0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
+            if (!active && rank < avail && e - s0 >= thr) {
+                zero = true;                      // a long chunk: hashed by the long lanes, take another
+            } else if (!active && rank < avail) {
                 k = kbP + head + rank;
                 pos = s0;
                 r = (e - s0) >> 6;
@@ -235,50 +356,7 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
             if (!ballot64(zero) && nidle <= avail) break;
         }
         if (!ballot64(active)) break;
-        if (active) {
-            if (kPairs) {
-                // two consecutive blocks from one 132-B window: each 128-B line of the chunk is
-                // fetched once per pair instead of by two compressions far apart in time (L2 misses)
-                const bool two = r >= 2;
-                const uint32_t apos = pos & ~3u;
-                const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
-                const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
-                uint32_t d[33];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
-                    d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-                }
-                d[16] = p[16];
-                if (two) {
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 17 + 4 * q);
-                        d[17 + 4 * q] = v.x; d[18 + 4 * q] = v.y; d[19 + 4 * q] = v.z; d[20 + 4 * q] = v.w;
-                    }
-                }
-                uint32_t m[16];
-#pragma unroll
-                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
-                if (HW == 5) sha1_compress(st, m);
-                else sha256_compress(st, m);
-                if (two) {
-#pragma unroll
-                    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 17], d[i + 16], sel);
-                    if (HW == 5) sha1_compress(st, m);
-                    else sha256_compress(st, m);
-                }
-                pos += two ? 128 : 64;
-                r -= two ? 2 : 1;
-            } else {
-                uint32_t m[16];
-                load_full(base, pos, m);
-                if (HW == 5) sha1_compress(st, m);
-                else sha256_compress(st, m);
-                pos += 64;
-                r--;
-            }
-        }
+        if (active) sha_step<HW>(base, pos, r, st);
     }
 }
 
@@ -316,10 +394,19 @@ __global__ void __launch_bounds__(256) sha_tail_kernel(const BlockDesc *__restri
 
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
-                      hipStream_t st, Marker *mk)
+                      bool long_lanes, hipStream_t st, Marker *mk)
 {
-    if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t) * nblocks, st)) return e;
+    if (nblocks > 64) return hipErrorInvalidValue;
+    if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t) * 65, st)) return e;
     mk->mark(st);
+    // HDRF_SHA_LONG: long-chunk threshold in bytes (>= kShaLong; 0 = no long lanes, for A/B runs)
+    // (the caller turns the lanes on while its batches hold long chunks: queue[64], set by sha_full)
+    static const uint32_t thr_env = [] {
+        const char *e = getenv("HDRF_SHA_LONG");
+        const long v = e ? atol(e) : (long)kShaLong;
+        return v <= 0 ? 0xffffffffu : (uint32_t)std::max<long>(v, kShaLong);
+    }();
+    const uint32_t thr = long_lanes ? thr_env : 0xffffffffu;
     // 2 waves per SIMD (r02, pipelined with chunking on its own stream: 992 GB/s vs 940 at 3 and
     // 919 at 4) — fewer concurrent per-lane streams thrash L2 less and leave CUs to the
     // co-running place / granule passes; env knobs for
@@ -327,14 +414,14 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : 2; }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     const int wpb = std::max(4, (per_simd * 1024 / nblocks) & ~3);
-    dim3 gf(wpb / 4, nblocks);
+    dim3 gf(wpb / 4, nblocks + 1);                 // y = 0: the long-chunk lanes
     dim3 gt((cap_blk + 255) / 256, nblocks);
     if (hasher == 0) {
-        hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue);
+        hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
         mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<5>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     } else {
-        hipLaunchKernelGGL(sha_full_kernel<7>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue);
+        hipLaunchKernelGGL(sha_full_kernel<7>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
         mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<7>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     }

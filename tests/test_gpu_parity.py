@@ -56,6 +56,18 @@ def test_more_boundaries_than_stitch_nodes(kind):
     run_sequence([blk], segment_bytes=1 << 16, max_block_bytes=136 << 20, max_batch_blocks=1)
 
 
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_long_chunk_sha_lanes(hasher):
+    """Chunks >= 64 KiB (the config-4 corpus's text segments hold forced 1,000,000-B cuts) are
+    hashed on sha_full's dedicated long lanes once a completed batch has shown them (sha.hip): the
+    first blocks run without them, the later ones with them, all bit-exact."""
+    roots = corpus_roots(3, 0, 1, 24)
+    mixed = corpus_block_host(3, roots, 0, 24, 1 << 20, mixed=True)
+    r = make_block("random", 2, 700_000)
+    blocks = [r, mixed[: 12 << 20], np.concatenate([r, mixed[5 << 20:]]), mixed[::-1].copy(), mixed]
+    run_sequence(blocks, hasher=hasher, max_block_bytes=32 << 20)
+
+
 def test_cross_block_dups_and_intra_block_dups():
     a = make_block("random", 1, 600_000)
     b = make_block("random", 2, 400_000)
