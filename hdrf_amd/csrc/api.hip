@@ -765,8 +765,12 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     // When batches are pipelined (one already in flight), this batch's place kernel overlaps the
     // next batch's front stage (the critical path): a dynamic-LDS reservation caps place at one
     // wave per SIMD so SHA keeps its wave slots (measured +1.5-2% on the config-2 bench; alone,
-    // place wants full occupancy).  HDRF_PLACE_LDS overrides the reservation (bytes).
-    static const int place_lds = [] { const char *e = getenv("HDRF_PLACE_LDS"); return e ? atoi(e) : 40960; }();
+    // place wants full occupancy).  Under compressor 2 the reservation is 16 KiB: place then fits on
+    // a CU as soon as one LZ4 wave of a draining pass leaves it (config 4: 36.96 / 37.01 vs 35.92 /
+    // 35.91 GB/s with 40 KiB; 24 KiB 36.5, 9 KiB 36.4; profiles/r02_c4_place_ab.txt).
+    // HDRF_PLACE_LDS overrides the reservation (bytes).
+    static const int place_lds_env = [] { const char *e = getenv("HDRF_PLACE_LDS"); return e ? atoi(e) : -1; }();
+    const int place_lds = place_lds_env >= 0 ? place_lds_env : (c.compressor == 2 ? 16384 : 40960);
     if (ctx->nsub > ctx->nwait) P.place_lds = place_lds;
     if (c.compressor == 2) {
         // The compression of earlier batches runs on the LZ4 streams, off stream B, so batch k+1's
