@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
             const uint32_t nl = s_nl;
             for (uint32_t i = t; i < nl; i += 256) {
                 const uint32_t e = s_long[i];
-                const int lb = (int)(e >> 24), lk = (int)(e & 0xffffffu);
+                const int lb = (int)(e >> 26), lk = (int)(e & 0x3ffffffu);   // block < 64, chunk < cap_blk < 2^26
                 const uint32_t *lo = offsets + (size_t)lb * cap_blk;
                 uint32_t pos = lk ? lo[lk - 1] : 0u;
                 uint32_t r = (lo[lk] - pos) >> 6;
@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
                 }
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-                    if (k0 + j < n && o[j + 1] - o[j] >= thr) s_long[atomicAdd(&s_nl, 1u)] = ((uint32_t)lb << 24) | (uint32_t)(k0 + j);
+                    if (k0 + j < n && o[j + 1] - o[j] >= thr) s_long[atomicAdd(&s_nl, 1u)] = ((uint32_t)lb << 26) | (uint32_t)(k0 + j);
                 __syncthreads();
                 const uint32_t cnt = s_nl;
                 __syncthreads();
