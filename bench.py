@@ -5,8 +5,8 @@ Workload (per GPU): a synthetic corpus of 512 blocks x 128 MiB (64 GiB) resident
 1 MiB segments, 50% of them copies of a segment of an EARLIER block (cross-block
 duplicates).  One step = one DataNode reducing the whole corpus in block
 order from a fresh index: window-max chunking -> SHA-1 -> GPU index (exact HDRF dedup
-semantics) -> container placement + gather into the container arena, in batches of 64
-blocks.  value = logical bytes reduced per second over all ranks (GB = 1e9 B).
+semantics) -> container placement + gather into the container arena, in batches of 32
+blocks (4 GiB), three batches in flight.  value = logical bytes reduced per second over all ranks (GB = 1e9 B).
 
 Multi-GPU (`torch.distributed.run`, BASELINE config 3): the GPUs of the node are ranks of ONE
 reduction, as the DataNodes of one host share one Redis, allocator and chunkDir in the reference
@@ -68,7 +68,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=20251015)
     ap.add_argument("--index-log2", type=int, default=27)
     ap.add_argument("--hasher", type=int, default=0)
-    ap.add_argument("--cpu-sample-blocks", type=int, default=24)
+    ap.add_argument("--cpu-sample-blocks", type=int, default=0,
+                    help="blocks of the CPU baseline sample (default: the first batch, checked chunk by chunk)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--serial", action="store_true",
                     help="one batch at a time (no stream overlap): clean per-kernel stage times")
@@ -429,8 +430,21 @@ def main():
     if rank == 0 and world == 1 and a.read_blocks > 0 and not host:
         read_side = read_bench(ctx, dev, S, min(a.read_blocks, nb), a.hasher, compressor)
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu and a.cpu_sample_blocks > 0:
-        cpu = cpu_baseline(ctx, dev, S, min(a.cpu_sample_blocks, nb), store, a.hasher, compressor)
+    m_cpu = min(a.cpu_sample_blocks or B, nb)
+    if rank == 0 and world == 1 and not a.no_cpu and m_cpu > 0:
+        # the GPU's per-chunk results for the sample (one untimed pass from a fresh index, the same
+        # batches as the timed steps), checked chunk by chunk against the all-cores oracle run
+        ctx.reset()
+        gpu_res, done = [], 0
+        for ptrs, lens, rd, ids in batches:
+            if done >= m_cpu:
+                break
+            ctx.reduce_batch(ptrs, lens, rd, ids)
+            for i in range(ctx.last_nblocks()):
+                if done < m_cpu:
+                    gpu_res.append(ctx.batch_result(i))
+                    done += 1
+        cpu = cpu_baseline(ctx, dev, S, m_cpu, store, a.hasher, compressor, gpu_res)
 
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
@@ -502,7 +516,7 @@ def read_bench(ctx, dev, S, m, hasher, compressor):
                     "one block per call (host round trip each)"}
 
 
-def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1):
+def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1, gpu_res=None):
     """CPU oracle (C restatement of the reference) on the first m blocks of the same corpus, timed
     in BASELINE.md's two shapes plus one thread:
       reference  the reference's own concurrency, blocks serialised: per block 1 chunking thread,
@@ -510,8 +524,10 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1):
                  (DN/DataDeduplicator.java:122-204, :578-641)
       all_cores  every usable core (sched_getaffinity): chunk + hash of later blocks on N-1 worker
                  threads ahead of 1 ordered index/store thread
-    All check per-block storeSize == the GPU's (bit-exact dedup ratio); for the compression stage a
-    fresh GPU context reducing the same m blocks must write byte-identical container files."""
+    All check per-block storeSize == the GPU's (bit-exact dedup ratio); the all-cores run also
+    returns every block's chunk END offsets, digests and is_new, compared chunk by chunk with the
+    GPU's (gpu_res); for the compression stage a fresh GPU context reducing the same m blocks
+    must write byte-identical container files."""
     from oracle.oracle import Oracle
     blks = [ctx.d2h(dev + b * S, S) for b in range(m)]
     ids = list(range(m))
@@ -527,8 +543,21 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1):
     nthr = max(1, usable - 1)
     par = Oracle(hasher=hasher, compressor=compressor)
     t0 = time.perf_counter()
-    ssp = par.reduce_many(blks, ids, nthr)
+    full = par.reduce_many_full(blks, ids, nthr)
     tp = time.perf_counter() - t0
+    ssp = [r["store_size"] for r in full]
+    chunk_bad = {"offsets": 0, "digests": 0, "is_new": 0}
+    n_chunks = 0
+    for b, r in enumerate(full):
+        g = gpu_res[b] if gpu_res is not None and b < len(gpu_res) else None
+        n_chunks += len(r["offsets"])
+        if g is None or len(g["offsets"]) != len(r["offsets"]):
+            for k in chunk_bad:
+                chunk_bad[k] += len(r["offsets"])
+            continue
+        chunk_bad["offsets"] += int((g["offsets"] != r["offsets"]).sum())
+        chunk_bad["digests"] += int((g["digests"] != r["digests"]).any(axis=1).sum())
+        chunk_bad["is_new"] += int((g["is_new"] != r["is_new"]).sum())
 
     def mism(ss):
         return int(sum(int(ss[b] != gpu_store[b]) for b in range(m)))
@@ -538,7 +567,11 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1):
     out = {"value": round(m * S / tp / 1e9, 4), "unit": "GB/s", "cores": nthr + 1, "kind": "port",
            "sample": sample + ", all usable cores: %d chunk+hash worker threads + 1 ordered index/store thread, %.1f s"
                      % (nthr, tp),
-           "store_size_mismatches": mism(ssp), "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+           "store_size_mismatches": mism(ssp),
+           "chunk_check": {"blocks": m, "chunks": n_chunks, "mismatches": chunk_bad,
+                           "what": "per chunk: END offset, digest, is_new (GPU from a fresh index over the same "
+                                   "batches vs the oracle in block order)"},
+           "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
            "usable_cores": usable,
            "reference_shape": {"value": round(m * S / tr / 1e9, 4), "unit": "GB/s", "cores": 4,
                                "threads": "per block 1 chunking + 3 hasher threads, then the ordered part; "

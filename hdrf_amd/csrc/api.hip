@@ -569,6 +569,10 @@ extern "C" int hdrf_reset(hdrf_ctx *ctx)
 {
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
+    // a receiver may still be appending to a buffer without the lock: refuse rather than race it
+    for (int i = 0; i < hdrf_ctx::kRx; i++)
+        if (ctx->rx[i].state.load() == 1)
+            return set_err(ctx, HDRF_E_INVAL, "a block is being received (hdrf_submit_slot or hdrf_rx_cancel first)");
     return init_state(ctx);
 }
 
@@ -1019,7 +1023,7 @@ extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data
         return set_err(ctx, HDRF_E_INVAL, "bad receive buffer or packet");
     }
     hdrf_ctx::Rx &r = ctx->rx[rx];
-    if (r.len + len > (uint64_t)ctx->cfg.max_block_bytes) {
+    if (len > (uint64_t)ctx->cfg.max_block_bytes - r.len) {       // r.len <= max_block_bytes: no wrap
         HDRF_LOCK(ctx);
         return set_err(ctx, HDRF_E_INVAL, "block larger than max_block_bytes");
     }
@@ -1039,6 +1043,26 @@ extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data
             }
         }
     }
+    return 0;
+}
+
+// A receive the DataNode abandons (client lost mid-block: the reference drops bf1): the buffer's
+// staging copies are waited for and the buffer is free again.  The receiver thread must have
+// stopped appending to it.
+extern "C" int hdrf_rx_cancel(hdrf_ctx *ctx, int32_t rx)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state.load() != 1)
+        return ctx ? set_err(ctx, HDRF_E_INVAL, "bad receive buffer (not receiving)") : HDRF_E_INVAL;
+    hdrf_ctx::Rx &r = ctx->rx[rx];
+    for (int c = 0; c < 2; c++)
+        if (r.busy[c]) {
+            HIPCK(hipEventSynchronize(r.ev[c]));
+            r.busy[c] = false;
+        }
+    r.len = r.fill = r.dst = 0;
+    r.cur = 0;
+    r.state.store(0);
     return 0;
 }
 

@@ -103,7 +103,7 @@ int hdrf_reduce_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_
  * first), so every submit pairs with exactly one wait.  The device buffers of a batch must stay
  * valid until it is completed.  Chunking of batch k+1 overlaps hashing of batch k and the
  * index/store stage of batch k-1 (latency-bound walk, VALU-bound SHA, HBM-bound store); the
- * bench keeps two batches in flight (five under compressor 2, where a batch's LZ4 pass outlasts
+ * bench keeps three batches in flight (five under compressor 2, where a batch's LZ4 pass outlasts
  * the front halves of the next ones).  Views (index, containers, allocator) complete all batches
  * first. */
 #define HDRF_PIPELINE_DEPTH 5
@@ -128,10 +128,15 @@ int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_
  * hdrf_submit_slot submits the received block as a one-block batch with no copy left (pair it
  * with hdrf_wait_batch like hdrf_submit_batch; HDRF_E_CAPACITY when the pipeline is full).  The
  * buffer is free again when that batch completes; hdrf_rx_begin returns HDRF_E_CAPACITY while all
- * eight are in use. */
+ * eight are in use.  hdrf_rx_cancel gives back a buffer whose block is abandoned (the client was
+ * lost mid-block; the reference drops bf1): its receiver must have stopped appending.  A packet
+ * that would take the block past max_block_bytes is refused (HDRF_E_INVAL) and copies nothing.
+ * hdrf_reset refuses (HDRF_E_INVAL) while a buffer is receiving; hdrf_close requires every
+ * receiver to have stopped. */
 int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx);
 int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data, uint64_t len);
 int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx);
+int hdrf_rx_cancel(hdrf_ctx *ctx, int32_t rx);
 /* Stream-mode schemes (DataNode.compressor 0/3/4/5: the whole block through a Hadoop codec,
  * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec, 0 = SnappyCodec, 3 = LzopCodec
  * (hadoop-lzo: LZO1X-1 blocks in an lzop file; the header's mtime is hdrf_set_lzop_mtime's value,
@@ -320,7 +325,8 @@ typedef struct {
 int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out);
 
 /* Reset the index, containers, allocator and recipes (a fresh DataNode + Redis); completes
- * the batches in flight first. */
+ * the batches in flight first.  HDRF_E_INVAL while a packet receive is open (hdrf_rx_begin not
+ * yet followed by hdrf_submit_slot or hdrf_rx_cancel). */
 int hdrf_reset(hdrf_ctx *ctx);
 
 /* ---- Node-global index over n_ranks GPUs (BASELINE config 3) -------------------

@@ -72,9 +72,9 @@ public final class HipReductionScheme extends ReductionScheme {
    * H2D copy runs on a side stream overlapped with the blocks already in flight.  `block` must
    * stay untouched until awaitOldest() has returned for it (keep a reference; BlockReceiver
    * allocates a fresh bf1 per block).  Completion is in submission order, like the FIFO
-   * (DataDeduplicator.java:124-158).  At most 3 blocks are in flight: a fourth reduceAsync throws
-   * IOException ("pipeline full") until awaitOldest() completed one, so every reduceAsync pairs
-   * with exactly one awaitOldest.
+   * (DataDeduplicator.java:124-158).  At most HDRF_PIPELINE_DEPTH (5, include/hdrf.h) blocks are in
+   * flight: a sixth reduceAsync throws IOException ("pipeline full") until awaitOldest() completed
+   * one, so every reduceAsync pairs with exactly one awaitOldest.
    */
   public void reduceAsync(ByteBuffer block, long blockId) throws IOException {
     if (!block.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
@@ -92,11 +92,22 @@ public final class HipReductionScheme extends ReductionScheme {
 
   public void packet(int rx, ByteBuffer pkt, int off, int len) throws IOException {
     if (!pkt.isDirect()) throw new IOException("HipReductionScheme needs a direct ByteBuffer");
+    if (off < 0 || len < 0 || off > pkt.capacity() - len)
+      throw new IOException("packet range [" + off + ", +" + len + ") outside the buffer");
     packet0(ctx, rx, pkt, off, len);
   }
 
   public void submitBlock(int rx) throws IOException {
     submitSlot0(ctx, rx);
+  }
+
+  /**
+   * Abandon a block being received (the client was lost mid-block; BlockReceiver drops bf1): the
+   * receive buffer is free again.  Call it from BlockReceiver's error path, after the receiver
+   * thread stopped calling packet().
+   */
+  public void abortBlock(int rx) throws IOException {
+    rxCancel0(ctx, rx);
   }
 
   /** Complete the oldest block submitted with reduceAsync (its index/containers/recipe are final). */
@@ -165,5 +176,6 @@ public final class HipReductionScheme extends ReductionScheme {
   private static native int rxBegin0(long ctx, long blockId) throws IOException;
   private static native void packet0(long ctx, int rx, ByteBuffer pkt, int off, int len) throws IOException;
   private static native void submitSlot0(long ctx, int rx) throws IOException;
+  private static native void rxCancel0(long ctx, int rx) throws IOException;
   private static native byte[] streamDecode0(long ctx, int codec, byte[] file, long blockId) throws IOException;
 }

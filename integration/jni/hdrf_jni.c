@@ -172,7 +172,9 @@ JNIEXPORT void JNICALL JFN(packet0)(JNIEnv *env, jclass cls, jlong h, jint rx, j
     (void)cls;
     hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
     const uint8_t *p = (const uint8_t *)(*env)->GetDirectBufferAddress(env, buf);
-    if (!p && len) { throw_io(env, ctx, HDRF_E_INVAL); return; }
+    const jlong cap = p ? (*env)->GetDirectBufferCapacity(env, buf) : 0;
+    /* a negative jint would become a huge uint64_t length: check the range before the library */
+    if (off < 0 || len < 0 || (jlong)off + (jlong)len > cap || (!p && len)) { throw_io(env, ctx, HDRF_E_INVAL); return; }
     int rc = hdrf_append_packet(ctx, rx, p + off, (uint64_t)len);   /* copied before return */
     if (rc) throw_io(env, ctx, rc);
 }
@@ -182,6 +184,14 @@ JNIEXPORT void JNICALL JFN(submitSlot0)(JNIEnv *env, jclass cls, jlong h, jint r
     (void)cls;
     hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
     int rc = hdrf_submit_slot(ctx, rx);
+    if (rc) throw_io(env, ctx, rc);
+}
+
+JNIEXPORT void JNICALL JFN(rxCancel0)(JNIEnv *env, jclass cls, jlong h, jint rx)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    int rc = hdrf_rx_cancel(ctx, rx);
     if (rc) throw_io(env, ctx, rc);
 }
 

@@ -523,6 +523,16 @@ static void *hash_worker(void *arg)
 int64_t hdrf_oracle_reduce_many(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
                                 const int64_t *ids, int64_t nblocks, int nthreads, int64_t *store_sizes)
 {
+    return hdrf_oracle_reduce_many_out(o, blocks, sizes, ids, nblocks, nthreads, store_sizes, NULL, NULL);
+}
+
+/* The same with every block's full result (the parity tests at the bench's batch shape):
+ * out[i] (may be NULL) receives what hdrf_oracle_reduce would write for block i, and
+ * counts[i] its chunk count; out[i].cap bounds the chunk arrays (-1 past it). */
+int64_t hdrf_oracle_reduce_many_out(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
+                                    const int64_t *ids, int64_t nblocks, int nthreads, int64_t *store_sizes,
+                                    const hdrf_oracle_out *out, int64_t *counts)
+{
     if (nthreads < 1) nthreads = 1;
     hash_pool p;
     memset(&p, 0, sizeof p);
@@ -541,8 +551,12 @@ int64_t hdrf_oracle_reduce_many(hdrf_oracle *o, const uint8_t *const *blocks, co
         while (!__atomic_load_n(&j->ready, __ATOMIC_ACQUIRE)) sched_yield();
         if (j->n < 0) { rc = j->n; break; }
         int64_t ss = 0;
-        const int64_t n = reduce_hashed(o, j->data, j->size, ids[i], j->off, j->n, j->dig, NULL, NULL, NULL, NULL, &ss);
+        const hdrf_oracle_out *w = out ? &out[i] : NULL;
+        if (w && j->n > w->cap) { rc = -1; break; }
+        const int64_t n = reduce_hashed(o, j->data, j->size, ids[i], j->off, j->n, j->dig, w ? w->offsets : NULL,
+                                        w ? w->digests : NULL, w ? w->is_new : NULL, w ? w->values : NULL, &ss);
         j->off = NULL; j->dig = NULL;
+        if (counts) counts[i] = n;
         if (n < 0) { rc = n; break; }
         if (store_sizes) store_sizes[i] = ss;
         __atomic_store_n(&p.consumed, i + 1, __ATOMIC_RELEASE);

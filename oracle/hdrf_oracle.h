@@ -51,6 +51,15 @@ int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, in
  * the ordered part handles them in arrival order; same results as hdrf_oracle_reduce in order. */
 int64_t hdrf_oracle_reduce_many(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
                                 const int64_t *ids, int64_t nblocks, int nthreads, int64_t *store_sizes);
+/* Per-block result buffers for hdrf_oracle_reduce_many_out (the arrays of hdrf_oracle_reduce). */
+typedef struct {
+    int64_t cap;
+    uint32_t *offsets;
+    uint8_t *digests, *is_new, *values;
+} hdrf_oracle_out;
+int64_t hdrf_oracle_reduce_many_out(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,
+                                    const int64_t *ids, int64_t nblocks, int nthreads, int64_t *store_sizes,
+                                    const hdrf_oracle_out *out, int64_t *counts);
 /* The reference's concurrency shape, blocks serialised: per block 1 chunking thread + nhash hasher
  * threads over chunk ranges, then the ordered part (BASELINE.md CPU plan 1). */
 int64_t hdrf_oracle_reduce_ref_shape(hdrf_oracle *o, const uint8_t *const *blocks, const int64_t *sizes,

@@ -69,6 +69,9 @@ def lib():
                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                               ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
         L.hdrf_oracle_reduce_many.restype = ctypes.c_int64
+        L.hdrf_oracle_reduce_many_out.argtypes = L.hdrf_oracle_reduce_many.argtypes + [ctypes.c_void_p,
+                                                                                        ctypes.POINTER(ctypes.c_int64)]
+        L.hdrf_oracle_reduce_many_out.restype = ctypes.c_int64
         L.hdrf_oracle_reduce_ref_shape.argtypes = L.hdrf_oracle_reduce_many.argtypes
         L.hdrf_oracle_reduce_ref_shape.restype = ctypes.c_int64
         L.hdrf_oracle_hadoop_lz4_stream_bound.argtypes = [ctypes.c_int64, ctypes.c_int64]
@@ -263,6 +266,11 @@ def hadoop_lz4_decode(data, cap):
     return None if n < 0 else out[:n].tobytes()
 
 
+class _OracleOut(ctypes.Structure):
+    _fields_ = [("cap", ctypes.c_int64), ("offsets", ctypes.c_void_p), ("digests", ctypes.c_void_p),
+                ("is_new", ctypes.c_void_p), ("values", ctypes.c_void_p)]
+
+
 class Oracle:
     """Stateful restatement of DataDeduplicator + Redis + chunkDir (one DataNode)."""
 
@@ -294,6 +302,44 @@ class Oracle:
         if rc < 0:
             raise RuntimeError(f"hdrf_oracle_reduce_many: {rc}")
         return ss[:n]
+
+    def reduce_many_full(self, blocks, block_ids, nthreads):
+        """reduce_many with every block's full result (offsets, digests, is_new, values,
+        store_size), as reduce() called on each block in order would return them."""
+        arrs = [_as_u8(b) for b in blocks]
+        n = len(arrs)
+        keep = [a if a.size else np.zeros(1, np.uint8) for a in arrs]
+        ptrs = (ctypes.c_void_p * max(n, 1))(*[a.ctypes.data for a in keep])
+        sizes = np.array([a.size for a in arrs], np.int64)
+        ids = np.ascontiguousarray(block_ids, np.int64)
+        ss = np.zeros(max(n, 1), np.int64)
+        cnt = np.zeros(max(n, 1), np.int64)
+        res = []
+        outs = (_OracleOut * max(n, 1))()
+        for i, a in enumerate(arrs):
+            cap = a.size // 700 + 2
+            r = {"offsets": np.zeros(cap, np.uint32), "digests": np.zeros(cap * self.H, np.uint8),
+                 "is_new": np.zeros(cap, np.uint8), "values": np.zeros(cap * 11, np.uint8)}
+            outs[i].cap = cap
+            outs[i].offsets = r["offsets"].ctypes.data
+            outs[i].digests = r["digests"].ctypes.data
+            outs[i].is_new = r["is_new"].ctypes.data
+            outs[i].values = r["values"].ctypes.data
+            res.append(r)
+        p64 = ctypes.POINTER(ctypes.c_int64)
+        rc = lib().hdrf_oracle_reduce_many_out(self._h, ptrs, sizes.ctypes.data_as(p64), ids.ctypes.data_as(p64), n,
+                                               int(nthreads), ss.ctypes.data_as(p64), ctypes.cast(outs, ctypes.c_void_p),
+                                               cnt.ctypes.data_as(p64))
+        if rc < 0:
+            raise RuntimeError(f"hdrf_oracle_reduce_many_out: {rc}")
+        for i, r in enumerate(res):
+            k = int(cnt[i])
+            r["offsets"] = r["offsets"][:k]
+            r["digests"] = r["digests"][:k * self.H].reshape(k, self.H)
+            r["is_new"] = r["is_new"][:k]
+            r["values"] = r["values"][:k * 11].reshape(k, 11)
+            r["store_size"] = int(ss[i])
+        return res
 
     def reduce_ref_shape(self, blocks, block_ids, nhash=3):
         """The reference's concurrency shape, blocks serialised: per block 1 chunking thread, nhash

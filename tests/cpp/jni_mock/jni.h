@@ -26,6 +26,7 @@ struct JNINativeInterface_ {
     jclass (*FindClass)(JNIEnv *env, const char *name);
     jint (*ThrowNew)(JNIEnv *env, jclass clazz, const char *msg);
     void *(*GetDirectBufferAddress)(JNIEnv *env, jobject buf);
+    jlong (*GetDirectBufferCapacity)(JNIEnv *env, jobject buf);
     jsize (*GetArrayLength)(JNIEnv *env, jarray array);
     jlong *(*GetLongArrayElements)(JNIEnv *env, jlongArray array, unsigned char *isCopy);
     void (*ReleaseLongArrayElements)(JNIEnv *env, jlongArray array, jlong *elems, jint mode);

@@ -1,0 +1,124 @@
+"""Full-state GPU parity at the headline's EXACT batch shape (BASELINE config 2, bench.py defaults).
+
+bench.py reduces the corpus in batches of 32 x 128 MiB = 4 GiB (batch offsets past 2^31 and
+2^32 bytes), three batches in flight (`--depth 3`), on a context opened with max_batch_blocks
+= 32.  Here the bench's first three batches (the same corpus: seed, 50 % dup, 1 MiB segments,
+prefix of the 512-block roots) go through that same context and pipeline, and every block is
+compared with the sequential oracle (DN/DataDeduplicator.java:124-204 ordering semantics,
+oracle/hdrf_oracle.c): chunk END offsets, digests, is_new, storeSize, container placement;
+then the full index dump, the allocator, every recipe and every container's bytes.
+
+The API's maximum batch (64 blocks, common.hpp kMaxBatch, index mask bits 8..63 of
+index.hip's per-entry block mask) is covered by 64 ragged 1-2 MiB blocks per batch whose
+duplicates come from blocks anywhere earlier in the same batch or the one before.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import compare_block, compare_state, prng_bytes
+from hdrf_amd.corpus import corpus_roots
+from hdrf_amd.lib import Context
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+S = 128 << 20
+SEG = 1 << 20
+SEED = 20251015          # bench.py --seed default
+
+
+def _threads():
+    return max(1, min(16, len(os.sched_getaffinity(0)) - 1))
+
+
+@pytest.mark.timeout(900)
+def test_bench_batches_4gib_depth3_full_state():
+    B, nbatch = 32, 3
+    nb = B * nbatch
+    spb = S // SEG
+    roots = corpus_roots(SEED, 500000, 512, spb)[: nb * spb]      # the bench's first 96 blocks
+    ctx = Context(max_block_bytes=S, max_batch_blocks=B, index_log2=25, arena_slots=512)
+    total = nb * S + 4096
+    dev = ctx.dev_alloc(total)
+    ctx.corpus_fill(dev, roots, nb, spb, SEG, SEED)
+    blocks = [ctx.d2h(dev + b * S, S) for b in range(nb)]
+    ids = list(range(nb))
+    ora = Oracle()
+    expect = ora.reduce_many_full(blocks, ids, _threads())
+
+    def submit(k):
+        g = range(k * B, (k + 1) * B)
+        ctx.submit_batch([dev + b * S for b in g], [S] * B, [total - b * S for b in g], [ids[b] for b in g])
+
+    def check(k):
+        assert ctx.last_nblocks() == B
+        for i in range(B):
+            b = k * B + i
+            compare_block(ctx.batch_result(i), expect[b], tag=f"bench batch {k} block {i}")
+
+    for k in range(nbatch):            # depth 3: all three in flight before the first wait
+        submit(k)
+    for k in range(nbatch):
+        ctx.wait_batch()
+        check(k)
+    # the dedup ratio the headline reports rests on these: duplicates were found across batches
+    new = sum(int(e["store_size"]) for e in expect)
+    assert 0.3 < 1 - new / (nb * S) < 0.6
+    compare_state(ctx, ora, ids, tag="bench shape")
+    for b in (0, B - 1, B, nb - 1):
+        assert np.array_equal(ctx.reconstruct_block(ids[b]), blocks[b]), f"block {b} not rebuilt"
+    ctx.dev_free(dev)
+    ctx.close()
+
+
+def _ragged_batch(seed, k0, n, pool):
+    """n blocks of 1-2 MiB: random bytes with 64 KiB pieces copied from earlier blocks (pool)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        size = int(rng.integers(1 << 20, (2 << 20) + 1))
+        blk = prng_bytes(seed * 1000 + k0 + i, size)
+        if pool:
+            for o in range(0, size - 65536, 65536):
+                if rng.random() < 0.5:
+                    src = pool[int(rng.integers(len(pool)))]
+                    so = int(rng.integers(0, len(src) - 65536))
+                    blk[o:o + 65536] = src[so:so + 65536]
+        out.append(blk)
+        pool.append(blk)
+    return out
+
+
+@pytest.mark.timeout(600)
+def test_max_batch_64_blocks_mask_bits():
+    B = 64
+    ctx = Context(max_block_bytes=2 << 20, max_batch_blocks=B, index_log2=22, arena_slots=64,
+                  container_max=4 << 20)
+    ora = Oracle(max_size=4 << 20)
+    pool = []
+    batches = [_ragged_batch(77, 0, B, pool), _ragged_batch(78, B, B, pool)]
+    ids = list(range(1000, 1000 + 2 * B))
+    expect = ora.reduce_many_full(batches[0] + batches[1], ids, _threads())
+    devs = []
+    for k, blks in enumerate(batches):
+        ptrs, lens = [], []
+        for blk in blks:
+            d = ctx.dev_alloc(len(blk) + 4096)
+            ctx.h2d(d, blk)
+            devs.append(d)
+            ptrs.append(d)
+            lens.append(len(blk))
+        ctx.submit_batch(ptrs, lens, [n + 4096 for n in lens], ids[k * B:(k + 1) * B])
+    for k in range(2):
+        ctx.wait_batch()
+        assert ctx.last_nblocks() == B
+        for i in range(B):
+            compare_block(ctx.batch_result(i), expect[k * B + i], tag=f"64-block batch {k} block {i}")
+    # later blocks of the batch must see the earlier blocks' chunks as duplicates (mask bits >= 8)
+    assert any(int(e["is_new"].sum()) < len(e["is_new"]) for e in expect[8:B])
+    compare_state(ctx, ora, ids, tag="64-block batches")
+    for d in devs:
+        ctx.dev_free(d)
+    ctx.close()

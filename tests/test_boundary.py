@@ -15,7 +15,7 @@ import threading
 import numpy as np
 import pytest
 
-from helpers import compare_block, compare_state, make_block
+from helpers import compare_block, compare_state, make_block, prng_bytes
 from hdrf_amd.lib import Context, HdrfError
 from oracle.oracle import Oracle
 
@@ -279,4 +279,86 @@ def test_packet_receivers_on_concurrent_threads():
         ctx.wait_batch()
         compare_block(ctx.batch_result(0), ora.reduce(blocks[b], ids[b]), tag=f"threaded packets {b}")
     compare_state(ctx, ora, ids, tag="threaded packets")
+    ctx.close()
+
+
+def test_packet_receivers_race_submit_and_wait():
+    """Receivers keep appending on their threads while the main thread submits and waits on the
+    blocks that finished earlier (hdrf_append_packet without the lock beside hdrf_submit_slot /
+    hdrf_wait_batch under it); every block matches the sequential oracle."""
+    import threading
+    blocks = _blocks(95, 6, 2_500_000)
+    ids = [9300 + i for i in range(len(blocks))]
+    ctx = Context(container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64)
+    ora = Oracle(max_size=1 << 20)
+    rxs = [ctx.rx_begin(i) for i in ids]
+    errs = []
+
+    def receive(b):
+        try:
+            rng = np.random.default_rng(300 + b)
+            buf = np.zeros(1 << 20, np.uint8)
+            o = 0
+            while o < len(blocks[b]):
+                n = int(rng.choice([1, 4096, 65536, 300_001]))
+                p = blocks[b][o:o + n]
+                buf[:len(p)] = p
+                ctx.append_packet(rxs[b], buf.ctypes.data, len(p))
+                o += len(p)
+        except Exception as e:                                  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=receive, args=(b,)) for b in range(len(blocks))]
+    for t in th:
+        t.start()
+    pending = []
+    for b in range(len(blocks)):                               # arrival order; later receivers still run
+        th[b].join()
+        assert not errs, errs
+        ctx.submit_slot(rxs[b])
+        pending.append(b)
+        if len(pending) == 2:
+            ctx.wait_batch()
+            g = pending.pop(0)
+            compare_block(ctx.batch_result(0), ora.reduce(blocks[g], ids[g]), tag=f"race block {g}")
+    while pending:
+        ctx.wait_batch()
+        g = pending.pop(0)
+        compare_block(ctx.batch_result(0), ora.reduce(blocks[g], ids[g]), tag=f"race block {g}")
+    compare_state(ctx, ora, ids, tag="race packets")
+    ctx.close()
+
+
+def test_packet_receive_cancel_overflow_and_reset_guard():
+    """hdrf_rx_cancel gives back an abandoned receive buffer (more than the 8 buffers are abandoned,
+    some with staging chunks still copying); a packet that would pass max_block_bytes -- including a
+    length that wraps a 64-bit sum -- is refused without copying; hdrf_reset refuses while a block is
+    being received.  A block received afterwards reduces exactly."""
+    ctx = Context(container_max=1 << 20, max_block_bytes=12 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64)
+    ora = Oracle(max_size=1 << 20)
+    junk = prng_bytes(5, 9 << 20)
+    for k in range(11):                                        # > 8 abandoned receives
+        rx = ctx.rx_begin(7000 + k)
+        n = (k + 1) * (800 << 10)                              # up to 8.6 MiB: staging chunks flushed
+        ctx.append_packet(rx, junk.ctypes.data, n)
+        if k == 0:
+            with pytest.raises(HdrfError):
+                ctx.reset()                                    # a block is being received
+            with pytest.raises(HdrfError):
+                ctx.append_packet(rx, junk.ctypes.data, (1 << 64) - 1)    # r.len + len wraps
+            with pytest.raises(HdrfError):
+                ctx.append_packet(rx, junk.ctypes.data, (12 << 20) - n + 1)
+        ctx.rx_cancel(rx)
+        with pytest.raises(HdrfError):
+            ctx.rx_cancel(rx)                                  # not receiving any more
+    ctx.reset()
+    blk = _blocks(97, 1, 3_000_000)[0]
+    rx = ctx.rx_begin(7100)
+    for o in range(0, len(blk), 65536):
+        p = np.ascontiguousarray(blk[o:o + 65536])
+        ctx.append_packet(rx, p.ctypes.data, len(p))
+    ctx.submit_slot(rx)
+    ctx.wait_batch()
+    compare_block(ctx.batch_result(0), ora.reduce(blk, 7100), tag="after cancels")
+    compare_state(ctx, ora, [7100], tag="after cancels")
     ctx.close()

@@ -131,3 +131,30 @@ def test_gpu_lzop_packet_writes_and_corruption():
     with pytest.raises(HdrfError):
         ctx.stream_file_decode(3, bytes(g), len(d))
     ctx.close()
+
+
+def test_lzop_fixed_bytes_fixture():
+    """The committed file bytes (tests/golden/lzop_fixed.npz, made by make_lzop_fixture.py): the
+    oracle must still write exactly them, and they decode to the input."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "lzop_fixed.npz"))
+    data, f, mtime = z["data"], z["lzop"], int(z["mtime"][0])
+    assert np.array_equal(lzop_stream(data, [len(data)], mtime=mtime), f)
+    assert np.array_equal(lzop_decode(f, len(data)), data)
+    assert f[:9].tobytes() == b"\x89LZO\x00\r\n\x1a\n"
+    assert mtime.to_bytes(4, "big") in f[9:40].tobytes()                 # header mtime field
+
+
+@pytest.mark.gpu
+def test_lzop_fixed_bytes_fixture_gpu():
+    """The GPU LzopCodec writes the committed fixture's bytes (same mtime) and reads them back."""
+    import os
+    from hdrf_amd.lib import Context
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "lzop_fixed.npz"))
+    data, f, mtime = z["data"], z["lzop"], int(z["mtime"][0])
+    ctx = Context(max_block_bytes=1 << 20, max_batch_blocks=1, index_log2=16, arena_slots=8)
+    ctx.set_lzop_mtime(mtime)
+    g = ctx.stream_block_host(3, 1, data, [len(data)])
+    assert np.array_equal(np.frombuffer(bytes(g), np.uint8), f)
+    assert np.array_equal(np.frombuffer(bytes(ctx.stream_file_decode(3, g, len(data))), np.uint8), data)
+    ctx.close()
