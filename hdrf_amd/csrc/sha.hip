@@ -166,7 +166,28 @@ __device__ __forceinline__ void set_iv(uint32_t st[8])
 #endif
 constexpr bool kPairs = HDRF_SHA_PAIRS != 0;
 
-template <int HW>
+// A lane's window [apos, apos + 132) spans the 128-B line L holding apos and line L + 1.  Line L was
+// fetched by the lane's previous iteration (as its L + 1) and is read here for the last time; line
+// L + 1 is read again by the next iteration.  With HDRF_SHA_NT the loads wholly inside line L are
+// nontemporal (last use), so L2 evicts those lines first and keeps the L + 1 lines the lanes come back
+// for (2 waves per SIMD x 64 lanes x 2 lines per XCD fill its 4 MiB L2; PMC: 1.40x the algorithmic
+// bytes were fetched with plain loads).
+// (buffer loads from a wave-uniform block base: the nt and plain forms are distinct instructions,
+// which the compiler would otherwise merge into one plain load)
+typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ u32x4a win_ld(const HDRF_GLOBAL uint32_t *p, __amdgpu_buffer_rsrc_t rs, uint32_t off, bool last)
+{
+    if (NT) {
+        u32x4b v;
+        if (last) v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 2);    // aux 2: nt
+        else v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
+        return u32x4a{v.x, v.y, v.z, v.w};
+    }
+    return *(const HDRF_GLOBAL u32x4a *)p;
+}
+
+template <int HW, bool NT = false>
 __device__ __forceinline__ void sha_step(const uint8_t *base, uint32_t &pos, uint32_t &r, uint32_t st[8])
 {
     if (kPairs) {
@@ -174,17 +195,20 @@ __device__ __forceinline__ void sha_step(const uint8_t *base, uint32_t &pos, uin
         const uint32_t apos = pos & ~3u;
         const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
         const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
+        // NT: base is wave-uniform (the caller's block), so the resource lives in SGPRs
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, -1, 0x00020000);
+        const uint32_t lo = apos & 127u;            // the 16 B at apos + o lie wholly in line L iff lo + o + 16 <= 128
         uint32_t d[33];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
+            u32x4a v = win_ld<NT>(p + 4 * q, rs, apos + 16 * q, lo + 16 * q + 16 <= 128u);
             d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
         }
         d[16] = p[16];
         if (two) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 17 + 4 * q);
+                u32x4a v = win_ld<NT>(p + 17 + 4 * q, rs, apos + 68 + 16 * q, lo + 68 + 16 * q + 16 <= 128u);
                 d[17 + 4 * q] = v.x; d[18 + 4 * q] = v.y; d[19 + 4 * q] = v.z; d[20 + 4 * q] = v.w;
             }
         }
@@ -230,7 +254,7 @@ constexpr int kShaTile = 1024;                 // chunks per scan tile (4 per th
 // compression chain; chunk offsets come from coalesced per-wave reservations of 64 chunks kept in
 // registers (pool P, with the next reservation Q fetched while P is consumed), so a lane that
 // finishes its chain takes the next chunk with two ds_bpermutes and no memory round trip.
-template <int HW>
+template <int HW, bool NT>
 __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restrict__ blocks,
                                                        const uint32_t *__restrict__ offsets,
                                                        const BlockState *__restrict__ bst, int cap_blk,
@@ -255,7 +279,7 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
                 uint32_t st[8];
                 set_iv<HW>(st);
                 const uint8_t *lbase = blocks[lb].data;
-                while (r) sha_step<HW>(lbase, pos, r, st);
+                while (r) sha_step<HW, false>(lbase, pos, r, st);        // lbase per lane: plain loads
                 uint32_t *dst = mid + ((size_t)lb * cap_blk + lk) * 8;
 #pragma unroll
                 for (int j = 0; j < (HW == 5 ? 5 : 8); j++) dst[j] = st[j];
@@ -356,7 +380,7 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
             if (!ballot64(zero) && nidle <= avail) break;
         }
         if (!ballot64(active)) break;
-        if (active) sha_step<HW>(base, pos, r, st);
+        if (active) sha_step<HW, NT>(base, pos, r, st);
     }
 }
 
@@ -416,12 +440,16 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     const int wpb = std::max(4, (per_simd * 1024 / nblocks) & ~3);
     dim3 gf(wpb / 4, nblocks + 1);                 // y = 0: the long-chunk lanes
     dim3 gt((cap_blk + 255) / 256, nblocks);
+    // HDRF_SHA_NT (default 1): last-use window loads nontemporal (sha_step)
+    static const bool nt = [] { const char *e = getenv("HDRF_SHA_NT"); return e ? atoi(e) != 0 : true; }();
     if (hasher == 0) {
-        hipLaunchKernelGGL(sha_full_kernel<5>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
+        if (nt) hipLaunchKernelGGL((sha_full_kernel<5, true>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
+        else hipLaunchKernelGGL((sha_full_kernel<5, false>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
         mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<5>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     } else {
-        hipLaunchKernelGGL(sha_full_kernel<7>, gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
+        if (nt) hipLaunchKernelGGL((sha_full_kernel<7, true>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
+        else hipLaunchKernelGGL((sha_full_kernel<7, false>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
         mk->mark(st);
         hipLaunchKernelGGL(sha_tail_kernel<7>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
     }
