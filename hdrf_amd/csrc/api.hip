@@ -63,7 +63,7 @@ struct Slot {
     size_t spec_words = 0, meta_cap = 0;      // capacity of d_spec (u32) / d_meta (segments), grown on demand
     int total_waves = 0, total_segs = 0, spec_cap = 0;   // lane walk of the batch in this slot
     BlockState *d_bst = nullptr;
-    uint32_t *d_off = nullptr, *d_dig = nullptr, *d_mid = nullptr, *d_slot = nullptr, *d_pre = nullptr;
+    uint32_t *d_off = nullptr, *d_dig = nullptr, *d_slot = nullptr, *d_pre = nullptr;
     uint8_t *d_flags = nullptr;
     uint32_t *d_tilesum = nullptr, *d_tilepre = nullptr;
     uint64_t *d_store = nullptr;
@@ -296,7 +296,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
 
 static void free_slot(Slot &S)
 {
-    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_mid, S.d_slot,
+    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_slot,
                    S.d_pre, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
                    S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err,
                    S.d_lzwork};
@@ -367,7 +367,7 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         (rc = dalloc(ctx, &S.d_meta, S.meta_cap)) || (rc = dalloc(ctx, &S.d_rq, S.meta_cap)) ||
         (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
         (rc = dalloc(ctx, &S.d_off, nchunk)) || (rc = dalloc(ctx, &S.d_dig, nchunk * ctx->HW)) ||
-        (rc = dalloc(ctx, &S.d_mid, nchunk * 8)) || (rc = dalloc(ctx, &S.d_slot, nchunk)) ||
+        (rc = dalloc(ctx, &S.d_slot, nchunk)) ||
         (rc = dalloc(ctx, &S.d_pre, nchunk)) || (rc = dalloc(ctx, &S.d_flags, nchunk)) ||
         (rc = dalloc(ctx, &S.d_tilesum, (size_t)B * ctx->ntiles)) ||
         (rc = dalloc(ctx, &S.d_tilepre, (size_t)B * ctx->ntiles)) || (rc = dalloc(ctx, &S.d_store, B)) ||
@@ -753,7 +753,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(A, S.recipe_done, 0));
     Marker ma;
     ma.ev = ctx->timing ? S.evA : nullptr;
-    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig, S.d_queue, ctx->sha_long, A,
+    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig, S.d_queue, ctx->sha_long, A,
                      &ma));
     ma.mark(A);
     HIPCK(hipEventRecord(S.front_done, A));
@@ -1803,7 +1803,7 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
                           c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst, S.d_off, ctx->cap_blk, S.d_err,
                           st, &mk));
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
-    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_mid, S.d_dig,
+    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig,
                      S.d_queue, ctx->sha_long, st, &mk));
     // local aggregation: a fresh scratch table, every entry "created" in batch 1
     HIPCK(hipMemsetAsync(ctx->d_scratch[si], 0, sizeof(IndexEntry) << ctx->scratch_log2, st));

@@ -6,7 +6,7 @@ namespace hdrf {
 
 // Stage markers: when timing is on, a HIP event is recorded on the launch stream at every
 // stage boundary (kernels of one stream run in order, so event deltas are kernel times).
-constexpr int kNumStages = 12;  // walk, stitch, sha_full, sha_tail, claim, apply, slow+decide, scan, flush, place, compress, gmax
+constexpr int kNumStages = 12;  // walk, stitch, sha, (unused), claim, apply, slow+decide, scan, flush, place, compress, gmax
 struct Marker {
     hipEvent_t *ev = nullptr;   // kNumStages + 1 events
     int next = 0;
@@ -48,8 +48,8 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
                            Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
-                      const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
-                      bool long_lanes, hipStream_t st, Marker *mk);   // queue: 65 words; [64] = long chunks seen
+                      const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
+                      hipStream_t st, Marker *mk);   // queue: 65 words; [64] = long chunks seen
 hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals, int n, IndexEntry *tab, int log2cap,
                              unsigned long long tag_mask, int *err, hipStream_t st);
 // GzipCodec read side (inflate.hip): one raw deflate stream -> dst; res[0] = length or < 0, res[1] =

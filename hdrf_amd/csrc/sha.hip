@@ -4,23 +4,19 @@
 // [off[k-1], off[k]) with utilities.sha1hash (hasher==0) or sha224hash (hasher==1),
 // DN/utilities.java:98-137 (nayuki native compress + FIPS 180-4 padding).
 //
-// Two kernels:
-//   sha_full — every FULL 64-B block of every chunk.  A lane owns one chunk's compression chain;
-//              a lane that finishes its chunk immediately takes the next one from the wave's
-//              register pool of reserved chunks (ballot + mbcnt + ds_bpermute), so lanes do not
-//              idle while the wave's longest chunk finishes.  No padding logic in this loop.
-//   sha_tail — one lane per chunk: the 1-2 padded final blocks (FIPS 180-4 padding) and the
-//              digest store.
+// One kernel: sha_chunk — a lane owns one chunk's whole compression chain, FIPS
+// 180-4 padding and digest included; a lane that finishes its chunk immediately takes the next one
+// from the wave's register pool of reserved chunks (ballot + mbcnt + ds_bpermute), so lanes do not
+// idle while the wave's longest chunk finishes.
 // Each 64-B block is fetched as 17 dword-aligned dwords (4 x dwordx4 + 1) and realigned +
 // byte-swapped with one v_perm_b32 per word.  Rotations are v_alignbit_b32, 3-way xor is
 // v_bitop3_b32 (gfx950), and so are Ch and Maj (one v_bitop3 each: 618 VALU per SHA-1 block).
-// Lanes hash two consecutive blocks per iteration from one 132-B window (4 + 4 dwordx4 + 1 dword),
-// so each 128-B line of a chunk is fetched once per pair: one block per iteration read every line
-// twice, far apart in time, and missed L2 2.3x the algorithmic bytes (PMC); pairs measured -9 % SHA
-// time alone and +4.5 % end to end in the pipeline (less memory contention with the place stage).
-// A lane with one block left idles through the second compression (~3 % of slots).
+// Lanes hash two consecutive blocks per iteration from one 132-B window (4 + 4 dwordx4 + 1 dword).
+// A lane with one block left idles through the second compression.
 // Measured against tools/sha_peak.hip (the same compression on register-resident data, no memory):
-// a software-pipelined prefetch variant and a two-chains-per-lane variant were both slower.
+// a software-pipelined prefetch variant and a two-chains-per-lane variant were both slower, and so
+// were nontemporal loads for the part of each window read for the last time (r03: 800 vs 980 GB/s,
+// more line fetches, not fewer).
 #include <algorithm>
 #include <cstdlib>
 
@@ -88,64 +84,6 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16])
     st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// Message block `bi` of a chunk [start, start+len) as 16 big-endian words, with FIPS 180-4
-// padding applied when the block reaches past the message end.
-__device__ __forceinline__ void load_block(const uint8_t *base, int64_t avail, int64_t start, int len, int bi,
-                                           int nblk, uint32_t m[16])
-{
-    const int64_t pos = start + 64 * (int64_t)bi;
-    const int64_t apos = pos & ~(int64_t)3;
-    const uint32_t sel = 0x00010203u + (uint32_t)(pos & 3) * 0x01010101u;
-    uint32_t d[17];
-    if (apos + 68 <= avail) {
-        const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
-            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-        }
-        d[16] = p[16];
-    } else {
-#pragma unroll
-        for (int q = 0; q < 17; q++) d[q] = load4_guard(base, apos + 4 * q, avail);
-    }
-#pragma unroll
-    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
-    const int off = 64 * bi;
-    if (off + 64 > len) {             // tail: zero past the end, 0x80 terminator, bit length
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            const int nv = len - (off + 4 * i);          // message bytes left at this word
-            uint32_t x = m[i];
-            if (nv <= 0) x = (nv == 0) ? 0x80000000u : 0u;
-            else if (nv < 4) x = (x & (0xffffffffu << (32 - 8 * nv))) | (0x80000000u >> (8 * nv));
-            m[i] = x;
-        }
-        if (bi == nblk - 1) {
-            m[14] = (uint32_t)((uint64_t)len >> 29);
-            m[15] = (uint32_t)len << 3;
-        }
-    }
-}
-
-// Full (unpadded) 64-B message block at byte `pos` of a block whose base is wave-uniform;
-// pos+68 <= len+4 <= readable, so no bounds guard is needed.
-__device__ __forceinline__ void load_full(const uint8_t *base, uint32_t pos, uint32_t m[16])
-{
-    const uint32_t apos = pos & ~3u;
-    const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
-    const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
-    uint32_t d[17];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
-        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-    }
-    d[16] = p[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
-}
-
 template <int HW>
 __device__ __forceinline__ void set_iv(uint32_t st[8])
 {
@@ -158,81 +96,82 @@ __device__ __forceinline__ void set_iv(uint32_t st[8])
     }
 }
 
-// One iteration of a lane's compression chain: two consecutive blocks from one 132-B window (one
-// when a single full block is left).  Each 128-B line of the chunk is fetched once per pair instead
-// of by two compressions far apart in time (L2 misses).
-#ifndef HDRF_SHA_PAIRS
-#define HDRF_SHA_PAIRS 1
-#endif
-constexpr bool kPairs = HDRF_SHA_PAIRS != 0;
-
-// A lane's window [apos, apos + 132) spans the 128-B line L holding apos and line L + 1.  Line L was
-// fetched by the lane's previous iteration (as its L + 1) and is read here for the last time; line
-// L + 1 is read again by the next iteration.  With HDRF_SHA_NT the loads wholly inside line L are
-// nontemporal (last use), so L2 evicts those lines first and keeps the L + 1 lines the lanes come back
-// for (2 waves per SIMD x 64 lanes x 2 lines per XCD fill its 4 MiB L2; PMC: 1.40x the algorithmic
-// bytes were fetched with plain loads).
-// (buffer loads from a wave-uniform block base: the nt and plain forms are distinct instructions,
-// which the compiler would otherwise merge into one plain load)
-typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
-template <bool NT>
-__device__ __forceinline__ u32x4a win_ld(const HDRF_GLOBAL uint32_t *p, __amdgpu_buffer_rsrc_t rs, uint32_t off, bool last)
+// FIPS 180-4 padding of block j of a len-byte message, in place on its big-endian words: the
+// message bytes [64 j, len) kept, 0x80 right after them, zeros, and the bit length in words 14-15
+// of the last block (j == nb - 1).  A block the message fills (64 j + 64 <= len) is left unchanged,
+// so the whole wave may run it.  e < 0: the length-only block after a tail of >= 56 bytes.
+__device__ __forceinline__ void pad_block(uint32_t m[16], uint32_t len, uint32_t j, uint32_t nb)
 {
-    if (NT) {
-        u32x4b v;
-        if (last) v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 2);    // aux 2: nt
-        else v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0);
-        return u32x4a{v.x, v.y, v.z, v.w};
+    const int e = (int)len - 64 * (int)j;
+    const int wt = e >> 2;                               // the word that takes the 0x80 byte
+    const uint32_t rb = (uint32_t)e & 3u;
+    const uint32_t hm = rb ? (0xffffffffu << (32 - 8 * rb)) : 0u;
+    const uint32_t tb = e >= 0 ? (0x80000000u >> (8 * rb)) : 0u;
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = i < wt ? m[i] : (i == wt ? ((m[i] & hm) | tb) : 0u);
+    if (j == nb - 1) {
+        m[14] = len >> 29;
+        m[15] = len << 3;
     }
-    return *(const HDRF_GLOBAL u32x4a *)p;
 }
 
-template <int HW, bool NT = false>
-__device__ __forceinline__ void sha_step(const uint8_t *base, uint32_t &pos, uint32_t &r, uint32_t st[8])
+// One iteration of a lane's compression chain (DN/utilities.java:98-137 over one chunk): blocks bi
+// and, when `two`, bi + 1 from one 132-B window, so each 128-B line of the chunk is fetched once per
+// pair (one block per iteration read every line twice, far apart in time: L2 misses 2.3x the
+// algorithmic bytes).  The pairing is aligned so that the block T holding the message end is the
+// SECOND of a pair (a chunk whose T is even starts with one single block): only slot 1 pads in
+// steady state, and slot 0 only for T == 0 (a chunk under 64 B) or the length-only block T + 1.
+// The padding is wave-uniform (ballot) because nearly every iteration has some lane at its tail;
+// for the lanes not at their tail it changes nothing.
+template <int HW>
+__device__ __forceinline__ void sha_iter(const uint8_t *base, uint64_t readable, uint32_t s0, uint32_t len, uint32_t T,
+                                         uint32_t nb, uint32_t &bi, uint32_t st[8])
 {
-    if (kPairs) {
-        const bool two = r >= 2;
-        const uint32_t apos = pos & ~3u;
-        const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
+    const bool two = bi < T && ((T - bi) & 1u);
+    const uint32_t pos = s0 + 64u * bi;
+    const uint32_t apos = pos & ~3u;
+    const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
+    uint32_t d[33];
+    if ((uint64_t)apos + 132u <= readable) {          // all but a block's last chunk
         const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
-        // NT: base is wave-uniform (the caller's block), so the resource lives in SGPRs
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, -1, 0x00020000);
-        const uint32_t lo = apos & 127u;            // the 16 B at apos + o lie wholly in line L iff lo + o + 16 <= 128
-        uint32_t d[33];
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            u32x4a v = win_ld<NT>(p + 4 * q, rs, apos + 16 * q, lo + 16 * q + 16 <= 128u);
+            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
             d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
         }
         d[16] = p[16];
         if (two) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                u32x4a v = win_ld<NT>(p + 17 + 4 * q, rs, apos + 68 + 16 * q, lo + 68 + 16 * q + 16 <= 128u);
+                u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 17 + 4 * q);
                 d[17 + 4 * q] = v.x; d[18 + 4 * q] = v.y; d[19 + 4 * q] = v.z; d[20 + 4 * q] = v.w;
             }
         }
-        uint32_t m[16];
+    } else {                                          // bytes past `readable` read as 0 (padding hides them)
 #pragma unroll
-        for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
-        if (HW == 5) sha1_compress(st, m);
-        else sha256_compress(st, m);
-        if (two) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 17], d[i + 16], sel);
-            if (HW == 5) sha1_compress(st, m);
-            else sha256_compress(st, m);
-        }
-        pos += two ? 128 : 64;
-        r -= two ? 2 : 1;
-    } else {
-        uint32_t m[16];
-        load_full(base, pos, m);
-        if (HW == 5) sha1_compress(st, m);
-        else sha256_compress(st, m);
-        pos += 64;
-        r--;
+        for (int q = 0; q < 33; q++) d[q] = load4_guard(base, (int64_t)apos + 4 * q, (int64_t)readable);
     }
+    uint32_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+    if (ballot64(bi >= T)) pad_block(m, len, bi, nb);
+    if (HW == 5) sha1_compress(st, m);
+    else sha256_compress(st, m);
+    if (two) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 17], d[i + 16], sel);
+        if (ballot64(bi + 1 == T)) pad_block(m, len, bi + 1, nb);
+        if (HW == 5) sha1_compress(st, m);
+        else sha256_compress(st, m);
+    }
+    bi += two ? 2u : 1u;
+}
+
+template <int HW>
+__device__ __forceinline__ void store_digest(uint32_t *dst, const uint32_t st[8])
+{
+#pragma unroll
+    for (int i = 0; i < HW; i++) dst[i] = __builtin_bswap32(st[i]);
 }
 
 // Long chunks (>= kShaLong bytes: forced cuts of low-entropy runs, up to max_chunk) are hashed by
@@ -243,23 +182,25 @@ __device__ __forceinline__ void sha_step(const uint8_t *base, uint32_t &pos, uin
 // bytes in such chunks: SHA alone 61 -> 26 ms per batch, config 4 33.5 -> 35.8 GB/s).  The scan
 // for them costs config 2 (no long chunks) ~3 %, so the lanes run only while the caller's recent
 // batches held long chunks (queue[64], set by the queue consumers whichever mode ran).  The
-// workgroups at y = 0 of sha_full (dispatched first) scan the offsets of every block (workgroup x
+// workgroups at y = 0 of sha_chunk (dispatched first) scan the offsets of every block (workgroup x
 // takes 1024-chunk tiles x, x + gridDim.x, ...), compact the long chunks into LDS and hash them one
-// lane each; the queue consumers skip them.  A separate list kernel ahead of sha_full cost config 2
+// lane each; the queue consumers skip them.  A separate list kernel ahead of sha_chunk cost config 2
 // 4 % (one more dependent launch on the SHA stream).
 constexpr uint32_t kShaLong = 65536;
 constexpr int kShaTile = 1024;                 // chunks per scan tile (4 per thread)
 
-// grid (waves_per_block/4, nblocks): every wave serves chunks of block b.  A lane owns one chunk's
-// compression chain; chunk offsets come from coalesced per-wave reservations of 64 chunks kept in
-// registers (pool P, with the next reservation Q fetched while P is consumed), so a lane that
-// finishes its chain takes the next chunk with two ds_bpermutes and no memory round trip.
-template <int HW, bool NT>
-__global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restrict__ blocks,
-                                                       const uint32_t *__restrict__ offsets,
-                                                       const BlockState *__restrict__ bst, int cap_blk,
-                                                       uint32_t *__restrict__ mid, uint32_t *__restrict__ queue,
-                                                       uint32_t thr)
+// grid (waves_per_block/4, nblocks + 1): every wave of y = b + 1 serves chunks of block b.  A lane
+// owns one chunk's whole compression chain, padding and digest included (the separate tail kernel
+// and its mid-state round trip are gone: 1.2 GB of 128-B line fetches per 4 GiB batch, PMC r03).
+// Chunk offsets come from coalesced per-wave reservations of 64 chunks kept in registers (pool P,
+// with the next reservation Q fetched while P is consumed), so a lane that finishes its chain takes
+// the next chunk with two ds_bpermutes and no memory round trip.
+template <int HW>
+__global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restrict__ blocks,
+                                                        const uint32_t *__restrict__ offsets,
+                                                        const BlockState *__restrict__ bst, int cap_blk,
+                                                        uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                                        uint32_t thr)
 {
     if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
         if (thr == 0xffffffffu) return;
@@ -274,15 +215,13 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
                 const uint32_t e = s_long[i];
                 const int lb = (int)(e >> 26), lk = (int)(e & 0x3ffffffu);   // block < 64, chunk < cap_blk < 2^26
                 const uint32_t *lo = offsets + (size_t)lb * cap_blk;
-                uint32_t pos = lk ? lo[lk - 1] : 0u;
-                uint32_t r = (lo[lk] - pos) >> 6;
-                uint32_t st[8];
+                const uint32_t s0 = lk ? lo[lk - 1] : 0u;
+                const uint32_t len = lo[lk] - s0, T = len >> 6, nb = (len + 8) / 64 + 1;
+                uint32_t st[8], bi = 0;
                 set_iv<HW>(st);
-                const uint8_t *lbase = blocks[lb].data;
-                while (r) sha_step<HW, false>(lbase, pos, r, st);        // lbase per lane: plain loads
-                uint32_t *dst = mid + ((size_t)lb * cap_blk + lk) * 8;
-#pragma unroll
-                for (int j = 0; j < (HW == 5 ? 5 : 8); j++) dst[j] = st[j];
+                const BlockDesc &lbd = blocks[lb];
+                while (bi < nb) sha_iter<HW>(lbd.data, lbd.readable, s0, len, T, nb, bi, st);
+                store_digest<HW>(digests + ((size_t)lb * cap_blk + lk) * HW, st);
             }
             __syncthreads();
             if (t == 0) s_nl = 0;
@@ -317,9 +256,11 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
     }
     const int b = blockIdx.y - 1;
     const int n = bst[b].n_chunks;
-    const uint8_t *base = blocks[b].data;
+    const BlockDesc &bd = blocks[b];
+    const uint8_t *base = bd.data;
+    const uint64_t readable = bd.readable;
     const uint32_t *off = offsets + (size_t)b * cap_blk;
-    uint32_t *mb = mid + (size_t)b * cap_blk * 8;
+    uint32_t *db = digests + (size_t)b * cap_blk * HW;
     const int l = lane_id();
     int kbP, cntP, kbQ, cntQ;
     uint32_t SP, EP, SQ, EQ;
@@ -337,13 +278,12 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
     int head = 0;
     bool active = false;
     int k = 0;
-    uint32_t pos = 0, r = 0;
+    uint32_t s0 = 0, len = 0, T = 0, nb = 0, bi = 0;
     uint32_t st[8];
     set_iv<HW>(st);
     for (;;) {
-        if (active && r == 0) {                   // chain done: mid-state for sha_tail
-#pragma unroll
-            for (int i = 0; i < (HW == 5 ? 5 : 8); i++) mb[(size_t)k * 8 + i] = st[i];
+        if (active && bi == nb) {                 // chain done: the digest
+            store_digest<HW>(db + (size_t)k * HW, st);
             active = false;
         }
         for (;;) {                                 // offer chunks to idle lanes
@@ -357,74 +297,39 @@ __global__ void __launch_bounds__(256) sha_full_kernel(const BlockDesc *__restri
             const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
             const int avail = cntP - head;
             const int idx = min(head + rank, 63);
-            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), s0 = (uint32_t)__shfl((int)SP, idx, 64);
-            bool zero = false;
-            if (ballot64(!active && rank < avail && e - s0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
-            if (!active && rank < avail && e - s0 >= thr) {
-                zero = true;                      // a long chunk: hashed by the long lanes, take another
+            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
+            bool skip = false;
+            if (ballot64(!active && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
+            if (!active && rank < avail && e - c0 >= thr) {
+                skip = true;                      // a long chunk: hashed by the long lanes, take another
             } else if (!active && rank < avail) {
                 k = kbP + head + rank;
-                pos = s0;
-                r = (e - s0) >> 6;
+                s0 = c0;
+                len = e - c0;
+                T = len >> 6;
+                nb = (len + 8) / 64 + 1;
+                bi = 0;
                 set_iv<HW>(st);
-                if (r == 0) {                     // no full block: sha_tail starts from the IV
-#pragma unroll
-                    for (int i = 0; i < (HW == 5 ? 5 : 8); i++) mb[(size_t)k * 8 + i] = st[i];
-                    zero = true;
-                } else {
-                    active = true;
-                }
+                active = true;
             }
             const int nidle = __popcll(idle);
             head += min(nidle, avail);
-            if (!ballot64(zero) && nidle <= avail) break;
+            if (!ballot64(skip) && nidle <= avail) break;
         }
         if (!ballot64(active)) break;
-        if (active) sha_step<HW, NT>(base, pos, r, st);
+        if (active) sha_iter<HW>(base, readable, s0, len, T, nb, bi, st);
     }
-}
-
-// one lane per chunk: padded final block(s) + digest
-template <int HW>
-__global__ void __launch_bounds__(256) sha_tail_kernel(const BlockDesc *__restrict__ blocks,
-                                                       const uint32_t *__restrict__ offsets,
-                                                       const BlockState *__restrict__ bst, int cap_blk,
-                                                       const uint32_t *__restrict__ mid, uint32_t *__restrict__ digests)
-{
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    const int n = bst[b].n_chunks;
-    if (k >= n) return;
-    const BlockDesc bd = blocks[b];
-    const uint32_t *off = offsets + (size_t)b * cap_blk;
-    const int64_t start = k ? off[k - 1] : 0;
-    const int len = (int)(off[k] - start);
-    const int full = len >> 6;
-    const int nblk = (len + 8) / 64 + 1;              // total blocks incl. padding
-    uint32_t st[8];
-    const uint32_t *ms = mid + ((size_t)b * cap_blk + k) * 8;
-#pragma unroll
-    for (int i = 0; i < (HW == 5 ? 5 : 8); i++) st[i] = ms[i];          // chaining state words
-    for (int bi = full; bi < nblk; bi++) {
-        uint32_t m[16];
-        load_block(bd.data, (int64_t)bd.readable, start, len, bi, nblk, m);
-        if (HW == 5) sha1_compress(st, m);
-        else sha256_compress(st, m);
-    }
-    uint32_t *dst = digests + ((size_t)b * cap_blk + k) * HW;
-#pragma unroll
-    for (int i = 0; i < HW; i++) dst[i] = __builtin_bswap32(st[i]);
 }
 
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
-                      const BlockState *bst, int cap_blk, uint32_t *mid, uint32_t *digests, uint32_t *queue,
-                      bool long_lanes, hipStream_t st, Marker *mk)
+                      const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
+                      hipStream_t st, Marker *mk)
 {
     if (nblocks > 64) return hipErrorInvalidValue;
     if (hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t) * 65, st)) return e;
     mk->mark(st);
     // HDRF_SHA_LONG: long-chunk threshold in bytes (>= kShaLong; 0 = no long lanes, for A/B runs)
-    // (the caller turns the lanes on while its batches hold long chunks: queue[64], set by sha_full)
+    // (the caller turns the lanes on while its batches hold long chunks: queue[64], set by sha_chunk)
     static const uint32_t thr_env = [] {
         const char *e = getenv("HDRF_SHA_LONG");
         const long v = e ? atol(e) : (long)kShaLong;
@@ -438,21 +343,12 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : 2; }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     const int wpb = std::max(4, (per_simd * 1024 / nblocks) & ~3);
-    dim3 gf(wpb / 4, nblocks + 1);                 // y = 0: the long-chunk lanes
-    dim3 gt((cap_blk + 255) / 256, nblocks);
-    // HDRF_SHA_NT (default 1): last-use window loads nontemporal (sha_step)
-    static const bool nt = [] { const char *e = getenv("HDRF_SHA_NT"); return e ? atoi(e) != 0 : true; }();
-    if (hasher == 0) {
-        if (nt) hipLaunchKernelGGL((sha_full_kernel<5, true>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
-        else hipLaunchKernelGGL((sha_full_kernel<5, false>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
-        mk->mark(st);
-        hipLaunchKernelGGL(sha_tail_kernel<5>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
-    } else {
-        if (nt) hipLaunchKernelGGL((sha_full_kernel<7, true>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
-        else hipLaunchKernelGGL((sha_full_kernel<7, false>), gf, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, mid, queue, thr);
-        mk->mark(st);
-        hipLaunchKernelGGL(sha_tail_kernel<7>, gt, dim3(256), 0, st, d_blocks, offsets, bst, cap_blk, mid, digests);
-    }
+    dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
+    if (hasher == 0)
+        hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    else
+        hipLaunchKernelGGL(sha_chunk_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    mk->mark(st);                                  // (the stage timer's former tail slot: empty)
     return hipGetLastError();
 }
 
