@@ -99,7 +99,7 @@ struct Slot {
     RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
     hipEvent_t recipe_done = nullptr;         // the copies read d_dig: the slot's next SHA waits
     bool recipe_pending = false;
-    hipEvent_t walk_done = nullptr, front_done = nullptr, back_done = nullptr;
+    hipEvent_t walk_done = nullptr, front_done = nullptr, back_done = nullptr, gmax_done = nullptr;
     hipEvent_t copy_done = nullptr;          // host path: the batch's H2D copies landed
     uint8_t *d_hstage = nullptr;              // host path: device copies of the batch's blocks
     uint64_t hstage_stride = 0;
@@ -114,6 +114,7 @@ struct hdrf_ctx {
     hipStream_t st = nullptr;    // stream A: SHA stage (also every synchronous helper)
     hipStream_t stB = nullptr;   // stream B: back stage (index + store)
     hipStream_t stW = nullptr;   // stream W: chunking stage
+    hipStream_t stG = nullptr;   // stream G: the granule-max pass (HDRF_GMAX_STREAM), ahead of W
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
     hipStream_t stL[2] = {};     // compressor 2: LZ4 streams, alternating by batch (off stream B)
     // chunks >= 64 KiB were seen in the last completed batch: sha_full hashes them on dedicated
@@ -305,7 +306,8 @@ static void free_slot(Slot &S)
     void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_long, S.h_closed, S.h_filelen, S.h_desc};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
-    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done, S.placed, S.lz_done};
+    hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done, S.placed, S.lz_done,
+                        S.gmax_done};
     if (S.d_rjobs) (void)hipFree(S.d_rjobs);
     if (S.h_rjobs) (void)hipHostFree(S.h_rjobs);
     if (S.d_hstage) (void)hipFree(S.d_hstage);
@@ -334,6 +336,7 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
     if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
+    if (ctx->stG) (void)hipStreamDestroy(ctx->stG);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
     for (auto L : ctx->stL)
         if (L) (void)hipStreamDestroy(L);
@@ -392,7 +395,8 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         hipEventCreateWithFlags(&S.front_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.placed, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&S.lz_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&S.lz_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.gmax_done, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
     for (auto &e : S.evW)
         if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
@@ -414,6 +418,7 @@ static int drain(hdrf_ctx *ctx)
         if (int r = wait_one(ctx)) rc = rc ? rc : r;
     HIPCK(hipStreamSynchronize(ctx->stC));
     for (auto L : ctx->stL) HIPCK(hipStreamSynchronize(L));
+    HIPCK(hipStreamSynchronize(ctx->stG));
     HIPCK(hipStreamSynchronize(ctx->stW));
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
@@ -497,6 +502,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, pa) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stB, hipStreamNonBlocking, pb) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pw) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stG, hipStreamNonBlocking, pw) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[0], hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[1], hipStreamNonBlocking) != hipSuccess) {
@@ -738,14 +744,18 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     // kernels and the HBM-bound granule pass overlap SHA's VALU stream of the previous batch
     static const int nstreams = [] { const char *e = getenv("HDRF_STREAMS"); return e ? atoi(e) : 3; }();
     hipStream_t W = nstreams == 3 ? ctx->stW : ctx->st, A = ctx->st, Bst = ctx->stB;
+    // HDRF_GMAX_STREAM=1: the granule-max pass on stream G, so the next batch's (HBM-bound) pass
+    // runs while W walks and stitches this one (latency-bound)
+    static const bool gstream = [] { const char *e = getenv("HDRF_GMAX_STREAM"); return e && atoi(e) != 0; }();
+    hipStream_t G = gstream ? ctx->stG : W;
     // ---- chunking on W: the slot's previous batch has completed (wait_one ran), so W may overwrite it
-    if (after_copy) HIPCK(hipStreamWaitEvent(W, S.copy_done, 0));
-    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, W));
+    if (after_copy) HIPCK(hipStreamWaitEvent(G, S.copy_done, 0));
+    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, G));
     Marker mw;
     mw.ev = ctx->timing ? S.evW : nullptr;
     HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs, chunk_scratch(S),
                           c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst, S.d_off, ctx->cap_blk, S.d_err,
-                          W, &mw));
+                          W, &mw, G, S.gmax_done));
     mw.mark(W);
     HIPCK(hipEventRecord(S.walk_done, W));
     // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig)

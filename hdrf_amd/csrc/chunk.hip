@@ -1120,22 +1120,31 @@ int lane_spec_cap(int seg_len, int w) { return seg_len / (w + 2) + 2 + kLaneOver
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
-                           Marker *mk)
+                           Marker *mk, hipStream_t stg, hipEvent_t gdone)
 {
     if ((max_len + 15) / 16 + 4 * kGmWin > X.gstride) return hipErrorInvalidValue;
     const int maxw = (max_nseg + 255) / 256;
     if (maxw > X.maxw) return hipErrorInvalidValue;
-    mk->mark(st);
+    const bool split = stg && stg != st && gdone;     // granule pass on its own stream, the walk waits for it
+    hipStream_t sg = split ? stg : st;
+    mk->mark(sg);
     hipError_t e = hipMemsetAsync(X.rq_count, 0, sizeof(int), st);
     if (e == hipSuccess) e = hipMemsetAsync(X.irr, 0, sizeof(uint32_t) * (size_t)(nsegs / 32 + 2), st);
     if (e != hipSuccess) return e;
     const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
     if (stream_knobs() & 1)
-        hipLaunchKernelGGL(gmax_kernel<true>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm, X.gstride);
+        hipLaunchKernelGGL(gmax_kernel<true>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride);
     else
-        hipLaunchKernelGGL(gmax_kernel<false>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm, X.gstride);
-    mk->mark(st);
-    hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), 0, st, d_blocks, nblocks, total_waves,
+        hipLaunchKernelGGL(gmax_kernel<false>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride);
+    mk->mark(sg);
+    if (split) {
+        if ((e = hipEventRecord(gdone, sg)) != hipSuccess || (e = hipStreamWaitEvent(st, gdone, 0)) != hipSuccess)
+            return e;
+    }
+    // HDRF_WALK_LDS: dynamic LDS per walk workgroup (occupancy throttle: fewer lanes in flight keep
+    // their granule-maximum lines in L2 between chunk steps)
+    static const int walk_lds = [] { const char *v = getenv("HDRF_WALK_LDS"); return v ? atoi(v) : 0; }();
+    hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
                        X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err);
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue

@@ -46,7 +46,7 @@ struct ChunkScratch {
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
-                           Marker *mk);
+                           Marker *mk, hipStream_t stg = nullptr, hipEvent_t gdone = nullptr);   // stg: gmax pass stream
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
                       hipStream_t st, Marker *mk);   // queue: 65 words; [64] = long chunks seen
