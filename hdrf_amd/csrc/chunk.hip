@@ -605,6 +605,44 @@ __device__ __forceinline__ void load_gm(uint32_t (&d)[kGmWin], const uint8_t *p)
 
 typedef __attribute__((address_space(3))) volatile uint16_t lds_u16v;
 typedef __attribute__((address_space(3))) volatile uint8_t lds_u8v;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// A lane's granule maxima, staged through LDS: a ring of two 128-granule lines (256 granules = 4 KiB
+// of data) in front of the lane's walk, so each 128-B line of maxima is fetched from memory once per
+// lane (it used to be re-fetched by every chunk step: ~2 line fetches per chunk, the lane's window
+// lines did not survive in L2 between its steps; PMC r03 1.55e7 requests per 4 GiB batch).  The window
+// of a step (128 maxima from W0 = G0 & ~3) is read from the ring at any dword offset.
+constexpr int kRingDw = 64;              // ring dwords per lane (a row: lanes read at their own, unrelated
+constexpr int kRingPitch = kRingDw;      // offsets, so no padding; 82 KB per workgroup -> 2 per CU)
+struct GmRing {
+    lds_u32 *r;                          // this lane's row
+    int rb = -(1 << 20);                 // ring holds granules [rb, rb + 256), rb a multiple of 128
+    __device__ __forceinline__ void fill(const uint8_t *gmb, int g)      // the line of granules [g, g + 128)
+    {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint4 v = ld16(gmb + g + 16 * i);
+            const int w = ((g >> 2) + 4 * i) & (kRingDw - 1);
+            r[w] = v.x; r[w + 1] = v.y; r[w + 2] = v.z; r[w + 3] = v.w;
+        }
+    }
+    __device__ __forceinline__ void get(uint32_t (&d)[kGmWin], const uint8_t *gmb, int W0)
+    {
+        if (W0 < rb || W0 + 4 * kGmWin > rb + 256) {
+            if (W0 >= rb + 128 && W0 + 4 * kGmWin <= rb + 384) {   // the window moved on by one line
+                fill(gmb, rb + 256);
+                rb += 128;
+            } else {                                              // first use, or a long search jumped
+                rb = W0 & ~127;
+                fill(gmb, rb);
+                fill(gmb, rb + 128);
+            }
+        }
+        const int w0 = W0 >> 2;
+#pragma unroll
+        for (int i = 0; i < kGmWin; i++) d[i] = r[(w0 + i) & (kRingDw - 1)];
+    }
+};
 
 __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
                                                         int total_waves, const uint8_t *__restrict__ gm,
@@ -616,6 +654,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
 {
     __shared__ uint16_t s_cuts[4][64 * kLdsCuts];
     __shared__ uint8_t s_cnt[4][64];
+    __shared__ uint32_t s_ring[4][64 * kRingPitch];
     const int wv = blockIdx.x * 4 + wave_id();
     if (wv >= total_waves) return;
     lds_u16v *vcuts = (lds_u16v *)s_cuts[wave_id()];      // read by the neighbouring lane:
@@ -644,6 +683,8 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
     bool active = exists, overflow = false;
     vcnt[l] = 0;
     uint32_t d[kGmWin];
+    GmRing ring;
+    ring.r = (lds_u32 *)&s_ring[wave_id()][l * kRingPitch];
     uint4 rh = make_uint4(0, 0, 0, 0);                    // raw bytes of the last hit granule gh
     int gh = -1;
     for (;;) {
@@ -654,7 +695,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
         const int lim = min(p + maxlen, size - 1);
         const int G0 = p >> 4, G1 = wend >> 4;
         int W0 = G0 & ~3;
-        load_gm(d, gmb + W0);
+        ring.get(d, gmb, W0);
         // M(p): granules G0+1 .. G1-1 are whole (bytes [a, b] of d, 1 <= a <= 4, 42 <= b <= 46); the
         // two edge granules need their raw bytes only when their maximum exceeds the rest (rare:
         // ~6 % of random-data windows), so most chunks touch no raw byte before the hit granule
@@ -707,7 +748,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
                     if (Gs >= W0 + 4 * kGmWin) {
                         if (16 * Gs > over_lim) { capped = true; break; }
                         W0 = Gs & ~3;
-                        load_gm(d, gmb + W0);
+                        ring.get(d, gmb, W0);
                     }
                     const unsigned long long m0 = gm_ge64(d, 0, C, Cm) & bits_from(Gs - W0) & bits_to(Glim - W0);
                     const unsigned long long m1 =
