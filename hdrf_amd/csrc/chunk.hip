@@ -614,23 +614,45 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // of a step (128 maxima from W0 = G0 & ~3) is read from the ring at any dword offset.
 constexpr int kRingDw = 64;              // ring dwords per lane (a row: lanes read at their own, unrelated
 constexpr int kRingPitch = kRingDw;      // offsets, so no padding; 82 KB per workgroup -> 2 per CU)
+// The next line is prefetched into registers at the end of a chunk step once the window has moved
+// into the ring's second line (after the step's raw load has been waited for, so that wait never
+// covers the prefetch), and written into the ring when the window reaches it.
 struct GmRing {
     lds_u32 *r;                          // this lane's row
     int rb = -(1 << 20);                 // ring holds granules [rb, rb + 256), rb a multiple of 128
-    __device__ __forceinline__ void fill(const uint8_t *gmb, int g)      // the line of granules [g, g + 128)
+    int w0 = 0;                          // the last window start
+    int pfg = -1;                        // granule of the line held in pf (-1: none)
+    uint4 pf[8];
+    __device__ __forceinline__ void put(int g, const uint4 (&v)[8])
     {
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            const uint4 v = ld16(gmb + g + 16 * i);
             const int w = ((g >> 2) + 4 * i) & (kRingDw - 1);
-            r[w] = v.x; r[w + 1] = v.y; r[w + 2] = v.z; r[w + 3] = v.w;
+            r[w] = v[i].x; r[w + 1] = v[i].y; r[w + 2] = v[i].z; r[w + 3] = v[i].w;
+        }
+    }
+    __device__ __forceinline__ void fill(const uint8_t *gmb, int g)      // the line of granules [g, g + 128)
+    {
+        uint4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = ld16(gmb + g + 16 * i);
+        put(g, v);
+    }
+    __device__ __forceinline__ void prefetch(const uint8_t *gmb)
+    {
+        if (pfg != rb + 256 && w0 >= rb + 128 - 4 * kGmWin + 32) {
+            pfg = rb + 256;
+#pragma unroll
+            for (int i = 0; i < 8; i++) pf[i] = ld16(gmb + pfg + 16 * i);
         }
     }
     __device__ __forceinline__ void get(uint32_t (&d)[kGmWin], const uint8_t *gmb, int W0)
     {
+        w0 = W0;
         if (W0 < rb || W0 + 4 * kGmWin > rb + 256) {
             if (W0 >= rb + 128 && W0 + 4 * kGmWin <= rb + 384) {   // the window moved on by one line
-                fill(gmb, rb + 256);
+                if (pfg == rb + 256) put(pfg, pf);
+                else fill(gmb, rb + 256);
                 rb += 128;
             } else {                                              // first use, or a long search jumped
                 rb = W0 & ~127;
@@ -786,6 +808,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
         }
         p = cut;
         first = false;
+        ring.prefetch(gmb);
         if (active && p >= over_lim && p + w <= size - 1) { sync = kSyncFail; active = false; }   // byte cap
         if (overflow) active = false;
     }
