@@ -97,14 +97,49 @@ def parse():
                          "0 = whole blocks through hdrf_submit_host")
     ap.add_argument("--packet-threads", type=int, default=4,
                     help="config5 packets: receiver threads appending different blocks' packets concurrently")
+    ap.add_argument("--packet-driver", choices=["python", "cpp"], default="python",
+                    help="config5 packets: 'cpp' runs tests/cpp/packet_driver.cpp (native receiver threads on the "
+                         "C-ABI the JNI binding calls, durable containers drained after every block) as a child "
+                         "process and reports its rate")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
                     help="config4: mixed-entropy blocks (random/text/binary), dedup + Lz4Codec containers; "
                          "config5: host-resident (pinned) blocks streamed H2D on a side stream (PCIe-inclusive)")
     return ap.parse_args()
 
 
+def packet_driver_line(a):
+    """config5 through the native packet driver (a child process; this process never touches the GPU)."""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "_build", "packet_driver")
+    if not os.path.exists(exe):
+        import __graft_entry__ as ge
+        exe = ge.build_packet_driver()
+    nb = 128 if a.blocks == 512 else a.blocks
+    pk = a.packet_kib or 64
+    t0 = time.perf_counter()
+    r = subprocess.run([exe, str(nb), str(a.block_mib), str(pk), str(a.packet_threads), str(a.steps)],
+                       capture_output=True, text=True, timeout=1500)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise SystemExit("packet driver failed: %s %s" % (r.stdout[-2000:], r.stderr[-2000:]))
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    S = a.block_mib << 20
+    line = {"metric": METRIC, "value": d["GB_s"], "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": 1,
+            "ms_per_step": round(nb * S / d["GB_s"] / 1e6, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "config5: %d x %d MiB host-resident (pinned) blocks, 50%% dup, %d KiB packets from %d "
+                                   "native receiver threads (hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot, "
+                                   "one block per submit, FIFO), durable containers drained after every block, "
+                                   "fresh index per step" % (nb, a.block_mib, pk, a.packet_threads),
+                       "blocks_per_gpu": nb, "block_bytes": S, "parallelism": "dp1"},
+            "roofline": None, "cpu_baseline": None, "packet_driver": d, "driver_wall_s": round(wall, 2)}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     a = parse()
+    if a.workload == "config5" and a.packet_driver == "cpp":
+        return packet_driver_line(a)
     if not a.depth:
         # config 2: depth 3 984 -> 1004 GB/s (three A/B pairs, scripts/ab_d23.txt): chunking of batch
         # k+2 starts while batch k+1 hashes instead of after batch k's read-back
@@ -150,8 +185,11 @@ def main():
     if host and a.blocks == 512:
         nb = 128                                         # 16 GiB of pinned host memory
     compressor = 2 if mixed else 1
+    # config 5 is the DataNode write path: durable containers (retain_containers, as the JNI binding
+    # opens it) handed out to pinned host memory after every completed batch, inside the timed region
     ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
-                  arena_slots=a.arena_slots, keep_recipes=a.keep_recipes, timing=1, n_ranks=world, rank=rank, compressor=compressor)
+                  arena_slots=a.arena_slots, keep_recipes=a.keep_recipes, timing=1, n_ranks=world, rank=rank,
+                  compressor=compressor, retain_containers=1 if host else 0)
     node = None
     if world > 1:
         from hdrf_amd.node import NodeRank, global_block
@@ -166,13 +204,13 @@ def main():
     total = nb * S + 4096
     dev = ctx.dev_alloc(total)
     ctx.corpus_fill(dev, roots, nb, spb, seg, seed, mixed=mixed)
-    hbuf, h2d_gbs = None, None
+    hbuf, h2d_gbs, dbuf = None, None, None
+    drained = {"events": 0, "bytes": 0}
     if host:                                             # the DataNode's received blocks, in host memory
         hbuf = ctx.host_alloc(nb * S)
         ctx.L.hdrf_memcpy_d2h(ctx._h, hbuf.ctypes.data, dev, nb * S)
-        t0 = time.perf_counter()                         # raw pinned H2D rate of the same bytes
-        ctx.L.hdrf_memcpy_h2d(ctx._h, dev, hbuf.ctypes.data, nb * S)
-        h2d_gbs = nb * S / (time.perf_counter() - t0) / 1e9
+        dbuf = ctx.host_alloc(1 << 30)                   # the drained container files (pinned)
+        h2d_gbs = raw_h2d_rate(torch, local, S)
     batches = []
     for b0 in range(0, nb, B):
         k = min(B, nb - b0)
@@ -181,6 +219,12 @@ def main():
 
     n_chunks = np.zeros(nb, np.int64)
     store = np.zeros(nb, np.int64)
+
+    def drain():
+        if dbuf is not None:
+            e, n = ctx.drain_into(dbuf.ctypes.data, dbuf.size)
+            drained["events"] += e
+            drained["bytes"] += n
 
     def step():
         if node is None:
@@ -228,22 +272,27 @@ def main():
                     if pend >= 5:
                         ctx.wait_batch()
                         collect()
+                        drain()
                         pend -= 1
                     ctx.submit_slot(rx)
                     pend += 1
             for _ in range(pend):
                 ctx.wait_batch()
                 collect()
+                drain()
         elif host:
-            # streaming: the H2D copies of batch k+1 (side stream) overlap the reduction of batch k
+            # streaming: the H2D copies of batch k+1 (side stream) overlap the reduction of batch k;
+            # after each completed batch its containers go D2H (stream D) while later batches run
             for k, (ptrs, lens, rd, ids) in enumerate(batches):
                 ctx.submit_host([hbuf.ctypes.data + (p - dev) for p in ptrs], lens, ids)
                 if k >= 2:
                     ctx.wait_batch()
                     collect()
+                    drain()
             for _ in range(min(2, len(batches))):
                 ctx.wait_batch()
                 collect()
+                drain()
         elif node is None:
             # pipelined: chunking of batch k+2, SHA of batch k+1 and index/store of batch k overlap
             depth = a.depth
@@ -270,6 +319,7 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    drained.update(events=0, bytes=0)
     ctx.stage_times(reset=True)
     if node is not None:
         node.phase_ms = {}
@@ -475,7 +525,14 @@ def main():
                                               "one block per submit" % (a.packet_kib, a.packet_threads)) if a.packet_kib else
                                              "whole blocks, hdrf_submit_host"))
             line["pcie"] = {"h2d_GB_s_raw_copy": round(h2d_gbs, 2), "value_over_raw_copy": round(value / h2d_gbs, 4),
-                            "note": "value is PCIe-inclusive: host buffers -> HBM -> reduced"}
+                            "raw_copy": "pinned host -> HBM, 128 MiB hipMemcpyAsync pieces, 4 in flight on one "
+                                        "stream, timed with HIP events (torch)",
+                            "drained_container_bytes_per_step": drained["bytes"] // max(1, a.steps),
+                            "drained_events_per_step": drained["events"] // max(1, a.steps),
+                            "d2h_GB_s_drain": round(drained["bytes"] / max(1, a.steps) / (el / a.steps) / 1e9, 2),
+                            "note": "value is PCIe-inclusive: host buffers -> HBM -> reduced, and every container "
+                                    "file (retain_containers, the JNI binding's mode) drained D2H to pinned host "
+                                    "memory after each completed batch, inside the timed region"}
         if node is not None and node.phase_ms.get("batches"):
             nbt = node.phase_ms["batches"]
             line["node_back_ms_per_batch"] = {k: round(v / nbt, 3) for k, v in node.phase_ms.items() if k != "batches"}
@@ -484,9 +541,33 @@ def main():
     ctx.dev_free(dev)
     if hbuf is not None:
         ctx.host_free(hbuf)
+        ctx.host_free(dbuf)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def raw_h2d_rate(torch, device, piece):
+    """The bare link: pinned host -> HBM in `piece`-byte async copies, 4 in flight on one stream
+    (the shape of the library's own H2D copies), 16 GiB, timed with HIP events."""
+    n = 4
+    src = torch.empty(n * piece, dtype=torch.uint8, pin_memory=True)
+    dst = torch.empty(n * piece, dtype=torch.uint8, device="cuda:%d" % device)
+    s = torch.cuda.Stream(device=device)
+    reps = max(1, (16 << 30) // (n * piece))
+    with torch.cuda.stream(s):
+        for i in range(n):                                # warm-up
+            dst[i * piece:(i + 1) * piece].copy_(src[i * piece:(i + 1) * piece], non_blocking=True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            for i in range(n):
+                dst[i * piece:(i + 1) * piece].copy_(src[i * piece:(i + 1) * piece], non_blocking=True)
+        e1.record(s)
+    e1.synchronize()
+    rate = reps * n * piece / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    return rate
 
 
 def read_bench(ctx, dev, S, m, hasher, compressor):

@@ -116,6 +116,7 @@ struct hdrf_ctx {
     hipStream_t stW = nullptr;   // stream W: chunking stage
     hipStream_t stG = nullptr;   // stream G: the granule-max pass (HDRF_GMAX_STREAM), ahead of W
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
+    hipStream_t stD = nullptr;   // stream D: container drain D2H (beside the H2D copies on C)
     hipStream_t stL[2] = {};     // compressor 2: LZ4 streams, alternating by batch (off stream B)
     // chunks >= 64 KiB were seen in the last completed batch: sha_full hashes them on dedicated
     // lanes (sha.hip); off otherwise, where the scan for them costs config 2 ~3 %
@@ -338,6 +339,7 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
     if (ctx->stG) (void)hipStreamDestroy(ctx->stG);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
+    if (ctx->stD) (void)hipStreamDestroy(ctx->stD);
     for (auto L : ctx->stL)
         if (L) (void)hipStreamDestroy(L);
     for (auto &r : ctx->rx)
@@ -504,6 +506,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pw) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stG, hipStreamNonBlocking, pw) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stD, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[0], hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[1], hipStreamNonBlocking) != hipSuccess) {
         free_all(ctx);
@@ -2501,7 +2504,11 @@ extern "C" int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out,
 // ---- durable containers: the chunkDir files of the storers (DN/DataDeduplicator.java:748-818) ----
 // Since the last drain: every container that closed (the whole file: raw bytes, or the Lz4Codec
 // stream under compressor 2, rewritten at :748-786) in close order, then every open container's
-// bytes appended since (:806-818).  Events are emitted whole, in order, while they fit.
+// bytes appended since (:806-818).  Events are emitted whole, in order, while they fit.  Only what
+// the COMPLETED batches (hdrf_wait_batch) produced is handed out; batches still in flight keep
+// running: their place kernels only append past the bytes copied here, and a closed container's
+// slot stays retained until it is drained.  The D2H copies run on stream D, so they overlap the
+// H2D copies of later batches on stream C (PCIe is full duplex).
 extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev, int64_t ev_cap, uint8_t *out,
                                          int64_t out_cap, int64_t *need)
 {
@@ -2511,7 +2518,6 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
     if (!ctx->cfg.retain_containers) return set_err(ctx, HDRF_E_INVAL, "hdrf_drain_containers needs cfg.retain_containers");
     if (ctx->G > 1) return set_err(ctx, HDRF_E_UNSUPPORTED, "container drain on node-global contexts");
     if (ev_cap < 0 || out_cap < 0 || (ev_cap && !ev) || (out_cap && !out)) return set_err(ctx, HDRF_E_INVAL, "bad buffers");
-    if (int rc = drain(ctx)) return rc;
     const hdrf_cfg &c = ctx->cfg;
     struct Pend { uint32_t id; int closed; int64_t off, n; ContainerInfo ci; };
     std::vector<Pend> todo;
@@ -2538,11 +2544,12 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
         }
         const uint8_t *src = (e.closed && c.compressor == 2) ? ctx->d_carena + (size_t)e.ci.slot * ctx->cslot
                                                              : ctx->d_arena + (size_t)e.ci.slot * c.container_max;
-        if (e.n) HIPCK(hipMemcpy(out + used, src + e.off, (size_t)e.n, hipMemcpyDeviceToHost));
+        if (e.n) HIPCK(hipMemcpyAsync(out + used, src + e.off, (size_t)e.n, hipMemcpyDeviceToHost, ctx->stD));
         ev[k] = hdrf_container_event{e.id, e.closed, e.off, e.n, used};
         used += e.n;
         k++;
     }
+    HIPCK(hipStreamSynchronize(ctx->stD));
     // the emitted ones are handed over
     const size_t kc = std::min<size_t>((size_t)k, nclosed);
     for (size_t i = 0; i < kc; i++) {

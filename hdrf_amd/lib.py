@@ -331,6 +331,20 @@ class Context:
             for e in ev[:n]:
                 out.append((e.id, e.closed, e.file_off, buf[e.data_off:e.data_off + e.nbytes].tobytes()))
 
+    def drain_into(self, ptr, cap, max_events=4096):
+        """hdrf_drain_containers into caller memory (e.g. pinned) until nothing is pending; the
+        bytes stay there (the bench's DataNode shape): returns (events, bytes) handed out."""
+        ev = (ContainerEvent * max_events)()
+        need = ctypes.c_int64()
+        nev = nbytes = 0
+        while True:
+            n = self._ck(self.L.hdrf_drain_containers(self._h, ev, max_events, ctypes.cast(ptr, _u8p), cap,
+                                                      ctypes.byref(need)))
+            if n == 0:
+                return nev, nbytes
+            nev += n
+            nbytes += sum(e.nbytes for e in ev[:n])
+
     def reduce_batch(self, dev_ptrs, lens, readable, block_ids):
         n = len(dev_ptrs)
         ptrs = (_vp * n)(*dev_ptrs)

@@ -241,8 +241,11 @@ int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t ca
  * The bytes of event i are out[data_off, data_off + nbytes).  Events come in order (closes in
  * close order, then the open containers) and whole; returns the number written, 0 when nothing is
  * pending, HDRF_E_CAPACITY (and *need = the next event's bytes) when not even one fits.  Call again
- * until it returns 0.  Completes the batches in flight first.  A drained closed container's slot
- * may then be reused; read it back with hdrf_container_load. */
+ * until it returns 0.  Hands out what the COMPLETED batches (hdrf_wait_batch) produced; batches
+ * still in flight keep running (their containers come with a later drain), so a DataNode drains
+ * after every hdrf_wait_batch without stalling the pipeline.  The copies run on a stream of their
+ * own, beside the H2D copies of later blocks.  A drained closed container's slot may then be
+ * reused; read it back with hdrf_container_load. */
 typedef struct {
     uint32_t id;             /* container id (utilities.bytesToBlockID ranges, DN/utilities.java:36-75) */
     int32_t closed;

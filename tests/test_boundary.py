@@ -172,6 +172,48 @@ def test_durable_containers_drain_wrap_and_rebuild(compressor):
     ctx2.close()
 
 
+@pytest.mark.parametrize("compressor", [1, 2])
+def test_durable_drain_with_batches_in_flight(compressor):
+    """The streaming DataNode shape (BASELINE config 5, hdrf_jni.c): blocks submitted from host
+    memory three deep, and after every hdrf_wait_batch a drain hands out what the completed batches
+    produced while the later ones keep running.  Every drained file equals the oracle's container
+    (DN/DataDeduplicator.java:748-818) and nothing is lost when the rings wrap."""
+    cmax = 1 << 20
+    blocks = _blocks(71 + compressor, 20, 2 << 20, dup_div=8)
+    ids = [6500 + i for i in range(len(blocks))]
+    ctx = Context(compressor=compressor, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=1,
+                  index_log2=20, arena_slots=64, retain_containers=1)
+    ora = Oracle(compressor=compressor, max_size=cmax)
+    disk, pend = {}, []
+    for b, i in zip(blocks, ids):
+        ctx.submit_host([b.ctypes.data], [len(b)], [i])
+        pend.append((b, i))
+        if len(pend) == 3:
+            ctx.wait_batch()
+            ob, oi = pend.pop(0)
+            compare_block(ctx.batch_result(0), ora.reduce(ob, oi), tag=f"in-flight drain block {oi}")
+            _apply(disk, ctx.drain_containers(buf_bytes=1 << 20))
+    while pend:
+        ctx.wait_batch()
+        ob, oi = pend.pop(0)
+        compare_block(ctx.batch_result(0), ora.reduce(ob, oi), tag=f"in-flight drain block {oi}")
+        _apply(disk, ctx.drain_containers(buf_bytes=1 << 20))
+    assert ctx.drain_containers() == []
+    alloc = ora.allocator()
+    n_cont = 0
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, oc = ora.container(cid)
+            if od is None:
+                continue
+            n_cont += 1
+            assert cid in disk and bytes(disk[cid][0]) == bytes(od) and disk[cid][1] == oc, f"container {cid}"
+    assert n_cont == len(disk) and n_cont > 16 * 3
+    compare_state(ctx, ora, ids, tag=f"in-flight drain c{compressor}", containers=False)
+    ctx.close()
+
+
 def test_pipeline_depth_is_refused_not_waited():
     """A submit beyond HDRF_PIPELINE_DEPTH returns HDRF_E_CAPACITY (the caller's awaitOldest pairs
     one to one with its submits) and leaves the batches in flight untouched."""
