@@ -1,0 +1,10 @@
+#!/bin/bash
+# walk ring + prefetch check, gmax-stream A/B, config 5 (durable drain, raw copy probe, native packets)
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
+FILES="tests/test_bench_shape.py tests/test_gpu_parity.py tests/test_config2_shape.py tests/test_boundary.py tests/test_packet_driver.py" TAG=c5 bash scripts/r03_check.sh || exit 1
+NO_PMC=1 bash scripts/r03_ab.sh HDRF_GMAX_STREAM=1 HDRF_NT=3 HDRF_GMAX_STREAM=1 || exit 1
+timeout -k 10 600 python -u bench.py --workload config5 --steps 2 --warmup 1 --no-cpu > gpurun_out/r03_c5_v1.json.log 2>&1 || { tail -20 gpurun_out/r03_c5_v1.json.log; exit 1; }
+tail -1 gpurun_out/r03_c5_v1.json.log | python3 -c "import json,sys; d=json.load(sys.stdin); print('config5', d['value'], d['pcie'])"
+timeout -k 10 900 python -u bench.py --workload config5 --packet-driver cpp --packet-kib 64 --steps 2 > gpurun_out/r03_c5_pk64_v1.json.log 2>&1 || { tail -20 gpurun_out/r03_c5_pk64_v1.json.log; exit 1; }
+tail -1 gpurun_out/r03_c5_pk64_v1.json.log | cut -c1-600
