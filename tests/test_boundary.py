@@ -153,7 +153,7 @@ def test_durable_containers_drain_wrap_and_rebuild(compressor):
             n_cont += 1
             assert cid in disk, f"container {cid} never drained"
             assert bytes(disk[cid][0]) == bytes(od) and disk[cid][1] == oc, f"container {cid} file differs"
-    assert n_cont == len(disk) and n_cont > 8 * 3, "the ring of 8 slots per range must have wrapped"
+    assert n_cont == len(disk) and n_cont > 16 * 3, "the ring of 16 slots per range must have wrapped"
     wrapped = sum(ctx.container(cid)[0] is None for cid in disk)
     assert wrapped > 0
     compare_state(ctx, ora, ids, tag=f"durable c{compressor}", containers=False)   # files compared above
@@ -179,10 +179,10 @@ def test_durable_drain_with_batches_in_flight(compressor):
     produced while the later ones keep running.  Every drained file equals the oracle's container
     (DN/DataDeduplicator.java:748-818) and nothing is lost when the rings wrap."""
     cmax = 1 << 20
-    blocks = _blocks(71 + compressor, 20, 2 << 20, dup_div=8)
+    blocks = _blocks(71 + compressor, 40, 2 << 20, dup_div=8)
     ids = [6500 + i for i in range(len(blocks))]
     ctx = Context(compressor=compressor, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=1,
-                  index_log2=20, arena_slots=32, retain_containers=1)
+                  index_log2=20, arena_slots=64, retain_containers=1)
     ora = Oracle(compressor=compressor, max_size=cmax)
     disk, pend = {}, []
     for b, i in zip(blocks, ids):
@@ -209,7 +209,7 @@ def test_durable_drain_with_batches_in_flight(compressor):
                 continue
             n_cont += 1
             assert cid in disk and bytes(disk[cid][0]) == bytes(od) and disk[cid][1] == oc, f"container {cid}"
-    assert n_cont == len(disk) and n_cont > 8 * 3, "the ring of 8 slots per range must have wrapped"
+    assert n_cont == len(disk) and n_cont > 16 * 3, "the ring of 16 slots per range must have wrapped"
     assert sum(ctx.container(cid)[0] is None for cid in disk) > 0
     compare_state(ctx, ora, ids, tag=f"in-flight drain c{compressor}", containers=False)
     ctx.close()
