@@ -153,7 +153,7 @@ def test_durable_containers_drain_wrap_and_rebuild(compressor):
             n_cont += 1
             assert cid in disk, f"container {cid} never drained"
             assert bytes(disk[cid][0]) == bytes(od) and disk[cid][1] == oc, f"container {cid} file differs"
-    assert n_cont == len(disk) and n_cont > 16 * 3, "the ring of 16 slots per range must have wrapped"
+    assert n_cont == len(disk) and n_cont > 8 * 3, "the ring of 8 slots per range must have wrapped"
     wrapped = sum(ctx.container(cid)[0] is None for cid in disk)
     assert wrapped > 0
     compare_state(ctx, ora, ids, tag=f"durable c{compressor}", containers=False)   # files compared above
