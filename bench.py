@@ -145,7 +145,10 @@ def main():
         # k+2 starts while batch k+1 hashes instead of after batch k's read-back
         a.depth = 5 if a.workload == "config4" else 3
     if not a.arena_slots:
-        a.arena_slots = 1792 if a.workload == "config4" else 512
+        # config 5 keeps durable containers: a submit is refused while the worst-case closes of the
+        # batches in flight (<= 2 x new bytes / maxSize + 1 per block and storer range, three 32-block
+        # batches) could reach an undrained slot, so its rings hold ~500 slots each (64 GiB of 288)
+        a.arena_slots = {"config4": 1792, "config5": 2048}.get(a.workload, 512)
     if a.workload == "config4":
         # two LZ4 streams beside the four of the batch pipeline: hardware queues for all six (HIP's
         # default is 4, and streams sharing a queue serialise); read when HIP initialises
