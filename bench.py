@@ -97,6 +97,8 @@ def parse():
                          "0 = whole blocks through hdrf_submit_host")
     ap.add_argument("--packet-threads", type=int, default=4,
                     help="config5 packets: receiver threads appending different blocks' packets concurrently")
+    ap.add_argument("--no-drain", action="store_true",
+                    help="config5: ring arena without durable containers (A/B of the drain's cost only)")
     ap.add_argument("--packet-driver", choices=["python", "cpp"], default="python",
                     help="config5 packets: 'cpp' runs tests/cpp/packet_driver.cpp (native receiver threads on the "
                          "C-ABI the JNI binding calls, durable containers drained after every block) as a child "
@@ -192,7 +194,7 @@ def main():
     # opens it) handed out to pinned host memory after every completed batch, inside the timed region
     ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
                   arena_slots=a.arena_slots, keep_recipes=a.keep_recipes, timing=1, n_ranks=world, rank=rank,
-                  compressor=compressor, retain_containers=1 if host else 0)
+                  compressor=compressor, retain_containers=1 if host and not a.no_drain else 0)
     node = None
     if world > 1:
         from hdrf_amd.node import NodeRank, global_block
@@ -212,7 +214,7 @@ def main():
     if host:                                             # the DataNode's received blocks, in host memory
         hbuf = ctx.host_alloc(nb * S)
         ctx.L.hdrf_memcpy_d2h(ctx._h, hbuf.ctypes.data, dev, nb * S)
-        dbuf = ctx.host_alloc(1 << 30)                   # the drained container files (pinned)
+        dbuf = None if a.no_drain else ctx.host_alloc(1 << 30)   # the drained container files (pinned)
         h2d_gbs = raw_h2d_rate(torch, local, S)
     batches = []
     for b0 in range(0, nb, B):
@@ -544,7 +546,8 @@ def main():
     ctx.dev_free(dev)
     if hbuf is not None:
         ctx.host_free(hbuf)
-        ctx.host_free(dbuf)
+        if dbuf is not None:
+            ctx.host_free(dbuf)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

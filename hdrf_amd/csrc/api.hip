@@ -117,6 +117,8 @@ struct hdrf_ctx {
     hipStream_t stG = nullptr;   // stream G: the granule-max pass (HDRF_GMAX_STREAM), ahead of W
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
     hipStream_t stD = nullptr;   // stream D: container drain D2H (beside the H2D copies on C)
+    XferJob *h_xfer = nullptr;   // drain copy jobs (pinned, read by xfer_kernel)
+    int xfer_cap = 0;
     hipStream_t stL[2] = {};     // compressor 2: LZ4 streams, alternating by batch (off stream B)
     // chunks >= 64 KiB were seen in the last completed batch: sha_full hashes them on dedicated
     // lanes (sha.hip); off otherwise, where the scan for them costs config 2 ~3 %
@@ -340,6 +342,7 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->stG) (void)hipStreamDestroy(ctx->stG);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
     if (ctx->stD) (void)hipStreamDestroy(ctx->stD);
+    if (ctx->h_xfer) (void)hipHostFree(ctx->h_xfer);
     for (auto L : ctx->stL)
         if (L) (void)hipStreamDestroy(L);
     for (auto &r : ctx->rx)
@@ -2536,7 +2539,20 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
         const int64_t done = ctx->handed.count(id) ? ctx->handed[id] : 0;
         if ((int64_t)it->second.len > done) todo.push_back(Pend{id, 0, done, (int64_t)it->second.len - done, it->second});
     }
+    // pinned (device-mapped) output: the CUs write it (xfer_kernel), beside the SDMA H2D of later
+    // blocks; pageable output: hipMemcpyAsync.  HDRF_DRAIN_KERNEL=0 forces the copy engine.
+    static const bool kern_env = [] { const char *e = getenv("HDRF_DRAIN_KERNEL"); return !e || atoi(e) != 0; }();
+    hipPointerAttribute_t pa;
+    const bool mapped = kern_env && out_cap > 0 && hipPointerGetAttributes(&pa, out) == hipSuccess &&
+                        pa.type == hipMemoryTypeHost && pa.devicePointer != nullptr;
+    (void)hipGetLastError();
+    if (mapped && ctx->xfer_cap == 0) {
+        HIPCK(hipHostMalloc((void **)&ctx->h_xfer, sizeof(XferJob) * 1024, hipHostMallocDefault));
+        ctx->xfer_cap = 1024;
+    }
     int64_t k = 0, used = 0;
+    int nj = 0;
+    uint64_t maxj = 0;
     for (const Pend &e : todo) {
         if (k >= ev_cap || used + e.n > out_cap) {
             if (need) *need = e.n;
@@ -2544,11 +2560,24 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
         }
         const uint8_t *src = (e.closed && c.compressor == 2) ? ctx->d_carena + (size_t)e.ci.slot * ctx->cslot
                                                              : ctx->d_arena + (size_t)e.ci.slot * c.container_max;
-        if (e.n) HIPCK(hipMemcpyAsync(out + used, src + e.off, (size_t)e.n, hipMemcpyDeviceToHost, ctx->stD));
+        if (e.n && mapped) {
+            if (nj == ctx->xfer_cap) {                    // job list full: flush it
+                HIPCK(launch_xfer(ctx->h_xfer, nj, maxj, ctx->stD));
+                HIPCK(hipStreamSynchronize(ctx->stD));
+                nj = 0;
+                maxj = 0;
+            }
+            ctx->h_xfer[nj++] = XferJob{(uint64_t)(uintptr_t)(src + e.off),
+                                        (uint64_t)(uintptr_t)((uint8_t *)pa.devicePointer + used), (uint64_t)e.n};
+            maxj = std::max<uint64_t>(maxj, (uint64_t)e.n);
+        } else if (e.n) {
+            HIPCK(hipMemcpyAsync(out + used, src + e.off, (size_t)e.n, hipMemcpyDeviceToHost, ctx->stD));
+        }
         ev[k] = hdrf_container_event{e.id, e.closed, e.off, e.n, used};
         used += e.n;
         k++;
     }
+    if (nj) HIPCK(launch_xfer(ctx->h_xfer, nj, maxj, ctx->stD));
     HIPCK(hipStreamSynchronize(ctx->stD));
     // the emitted ones are handed over
     const size_t kc = std::min<size_t>((size_t)k, nclosed);

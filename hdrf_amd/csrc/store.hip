@@ -521,6 +521,27 @@ __global__ void __launch_bounds__(256) recipe_copy_kernel(const RecipeCopy *__re
     for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < j.words; i += gridDim.y * 256) dst[i] = src[i];
 }
 
+// Container drain (api.hip hdrf_drain_containers) into pinned host memory: the CUs write the bytes
+// straight across PCIe (the host buffer is device-mapped), so the D2H of a DataNode's container files
+// runs beside the SDMA engine's H2D copies of the next blocks instead of queueing behind them.
+// grid (jobs, pieces): workgroup (j, y) copies piece y (kXferPiece bytes) of job j.
+constexpr uint64_t kXferPiece = 256 << 10;
+__global__ void __launch_bounds__(256) xfer_kernel(const XferJob *__restrict__ jobs)
+{
+    const XferJob J = jobs[blockIdx.x];
+    const uint64_t o = (uint64_t)blockIdx.y * kXferPiece;
+    if (o >= J.n) return;
+    const uint64_t n = J.n - o < kXferPiece ? J.n - o : kXferPiece;
+    wg_copy<false>((uint8_t *)(uintptr_t)(J.dst + o), (const uint8_t *)(uintptr_t)(J.src + o), (uint32_t)n);
+}
+
+hipError_t launch_xfer(const XferJob *jobs, int n, uint64_t max_bytes, hipStream_t st)
+{
+    const uint64_t pieces = (max_bytes + kXferPiece - 1) / kXferPiece;
+    if (n > 0 && pieces > 0) hipLaunchKernelGGL(xfer_kernel, dim3(n, (unsigned)pieces), dim3(256), 0, st, jobs);
+    return hipGetLastError();
+}
+
 hipError_t launch_recipe_copy(const RecipeCopy *jobs, int n, hipStream_t st)
 {
     if (n > 0) hipLaunchKernelGGL(recipe_copy_kernel, dim3(n, 8), dim3(256), 0, st, jobs, n);

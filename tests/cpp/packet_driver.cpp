@@ -84,7 +84,7 @@ int main(int argc, char **argv)
     cfg.max_batch_blocks = 1;
     cfg.index_log2 = 27;
     cfg.arena_slots = 512;
-    cfg.retain_containers = 1;
+    cfg.retain_containers = std::getenv("HDRF_DRIVER_NODRAIN") ? 0 : 1;
     if (int rc = hdrf_open(&cfg, &ctx)) {
         std::fprintf(stderr, "hdrf_open: %d\n", rc);
         return 1;
@@ -115,11 +115,12 @@ int main(int argc, char **argv)
             for (int64_t i = 0; i < n; i++) drained_bytes += ev[(size_t)i].nbytes;
         }
     };
+    const bool no_drain = std::getenv("HDRF_DRIVER_NODRAIN") != nullptr;      // A/B only
     auto complete = [&]() {
         CK(hdrf_wait_batch(ctx));
         CK(hdrf_batch_info(ctx, 0, &n_chunks[(size_t)done], &store[(size_t)done]));
         done++;
-        drain();
+        if (!no_drain) drain();
     };
     const int kDepth = 5, kRx = 8;                 // HDRF_PIPELINE_DEPTH, receive buffers
     double best = 0, total_s = 0;
