@@ -532,6 +532,11 @@ def main():
             line["pcie"] = {"h2d_GB_s_raw_copy": round(h2d_gbs, 2), "value_over_raw_copy": round(value / h2d_gbs, 4),
                             "raw_copy": "pinned host -> HBM, 128 MiB hipMemcpyAsync pieces, 4 in flight on one "
                                         "stream, timed with HIP events (torch)",
+                            "link_GB_s": round((nb * S + drained["bytes"] / max(1, a.steps)) / (el / a.steps) / 1e9, 2),
+                            "link_frac_of_raw_copy": round((nb * S + drained["bytes"] / max(1, a.steps)) / (el / a.steps)
+                                                           / 1e9 / h2d_gbs, 4),
+                            "link_note": "H2D block bytes + D2H container bytes per second over the measured raw "
+                                         "copy rate: the PCIe link carries both directions at about that total rate",
                             "drained_container_bytes_per_step": drained["bytes"] // max(1, a.steps),
                             "drained_events_per_step": drained["events"] // max(1, a.steps),
                             "d2h_GB_s_drain": round(drained["bytes"] / max(1, a.steps) / (el / a.steps) / 1e9, 2),
