@@ -123,15 +123,11 @@ __device__ __forceinline__ void pad_block(uint32_t m[16], uint32_t len, uint32_t
 // steady state, and slot 0 only for T == 0 (a chunk under 64 B) or the length-only block T + 1.
 // The padding is wave-uniform (ballot) because nearly every iteration has some lane at its tail;
 // for the lanes not at their tail it changes nothing.
-template <int HW>
-__device__ __forceinline__ void sha_iter(const uint8_t *base, uint64_t readable, uint32_t s0, uint32_t len, uint32_t T,
-                                         uint32_t nb, uint32_t &bi, uint32_t st[8])
+// The 33 dwords (132 B) of a window at pos (4-aligned down); `two`: both blocks of a pair.  Near
+// the end of the readable bytes the guarded path reads past-the-end bytes as 0 (padding hides them).
+__device__ __forceinline__ void load_win(const uint8_t *base, uint64_t readable, uint32_t pos, bool two, uint32_t d[33])
 {
-    const bool two = bi < T && ((T - bi) & 1u);
-    const uint32_t pos = s0 + 64u * bi;
     const uint32_t apos = pos & ~3u;
-    const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
-    uint32_t d[33];
     if ((uint64_t)apos + 132u <= readable) {          // all but a block's last chunk
         const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
 #pragma unroll
@@ -147,10 +143,20 @@ __device__ __forceinline__ void sha_iter(const uint8_t *base, uint64_t readable,
                 d[17 + 4 * q] = v.x; d[18 + 4 * q] = v.y; d[19 + 4 * q] = v.z; d[20 + 4 * q] = v.w;
             }
         }
-    } else {                                          // bytes past `readable` read as 0 (padding hides them)
+    } else {
 #pragma unroll
         for (int q = 0; q < 33; q++) d[q] = load4_guard(base, (int64_t)apos + 4 * q, (int64_t)readable);
     }
+}
+
+__device__ __forceinline__ bool pair_at(uint32_t bi, uint32_t T) { return bi < T && ((T - bi) & 1u); }
+
+// The compressions of one iteration from a loaded window (see sha_iter).
+template <int HW>
+__device__ __forceinline__ void sha_compute(const uint32_t d[33], uint32_t pos, uint32_t len, uint32_t T, uint32_t nb,
+                                            uint32_t bi, bool two, uint32_t st[8])
+{
+    const uint32_t sel = 0x00010203u + (pos & 3u) * 0x01010101u;
     uint32_t m[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
@@ -164,6 +170,17 @@ __device__ __forceinline__ void sha_iter(const uint8_t *base, uint64_t readable,
         if (HW == 5) sha1_compress(st, m);
         else sha256_compress(st, m);
     }
+}
+
+template <int HW>
+__device__ __forceinline__ void sha_iter(const uint8_t *base, uint64_t readable, uint32_t s0, uint32_t len, uint32_t T,
+                                         uint32_t nb, uint32_t &bi, uint32_t st[8])
+{
+    const bool two = pair_at(bi, T);
+    const uint32_t pos = s0 + 64u * bi;
+    uint32_t d[33];
+    load_win(base, readable, pos, two, d);
+    sha_compute<HW>(d, pos, len, T, nb, bi, two, st);
     bi += two ? 2u : 1u;
 }
 
@@ -189,6 +206,63 @@ __device__ __forceinline__ void store_digest(uint32_t *dst, const uint32_t st[8]
 constexpr uint32_t kShaLong = 65536;
 constexpr int kShaTile = 1024;                 // chunks per scan tile (4 per thread)
 
+// The long-chunk lanes: workgroups at y = 0 of the SHA grid (see above).
+template <int HW>
+__device__ __forceinline__ void sha_long_lanes(const BlockDesc *__restrict__ blocks, const uint32_t *__restrict__ offsets,
+                                               const BlockState *__restrict__ bst, int cap_blk,
+                                               uint32_t *__restrict__ digests, uint32_t thr)
+{
+    if (thr == 0xffffffffu) return;
+    __shared__ uint32_t s_long[kShaTile + 256];
+    __shared__ uint32_t s_nl;
+    const int t = threadIdx.x;
+    if (t == 0) s_nl = 0;
+    __syncthreads();
+    auto drain = [&]() {                       // every listed chunk: one lane's chain
+        const uint32_t nl = s_nl;
+        for (uint32_t i = t; i < nl; i += 256) {
+            const uint32_t e = s_long[i];
+            const int lb = (int)(e >> 26), lk = (int)(e & 0x3ffffffu);   // block < 64, chunk < cap_blk < 2^26
+            const uint32_t *lo = offsets + (size_t)lb * cap_blk;
+            const uint32_t s0 = lk ? lo[lk - 1] : 0u;
+            const uint32_t len = lo[lk] - s0, T = len >> 6, nb = (len + 8) / 64 + 1;
+            uint32_t st[8], bi = 0;
+            set_iv<HW>(st);
+            const BlockDesc &lbd = blocks[lb];
+            while (bi < nb) sha_iter<HW>(lbd.data, lbd.readable, s0, len, T, nb, bi, st);
+            store_digest<HW>(digests + ((size_t)lb * cap_blk + lk) * HW, st);
+        }
+        __syncthreads();
+        if (t == 0) s_nl = 0;
+        __syncthreads();
+    };
+    const int nblk = (int)gridDim.y - 1;
+    for (int lb = 0; lb < nblk; lb++) {
+        const int n = bst[lb].n_chunks;
+        const uint32_t *lo = offsets + (size_t)lb * cap_blk;
+        for (int tb = blockIdx.x * kShaTile; tb < n; tb += gridDim.x * kShaTile) {
+            const int k0 = tb + 4 * t;
+            uint32_t o[5];
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const int k = k0 - 1 + j;
+                o[j] = (k >= 0 && k < n) ? lo[k] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (k0 + j < n && o[j + 1] - o[j] >= thr) s_long[atomicAdd(&s_nl, 1u)] = ((uint32_t)lb << 26) | (uint32_t)(k0 + j);
+            __syncthreads();
+            const uint32_t cnt = s_nl;
+            __syncthreads();
+            if (cnt >= 256) drain();          // <= 255 + kShaTile entries at any time
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = s_nl;
+    __syncthreads();
+    if (cnt) drain();
+}
+
 // grid (waves_per_block/4, nblocks + 1): every wave of y = b + 1 serves chunks of block b.  A lane
 // owns one chunk's whole compression chain, padding and digest included (the separate tail kernel
 // and its mid-state round trip are gone: 1.2 GB of 128-B line fetches per 4 GiB batch, PMC r03).
@@ -203,55 +277,7 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
                                                         uint32_t thr)
 {
     if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
-        if (thr == 0xffffffffu) return;
-        __shared__ uint32_t s_long[kShaTile + 256];
-        __shared__ uint32_t s_nl;
-        const int t = threadIdx.x;
-        if (t == 0) s_nl = 0;
-        __syncthreads();
-        auto drain = [&]() {                       // every listed chunk: one lane's chain
-            const uint32_t nl = s_nl;
-            for (uint32_t i = t; i < nl; i += 256) {
-                const uint32_t e = s_long[i];
-                const int lb = (int)(e >> 26), lk = (int)(e & 0x3ffffffu);   // block < 64, chunk < cap_blk < 2^26
-                const uint32_t *lo = offsets + (size_t)lb * cap_blk;
-                const uint32_t s0 = lk ? lo[lk - 1] : 0u;
-                const uint32_t len = lo[lk] - s0, T = len >> 6, nb = (len + 8) / 64 + 1;
-                uint32_t st[8], bi = 0;
-                set_iv<HW>(st);
-                const BlockDesc &lbd = blocks[lb];
-                while (bi < nb) sha_iter<HW>(lbd.data, lbd.readable, s0, len, T, nb, bi, st);
-                store_digest<HW>(digests + ((size_t)lb * cap_blk + lk) * HW, st);
-            }
-            __syncthreads();
-            if (t == 0) s_nl = 0;
-            __syncthreads();
-        };
-        const int nblk = (int)gridDim.y - 1;
-        for (int lb = 0; lb < nblk; lb++) {
-            const int n = bst[lb].n_chunks;
-            const uint32_t *lo = offsets + (size_t)lb * cap_blk;
-            for (int tb = blockIdx.x * kShaTile; tb < n; tb += gridDim.x * kShaTile) {
-                const int k0 = tb + 4 * t;
-                uint32_t o[5];
-#pragma unroll
-                for (int j = 0; j < 5; j++) {
-                    const int k = k0 - 1 + j;
-                    o[j] = (k >= 0 && k < n) ? lo[k] : 0u;
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (k0 + j < n && o[j + 1] - o[j] >= thr) s_long[atomicAdd(&s_nl, 1u)] = ((uint32_t)lb << 26) | (uint32_t)(k0 + j);
-                __syncthreads();
-                const uint32_t cnt = s_nl;
-                __syncthreads();
-                if (cnt >= 256) drain();          // <= 255 + kShaTile entries at any time
-            }
-        }
-        __syncthreads();
-        const uint32_t cnt = s_nl;
-        __syncthreads();
-        if (cnt) drain();
+        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr);
         return;
     }
     const int b = blockIdx.y - 1;
@@ -321,6 +347,123 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
     }
 }
 
+// sha_pf: the same work at ONE wave per SIMD, each lane's next window loaded one iteration ahead
+// (two register windows, the loop unrolled twice so neither is copied).  At two waves per SIMD the
+// lanes' pending 128-B lines (the second line of each window, re-read by the next iteration) fill
+// the 4 MiB L2 of an XCD and ~48 % of them are fetched twice (PMC r03: 1.48x the algorithmic bytes);
+// one wave per SIMD halves the lines in flight (1.19x), and the prefetch keeps the SIMD busy while
+// the next window is on its way.  A lane finishing its chunk in this iteration takes its next chunk
+// before the prefetch is issued, so the next chunk's first window is prefetched too.
+template <int HW>
+__global__ void __launch_bounds__(256) sha_pf_kernel(const BlockDesc *__restrict__ blocks,
+                                                     const uint32_t *__restrict__ offsets,
+                                                     const BlockState *__restrict__ bst, int cap_blk,
+                                                     uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                                     uint32_t thr)
+{
+    if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
+        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr);
+        return;
+    }
+    const int b = blockIdx.y - 1;
+    const int n = bst[b].n_chunks;
+    const BlockDesc &bd = blocks[b];
+    const uint8_t *base = bd.data;
+    const uint64_t readable = bd.readable;
+    const uint32_t *off = offsets + (size_t)b * cap_blk;
+    uint32_t *db = digests + (size_t)b * cap_blk * HW;
+    const int l = lane_id();
+    int kbP, cntP, kbQ, cntQ;
+    uint32_t SP, EP, SQ, EQ;
+    auto reserve = [&](int &kb, int &cnt, uint32_t &S, uint32_t &E) {
+        uint32_t got = 0;
+        if (l == 0) got = atomicAdd(queue + b, 64u);
+        kb = (int)rdfirst(got);
+        cnt = max(0, min(64, n - kb));
+        const int k = kb + l;
+        E = l < cnt ? ld4(off + k) : 0u;
+        S = (l < cnt && k > 0) ? ld4(off + k - 1) : 0u;
+    };
+    reserve(kbP, cntP, SP, EP);
+    reserve(kbQ, cntQ, SQ, EQ);
+    int head = 0;
+    bool act = false, has_n = false;
+    int k = 0, k2 = 0;
+    uint32_t s0 = 0, len = 0, T = 0, nb = 0, bi = 0, s2 = 0, len2 = 0;
+    uint32_t st[8];
+    set_iv<HW>(st);
+    // lanes with `want` and no next chunk get one from the pool (long chunks are skipped: the long
+    // lanes hash them)
+    auto take = [&](bool want) {
+        for (;;) {
+            const unsigned long long req = ballot64(want && !has_n);
+            if (!req) break;
+            if (head >= cntP) {                   // pool P exhausted: rotate in Q, fetch the next
+                if (cntQ == 0) break;
+                kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
+                reserve(kbQ, cntQ, SQ, EQ);
+            }
+            const bool mine = want && !has_n;
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(req >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req, 0));
+            const int avail = cntP - head;
+            const int idx = min(head + rank, 63);
+            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
+            bool skip = false;
+            if (ballot64(mine && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
+            if (mine && rank < avail) {
+                if (e - c0 >= thr) {
+                    skip = true;
+                } else {
+                    k2 = kbP + head + rank;
+                    s2 = c0;
+                    len2 = e - c0;
+                    has_n = true;
+                }
+            }
+            const int nreq = __popcll(req);
+            head += min(nreq, avail);
+            if (!ballot64(skip) && nreq <= avail) break;
+        }
+    };
+    auto promote = [&]() {
+        k = k2; s0 = s2; len = len2;
+        T = len >> 6;
+        nb = (len + 8) / 64 + 1;
+        bi = 0;
+        set_iv<HW>(st);
+        has_n = false;
+    };
+    // one iteration on window dc (blocks bi, bi + 1 of the current chunk), prefetching into dn
+    auto step = [&](uint32_t (&dc)[33], uint32_t (&dn)[33]) -> bool {
+        take(!act);                                // idle lanes (start, or after a pool gap)
+        if (!act && has_n) {
+            promote();
+            act = true;
+            load_win(base, readable, s0, true, dc);   // not prefetched: waits this iteration
+        }
+        if (!ballot64(act)) return false;
+        const bool two = act && pair_at(bi, T);
+        const uint32_t bin = bi + (two ? 2u : 1u);
+        take(act && bin >= nb);                    // finishing now: the next chunk, to prefetch it
+        if (act && (bin < nb || has_n)) load_win(base, readable, bin < nb ? s0 + 64u * bin : s2, true, dn);
+        if (act) {
+            sha_compute<HW>(dc, s0 + 64u * bi, len, T, nb, bi, two, st);
+            bi = bin;
+            if (bi >= nb) {                        // chain done: the digest
+                store_digest<HW>(db + (size_t)k * HW, st);
+                if (has_n) promote();
+                else act = false;
+            }
+        }
+        return true;
+    };
+    uint32_t da[33], dd[33];
+    for (;;) {
+        if (!step(da, dd)) break;
+        if (!step(dd, da)) break;
+    }
+}
+
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
                       hipStream_t st, Marker *mk)
@@ -340,11 +483,17 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     // 919 at 4) — fewer concurrent per-lane streams thrash L2 less and leave CUs to the
     // co-running place / granule passes; env knobs for
     // experiments: HDRF_SHA_WAVES (waves per SIMD over 1024 SIMDs), HDRF_SHA_LDS (bytes per WG)
-    static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : 2; }();
+    // HDRF_SHA_PF: 1 = sha_pf (one wave per SIMD, windows prefetched), 0 = sha_chunk (two waves per SIMD)
+    static const bool pf = [] { const char *e = getenv("HDRF_SHA_PF"); return e ? atoi(e) != 0 : false; }();
+    static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : (pf ? 1 : 2); }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     const int wpb = std::max(4, (per_simd * 1024 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
-    if (hasher == 0)
+    if (pf && hasher == 0)
+        hipLaunchKernelGGL(sha_pf_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    else if (pf)
+        hipLaunchKernelGGL(sha_pf_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    else if (hasher == 0)
         hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
     else
         hipLaunchKernelGGL(sha_chunk_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
