@@ -21,7 +21,10 @@ done
 [ -n "$NO_PMC" ] && exit 0
 export TMPDIR=/tmp
 j=0
-for v in $(printf '%s\n' "$@" | sort -u); do
+declare -A seen
+for v in "$@"; do
+  [ -n "${seen[$v]}" ] && continue
+  seen[$v]=1
   j=$((j+1))
   OUT=$R/gpurun_out/pmc_${TAG}_$j; mkdir -p $OUT
   echo "$v" > $OUT/variant.txt
