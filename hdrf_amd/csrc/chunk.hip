@@ -519,7 +519,7 @@ __global__ void __launch_bounds__(256) gmax_kernel(const BlockDesc *__restrict__
 //     LDS only), so every boundary is settled inside one wave.  A lane that meets no shared cut
 //     within kLaneOver cuts or ~seg_len bytes reports kSyncFail and queues its boundary for the
 //     repair pass.
-constexpr int kGmWin = 32;               // dwords of granule maxima a lane holds (128 granules)
+constexpr int kGmWin = 16;               // dwords of granule maxima a lane holds (64 granules)
 
 __device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b)
 {
@@ -607,62 +607,63 @@ typedef __attribute__((address_space(3))) volatile uint16_t lds_u16v;
 typedef __attribute__((address_space(3))) volatile uint8_t lds_u8v;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
-// A lane's granule maxima, staged through LDS: a ring of two 128-granule lines (256 granules = 4 KiB
-// of data) in front of the lane's walk, so each 128-B line of maxima is fetched from memory once per
-// lane (it used to be re-fetched by every chunk step: ~2 line fetches per chunk, the lane's window
-// lines did not survive in L2 between its steps; PMC r03 1.55e7 requests per 4 GiB batch).  The window
-// of a step (128 maxima from W0 = G0 & ~3) is read from the ring at any dword offset.
-constexpr int kRingDw = 64;              // ring dwords per lane (a row: lanes read at their own, unrelated
-constexpr int kRingPitch = kRingDw;      // offsets, so no padding; 82 KB per workgroup -> 2 per CU)
-// The next line is prefetched into registers at the end of a chunk step once the window has moved
-// into the ring's second line (after the step's raw load has been waited for, so that wait never
-// covers the prefetch), and written into the ring when the window reaches it.
+// A lane's granule maxima, staged through LDS: a ring of two 64-granule units (128 granules = 2 KiB
+// of data) in front of the lane's walk, so each granule maximum is fetched from memory once per lane
+// (they used to be re-fetched by every chunk step: ~2 line fetches per chunk, the lane's window lines
+// did not survive in L2 between its steps; PMC r03 1.55e7 -> 8.3e6 requests per 4 GiB batch).  The
+// window of a step (64 maxima from W0 = G0 & ~3) is read from the ring at any dword offset.  The
+// next unit is prefetched into registers at the end of a chunk step once the window has moved into
+// the ring's second unit (after the step's raw load was waited for, so that wait never covers the
+// prefetch), and written into the ring when the window reaches it.  12 KiB of LDS per wave.
+constexpr int kRingU = 4 * kGmWin;       // granules per ring unit (= the window)
+constexpr int kRingDw = 2 * kGmWin;      // ring dwords per lane (lanes read at their own, unrelated
+constexpr int kRingPitch = kRingDw;      // offsets, so rows are not padded)
 struct GmRing {
     lds_u32 *r;                          // this lane's row
-    int rb = -(1 << 20);                 // ring holds granules [rb, rb + 256), rb a multiple of 128
+    int rb = -(1 << 20);                 // ring holds granules [rb, rb + 2U), rb a multiple of U
     int w0 = 0;                          // the last window start
-    int pfg = -1;                        // granule of the line held in pf (-1: none)
-    uint4 pf[8];
-    __device__ __forceinline__ void put(int g, const uint4 (&v)[8])
+    int pfg = -1;                        // granule of the unit held in pf (-1: none)
+    uint4 pf[kGmWin / 4];
+    __device__ __forceinline__ void put(int g, const uint4 (&v)[kGmWin / 4])
     {
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
+        for (int i = 0; i < kGmWin / 4; i++) {
             const int w = ((g >> 2) + 4 * i) & (kRingDw - 1);
             r[w] = v[i].x; r[w + 1] = v[i].y; r[w + 2] = v[i].z; r[w + 3] = v[i].w;
         }
     }
-    __device__ __forceinline__ void fill(const uint8_t *gmb, int g)      // the line of granules [g, g + 128)
+    __device__ __forceinline__ void fill(const uint8_t *gmb, int g)      // the unit of granules [g, g + U)
     {
-        uint4 v[8];
+        uint4 v[kGmWin / 4];
 #pragma unroll
-        for (int i = 0; i < 8; i++) v[i] = ld16(gmb + g + 16 * i);
+        for (int i = 0; i < kGmWin / 4; i++) v[i] = ld16(gmb + g + 16 * i);
         put(g, v);
     }
     __device__ __forceinline__ void prefetch(const uint8_t *gmb)
     {
-        if (pfg != rb + 256 && w0 >= rb + 128 - 4 * kGmWin + 32) {
-            pfg = rb + 256;
+        if (pfg != rb + 2 * kRingU && w0 >= rb + kRingU / 2) {
+            pfg = rb + 2 * kRingU;
 #pragma unroll
-            for (int i = 0; i < 8; i++) pf[i] = ld16(gmb + pfg + 16 * i);
+            for (int i = 0; i < kGmWin / 4; i++) pf[i] = ld16(gmb + pfg + 16 * i);
         }
     }
     __device__ __forceinline__ void get(uint32_t (&d)[kGmWin], const uint8_t *gmb, int W0)
     {
         w0 = W0;
-        if (W0 < rb || W0 + 4 * kGmWin > rb + 256) {
-            if (W0 >= rb + 128 && W0 + 4 * kGmWin <= rb + 384) {   // the window moved on by one line
-                if (pfg == rb + 256) put(pfg, pf);
-                else fill(gmb, rb + 256);
-                rb += 128;
+        if (W0 < rb || W0 > rb + kRingU) {
+            if (W0 <= rb + 2 * kRingU) {                          // the window moved on by one unit
+                if (pfg == rb + 2 * kRingU) put(pfg, pf);
+                else fill(gmb, rb + 2 * kRingU);
+                rb += kRingU;
             } else {                                              // first use, or a long search jumped
-                rb = W0 & ~127;
+                rb = W0 & ~(kRingU - 1);
                 fill(gmb, rb);
-                fill(gmb, rb + 128);
+                fill(gmb, rb + kRingU);
             }
         }
-        const int w0 = W0 >> 2;
+        const int wd = W0 >> 2;
 #pragma unroll
-        for (int i = 0; i < kGmWin; i++) d[i] = r[(w0 + i) & (kRingDw - 1)];
+        for (int i = 0; i < kGmWin; i++) d[i] = r[(wd + i) & (kRingDw - 1)];
     }
 };
 
@@ -773,10 +774,8 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
                         ring.get(d, gmb, W0);
                     }
                     const unsigned long long m0 = gm_ge64(d, 0, C, Cm) & bits_from(Gs - W0) & bits_to(Glim - W0);
-                    const unsigned long long m1 =
-                        gm_ge64(d, 1, C, Cm) & bits_from(Gs - W0 - 64) & bits_to(Glim - W0 - 64);
-                    if (m0 | m1) {
-                        const int g = W0 + (m0 ? __builtin_ctzll(m0) : 64 + __builtin_ctzll(m1));
+                    if (m0) {
+                        const int g = W0 + __builtin_ctzll(m0);
                         rh = ld16(base + 16 * g);
                         gh = g;
                         const uint32_t h = gran_ge(rh, C, Cm) & range16(0, lim - 16 * g);
