@@ -485,9 +485,15 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     // experiments: HDRF_SHA_WAVES (waves per SIMD over 1024 SIMDs), HDRF_SHA_LDS (bytes per WG)
     // HDRF_SHA_PF: 1 = sha_pf (one wave per SIMD, windows prefetched), 0 = sha_chunk (two waves per SIMD)
     static const bool pf = [] { const char *e = getenv("HDRF_SHA_PF"); return e ? atoi(e) != 0 : false; }();
-    static const int per_simd = [] { const char *e = getenv("HDRF_SHA_WAVES"); return e ? atoi(e) : (pf ? 1 : 2); }();
+    // HDRF_SHA_WPC: waves per CU over the chip's 256 CUs (overrides HDRF_SHA_WAVES x 4)
+    static const int per_cu = [] {
+        const char *c = getenv("HDRF_SHA_WPC");
+        if (c) return atoi(c);
+        const char *e = getenv("HDRF_SHA_WAVES");
+        return 4 * (e ? atoi(e) : (pf ? 1 : 2));
+    }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
-    const int wpb = std::max(4, (per_simd * 1024 / nblocks) & ~3);
+    const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
     if (pf && hasher == 0)
         hipLaunchKernelGGL(sha_pf_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
