@@ -347,32 +347,57 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
     }
 }
 
-// sha_pf: the same work at ONE wave per SIMD, each lane's next window loaded one iteration ahead
-// (two register windows, the loop unrolled twice so neither is copied).  At two waves per SIMD the
-// lanes' pending 128-B lines (the second line of each window, re-read by the next iteration) fill
-// the 4 MiB L2 of an XCD and ~48 % of them are fetched twice (PMC r03: 1.48x the algorithmic bytes);
-// one wave per SIMD halves the lines in flight (1.19x), and the prefetch keeps the SIMD busy while
-// the next window is on its way.  A lane finishing its chunk in this iteration takes its next chunk
-// before the prefetch is issued, so the next chunk's first window is prefetched too.
+// sha_ring: the same lanes, but no 128-B line is fetched twice.  A lane's pair window (132 B from
+// a 4-aligned start) spans the absolute 128-B line L holding its start and line L + 1.  The lane keeps
+// line L in an LDS slot of its own; each iteration loads line L + 1 whole (8 x 16 B, aligned), reads
+// the window's part in L from the slot, overwrites the slot with L + 1, reads the part in L + 1 (the
+// slot read at a per-lane dword offset is the realignment), and the next window starts in L + 1.  So
+// a chunk's lines are fetched once each (plus the line it shares with its neighbour), instead of the
+// 1.48x of sha_chunk, whose lanes' re-read lines did not survive in L2 (PMC r03).  Pairing as in
+// sha_iter: a chunk whose block T (the message end) is even starts one block early (a skipped slot),
+// so every iteration steps by 128 B, T is always in the second slot, and the length-only block T + 1
+// (if any) is the first slot of a last iteration that loads nothing.
+constexpr int kSlotDw = 33;                   // 32 dwords + 1 pad (bank spread) per lane
+typedef __attribute__((address_space(3))) uint32_t lds_w;
+
+// the absolute 128-B line at block offset lo (may start before the block: those bytes read as 0)
+__device__ __forceinline__ void load_line(const uint8_t *base, int64_t readable, int64_t lo, uint32_t (&R)[32])
+{
+    if (lo >= 0 && lo + 128 <= readable) {
+        const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + lo);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
+            R[4 * q] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 32; q++) R[q] = lo + 4 * q >= 0 ? load4_guard(base, lo + 4 * q, readable) : 0u;
+    }
+}
+
 template <int HW>
-__global__ void __launch_bounds__(256) sha_pf_kernel(const BlockDesc *__restrict__ blocks,
-                                                     const uint32_t *__restrict__ offsets,
-                                                     const BlockState *__restrict__ bst, int cap_blk,
-                                                     uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                     uint32_t thr)
+__global__ void __launch_bounds__(256) sha_ring_kernel(const BlockDesc *__restrict__ blocks,
+                                                       const uint32_t *__restrict__ offsets,
+                                                       const BlockState *__restrict__ bst, int cap_blk,
+                                                       uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                                       uint32_t thr)
 {
     if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
         sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr);
         return;
     }
+    __shared__ uint32_t s_slot[4 * 64 * kSlotDw];
     const int b = blockIdx.y - 1;
     const int n = bst[b].n_chunks;
     const BlockDesc &bd = blocks[b];
     const uint8_t *base = bd.data;
-    const uint64_t readable = bd.readable;
+    const int64_t readable = (int64_t)bd.readable;
+    const int64_t bmis = (int64_t)((uintptr_t)base & 127u);     // block start's offset in its line
     const uint32_t *off = offsets + (size_t)b * cap_blk;
     uint32_t *db = digests + (size_t)b * cap_blk * HW;
     const int l = lane_id();
+    lds_w *slot = (lds_w *)&s_slot[(wave_id() * 64 + l) * kSlotDw];
     int kbP, cntP, kbQ, cntQ;
     uint32_t SP, EP, SQ, EQ;
     auto reserve = [&](int &kb, int &cnt, uint32_t &S, uint32_t &E) {
@@ -387,80 +412,94 @@ __global__ void __launch_bounds__(256) sha_pf_kernel(const BlockDesc *__restrict
     reserve(kbP, cntP, SP, EP);
     reserve(kbQ, cntQ, SQ, EQ);
     int head = 0;
-    bool act = false, has_n = false;
-    int k = 0, k2 = 0;
-    uint32_t s0 = 0, len = 0, T = 0, nb = 0, bi = 0, s2 = 0, len2 = 0;
+    bool active = false, fresh = false;
+    int k = 0;
+    uint32_t len = 0, T = 0, nb = 0;
+    int b0 = 0;                                   // block index of the window's first slot (-1: skipped)
+    int64_t wb = 0;                               // window start, block offset (b0 * 64 from the chunk)
     uint32_t st[8];
     set_iv<HW>(st);
-    // lanes with `want` and no next chunk get one from the pool (long chunks are skipped: the long
-    // lanes hash them)
-    auto take = [&](bool want) {
-        for (;;) {
-            const unsigned long long req = ballot64(want && !has_n);
-            if (!req) break;
-            if (head >= cntP) {                   // pool P exhausted: rotate in Q, fetch the next
+    uint32_t N0[32];                              // a fresh chunk's first line
+    for (;;) {
+        if (active && b0 >= (int)nb) {            // chain done: the digest
+            store_digest<HW>(db + (size_t)k * HW, st);
+            active = false;
+        }
+        for (;;) {                                 // offer chunks to idle lanes
+            const unsigned long long idle = ballot64(!active);
+            if (!idle) break;
+            if (head >= cntP) {
                 if (cntQ == 0) break;
                 kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
                 reserve(kbQ, cntQ, SQ, EQ);
             }
-            const bool mine = want && !has_n;
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(req >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)req, 0));
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
             const int avail = cntP - head;
             const int idx = min(head + rank, 63);
             const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
             bool skip = false;
-            if (ballot64(mine && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
-            if (mine && rank < avail) {
-                if (e - c0 >= thr) {
-                    skip = true;
-                } else {
-                    k2 = kbP + head + rank;
-                    s2 = c0;
-                    len2 = e - c0;
-                    has_n = true;
-                }
+            if (ballot64(!active && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
+            if (!active && rank < avail && e - c0 >= thr) {
+                skip = true;
+            } else if (!active && rank < avail) {
+                k = kbP + head + rank;
+                len = e - c0;
+                T = len >> 6;
+                nb = (len + 8) / 64 + 1;
+                const bool teven = (T & 1u) == 0;
+                b0 = teven ? -1 : 0;
+                wb = (int64_t)c0 - (teven ? 64 : 0);
+                set_iv<HW>(st);
+                active = true;
+                fresh = true;
+                load_line(base, readable, ((bmis + wb) & ~(int64_t)127) - bmis, N0);
             }
-            const int nreq = __popcll(req);
-            head += min(nreq, avail);
-            if (!ballot64(skip) && nreq <= avail) break;
+            const int nidle = __popcll(idle);
+            head += min(nidle, avail);
+            if (!ballot64(skip) && nidle <= avail) break;
         }
-    };
-    auto promote = [&]() {
-        k = k2; s0 = s2; len = len2;
-        T = len >> 6;
-        nb = (len + 8) / 64 + 1;
-        bi = 0;
-        set_iv<HW>(st);
-        has_n = false;
-    };
-    // one iteration on window dc (blocks bi, bi + 1 of the current chunk), prefetching into dn
-    auto step = [&](uint32_t (&dc)[33], uint32_t (&dn)[33]) -> bool {
-        take(!act);                                // idle lanes (start, or after a pool gap)
-        if (!act && has_n) {
-            promote();
-            act = true;
-            load_win(base, readable, s0, true, dc);   // not prefetched: waits this iteration
-        }
-        if (!ballot64(act)) return false;
-        const bool two = act && pair_at(bi, T);
-        const uint32_t bin = bi + (two ? 2u : 1u);
-        take(act && bin >= nb);                    // finishing now: the next chunk, to prefetch it
-        if (act && (bin < nb || has_n)) load_win(base, readable, bin < nb ? s0 + 64u * bin : s2, true, dn);
-        if (act) {
-            sha_compute<HW>(dc, s0 + 64u * bi, len, T, nb, bi, two, st);
-            bi = bin;
-            if (bi >= nb) {                        // chain done: the digest
-                store_digest<HW>(db + (size_t)k * HW, st);
-                if (has_n) promote();
-                else act = false;
+        if (!ballot64(active)) break;
+        const bool data = active && b0 <= (int)T;  // not the length-only block alone
+        const int64_t lo = ((bmis + wb) & ~(int64_t)127) - bmis;   // line L, block offset
+        const uint32_t q0 = (uint32_t)((bmis + wb) & 124);          // window's first dword in L (x4)
+        uint32_t R[32], d[33];
+        if (data) load_line(base, readable, lo + 128, R);
+        if (ballot64(fresh)) {
+            if (fresh) {
+#pragma unroll
+                for (int i = 0; i < 32; i++) slot[i] = N0[i];
             }
+            fresh = false;
         }
-        return true;
-    };
-    uint32_t da[33], dd[33];
-    for (;;) {
-        if (!step(da, dd)) break;
-        if (!step(dd, da)) break;
+        if (data) {
+#pragma unroll
+            for (int j = 0; j < 33; j++) d[j] = slot[((q0 >> 2) + j) & 31];
+#pragma unroll
+            for (int i = 0; i < 32; i++) slot[i] = R[i];
+#pragma unroll
+            for (int j = 0; j < 33; j++)
+                if ((q0 >> 2) + j >= 32) d[j] = slot[((q0 >> 2) + j) & 31];
+        }
+        if (active) {
+            const uint32_t sel = 0x00010203u + (uint32_t)(wb & 3) * 0x01010101u;
+            uint32_t m[16];
+            if (b0 >= 0) {                        // slot 0 (the length-only block pads)
+#pragma unroll
+                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+                if (ballot64(b0 > (int)T)) pad_block(m, len, (uint32_t)b0, nb);
+                if (HW == 5) sha1_compress(st, m);
+                else sha256_compress(st, m);
+            }
+            if (b0 + 1 < (int)nb) {               // slot 1 (T pads)
+#pragma unroll
+                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 17], d[i + 16], sel);
+                if (ballot64(b0 + 1 == (int)T)) pad_block(m, len, (uint32_t)(b0 + 1), nb);
+                if (HW == 5) sha1_compress(st, m);
+                else sha256_compress(st, m);
+            }
+            b0 += 2;
+            wb += 128;
+        }
     }
 }
 
@@ -483,22 +522,22 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     // 919 at 4) — fewer concurrent per-lane streams thrash L2 less and leave CUs to the
     // co-running place / granule passes; env knobs for
     // experiments: HDRF_SHA_WAVES (waves per SIMD over 1024 SIMDs), HDRF_SHA_LDS (bytes per WG)
-    // HDRF_SHA_PF: 1 = sha_pf (one wave per SIMD, windows prefetched), 0 = sha_chunk (two waves per SIMD)
-    static const bool pf = [] { const char *e = getenv("HDRF_SHA_PF"); return e ? atoi(e) != 0 : false; }();
+    // HDRF_SHA_RING: 1 = sha_ring (each line fetched once, LDS line slots), 0 = sha_chunk
+    static const bool ring = [] { const char *e = getenv("HDRF_SHA_RING"); return e ? atoi(e) != 0 : false; }();
     // HDRF_SHA_WPC: waves per CU over the chip's 256 CUs (overrides HDRF_SHA_WAVES x 4)
     static const int per_cu = [] {
         const char *c = getenv("HDRF_SHA_WPC");
         if (c) return atoi(c);
         const char *e = getenv("HDRF_SHA_WAVES");
-        return 4 * (e ? atoi(e) : (pf ? 1 : 2));
+        return 4 * (e ? atoi(e) : 2);
     }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
-    if (pf && hasher == 0)
-        hipLaunchKernelGGL(sha_pf_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
-    else if (pf)
-        hipLaunchKernelGGL(sha_pf_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    if (ring && hasher == 0)
+        hipLaunchKernelGGL(sha_ring_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    else if (ring)
+        hipLaunchKernelGGL(sha_ring_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
     else if (hasher == 0)
         hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
     else
