@@ -641,15 +641,24 @@ struct GmRing {
     }
     __device__ __forceinline__ void prefetch(const uint8_t *gmb)
     {
-        if (pfg != rb + 2 * kRingU && w0 >= rb + kRingU / 2) {
+        if (on && pfg != rb + 2 * kRingU && w0 >= rb + kRingU / 2) {
             pfg = rb + 2 * kRingU;
 #pragma unroll
             for (int i = 0; i < kGmWin / 4; i++) pf[i] = ld16(gmb + pfg + 16 * i);
         }
     }
+    bool on = true;                      // false: HDRF_WALK_RING=0, the maxima straight from memory (A/B)
     __device__ __forceinline__ void get(uint32_t (&d)[kGmWin], const uint8_t *gmb, int W0)
     {
         w0 = W0;
+        if (!on) {
+#pragma unroll
+            for (int i = 0; i < kGmWin / 4; i++) {
+                const uint4 v = ld16(gmb + W0 + 16 * i);
+                d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+            }
+            return;
+        }
         if (W0 < rb || W0 > rb + kRingU) {
             if (W0 <= rb + 2 * kRingU) {                          // the window moved on by one unit
                 if (pfg == rb + 2 * kRingU) put(pfg, pf);
@@ -673,7 +682,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
                                                         uint32_t *__restrict__ spec, int cap,
                                                         SegMeta *__restrict__ meta, int *__restrict__ rq,
                                                         int *__restrict__ rq_count, int rq_cap,
-                                                        uint32_t *__restrict__ irr, int *__restrict__ err)
+                                                        uint32_t *__restrict__ irr, int *__restrict__ err, int ring_on)
 {
     __shared__ uint16_t s_cuts[4][64 * kLdsCuts];
     __shared__ uint8_t s_cnt[4][64];
@@ -708,6 +717,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
     uint32_t d[kGmWin];
     GmRing ring;
     ring.r = (lds_u32 *)&s_ring[wave_id()][l * kRingPitch];
+    ring.on = ring_on != 0;
     uint4 rh = make_uint4(0, 0, 0, 0);                    // raw bytes of the last hit granule gh
     int gh = -1;
     for (;;) {
@@ -1207,8 +1217,9 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     // HDRF_WALK_LDS: dynamic LDS per walk workgroup (occupancy throttle: fewer lanes in flight keep
     // their granule-maximum lines in L2 between chunk steps)
     static const int walk_lds = [] { const char *v = getenv("HDRF_WALK_LDS"); return v ? atoi(v) : 0; }();
+    static const int ring_on = [] { const char *v = getenv("HDRF_WALK_RING"); return v ? atoi(v) : 1; }();
     hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
-                       X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err);
+                       X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, ring_on);
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
