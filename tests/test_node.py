@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     (2, 0, [[2, 3], [3, 1], [1, 1]]),
     (3, 1, [[2, 2, 2], [1, 3, 2]]),
     (4, 0, [[1, 2, 1, 2], [2, 1, 1, 1]]),
+    (8, 0, [[1, 2, 1, 1, 2, 1, 1, 1], [2, 1, 1, 2, 1, 1, 2, 1]]),    # the node's rank count
 ])
 def test_node_loopback_matches_single_sequence(G, hasher, sched):
     import torch  # noqa: F401
@@ -100,7 +101,7 @@ def test_node_loopback_matches_single_sequence(G, hasher, sched):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G,hasher", [(2, 1), (3, 0)])
+@pytest.mark.parametrize("G,hasher", [(2, 1), (3, 0), (8, 1)])
 def test_node_loopback_pipelined_matches_single_sequence(G, hasher):
     """The pipelined phase order (hdrf_gx_front_launch of batch j+1 before batch j's exchanges,
     two slots, front on stream A, back phases on stream B) gives the same bytes as the oracle."""
@@ -109,7 +110,7 @@ def test_node_loopback_pipelined_matches_single_sequence(G, hasher):
     from oracle.oracle import Oracle
 
     cmax = 1 << 20
-    sched = [[2, 1, 2][:G], [1, 2, 1][:G], [2, 2, 1][:G], [1, 1, 2][:G]]
+    sched = [([2, 1, 2] * 3)[:G], ([1, 2, 1] * 3)[:G], ([2, 2, 1] * 3)[:G], ([1, 1, 2] * 3)[:G]]
     seq = _plan(sched)
     blocks = _mixed_blocks(41 + G, len(seq), 600_000)
     ctxs = open_ranks(G, hasher=hasher, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=4,
