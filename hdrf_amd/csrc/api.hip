@@ -485,7 +485,6 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     // 1 = dedup, 2 = dedup + Lz4Codec containers (single-node contexts; the node-global mode
     // assembles containers from several GPUs and compresses them in a later step: unsupported yet)
     if (c.compressor != 1 && c.compressor != 2) return HDRF_E_UNSUPPORTED;
-    if (c.compressor == 2 && c.n_ranks > 1) return HDRF_E_UNSUPPORTED;
     hdrf_ctx *ctx = new (std::nothrow) hdrf_ctx();
     if (!ctx) return HDRF_E_NOMEM;
     ctx->cfg = c;
@@ -912,7 +911,8 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
     S.close_bound = 0;
     for (uint32_t i = 0; i < nclosed; i++) {
         const ClosedRec &r = S.h_closed[i];
-        const uint32_t flen = c.compressor == 2 ? S.h_filelen[i] : r.len;
+        // (node-global contexts compress after the head pieces are gathered: hdrf_gx_compress)
+        const uint32_t flen = c.compressor == 2 && ctx->G == 1 ? S.h_filelen[i] : r.len;
         note_container(ctx, r.id, r.slot, r.len, 1, flen);
         if (c.retain_containers) {
             ctx->pend_closed.push_back(r.id);
@@ -2118,6 +2118,64 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
     ctx->gx_bphase = 4;
     return 0;
+}
+
+// ---- node-global compressor 2 (DN/DataDeduplicator.java:748-797: a closing container is rewritten
+// as one Lz4Codec file).  A node-global container's bytes lie on the ranks that placed into it (rank
+// r continues the container rank r - 1 left open, in the same arena slot index), so the rank whose
+// flush walk closes a container first gathers the head pieces the earlier ranks hold
+// (hdrf_gx_piece, planned on the host from every rank's hdrf_gx_alloc_io), then compresses the
+// containers it closed (hdrf_gx_compress), all between hdrf_gx_place and hdrf_gx_commit.
+extern "C" int hdrf_gx_alloc_io(hdrf_ctx *ctx, uint8_t *alloc_in, uint8_t *alloc_out)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || ctx->G < 2 || !alloc_in || !alloc_out) return ctx ? set_err(ctx, HDRF_E_INVAL, "bad arguments") : HDRF_E_INVAL;
+    if (ctx->gx_bphase != 3 && ctx->gx_bphase != 4) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_alloc_io after hdrf_gx_flush");
+    std::memset(alloc_in, 0, HDRF_ALLOC_STATE_BYTES);
+    std::memcpy(alloc_in, &ctx->gx_ain, sizeof(AllocState));
+    std::memset(alloc_out, 0, HDRF_ALLOC_STATE_BYTES);
+    std::memcpy(alloc_out, &ctx->gx_aout, sizeof(AllocState));
+    return 0;
+}
+
+extern "C" int hdrf_gx_piece(hdrf_ctx *ctx, uint32_t id, uint64_t off, uint64_t n, void *dev, int32_t write)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || ctx->G < 2 || (n && !dev)) return ctx ? set_err(ctx, HDRF_E_INVAL, "bad arguments") : HDRF_E_INVAL;
+    auto it = ctx->containers.find(id);
+    if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_NOTFOUND, "container not resident on this rank");
+    if (off > ctx->cfg.container_max || n > ctx->cfg.container_max - off) return set_err(ctx, HDRF_E_INVAL, "piece outside the container");
+    uint8_t *p = ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max + off;
+    if (n) {
+        HIPCK(hipMemcpyAsync(write ? (void *)p : dev, write ? (const void *)dev : (const void *)p, n, hipMemcpyDeviceToDevice,
+                             ctx->stB));
+        HIPCK(hipStreamSynchronize(ctx->stB));
+    }
+    return 0;
+}
+
+extern "C" int hdrf_gx_compress(hdrf_ctx *ctx)
+{
+    HDRF_LOCK(ctx);
+    if (int rc = gx_check(ctx, 4)) return rc;
+    const hdrf_cfg &c = ctx->cfg;
+    if (c.compressor != 2) return 0;
+    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    const uint32_t nclosed = *S.h_nclosed;
+    if (!nclosed) return 0;
+    hipStream_t st = ctx->stB;
+    HIPCK(launch_lz4(S.d_closed, S.d_nclosed, ctx->closed_cap, c.container_max, ctx->d_arena, ctx->d_carena, ctx->cslot,
+                     S.d_segclen, S.d_filelen, S.d_lzwork, st));
+    HIPCK(hipMemcpyAsync(S.h_filelen, S.d_filelen, sizeof(uint32_t) * nclosed, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < nclosed; i++) {
+        const ClosedRec &r = S.h_closed[i];
+        auto it = ctx->containers.find(r.id);
+        if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_DEVICE, "closed container missing");
+        it->second.clen = S.h_filelen[i];
+        ctx->stats.closed_file_bytes += (int64_t)S.h_filelen[i] - (int64_t)r.len;
+    }
+    return (int)nclosed;
 }
 
 extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts)

@@ -26,7 +26,7 @@ EXPORTS = [
     "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_front_launch", "hdrf_gx_front_wait", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
-    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
+    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_gx_alloc_io", "hdrf_gx_piece", "hdrf_gx_compress", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
     "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_stream_block_host", "hdrf_lz4_file_decode",
     "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
@@ -197,6 +197,9 @@ def load():
         "hdrf_gx_flush": (ctypes.c_int, [_vp, _u8p, _u8p]),
         "hdrf_gx_place": (ctypes.c_int, [_vp, _u8p, _vp, _i64p]),
         "hdrf_gx_commit": (ctypes.c_int, [_vp, _vp, _i64p]),
+        "hdrf_gx_alloc_io": (ctypes.c_int, [_vp, _u8p, _u8p]),
+        "hdrf_gx_piece": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_int32]),
+        "hdrf_gx_compress": (ctypes.c_int, [_vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -689,6 +692,19 @@ class Context:
         loc = np.ascontiguousarray(loc, np.uint32)
         return self._ck(self.L.hdrf_gx_read_fill(self._h, loc.ctypes.data if loc.size else None, loc.shape[0],
                                                  dev_out, cap))
+
+    def gx_alloc_io(self):
+        """This rank's allocator state before and after its flush walk (128 B each)."""
+        a = np.zeros(ALLOC_STATE_BYTES, np.uint8)
+        b = np.zeros(ALLOC_STATE_BYTES, np.uint8)
+        self._ck(self.L.hdrf_gx_alloc_io(self._h, _p(a), _p(b)))
+        return a, b
+
+    def gx_piece(self, cid, off, n, dev_ptr, write):
+        self._ck(self.L.hdrf_gx_piece(self._h, cid, off, n, dev_ptr, 1 if write else 0))
+
+    def gx_compress(self):
+        return self._ck(self.L.hdrf_gx_compress(self._h))
 
     def gx_commit(self, x3_recv, recv_counts):
         rc = np.ascontiguousarray(recv_counts, np.int64)

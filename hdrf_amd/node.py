@@ -100,6 +100,51 @@ class Exchange:
         return fin.cpu().numpy()
 
 
+def alloc_fields(a):
+    """AllocState (hdrf_amd/csrc/common.hpp) from its 128-B image: id, cur, pos, slot, exists per range."""
+    w = np.frombuffer(np.ascontiguousarray(a, np.uint8).tobytes()[:88], np.uint32)
+    return {"id": w[0:4], "cur": w[4:8], "slot": w[12:16], "exists": w[18:22]}
+
+
+class ContainerPieces:
+    """Which rank holds which bytes of each storer range's open node-global container
+    (DN/DataDeduplicator.java:723-818 over the global block order): rank r continues the container
+    rank r - 1 left open, so a container closed by rank s may hold head pieces written by earlier
+    ranks (or batches).  Every rank runs the same plan from the all-gathered allocator states, so
+    they agree on the transfers without further exchange."""
+
+    def __init__(self, n_thread=3):
+        self.n_thread = n_thread
+        self.open = {}                       # range t -> (cid, [(rank, start, end), ...])
+
+    def batch(self, ains, aouts):
+        """ains / aouts[r]: rank r's allocator state before / after its flush walk (rank order).
+        Returns the transfers (src rank, dst rank, cid, start, end) the closers need."""
+        xfer = []
+        for t in range(self.n_thread):
+            for s, (ai, ao) in enumerate(zip(ains, aouts)):
+                fi, fo = alloc_fields(ai), alloc_fields(ao)
+                if (fi["id"][t], fi["cur"][t], fi["exists"][t]) == (fo["id"][t], fo["cur"][t], fo["exists"][t]):
+                    continue                 # rank s placed nothing in range t
+                c0 = int(fi["id"][t])
+                x0 = int(fi["cur"][t]) if fi["exists"][t] else 0
+                c1, x1 = int(fo["id"][t]), int(fo["cur"][t])
+                cid, pieces = self.open.get(t, (c0, []))
+                if cid != c0:
+                    pieces = []
+                if c1 == c0:
+                    self.open[t] = (c0, pieces + [(s, x0, x1)])
+                    continue
+                for q, a, b in pieces:       # c0 closes on rank s: the heads the others hold
+                    if q != s and b > a:
+                        xfer.append((q, s, c0, a, b))
+                self.open[t] = (c1, [(s, 0, x1)])
+        return xfer
+
+    def reset(self):
+        self.open = {}
+
+
 class NodeRank:
     """One GPU's share of a node-global reduction (ctx must be opened with n_ranks = G > 1)."""
 
@@ -120,12 +165,45 @@ class NodeRank:
         self.x2s, self.x2r = mk(self.w[1]), mk(self.w[1])
         self.x3s, self.x3r = mk(self.w[2]), mk(self.w[2])
         self.alloc = None          # node allocator after the last batch (None: initial state)
+        self.pieces = ContainerPieces(int(ctx.cfg.n_thread))   # compressor 2: head-piece plan
         self.phase_ms = {}         # host wall time per back phase, summed over batches
         self.chain = os.environ.get("HDRF_NODE_CHAIN") == "1"   # A/B: the old rank-to-rank chain
 
     def reset(self):
         self.ctx.reset()
         self.alloc = None
+        self.pieces.reset()
+
+    def _compress(self):
+        """Compressor 2: gather the head pieces of the containers this rank closes (the plan every
+        rank derives from the all-gathered allocator states), then compress them."""
+        ctx, r = self.ctx, self.rank
+        ai, ao = ctx.gx_alloc_io()
+        both = self.xc.all_gather_i64(np.concatenate([ai, ao]).astype(np.int64))
+        ains = [b[:len(ai)].astype(np.uint8) for b in both]
+        aouts = [b[len(ai):].astype(np.uint8) for b in both]
+        xfer = self.pieces.batch(ains, aouts)
+        ops, bufs = [], []
+        dev = self.device if self.xc.nccl else torch.device("cpu")
+        for q, s, cid, a, b in xfer:
+            if r not in (q, s):
+                continue
+            buf = torch.empty(b - a, dtype=torch.uint8, device=self.device)
+            if r == q:
+                ctx.gx_piece(cid, a, b - a, buf.data_ptr(), write=False)
+                ops.append(dist.P2POp(dist.isend, buf.to(dev), s))
+            else:
+                rb = torch.empty(b - a, dtype=torch.uint8, device=dev)
+                ops.append(dist.P2POp(dist.irecv, rb, q))
+                bufs.append((cid, a, b, rb))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for cid, a, b, rb in bufs:
+            t = rb.to(self.device)
+            torch.cuda.synchronize(self.device)
+            ctx.gx_piece(cid, a, b - a, t.data_ptr(), write=True)
+        return ctx.gx_compress()
 
     def reduce_batch(self, dev_ptrs, lens, readable, block_ids, gbase):
         """Reduce this rank's blocks of one global batch; gbase = its first batch position."""
@@ -160,6 +238,8 @@ class NodeRank:
             ctx.gx_flush(a_in, want_out=False)
         t4 = time.perf_counter()
         c3 = ctx.gx_place(self.alloc, self.x3s.data_ptr())
+        if int(ctx.cfg.compressor) == 2:
+            self._compress()
         t5 = time.perf_counter()
         r3 = xc.counts(c3)
         xc.records(self.x3s, self.x3r, c3, r3, cap, w3)

@@ -387,6 +387,16 @@ int hdrf_gx_alloc_scan(hdrf_ctx *ctx, const int64_t *descs, const int64_t *lens,
 int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out);
 /* alloc_final: the node's state after the last rank's flush (becomes this context's state). */
 int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts);
+/* Node-global compressor 2 (between hdrf_gx_place and hdrf_gx_commit): every rank's allocator
+ * state before and after its flush walk (hdrf_gx_alloc_io, 128 B each; all-gathered by the caller,
+ * they tell every rank which rank holds which bytes of each container); the head pieces of a
+ * container another rank closes are copied out of / into arena slots (hdrf_gx_piece: write = 0 reads
+ * the bytes [off, off + n) of container id into dev, 1 writes them); then each rank compresses the
+ * containers its flush walk closed (hdrf_gx_compress: the Lz4Codec files of DN/DataDeduplicator.java
+ * :748-797, returns how many).  hdrf_amd/node.py plans and runs the transfers. */
+int hdrf_gx_alloc_io(hdrf_ctx *ctx, uint8_t *alloc_in, uint8_t *alloc_out);
+int hdrf_gx_piece(hdrf_ctx *ctx, uint32_t id, uint64_t off, uint64_t n, void *dev, int32_t write);
+int hdrf_gx_compress(hdrf_ctx *ctx);
 int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts);
 
 #ifdef __cplusplus

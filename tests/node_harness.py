@@ -30,6 +30,24 @@ class Loopback:
         self.x2s, self.x2r = mk(self.w[1]), mk(self.w[1])
         self.x3s, self.x3r = mk(self.w[2]), mk(self.w[2])
         self.alloc = None
+        from hdrf_amd.node import ContainerPieces
+        self.pieces = ContainerPieces(int(ctxs[0].cfg.n_thread))
+        self.dev = dev
+
+    def _compress(self):
+        """Compressor 2 (NodeRank._compress in one process): the closers gather the head pieces,
+        then every rank compresses what it closed."""
+        if int(self.ctxs[0].cfg.compressor) != 2:
+            return
+        io = [c.gx_alloc_io() for c in self.ctxs]
+        for q, s, cid, a, b in self.pieces.batch([x[0] for x in io], [x[1] for x in io]):
+            buf = torch.empty(b - a, dtype=torch.uint8, device=self.dev)
+            torch.cuda.synchronize()
+            self.ctxs[q].gx_piece(cid, a, b - a, buf.data_ptr(), write=False)
+            self.ctxs[s].gx_piece(cid, a, b - a, buf.data_ptr(), write=True)
+            self.moved = getattr(self, "moved", 0) + (b - a)
+        for c in self.ctxs:
+            c.gx_compress()
 
     def _a2a(self, send, recv, counts, w):
         """counts[s][d] records from rank s to rank d; returns recv counts [d][s]."""
@@ -58,6 +76,7 @@ class Loopback:
             a = ctxs[r].gx_flush(a)
         self.alloc = a
         c3 = [ctxs[r].gx_place(a, self.x3s[r].data_ptr()) for r in range(G)]
+        self._compress()
         r3 = self._a2a(self.x3s, self.x3r, c3, self.w[2])
         for d in range(G):
             ctxs[d].gx_commit(self.x3r[d].data_ptr(), r3[d])
@@ -98,6 +117,7 @@ class Loopback:
                 ctxs[r].gx_flush(a_in, want_out=(r % 2 == 0))   # both the checked and the async form
             a = self.alloc = fin
             c3 = [ctxs[r].gx_place(a, self.x3s[r].data_ptr()) for r in range(G)]
+            self._compress()
             r3 = self._a2a(self.x3s, self.x3r, c3, self.w[2])
             for d in range(G):
                 ctxs[d].gx_commit(self.x3r[d].data_ptr(), r3[d])

@@ -158,6 +158,77 @@ def test_node_loopback_pipelined_matches_single_sequence(G, hasher):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("G,pipelined", [(3, False), (8, True)])
+def test_node_loopback_compressor2_matches_single_sequence(G, pipelined):
+    """The reference's default mode (compressor 2, DN/DataNode.java:438) on a node-global index:
+    a container closed by rank s whose head earlier ranks wrote is gathered on s and rewritten as
+    one Lz4Codec file (DN/DataDeduplicator.java:748-797).  Every closed container's file equals the
+    oracle's, byte for byte, on the rank that closed it; blocks, index and allocator as before."""
+    import torch  # noqa: F401
+    from node_harness import Loopback, merged_index, open_ranks
+    from oracle.oracle import Oracle
+
+    cmax = 1 << 20
+    sched = [([2, 1, 2] * 3)[:G], ([1, 2, 1] * 3)[:G], ([2, 2, 1] * 3)[:G]]
+    seq = _plan(sched)
+    blocks = _mixed_blocks(61 + G, len(seq), 700_000)
+    ctxs = open_ranks(G, hasher=0, compressor=2, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=4,
+                      index_log2=20, arena_slots=256)
+    lb = Loopback(ctxs)
+    ora = Oracle(hasher=0, compressor=2, max_size=cmax)
+    devs, per_batch, where = [], [], []
+    g = 0
+    for per in sched:
+        pr, wj = [], []
+        for r, n in enumerate(per):
+            ptrs, lens, rd, ids = [], [], [], []
+            for i in range(n):
+                blk = blocks[g]
+                p = ctxs[r].dev_alloc(len(blk) + 4096)
+                ctxs[r].h2d(p, blk)
+                devs.append((ctxs[r], p))
+                ptrs.append(p); lens.append(len(blk)); rd.append(len(blk) + 4096); ids.append(0x900 + g)
+                wj.append((r, i, g))
+                g += 1
+            pr.append((ptrs, lens, rd, ids))
+        per_batch.append(pr)
+        where.append(wj)
+
+    def done(j):
+        for r, i, gi in where[j]:
+            compare_block(ctxs[r].batch_result(i), ora.reduce(blocks[gi], 0x900 + gi),
+                          tag=f"c2 G={G} batch {j} rank {r} block {i}")
+    if pipelined:
+        lb.batches_pipelined(per_batch, done)
+    else:
+        for j, pr in enumerate(per_batch):
+            lb.batch(pr)
+            done(j)
+    gk, gv = merged_index(ctxs)
+    ok, ov = ora.index_dump()
+    assert np.array_equal(gk, ok) and np.array_equal(gv, ov), "node index differs"
+    alloc = ora.allocator()
+    n_closed = 0
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, oc = ora.container(cid)
+            if od is None or not oc:
+                continue
+            files = [f for f, closed in (c.container(cid) for c in ctxs) if closed]
+            assert len(files) == 1, f"container {cid:#x} closed on {len(files)} ranks"
+            assert files[0] == od, f"container {cid:#x}: Lz4Codec file differs ({len(files[0])} vs {len(od)} B)"
+            n_closed += 1
+    assert n_closed >= 6 and getattr(lb, "moved", 0) > 0, "no head piece was gathered"
+    st = [c.stats() for c in ctxs]
+    assert sum(x["closed_containers"] for x in st) == n_closed
+    for c, p in devs:
+        c.dev_free(p)
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.gpu
 def test_node_context_rejects_single_node_calls():
     from hdrf_amd.lib import Context, HdrfError
     ctx = Context(n_ranks=2, rank=1, max_block_bytes=1 << 20, max_batch_blocks=2, index_log2=16, arena_slots=16,
