@@ -8,8 +8,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCHED = [[2, 2], [1, 2], [2, 1]]
-CMAX = 1 << 20
-SIZE = 600_000
+COMPRESSOR = int(os.environ.get("HDRF_NW_COMPRESSOR", "1"))   # 2: node-global Lz4Codec containers
+CMAX = (1 << 20) if COMPRESSOR == 1 else (512 << 10)
+SIZE = 600_000 if COMPRESSOR == 1 else 900_000
 
 
 def blocks():
@@ -26,7 +27,7 @@ def main(out):
     r, G = dist.get_rank(), dist.get_world_size()
     seq, blks = blocks()
     ctx = Context(device=0, n_ranks=G, rank=r, container_max=CMAX, max_block_bytes=2 << 20, max_batch_blocks=4,
-                  index_log2=20, arena_slots=128)
+                  index_log2=20, arena_slots=128, compressor=COMPRESSOR)
     node = NodeRank(ctx)
     res = {}
     batches, mines, allp = [], [], []
@@ -62,6 +63,13 @@ def main(out):
     k, v = ctx.index_dump()
     res["index_keys"], res["index_vals"] = k, v
     res["alloc"] = np.frombuffer(ctx.allocator(), np.uint8)
+    alloc = ctx.allocator()
+    for t in range(3):                 # the containers this rank closed (compressor 2: Lz4Codec files)
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            f, closed = ctx.container(cid)
+            if f is not None and closed:
+                res[f"closed_{cid}"] = np.frombuffer(f, np.uint8)
     np.savez(os.path.join(out, f"rank{r}.npz"), **res)
     ctx.close()
     dist.destroy_process_group()
@@ -72,7 +80,7 @@ def check_outputs(out, G):
     from oracle.oracle import Oracle
     seq, blks = blocks()
     ranks = [np.load(os.path.join(out, f"rank{r}.npz")) for r in range(G)]
-    ora = Oracle(hasher=0, compressor=1, max_size=CMAX)
+    ora = Oracle(hasher=0, compressor=COMPRESSOR, max_size=CMAX)
     for gi, (_, r, _) in enumerate(seq):
         o = ora.reduce(blks[gi], 0x900 + gi)
         z = ranks[r]
@@ -98,6 +106,18 @@ def check_outputs(out, G):
     assert np.array_equal(k[order], ok) and np.array_equal(v[order], ov), "node index differs"
     for z in ranks:
         assert z["alloc"].tobytes() == ora.allocator()
+    alloc = ora.allocator()
+    n_closed = 0
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, oc = ora.container(cid)
+            if od is None or not oc:
+                continue
+            files = [z[f"closed_{cid}"] for z in ranks if f"closed_{cid}" in z.files]
+            assert len(files) == 1 and files[0].tobytes() == od, f"closed container {cid:#x}"
+            n_closed += 1
+    return n_closed
 
 
 if __name__ == "__main__":

@@ -254,6 +254,56 @@ def test_node_two_processes_gloo(tmp_path):
     check_outputs(out, 2)
 
 
+@pytest.mark.gpu
+def test_node_two_processes_gloo_compressor2(tmp_path):
+    """Two real ranks over gloo with compressor 2: the head pieces cross processes (batched
+    isend/irecv in NodeRank._compress) and every closed container's Lz4Codec file is the oracle's."""
+    out = str(tmp_path)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", "29633", os.path.join(ROOT, "tests", "node_worker.py"), out]
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.path.join(ROOT, "tests"), HDRF_NW_COMPRESSOR="2")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    os.environ["HDRF_NW_COMPRESSOR"] = "2"
+    try:
+        import importlib
+        import node_worker
+        importlib.reload(node_worker)
+        assert node_worker.check_outputs(out, 2) >= 4
+    finally:
+        del os.environ["HDRF_NW_COMPRESSOR"]
+        importlib.reload(node_worker)
+
+
+def test_container_pieces_plan_cpu():
+    """hdrf_amd.node.ContainerPieces: the head pieces a closer needs, from allocator states only
+    (three ranks; range 0's container 0 spans ranks 0-2 and closes on rank 2; range 1's closes on
+    the rank that opened it; range 2 idle)."""
+    from hdrf_amd.node import ContainerPieces
+
+    def st(ids, curs, exists):
+        w = np.zeros(32, np.uint32)
+        w[0:3], w[4:7], w[18:21] = ids, curs, exists
+        return w.view(np.uint8)
+
+    t1, t2 = 1 << 22, 2 << 22
+    ains = [st([0, t1, t2], [0, 0, 0], [0, 0, 0]), st([0, t1 + 1, t2], [100, 5, 0], [1, 1, 0]),
+            st([0, t1 + 1, t2], [250, 9, 0], [1, 1, 0])]
+    aouts = [st([0, t1 + 1, t2], [100, 5, 0], [1, 1, 0]), st([0, t1 + 1, t2], [250, 9, 0], [1, 1, 0]),
+             st([1, t1 + 1, t2], [40, 9, 0], [1, 1, 0])]
+    cp = ContainerPieces(3)
+    x = cp.batch(ains, aouts)
+    assert sorted(x) == [(0, 2, 0, 0, 100), (1, 2, 0, 100, 250)]
+    assert cp.open[0] == (1, [(2, 0, 40)])
+    # range 1: rank 0 closed t1 itself (no transfer), ranks 1 continued t1 + 1
+    assert cp.open[1] == (t1 + 1, [(0, 0, 5), (1, 5, 9)])
+    # next batch: rank 0 closes t1 + 1 -> rank 1's piece [5, 9) moves, rank 0's own [0, 5) stays
+    ains2 = [st([1, t1 + 1, t2], [40, 9, 0], [1, 1, 0])] * 3
+    aouts2 = [st([1, t1 + 2, t2], [40, 3, 0], [1, 1, 0])] + [st([1, t1 + 2, t2], [40, 3, 0], [1, 1, 0])] * 2
+    x2 = cp.batch(ains2, [aouts2[0], ains2[1], ains2[2]])
+    assert x2 == [(1, 0, t1 + 1, 5, 9)]
+
+
 def test_exchange_gloo_cpu_world2():
     """hdrf_amd.node.Exchange on CPU tensors, world_size 2 over gloo: counts, variable regions and
     the allocator hand-off chain."""
