@@ -9,8 +9,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCHED = [[2, 2], [1, 2], [2, 1]]
 COMPRESSOR = int(os.environ.get("HDRF_NW_COMPRESSOR", "1"))   # 2: node-global Lz4Codec containers
-CMAX = (1 << 20) if COMPRESSOR == 1 else (512 << 10)
-SIZE = 600_000 if COMPRESSOR == 1 else 900_000
+CMAX = 1 << 20
+SIZE = 600_000 if COMPRESSOR == 1 else 1_400_000
 
 
 def blocks():

@@ -168,10 +168,10 @@ def test_node_loopback_compressor2_matches_single_sequence(G, pipelined):
     from node_harness import Loopback, merged_index, open_ranks
     from oracle.oracle import Oracle
 
-    cmax = 512 << 10
+    cmax = 1 << 20                                   # the smallest container that holds a maximal chunk
     sched = [([2, 1, 2] * 3)[:G], ([1, 2, 1] * 3)[:G], ([2, 2, 1] * 3)[:G], ([1, 1, 2] * 3)[:G]]
     seq = _plan(sched)
-    blocks = _mixed_blocks(61 + G, len(seq), 900_000)
+    blocks = _mixed_blocks(61 + G, len(seq), 1_400_000)
     ctxs = open_ranks(G, hasher=0, compressor=2, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=4,
                       index_log2=20, arena_slots=256)
     lb = Loopback(ctxs)
