@@ -33,11 +33,12 @@ METRIC = "logical GB/s reduced per node (1/2/4/8 GPUs) at 50% dup, bit-exact ded
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_WI_NS = 1033.0       # v_add_u32 wave-instructions/ns, chip-wide (tools/valu_peak.hip)
 KERNEL_OF = {"gmax(gmax_kernel)": "gmax_kernel", "walk(lane_walk_kernel)": "lane_walk_kernel",
-             "sha_full(sha_full_kernel)": "sha_full_kernel", "place(place_kernel)": "place_kernel"}
+             "sha(sha_chunk_kernel)": "sha_ring_kernel" if os.environ.get("HDRF_SHA_RING", "0") not in ("", "0")
+             else "sha_chunk_kernel", "place(place_kernel)": "place_kernel"}
 # stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index + store,
 # L the LZ4 pass of closed containers (compressor 2; two LZ4 streams alternating by batch)
 CHAINS = {"W: chunking": ["gmax(gmax_kernel)", "walk(lane_walk_kernel)", "stitch(repair/path/count/scan/copy/fallback)"],
-          "A: SHA": ["sha_full(sha_full_kernel)", "sha_tail(sha_tail_kernel)"],
+          "A: SHA": ["sha(sha_chunk_kernel)", "sha_tail(none: padding inside the sha kernel)"],
           "B: index+store": ["index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
                              "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
                              "place(place_kernel)"],
@@ -378,7 +379,7 @@ def main():
     want = {"blocks": nb, "block_mib": a.block_mib, "batch": B, "n_gpus": world, "hasher": a.hasher}
     if any(pmc.get("_config", {}).get(k) != v for k, v in want.items()):
         pmc, pmc_src = {}, None                        # profiled on another workload: not this one's traffic
-    sha_k = "sha_full_kernel" + ("<5>" if a.hasher == 0 else "<7>")
+    sha_k = KERNEL_OF[STAGES[2]] + ("<5>" if a.hasher == 0 else "<7>")
 
     def hbm_entry(name):
         ms = avg[name]

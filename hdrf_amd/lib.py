@@ -42,8 +42,8 @@ PIPELINE_DEPTH = 5          # HDRF_PIPELINE_DEPTH: batches in flight
 
 
 # per-stage timers of hdrf_stage_times (kernel names in parentheses)
-STAGES = ["walk(lane_walk_kernel)", "stitch(repair/path/count/scan/copy/fallback)", "sha_full(sha_full_kernel)",
-          "sha_tail(sha_tail_kernel)", "index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
+STAGES = ["walk(lane_walk_kernel)", "stitch(repair/path/count/scan/copy/fallback)", "sha(sha_chunk_kernel)",
+          "sha_tail(none: padding inside the sha kernel)", "index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
           "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
           "place(place_kernel)", "compress(lz4_seg/lz4_pack)", "gmax(gmax_kernel)"]
 

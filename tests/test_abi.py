@@ -38,8 +38,8 @@ def test_default_config_and_bad_config_are_rejected_without_gpu():
     assert lib.load().hdrf_open(ctypes.byref(bad), ctypes.byref(h)) == -1
     unsupported = lib.default_config(compressor=3)          # stream codecs: not in this build
     assert lib.load().hdrf_open(ctypes.byref(unsupported), ctypes.byref(h)) == -6
-    node_lz4 = lib.default_config(compressor=2, n_ranks=2, rank=0)
-    assert lib.load().hdrf_open(ctypes.byref(node_lz4), ctypes.byref(h)) == -6
+    node_lz4 = lib.default_config(compressor=2, n_ranks=2, rank=0)   # node-global compressor 2: accepted
+    assert lib.load().hdrf_open(ctypes.byref(node_lz4), ctypes.byref(h)) != -6
     bad_rank = lib.default_config(n_ranks=2, rank=2)
     assert lib.load().hdrf_open(ctypes.byref(bad_rank), ctypes.byref(h)) == -1
 
