@@ -1890,15 +1890,17 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
     HIPCK(launch_gx_owner(ctx->cfg.hasher, x1_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap,
                           ctx->G, ctx->d_tab, ctx->cfg.index_log2, S.gx_batch, tag_mask(ctx), ctx->d_oslot,
                           ctx->d_oflags, S.d_coll, S.d_ncoll, ctx->coll_cap, x2_send, S.d_err, st));
-    int herr = 0;
-    HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
-    if (herr) {
-        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
-        HIPCK(hipStreamSynchronize(st));
-        return device_error(ctx, herr);
-    }
+    // no host round trip: a device error (S.d_err) is read back with the batch by hdrf_gx_place, and
+    // the X2 exchange may be enqueued on stream B right behind this kernel (hdrf_gx_stream)
     ctx->gx_bphase = 1;
+    return 0;
+}
+
+extern "C" int hdrf_gx_stream(hdrf_ctx *ctx, void **stream)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx || !stream) return HDRF_E_INVAL;
+    *stream = (void *)ctx->stB;
     return 0;
 }
 

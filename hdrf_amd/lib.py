@@ -26,7 +26,7 @@ EXPORTS = [
     "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_front_launch", "hdrf_gx_front_wait", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
-    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_gx_alloc_io", "hdrf_gx_piece", "hdrf_gx_compress", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
+    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_gx_stream", "hdrf_gx_alloc_io", "hdrf_gx_piece", "hdrf_gx_compress", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
     "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_stream_block_host", "hdrf_lz4_file_decode",
     "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
@@ -197,6 +197,7 @@ def load():
         "hdrf_gx_flush": (ctypes.c_int, [_vp, _u8p, _u8p]),
         "hdrf_gx_place": (ctypes.c_int, [_vp, _u8p, _vp, _i64p]),
         "hdrf_gx_commit": (ctypes.c_int, [_vp, _vp, _i64p]),
+        "hdrf_gx_stream": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p)]),
         "hdrf_gx_alloc_io": (ctypes.c_int, [_vp, _u8p, _u8p]),
         "hdrf_gx_piece": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_int32]),
         "hdrf_gx_compress": (ctypes.c_int, [_vp]),
@@ -642,6 +643,12 @@ class Context:
     def gx_owner(self, x1_recv, recv_counts, x2_send):
         rc = np.ascontiguousarray(recv_counts, np.int64)
         self._ck(self.L.hdrf_gx_owner(self._h, x1_recv, _p(rc, _i64p), x2_send))
+
+    def gx_stream(self):
+        """hipStream_t (as an int) the back phases run on: RCCL exchanges enqueued on it need no host sync."""
+        s = ctypes.c_void_p()
+        self._ck(self.L.hdrf_gx_stream(self._h, ctypes.byref(s)))
+        return int(s.value or 0)
 
     def gx_decide(self, x2_recv):
         self._ck(self.L.hdrf_gx_decide(self._h, x2_recv))

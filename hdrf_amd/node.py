@@ -26,11 +26,15 @@ from .lib import ALLOC_STATE_BYTES, HdrfError
 class Exchange:
     """all-to-all of variable-length record regions laid out [G][cap][words] (int32 words)."""
 
-    def __init__(self, G, rank, device):
+    def __init__(self, G, rank, device, stream=None):
         self.G, self.rank, self.device = G, rank, device      # default process group, rank = GPU
         self.nccl = dist.get_backend() == "nccl"
         if self.nccl and (device is None or device.type != "cuda"):
             raise ValueError("the nccl (RCCL) exchange needs a GPU device")
+        # RCCL: the record exchanges are enqueued on the library's back stream (hdrf_gx_stream), so
+        # the phase that reads a receive buffer is ordered after the exchange on the device, with no
+        # host synchronisation in between
+        self.stream = stream if self.nccl else None
 
     def counts(self, send_counts):
         """Every rank's send counts -> this rank's receive counts (int64[G])."""
@@ -47,11 +51,18 @@ class Exchange:
         if self.nccl:
             sv = [send[d * cap * words:(d * cap + int(send_counts[d])) * words] for d in range(G)]
             rv = [recv[s * cap * words:(s * cap + int(recv_counts[s])) * words] for s in range(G)]
+            if self.stream is not None:
+                with torch.cuda.stream(self.stream):   # ordered on the back stream: no host sync
+                    dist.all_to_all(rv, sv)
+                return
             dist.all_to_all(rv, sv)
             torch.cuda.current_stream(self.device).synchronize()
             return
         # (a CPU device is allowed here: the multi-process CPU tests drive this path directly)
-        # gloo: stage through host memory, packed for all_to_all_single
+        # gloo: stage through host memory, packed for all_to_all_single; the send buffer may still be
+        # being written on the library's back stream (hdrf_gx_owner does not wait), so the device first
+        if send.is_cuda:
+            torch.cuda.synchronize(send.device)
         packed = torch.cat([send[d * cap * words:(d * cap + int(send_counts[d])) * words].cpu() for d in range(G)])
         out = torch.empty(int(np.sum(recv_counts)) * words, dtype=send.dtype)
         dist.all_to_all_single(out, packed, [int(c) * words for c in recv_counts],
@@ -155,7 +166,10 @@ class NodeRank:
         if self.G < 2:
             raise ValueError("NodeRank needs a context opened with n_ranks > 1")
         self.device = torch.device("cuda", int(ctx.cfg.device))
-        self.xc = Exchange(self.G, self.rank, self.device)
+        ext = None
+        if dist.get_backend() == "nccl":
+            ext = torch.cuda.ExternalStream(ctx.gx_stream(), device=self.device)
+        self.xc = Exchange(self.G, self.rank, self.device, ext)
         lay = ctx.gx_layout()
         self.cap, self.w = int(lay.cap), (int(lay.x1_words), int(lay.x2_words), int(lay.x3_words))
         n = self.G * self.cap

@@ -398,6 +398,12 @@ int hdrf_gx_alloc_io(hdrf_ctx *ctx, uint8_t *alloc_in, uint8_t *alloc_out);
 int hdrf_gx_piece(hdrf_ctx *ctx, uint32_t id, uint64_t off, uint64_t n, void *dev, int32_t write);
 int hdrf_gx_compress(hdrf_ctx *ctx);
 int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts);
+/* The stream the back phases (hdrf_gx_owner .. hdrf_gx_commit) run on (a hipStream_t).  A caller
+ * that enqueues its X1 / X2 record exchanges on it (RCCL collectives issued on this stream,
+ * torch.cuda.ExternalStream in hdrf_amd/node.py) needs no host synchronisation between an exchange
+ * and the phase that reads its receive buffer: hdrf_gx_owner and hdrf_gx_decide only enqueue, and
+ * a device error they raise is reported by hdrf_gx_place. */
+int hdrf_gx_stream(hdrf_ctx *ctx, void **stream);
 
 #ifdef __cplusplus
 }

@@ -52,6 +52,7 @@ class Loopback:
     def _a2a(self, send, recv, counts, w):
         """counts[s][d] records from rank s to rank d; returns recv counts [d][s]."""
         cap, G = self.cap, self.G
+        torch.cuda.synchronize()                 # the phases only enqueue on the contexts' streams
         for s in range(G):
             for d in range(G):
                 n = int(counts[s][d]) * w
