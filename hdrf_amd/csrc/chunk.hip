@@ -648,15 +648,19 @@ struct GmRing {
         }
     }
     bool on = true;                      // false: HDRF_WALK_RING=0, the maxima straight from memory (A/B)
+    __device__ __forceinline__ void direct(uint32_t (&d)[kGmWin], const uint8_t *gmb, int W0)
+    {
+#pragma unroll
+        for (int i = 0; i < kGmWin / 4; i++) {
+            const uint4 v = ld16(gmb + W0 + 16 * i);
+            d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
+        }
+    }
     __device__ __forceinline__ void get(uint32_t (&d)[kGmWin], const uint8_t *gmb, int W0)
     {
         w0 = W0;
         if (!on) {
-#pragma unroll
-            for (int i = 0; i < kGmWin / 4; i++) {
-                const uint4 v = ld16(gmb + W0 + 16 * i);
-                d[4 * i] = v.x; d[4 * i + 1] = v.y; d[4 * i + 2] = v.z; d[4 * i + 3] = v.w;
-            }
+            direct(d, gmb, W0);
             return;
         }
         if (W0 < rb || W0 > rb + kRingU) {
@@ -777,11 +781,17 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
             } else {
                 const int Glim = lim >> 4;
                 int Gs = G1 + 1;
+                int adv = 0;
                 while (Gs <= Glim) {
                     if (Gs >= W0 + 4 * kGmWin) {
                         if (16 * Gs > over_lim) { capped = true; break; }
                         W0 = Gs & ~3;
-                        ring.get(d, gmb, W0);
+                        // the first advance usually stays in the ring's next unit; a long search
+                        // (forced-cut regime: runs of >= 1 MB under the maximum) reads each unit
+                        // once, straight from memory: through the ring every unit also cost an LDS
+                        // write + read round trip (config 4 walk 47 -> 71 ms per batch, r03)
+                        if (adv++ == 0) ring.get(d, gmb, W0);
+                        else ring.direct(d, gmb, W0);
                     }
                     const unsigned long long m0 = gm_ge64(d, 0, C, Cm) & bits_from(Gs - W0) & bits_to(Glim - W0);
                     if (m0) {
