@@ -376,7 +376,32 @@ __device__ __forceinline__ void load_line(const uint8_t *base, int64_t readable,
     }
 }
 
-template <int HW>
+// Window of the line variant: dwords [q, q + 33) of the two lines P ++ R, q in [0, 31] per lane, by
+// a 5-stage barrel shift of selects (191 v_cndmask, no LDS, no memory).
+__device__ __forceinline__ void shift_window(const uint32_t (&P)[32], const uint32_t (&R)[32], uint32_t q, uint32_t (&d)[33])
+{
+    // per-lane masks (all ones where the stage shifts); the blends are on values (bfi), never a
+    // select of element addresses, so the arrays stay in registers
+    const uint32_t m16 = 0u - ((q >> 4) & 1u), m8 = 0u - ((q >> 3) & 1u), m4 = 0u - ((q >> 2) & 1u),
+                   m2 = 0u - ((q >> 1) & 1u), m1 = 0u - (q & 1u);
+    uint32_t y[48], z[40], w[36], v[34];
+#pragma unroll
+    for (int i = 0; i < 48; i++) y[i] = bfi(m16, i + 16 < 32 ? P[i + 16] : R[i - 16], i < 32 ? P[i] : R[i - 32]);
+#pragma unroll
+    for (int i = 0; i < 40; i++) z[i] = bfi(m8, y[i + 8], y[i]);
+#pragma unroll
+    for (int i = 0; i < 36; i++) w[i] = bfi(m4, z[i + 4], z[i]);
+#pragma unroll
+    for (int i = 0; i < 34; i++) v[i] = bfi(m2, w[i + 2], w[i]);
+#pragma unroll
+    for (int i = 0; i < 33; i++) d[i] = bfi(m1, v[i + 1], v[i]);
+}
+
+// LINE = false: sha_ring (the carried line in an LDS slot); LINE = true: sha_line, the carried line in
+// registers and the window cut out of the two lines by shift_window (every line fetched once, no LDS:
+// the ring's slot reads and writes, ~100 LDS instructions per iteration, and its 34 KiB per workgroup
+// cost more than the re-fetches they saved, r03).
+template <int HW, bool LINE>
 __global__ void __launch_bounds__(256) sha_ring_kernel(const BlockDesc *__restrict__ blocks,
                                                        const uint32_t *__restrict__ offsets,
                                                        const BlockState *__restrict__ bst, int cap_blk,
@@ -387,7 +412,7 @@ __global__ void __launch_bounds__(256) sha_ring_kernel(const BlockDesc *__restri
         sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr);
         return;
     }
-    __shared__ uint32_t s_slot[4 * 64 * kSlotDw];
+    __shared__ uint32_t s_slot[LINE ? 1 : 4 * 64 * kSlotDw];
     const int b = blockIdx.y - 1;
     const int n = bst[b].n_chunks;
     const BlockDesc &bd = blocks[b];
@@ -419,7 +444,7 @@ __global__ void __launch_bounds__(256) sha_ring_kernel(const BlockDesc *__restri
     int64_t wb = 0;                               // window start, block offset (b0 * 64 from the chunk)
     uint32_t st[8];
     set_iv<HW>(st);
-    uint32_t N0[32];                              // a fresh chunk's first line
+    uint32_t N0[32];                              // a fresh chunk's first line (LINE: the carried line)
     for (;;) {
         if (active && b0 >= (int)nb) {            // chain done: the digest
             store_digest<HW>(db + (size_t)k * HW, st);
@@ -464,14 +489,21 @@ __global__ void __launch_bounds__(256) sha_ring_kernel(const BlockDesc *__restri
         const uint32_t q0 = (uint32_t)((bmis + wb) & 124);          // window's first dword in L (x4)
         uint32_t R[32], d[33];
         if (data) load_line(base, readable, lo + 128, R);
-        if (ballot64(fresh)) {
+        if (LINE) {
+            if (data) {
+                shift_window(N0, R, q0 >> 2, d);
+#pragma unroll
+                for (int i = 0; i < 32; i++) N0[i] = R[i];
+            }
+            fresh = false;
+        } else if (ballot64(fresh)) {
             if (fresh) {
 #pragma unroll
                 for (int i = 0; i < 32; i++) slot[i] = N0[i];
             }
             fresh = false;
         }
-        if (data) {
+        if (!LINE && data) {
 #pragma unroll
             for (int j = 0; j < 33; j++) d[j] = slot[((q0 >> 2) + j) & 31];
 #pragma unroll
@@ -524,6 +556,8 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     // experiments: HDRF_SHA_WAVES (waves per SIMD over 1024 SIMDs), HDRF_SHA_LDS (bytes per WG)
     // HDRF_SHA_RING: 1 = sha_ring (each line fetched once, LDS line slots), 0 = sha_chunk
     static const bool ring = [] { const char *e = getenv("HDRF_SHA_RING"); return e ? atoi(e) != 0 : false; }();
+    // HDRF_SHA_LINE: 1 = sha_line (each line fetched once, window by a register barrel shift)
+    static const bool line = [] { const char *e = getenv("HDRF_SHA_LINE"); return e ? atoi(e) != 0 : false; }();
     // HDRF_SHA_WPC: waves per CU over the chip's 256 CUs (overrides HDRF_SHA_WAVES x 4)
     static const int per_cu = [] {
         const char *c = getenv("HDRF_SHA_WPC");
@@ -534,10 +568,14 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
-    if (ring && hasher == 0)
-        hipLaunchKernelGGL(sha_ring_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    if (line && hasher == 0)
+        hipLaunchKernelGGL((sha_ring_kernel<5, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    else if (line)
+        hipLaunchKernelGGL((sha_ring_kernel<7, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+    else if (ring && hasher == 0)
+        hipLaunchKernelGGL((sha_ring_kernel<5, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
     else if (ring)
-        hipLaunchKernelGGL(sha_ring_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+        hipLaunchKernelGGL((sha_ring_kernel<7, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
     else if (hasher == 0)
         hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
     else

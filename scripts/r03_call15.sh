@@ -1,0 +1,8 @@
+#!/bin/bash
+# Round 3: sha_line (each 128-B line fetched once, window cut out of two register-held lines by a
+# barrel shift): parity under HDRF_SHA_LINE=1, then A/B against sha_chunk with a request-count pass.
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
+HDRF_SHA_LINE=1 timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_parity.py tests/test_config2_shape.py tests/test_bench_shape.py -m gpu > gpurun_out/c15_tests.log 2>&1 || { tail -30 gpurun_out/c15_tests.log; exit 1; }
+tail -1 gpurun_out/c15_tests.log
+TAG=line bash scripts/r03_ab.sh HDRF_SHA_LINE=1 HDRF_SHA_LINE=0 HDRF_SHA_LINE=1 HDRF_SHA_LINE=0 "HDRF_SHA_LINE=1 HDRF_SHA_WPC=6" "HDRF_SHA_LINE=1 HDRF_SHA_WPC=12"
