@@ -922,6 +922,10 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
                     meta[G].sync = kSyncJump;
                 } else {
                     meta[G].sync = kSyncGiveUp;
+#ifdef HDRF_DEBUG_CHUNK
+                    printf("repair give-up: block %d seg %d p0 %d cuts %d status %d lim %d\n", bi, k, p0, sink.cnt,
+                           st.status, st.lim_cut);
+#endif
                 }
             }
         } else {
@@ -1181,6 +1185,10 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
         NoStop nostop;
         bool ok = walk_chain(W, p0, first, sink, nostop);
         sink.flush();
+#ifdef HDRF_DEBUG_CHUNK
+        if (lane_id() == 0)
+            printf("fallback: block %d fail_dst %d p0 %d cuts %d len %d\n", b, s.fail_dst, p0, sink.cnt, (int)bd.len);
+#endif
         if (!ok && lane_id() == 0) atomicOr(err, 1);
         s.n_cuts = s.fail_dst + sink.cnt;
     }

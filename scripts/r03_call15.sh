@@ -6,3 +6,5 @@ cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
 HDRF_SHA_LINE=1 timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_parity.py tests/test_config2_shape.py tests/test_bench_shape.py -m gpu > gpurun_out/c15_tests.log 2>&1 || { tail -30 gpurun_out/c15_tests.log; exit 1; }
 tail -1 gpurun_out/c15_tests.log
 TAG=line bash scripts/r03_ab.sh HDRF_SHA_LINE=1 HDRF_SHA_LINE=0 HDRF_SHA_LINE=1 HDRF_SHA_LINE=0 "HDRF_SHA_LINE=1 HDRF_SHA_WPC=6" "HDRF_SHA_LINE=1 HDRF_SHA_WPC=12"
+HDRF_LIB_PATH=$(pwd)/hdrf_amd/_build_dbg/libhdrf.so timeout -k 10 300 python -u scripts/c4_fallback_dbg.py > gpurun_out/c4_fallback_dbg.log 2>&1 || { tail -20 gpurun_out/c4_fallback_dbg.log; exit 1; }
+grep -c "give-up" gpurun_out/c4_fallback_dbg.log; grep -c "fallback:" gpurun_out/c4_fallback_dbg.log; grep -E "fallback:|stages" gpurun_out/c4_fallback_dbg.log | head -20; grep "give-up" gpurun_out/c4_fallback_dbg.log | head -10
