@@ -602,9 +602,10 @@ static void note_container(hdrf_ctx *ctx, uint32_t id, uint32_t slot, uint32_t l
     ctx->containers[id] = ContainerInfo{slot, len, closed, clen};
 }
 
-static ChunkScratch chunk_scratch(Slot &S)
+static ChunkScratch chunk_scratch(Slot &S, int compressor = 1)
 {
     ChunkScratch X;
+    X.ring = compressor == 2 ? 0 : 1;
     X.gm = S.d_gm; X.gstride = S.gstride; X.rq = S.d_rq; X.rq_count = S.d_rq_count; X.rq_cap = (int)S.meta_cap;
     X.irr = S.d_irr; X.path = S.d_path; X.jx = S.d_jx; X.jt = S.d_jt; X.wgsum = S.d_wgsum; X.maxw = S.maxw_cap;
     return X;
@@ -758,9 +759,9 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, G));
     Marker mw;
     mw.ev = ctx->timing ? S.evW : nullptr;
-    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs, chunk_scratch(S),
-                          c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst, S.d_off, ctx->cap_blk, S.d_err,
-                          W, &mw, G, S.gmax_done));
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs,
+                          chunk_scratch(S, c.compressor), c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst,
+                          S.d_off, ctx->cap_blk, S.d_err, W, &mw, G, S.gmax_done));
     mw.mark(W);
     HIPCK(hipEventRecord(S.walk_done, W));
     // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig)
@@ -1815,9 +1816,9 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
     Marker mk;
     mk.ev = ctx->timing ? S.evB : nullptr;             // 9 markers: gmax, walk .. slow+decide, end
-    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs, chunk_scratch(S),
-                          c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst, S.d_off, ctx->cap_blk, S.d_err,
-                          st, &mk));
+    HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs,
+                          chunk_scratch(S, c.compressor), c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst,
+                          S.d_off, ctx->cap_blk, S.d_err, st, &mk));
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig,
                      S.d_queue, ctx->sha_long, st, &mk));

@@ -680,6 +680,10 @@ struct GmRing {
     }
 };
 
+// RING: the granule maxima through the per-lane LDS ring (32 KiB of the workgroup's 48.6 KiB).  Off
+// under compressor 2: a CU holding 16 LZ4 waves has 16 KiB of LDS left, so a ring workgroup could
+// only start in the pass tails (config 4 walk 47 -> 65 ms per batch with the ring, r03).
+template <bool RING>
 __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
                                                         int total_waves, const uint8_t *__restrict__ gm,
                                                         int gstride, int w, int maxlen,
@@ -690,7 +694,7 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
 {
     __shared__ uint16_t s_cuts[4][64 * kLdsCuts];
     __shared__ uint8_t s_cnt[4][64];
-    __shared__ uint32_t s_ring[4][64 * kRingPitch];
+    __shared__ uint32_t s_ring[4][RING ? 64 * kRingPitch : 1];
     const int wv = blockIdx.x * 4 + wave_id();
     if (wv >= total_waves) return;
     lds_u16v *vcuts = (lds_u16v *)s_cuts[wave_id()];      // read by the neighbouring lane:
@@ -720,8 +724,8 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
     vcnt[l] = 0;
     uint32_t d[kGmWin];
     GmRing ring;
-    ring.r = (lds_u32 *)&s_ring[wave_id()][l * kRingPitch];
-    ring.on = ring_on != 0;
+    ring.r = (lds_u32 *)&s_ring[wave_id()][RING ? l * kRingPitch : 0];
+    ring.on = RING && ring_on != 0;
     uint4 rh = make_uint4(0, 0, 0, 0);                    // raw bytes of the last hit granule gh
     int gh = -1;
     for (;;) {
@@ -1235,8 +1239,14 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     // HDRF_WALK_LDS: dynamic LDS per walk workgroup (occupancy throttle: fewer lanes in flight keep
     // their granule-maximum lines in L2 between chunk steps)
     static const int walk_lds = [] { const char *v = getenv("HDRF_WALK_LDS"); return v ? atoi(v) : 0; }();
-    static const int ring_on = [] { const char *v = getenv("HDRF_WALK_RING"); return v ? atoi(v) : 1; }();
-    hipLaunchKernelGGL(lane_walk_kernel, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
+    // HDRF_WALK_RING: 1 / 0 force the ring on / off; default: X.ring (the caller's choice)
+    static const int ring_env = [] { const char *v = getenv("HDRF_WALK_RING"); return v ? atoi(v) : -1; }();
+    const int ring_on = ring_env >= 0 ? ring_env : X.ring;
+    if (ring_on)
+        hipLaunchKernelGGL(lane_walk_kernel<true>, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
+                           X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, 1);
+    else
+    hipLaunchKernelGGL(lane_walk_kernel<false>, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
                        X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, ring_on);
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue

@@ -42,6 +42,7 @@ struct ChunkScratch {
     uint32_t *jt;            // [nblocks][2048] targets | shared-cut index << 24
     uint32_t *wgsum;         // [nblocks][maxw] piece sums per 256 segments
     int maxw;
+    int ring = 1;            // lane walk: granule maxima through the LDS ring (off beside LZ4 passes)
 };
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
