@@ -690,8 +690,9 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
                                                         uint32_t *__restrict__ spec, int cap,
                                                         SegMeta *__restrict__ meta, int *__restrict__ rq,
                                                         int *__restrict__ rq_count, int rq_cap,
-                                                        uint32_t *__restrict__ irr, int *__restrict__ err, int ring_on)
-{
+                                                        uint32_t *__restrict__ irr, int *__restrict__ err, int ring_on, int prio)
+{    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
+
     __shared__ uint16_t s_cuts[4][64 * kLdsCuts];
     __shared__ uint8_t s_cnt[4][64];
     __shared__ uint32_t s_ring[4][RING ? 64 * kRingPitch : 1];
@@ -891,8 +892,9 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
                                                           const uint32_t *__restrict__ spec, int cap,
                                                           SegMeta *__restrict__ meta, uint32_t *__restrict__ offsets,
                                                           int cap_blk, const uint8_t *__restrict__ gm, int gstride,
-                                                          int emit)
-{
+                                                          int emit, int prio)
+{    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
+
     const int nw = gridDim.x * 4;
     const int cnt = min(*rq_count, rq_cap);
     for (int q = blockIdx.x * 4 + wave_id(); q < cnt; q += nw) {
@@ -965,8 +967,9 @@ __global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__res
                                                           const uint32_t *__restrict__ irr,
                                                           const SegMeta *__restrict__ meta,
                                                           PathInfo *__restrict__ path, int *__restrict__ jx_all,
-                                                          uint32_t *__restrict__ jt_all)
-{
+                                                          uint32_t *__restrict__ jt_all, int prio)
+{    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
+
     __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes (ascending)
     __shared__ uint32_t s_nv[kStitchNodes];  // status: bit 31 jump (jmp in bits 0..23, jj in 24..29), bit 30 end
     __shared__ uint32_t s_sum[256];
@@ -1172,8 +1175,9 @@ __global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__res
 __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__restrict__ blocks, int w, int maxlen,
                                                            uint32_t *__restrict__ offsets, int cap_blk,
                                                            BlockState *__restrict__ bst, const uint8_t *__restrict__ gm,
-                                                           int gstride, int *__restrict__ err)
-{
+                                                           int gstride, int *__restrict__ err, int prio)
+{    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
+
     const int b = blockIdx.x;
     const BlockDesc bd = blocks[b];
     BlockState s = bst[b];
@@ -1212,6 +1216,12 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
 namespace hdrf {
 int lane_spec_cap(int seg_len, int w) { return seg_len / (w + 2) + 2 + kLaneOver; }
 
+int setprio_mask()
+{
+    static const int m = [] { const char *e = getenv("HDRF_SETPRIO"); return e ? atoi(e) : 0; }();
+    return m;
+}
+
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
@@ -1239,20 +1249,25 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     // HDRF_WALK_LDS: dynamic LDS per walk workgroup (occupancy throttle: fewer lanes in flight keep
     // their granule-maximum lines in L2 between chunk steps)
     static const int walk_lds = [] { const char *v = getenv("HDRF_WALK_LDS"); return v ? atoi(v) : 0; }();
+    // HDRF_SETPRIO (bit mask): raise the issue priority of the latency-bound chunking kernels over
+    // the co-running waves (bit 0 the lane walk, bit 1 repair / stitch path / sequential fallback;
+    // bit 2 the long SHA lanes, sha.hip)
+    const int prio = setprio_mask();
     // HDRF_WALK_RING: 1 / 0 force the ring on / off; default: X.ring (the caller's choice)
     static const int ring_env = [] { const char *v = getenv("HDRF_WALK_RING"); return v ? atoi(v) : -1; }();
     const int ring_on = ring_env >= 0 ? ring_env : X.ring;
     if (ring_on)
         hipLaunchKernelGGL(lane_walk_kernel<true>, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
-                           X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, 1);
+                           X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, 1,
+                           prio & 1);
     else
     hipLaunchKernelGGL(lane_walk_kernel<false>, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
-                       X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, ring_on);
+                       X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, ring_on, prio & 1);
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0);
-    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0, (prio >> 1) & 1);
+    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, (prio >> 1) & 1);
     hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt,
                        X.wgsum, maxw, err);
     hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
@@ -1260,9 +1275,9 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     hipLaunchKernelGGL(stitch_copy_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, spec, spec_cap,
                        X.wgsum, maxw, bst, offsets, cap_blk);
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1, (prio >> 1) & 1);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
-                       cap_blk, bst, X.gm, X.gstride, err);
+                       cap_blk, bst, X.gm, X.gstride, err, (prio >> 1) & 1);
     return hipGetLastError();
 }
 }  // namespace hdrf

@@ -210,9 +210,10 @@ constexpr int kShaTile = 1024;                 // chunks per scan tile (4 per th
 template <int HW>
 __device__ __forceinline__ void sha_long_lanes(const BlockDesc *__restrict__ blocks, const uint32_t *__restrict__ offsets,
                                                const BlockState *__restrict__ bst, int cap_blk,
-                                               uint32_t *__restrict__ digests, uint32_t thr)
+                                               uint32_t *__restrict__ digests, uint32_t thr, int setprio_long)
 {
     if (thr == 0xffffffffu) return;
+    if (setprio_long) __builtin_amdgcn_s_setprio(3);   // one lane's 15,625-compression chain per 1 MB chunk
     __shared__ uint32_t s_long[kShaTile + 256];
     __shared__ uint32_t s_nl;
     const int t = threadIdx.x;
@@ -274,12 +275,13 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
                                                         const uint32_t *__restrict__ offsets,
                                                         const BlockState *__restrict__ bst, int cap_blk,
                                                         uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                        uint32_t thr)
+                                                        uint32_t thr, int prio)
 {
     if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
-        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr);
+        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr, prio & 1);
         return;
     }
+    if (prio & 2) __builtin_amdgcn_s_setprio(2);        // HDRF_SETPRIO bit 3: the chunk lanes too
     const int b = blockIdx.y - 1;
     const int n = bst[b].n_chunks;
     const BlockDesc &bd = blocks[b];
@@ -406,13 +408,14 @@ __global__ void __launch_bounds__(256) sha_ring_kernel(const BlockDesc *__restri
                                                        const uint32_t *__restrict__ offsets,
                                                        const BlockState *__restrict__ bst, int cap_blk,
                                                        uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                       uint32_t thr)
+                                                       uint32_t thr, int prio)
 {
     if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
-        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr);
+        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr, prio & 1);
         return;
     }
     __shared__ uint32_t s_slot[LINE ? 1 : 4 * 64 * kSlotDw];
+    if (prio & 2) __builtin_amdgcn_s_setprio(2);
     const int b = blockIdx.y - 1;
     const int n = bst[b].n_chunks;
     const BlockDesc &bd = blocks[b];
@@ -569,17 +572,17 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
     if (line && hasher == 0)
-        hipLaunchKernelGGL((sha_ring_kernel<5, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+        hipLaunchKernelGGL((sha_ring_kernel<5, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (line)
-        hipLaunchKernelGGL((sha_ring_kernel<7, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+        hipLaunchKernelGGL((sha_ring_kernel<7, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (ring && hasher == 0)
-        hipLaunchKernelGGL((sha_ring_kernel<5, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+        hipLaunchKernelGGL((sha_ring_kernel<5, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (ring)
-        hipLaunchKernelGGL((sha_ring_kernel<7, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+        hipLaunchKernelGGL((sha_ring_kernel<7, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (hasher == 0)
-        hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+        hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else
-        hipLaunchKernelGGL(sha_chunk_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr);
+        hipLaunchKernelGGL(sha_chunk_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     mk->mark(st);                                  // (the stage timer's former tail slot: empty)
     return hipGetLastError();
 }

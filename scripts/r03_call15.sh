@@ -10,3 +10,6 @@ HDRF_LIB_PATH=$(pwd)/hdrf_amd/_build_dbg/libhdrf.so timeout -k 10 300 python -u 
 grep -c "give-up" gpurun_out/c4_fallback_dbg.log; grep -c "fallback:" gpurun_out/c4_fallback_dbg.log; grep -E "fallback:|stages" gpurun_out/c4_fallback_dbg.log | head -20; grep "give-up" gpurun_out/c4_fallback_dbg.log | head -10
 timeout -k 10 600 python -u bench.py --workload config4 --steps 2 --warmup 1 --no-cpu > gpurun_out/r03_c4_v3.json.log 2>&1 || { tail -20 gpurun_out/r03_c4_v3.json.log; exit 1; }
 tail -1 gpurun_out/r03_c4_v3.json.log | python3 -c "import json,sys; d=json.load(sys.stdin); print('config4', d['value'], d['roofline']['chains_ms_per_batch']); print({k:v['avg_launch_ms'] for k,v in d['stages'].items()})"
+HDRF_SETPRIO=7 timeout -k 10 600 python -u bench.py --workload config4 --steps 2 --warmup 1 --no-cpu > gpurun_out/r03_c4_v3p.json.log 2>&1 || { tail -20 gpurun_out/r03_c4_v3p.json.log; exit 1; }
+tail -1 gpurun_out/r03_c4_v3p.json.log | python3 -c "import json,sys; d=json.load(sys.stdin); print('config4 prio7', d['value'], d['roofline']['chains_ms_per_batch']); print({k:v['avg_launch_ms'] for k,v in d['stages'].items()})"
+NO_PMC=1 TAG=prio bash scripts/r03_ab.sh HDRF_SETPRIO=0 HDRF_SETPRIO=3 HDRF_SETPRIO=7 HDRF_SETPRIO=15 HDRF_SETPRIO=3
