@@ -55,8 +55,9 @@ struct Slot {
     int max_nseg = 0;                         // most segments of one block of the batch
     uint32_t *d_irr = nullptr;                // irregular-boundary bitmask (meta_cap / 32 + 2 words)
     PathInfo *d_path = nullptr;               // [B]
-    int *d_jx = nullptr;                      // [B][2048]
-    uint32_t *d_jt = nullptr;                 // [B][2048]
+    int *d_jx = nullptr;                      // [B][jcap]
+    uint32_t *d_jt = nullptr;                 // [B][jcap]
+    int jcap = 0;
     uint32_t *d_wgsum = nullptr;              // [B][maxw_cap]
     int maxw_cap = 0;
     int *d_rq = nullptr, *d_rq_count = nullptr;   // failed speculative boundaries (repair queue), meta_cap entries
@@ -368,9 +369,11 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
     S.meta_cap = (size_t)B * (size_t)(c.max_block_bytes / seg_len0 + 2);
     S.spec_words = S.meta_cap * (size_t)lane_spec_cap(seg_len0, c.window);
     S.gstride = (int)(((c.max_block_bytes + 15) / 16 + 1024 + 255) & ~(int64_t)255);
+    // on-path stitch jumps: at most one per segment boundary at the finest segmentation
+    S.jcap = (int)(c.max_block_bytes / ((int64_t)kSegMinWin * (c.window + 2)) + 2);
     if ((rc = dalloc(ctx, &S.d_blocks, B)) || (rc = dalloc(ctx, &S.d_spec, S.spec_words)) ||
         (rc = dalloc(ctx, &S.d_gm, (size_t)B * S.gstride)) || (rc = dalloc(ctx, &S.d_path, B)) ||
-        (rc = dalloc(ctx, &S.d_jx, (size_t)B * 2048)) || (rc = dalloc(ctx, &S.d_jt, (size_t)B * 2048)) ||
+        (rc = dalloc(ctx, &S.d_jx, (size_t)B * S.jcap)) || (rc = dalloc(ctx, &S.d_jt, (size_t)B * S.jcap)) ||
         (rc = dalloc(ctx, &S.d_irr, S.meta_cap / 32 + 2)) ||
         (rc = dalloc(ctx, &S.d_meta, S.meta_cap)) || (rc = dalloc(ctx, &S.d_rq, S.meta_cap)) ||
         (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
@@ -607,7 +610,8 @@ static ChunkScratch chunk_scratch(Slot &S, int compressor = 1)
     ChunkScratch X;
     X.ring = compressor == 2 ? 0 : 1;
     X.gm = S.d_gm; X.gstride = S.gstride; X.rq = S.d_rq; X.rq_count = S.d_rq_count; X.rq_cap = (int)S.meta_cap;
-    X.irr = S.d_irr; X.path = S.d_path; X.jx = S.d_jx; X.jt = S.d_jt; X.wgsum = S.d_wgsum; X.maxw = S.maxw_cap;
+    X.irr = S.d_irr; X.path = S.d_path; X.jx = S.d_jx; X.jt = S.d_jt; X.jcap = S.jcap; X.wgsum = S.d_wgsum;
+    X.maxw = S.maxw_cap;
     return X;
 }
 

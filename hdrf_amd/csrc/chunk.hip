@@ -473,8 +473,9 @@ constexpr int kGmPerWg = 4096;           // granules per workgroup (64 KiB of da
 
 template <bool NT>
 __global__ void __launch_bounds__(256) gmax_kernel(const BlockDesc *__restrict__ blocks, uint8_t *__restrict__ gm,
-                                                   int gstride)
+                                                   int gstride, int prio)
 {
+    if (prio) __builtin_amdgcn_s_setprio(2);        // HDRF_SETPRIO bit 4: ahead of SHA's VALU stream
     const BlockDesc bd = blocks[blockIdx.y];
     const int64_t ngran = (int64_t)((bd.len + 15) >> 4);
     const int64_t g0 = (int64_t)blockIdx.x * kGmPerWg;
@@ -956,23 +957,26 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
 //      count  one thread per segment: its piece (first list index, cuts, repair cuts) + workgroup sums
 //      scan   one workgroup per block: prefix over the workgroup sums; n_cuts / fail_dst
 //      copy   one thread per segment: workgroup prefix -> destination; the piece is copied
-// Irregular boundaries per block followed (more: the fallback takes over there, exact either way).
-// The LDS this sizes (path 17 KiB, count 16.5 KiB) does not fit beside a compressor-2 LZ4 pass at
-// 16 waves per CU (16 KiB left), so in config 4 the stitch kernels of the next batches run in the
-// pass tails; with 1024 nodes they co-run with the pass and config 4 drops from 33 to 27 GB/s
-// (stitch stage 70 -> 115 ms, profiles/r02_c4_stitch1024_ab.txt): kept at 2048.
-constexpr int kStitchNodes = 2048;
+// The irregular boundaries are compacted kStitchNodes at a time (a window of the ordered node list
+// in LDS); thread 0 follows the path through a window and the next window is loaded when the path
+// leaves it, so any number of irregular boundaries is followed (round 2 capped them at 2048 per block
+// and handed the rest of the block to the sequential fallback: config-4 blocks of binary records
+// reach that many, and their last 1-18 MiB were walked by one wave, 34 ms per batch, r03).  The
+// on-path jumps go to jx / jt (jcap per block: every segment boundary at most once).  8.5 KiB of LDS
+// (path) and 2 KiB (count) let both start beside a compressor-2 LZ4 pass (16 KiB free per CU).
+constexpr int kStitchNodes = 1024;
 
 __global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__restrict__ blocks,
                                                           const uint32_t *__restrict__ irr,
                                                           const SegMeta *__restrict__ meta,
                                                           PathInfo *__restrict__ path, int *__restrict__ jx_all,
-                                                          uint32_t *__restrict__ jt_all, int prio)
-{    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
-
-    __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes (ascending)
+                                                          uint32_t *__restrict__ jt_all, int jcap, int prio)
+{
+    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
+    __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes of the window (ascending)
     __shared__ uint32_t s_nv[kStitchNodes];  // status: bit 31 jump (jmp in bits 0..23, jj in 24..29), bit 30 end
     __shared__ uint32_t s_sum[256];
+    __shared__ int s_go, s_cur;
     const int b = blockIdx.x, t = threadIdx.x;
     const BlockDesc bd = blocks[b];
     const int nseg = bd.nseg, s0 = bd.seg0;
@@ -998,43 +1002,56 @@ __global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__res
         s_sum[t] += x;
         __syncthreads();
     }
-    uint32_t pos = s_sum[t] - cnt;
+    const uint32_t pos0 = s_sum[t] - cnt;    // this thread's first node in the ordered list
     const int tot = (int)s_sum[255];
-    for (int i = w0; i < w1; i++)
-        for (uint32_t v = word(i); v; v &= v - 1) {
-            const int k = 32 * i + __builtin_ctz(v);
-            if (pos < (uint32_t)kStitchNodes) {
-                s_nx[pos] = k;
-                const int sy = mt[k].sync;
-                s_nv[pos] = sy == kSyncJump ? (0x80000000u | ((uint32_t)mt[k].jj << 24) | (uint32_t)mt[k].jmp)
-                                            : (sy == kSyncEnd ? 0x40000000u : 0u);
-            }
-            pos++;
+    int *jx = jx_all + (size_t)b * jcap;
+    uint32_t *jt = jt_all + (size_t)b * jcap;
+    int cur = 0, nj = 0, term = nseg - 1, fb = 0;        // thread 0's path state
+    for (int wb = 0;; wb += kStitchNodes) {
+        // window [wb, wb + kStitchNodes) of the node list
+        if (pos0 < (uint32_t)(wb + kStitchNodes) && pos0 + cnt > (uint32_t)wb) {
+            uint32_t pos = pos0;
+            for (int i = w0; i < w1 && pos < (uint32_t)(wb + kStitchNodes); i++)
+                for (uint32_t v = word(i); v; v &= v - 1) {
+                    if (pos >= (uint32_t)wb && pos < (uint32_t)(wb + kStitchNodes)) {
+                        const int k = 32 * i + __builtin_ctz(v);
+                        const int sy = mt[k].sync;
+                        s_nx[pos - wb] = k;
+                        s_nv[pos - wb] = sy == kSyncJump ? (0x80000000u | ((uint32_t)mt[k].jj << 24) | (uint32_t)mt[k].jmp)
+                                                         : (sy == kSyncEnd ? 0x40000000u : 0u);
+                    }
+                    pos++;
+                }
         }
-    __syncthreads();
-    if (t == 0) {
-        const int nnx = min(tot, kStitchNodes);
-        int *jx = jx_all + (size_t)b * kStitchNodes;
-        uint32_t *jt = jt_all + (size_t)b * kStitchNodes;
-        int cur = 0, i = 0, nj = 0, term = nseg - 1, fb = 0;
-        for (;;) {
-            while (i < nnx && s_nx[i] < cur) i++;
-            if (i >= nnx) {
-                if (tot > kStitchNodes) { term = cur; fb = 1; }   // uncompacted nodes ahead: fall back here
+        __syncthreads();
+        if (t == 0) {
+            const int nnx = min(tot - wb, kStitchNodes);
+            int i = 0, go = 0;
+            for (;;) {
+                while (i < nnx && s_nx[i] < cur) i++;
+                if (i >= nnx) {
+                    go = wb + kStitchNodes < tot;          // nodes ahead: the next window
+                    break;
+                }
+                const int x = s_nx[i];
+                const uint32_t v = s_nv[i];
+                if (v & 0x80000000u) {
+                    if (nj >= jcap) { term = x; fb = 1; break; }    // (cannot happen: one jump per boundary)
+                    const int tgt = x + (int)(v & 0xffffffu);
+                    jx[nj] = x; jt[nj] = (uint32_t)tgt | (v & 0x3f000000u); nj++;
+                    cur = tgt;
+                    continue;
+                }
+                term = x;
+                fb = (v & 0x40000000u) == 0;
                 break;
             }
-            const int x = s_nx[i];
-            const uint32_t v = s_nv[i];
-            if ((v & 0x80000000u) && nj < kStitchNodes) {
-                const int tgt = x + (int)(v & 0xffffffu);
-                jx[nj] = x; jt[nj] = (uint32_t)tgt | (v & 0x3f000000u); nj++;
-                cur = tgt;
-                continue;
-            }
-            term = x;
-            fb = (v & 0x40000000u) == 0;
-            break;
+            s_go = go;
         }
+        __syncthreads();
+        if (!s_go) break;
+    }
+    if (t == 0) {
         PathInfo pi;
         pi.nj = nj; pi.term = term; pi.fb = fb; pi.pad = 0;
         path[b] = pi;
@@ -1057,31 +1074,47 @@ __global__ void __launch_bounds__(256) stitch_count_kernel(const BlockDesc *__re
                                                            SegMeta *__restrict__ meta,
                                                            const PathInfo *__restrict__ path,
                                                            const int *__restrict__ jx_all,
-                                                           const uint32_t *__restrict__ jt_all,
+                                                           const uint32_t *__restrict__ jt_all, int jcap,
                                                            uint32_t *__restrict__ wgsum, int maxw,
                                                            int *__restrict__ err)
 {
-    __shared__ int s_jx[kStitchNodes];
-    __shared__ uint32_t s_jt[kStitchNodes];
+    // the jumps that matter to this workgroup's 256 segments: the last one with source < k0 and those
+    // with source in [k0, k0 + 256) (sources ascend along the path, one per boundary at most)
+    __shared__ int s_jx[257];
+    __shared__ uint32_t s_jt[257];
+    __shared__ int s_j0, s_nr;
     __shared__ uint32_t s_w[4];
     const int b = blockIdx.y, t = threadIdx.x;
     const BlockDesc bd = blocks[b];
     const int nseg = bd.nseg;
     if ((int)blockIdx.x * 256 >= nseg) return;            // whole workgroup
-    const int k = blockIdx.x * 256 + t;
+    const int k0 = blockIdx.x * 256;
+    const int k = k0 + t;
     const PathInfo pi = path[b];
-    const int nj = pi.nj, term = pi.term;
-    for (int i = t; i < nj; i += 256) {
-        s_jx[i] = jx_all[(size_t)b * kStitchNodes + i];
-        s_jt[i] = jt_all[(size_t)b * kStitchNodes + i];
+    const int term = pi.term;
+    const int *jxb = jx_all + (size_t)b * jcap;
+    const uint32_t *jtb = jt_all + (size_t)b * jcap;
+    if (t == 0) {
+        int lo = 0, hi = pi.nj;                            // first jump with source >= k0
+        while (lo < hi) { const int mid = (lo + hi) >> 1; if (jxb[mid] < k0) lo = mid + 1; else hi = mid; }
+        int e = lo, ehi = pi.nj;                           // first jump with source >= k0 + 256
+        while (e < ehi) { const int mid = (e + ehi) >> 1; if (jxb[mid] < k0 + 256) e = mid + 1; else ehi = mid; }
+        s_j0 = lo - 1;
+        s_nr = e - (lo - 1);
     }
     __syncthreads();
+    const int j0 = s_j0, nr = s_nr;
+    for (int i = t; i < nr; i += 256)
+        if (j0 + i >= 0) { s_jx[i] = jxb[j0 + i]; s_jt[i] = jtb[j0 + i]; }
+    __syncthreads();
+    const int nj = nr;                                     // local indices: jump j0 + i at i
     SegMeta *mt = meta + bd.seg0;
     int from = 0, cnt = 0, ext = -1;
     if (k < nseg && k <= term) {
-        int lo = 0, hi = nj;                               // last jump with source < k
+        const int i0 = j0 < 0 ? 1 : 0;                     // local entry 0 is jump j0 (none when j0 < 0)
+        int lo = i0, hi = nj;                              // last jump with source < k
         while (lo < hi) { const int mid = (lo + hi) >> 1; if (s_jx[mid] < k) lo = mid + 1; else hi = mid; }
-        const int ji = lo - 1;
+        const int ji = lo - 1 >= i0 ? lo - 1 : -1;
         bool target = false, over = false;
         if (ji >= 0) {
             const int tgt = (int)(s_jt[ji] & 0xffffffu);
@@ -1236,11 +1269,15 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     hipError_t e = hipMemsetAsync(X.rq_count, 0, sizeof(int), st);
     if (e == hipSuccess) e = hipMemsetAsync(X.irr, 0, sizeof(uint32_t) * (size_t)(nsegs / 32 + 2), st);
     if (e != hipSuccess) return e;
+    // HDRF_SETPRIO (bit mask): raise the issue priority of kernels over the co-running waves (bit 0
+    // the lane walk, bit 1 repair / stitch path / sequential fallback, bit 2 the long SHA lanes, bit 3
+    // all SHA lanes (sha.hip), bit 4 the granule pass, bit 5 place (store.hip))
+    const int prio = setprio_mask();
     const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
     if (stream_knobs() & 1)
-        hipLaunchKernelGGL(gmax_kernel<true>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride);
+        hipLaunchKernelGGL(gmax_kernel<true>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride, (prio >> 4) & 1);
     else
-        hipLaunchKernelGGL(gmax_kernel<false>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride);
+        hipLaunchKernelGGL(gmax_kernel<false>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride, (prio >> 4) & 1);
     mk->mark(sg);
     if (split) {
         if ((e = hipEventRecord(gdone, sg)) != hipSuccess || (e = hipStreamWaitEvent(st, gdone, 0)) != hipSuccess)
@@ -1249,10 +1286,6 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     // HDRF_WALK_LDS: dynamic LDS per walk workgroup (occupancy throttle: fewer lanes in flight keep
     // their granule-maximum lines in L2 between chunk steps)
     static const int walk_lds = [] { const char *v = getenv("HDRF_WALK_LDS"); return v ? atoi(v) : 0; }();
-    // HDRF_SETPRIO (bit mask): raise the issue priority of the latency-bound chunking kernels over
-    // the co-running waves (bit 0 the lane walk, bit 1 repair / stitch path / sequential fallback;
-    // bit 2 the long SHA lanes, sha.hip)
-    const int prio = setprio_mask();
     // HDRF_WALK_RING: 1 / 0 force the ring on / off; default: X.ring (the caller's choice)
     static const int ring_env = [] { const char *v = getenv("HDRF_WALK_RING"); return v ? atoi(v) : -1; }();
     const int ring_on = ring_env >= 0 ? ring_env : X.ring;
@@ -1267,8 +1300,9 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     const int rgrid = 512;                             // 2048 repair waves loop over the queue
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
                        w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0, (prio >> 1) & 1);
-    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, (prio >> 1) & 1);
-    hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt,
+    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
+                       (prio >> 1) & 1);
+    hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt, X.jcap,
                        X.wgsum, maxw, err);
     hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
                        cap_blk, err);

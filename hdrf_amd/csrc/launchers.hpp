@@ -38,8 +38,9 @@ struct ChunkScratch {
     int rq_cap;
     uint32_t *irr;           // irregular-boundary bitmask over the batch's segments (+2 words)
     PathInfo *path;          // [nblocks]
-    int *jx;                 // [nblocks][2048] on-path jump sources
-    uint32_t *jt;            // [nblocks][2048] targets | shared-cut index << 24
+    int *jx;                 // [nblocks][jcap] on-path jump sources
+    uint32_t *jt;            // [nblocks][jcap] targets | shared-cut index << 24
+    int jcap;                // jumps per block (>= its segment boundaries)
     uint32_t *wgsum;         // [nblocks][maxw] piece sums per 256 segments
     int maxw;
     int ring = 1;            // lane walk: granule maxima through the LDS ring (off beside LZ4 passes)

@@ -334,8 +334,9 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
                                                     const FlushEv *__restrict__ events, const uint32_t *__restrict__ slot,
                                                     IndexEntry *__restrict__ tab, uint8_t *__restrict__ arena,
                                                     uint32_t *__restrict__ place_cid, uint32_t *__restrict__ place_pos,
-                                                    GxPlace gx)
+                                                    GxPlace gx, int prio)
 {
+    if (prio) __builtin_amdgcn_s_setprio(2);        // HDRF_SETPRIO bit 5
     const int b = blockIdx.y;
     const int k = blockIdx.x * 256 + threadIdx.x;
     const int n = bst[b].n_chunks;
@@ -482,10 +483,12 @@ hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, c
         if (hipError_t e = hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st)) return e;
     if (stream_knobs() & 2)
         hipLaunchKernelGGL(place_kernel<true>, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst,
-                           offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx);
+                           offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx,
+                           (setprio_mask() >> 5) & 1);
     else
         hipLaunchKernelGGL(place_kernel<false>, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst,
-                           offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx);
+                           offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx,
+                           (setprio_mask() >> 5) & 1);
     return hipGetLastError();
 }
 
