@@ -349,6 +349,194 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
     }
 }
 
+// sha_dual: every lane runs TWO independent chunk chains (A and B, both fed from the wave's pool) and
+// their compressions are interleaved round by round (sha*_compress2), so one wave per SIMD has the
+// instruction-level parallelism two waves had.  The point is the waves it frees: at 8 SHA waves per
+// CU the granule pass, walk, place and index kernels ran 1.6-2.7x slower than at 4 (r03: gmax 2.7 vs
+// 1.0 ms per batch in the pipeline), but single-chain SHA at 4 waves per CU left its VALU latency
+// exposed (3.9 ms per batch).  A lane whose chain has nothing to do computes a discarded compression.
+__device__ __forceinline__ void sha1_compress2(uint32_t sa[5], uint32_t wa[16], uint32_t sb[5], uint32_t wb[16])
+{
+    uint32_t a = sa[0], b = sa[1], c = sa[2], d = sa[3], e = sa[4];
+    uint32_t A = sb[0], B = sb[1], C = sb[2], D = sb[3], E = sb[4];
+#pragma unroll
+    for (int i = 0; i < 80; i++) {
+        if (i >= 16) {
+            wa[i & 15] = rotl(xor3(wa[(i - 3) & 15], wa[(i - 8) & 15], wa[(i - 14) & 15]) ^ wa[i & 15], 1);
+            wb[i & 15] = rotl(xor3(wb[(i - 3) & 15], wb[(i - 8) & 15], wb[(i - 14) & 15]) ^ wb[i & 15], 1);
+        }
+        uint32_t f, F, k;
+        if (i < 20)      { f = ch(b, c, d);   F = ch(B, C, D);   k = 0x5A827999u; }
+        else if (i < 40) { f = xor3(b, c, d); F = xor3(B, C, D); k = 0x6ED9EBA1u; }
+        else if (i < 60) { f = maj(b, c, d);  F = maj(B, C, D);  k = 0x8F1BBCDCu; }
+        else             { f = xor3(b, c, d); F = xor3(B, C, D); k = 0xCA62C1D6u; }
+        const uint32_t t = rotl(a, 5) + f + e + k + wa[i & 15];
+        const uint32_t T = rotl(A, 5) + F + E + k + wb[i & 15];
+        e = d; d = c; c = rotl(b, 30); b = a; a = t;
+        E = D; D = C; C = rotl(B, 30); B = A; A = T;
+    }
+    sa[0] += a; sa[1] += b; sa[2] += c; sa[3] += d; sa[4] += e;
+    sb[0] += A; sb[1] += B; sb[2] += C; sb[3] += D; sb[4] += E;
+}
+
+__device__ __forceinline__ void sha256_compress2(uint32_t sa[8], uint32_t wa[16], uint32_t sb[8], uint32_t wb[16])
+{
+    uint32_t a = sa[0], b = sa[1], c = sa[2], d = sa[3], e = sa[4], f = sa[5], g = sa[6], h = sa[7];
+    uint32_t A = sb[0], B = sb[1], C = sb[2], D = sb[3], E = sb[4], F = sb[5], G = sb[6], H = sb[7];
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+        if (i >= 16) {
+            {
+                const uint32_t w15 = wa[(i - 15) & 15], w2 = wa[(i - 2) & 15];
+                wa[i & 15] = wa[i & 15] + xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3) + wa[(i - 7) & 15] +
+                             xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            }
+            {
+                const uint32_t w15 = wb[(i - 15) & 15], w2 = wb[(i - 2) & 15];
+                wb[i & 15] = wb[i & 15] + xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3) + wb[(i - 7) & 15] +
+                             xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+            }
+        }
+        const uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) + kK256[i] + wa[i & 15];
+        const uint32_t T1 = H + xor3(rotr(E, 6), rotr(E, 11), rotr(E, 25)) + ch(E, F, G) + kK256[i] + wb[i & 15];
+        const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
+        const uint32_t T2 = xor3(rotr(A, 2), rotr(A, 13), rotr(A, 22)) + maj(A, B, C);
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        H = G; G = F; F = E; E = D + T1; D = C; C = B; B = A; A = T1 + T2;
+    }
+    sa[0] += a; sa[1] += b; sa[2] += c; sa[3] += d; sa[4] += e; sa[5] += f; sa[6] += g; sa[7] += h;
+    sb[0] += A; sb[1] += B; sb[2] += C; sb[3] += D; sb[4] += E; sb[5] += F; sb[6] += G; sb[7] += H;
+}
+
+struct ShaChain {
+    bool active = false;
+    int k = 0;
+    uint32_t s0 = 0, len = 0, T = 0, nb = 0, bi = 0;
+    uint32_t st[8];
+};
+
+// the two compressions of one slot of both chains; a chain's state changes only where `use`
+template <int HW>
+__device__ __forceinline__ void compress_both(ShaChain &A, uint32_t ma[16], bool useA, ShaChain &B, uint32_t mb[16],
+                                              bool useB)
+{
+    uint32_t na[8], nb[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) { na[i] = A.st[i]; nb[i] = B.st[i]; }
+    if (HW == 5) sha1_compress2(na, ma, nb, mb);
+    else sha256_compress2(na, ma, nb, mb);
+#pragma unroll
+    for (int i = 0; i < HW; i++) {
+        A.st[i] = useA ? na[i] : A.st[i];
+        B.st[i] = useB ? nb[i] : B.st[i];
+    }
+}
+
+template <int HW>
+__global__ void __launch_bounds__(256) sha_dual_kernel(const BlockDesc *__restrict__ blocks,
+                                                       const uint32_t *__restrict__ offsets,
+                                                       const BlockState *__restrict__ bst, int cap_blk,
+                                                       uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                                       uint32_t thr, int prio)
+{
+    if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
+        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr, prio & 1);
+        return;
+    }
+    if (prio & 2) __builtin_amdgcn_s_setprio(2);
+    const int b = blockIdx.y - 1;
+    const int n = bst[b].n_chunks;
+    const BlockDesc &bd = blocks[b];
+    const uint8_t *base = bd.data;
+    const uint64_t readable = bd.readable;
+    const uint32_t *off = offsets + (size_t)b * cap_blk;
+    uint32_t *db = digests + (size_t)b * cap_blk * HW;
+    const int l = lane_id();
+    int kbP, cntP, kbQ, cntQ;
+    uint32_t SP, EP, SQ, EQ;
+    auto reserve = [&](int &kb, int &cnt, uint32_t &S, uint32_t &E) {
+        uint32_t got = 0;
+        if (l == 0) got = atomicAdd(queue + b, 64u);
+        kb = (int)rdfirst(got);
+        cnt = max(0, min(64, n - kb));
+        const int k = kb + l;
+        E = l < cnt ? ld4(off + k) : 0u;
+        S = (l < cnt && k > 0) ? ld4(off + k - 1) : 0u;
+    };
+    reserve(kbP, cntP, SP, EP);
+    reserve(kbQ, cntQ, SQ, EQ);
+    int head = 0;
+    ShaChain A, B;
+    set_iv<HW>(A.st);
+    set_iv<HW>(B.st);
+    auto offer = [&](ShaChain &c) {               // hand chunks of the pool to the lanes whose chain c is idle
+        for (;;) {
+            const unsigned long long idle = ballot64(!c.active);
+            if (!idle) break;
+            if (head >= cntP) {
+                if (cntQ == 0) break;
+                kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
+                reserve(kbQ, cntQ, SQ, EQ);
+            }
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
+            const int avail = cntP - head;
+            const int idx = min(head + rank, 63);
+            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
+            bool skip = false;
+            if (ballot64(!c.active && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
+            if (!c.active && rank < avail && e - c0 >= thr) {
+                skip = true;
+            } else if (!c.active && rank < avail) {
+                c.k = kbP + head + rank;
+                c.s0 = c0;
+                c.len = e - c0;
+                c.T = c.len >> 6;
+                c.nb = (c.len + 8) / 64 + 1;
+                c.bi = 0;
+                set_iv<HW>(c.st);
+                c.active = true;
+            }
+            const int nidle = __popcll(idle);
+            head += min(nidle, avail);
+            if (!ballot64(skip) && nidle <= avail) break;
+        }
+    };
+    for (;;) {
+        if (A.active && A.bi == A.nb) { store_digest<HW>(db + (size_t)A.k * HW, A.st); A.active = false; }
+        if (B.active && B.bi == B.nb) { store_digest<HW>(db + (size_t)B.k * HW, B.st); B.active = false; }
+        offer(A);
+        offer(B);
+        if (!ballot64(A.active || B.active)) break;
+        const bool twoA = A.active && pair_at(A.bi, A.T), twoB = B.active && pair_at(B.bi, B.T);
+        const uint32_t posA = A.s0 + 64u * A.bi, posB = B.s0 + 64u * B.bi;
+        uint32_t dA[33], dB[33];
+        if (A.active) load_win(base, readable, posA, twoA, dA);
+        if (B.active) load_win(base, readable, posB, twoB, dB);
+        const uint32_t selA = 0x00010203u + (posA & 3u) * 0x01010101u, selB = 0x00010203u + (posB & 3u) * 0x01010101u;
+        uint32_t ma[16], mb[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            ma[i] = __builtin_amdgcn_perm(dA[i + 1], dA[i], selA);
+            mb[i] = __builtin_amdgcn_perm(dB[i + 1], dB[i], selB);
+        }
+        if (ballot64(A.active && A.bi >= A.T)) pad_block(ma, A.len, A.bi, A.nb);
+        if (ballot64(B.active && B.bi >= B.T)) pad_block(mb, B.len, B.bi, B.nb);
+        compress_both<HW>(A, ma, A.active, B, mb, B.active);
+        if (ballot64(twoA || twoB)) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                ma[i] = __builtin_amdgcn_perm(dA[i + 17], dA[i + 16], selA);
+                mb[i] = __builtin_amdgcn_perm(dB[i + 17], dB[i + 16], selB);
+            }
+            if (ballot64(twoA && A.bi + 1 == A.T)) pad_block(ma, A.len, A.bi + 1, A.nb);
+            if (ballot64(twoB && B.bi + 1 == B.T)) pad_block(mb, B.len, B.bi + 1, B.nb);
+            compress_both<HW>(A, ma, twoA, B, mb, twoB);
+        }
+        if (A.active) A.bi += twoA ? 2u : 1u;
+        if (B.active) B.bi += twoB ? 2u : 1u;
+    }
+}
+
 // sha_ring: the same lanes, but no 128-B line is fetched twice.  A lane's pair window (132 B from
 // a 4-aligned start) spans the absolute 128-B line L holding its start and line L + 1.  The lane keeps
 // line L in an LDS slot of its own; each iteration loads line L + 1 whole (8 x 16 B, aligned), reads
@@ -561,17 +749,24 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     static const bool ring = [] { const char *e = getenv("HDRF_SHA_RING"); return e ? atoi(e) != 0 : false; }();
     // HDRF_SHA_LINE: 1 = sha_line (each line fetched once, window by a register barrel shift)
     static const bool line = [] { const char *e = getenv("HDRF_SHA_LINE"); return e ? atoi(e) != 0 : false; }();
+    // HDRF_SHA_DUAL: 1 = sha_dual (two interleaved chains per lane; its default grid is 4 waves per CU)
+    static const bool dual = [] { const char *e = getenv("HDRF_SHA_DUAL"); return e ? atoi(e) != 0 : false; }();
     // HDRF_SHA_WPC: waves per CU over the chip's 256 CUs (overrides HDRF_SHA_WAVES x 4)
     static const int per_cu = [] {
         const char *c = getenv("HDRF_SHA_WPC");
         if (c) return atoi(c);
         const char *e = getenv("HDRF_SHA_WAVES");
-        return 4 * (e ? atoi(e) : 2);
+        const char *d = getenv("HDRF_SHA_DUAL");
+        return 4 * (e ? atoi(e) : (d && atoi(d) ? 1 : 2));
     }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
-    if (line && hasher == 0)
+    if (dual && hasher == 0)
+        hipLaunchKernelGGL(sha_dual_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (dual)
+        hipLaunchKernelGGL(sha_dual_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (line && hasher == 0)
         hipLaunchKernelGGL((sha_ring_kernel<5, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (line)
         hipLaunchKernelGGL((sha_ring_kernel<7, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
