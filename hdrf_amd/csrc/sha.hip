@@ -426,7 +426,7 @@ __device__ __forceinline__ void compress_both(ShaChain &A, uint32_t ma[16], bool
     if (HW == 5) sha1_compress2(na, ma, nb, mb);
     else sha256_compress2(na, ma, nb, mb);
 #pragma unroll
-    for (int i = 0; i < HW; i++) {
+    for (int i = 0; i < (HW == 5 ? 5 : 8); i++) {           // SHA-224 keeps all 8 state words
         A.st[i] = useA ? na[i] : A.st[i];
         B.st[i] = useB ? nb[i] : B.st[i];
     }
