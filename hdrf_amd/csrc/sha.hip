@@ -409,10 +409,13 @@ __device__ __forceinline__ void sha256_compress2(uint32_t sa[8], uint32_t wa[16]
 }
 
 struct ShaChain {
-    bool active = false;
+    bool active = false;         // a chunk in progress (its window for this iteration is in d)
     int k = 0;
     uint32_t s0 = 0, len = 0, T = 0, nb = 0, bi = 0;
     uint32_t st[8];
+    bool has_next = false;       // the chunk this chain takes when the current one ends (pre-assigned)
+    int nk = 0;
+    uint32_t ns0 = 0, nlen = 0;
 };
 
 // the two compressions of one slot of both chains; a chain's state changes only where `use`
@@ -432,6 +435,9 @@ __device__ __forceinline__ void compress_both(ShaChain &A, uint32_t ma[16], bool
     }
 }
 
+// The windows are loaded one iteration ahead: before an iteration computes, every lane issues the load
+// of the window its chain needs next (the next pair of the current chunk, or the first pair of the
+// chunk pre-assigned to follow it), so the loads are in flight under the four compressions.
 template <int HW>
 __global__ void __launch_bounds__(256) sha_dual_kernel(const BlockDesc *__restrict__ blocks,
                                                        const uint32_t *__restrict__ offsets,
@@ -469,49 +475,73 @@ __global__ void __launch_bounds__(256) sha_dual_kernel(const BlockDesc *__restri
     ShaChain A, B;
     set_iv<HW>(A.st);
     set_iv<HW>(B.st);
-    auto offer = [&](ShaChain &c) {               // hand chunks of the pool to the lanes whose chain c is idle
+    // pre-assign a next chunk to the lanes of chain c with `want` (long chunks go to the long lanes)
+    auto offer = [&](ShaChain &c, bool want) {
         for (;;) {
-            const unsigned long long idle = ballot64(!c.active);
+            const unsigned long long idle = ballot64(want && !c.has_next);
             if (!idle) break;
             if (head >= cntP) {
                 if (cntQ == 0) break;
                 kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
                 reserve(kbQ, cntQ, SQ, EQ);
             }
+            const bool me = want && !c.has_next;
             const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
             const int avail = cntP - head;
             const int idx = min(head + rank, 63);
             const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
             bool skip = false;
-            if (ballot64(!c.active && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
-            if (!c.active && rank < avail && e - c0 >= thr) {
+            if (ballot64(me && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
+            if (me && rank < avail && e - c0 >= thr) {
                 skip = true;
-            } else if (!c.active && rank < avail) {
-                c.k = kbP + head + rank;
-                c.s0 = c0;
-                c.len = e - c0;
-                c.T = c.len >> 6;
-                c.nb = (c.len + 8) / 64 + 1;
-                c.bi = 0;
-                set_iv<HW>(c.st);
-                c.active = true;
+            } else if (me && rank < avail) {
+                c.nk = kbP + head + rank;
+                c.ns0 = c0;
+                c.nlen = e - c0;
+                c.has_next = true;
             }
             const int nidle = __popcll(idle);
             head += min(nidle, avail);
             if (!ballot64(skip) && nidle <= avail) break;
         }
     };
+    auto take_next = [&](ShaChain &c) {           // the pre-assigned chunk becomes the current one
+        if (!c.active && c.has_next) {
+            c.k = c.nk; c.s0 = c.ns0; c.len = c.nlen;
+            c.T = c.len >> 6; c.nb = (c.len + 8) / 64 + 1; c.bi = 0;
+            set_iv<HW>(c.st);
+            c.active = true;
+            c.has_next = false;
+        }
+    };
+    uint32_t dA[33], dB[33];
+    // prologue: first chunks and their windows
+    offer(A, true);
+    offer(B, true);
+    take_next(A);
+    take_next(B);
+    if (A.active) load_win(base, readable, A.s0, pair_at(0, A.T), dA);
+    if (B.active) load_win(base, readable, B.s0, pair_at(0, B.T), dB);
     for (;;) {
-        if (A.active && A.bi == A.nb) { store_digest<HW>(db + (size_t)A.k * HW, A.st); A.active = false; }
-        if (B.active && B.bi == B.nb) { store_digest<HW>(db + (size_t)B.k * HW, B.st); B.active = false; }
-        offer(A);
-        offer(B);
         if (!ballot64(A.active || B.active)) break;
         const bool twoA = A.active && pair_at(A.bi, A.T), twoB = B.active && pair_at(B.bi, B.T);
+        const uint32_t stepA = twoA ? 2u : 1u, stepB = twoB ? 2u : 1u;
+        const bool endA = !A.active || A.bi + stepA >= A.nb, endB = !B.active || B.bi + stepB >= B.nb;
+        offer(A, endA);                           // the chunk after the current one, before it ends
+        offer(B, endB);
+        // next windows (in flight under this iteration's compressions)
+        uint32_t xA[33], xB[33];
+        {
+            const bool goA = A.active && !endA, nxA = endA && A.has_next;
+            const uint32_t pA = goA ? A.s0 + 64u * (A.bi + stepA) : A.ns0;
+            const bool tA = goA ? pair_at(A.bi + stepA, A.T) : pair_at(0, A.nlen >> 6);
+            if (goA || nxA) load_win(base, readable, pA, tA, xA);
+            const bool goB = B.active && !endB, nxB = endB && B.has_next;
+            const uint32_t pB = goB ? B.s0 + 64u * (B.bi + stepB) : B.ns0;
+            const bool tB = goB ? pair_at(B.bi + stepB, B.T) : pair_at(0, B.nlen >> 6);
+            if (goB || nxB) load_win(base, readable, pB, tB, xB);
+        }
         const uint32_t posA = A.s0 + 64u * A.bi, posB = B.s0 + 64u * B.bi;
-        uint32_t dA[33], dB[33];
-        if (A.active) load_win(base, readable, posA, twoA, dA);
-        if (B.active) load_win(base, readable, posB, twoB, dB);
         const uint32_t selA = 0x00010203u + (posA & 3u) * 0x01010101u, selB = 0x00010203u + (posB & 3u) * 0x01010101u;
         uint32_t ma[16], mb[16];
 #pragma unroll
@@ -532,8 +562,18 @@ __global__ void __launch_bounds__(256) sha_dual_kernel(const BlockDesc *__restri
             if (ballot64(twoB && B.bi + 1 == B.T)) pad_block(mb, B.len, B.bi + 1, B.nb);
             compress_both<HW>(A, ma, twoA, B, mb, twoB);
         }
-        if (A.active) A.bi += twoA ? 2u : 1u;
-        if (B.active) B.bi += twoB ? 2u : 1u;
+        if (A.active) {
+            A.bi += stepA;
+            if (A.bi >= A.nb) { store_digest<HW>(db + (size_t)A.k * HW, A.st); A.active = false; }
+        }
+        if (B.active) {
+            B.bi += stepB;
+            if (B.bi >= B.nb) { store_digest<HW>(db + (size_t)B.k * HW, B.st); B.active = false; }
+        }
+        take_next(A);
+        take_next(B);
+#pragma unroll
+        for (int i = 0; i < 33; i++) { dA[i] = xA[i]; dB[i] = xB[i]; }
     }
 }
 
