@@ -501,6 +501,60 @@ __global__ void __launch_bounds__(256) gmax_kernel(const BlockDesc *__restrict__
     }
 }
 
+// gmax16 without the bias pass: the signed maximum of the 16 bytes from packed signed 16-bit maxima
+// (a 16-bit signed compare orders by its high byte first, so the high byte of a v_pk_max_i16 result is
+// the signed maximum of the high bytes), odd bytes from the raw words, even bytes from the words
+// shifted up by 8; then the biased byte.  15 VALU per granule instead of ~27.
+typedef short ss2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ ss2 as_ss2(uint32_t x) { return __builtin_bit_cast(ss2, x); }
+__device__ __forceinline__ uint32_t gmax16_s(uint4 v)
+{
+    const ss2 o = __builtin_elementwise_max(__builtin_elementwise_max(as_ss2(v.x), as_ss2(v.y)),
+                                            __builtin_elementwise_max(as_ss2(v.z), as_ss2(v.w)));
+    const ss2 e = __builtin_elementwise_max(__builtin_elementwise_max(as_ss2(v.x << 8), as_ss2(v.y << 8)),
+                                            __builtin_elementwise_max(as_ss2(v.z << 8), as_ss2(v.w << 8)));
+    const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(o, e));
+    const int hi = (int)t >> 24, lo = (int)(t << 16) >> 24;       // sign-extended high bytes of both halves
+    return (uint32_t)(max(hi, lo) + 128);                         // biased: signed order == unsigned order
+}
+
+// 1a'. the same pass, 15 VALU per granule, and the 16 granule bytes of a thread (256 apart) staged
+// through LDS so each thread writes one 16-B word of consecutive maxima (1 store instead of 16).
+template <bool NT>
+__global__ void __launch_bounds__(256) gmax2_kernel(const BlockDesc *__restrict__ blocks, uint8_t *__restrict__ gm,
+                                                    int gstride, int prio)
+{
+    if (prio) __builtin_amdgcn_s_setprio(2);
+    __shared__ __attribute__((aligned(16))) uint8_t s_g[kGmPerWg];
+    const BlockDesc bd = blocks[blockIdx.y];
+    const int64_t ngran = (int64_t)((bd.len + 15) >> 4);
+    const int64_t g0 = (int64_t)blockIdx.x * kGmPerWg;
+    if (g0 >= ngran) return;
+    const uint8_t *base = bd.data;
+    uint8_t *out = gm + (size_t)blockIdx.y * gstride;
+    const int t = threadIdx.x;
+    uint4 v[16];
+    if ((g0 + kGmPerWg) * 16 <= (int64_t)bd.readable) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = ld16_t<NT>(base + (g0 + 256 * i + t) * 16);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int64_t g = g0 + 256 * i + t;
+            v[i] = g < ngran ? load16_guard(base, g * 16, (int64_t)bd.readable) : make_uint4(0, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) s_g[256 * i + t] = (uint8_t)gmax16_s(v[i]);
+    __syncthreads();
+    const int64_t gw = g0 + 16 * t;                               // this thread's 16 consecutive granules
+    if (gw + 16 <= ngran) {
+        *(uint4 *)(out + gw) = *(const uint4 *)&s_g[16 * t];    // gstride and g0 + 16 t: 16-B aligned
+    } else {
+        for (int j = 0; j < 16 && gw + j < ngran; j++) out[gw + j] = s_g[16 * t + j];
+    }
+}
+
 // 1b. lane walk (the speculative pass).  Every block is cut into segments of seg_len bytes (a
 //     multiple of 702); lane l of a wave walks the chain from the start of segment k = 63*wl + l as
 //     if a cut were there, one CHUNK per loop iteration, in VALU, from the granule maxima:
@@ -976,7 +1030,7 @@ __global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__res
     __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes of the window (ascending)
     __shared__ uint32_t s_nv[kStitchNodes];  // status: bit 31 jump (jmp in bits 0..23, jj in 24..29), bit 30 end
     __shared__ uint32_t s_sum[256];
-    __shared__ int s_go, s_cur;
+    __shared__ int s_go;
     const int b = blockIdx.x, t = threadIdx.x;
     const BlockDesc bd = blocks[b];
     const int nseg = bd.nseg, s0 = bd.seg0;
@@ -1274,7 +1328,13 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     // all SHA lanes (sha.hip), bit 4 the granule pass, bit 5 place (store.hip))
     const int prio = setprio_mask();
     const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
-    if (stream_knobs() & 1)
+    // HDRF_GMAX_V: 2 (default) gmax2 (15 VALU per granule, one 16-B store per thread), 1 the round-2 pass
+    static const int gver = [] { const char *e = getenv("HDRF_GMAX_V"); return e ? atoi(e) : 2; }();
+    if (gver == 2 && (stream_knobs() & 1))
+        hipLaunchKernelGGL(gmax2_kernel<true>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride, (prio >> 4) & 1);
+    else if (gver == 2)
+        hipLaunchKernelGGL(gmax2_kernel<false>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride, (prio >> 4) & 1);
+    else if (stream_knobs() & 1)
         hipLaunchKernelGGL(gmax_kernel<true>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride, (prio >> 4) & 1);
     else
         hipLaunchKernelGGL(gmax_kernel<false>, dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, sg, d_blocks, X.gm, X.gstride, (prio >> 4) & 1);
