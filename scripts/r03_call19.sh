@@ -6,3 +6,4 @@ HDRF_SHA_DUAL=1 timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --time
 tail -1 gpurun_out/c19_tests.log
 NO_PMC=1 TAG=dual2 bash scripts/r03_ab.sh HDRF_SHA_DUAL=1 HDRF_SHA_DUAL=0 HDRF_SHA_DUAL=1 HDRF_SHA_DUAL=0 "HDRF_SHA_DUAL=1 HDRF_SHA_WPC=6" "HDRF_SHA_DUAL=1 HDRF_SHA_WPC=8"
 bash scripts/r03_call18.sh
+NO_PMC=1 TAG=gv bash scripts/r03_ab.sh HDRF_GMAX_V=2 HDRF_GMAX_V=1 HDRF_GMAX_V=2 HDRF_GMAX_V=1
