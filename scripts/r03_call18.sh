@@ -4,7 +4,7 @@
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; mkdir -p gpurun_out
 i=0
-for v in "HDRF_SETPRIO=0" "HDRF_SETPRIO=12" "HDRF_SETPRIO=8" "HDRF_LZ4_WAVES=14" "HDRF_SHA_DUAL=1" "HDRF_SETPRIO=0"; do
+for v in "HDRF_SETPRIO=0" "HDRF_SETPRIO=12" "HDRF_LZ4_WAVES=14" "HDRF_SHA_DUAL=1"; do
   i=$((i+1))
   env $v timeout -k 10 600 python -u bench.py --workload config4 --steps 2 --warmup 1 --no-cpu > gpurun_out/c18_$i.json.log 2>&1 || { echo "variant $v failed"; tail -20 gpurun_out/c18_$i.json.log; exit 1; }
   tail -1 gpurun_out/c18_$i.json.log | python3 -c "
