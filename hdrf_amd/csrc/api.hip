@@ -66,6 +66,7 @@ struct Slot {
     BlockState *d_bst = nullptr;
     uint32_t *d_off = nullptr, *d_dig = nullptr, *d_slot = nullptr, *d_pre = nullptr;
     uint8_t *d_flags = nullptr;
+    uint8_t *d_dcnt = nullptr;                // designated chunks: blocks of the batch holding the digest
     uint32_t *d_tilesum = nullptr, *d_tilepre = nullptr;
     uint64_t *d_store = nullptr;
     RangeState *d_rstate = nullptr;
@@ -93,7 +94,8 @@ struct Slot {
     bool pending = false;
     uint32_t close_bound = 0;                 // durable containers: closes this batch may make per range
     uint32_t lz_bound = 0;                    // compressor 2: closes this batch may make per range (LZ4 lag)
-    hipEvent_t placed = nullptr;              // compressor 2: the batch's place kernel finished (stream B)
+    hipEvent_t placed = nullptr;              // compressor 2: the batch's place kernel finished (stream B2)
+    hipEvent_t idx_done = nullptr;            // index stage (claim .. finalize) of the batch done (stream B)
     hipEvent_t lz_done = nullptr;             // compressor 2: its closed containers are Lz4Codec files
     int rx_release = -1;                      // packet path: receive buffer to free when the batch completes
     uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
@@ -113,7 +115,8 @@ struct hdrf_ctx {
     hdrf_cfg cfg{};
     int H = 20, HW = 5;
     hipStream_t st = nullptr;    // stream A: SHA stage (also every synchronous helper)
-    hipStream_t stB = nullptr;   // stream B: back stage (index + store)
+    hipStream_t stB = nullptr;   // stream B: back stage, index part (and the node-global phases)
+    hipStream_t stB2 = nullptr;  // stream B2: back stage, store part (scan, flush, place, read-back)
     hipStream_t stW = nullptr;   // stream W: chunking stage
     hipStream_t stG = nullptr;   // stream G: the granule-max pass (HDRF_GMAX_STREAM), ahead of W
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
@@ -302,7 +305,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
 static void free_slot(Slot &S)
 {
     void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_slot,
-                   S.d_pre, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
+                   S.d_pre, S.d_flags, S.d_dcnt, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
                    S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err,
                    S.d_lzwork};
     for (void *p : dev)
@@ -311,7 +314,7 @@ static void free_slot(Slot &S)
     for (void *p : host)
         if (p) (void)hipHostFree(p);
     hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done, S.placed, S.lz_done,
-                        S.gmax_done};
+                        S.gmax_done, S.idx_done};
     if (S.d_rjobs) (void)hipFree(S.d_rjobs);
     if (S.h_rjobs) (void)hipHostFree(S.h_rjobs);
     if (S.d_hstage) (void)hipFree(S.d_hstage);
@@ -339,6 +342,7 @@ static void free_all(hdrf_ctx *ctx)
         if (p) (void)hipFree(p);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
+    if (ctx->stB2) (void)hipStreamDestroy(ctx->stB2);
     if (ctx->stW) (void)hipStreamDestroy(ctx->stW);
     if (ctx->stG) (void)hipStreamDestroy(ctx->stG);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
@@ -379,7 +383,7 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
         (rc = dalloc(ctx, &S.d_off, nchunk)) || (rc = dalloc(ctx, &S.d_dig, nchunk * ctx->HW)) ||
         (rc = dalloc(ctx, &S.d_slot, nchunk)) ||
-        (rc = dalloc(ctx, &S.d_pre, nchunk)) || (rc = dalloc(ctx, &S.d_flags, nchunk)) ||
+        (rc = dalloc(ctx, &S.d_pre, nchunk)) || (rc = dalloc(ctx, &S.d_flags, nchunk)) || (rc = dalloc(ctx, &S.d_dcnt, nchunk)) ||
         (rc = dalloc(ctx, &S.d_tilesum, (size_t)B * ctx->ntiles)) ||
         (rc = dalloc(ctx, &S.d_tilepre, (size_t)B * ctx->ntiles)) || (rc = dalloc(ctx, &S.d_store, B)) ||
         (rc = dalloc(ctx, &S.d_rstate, (size_t)B * 4)) || (rc = dalloc(ctx, &S.d_ev, (size_t)3 * ctx->ev_cap)) ||
@@ -404,7 +408,8 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         hipEventCreateWithFlags(&S.back_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.placed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.lz_done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&S.gmax_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&S.gmax_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.idx_done, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
     for (auto &e : S.evW)
         if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
@@ -430,6 +435,7 @@ static int drain(hdrf_ctx *ctx)
     HIPCK(hipStreamSynchronize(ctx->stW));
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
+    HIPCK(hipStreamSynchronize(ctx->stB2));
     return rc;
 }
 
@@ -508,6 +514,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     if (hipSetDevice(c.device) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->st, hipStreamNonBlocking, pa) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stB, hipStreamNonBlocking, pb) != hipSuccess ||
+        hipStreamCreateWithPriority(&ctx->stB2, hipStreamNonBlocking, pb) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stW, hipStreamNonBlocking, pw) != hipSuccess ||
         hipStreamCreateWithPriority(&ctx->stG, hipStreamNonBlocking, pw) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
@@ -777,14 +784,25 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
                      &ma));
     ma.mark(A);
     HIPCK(hipEventRecord(S.front_done, A));
-    // ---- back: in block order on stream B
+    // ---- back, index part, in block order on stream B: claim .. decide, then idx_finalize takes the
+    // batch-local state out of the index (designated chunks, block counts, entries cleared), so the
+    // next batch's index part may run while this batch is stored on stream B2
     HIPCK(hipStreamWaitEvent(Bst, S.front_done, 0));
-    HIPCK(hipMemsetAsync(S.d_nclosed, 0, sizeof(uint32_t), Bst));
     Marker mb;
     mb.ev = ctx->timing ? S.evB : nullptr;
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_tab, c.index_log2, cur,
                        tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap, S.d_flags, S.d_tilesum, ctx->ntiles,
                        S.d_err, Bst, &mb));
+    HIPCK(launch_index_finalize(S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, ctx->d_tab, S.d_slot, S.d_flags, S.d_dcnt,
+                                Bst));
+    if (ctx->timing) HIPCK(hipEventRecord(S.evB[9], Bst));
+    HIPCK(hipEventRecord(S.idx_done, Bst));
+    // ---- back, store part, in block order on stream B2 (scans, flush walk, place, read-back)
+    // HDRF_SPLIT_B=0: the store part on stream B too (A/B of the split)
+    static const bool split_b = [] { const char *e = getenv("HDRF_SPLIT_B"); return !e || atoi(e) != 0; }();
+    hipStream_t B2 = split_b ? ctx->stB2 : Bst;
+    HIPCK(hipStreamWaitEvent(B2, S.idx_done, 0));
+    HIPCK(hipMemsetAsync(S.d_nclosed, 0, sizeof(uint32_t), B2));
     StoreParams P = store_params(ctx, nblocks);
     // When batches are pipelined (one already in flight), this batch's place kernel overlaps the
     // next batch's front stage (the critical path): a dynamic-LDS reservation caps place at one
@@ -812,16 +830,16 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         for (uint64_t j = ctx->nsub - 1; j + 1 > ctx->nwait; j--) {   // in flight, newest first
             const Slot &Pj = ctx->sl[j % kSlots];
             sum += Pj.lz_bound;
-            if (sum + 1 >= per) HIPCK(hipStreamWaitEvent(Bst, Pj.lz_done, 0));
+            if (sum + 1 >= per) HIPCK(hipStreamWaitEvent(B2, Pj.lz_done, 0));
             if (j == 0) break;
         }
     }
     HIPCK(launch_store(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store, S.d_pre,
                        ctx->d_alloc, S.d_rstate, S.d_ev, S.d_closed, S.d_nclosed, S.d_slot, ctx->d_tab, ctx->d_arena,
-                       S.d_pcid, S.d_ppos, S.d_err, Bst, &mb));
+                       S.d_pcid, S.d_ppos, S.d_err, B2, &mb, nullptr, S.d_dcnt));
     if (c.compressor == 2) {    // compression stage: closed containers -> Lz4Codec files (:770-779)
         hipStream_t L = ctx->stL[cur & 1];
-        HIPCK(hipEventRecord(S.placed, Bst));
+        HIPCK(hipEventRecord(S.placed, B2));
         HIPCK(hipStreamWaitEvent(L, S.placed, 0));
         HIPCK(launch_lz4(S.d_closed, S.d_nclosed, ctx->closed_cap, c.container_max, ctx->d_arena, ctx->d_carena,
                          ctx->cslot, S.d_segclen, S.d_filelen, S.d_lzwork, L));
@@ -829,16 +847,16 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         HIPCK(hipMemcpyAsync(S.h_filelen, S.d_filelen, sizeof(uint32_t) * ctx->closed_cap, hipMemcpyDeviceToHost, L));
         HIPCK(hipEventRecord(S.lz_done, L));
     } else {
-        mb.mark(Bst);
+        mb.mark(B2);
     }
-    HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nblocks, hipMemcpyDeviceToHost, Bst));
-    HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nblocks, hipMemcpyDeviceToHost, Bst));
-    HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, Bst));
-    HIPCK(hipMemcpyAsync(S.h_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, Bst));
-    HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, Bst));
-    HIPCK(hipMemcpyAsync(S.h_long, S.d_queue + 64, sizeof(uint32_t), hipMemcpyDeviceToHost, Bst));
-    HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, Bst));
-    HIPCK(hipEventRecord(S.back_done, Bst));
+    HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nblocks, hipMemcpyDeviceToHost, B2));
+    HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nblocks, hipMemcpyDeviceToHost, B2));
+    HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, B2));
+    HIPCK(hipMemcpyAsync(S.h_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, B2));
+    HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, B2));
+    HIPCK(hipMemcpyAsync(S.h_long, S.d_queue + 64, sizeof(uint32_t), hipMemcpyDeviceToHost, B2));
+    HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, B2));
+    HIPCK(hipEventRecord(S.back_done, B2));
     S.pending = true;
     ctx->nsub++;
     return 0;
@@ -890,7 +908,8 @@ static int complete_slot(hdrf_ctx *ctx, int si, bool timed)
         ctx->stage_ms[11] += elapsed(S.evW[0], S.evW[1]);
         for (int i = 0; i < 2; i++) ctx->stage_ms[i] += elapsed(S.evW[i + 1], S.evW[i + 2]);
         for (int i = 0; i < 2; i++) ctx->stage_ms[2 + i] += elapsed(S.evA[i], S.evA[i + 1]);
-        for (int i = 0; i < 6; i++) ctx->stage_ms[4 + i] += elapsed(S.evB[i], S.evB[i + 1]);
+        // (evB[9]: the end of the index part on stream B; evB[3..]: the store part on stream B2)
+        for (int i = 0; i < 6; i++) ctx->stage_ms[4 + i] += elapsed(S.evB[i], i == 2 ? S.evB[9] : S.evB[i + 1]);
         ctx->stage_ms[10] += elapsed(S.evB[7], S.evB[8]);
     }
     ctx->res = si;
@@ -2887,6 +2906,7 @@ extern "C" int hdrf_memcpy_d2h(hdrf_ctx *ctx, void *dst, const void *src, uint64
     if (!ctx) return HDRF_E_INVAL;
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
+    HIPCK(hipStreamSynchronize(ctx->stB2));
     HIPCK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return 0;
 }

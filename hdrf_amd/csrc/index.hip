@@ -233,6 +233,42 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
         tilesum[(size_t)b * ntiles + blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
 }
 
+// ---- finalize: the designated chunk of every touched entry, its block count, and the entry's
+// batch-local state cleared, right after decide (single-node contexts).  The store stage then needs
+// nothing batch-local from the index, so the next batch's claim / apply / decide (stream B) run while
+// this batch is placed (stream B2): place writes only the value fields, which the index kernels never
+// read.  flags bit 5 = designated; dcnt = popcount(mask) (blocks of the batch holding the digest).
+// The designated chunk (min block, last occurrence) is unique per entry, and the other chunks read
+// only `first` (to learn they are not designated: after the clear they read 0, which is no chunk's
+// k + 1), so its clear cannot change another chunk's answer.
+__global__ void __launch_bounds__(256) idx_finalize_kernel(const BlockState *__restrict__ bst, int cap_blk,
+                                                           IndexEntry *__restrict__ tab,
+                                                           const uint32_t *__restrict__ slot,
+                                                           uint8_t *__restrict__ flags, uint8_t *__restrict__ dcnt)
+{
+    const int b = blockIdx.y;
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= bst[b].n_chunks) return;
+    const size_t c = (size_t)b * cap_blk + k;
+    const uint8_t f = flags[c];
+    if (!(f & 2)) return;                              // not in the entry's min block
+    IndexEntry *e = tab + slot[c];
+    bool desig = true;
+    if (f & 16) desig = (uint32_t)e->first == (uint32_t)(k + 1);   // the min block repeats it: last occurrence
+    if (!desig) return;
+    dcnt[c] = (uint8_t)__popcll(e->mask);
+    flags[c] = f | 32;
+    e->mask = 0;
+    e->first = 0;
+}
+
+hipError_t launch_index_finalize(const BlockState *bst, int nblocks, int cap_blk, int ntiles, IndexEntry *tab,
+                                 const uint32_t *slot, uint8_t *flags, uint8_t *dcnt, hipStream_t st)
+{
+    hipLaunchKernelGGL(idx_finalize_kernel, dim3(ntiles, nblocks), dim3(256), 0, st, bst, cap_blk, tab, slot, flags, dcnt);
+    return hipGetLastError();
+}
+
 // A fresh DataNode (empty Redis): zero the table with 16-B streaming stores (rocclr's fill
 // reached ~1 TB/s on the 8.6 GB table) and seed the allocator, both on the stream that owns
 // the index, so the front half of the next batch overlaps the clear.

@@ -88,7 +88,7 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
                         uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
                         ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
                         uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk,
-                        const GxPlace *gx = nullptr);
+                        const GxPlace *gx = nullptr, const uint8_t *dcnt = nullptr);
 // flush only / place only (the node-global mode chains the flush walk across ranks)
 hipError_t launch_store_scan(const StoreParams &P, const BlockState *bst, const uint32_t *offsets, const uint8_t *flags,
                              const uint32_t *tilesum, uint32_t *tilepre, uint64_t *store_size, uint32_t *pre,
@@ -103,7 +103,10 @@ hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, c
                               const uint32_t *offsets, const uint8_t *flags, const uint32_t *pre,
                               const RangeState *rstate, const FlushEv *events, const uint32_t *slot, IndexEntry *tab,
                               uint8_t *arena, uint32_t *place_cid, uint32_t *place_pos, const GxPlace &gx,
-                              hipStream_t st);
+                              hipStream_t st, const uint8_t *dcnt = nullptr);
+// designated chunk, its block count and the cleared batch-local entry state, after decide (index.hip)
+hipError_t launch_index_finalize(const BlockState *bst, int nblocks, int cap_blk, int ntiles, IndexEntry *tab,
+                                 const uint32_t *slot, uint8_t *flags, uint8_t *dcnt, hipStream_t st);
 hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int cap_blk, int ntiles,
                           const uint32_t *digests, IndexEntry *scratch, const uint32_t *slot, const uint8_t *flags,
                           uint32_t gbase, int G, uint32_t *x1, int64_t cap, unsigned long long *counts, int *err,

@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
                                                     const FlushEv *__restrict__ events, const uint32_t *__restrict__ slot,
                                                     IndexEntry *__restrict__ tab, uint8_t *__restrict__ arena,
                                                     uint32_t *__restrict__ place_cid, uint32_t *__restrict__ place_pos,
-                                                    GxPlace gx, int prio)
+                                                    GxPlace gx, int prio, const uint8_t *__restrict__ dcnt)
 {
     if (prio) __builtin_amdgcn_s_setprio(2);        // HDRF_SETPRIO bit 5
     const int b = blockIdx.y;
@@ -376,7 +376,8 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
         }
         bool desig = (f & 2) != 0;                         // in the entry's min block ...
         IndexEntry *e = tab + slot[c];
-        if (desig && (f & 16))                             // ... and its last occurrence there
+        if (dcnt) desig = (f & 32) != 0;                   // (idx_finalize already decided and cleared)
+        else if (desig && (f & 16))                        // ... and its last occurrence there
             desig = (uint32_t)e->first == (uint32_t)(k + 1);
         if (desig && gx.x3) {                              // node-global index (gx.hip): the
             if (f & 4) {                                   // owner commits the new entry's location
@@ -388,16 +389,17 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
                 rec[1] = cid; rec[2] = pos; rec[3] = pos + ((f & 1) && do_copy ? len : 0u);
             }
         } else if (desig) {                                // designated: final index value
-            const unsigned long long m = e->mask;
-            const uint32_t cnt = (uint32_t)__popcll(m);
+            const uint32_t cnt = dcnt ? (uint32_t)dcnt[c] : (uint32_t)__popcll(e->mask);
             if (f & 4) {
                 e->ncopy = cnt & 0xffu;
                 e->cid = cid; e->start = pos; e->stop = pos + ((f & 1) && do_copy ? len : 0u);
             } else {
                 e->ncopy = (e->ncopy + cnt) & 0xffu;
             }
-            e->mask = 0;
-            e->first = 0;
+            if (!dcnt) {
+                e->mask = 0;
+                e->first = 0;
+            }
         }
     }
     // ---- runs: consecutive new chunks of this tile that are contiguous in one container are
@@ -477,18 +479,18 @@ hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, c
                               const uint32_t *offsets, const uint8_t *flags, const uint32_t *pre,
                               const RangeState *rstate, const FlushEv *events, const uint32_t *slot, IndexEntry *tab,
                               uint8_t *arena, uint32_t *place_cid, uint32_t *place_pos, const GxPlace &gx,
-                              hipStream_t st)
+                              hipStream_t st, const uint8_t *dcnt)
 {
     if (gx.x3)
         if (hipError_t e = hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st)) return e;
     if (stream_knobs() & 2)
         hipLaunchKernelGGL(place_kernel<true>, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst,
                            offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx,
-                           (setprio_mask() >> 5) & 1);
+                           (setprio_mask() >> 5) & 1, dcnt);
     else
         hipLaunchKernelGGL(place_kernel<false>, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst,
                            offsets, flags, pre, rstate, events, slot, tab, arena, place_cid, place_pos, gx,
-                           (setprio_mask() >> 5) & 1);
+                           (setprio_mask() >> 5) & 1, dcnt);
     return hipGetLastError();
 }
 
@@ -497,7 +499,7 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
                         uint64_t *store_size, uint32_t *pre, AllocState *alloc, RangeState *rstate, FlushEv *events,
                         ClosedRec *closed, uint32_t *nclosed, const uint32_t *slot, IndexEntry *tab, uint8_t *arena,
                         uint32_t *place_cid, uint32_t *place_pos, int *err, hipStream_t st, Marker *mk,
-                        const GxPlace *gx)
+                        const GxPlace *gx, const uint8_t *dcnt)
 {
     const GxPlace gxp = gx ? *gx : GxPlace{};
     mk->mark(st);
@@ -507,7 +509,7 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
     mk->mark(st);
     if (e == hipSuccess)
         e = launch_store_place(P, d_blocks, bst, offsets, flags, pre, rstate, events, slot, tab, arena, place_cid,
-                               place_pos, gxp, st);
+                               place_pos, gxp, st, dcnt);
     mk->mark(st);
     mk->mark(st);   // spare stage (kept so stage indices stay stable)
     return e;
