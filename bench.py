@@ -152,10 +152,10 @@ def main():
         # batches in flight (<= 2 x new bytes / maxSize + 1 per block and storer range, three 32-block
         # batches) could reach an undrained slot, so its rings hold ~500 slots each (64 GiB of 288)
         a.arena_slots = {"config4": 1792, "config5": 2048}.get(a.workload, 512)
-    if a.workload == "config4":
-        # two LZ4 streams beside the four of the batch pipeline: hardware queues for all six (HIP's
-        # default is 4, and streams sharing a queue serialise); read when HIP initialises
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # the batch pipeline uses five streams (chunking, SHA, index, store, recipe copies) and config 4
+    # two more LZ4 streams: hardware queues for all of them (HIP's default is 4, and streams sharing
+    # a queue serialise); read when HIP initialises
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
