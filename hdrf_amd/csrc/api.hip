@@ -1764,8 +1764,23 @@ extern "C" int hdrf_host_free(hdrf_ctx *ctx, void *p)
 
 extern "C" int hdrf_wait_batch(hdrf_ctx *ctx)
 {
-    HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
+    // Block on the oldest batch's completion events WITHOUT the context lock, so receiver threads
+    // (hdrf_rx_begin, hdrf_submit_slot) and drains are not stalled behind a GPU wait; wait_one then
+    // finds the events complete.  (Should the slot be waited and reused meanwhile, its events
+    // belong to a newer batch: this only waits longer.)
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    {
+        HDRF_LOCK(ctx);
+        if (ctx->nwait < ctx->nsub) {
+            const Slot &S = ctx->sl[(int)(ctx->nwait % kSlots)];
+            ev[0] = S.back_done;
+            if (ctx->cfg.compressor == 2) ev[1] = S.lz_done;
+        }
+    }
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventSynchronize(e);           // errors are reported by wait_one below
+    HDRF_LOCK(ctx);
     return wait_one(ctx);
 }
 

@@ -115,12 +115,12 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         // takes its attempt words from a forward window (Sw at sb) when the batch fits in it, and a
         // match found by the search loads one window pair 64 bytes before the match that serves
         // the catch-up, the literals (<= 64 bytes) and the first extension step at once.
-        auto wload = [&](int at) -> uint32_t {        // guarded lane word at src + at + 4l (branch-free)
-            const int q = at + 4 * l;
-            const int qc = q < 0 ? 0 : (q + 4 > n ? max(n - 4, 0) : q);
-            const uint32_t raw = rd32u(src + qc);
-            return (q >= 0 && q + 4 <= n) ? raw : (q < 0 && q > -4) ? raw << (8 * (-q)) : 0u;   // straddle: real bytes
-        };
+        // lane word at src + at + 4l, for at >= 0 (every caller: the fast catch-up below takes its
+        // windows only when both start at or after byte 0).  A lane reaching past byte n - 4 reads
+        // the last word instead; no such lane's bytes are ever used (every use is bounded by
+        // mflimit / matchlimit, at least 5 bytes before n), so one clamp replaces the guards.
+        const int nm4 = n - 4;
+        auto wload = [&](int at) -> uint32_t { return rd32u(src + min(at + 4 * l, nm4)); };
         auto lane_word = [&](uint32_t w, int o) -> uint32_t {   // bytes [o, o + 4) of a window
             const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((o >> 2) << 2, (int)w);
             const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) + 1) << 2, (int)w);
@@ -198,7 +198,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 int mref = (int)rdlane((uint32_t)ref, istar);
                 int tpos;
                 uint32_t tok;
-                bool fast = ip - anchor <= 64;
+                bool fast = ip - anchor <= 64 && ip >= 64 && mref >= 64;
                 if (fast) {
                     // one window pair at ip - 64: catch-up, literals and the first extension step
                     const int wb0 = ip - 64, d0 = mref - ip;
@@ -264,10 +264,13 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     else { wb = hwb; l0 = (ip + 4 - hwb) >> 2; }
                     anchor = ip + 4;
                     for (;;) {                             // match extension
-                        const int p = wb + 4 * l;
                         uint32_t x = Fw ^ Rw;
-                        bool stop = p + 4 > matchlimit;
-                        if (stop) x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
+                        bool stop = false;
+                        if (wb + 256 > matchlimit) {       // (uniform) the window reaches matchlimit
+                            const int p = wb + 4 * l;
+                            stop = p + 4 > matchlimit;
+                            if (stop) x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
+                        }
                         if (l < l0) { x = 0u; stop = false; }
                         const unsigned long long mm = ballot64(x != 0u || stop);
                         if (!mm) { wb += 256; l0 = 0; Fw = wload(wb); Rw = wload(wb + dr); continue; }
@@ -299,12 +302,16 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     const int o2 = ip - 2 - wb;
                     uint32_t v2, v0;
                     if (o2 >= 0 && ((o2 + 2) >> 2) + 1 <= 63) {
+                        // three lanes of the window into scalar registers, the two words by 64-bit
+                        // scalar shifts (the hashes below stay scalar too: no VALU round trip)
                         const int a2 = o2 >> 2, a0 = (o2 + 2) >> 2;
-                        v2 = __builtin_amdgcn_alignbyte(rdlane(Fw, a2 + 1), rdlane(Fw, a2), (uint32_t)(o2 & 3));
-                        v0 = __builtin_amdgcn_alignbyte(rdlane(Fw, a0 + 1), rdlane(Fw, a0), (uint32_t)((o2 + 2) & 3));
+                        const uint64_t pA = ((uint64_t)rdlane(Fw, a2 + 1) << 32) | rdlane(Fw, a2);
+                        const uint64_t pB = a0 == a2 ? pA : ((uint64_t)rdlane(Fw, a0 + 1) << 32) | (pA >> 32);
+                        v2 = (uint32_t)(pA >> (8 * (o2 & 3)));
+                        v0 = (uint32_t)(pB >> (8 * ((o2 + 2) & 3)));
                     } else {
-                        v2 = rd32u(src + ip - 2);
-                        v0 = rd32u(src + ip);
+                        v2 = rdfirst(rd32u(src + ip - 2));
+                        v0 = rdfirst(rd32u(src + ip));
                     }
                     // table: [h2] = ip - 2, r = [h0], [h0] = ip.  Distinct hashes: lanes 0 and 1
                     // do the two slots in one pass; equal hashes: r is ip - 2.
@@ -378,12 +385,13 @@ last_literals:
 // SHA and chunking kernels get a slot per SIMD while this pass runs, so the next pass is ready
 // when this one drains (otherwise SHA waited for the pass's waves to retire: one pass at a time).
 template <bool kSmall>
-__global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed,
-                                                     const uint32_t *__restrict__ nclosed, const uint8_t *__restrict__ arena,
-                                                     uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
-                                                     uint32_t *__restrict__ seg_clen, int nseg_max, uint32_t *__restrict__ work)
+__device__ __forceinline__ void lz4_seg_body(const ClosedRec *__restrict__ closed,
+                                             const uint32_t *__restrict__ nclosed, const uint8_t *__restrict__ arena,
+                                             uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
+                                             uint32_t *__restrict__ seg_clen, int nseg_max, uint32_t *__restrict__ work,
+                                             uint8_t *tabmem, int prio)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t tabmem[kSmall ? kLzTabU16 : kLzTabU32];
+    if (prio) __builtin_amdgcn_s_setprio(3);                 // HDRF_SETPRIO bit 6
     const uint32_t nc = *nclosed;
     const uint32_t per = kSmall ? 1u : (uint32_t)nseg_max;
     const uint32_t total = nc * per;
@@ -406,6 +414,28 @@ __global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict
         __builtin_amdgcn_s_waitcnt(0);                        // the table is reused by the next item
         asm volatile("" ::: "memory");
     }
+}
+
+template <bool kSmall>
+__global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict__ closed,
+                                                     const uint32_t *__restrict__ nclosed, const uint8_t *__restrict__ arena,
+                                                     uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
+                                                     uint32_t *__restrict__ seg_clen, int nseg_max, uint32_t *__restrict__ work,
+                                                     int prio)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t tabmem[kSmall ? kLzTabU16 : kLzTabU32];
+    lz4_seg_body<kSmall>(closed, nclosed, arena, cmax, carena, cslot, seg_clen, nseg_max, work, tabmem, prio);
+}
+
+// The byU32 pass held to 96 VGPRs (5 waves per SIMD; 101 unconstrained, no spills either way), so a
+// SIMD holding four of its waves keeps 128 registers for one sha_chunk_vc wave (HDRF_VCAP).
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
+lz4_seg_vc_kernel(const ClosedRec *__restrict__ closed, const uint32_t *__restrict__ nclosed,
+                  const uint8_t *__restrict__ arena, uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
+                  uint32_t *__restrict__ seg_clen, int nseg_max, uint32_t *__restrict__ work, int prio)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t tabmem[kLzTabU32];
+    lz4_seg_body<false>(closed, nclosed, arena, cmax, carena, cslot, seg_clen, nseg_max, work, tabmem, prio);
 }
 
 // grid nclosed x 256 threads: frame the segments in place, [BE32 len] ([BE32 clen] block)* [BE32 0].
@@ -644,10 +674,15 @@ hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int clos
     static const int wpc = [] { const char *e = getenv("HDRF_LZ4_WAVES"); const int v = e ? atoi(e) : 16; return v > 0 ? v : 16; }();
     const int nseg_max = (int)((cmax + kLzMaxIn - 1) / kLzMaxIn);
     if (hipError_t e = hipMemsetAsync(work, 0, 2 * sizeof(uint32_t), st)) return e;
+    const int prio = (setprio_mask() >> 6) & 1;
     hipLaunchKernelGGL(lz4_seg_kernel<true>, dim3(std::min(closed_cap, 4 * ncu)), dim3(64), 0, st, closed, nclosed,
-                       arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work);
-    hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(std::min(closed_cap * nseg_max, wpc * ncu)), dim3(64), 0, st, closed,
-                       nclosed, arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work + 1);
+                       arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work, prio);
+    if (vcap_mode() & 1)                                   // HDRF_VCAP bit 0
+        hipLaunchKernelGGL(lz4_seg_vc_kernel, dim3(std::min(closed_cap * nseg_max, wpc * ncu)), dim3(64), 0, st, closed,
+                           nclosed, arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work + 1, prio);
+    else
+        hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(std::min(closed_cap * nseg_max, wpc * ncu)), dim3(64), 0, st, closed,
+                           nclosed, arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work + 1, prio);
     hipLaunchKernelGGL(lz4_pack_kernel, dim3(closed_cap), dim3(256), 0, st, closed, nclosed, carena, cslot, seg_clen,
                        nseg_max, file_len);
     return hipGetLastError();

@@ -271,11 +271,11 @@ __device__ __forceinline__ void sha_long_lanes(const BlockDesc *__restrict__ blo
 // with the next reservation Q fetched while P is consumed), so a lane that finishes its chain takes
 // the next chunk with two ds_bpermutes and no memory round trip.
 template <int HW>
-__global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restrict__ blocks,
-                                                        const uint32_t *__restrict__ offsets,
-                                                        const BlockState *__restrict__ bst, int cap_blk,
-                                                        uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                        uint32_t thr, int prio)
+__device__ __forceinline__ void sha_chunk_body(const BlockDesc *__restrict__ blocks,
+                                               const uint32_t *__restrict__ offsets,
+                                               const BlockState *__restrict__ bst, int cap_blk,
+                                               uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                               uint32_t thr, int prio)
 {
     if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
         sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr, prio & 1);
@@ -347,6 +347,28 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
         if (!ballot64(active)) break;
         if (active) sha_iter<HW>(base, readable, s0, len, T, nb, bi, st);
     }
+}
+
+template <int HW>
+__global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restrict__ blocks,
+                                                        const uint32_t *__restrict__ offsets,
+                                                        const BlockState *__restrict__ bst, int cap_blk,
+                                                        uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                                        uint32_t thr, int prio)
+{
+    sha_chunk_body<HW>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
+}
+
+// The same kernel held to 128 VGPRs (4 waves per SIMD), so one SHA wave fits on a SIMD beside four
+// LZ4 waves of lz4_seg_vc_kernel (96 VGPRs): 4 x 96 + 128 = 512, the SIMD's register file.  Without
+// the caps (133 + 4 x 104) a SIMD running four LZ4 waves has no room for SHA at all (config 4).
+template <int HW>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+sha_chunk_vc_kernel(const BlockDesc *__restrict__ blocks, const uint32_t *__restrict__ offsets,
+                    const BlockState *__restrict__ bst, int cap_blk, uint32_t *__restrict__ digests,
+                    uint32_t *__restrict__ queue, uint32_t thr, int prio)
+{
+    sha_chunk_body<HW>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
 }
 
 // sha_dual: every lane runs TWO independent chunk chains (A and B, both fed from the wave's pool) and
@@ -800,6 +822,8 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
         return 4 * (e ? atoi(e) : (d && atoi(d) ? 1 : 2));
     }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
+    // HDRF_VCAP bit 1: the register-capped SHA kernel (sha_chunk_vc)
+    const bool vcap = (vcap_mode() & 2) != 0;
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
     if (dual && hasher == 0)
@@ -814,6 +838,10 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
         hipLaunchKernelGGL((sha_ring_kernel<5, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (ring)
         hipLaunchKernelGGL((sha_ring_kernel<7, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (vcap && hasher == 0)
+        hipLaunchKernelGGL(sha_chunk_vc_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (vcap)
+        hipLaunchKernelGGL(sha_chunk_vc_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (hasher == 0)
         hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else

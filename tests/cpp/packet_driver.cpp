@@ -8,8 +8,9 @@
 // (:1258-1261).  Here T receiver threads each own one block at a time and call
 // hdrf_append_packet once per packet from pinned host memory; the main thread opens receive
 // buffers (hdrf_rx_begin) in block order, submits the received blocks in that order
-// (hdrf_submit_slot: the FIFO) and completes them (hdrf_wait_batch), draining the durable
-// containers after every completed block (hdrf_drain_containers, as hdrf_jni.c does).
+// (hdrf_submit_slot: the FIFO); a completer thread completes them (hdrf_wait_batch, which blocks
+// without the context lock) and drains the durable containers after every completed block
+// (hdrf_drain_containers, as hdrf_jni.c does) while the receivers take the next blocks.
 //
 // usage: packet_driver BLOCKS BLOCK_MIB PACKET_KIB THREADS STEPS [OUT_FILE]
 //   The corpus is BASELINE config 2's (1 MiB segments, 50 % cross-block duplicates, seed
@@ -18,10 +19,12 @@
 //   the last step (the parity test compares them with the oracle).
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -116,6 +119,10 @@ int main(int argc, char **argv)
         }
     };
     const bool no_drain = std::getenv("HDRF_DRIVER_NODRAIN") != nullptr;      // A/B only
+    // HDRF_DRIVER_SERIAL (A/B only): the main thread completes and drains between receive rounds
+    // (round-3 c1 shape); default: a completer thread does it while the receivers run, as the
+    // reference's reducer/storer runs apart from the DataXceiver threads.
+    const bool serial = std::getenv("HDRF_DRIVER_SERIAL") != nullptr;
     auto complete = [&]() {
         CK(hdrf_wait_batch(ctx));
         CK(hdrf_batch_info(ctx, 0, &n_chunks[(size_t)done], &store[(size_t)done]));
@@ -128,11 +135,42 @@ int main(int argc, char **argv)
         CK(hdrf_reset(ctx));
         done = 0;
         drained_bytes = 0;
+        std::mutex mu;
+        std::condition_variable cv;
+        int64_t submitted = 0, completed = 0;      // guarded by mu
+        std::thread completer;
+        if (!serial)
+            completer = std::thread([&]() {
+                for (int64_t c = 0; c < nb; c++) {
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return submitted > c; });
+                    }
+                    complete();
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        completed = c + 1;
+                    }
+                    cv.notify_all();
+                }
+            });
+        auto in_flight = [&]() { std::lock_guard<std::mutex> lk(mu); return submitted - completed; };
+        auto wait_until = [&](int64_t max_in_flight) {          // completer frees slots / buffers
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return submitted - completed <= max_in_flight; });
+        };
         const auto t0 = std::chrono::steady_clock::now();
-        int pend = 0;
         for (int64_t g = 0; g < nb; g += T) {
             const int k = (int)std::min<int64_t>(T, nb - g);
-            while (pend + k > kRx || pend >= kDepth) { complete(); pend--; }
+            if (serial) {
+                while (in_flight() + k > kRx || in_flight() >= kDepth) {
+                    complete();
+                    std::lock_guard<std::mutex> lk(mu);
+                    completed++;
+                }
+            } else {
+                wait_until(kRx - k);
+            }
             std::vector<int32_t> rx((size_t)k);
             for (int i = 0; i < k; i++) CK(hdrf_rx_begin(ctx, (uint64_t)(g + i), &rx[(size_t)i]));
             std::vector<std::thread> th;
@@ -149,12 +187,31 @@ int main(int argc, char **argv)
                 return 1;
             }
             for (int i = 0; i < k; i++) {
-                if (pend >= kDepth) { complete(); pend--; }
+                if (serial) {
+                    if (in_flight() >= kDepth) {
+                        complete();
+                        std::lock_guard<std::mutex> lk(mu);
+                        completed++;
+                    }
+                } else {
+                    wait_until(kDepth - 1);
+                }
                 CK(hdrf_submit_slot(ctx, rx[(size_t)i]));
-                pend++;
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    submitted++;
+                }
+                cv.notify_all();
             }
         }
-        while (pend) { complete(); pend--; }
+        if (serial)
+            while (in_flight()) {
+                complete();
+                std::lock_guard<std::mutex> lk(mu);
+                completed++;
+            }
+        else
+            completer.join();
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (step > 0) {
             total_s += s;
