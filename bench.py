@@ -35,25 +35,34 @@ VALU_PEAK_WI_NS = 1033.0       # v_add_u32 wave-instructions/ns, chip-wide (tool
 KERNEL_OF = {"gmax(gmax_kernel)": "gmax_kernel", "walk(lane_walk_kernel)": "lane_walk_kernel",
              "sha(sha_chunk_kernel)": "sha_ring_kernel" if os.environ.get("HDRF_SHA_RING", "0") not in ("", "0")
              else "sha_chunk_kernel", "place(place_kernel)": "place_kernel"}
-# stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index + store,
-# L the LZ4 pass of closed containers (compressor 2; two LZ4 streams alternating by batch)
+# stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index (claim ..
+# finalize), B2 store (scans, flush, place; on stream B itself with HDRF_SPLIT_B=0), L the LZ4 pass
+# of closed containers (compressor 2; two LZ4 streams alternating by batch)
+_INDEX = ["index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)", "index_slow_decide(idx_slow/decide)"]
+_STORE = ["scan(tile/chunk_scan)", "flush(flush_kernel)", "place(place_kernel)"]
 CHAINS = {"W: chunking": ["gmax(gmax_kernel)", "walk(lane_walk_kernel)", "stitch(repair/path/count/scan/copy/fallback)"],
-          "A: SHA": ["sha(sha_chunk_kernel)", "sha_tail(none: padding inside the sha kernel)"],
-          "B: index+store": ["index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
-                             "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
-                             "place(place_kernel)"],
-          "L: LZ4": ["compress(lz4_seg/lz4_pack)"]}
+          "A: SHA": ["sha(sha_chunk_kernel)", "sha_tail(none: padding inside the sha kernel)"]}
+if os.environ.get("HDRF_SPLIT_B", "1") not in ("", "0"):
+    CHAINS.update({"B: index": _INDEX, "B2: store": _STORE})
+else:
+    CHAINS["B: index+store"] = _INDEX + _STORE
+CHAINS["L: LZ4"] = ["compress(lz4_seg/lz4_pack)"]
 SHA_MIX_CEILING_WI_NS = 425.0  # tools/sha_peak.hip: the SHA-1 instruction mix on register-resident data
 
 
-def load_pmc():
-    """Per-launch PMC figures of the newest committed rocprofv3 pass (scripts/pmc.sh ->
-    scripts/traffic.py -> profiles/*_traffic.json), measured on this same workload."""
+def load_pmc(want):
+    """Per-launch PMC figures of the newest committed rocprofv3 pass (scripts/r02_traffic.sh ->
+    scripts/traffic.py -> profiles/*_traffic.json) taken on this same workload (`want`: the
+    workload's `_config` keys; a file without "workload" was taken on config 2)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))   # names sort by round, version
-    if not files:
-        return {}, None
-    return json.load(open(files[-1])), os.path.relpath(files[-1], ROOT)
+    for f in reversed(files):
+        d = json.load(open(f))
+        cfg = dict(d.get("_config", {}))
+        cfg.setdefault("workload", "config2")
+        if all(cfg.get(k) == v for k, v in want.items()):
+            return d, os.path.relpath(f, ROOT)
+    return {}, None
 
 
 def parse():
@@ -375,10 +384,8 @@ def main():
         if name in per_launch and avg[name] > 0:
             d["GB_s"] = round(per_launch[name] / (avg[name] * 1e-3) / 1e9, 1)
         stages[name] = d
-    pmc, pmc_src = load_pmc()
-    want = {"blocks": nb, "block_mib": a.block_mib, "batch": B, "n_gpus": world, "hasher": a.hasher}
-    if any(pmc.get("_config", {}).get(k) != v for k, v in want.items()):
-        pmc, pmc_src = {}, None                        # profiled on another workload: not this one's traffic
+    pmc, pmc_src = load_pmc({"blocks": nb, "block_mib": a.block_mib, "batch": B, "n_gpus": world,
+                             "hasher": a.hasher, "workload": a.workload})
     sha_k = KERNEL_OF[STAGES[2]] + ("<5>" if a.hasher == 0 else "<7>")
 
     def hbm_entry(name):
@@ -423,11 +430,15 @@ def main():
         ach = lz_bytes / (lz_ms * 1e-3) / 1e9 if lz_ms > 0 else 0.0
         lz4 = {"bound": "hbm", "kernel": "lz4_seg_kernel", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(lz_ms, 4),
-               "algorithmic_bytes_per_launch": int(lz_bytes), "traffic": None,
-               "limiter": "per-sequence dependent instruction chain of the greedy parse (one wave per 261,100-B "
-                          "segment, LDS table caps 17 waves/CU); profiles/r02_lz4_phases.txt"}
+               "algorithmic_bytes_per_launch": int(lz_bytes),
+               "traffic": pmc.get("lz4_seg_kernel<false>", {}).get("hbm_bytes_per_launch"),
+               "limiter": "latency of the greedy parse's per-sequence chain (one wave per 261,100-B segment; "
+                          "101 VGPRs allow 4 waves/SIMD, the 9 KiB LDS table 17/CU; half of wave time at s_waitcnt "
+                          "on the candidate load and table round trips); profiles/r02_lz4_phases.txt, "
+                          "profiles/r03_c4_v1_pmc.txt"}
     # the line's roofline: the dominant kernel of the critical chain
-    top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place, "L: LZ4": lz4}[crit]
+    top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place, "B2: store": place,
+           "B: index": place, "L: LZ4": lz4}[crit]
     roofline = dict(top)
     roofline.update({"traffic_source": pmc_src, "critical_path": crit, "chains_ms_per_batch": chains,
                      "batch_period_ms": round(el / a.steps / nbatch * 1e3, 4),
