@@ -13,7 +13,7 @@ tail -1 gpurun_out/r03_tests_$V.log
 TAG=r03_prof_$V BENCH="--steps 2 --warmup 1 --no-cpu --no-alone" bash scripts/r02_prof.sh > gpurun_out/r03_prof_$V.txt 2>&1 || { tail -20 gpurun_out/r03_prof_$V.txt; exit 1; }
 head -12 gpurun_out/r03_prof_$V.txt | cut -c1-160
 TAG=r03_$V EXTRA_GROUPS="SQ_INSTS_VALU" bash scripts/r02_traffic.sh > gpurun_out/r03_traffic_$V.txt 2>&1 || { tail -20 gpurun_out/r03_traffic_$V.txt; exit 1; }
-cp gpurun_out/r03_${V}_traffic.json profiles/r03_${V}_traffic.json
+cp gpurun_out/r03_${V}_traffic.json profiles/r03_v${V}_traffic.json   # sorts after r03_v2 (bench takes the newest name)
 timeout -k 10 600 python -u bench.py > gpurun_out/r03_bench_$V.json.log 2>&1 || { tail -20 gpurun_out/r03_bench_$V.json.log; exit 1; }
 tail -1 gpurun_out/r03_bench_$V.json.log | cut -c1-300
 fi
