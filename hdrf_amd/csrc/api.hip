@@ -195,7 +195,7 @@ struct hdrf_ctx {
     bool lost = false;
     // packet-granular receive (hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot): device
     // receive buffers, and a pinned chunk ring the packets are copied into before their H2D
-    static constexpr int kRx = 8;
+    static constexpr int kRx = 16;
     static constexpr uint64_t kRingChunk = 4ull << 20;
     // one receive buffer per block being received: device copy of the block, and two pinned 4 MiB
     // staging chunks of its own, so receivers of different blocks (one DataXceiver thread each)
@@ -211,6 +211,7 @@ struct hdrf_ctx {
         std::atomic<int> state{0};              // 0 free 1 receiving 2 submitted
     };
     Rx rx[kRx];
+    bool rx_used = false;                       // a packet receive was opened (drain engine choice)
     // timing
     bool timing = false;
     double stage_ms[kStages] = {};
@@ -1049,6 +1050,7 @@ extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
         r.dst = 0;
         r.id = block_id;
         r.state.store(1);
+        ctx->rx_used = true;                       // packet mode: drains on the copy engine
         *rx = i;
         return 0;
     }
@@ -2639,10 +2641,14 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
         if ((int64_t)it->second.len > done) todo.push_back(Pend{id, 0, done, (int64_t)it->second.len - done, it->second});
     }
     // pinned (device-mapped) output: the CUs write it (xfer_kernel), beside the SDMA H2D of later
-    // blocks; pageable output: hipMemcpyAsync.  HDRF_DRAIN_KERNEL=0 forces the copy engine.
-    static const bool kern_env = [] { const char *e = getenv("HDRF_DRAIN_KERNEL"); return !e || atoi(e) != 0; }();
+    // batches (whole blocks through hdrf_submit_host: 38.8 / 39.1 vs 34.7 / 35.5 GB/s with the copy
+    // engine); once the context receives packets (hdrf_rx_begin), the copy engine (22.0 vs 28.3 GB/s
+    // for 64 KiB packets, profiles/r03_c5_drain_ab.txt); pageable output: hipMemcpyAsync.
+    // HDRF_DRAIN_KERNEL=1 / 0 forces the CUs / the copy engine.
+    static const int kern_env = [] { const char *e = getenv("HDRF_DRAIN_KERNEL"); return e ? (atoi(e) != 0) : -1; }();
+    const bool kern = kern_env >= 0 ? kern_env != 0 : !ctx->rx_used;
     hipPointerAttribute_t pa;
-    const bool mapped = kern_env && out_cap > 0 && hipPointerGetAttributes(&pa, out) == hipSuccess &&
+    const bool mapped = kern && out_cap > 0 && hipPointerGetAttributes(&pa, out) == hipSuccess &&
                         pa.type == hipMemoryTypeHost && pa.devicePointer != nullptr;
     (void)hipGetLastError();
     if (mapped && ctx->xfer_cap == 0) {

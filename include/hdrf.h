@@ -119,7 +119,8 @@ int hdrf_wait_batch(hdrf_ctx *ctx);
 int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_data, const uint64_t *len,
                      const uint64_t *block_ids);
 /* Packet-granular receive (DN/BlockReceiver.java:877-896, 1258-1261): hdrf_rx_begin reserves one of
- * 8 device receive buffers for a block; hdrf_append_packet copies each packet as it arrives into the
+ * 16 device receive buffers for a block (blocks received concurrently, as a DataNode runs one
+ * DataXceiver per block being written); hdrf_append_packet copies each packet as it arrives into the
  * buffer's own pair of pinned 4 MiB staging chunks (the packet may be reused when the call returns)
  * and sends every full chunk H2D on a side stream, overlapped with the next packets and with the
  * blocks in flight.  The packets of one receive buffer come from one thread at a time (the block's
@@ -128,7 +129,7 @@ int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_
  * hdrf_submit_slot submits the received block as a one-block batch with no copy left (pair it
  * with hdrf_wait_batch like hdrf_submit_batch; HDRF_E_CAPACITY when the pipeline is full).  The
  * buffer is free again when that batch completes; hdrf_rx_begin returns HDRF_E_CAPACITY while all
- * eight are in use.  hdrf_rx_cancel gives back a buffer whose block is abandoned (the client was
+ * sixteen are in use.  hdrf_rx_cancel gives back a buffer whose block is abandoned (the client was
  * lost mid-block; the reference drops bf1): its receiver must have stopped appending.  A packet
  * that would take the block past max_block_bytes is refused (HDRF_E_INVAL) and copies nothing.
  * hdrf_reset refuses (HDRF_E_INVAL) while a buffer is receiving; hdrf_close requires every

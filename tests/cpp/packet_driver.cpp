@@ -78,7 +78,7 @@ int main(int argc, char **argv)
     const int steps = std::atoi(argv[5]);
     const char *out_file = argc > 6 ? argv[6] : nullptr;
     const int64_t seg = 1 << 20, spb = S / seg;
-    if (nb < 1 || S < seg || P < 1 || T < 1 || T > 8 || steps < 1) return 2;
+    if (nb < 1 || S < seg || P < 1 || T < 1 || T > 16 || steps < 1) return 2;
 
     hdrf_ctx *ctx = nullptr;
     hdrf_cfg cfg;
@@ -129,7 +129,7 @@ int main(int argc, char **argv)
         done++;
         if (!no_drain) drain();
     };
-    const int kDepth = 5, kRx = 8;                 // HDRF_PIPELINE_DEPTH, receive buffers
+    const int kDepth = 5, kRx = 16;                // HDRF_PIPELINE_DEPTH, receive buffers (hdrf.h)
     double best = 0, total_s = 0;
     for (int step = 0; step <= steps; step++) {    // step 0: warm-up
         CK(hdrf_reset(ctx));

@@ -373,16 +373,16 @@ def test_packet_receivers_race_submit_and_wait():
 
 
 def test_packet_receive_cancel_overflow_and_reset_guard():
-    """hdrf_rx_cancel gives back an abandoned receive buffer (more than the 8 buffers are abandoned,
+    """hdrf_rx_cancel gives back an abandoned receive buffer (more than the 16 buffers are abandoned,
     some with staging chunks still copying); a packet that would pass max_block_bytes -- including a
     length that wraps a 64-bit sum -- is refused without copying; hdrf_reset refuses while a block is
     being received.  A block received afterwards reduces exactly."""
     ctx = Context(container_max=1 << 20, max_block_bytes=12 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64)
     ora = Oracle(max_size=1 << 20)
     junk = prng_bytes(5, 9 << 20)
-    for k in range(11):                                        # > 8 abandoned receives
+    for k in range(19):                                        # > 16 abandoned receives
         rx = ctx.rx_begin(7000 + k)
-        n = (k + 1) * (800 << 10)                              # up to 8.6 MiB: staging chunks flushed
+        n = (k % 11 + 1) * (800 << 10)                         # up to 8.6 MiB: staging chunks flushed
         ctx.append_packet(rx, junk.ctypes.data, n)
         if k == 0:
             with pytest.raises(HdrfError):
