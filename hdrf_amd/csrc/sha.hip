@@ -149,6 +149,25 @@ __device__ __forceinline__ void load_win(const uint8_t *base, uint64_t readable,
     }
 }
 
+// sha_carry: the 65 dwords (260 B) of four blocks at pos (4-aligned down); the second pair's half
+// is carried in registers to the lane's next iteration.
+__device__ __forceinline__ void load_win65(const uint8_t *base, uint64_t readable, uint32_t pos, uint32_t d[65])
+{
+    const uint32_t apos = pos & ~3u;
+    if ((uint64_t)apos + 260u <= readable) {
+        const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
+            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+        }
+        d[64] = p[64];
+    } else {
+#pragma unroll
+        for (int q = 0; q < 65; q++) d[q] = load4_guard(base, (int64_t)apos + 4 * q, (int64_t)readable);
+    }
+}
+
 __device__ __forceinline__ bool pair_at(uint32_t bi, uint32_t T) { return bi < T && ((T - bi) & 1u); }
 
 // The compressions of one iteration from a loaded window (see sha_iter).
@@ -270,7 +289,7 @@ __device__ __forceinline__ void sha_long_lanes(const BlockDesc *__restrict__ blo
 // Chunk offsets come from coalesced per-wave reservations of 64 chunks kept in registers (pool P,
 // with the next reservation Q fetched while P is consumed), so a lane that finishes its chain takes
 // the next chunk with two ds_bpermutes and no memory round trip.
-template <int HW>
+template <int HW, bool CARRY>
 __device__ __forceinline__ void sha_chunk_body(const BlockDesc *__restrict__ blocks,
                                                const uint32_t *__restrict__ offsets,
                                                const BlockState *__restrict__ bst, int cap_blk,
@@ -309,6 +328,8 @@ __device__ __forceinline__ void sha_chunk_body(const BlockDesc *__restrict__ blo
     uint32_t s0 = 0, len = 0, T = 0, nb = 0, bi = 0;
     uint32_t st[8];
     set_iv<HW>(st);
+    uint32_t dw[CARRY ? 65 : 1];                  // sha_carry: the lane's 4-block window
+    bool carry = false;                           // its second pair is the lane's next iteration
     for (;;) {
         if (active && bi == nb) {                 // chain done: the digest
             store_digest<HW>(db + (size_t)k * HW, st);
@@ -339,16 +360,39 @@ __device__ __forceinline__ void sha_chunk_body(const BlockDesc *__restrict__ blo
                 bi = 0;
                 set_iv<HW>(st);
                 active = true;
+                carry = false;
             }
             const int nidle = __popcll(idle);
             head += min(nidle, avail);
             if (!ballot64(skip) && nidle <= avail) break;
         }
         if (!ballot64(active)) break;
-        if (active) sha_iter<HW>(base, readable, s0, len, T, nb, bi, st);
+        if constexpr (CARRY) {
+            // Lanes alternate: load four blocks (260 B) and run the first pair, then run the second
+            // pair from registers (33 moves per four blocks).  Each 128-B line is then shared by two windows once per 256 B of
+            // chunk instead of once per 128 B (the 132-B window re-fetches it: 1.41x the bytes).
+            if (active) {
+                const bool two = pair_at(bi, T);
+                const uint32_t pos = s0 + 64u * bi;
+                if (carry) {
+#pragma unroll
+                    for (int i = 0; i < 33; i++) dw[i] = dw[i + 32];
+                } else {
+                    load_win65(base, readable, pos, dw);
+                }
+                sha_compute<HW>(dw, pos, len, T, nb, bi, two, st);
+                carry = !carry && two && bi + 2u < nb;
+                bi += two ? 2u : 1u;
+            }
+        } else {
+            if (active) sha_iter<HW>(base, readable, s0, len, T, nb, bi, st);
+        }
     }
 }
 
+// The default: 4-block windows with the second pair carried in registers (154 VGPRs; config 2
+// 1038.6 / 1034.6 / 1032.1 vs 1016.7 / 1013.8 / 1011.9 GB/s for the 132-B window per iteration,
+// SHA 2.55 vs 2.71 ms per batch in the pipeline, profiles/r03_sha_carry_ab.txt).
 template <int HW>
 __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restrict__ blocks,
                                                         const uint32_t *__restrict__ offsets,
@@ -356,7 +400,18 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
                                                         uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
                                                         uint32_t thr, int prio)
 {
-    sha_chunk_body<HW>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
+    sha_chunk_body<HW, true>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
+}
+
+// HDRF_SHA_CARRY=0: one 132-B window loaded per iteration (round 3 c1/c2 default), for A/B.
+template <int HW>
+__global__ void __launch_bounds__(256) sha_pair_kernel(const BlockDesc *__restrict__ blocks,
+                                                       const uint32_t *__restrict__ offsets,
+                                                       const BlockState *__restrict__ bst, int cap_blk,
+                                                       uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                                       uint32_t thr, int prio)
+{
+    sha_chunk_body<HW, false>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
 }
 
 // The same kernel held to 128 VGPRs (4 waves per SIMD), so one SHA wave fits on a SIMD beside four
@@ -368,7 +423,7 @@ sha_chunk_vc_kernel(const BlockDesc *__restrict__ blocks, const uint32_t *__rest
                     const BlockState *__restrict__ bst, int cap_blk, uint32_t *__restrict__ digests,
                     uint32_t *__restrict__ queue, uint32_t thr, int prio)
 {
-    sha_chunk_body<HW>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
+    sha_chunk_body<HW, false>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
 }
 
 // sha_dual: every lane runs TWO independent chunk chains (A and B, both fed from the wave's pool) and
@@ -822,6 +877,8 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
         return 4 * (e ? atoi(e) : (d && atoi(d) ? 1 : 2));
     }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
+    // HDRF_SHA_CARRY: 0 = sha_pair (a 132-B window per iteration; the default carries 4-block windows)
+    static const bool pairk = [] { const char *e = getenv("HDRF_SHA_CARRY"); return e && atoi(e) == 0; }();
     // HDRF_VCAP bit 1: the register-capped SHA kernel (sha_chunk_vc)
     const bool vcap = (vcap_mode() & 2) != 0;
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
@@ -838,6 +895,10 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
         hipLaunchKernelGGL((sha_ring_kernel<5, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (ring)
         hipLaunchKernelGGL((sha_ring_kernel<7, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (pairk && hasher == 0)
+        hipLaunchKernelGGL(sha_pair_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (pairk)
+        hipLaunchKernelGGL(sha_pair_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (vcap && hasher == 0)
         hipLaunchKernelGGL(sha_chunk_vc_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (vcap)
