@@ -815,6 +815,9 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     static const int place_lds_env = [] { const char *e = getenv("HDRF_PLACE_LDS"); return e ? atoi(e) : -1; }();
     const int place_lds = place_lds_env >= 0 ? place_lds_env : (c.compressor == 2 ? 16384 : 40960);
     if (ctx->nsub > ctx->nwait) P.place_lds = place_lds;
+    // HDRF_PLACE_DEEP=1: the place copy keeps four 16-B words per thread in flight instead of two
+    static const int place_deep_env = [] { const char *e = getenv("HDRF_PLACE_DEEP"); return e ? atoi(e) : 0; }();
+    P.place_deep = place_deep_env;
     if (c.compressor == 2) {
         // The compression of earlier batches runs on the LZ4 streams, off stream B, so batch k+1's
         // index and store overlap batch k's LZ4 and the LZ4 passes of consecutive batches overlap

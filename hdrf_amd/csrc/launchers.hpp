@@ -25,6 +25,7 @@ struct StoreParams {
     int ev_cap;                // flush events per range per batch
     int closed_cap;            // closed containers per batch
     int place_lds = 0;         // dynamic LDS per place workgroup (occupancy throttle, 0 = none)
+    int place_deep = 0;        // place copies 4 (1) or 2 (0) 16-B words per thread in flight (HDRF_PLACE_DEEP)
 };
 
 // chunking: granule maxima -> lane walk (total_waves waves over the batch's segments) -> repair ->

@@ -378,6 +378,9 @@ __device__ __forceinline__ void sha_chunk_body(const BlockDesc *__restrict__ blo
 #pragma unroll
                     for (int i = 0; i < 33; i++) dw[i] = dw[i + 32];
                 } else {
+                    // four blocks even when the chain has fewer left: a third branch loading only
+                    // 132 B for the last pair made the wave wait twice (SHA 2.55 -> 2.85 ms per
+                    // batch, profiles/r03_sha_carry_trim_ab.txt)
                     load_win65(base, readable, pos, dw);
                 }
                 sha_compute<HW>(dw, pos, len, T, nb, bi, two, st);
@@ -390,9 +393,6 @@ __device__ __forceinline__ void sha_chunk_body(const BlockDesc *__restrict__ blo
     }
 }
 
-// The default: 4-block windows with the second pair carried in registers (154 VGPRs; config 2
-// 1038.6 / 1034.6 / 1032.1 vs 1016.7 / 1013.8 / 1011.9 GB/s for the 132-B window per iteration,
-// SHA 2.55 vs 2.71 ms per batch in the pipeline, profiles/r03_sha_carry_ab.txt).
 template <int HW>
 __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restrict__ blocks,
                                                         const uint32_t *__restrict__ offsets,
@@ -400,18 +400,21 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
                                                         uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
                                                         uint32_t thr, int prio)
 {
-    sha_chunk_body<HW, true>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
+    sha_chunk_body<HW, false>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
 }
 
-// HDRF_SHA_CARRY=0: one 132-B window loaded per iteration (round 3 c1/c2 default), for A/B.
+// HDRF_SHA_CARRY=1: 4-block windows with the second pair carried in registers (154 VGPRs).  A/B on
+// two boxes: +2.0 % (1032-1039 vs 1012-1017 GB/s) and -0.5 % (1022-1027 vs 1026-1033): its extra
+// line fetches (7.0 vs 6.57 GB per batch) slow the granule pass as much as SHA gains
+// (profiles/r03_sha_carry_ab.txt, profiles/r03_sha_carry_ab2.txt); not the default.
 template <int HW>
-__global__ void __launch_bounds__(256) sha_pair_kernel(const BlockDesc *__restrict__ blocks,
-                                                       const uint32_t *__restrict__ offsets,
-                                                       const BlockState *__restrict__ bst, int cap_blk,
-                                                       uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                       uint32_t thr, int prio)
+__global__ void __launch_bounds__(256) sha_carry_kernel(const BlockDesc *__restrict__ blocks,
+                                                        const uint32_t *__restrict__ offsets,
+                                                        const BlockState *__restrict__ bst, int cap_blk,
+                                                        uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
+                                                        uint32_t thr, int prio)
 {
-    sha_chunk_body<HW, false>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
+    sha_chunk_body<HW, true>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
 }
 
 // The same kernel held to 128 VGPRs (4 waves per SIMD), so one SHA wave fits on a SIMD beside four
@@ -877,8 +880,8 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
         return 4 * (e ? atoi(e) : (d && atoi(d) ? 1 : 2));
     }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
-    // HDRF_SHA_CARRY: 0 = sha_pair (a 132-B window per iteration; the default carries 4-block windows)
-    static const bool pairk = [] { const char *e = getenv("HDRF_SHA_CARRY"); return e && atoi(e) == 0; }();
+    // HDRF_SHA_CARRY: 1 = sha_carry (4-block windows, the second pair carried in registers)
+    static const bool carryk = [] { const char *e = getenv("HDRF_SHA_CARRY"); return e && atoi(e) != 0; }();
     // HDRF_VCAP bit 1: the register-capped SHA kernel (sha_chunk_vc)
     const bool vcap = (vcap_mode() & 2) != 0;
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
@@ -895,10 +898,10 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
         hipLaunchKernelGGL((sha_ring_kernel<5, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (ring)
         hipLaunchKernelGGL((sha_ring_kernel<7, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (pairk && hasher == 0)
-        hipLaunchKernelGGL(sha_pair_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (pairk)
-        hipLaunchKernelGGL(sha_pair_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (carryk && hasher == 0)
+        hipLaunchKernelGGL(sha_carry_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
+    else if (carryk)
+        hipLaunchKernelGGL(sha_carry_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (vcap && hasher == 0)
         hipLaunchKernelGGL(sha_chunk_vc_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (vcap)

@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(256) fn_chain_kernel(StoreParams P, const uint
 
 // workgroup-cooperative copy of one contiguous run (16-B aligned destination stores)
 template <bool NT>
-__device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32_t len)
+__device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32_t len, bool deep = false)
 {
     const int t = threadIdx.x;
     uint32_t head = (uint32_t)((16 - ((uintptr_t)dst & 15)) & 15);
@@ -313,6 +313,17 @@ __device__ __forceinline__ void wg_copy(uint8_t *dst, const uint8_t *src, uint32
     const int sh = (int)((uintptr_t)sp & 15);
     const uint8_t *sa = sp - sh;
     uint32_t i = t;
+    if (deep)                                       // (uniform) four 16-B words per thread in flight
+        for (; i + 768 < n16; i += 1024) {
+            const uint4 v0 = load16_shift<NT>(sa + 16 * (size_t)i, sh);
+            const uint4 v1 = load16_shift<NT>(sa + 16 * (size_t)(i + 256), sh);
+            const uint4 v2 = load16_shift<NT>(sa + 16 * (size_t)(i + 512), sh);
+            const uint4 v3 = load16_shift<NT>(sa + 16 * (size_t)(i + 768), sh);
+            st16_t<NT>(d + 16 * (size_t)i, v0);
+            st16_t<NT>(d + 16 * (size_t)(i + 256), v1);
+            st16_t<NT>(d + 16 * (size_t)(i + 512), v2);
+            st16_t<NT>(d + 16 * (size_t)(i + 768), v3);
+        }
     for (; i + 256 < n16; i += 512) {               // two 16-B words per thread in flight
         const uint4 v0 = load16_shift<NT>(sa + 16 * (size_t)i, sh);
         const uint4 v1 = load16_shift<NT>(sa + 16 * (size_t)(i + 256), sh);
@@ -433,7 +444,7 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
     __syncthreads();
     for (uint32_t r = 0; r < nruns; r++) {
         const uint64_t dsto = ((uint64_t)r_dst_hi[r] << 32) | r_dst_lo[r];
-        wg_copy<NT>(arena + dsto, bd.data + r_src[r], r_end[r] - r_src[r]);
+        wg_copy<NT>(arena + dsto, bd.data + r_src[r], r_end[r] - r_src[r], P.place_deep != 0);
     }
 }
 

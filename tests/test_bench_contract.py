@@ -39,3 +39,12 @@ def test_traffic_is_matched_by_workload(monkeypatch):
     assert d2.get("_config", {}).get("workload", "config2") == "config2"
     assert "lz4_seg_kernel<false>" in d4 and "place_kernel<true>" in d2
     assert b.load_pmc(dict(WANT, workload="config5", blocks=128)) == ({}, None)
+
+
+def test_named_kernels_have_committed_traffic(monkeypatch):
+    """Every kernel the config-2 line names (its roofline entries) is in the newest config-2 traffic
+    file, so a renamed kernel cannot silently drop the line's `traffic`."""
+    b = _bench(monkeypatch)
+    d, _ = b.load_pmc(dict(WANT, workload="config2"))
+    for name, kern in b.KERNEL_OF.items():
+        assert any(kern + t in d for t in ("", "<5>", "<true>")), (name, kern)
