@@ -789,11 +789,13 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     // batch-local state out of the index (designated chunks, block counts, entries cleared), so the
     // next batch's index part may run while this batch is stored on stream B2
     HIPCK(hipStreamWaitEvent(Bst, S.front_done, 0));
+    // HDRF_DECIDE_DESIG=0 (A/B): idx_finalize reads every designated entry (round-3 c2 behaviour)
+    static const bool decide_desig = [] { const char *e = getenv("HDRF_DECIDE_DESIG"); return !e || atoi(e) != 0; }();
     Marker mb;
     mb.ev = ctx->timing ? S.evB : nullptr;
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_tab, c.index_log2, cur,
                        tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap, S.d_flags, S.d_tilesum, ctx->ntiles,
-                       S.d_err, Bst, &mb));
+                       S.d_err, Bst, &mb, decide_desig ? S.d_dcnt : nullptr));
     HIPCK(launch_index_finalize(S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, ctx->d_tab, S.d_slot, S.d_flags, S.d_dcnt,
                                 Bst));
     if (ctx->timing) HIPCK(hipEventRecord(S.evB[9], Bst));

@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
                                                          IndexEntry *__restrict__ tab,
                                                          const uint32_t *__restrict__ slot, uint32_t cur,
                                                          uint8_t *__restrict__ flags, uint32_t *__restrict__ tilesum,
-                                                         int ntiles)
+                                                         int ntiles, uint8_t *__restrict__ dcnt)
 {
     __shared__ uint32_t s_part[4];
     const int b = blockIdx.y;
@@ -218,7 +218,13 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
         const bool rep = b == minb && f != 0 && (63 - (int)(f >> 32)) == minb;
         if (rep) atomicMax(&e->first, ((unsigned long long)(63 - b) << 32) | (unsigned)(k + 1));
         // bit1: in the min block (designated unless it has repeats: resolved in place_kernel)
-        flags[c] = (uint8_t)((is_new ? 1 : 0) | (b == minb ? 2 : 0) | (created ? 4 : 0) | (rep ? 16 : 0));
+        // with dcnt (idx_finalize follows): a min-block chunk without repeats is the designated one
+        // already — its block count and flag 32 are written here, from the mask this kernel read,
+        // so idx_finalize only clears its entry (stores, no line fetch)
+        const bool desig_now = dcnt && b == minb && !rep;
+        if (desig_now) dcnt[c] = (uint8_t)__popcll(m);
+        flags[c] = (uint8_t)((is_new ? 1 : 0) | (b == minb ? 2 : 0) | (created ? 4 : 0) | (rep ? 16 : 0) |
+                             (desig_now ? 32 : 0));
         if (is_new) {
             const uint32_t *off = offsets + (size_t)b * cap_blk;
             newlen = off[k] - (k ? off[k - 1] : 0u);
@@ -253,13 +259,13 @@ __global__ void __launch_bounds__(256) idx_finalize_kernel(const BlockState *__r
     const uint8_t f = flags[c];
     if (!(f & 2)) return;                              // not in the entry's min block
     IndexEntry *e = tab + slot[c];
-    bool desig = true;
-    if (f & 16) desig = (uint32_t)e->first == (uint32_t)(k + 1);   // the min block repeats it: last occurrence
-    if (!desig) return;
-    dcnt[c] = (uint8_t)__popcll(e->mask);
-    flags[c] = f | 32;
-    e->mask = 0;
-    e->first = 0;
+    if (!(f & 32)) {                                   // not settled by idx_decide:
+        if ((f & 16) && (uint32_t)e->first != (uint32_t)(k + 1)) return;   // repeats: the last occurrence
+        dcnt[c] = (uint8_t)__popcll(e->mask);
+        flags[c] = f | 32;
+    }
+    e->mask = 0;                                       // (designated without repeats: decided in
+    e->first = 0;                                      //  idx_decide, no read of the entry here)
 }
 
 hipError_t launch_index_finalize(const BlockState *bst, int nblocks, int cap_blk, int ntiles, IndexEntry *tab,
@@ -398,7 +404,7 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,
                         unsigned long long tag_mask, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
-                        int ntiles, int *err, hipStream_t st, Marker *mk)
+                        int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt)
 {
     mk->mark(st);
     dim3 g(ntiles, nblocks);
@@ -426,7 +432,7 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                            coll, ncoll, coll_cap, err);
     }
     hipLaunchKernelGGL(idx_decide_kernel, g, dim3(256), 0, st, bst, cap_blk, offsets, tab, slot, cur, flags, tilesum,
-                       ntiles);
+                       ntiles, dcnt);
     return hipGetLastError();
 }
 

@@ -75,7 +75,9 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,
                         unsigned long long tag_mask, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
-                        int ntiles, int *err, hipStream_t st, Marker *mk);
+                        int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt = nullptr);
+// (dcnt: idx_finalize follows and hands place the designated chunks; decide settles the chunks
+//  without repeats in their min block itself)
 // node-global index mode (gx.hip): place_kernel emits (owner slot, cid, start, stop) for new entries
 struct GxPlace {
     const uint32_t *x2 = nullptr;          // owner responses, indexed by scratch IndexEntry::cid
