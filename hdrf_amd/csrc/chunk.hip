@@ -1309,12 +1309,6 @@ int setprio_mask()
     return m;
 }
 
-int vcap_mode()
-{
-    static const int v = [] { const char *e = getenv("HDRF_VCAP"); return e ? atoi(e) : 0; }();
-    return v;
-}
-
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,

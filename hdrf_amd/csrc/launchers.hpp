@@ -47,7 +47,6 @@ struct ChunkScratch {
     int ring = 1;            // lane walk: granule maxima through the LDS ring (off beside LZ4 passes)
 };
 int setprio_mask();   // HDRF_SETPRIO (chunk.hip)
-int vcap_mode();      // HDRF_VCAP (chunk.hip): register-capped kernels, bit 0 LZ4, bit 1 SHA
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,

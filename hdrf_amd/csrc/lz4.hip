@@ -427,17 +427,6 @@ __global__ void __launch_bounds__(64) lz4_seg_kernel(const ClosedRec *__restrict
     lz4_seg_body<kSmall>(closed, nclosed, arena, cmax, carena, cslot, seg_clen, nseg_max, work, tabmem, prio);
 }
 
-// The byU32 pass held to 96 VGPRs (5 waves per SIMD; 101 unconstrained, no spills either way), so a
-// SIMD holding four of its waves keeps 128 registers for one sha_chunk_vc wave (HDRF_VCAP).
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
-lz4_seg_vc_kernel(const ClosedRec *__restrict__ closed, const uint32_t *__restrict__ nclosed,
-                  const uint8_t *__restrict__ arena, uint64_t cmax, uint8_t *__restrict__ carena, uint64_t cslot,
-                  uint32_t *__restrict__ seg_clen, int nseg_max, uint32_t *__restrict__ work, int prio)
-{
-    __shared__ __attribute__((aligned(16))) uint8_t tabmem[kLzTabU32];
-    lz4_seg_body<false>(closed, nclosed, arena, cmax, carena, cslot, seg_clen, nseg_max, work, tabmem, prio);
-}
-
 // grid nclosed x 256 threads: frame the segments in place, [BE32 len] ([BE32 clen] block)* [BE32 0].
 // Every segment moves to a lower (or equal) offset, so tiles copied in order — all loads of a tile
 // before any of its stores — never overwrite bytes not yet read.  A tile is 16 KiB (four 16-B
@@ -677,12 +666,8 @@ hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int clos
     const int prio = (setprio_mask() >> 6) & 1;
     hipLaunchKernelGGL(lz4_seg_kernel<true>, dim3(std::min(closed_cap, 4 * ncu)), dim3(64), 0, st, closed, nclosed,
                        arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work, prio);
-    if (vcap_mode() & 1)                                   // HDRF_VCAP bit 0
-        hipLaunchKernelGGL(lz4_seg_vc_kernel, dim3(std::min(closed_cap * nseg_max, wpc * ncu)), dim3(64), 0, st, closed,
-                           nclosed, arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work + 1, prio);
-    else
-        hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(std::min(closed_cap * nseg_max, wpc * ncu)), dim3(64), 0, st, closed,
-                           nclosed, arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work + 1, prio);
+    hipLaunchKernelGGL(lz4_seg_kernel<false>, dim3(std::min(closed_cap * nseg_max, wpc * ncu)), dim3(64), 0, st, closed,
+                       nclosed, arena, (uint64_t)cmax, carena, cslot, seg_clen, nseg_max, work + 1, prio);
     hipLaunchKernelGGL(lz4_pack_kernel, dim3(closed_cap), dim3(256), 0, st, closed, nclosed, carena, cslot, seg_clen,
                        nseg_max, file_len);
     return hipGetLastError();

@@ -417,434 +417,6 @@ __global__ void __launch_bounds__(256) sha_carry_kernel(const BlockDesc *__restr
     sha_chunk_body<HW, true>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
 }
 
-// The same kernel held to 128 VGPRs (4 waves per SIMD), so one SHA wave fits on a SIMD beside four
-// LZ4 waves of lz4_seg_vc_kernel (96 VGPRs): 4 x 96 + 128 = 512, the SIMD's register file.  Without
-// the caps (133 + 4 x 104) a SIMD running four LZ4 waves has no room for SHA at all (config 4).
-template <int HW>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-sha_chunk_vc_kernel(const BlockDesc *__restrict__ blocks, const uint32_t *__restrict__ offsets,
-                    const BlockState *__restrict__ bst, int cap_blk, uint32_t *__restrict__ digests,
-                    uint32_t *__restrict__ queue, uint32_t thr, int prio)
-{
-    sha_chunk_body<HW, false>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
-}
-
-// sha_dual: every lane runs TWO independent chunk chains (A and B, both fed from the wave's pool) and
-// their compressions are interleaved round by round (sha*_compress2), so one wave per SIMD has the
-// instruction-level parallelism two waves had.  The point is the waves it frees: at 8 SHA waves per
-// CU the granule pass, walk, place and index kernels ran 1.6-2.7x slower than at 4 (r03: gmax 2.7 vs
-// 1.0 ms per batch in the pipeline), but single-chain SHA at 4 waves per CU left its VALU latency
-// exposed (3.9 ms per batch).  A lane whose chain has nothing to do computes a discarded compression.
-__device__ __forceinline__ void sha1_compress2(uint32_t sa[5], uint32_t wa[16], uint32_t sb[5], uint32_t wb[16])
-{
-    uint32_t a = sa[0], b = sa[1], c = sa[2], d = sa[3], e = sa[4];
-    uint32_t A = sb[0], B = sb[1], C = sb[2], D = sb[3], E = sb[4];
-#pragma unroll
-    for (int i = 0; i < 80; i++) {
-        if (i >= 16) {
-            wa[i & 15] = rotl(xor3(wa[(i - 3) & 15], wa[(i - 8) & 15], wa[(i - 14) & 15]) ^ wa[i & 15], 1);
-            wb[i & 15] = rotl(xor3(wb[(i - 3) & 15], wb[(i - 8) & 15], wb[(i - 14) & 15]) ^ wb[i & 15], 1);
-        }
-        uint32_t f, F, k;
-        if (i < 20)      { f = ch(b, c, d);   F = ch(B, C, D);   k = 0x5A827999u; }
-        else if (i < 40) { f = xor3(b, c, d); F = xor3(B, C, D); k = 0x6ED9EBA1u; }
-        else if (i < 60) { f = maj(b, c, d);  F = maj(B, C, D);  k = 0x8F1BBCDCu; }
-        else             { f = xor3(b, c, d); F = xor3(B, C, D); k = 0xCA62C1D6u; }
-        const uint32_t t = rotl(a, 5) + f + e + k + wa[i & 15];
-        const uint32_t T = rotl(A, 5) + F + E + k + wb[i & 15];
-        e = d; d = c; c = rotl(b, 30); b = a; a = t;
-        E = D; D = C; C = rotl(B, 30); B = A; A = T;
-    }
-    sa[0] += a; sa[1] += b; sa[2] += c; sa[3] += d; sa[4] += e;
-    sb[0] += A; sb[1] += B; sb[2] += C; sb[3] += D; sb[4] += E;
-}
-
-__device__ __forceinline__ void sha256_compress2(uint32_t sa[8], uint32_t wa[16], uint32_t sb[8], uint32_t wb[16])
-{
-    uint32_t a = sa[0], b = sa[1], c = sa[2], d = sa[3], e = sa[4], f = sa[5], g = sa[6], h = sa[7];
-    uint32_t A = sb[0], B = sb[1], C = sb[2], D = sb[3], E = sb[4], F = sb[5], G = sb[6], H = sb[7];
-#pragma unroll
-    for (int i = 0; i < 64; i++) {
-        if (i >= 16) {
-            {
-                const uint32_t w15 = wa[(i - 15) & 15], w2 = wa[(i - 2) & 15];
-                wa[i & 15] = wa[i & 15] + xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3) + wa[(i - 7) & 15] +
-                             xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-            }
-            {
-                const uint32_t w15 = wb[(i - 15) & 15], w2 = wb[(i - 2) & 15];
-                wb[i & 15] = wb[i & 15] + xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3) + wb[(i - 7) & 15] +
-                             xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
-            }
-        }
-        const uint32_t t1 = h + xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25)) + ch(e, f, g) + kK256[i] + wa[i & 15];
-        const uint32_t T1 = H + xor3(rotr(E, 6), rotr(E, 11), rotr(E, 25)) + ch(E, F, G) + kK256[i] + wb[i & 15];
-        const uint32_t t2 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22)) + maj(a, b, c);
-        const uint32_t T2 = xor3(rotr(A, 2), rotr(A, 13), rotr(A, 22)) + maj(A, B, C);
-        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-        H = G; G = F; F = E; E = D + T1; D = C; C = B; B = A; A = T1 + T2;
-    }
-    sa[0] += a; sa[1] += b; sa[2] += c; sa[3] += d; sa[4] += e; sa[5] += f; sa[6] += g; sa[7] += h;
-    sb[0] += A; sb[1] += B; sb[2] += C; sb[3] += D; sb[4] += E; sb[5] += F; sb[6] += G; sb[7] += H;
-}
-
-struct ShaChain {
-    bool active = false;         // a chunk in progress (its window for this iteration is in d)
-    int k = 0;
-    uint32_t s0 = 0, len = 0, T = 0, nb = 0, bi = 0;
-    uint32_t st[8];
-    bool has_next = false;       // the chunk this chain takes when the current one ends (pre-assigned)
-    int nk = 0;
-    uint32_t ns0 = 0, nlen = 0;
-};
-
-// the two compressions of one slot of both chains; a chain's state changes only where `use`
-template <int HW>
-__device__ __forceinline__ void compress_both(ShaChain &A, uint32_t ma[16], bool useA, ShaChain &B, uint32_t mb[16],
-                                              bool useB)
-{
-    uint32_t na[8], nb[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) { na[i] = A.st[i]; nb[i] = B.st[i]; }
-    if (HW == 5) sha1_compress2(na, ma, nb, mb);
-    else sha256_compress2(na, ma, nb, mb);
-#pragma unroll
-    for (int i = 0; i < (HW == 5 ? 5 : 8); i++) {           // SHA-224 keeps all 8 state words
-        A.st[i] = useA ? na[i] : A.st[i];
-        B.st[i] = useB ? nb[i] : B.st[i];
-    }
-}
-
-// The windows are loaded one iteration ahead: before an iteration computes, every lane issues the load
-// of the window its chain needs next (the next pair of the current chunk, or the first pair of the
-// chunk pre-assigned to follow it), so the loads are in flight under the four compressions.
-template <int HW>
-__global__ void __launch_bounds__(256) sha_dual_kernel(const BlockDesc *__restrict__ blocks,
-                                                       const uint32_t *__restrict__ offsets,
-                                                       const BlockState *__restrict__ bst, int cap_blk,
-                                                       uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                       uint32_t thr, int prio)
-{
-    if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
-        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr, prio & 1);
-        return;
-    }
-    if (prio & 2) __builtin_amdgcn_s_setprio(2);
-    const int b = blockIdx.y - 1;
-    const int n = bst[b].n_chunks;
-    const BlockDesc &bd = blocks[b];
-    const uint8_t *base = bd.data;
-    const uint64_t readable = bd.readable;
-    const uint32_t *off = offsets + (size_t)b * cap_blk;
-    uint32_t *db = digests + (size_t)b * cap_blk * HW;
-    const int l = lane_id();
-    int kbP, cntP, kbQ, cntQ;
-    uint32_t SP, EP, SQ, EQ;
-    auto reserve = [&](int &kb, int &cnt, uint32_t &S, uint32_t &E) {
-        uint32_t got = 0;
-        if (l == 0) got = atomicAdd(queue + b, 64u);
-        kb = (int)rdfirst(got);
-        cnt = max(0, min(64, n - kb));
-        const int k = kb + l;
-        E = l < cnt ? ld4(off + k) : 0u;
-        S = (l < cnt && k > 0) ? ld4(off + k - 1) : 0u;
-    };
-    reserve(kbP, cntP, SP, EP);
-    reserve(kbQ, cntQ, SQ, EQ);
-    int head = 0;
-    ShaChain A, B;
-    set_iv<HW>(A.st);
-    set_iv<HW>(B.st);
-    // pre-assign a next chunk to the lanes of chain c with `want` (long chunks go to the long lanes)
-    auto offer = [&](ShaChain &c, bool want) {
-        for (;;) {
-            const unsigned long long idle = ballot64(want && !c.has_next);
-            if (!idle) break;
-            if (head >= cntP) {
-                if (cntQ == 0) break;
-                kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
-                reserve(kbQ, cntQ, SQ, EQ);
-            }
-            const bool me = want && !c.has_next;
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
-            const int avail = cntP - head;
-            const int idx = min(head + rank, 63);
-            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
-            bool skip = false;
-            if (ballot64(me && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
-            if (me && rank < avail && e - c0 >= thr) {
-                skip = true;
-            } else if (me && rank < avail) {
-                c.nk = kbP + head + rank;
-                c.ns0 = c0;
-                c.nlen = e - c0;
-                c.has_next = true;
-            }
-            const int nidle = __popcll(idle);
-            head += min(nidle, avail);
-            if (!ballot64(skip) && nidle <= avail) break;
-        }
-    };
-    auto take_next = [&](ShaChain &c) {           // the pre-assigned chunk becomes the current one
-        if (!c.active && c.has_next) {
-            c.k = c.nk; c.s0 = c.ns0; c.len = c.nlen;
-            c.T = c.len >> 6; c.nb = (c.len + 8) / 64 + 1; c.bi = 0;
-            set_iv<HW>(c.st);
-            c.active = true;
-            c.has_next = false;
-        }
-    };
-    uint32_t dA[33], dB[33];
-    // prologue: first chunks and their windows
-    offer(A, true);
-    offer(B, true);
-    take_next(A);
-    take_next(B);
-    if (A.active) load_win(base, readable, A.s0, pair_at(0, A.T), dA);
-    if (B.active) load_win(base, readable, B.s0, pair_at(0, B.T), dB);
-    for (;;) {
-        if (!ballot64(A.active || B.active)) break;
-        const bool twoA = A.active && pair_at(A.bi, A.T), twoB = B.active && pair_at(B.bi, B.T);
-        const uint32_t stepA = twoA ? 2u : 1u, stepB = twoB ? 2u : 1u;
-        const bool endA = !A.active || A.bi + stepA >= A.nb, endB = !B.active || B.bi + stepB >= B.nb;
-        offer(A, endA);                           // the chunk after the current one, before it ends
-        offer(B, endB);
-        // next windows (in flight under this iteration's compressions)
-        uint32_t xA[33], xB[33];
-        {
-            const bool goA = A.active && !endA, nxA = endA && A.has_next;
-            const uint32_t pA = goA ? A.s0 + 64u * (A.bi + stepA) : A.ns0;
-            const bool tA = goA ? pair_at(A.bi + stepA, A.T) : pair_at(0, A.nlen >> 6);
-            if (goA || nxA) load_win(base, readable, pA, tA, xA);
-            const bool goB = B.active && !endB, nxB = endB && B.has_next;
-            const uint32_t pB = goB ? B.s0 + 64u * (B.bi + stepB) : B.ns0;
-            const bool tB = goB ? pair_at(B.bi + stepB, B.T) : pair_at(0, B.nlen >> 6);
-            if (goB || nxB) load_win(base, readable, pB, tB, xB);
-        }
-        const uint32_t posA = A.s0 + 64u * A.bi, posB = B.s0 + 64u * B.bi;
-        const uint32_t selA = 0x00010203u + (posA & 3u) * 0x01010101u, selB = 0x00010203u + (posB & 3u) * 0x01010101u;
-        uint32_t ma[16], mb[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            ma[i] = __builtin_amdgcn_perm(dA[i + 1], dA[i], selA);
-            mb[i] = __builtin_amdgcn_perm(dB[i + 1], dB[i], selB);
-        }
-        if (ballot64(A.active && A.bi >= A.T)) pad_block(ma, A.len, A.bi, A.nb);
-        if (ballot64(B.active && B.bi >= B.T)) pad_block(mb, B.len, B.bi, B.nb);
-        compress_both<HW>(A, ma, A.active, B, mb, B.active);
-        if (ballot64(twoA || twoB)) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                ma[i] = __builtin_amdgcn_perm(dA[i + 17], dA[i + 16], selA);
-                mb[i] = __builtin_amdgcn_perm(dB[i + 17], dB[i + 16], selB);
-            }
-            if (ballot64(twoA && A.bi + 1 == A.T)) pad_block(ma, A.len, A.bi + 1, A.nb);
-            if (ballot64(twoB && B.bi + 1 == B.T)) pad_block(mb, B.len, B.bi + 1, B.nb);
-            compress_both<HW>(A, ma, twoA, B, mb, twoB);
-        }
-        if (A.active) {
-            A.bi += stepA;
-            if (A.bi >= A.nb) { store_digest<HW>(db + (size_t)A.k * HW, A.st); A.active = false; }
-        }
-        if (B.active) {
-            B.bi += stepB;
-            if (B.bi >= B.nb) { store_digest<HW>(db + (size_t)B.k * HW, B.st); B.active = false; }
-        }
-        take_next(A);
-        take_next(B);
-#pragma unroll
-        for (int i = 0; i < 33; i++) { dA[i] = xA[i]; dB[i] = xB[i]; }
-    }
-}
-
-// sha_ring: the same lanes, but no 128-B line is fetched twice.  A lane's pair window (132 B from
-// a 4-aligned start) spans the absolute 128-B line L holding its start and line L + 1.  The lane keeps
-// line L in an LDS slot of its own; each iteration loads line L + 1 whole (8 x 16 B, aligned), reads
-// the window's part in L from the slot, overwrites the slot with L + 1, reads the part in L + 1 (the
-// slot read at a per-lane dword offset is the realignment), and the next window starts in L + 1.  So
-// a chunk's lines are fetched once each (plus the line it shares with its neighbour), instead of the
-// 1.48x of sha_chunk, whose lanes' re-read lines did not survive in L2 (PMC r03).  Pairing as in
-// sha_iter: a chunk whose block T (the message end) is even starts one block early (a skipped slot),
-// so every iteration steps by 128 B, T is always in the second slot, and the length-only block T + 1
-// (if any) is the first slot of a last iteration that loads nothing.
-constexpr int kSlotDw = 33;                   // 32 dwords + 1 pad (bank spread) per lane
-typedef __attribute__((address_space(3))) uint32_t lds_w;
-
-// the absolute 128-B line at block offset lo (may start before the block: those bytes read as 0)
-__device__ __forceinline__ void load_line(const uint8_t *base, int64_t readable, int64_t lo, uint32_t (&R)[32])
-{
-    if (lo >= 0 && lo + 128 <= readable) {
-        const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + lo);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
-            R[4 * q] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < 32; q++) R[q] = lo + 4 * q >= 0 ? load4_guard(base, lo + 4 * q, readable) : 0u;
-    }
-}
-
-// Window of the line variant: dwords [q, q + 33) of the two lines P ++ R, q in [0, 31] per lane, by
-// a 5-stage barrel shift of selects (191 v_cndmask, no LDS, no memory).
-__device__ __forceinline__ void shift_window(const uint32_t (&P)[32], const uint32_t (&R)[32], uint32_t q, uint32_t (&d)[33])
-{
-    // per-lane masks (all ones where the stage shifts); the blends are on values (bfi), never a
-    // select of element addresses, so the arrays stay in registers
-    const uint32_t m16 = 0u - ((q >> 4) & 1u), m8 = 0u - ((q >> 3) & 1u), m4 = 0u - ((q >> 2) & 1u),
-                   m2 = 0u - ((q >> 1) & 1u), m1 = 0u - (q & 1u);
-    uint32_t y[48], z[40], w[36], v[34];
-#pragma unroll
-    for (int i = 0; i < 48; i++) y[i] = bfi(m16, i + 16 < 32 ? P[i + 16] : R[i - 16], i < 32 ? P[i] : R[i - 32]);
-#pragma unroll
-    for (int i = 0; i < 40; i++) z[i] = bfi(m8, y[i + 8], y[i]);
-#pragma unroll
-    for (int i = 0; i < 36; i++) w[i] = bfi(m4, z[i + 4], z[i]);
-#pragma unroll
-    for (int i = 0; i < 34; i++) v[i] = bfi(m2, w[i + 2], w[i]);
-#pragma unroll
-    for (int i = 0; i < 33; i++) d[i] = bfi(m1, v[i + 1], v[i]);
-}
-
-// LINE = false: sha_ring (the carried line in an LDS slot); LINE = true: sha_line, the carried line in
-// registers and the window cut out of the two lines by shift_window (every line fetched once, no LDS:
-// the ring's slot reads and writes, ~100 LDS instructions per iteration, and its 34 KiB per workgroup
-// cost more than the re-fetches they saved, r03).
-template <int HW, bool LINE>
-__global__ void __launch_bounds__(256) sha_ring_kernel(const BlockDesc *__restrict__ blocks,
-                                                       const uint32_t *__restrict__ offsets,
-                                                       const BlockState *__restrict__ bst, int cap_blk,
-                                                       uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                       uint32_t thr, int prio)
-{
-    if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
-        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr, prio & 1);
-        return;
-    }
-    __shared__ uint32_t s_slot[LINE ? 1 : 4 * 64 * kSlotDw];
-    if (prio & 2) __builtin_amdgcn_s_setprio(2);
-    const int b = blockIdx.y - 1;
-    const int n = bst[b].n_chunks;
-    const BlockDesc &bd = blocks[b];
-    const uint8_t *base = bd.data;
-    const int64_t readable = (int64_t)bd.readable;
-    const int64_t bmis = (int64_t)((uintptr_t)base & 127u);     // block start's offset in its line
-    const uint32_t *off = offsets + (size_t)b * cap_blk;
-    uint32_t *db = digests + (size_t)b * cap_blk * HW;
-    const int l = lane_id();
-    lds_w *slot = (lds_w *)&s_slot[(wave_id() * 64 + l) * kSlotDw];
-    int kbP, cntP, kbQ, cntQ;
-    uint32_t SP, EP, SQ, EQ;
-    auto reserve = [&](int &kb, int &cnt, uint32_t &S, uint32_t &E) {
-        uint32_t got = 0;
-        if (l == 0) got = atomicAdd(queue + b, 64u);
-        kb = (int)rdfirst(got);
-        cnt = max(0, min(64, n - kb));
-        const int k = kb + l;
-        E = l < cnt ? ld4(off + k) : 0u;
-        S = (l < cnt && k > 0) ? ld4(off + k - 1) : 0u;
-    };
-    reserve(kbP, cntP, SP, EP);
-    reserve(kbQ, cntQ, SQ, EQ);
-    int head = 0;
-    bool active = false, fresh = false;
-    int k = 0;
-    uint32_t len = 0, T = 0, nb = 0;
-    int b0 = 0;                                   // block index of the window's first slot (-1: skipped)
-    int64_t wb = 0;                               // window start, block offset (b0 * 64 from the chunk)
-    uint32_t st[8];
-    set_iv<HW>(st);
-    uint32_t N0[32];                              // a fresh chunk's first line (LINE: the carried line)
-    for (;;) {
-        if (active && b0 >= (int)nb) {            // chain done: the digest
-            store_digest<HW>(db + (size_t)k * HW, st);
-            active = false;
-        }
-        for (;;) {                                 // offer chunks to idle lanes
-            const unsigned long long idle = ballot64(!active);
-            if (!idle) break;
-            if (head >= cntP) {
-                if (cntQ == 0) break;
-                kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
-                reserve(kbQ, cntQ, SQ, EQ);
-            }
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
-            const int avail = cntP - head;
-            const int idx = min(head + rank, 63);
-            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
-            bool skip = false;
-            if (ballot64(!active && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
-            if (!active && rank < avail && e - c0 >= thr) {
-                skip = true;
-            } else if (!active && rank < avail) {
-                k = kbP + head + rank;
-                len = e - c0;
-                T = len >> 6;
-                nb = (len + 8) / 64 + 1;
-                const bool teven = (T & 1u) == 0;
-                b0 = teven ? -1 : 0;
-                wb = (int64_t)c0 - (teven ? 64 : 0);
-                set_iv<HW>(st);
-                active = true;
-                fresh = true;
-                load_line(base, readable, ((bmis + wb) & ~(int64_t)127) - bmis, N0);
-            }
-            const int nidle = __popcll(idle);
-            head += min(nidle, avail);
-            if (!ballot64(skip) && nidle <= avail) break;
-        }
-        if (!ballot64(active)) break;
-        const bool data = active && b0 <= (int)T;  // not the length-only block alone
-        const int64_t lo = ((bmis + wb) & ~(int64_t)127) - bmis;   // line L, block offset
-        const uint32_t q0 = (uint32_t)((bmis + wb) & 124);          // window's first dword in L (x4)
-        uint32_t R[32], d[33];
-        if (data) load_line(base, readable, lo + 128, R);
-        if (LINE) {
-            if (data) {
-                shift_window(N0, R, q0 >> 2, d);
-#pragma unroll
-                for (int i = 0; i < 32; i++) N0[i] = R[i];
-            }
-            fresh = false;
-        } else if (ballot64(fresh)) {
-            if (fresh) {
-#pragma unroll
-                for (int i = 0; i < 32; i++) slot[i] = N0[i];
-            }
-            fresh = false;
-        }
-        if (!LINE && data) {
-#pragma unroll
-            for (int j = 0; j < 33; j++) d[j] = slot[((q0 >> 2) + j) & 31];
-#pragma unroll
-            for (int i = 0; i < 32; i++) slot[i] = R[i];
-#pragma unroll
-            for (int j = 0; j < 33; j++)
-                if ((q0 >> 2) + j >= 32) d[j] = slot[((q0 >> 2) + j) & 31];
-        }
-        if (active) {
-            const uint32_t sel = 0x00010203u + (uint32_t)(wb & 3) * 0x01010101u;
-            uint32_t m[16];
-            if (b0 >= 0) {                        // slot 0 (the length-only block pads)
-#pragma unroll
-                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
-                if (ballot64(b0 > (int)T)) pad_block(m, len, (uint32_t)b0, nb);
-                if (HW == 5) sha1_compress(st, m);
-                else sha256_compress(st, m);
-            }
-            if (b0 + 1 < (int)nb) {               // slot 1 (T pads)
-#pragma unroll
-                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 17], d[i + 16], sel);
-                if (ballot64(b0 + 1 == (int)T)) pad_block(m, len, (uint32_t)(b0 + 1), nb);
-                if (HW == 5) sha1_compress(st, m);
-                else sha256_compress(st, m);
-            }
-            b0 += 2;
-            wb += 128;
-        }
-    }
-}
 
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
@@ -865,47 +437,22 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     // 919 at 4) — fewer concurrent per-lane streams thrash L2 less and leave CUs to the
     // co-running place / granule passes; env knobs for
     // experiments: HDRF_SHA_WAVES (waves per SIMD over 1024 SIMDs), HDRF_SHA_LDS (bytes per WG)
-    // HDRF_SHA_RING: 1 = sha_ring (each line fetched once, LDS line slots), 0 = sha_chunk
-    static const bool ring = [] { const char *e = getenv("HDRF_SHA_RING"); return e ? atoi(e) != 0 : false; }();
-    // HDRF_SHA_LINE: 1 = sha_line (each line fetched once, window by a register barrel shift)
-    static const bool line = [] { const char *e = getenv("HDRF_SHA_LINE"); return e ? atoi(e) != 0 : false; }();
-    // HDRF_SHA_DUAL: 1 = sha_dual (two interleaved chains per lane; its default grid is 4 waves per CU)
-    static const bool dual = [] { const char *e = getenv("HDRF_SHA_DUAL"); return e ? atoi(e) != 0 : false; }();
     // HDRF_SHA_WPC: waves per CU over the chip's 256 CUs (overrides HDRF_SHA_WAVES x 4)
     static const int per_cu = [] {
         const char *c = getenv("HDRF_SHA_WPC");
         if (c) return atoi(c);
         const char *e = getenv("HDRF_SHA_WAVES");
-        const char *d = getenv("HDRF_SHA_DUAL");
-        return 4 * (e ? atoi(e) : (d && atoi(d) ? 1 : 2));
+        return 4 * (e ? atoi(e) : 2);
     }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     // HDRF_SHA_CARRY: 1 = sha_carry (4-block windows, the second pair carried in registers)
     static const bool carryk = [] { const char *e = getenv("HDRF_SHA_CARRY"); return e && atoi(e) != 0; }();
-    // HDRF_VCAP bit 1: the register-capped SHA kernel (sha_chunk_vc)
-    const bool vcap = (vcap_mode() & 2) != 0;
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
-    if (dual && hasher == 0)
-        hipLaunchKernelGGL(sha_dual_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (dual)
-        hipLaunchKernelGGL(sha_dual_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (line && hasher == 0)
-        hipLaunchKernelGGL((sha_ring_kernel<5, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (line)
-        hipLaunchKernelGGL((sha_ring_kernel<7, true>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (ring && hasher == 0)
-        hipLaunchKernelGGL((sha_ring_kernel<5, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (ring)
-        hipLaunchKernelGGL((sha_ring_kernel<7, false>), g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (carryk && hasher == 0)
+    if (carryk && hasher == 0)
         hipLaunchKernelGGL(sha_carry_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (carryk)
         hipLaunchKernelGGL(sha_carry_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (vcap && hasher == 0)
-        hipLaunchKernelGGL(sha_chunk_vc_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (vcap)
-        hipLaunchKernelGGL(sha_chunk_vc_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (hasher == 0)
         hipLaunchKernelGGL(sha_chunk_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else
