@@ -196,7 +196,12 @@ struct hdrf_ctx {
     // packet-granular receive (hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot): device
     // receive buffers, and a pinned chunk ring the packets are copied into before their H2D
     static constexpr int kRx = 16;
-    static constexpr uint64_t kRingChunk = 4ull << 20;
+    // pinned staging chunk per receive buffer (two alternate): 4 MiB, HDRF_RX_CHUNK_MB for A/B
+    const uint64_t kRingChunk = [] {
+        const char *e = getenv("HDRF_RX_CHUNK_MB");
+        const long v = e ? atol(e) : 4;
+        return (uint64_t)(v >= 1 && v <= 64 ? v : 4) << 20;
+    }();
     // one receive buffer per block being received: device copy of the block, and two pinned 4 MiB
     // staging chunks of its own, so receivers of different blocks (one DataXceiver thread each)
     // copy their packets concurrently, outside the context lock
@@ -1023,7 +1028,7 @@ static hipError_t rx_flush(hdrf_ctx *ctx, hdrf_ctx::Rx &r)
 {
     if (r.fill == 0) return hipSuccess;
     const int c = r.cur;
-    hipError_t e = hipMemcpyAsync(r.d + r.dst, r.h + (uint64_t)c * hdrf_ctx::kRingChunk, r.fill, hipMemcpyHostToDevice,
+    hipError_t e = hipMemcpyAsync(r.d + r.dst, r.h + (uint64_t)c * ctx->kRingChunk, r.fill, hipMemcpyHostToDevice,
                                   ctx->stC);
     if (e == hipSuccess) e = hipEventRecord(r.ev[c], ctx->stC);
     if (e != hipSuccess) return e;
@@ -1047,7 +1052,7 @@ extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
         if (r.state.load() != 0) continue;
         if (!r.d) HIPCK(hipMalloc((void **)&r.d, (uint64_t)ctx->cfg.max_block_bytes + kSlack + 256));
         if (!r.h) {
-            HIPCK(hipHostMalloc((void **)&r.h, 2 * hdrf_ctx::kRingChunk));
+            HIPCK(hipHostMalloc((void **)&r.h, 2 * ctx->kRingChunk));
             for (auto &e : r.ev) HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         r.len = 0;
@@ -1076,13 +1081,13 @@ extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data
     }
     while (len) {
         if (r.fill == 0) r.dst = r.len;
-        const uint64_t n = std::min(len, hdrf_ctx::kRingChunk - r.fill);
-        std::memcpy(r.h + (uint64_t)r.cur * hdrf_ctx::kRingChunk + r.fill, data, n);
+        const uint64_t n = std::min(len, ctx->kRingChunk - r.fill);
+        std::memcpy(r.h + (uint64_t)r.cur * ctx->kRingChunk + r.fill, data, n);
         r.fill += n;
         r.len += n;
         data += n;
         len -= n;
-        if (r.fill == hdrf_ctx::kRingChunk) {
+        if (r.fill == ctx->kRingChunk) {
             const hipError_t e = rx_flush(ctx, r);
             if (e != hipSuccess) {
                 HDRF_LOCK(ctx);
