@@ -99,6 +99,7 @@ struct Slot {
     hipEvent_t lz_done = nullptr;             // compressor 2: its closed containers are Lz4Codec files
     int rx_release = -1;                      // packet path: receive buffer to free when the batch completes
     uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
+    bool gx_compressed = false;               // node-global compressor 2: hdrf_gx_compress ran for the batch
     RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
     hipEvent_t recipe_done = nullptr;         // the copies read d_dig: the slot's next SHA waits
     bool recipe_pending = false;
@@ -256,6 +257,8 @@ static int device_error(hdrf_ctx *ctx, int herr)
     if (herr & 2) m += " (index table full)";
     if (herr & 1) m += " (chunking: offsets capacity or an unterminated fallback walk)";
     if (herr & 192) m += " (chunking: speculative list overflow / inconsistent stitch)";
+    if (herr & 4) m += " (tag-collision list full)";
+    if (herr & 256) m += " (node-global: an X3 location names no index entry)";
     return set_err(ctx, (herr & kErrCapacity) ? HDRF_E_CAPACITY : HDRF_E_DEVICE, m);
 }
 
@@ -567,6 +570,10 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
             (rc = dalloc(ctx, &ctx->d_gx_rcounts, 64)) || (rc = dalloc(ctx, &ctx->d_oslot, nrec)) ||
             (rc = dalloc(ctx, &ctx->d_oflags, nrec))) {
         }
+        // owner slots start defined (hdrf_gx_owner's kernels never read a slot the claim did not write
+        // once an error is raised, but a defined value keeps any later misuse inside the table)
+        if (!rc && hipMemset(ctx->d_oslot, 0, sizeof(uint32_t) * nrec) != hipSuccess)
+            rc = set_err(ctx, HDRF_E_HIP, "hipMemset failed");
     }
     ctx->timing = c.timing != 0;
     if (!rc) rc = init_state(ctx);
@@ -749,11 +756,17 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         uint64_t bytes = 0;
         for (int b = 0; b < nblocks; b++) bytes += len[b];
         const uint32_t bound = close_bound(c, bytes), per = (uint32_t)(c.arena_slots / 4);
+        // Only completed batches' containers can be drained: when the batches in flight are part of
+        // what fills the ring, the recovery is hdrf_wait_batch (oldest), then hdrf_drain_containers,
+        // then the submit again; the message names the step.
         for (int t = 0; t < c.n_thread; t++)
             if ((uint64_t)ctx->undrained[t] + ctx->inflight_bound + bound > per - 1)
-                return set_err(ctx, HDRF_E_CAPACITY, "container arena: undrained closed containers fill the ring of "
-                                                     "storer range " + std::to_string(t) +
-                                                     " (hdrf_drain_containers first)");
+                return set_err(ctx, HDRF_E_CAPACITY,
+                               "container arena: the ring of storer range " + std::to_string(t) + " is full (" +
+                                   std::to_string(ctx->undrained[t]) + " undrained closed containers, " +
+                                   std::to_string(ctx->inflight_bound) + " closes bounded for batches in flight)" +
+                                   (ctx->inflight_bound ? " (hdrf_wait_batch, then hdrf_drain_containers)"
+                                                        : " (hdrf_drain_containers first)"));
         S.close_bound = bound;
         ctx->inflight_bound += bound;
     }
@@ -2167,6 +2180,7 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     for (const AllocState *a : {&ctx->gx_ain, &ctx->gx_aout})
         for (int t = 0; t < ctx->cfg.n_thread; t++)
             if (a->exists[t] && !ctx->containers.count(a->id[t])) note_container(ctx, a->id[t], a->slot[t], a->cur[t], 0);
+    S.gx_compressed = false;
     if (int rc = complete_slot(ctx, si, false)) return rc;
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
     ctx->gx_bphase = 4;
@@ -2202,7 +2216,9 @@ extern "C" int hdrf_gx_piece(hdrf_ctx *ctx, uint32_t id, uint64_t off, uint64_t 
     if (n) {
         HIPCK(hipMemcpyAsync(write ? (void *)p : dev, write ? (const void *)dev : (const void *)p, n, hipMemcpyDeviceToDevice,
                              ctx->stB));
-        HIPCK(hipStreamSynchronize(ctx->stB));
+        // a read hands the bytes to the caller (who ships them to the closer): complete on return; a
+        // write is ordered before hdrf_gx_compress on the same stream, which synchronises
+        if (!write) HIPCK(hipStreamSynchronize(ctx->stB));
     }
     return 0;
 }
@@ -2215,7 +2231,10 @@ extern "C" int hdrf_gx_compress(hdrf_ctx *ctx)
     if (c.compressor != 2) return 0;
     Slot &S = ctx->sl[ctx->gx_nback % 2];
     const uint32_t nclosed = *S.h_nclosed;
-    if (!nclosed) return 0;
+    if (!nclosed || S.gx_compressed) {                  // once per batch: a second call changes nothing
+        HIPCK(hipStreamSynchronize(ctx->stB));         // (hdrf_gx_piece writes are complete on return)
+        return 0;
+    }
     hipStream_t st = ctx->stB;
     HIPCK(launch_lz4(S.d_closed, S.d_nclosed, ctx->closed_cap, c.container_max, ctx->d_arena, ctx->d_carena, ctx->cslot,
                      S.d_segclen, S.d_filelen, S.d_lzwork, st));
@@ -2228,6 +2247,7 @@ extern "C" int hdrf_gx_compress(hdrf_ctx *ctx)
         it->second.clen = S.h_filelen[i];
         ctx->stats.closed_file_bytes += (int64_t)S.h_filelen[i] - (int64_t)r.len;
     }
+    S.gx_compressed = true;
     return (int)nclosed;
 }
 
@@ -2238,12 +2258,25 @@ extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int6
     if (!x3_recv || !recv_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     for (int s = 0; s < ctx->G; s++)
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
+    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    // compressor 2: the containers this rank closed must be Lz4Codec files before the batch commits
+    // (container reads of closed containers take their bytes from the compressed arena)
+    if (ctx->cfg.compressor == 2 && *S.h_nclosed && !S.gx_compressed)
+        return set_err(ctx, HDRF_E_INVAL, "compressor 2: hdrf_gx_compress must run between hdrf_gx_place and hdrf_gx_commit");
     hipStream_t st = ctx->stB;
     HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
-    HIPCK(launch_gx_commit(x3_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap, ctx->G, ctx->d_tab, st));
+    HIPCK(launch_gx_commit(x3_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap, ctx->G, ctx->d_tab,
+                           ctx->cfg.index_log2, S.d_err, st));
+    int herr = 0;
+    HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     ctx->gx_bphase = 0;
     ctx->gx_nback++;
+    if (herr) {
+        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
+        HIPCK(hipStreamSynchronize(st));
+        return device_error(ctx, herr);
+    }
     return 0;
 }
 

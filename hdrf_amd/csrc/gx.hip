@@ -212,15 +212,25 @@ __global__ void own_slow_kernel(const uint32_t *__restrict__ x1, IndexEntry *__r
 
 // response per record: {owner slot, bit0 created this batch, bit1 record holds the minimum block}.
 // The record holding the minimum block (exactly one per entry) finalises nCopy.
+// After a claim error (table full: a record's oslot was never written; collision list overflow:
+// its oslot names an entry holding another digest) no record touches the table again: every
+// response is "not created, not the minimum" so the sources designate nothing and send no X3
+// location, and the error is reported by hdrf_gx_place.
 __global__ void __launch_bounds__(256) own_decide_kernel(const uint32_t *__restrict__ x1, int rw,
                                                          const int64_t *__restrict__ counts, int64_t cap,
                                                          IndexEntry *__restrict__ tab, const uint32_t *__restrict__ oslot,
-                                                         uint32_t cur, uint32_t *__restrict__ x2)
+                                                         uint32_t cur, uint32_t *__restrict__ x2,
+                                                         const int *__restrict__ err)
 {
     const int s = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= counts[s]) return;
     const size_t r = (size_t)s * cap + i;
+    if (*err & 6) {
+        x2[2 * r] = 0;
+        x2[2 * r + 1] = 0;
+        return;
+    }
     const uint32_t gpos = x1[r * rw + rw - 2];
     const uint32_t h = oslot[r];
     IndexEntry *e = tab + h;
@@ -236,11 +246,11 @@ __global__ void __launch_bounds__(256) own_decide_kernel(const uint32_t *__restr
 }
 
 __global__ void __launch_bounds__(256) own_finish_kernel(const uint32_t *__restrict__ x2, const int64_t *__restrict__ counts,
-                                                         int64_t cap, IndexEntry *__restrict__ tab)
+                                                         int64_t cap, IndexEntry *__restrict__ tab, const int *__restrict__ err)
 {
     const int s = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= counts[s]) return;
+    if (i >= counts[s] || (*err & 6)) return;
     const size_t r = (size_t)s * cap + i;
     if (x2[2 * r + 1] & 2) {
         IndexEntry *e = tab + x2[2 * r];
@@ -287,12 +297,14 @@ __global__ void __launch_bounds__(256) gx_decide_kernel(const BlockState *__rest
 
 // ---- owner: commit locations of entries created this batch (X3) ---------------------------
 __global__ void __launch_bounds__(256) own_commit_kernel(const uint32_t *__restrict__ x3, const int64_t *__restrict__ counts,
-                                                         int64_t cap, IndexEntry *__restrict__ tab)
+                                                         int64_t cap, IndexEntry *__restrict__ tab, uint64_t tab_n,
+                                                         int *__restrict__ err)
 {
     const int s = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= counts[s]) return;
     const uint32_t *rec = x3 + ((size_t)s * cap + i) * 4;
+    if (rec[0] >= tab_n) { atomicOr(err, 256); return; }    // a peer's malformed location: never write outside
     IndexEntry *e = tab + rec[0];
     e->cid = rec[1] | ((uint32_t)(s + 1) << 24);          // ids are < 2^24: bits 24-31 = placing rank + 1
     e->start = rec[2];
@@ -341,8 +353,8 @@ hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts
         hipLaunchKernelGGL(own_slow_kernel<7>, dim3(1), dim3(64), 0, st, x1, tab, log2cap, cur, tag_mask, oslot, coll,
                            ncoll, coll_cap, err);
     }
-    hipLaunchKernelGGL(own_decide_kernel, g, dim3(256), 0, st, x1, HW + 2, counts, cap, tab, oslot, cur, x2);
-    hipLaunchKernelGGL(own_finish_kernel, g, dim3(256), 0, st, x2, counts, cap, tab);
+    hipLaunchKernelGGL(own_decide_kernel, g, dim3(256), 0, st, x1, HW + 2, counts, cap, tab, oslot, cur, x2, err);
+    hipLaunchKernelGGL(own_finish_kernel, g, dim3(256), 0, st, x2, counts, cap, tab, err);
     return hipGetLastError();
 }
 
@@ -356,9 +368,10 @@ hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int
 }
 
 hipError_t launch_gx_commit(const uint32_t *x3, const int64_t *counts, int64_t max_count, int64_t cap, int G,
-                            IndexEntry *tab, hipStream_t st)
+                            IndexEntry *tab, int log2cap, int *err, hipStream_t st)
 {
-    hipLaunchKernelGGL(own_commit_kernel, dim3(gx_tiles(max_count), G), dim3(256), 0, st, x3, counts, cap, tab);
+    hipLaunchKernelGGL(own_commit_kernel, dim3(gx_tiles(max_count), G), dim3(256), 0, st, x3, counts, cap, tab,
+                       (uint64_t)1 << log2cap, err);
     return hipGetLastError();
 }
 

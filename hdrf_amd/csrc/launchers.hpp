@@ -122,7 +122,7 @@ hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int
                             const IndexEntry *scratch, const uint32_t *slot, const uint32_t *x2, uint8_t *flags,
                             uint32_t *tilesum, hipStream_t st);
 hipError_t launch_gx_commit(const uint32_t *x3, const int64_t *counts, int64_t max_count, int64_t cap, int G,
-                            IndexEntry *tab, hipStream_t st);
+                            IndexEntry *tab, int log2cap, int *err, hipStream_t st);
 // recipes (storeDB): a batch's digests copied into the device recipe store
 struct RecipeCopy {
     uint64_t src, dst;       // device addresses (4-B aligned)

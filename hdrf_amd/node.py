@@ -213,11 +213,17 @@ class NodeRank:
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
-        for cid, a, b, rb in bufs:
-            t = rb.to(self.device)
+        # one device synchronisation for every received piece (gloo: their H2D copies on torch's
+        # stream); the writes are then enqueued on the back stream ahead of gx_compress, which keeps
+        # the order and synchronises once, so the pieces stay referenced until it returned
+        held = [(cid, a, b, rb.to(self.device)) for cid, a, b, rb in bufs]
+        if held:
             torch.cuda.synchronize(self.device)
+        for cid, a, b, t in held:
             ctx.gx_piece(cid, a, b - a, t.data_ptr(), write=True)
-        return ctx.gx_compress()
+        n = ctx.gx_compress()
+        del held
+        return n
 
     def reduce_batch(self, dev_ptrs, lens, readable, block_ids, gbase):
         """Reduce this rank's blocks of one global batch; gbase = its first batch position."""

@@ -392,7 +392,9 @@ int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, 
  * state before and after its flush walk (hdrf_gx_alloc_io, 128 B each; all-gathered by the caller,
  * they tell every rank which rank holds which bytes of each container); the head pieces of a
  * container another rank closes are copied out of / into arena slots (hdrf_gx_piece: write = 0 reads
- * the bytes [off, off + n) of container id into dev, 1 writes them); then each rank compresses the
+ * the bytes [off, off + n) of container id into dev and returns when they are there; write = 1
+ * enqueues the copy from dev on the back stream and returns at once, so dev must stay valid until
+ * hdrf_gx_compress has returned, which runs after the copies); then each rank compresses the
  * containers its flush walk closed (hdrf_gx_compress: the Lz4Codec files of DN/DataDeduplicator.java
  * :748-797, returns how many).  hdrf_amd/node.py plans and runs the transfers. */
 int hdrf_gx_alloc_io(hdrf_ctx *ctx, uint8_t *alloc_in, uint8_t *alloc_out);

@@ -40,14 +40,17 @@ class Loopback:
         if int(self.ctxs[0].cfg.compressor) != 2:
             return
         io = [c.gx_alloc_io() for c in self.ctxs]
+        held = []                                # a write is enqueued: keep its source until gx_compress
         for q, s, cid, a, b in self.pieces.batch([x[0] for x in io], [x[1] for x in io]):
             buf = torch.empty(b - a, dtype=torch.uint8, device=self.dev)
             torch.cuda.synchronize()
             self.ctxs[q].gx_piece(cid, a, b - a, buf.data_ptr(), write=False)
             self.ctxs[s].gx_piece(cid, a, b - a, buf.data_ptr(), write=True)
+            held.append(buf)
             self.moved = getattr(self, "moved", 0) + (b - a)
         for c in self.ctxs:
             c.gx_compress()
+        del held
 
     def _a2a(self, send, recv, counts, w):
         """counts[s][d] records from rank s to rank d; returns recv counts [d][s]."""

@@ -73,6 +73,46 @@ def test_bench_batches_4gib_depth3_full_state():
     ctx.close()
 
 
+@pytest.mark.timeout(1200)
+def test_config4_bench_batches_depth5_full_state():
+    """BASELINE config 4 at the bench's exact shape (bench.py --workload config4 defaults): mixed-
+    entropy 128 MiB corpus blocks (random / text / binary segments), batches of 32, depth 5 (both
+    batches in flight before the first wait), arena_slots 1792, compressor 2 (the reference default,
+    DN/DataNode.java:438) with 32 MiB containers, so closed containers become Lz4Codec files on the
+    LZ4 streams while the next batch is placed.  Every block's END offsets, digests, is_new,
+    storeSize and placement, then the full index, allocator, recipes and EVERY container (closed:
+    the Lz4Codec file byte for byte; open: raw bytes) equal the sequential oracle's
+    (DN/DataDeduplicator.java:702-836 with lz4 r123 + BlockCompressorStream)."""
+    B, nbatch = 32, 2
+    nb = B * nbatch
+    spb = S // SEG
+    roots = corpus_roots(SEED, 500000, 512, spb)[: nb * spb]      # the bench's first 64 blocks
+    ctx = Context(max_block_bytes=S, max_batch_blocks=B, index_log2=25, arena_slots=1792, compressor=2)
+    total = nb * S + 4096
+    dev = ctx.dev_alloc(total)
+    ctx.corpus_fill(dev, roots, nb, spb, SEG, SEED, mixed=True)
+    blocks = [ctx.d2h(dev + b * S, S) for b in range(nb)]
+    ids = list(range(nb))
+    ora = Oracle(compressor=2)
+    expect = ora.reduce_many_full(blocks, ids, _threads())
+    for k in range(nbatch):            # depth 5: every batch in flight before the first wait
+        g = range(k * B, (k + 1) * B)
+        ctx.submit_batch([dev + b * S for b in g], [S] * B, [total - b * S for b in g], [ids[b] for b in g])
+    for k in range(nbatch):
+        ctx.wait_batch()
+        assert ctx.last_nblocks() == B
+        for i in range(B):
+            compare_block(ctx.batch_result(i), expect[k * B + i], tag=f"config4 batch {k} block {i}")
+    st = ctx.stats()
+    assert st["closed_containers"] >= 64, f"only {st['closed_containers']} containers closed"
+    assert st["closed_file_bytes"] < st["closed_raw_bytes"], "Lz4Codec files must compress the text/binary data"
+    compare_state(ctx, ora, ids, tag="config4 bench shape")
+    for b in (0, nb - 1):
+        assert np.array_equal(ctx.reconstruct_block(ids[b]), blocks[b]), f"block {b} not rebuilt"
+    ctx.dev_free(dev)
+    ctx.close()
+
+
 def _ragged_batch(seed, k0, n, pool):
     """n blocks of 1-2 MiB: random bytes with 64 KiB pieces copied from earlier blocks (pool)."""
     rng = np.random.default_rng(seed)

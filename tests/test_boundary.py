@@ -215,6 +215,55 @@ def test_durable_drain_with_batches_in_flight(compressor):
     ctx.close()
 
 
+def test_capacity_refusal_names_its_recovery():
+    """a durable-container submit refused because the batches IN FLIGHT bound the ring
+    (their closes cannot be drained yet) names hdrf_wait_batch; the documented recovery (wait the
+    oldest, drain, submit again) succeeds.  With nothing in flight, undrained containers alone name
+    hdrf_drain_containers.  Every block still equals the oracle's, every drained file its container."""
+    cmax = 1 << 20
+    blocks = _blocks(81, 10, 2 << 20, dup_div=8)
+    ids = [6800 + i for i in range(len(blocks))]
+    ctx = Context(container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=32,
+                  retain_containers=1)
+    ora = Oracle(max_size=cmax)
+    disk, pend, refused_inflight = {}, [], 0
+
+    def complete():
+        ctx.wait_batch()
+        ob, oi = pend.pop(0)
+        compare_block(ctx.batch_result(0), ora.reduce(ob, oi), tag=f"recovery block {oi}")
+
+    for b, i in zip(blocks, ids):
+        try:
+            ctx.submit_host([b.ctypes.data], [len(b)], [i])
+        except HdrfError as e:
+            assert e.code == -4 and "hdrf_wait_batch" in str(e), str(e)
+            refused_inflight += 1
+            complete()                                       # the oldest batch, then its containers
+            _apply(disk, ctx.drain_containers())
+            ctx.submit_host([b.ctypes.data], [len(b)], [i])  # the retry succeeds
+        pend.append((b, i))
+    assert refused_inflight > 0, "the ring never filled with a batch in flight"
+    while pend:
+        complete()
+    # nothing in flight, nothing drained: the refusal names the drain
+    extra = _blocks(82, 6, 2 << 20, dup_div=8)
+    with pytest.raises(HdrfError) as ei:
+        for j, b in enumerate(extra):
+            ctx.reduce_block(b, 6900 + j)
+            ora.reduce(b, 6900 + j)
+    assert ei.value.code == -4 and "hdrf_drain_containers first" in str(ei.value), str(ei.value)
+    _apply(disk, ctx.drain_containers())
+    alloc = ora.allocator()
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, oc = ora.container(cid)
+            if od is not None and cid in disk:
+                assert bytes(disk[cid][0]) == bytes(od), f"container {cid}"
+    ctx.close()
+
+
 def test_pipeline_depth_is_refused_not_waited():
     """A submit beyond HDRF_PIPELINE_DEPTH returns HDRF_E_CAPACITY (the caller's awaitOldest pairs
     one to one with its submits) and leaves the batches in flight untouched."""

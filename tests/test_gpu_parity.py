@@ -49,9 +49,11 @@ def test_many_segments_random_large():
 
 @pytest.mark.parametrize("kind", ["periodic", "zeros", "text", "sparse"])
 def test_more_boundaries_than_stitch_nodes(kind):
-    """A 132 MiB block at 64 KiB segments has 2112 segment boundaries, more than the 2048 irregular
-    ones the stitch path follows in LDS (chunk.hip kStitchNodes): past them the fallback walk takes
-    over, with the same cuts."""
+    """A 132 MiB block at 64 KiB segments has 2112 segment boundaries, more than the 1,024 irregular
+    boundaries one LDS window of the stitch holds (chunk.hip kStitchNodes): the windowed stitch
+    compacts the ordered node list window by window and follows any number of them (round 3), and a
+    path that ends at an unrepaired boundary continues with the sequential walk; the cuts are the
+    oracle's either way."""
     blk = make_block(kind, 23, 132 * 1024 * 1024 + 77)
     run_sequence([blk], segment_bytes=1 << 16, max_block_bytes=136 << 20, max_batch_blocks=1)
 

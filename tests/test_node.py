@@ -229,6 +229,135 @@ def test_node_loopback_compressor2_matches_single_sequence(G, pipelined):
         c.close()
 
 
+def _load_ranks(ctxs, blocks_per_rank, id0):
+    per_rank, devs = [], []
+    for r, blks in enumerate(blocks_per_rank):
+        ptrs, lens, rd, ids = [], [], [], []
+        for i, blk in enumerate(blks):
+            p = ctxs[r].dev_alloc(len(blk) + 4096)
+            ctxs[r].h2d(p, blk)
+            devs.append((ctxs[r], p))
+            ptrs.append(p); lens.append(len(blk)); rd.append(len(blk) + 4096); ids.append(id0 + 16 * r + i)
+        per_rank.append((ptrs, lens, rd, ids))
+    return per_rank, devs
+
+
+@pytest.mark.gpu
+def test_node_owner_table_full_is_a_clean_error():
+    """an owner whose index partition fills during hdrf_gx_owner (device error 2; the
+    failing records' owner slots are never written) must not touch the table again.  Its X2
+    responses are "not created, not the minimum" for every record, so no source designates a
+    chunk or sends an X3 location, and hdrf_gx_place reports HDRF_E_CAPACITY ("index table full").
+    The device keeps working: a fresh node on the same GPU reduces correctly afterwards."""
+    import torch
+    from node_harness import Loopback, open_ranks
+    from hdrf_amd.lib import HdrfError
+    G = 2
+    blocks = [[make_block("random", 900 + 2 * r + i, 700_000) for i in range(2)] for r in range(G)]
+    ctxs = open_ranks(G, container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=4, index_log2=10,
+                      arena_slots=64)
+    lb = Loopback(ctxs)
+    per_rank, devs = _load_ranks(ctxs, blocks, 0x900)
+    c1 = [ctxs[r].gx_front(*per_rank[r], 2 * r, lb.x1s[r].data_ptr()) for r in range(G)]
+    r1 = lb._a2a(lb.x1s, lb.x1r, c1, lb.w[0])
+    assert all(sum(r1[d]) > 1024 for d in range(G)), "each owner must receive more digests than its 1024 entries"
+    for d in range(G):
+        ctxs[d].gx_owner(lb.x1r[d].data_ptr(), r1[d], lb.x2s[d].data_ptr())
+    torch.cuda.synchronize()
+    for d in range(G):
+        x2 = lb.x2s[d].view(G, lb.cap, 2)
+        for s_ in range(G):
+            assert int(x2[s_, :r1[d][s_]].abs().sum()) == 0, "responses after a full table must decide nothing"
+    lb._a2a(lb.x2s, lb.x2r, r1, lb.w[1])
+    for r in range(G):
+        ctxs[r].gx_decide(lb.x2r[r].data_ptr())
+    a = None
+    for r in range(G):
+        a = ctxs[r].gx_flush(a)
+    with pytest.raises(HdrfError) as ei:
+        ctxs[0].gx_place(a, lb.x3s[0].data_ptr())
+    assert ei.value.code == -4 and "index table full" in str(ei.value), str(ei.value)
+    torch.cuda.synchronize()
+    for c, p in devs:
+        c.dev_free(p)
+    for c in ctxs:
+        c.close()
+    # the GPU is healthy: a node with a large enough partition reduces the same blocks exactly
+    from oracle.oracle import Oracle
+    ctxs = open_ranks(G, container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=4, index_log2=16,
+                      arena_slots=64)
+    lb = Loopback(ctxs)
+    per_rank, devs = _load_ranks(ctxs, blocks, 0x900)
+    lb.batch(per_rank)
+    ora = Oracle(max_size=1 << 20)
+    for r in range(G):
+        for i in range(2):
+            compare_block(ctxs[r].batch_result(i), ora.reduce(blocks[r][i], 0x900 + 16 * r + i), tag=f"after error r{r} b{i}")
+    for c, p in devs:
+        c.dev_free(p)
+    for c in ctxs:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_node_compress_step_is_enforced_and_idempotent():
+    """under compressor 2 on a node-global context, hdrf_gx_commit refuses a batch whose
+    closed containers were not compressed (their reads would come from an unwritten compressed
+    arena), and a second hdrf_gx_compress changes nothing (file lengths and closed_file_bytes stay
+    those of one pass)."""
+    import torch  # noqa: F401
+    from node_harness import Loopback, open_ranks
+    from hdrf_amd.lib import HdrfError
+    from oracle.oracle import Oracle
+    G, cmax = 2, 1 << 20
+    blocks = [[make_block("text", 950 + 2 * r + i, 1_500_000) for i in range(2)] for r in range(G)]
+    ctxs = open_ranks(G, compressor=2, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=4,
+                      index_log2=18, arena_slots=64)
+    lb = Loopback(ctxs)
+    per_rank, devs = _load_ranks(ctxs, blocks, 0xA00)
+    c1 = [ctxs[r].gx_front(*per_rank[r], 2 * r, lb.x1s[r].data_ptr()) for r in range(G)]
+    r1 = lb._a2a(lb.x1s, lb.x1r, c1, lb.w[0])
+    for d in range(G):
+        ctxs[d].gx_owner(lb.x1r[d].data_ptr(), r1[d], lb.x2s[d].data_ptr())
+    lb._a2a(lb.x2s, lb.x2r, r1, lb.w[1])
+    for r in range(G):
+        ctxs[r].gx_decide(lb.x2r[r].data_ptr())
+    a = None
+    for r in range(G):
+        a = ctxs[r].gx_flush(a)
+    c3 = [ctxs[r].gx_place(a, lb.x3s[r].data_ptr()) for r in range(G)]
+    r3 = lb._a2a(lb.x3s, lb.x3r, c3, lb.w[2])
+    closers = [r for r in range(G) if ctxs[r].stats()["closed_containers"] > 0]
+    assert closers, "some rank must close a container"
+    with pytest.raises(HdrfError) as ei:
+        ctxs[closers[0]].gx_commit(lb.x3r[closers[0]].data_ptr(), r3[closers[0]])
+    assert ei.value.code == -1 and "hdrf_gx_compress" in str(ei.value)
+    lb._compress()
+    before = [ctxs[r].stats()["closed_file_bytes"] for r in range(G)]
+    for r in range(G):
+        assert ctxs[r].gx_compress() == 0, "a second compress is a no-op"
+    assert [ctxs[r].stats()["closed_file_bytes"] for r in range(G)] == before
+    for d in range(G):
+        ctxs[d].gx_commit(lb.x3r[d].data_ptr(), r3[d])
+    ora = Oracle(compressor=2, max_size=cmax)
+    for r in range(G):
+        for i in range(2):
+            compare_block(ctxs[r].batch_result(i), ora.reduce(blocks[r][i], 0xA00 + 16 * r + i), tag=f"c2 r{r} b{i}")
+    alloc, n_closed = ora.allocator(), 0
+    for t in range(3):
+        for cid in range(t << 22, int.from_bytes(alloc[3 * t:3 * t + 3], "big") + 1):
+            od, oc = ora.container(cid)
+            if od is not None and oc:
+                files = [f for f, closed in (c.container(cid) for c in ctxs) if closed]
+                assert files == [od], f"container {cid:#x}: Lz4Codec file differs"
+                n_closed += 1
+    assert n_closed > 0
+    for c, p in devs:
+        c.dev_free(p)
+    for c in ctxs:
+        c.close()
+
+
 @pytest.mark.gpu
 def test_node_context_rejects_single_node_calls():
     from hdrf_amd.lib import Context, HdrfError
