@@ -247,7 +247,7 @@ def test_capacity_refusal_names_its_recovery():
     while pend:
         complete()
     # nothing in flight, nothing drained: the refusal names the drain
-    extra = _blocks(82, 6, 2 << 20, dup_div=8)
+    extra = _blocks(82, 24, 2 << 20, dup_div=8)
     with pytest.raises(HdrfError) as ei:
         for j, b in enumerate(extra):
             ctx.reduce_block(b, 6900 + j)
