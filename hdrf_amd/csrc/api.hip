@@ -143,7 +143,10 @@ struct hdrf_ctx {
     uint8_t *d_rd = nullptr;                     // reconstruction scratch (grows)
     uint64_t rd_cap = 0;
     // host state
-    uint32_t batch = 0;
+    uint32_t batch = 0;                              // batch ids: grow over the context's life (never reset)
+    uint32_t epoch = 1;                              // index generation in the tag words (1..255)
+    uint32_t bfirst = 1;                             // first batch id of the current epoch
+    uint32_t scratch_epoch[2] = {0, 0};              // node-global: generation of each scratch table
     int have_alloc = 0;
     int last_nblocks = 0;
     AllocState h_alloc{};
@@ -238,10 +241,16 @@ struct hdrf_ctx {
     std::unique_lock<std::recursive_mutex> lk_ =                                                     \
         (c) ? std::unique_lock<std::recursive_mutex>((c)->mu) : std::unique_lock<std::recursive_mutex>()
 
-static unsigned long long tag_mask(const hdrf_ctx *ctx)
+// tag key of the index (common.hpp tag_word): the current epoch over the tag-bit mask (all ones
+// except under the debug_tag_bits collision hook)
+static unsigned long long tag_bits(const hdrf_ctx *ctx)
 {
     const int bits = ctx->cfg.debug_tag_bits;
-    return (bits <= 0 || bits >= 64) ? ~0ull : ((1ull << bits) - 1);
+    return ((bits <= 0 || bits >= 56) ? ~0ull : ((1ull << bits) - 1)) & kTag56;
+}
+static unsigned long long tag_mask(const hdrf_ctx *ctx)
+{
+    return ((unsigned long long)ctx->epoch << 56) | tag_bits(ctx);
 }
 
 static int set_err(hdrf_ctx *ctx, int code, const std::string &msg)
@@ -448,7 +457,7 @@ static int drain(hdrf_ctx *ctx)
     return rc;
 }
 
-static int init_state(hdrf_ctx *ctx)
+static int init_state(hdrf_ctx *ctx, bool fresh)
 {
     (void)drain(ctx);
     AllocState a{};
@@ -459,11 +468,23 @@ static int init_state(hdrf_ctx *ctx)
     }
     for (auto &S : ctx->sl) HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
-    // the index and allocator belong to the back stream (also for the node-global back phases)
+    // the index and allocator belong to the back stream (also for the node-global back phases).
+    // A fresh index is a new epoch: every entry tagged with another one is empty (common.hpp), so
+    // the 2^k x 64 B table is cleared only at open and once every 255 resets; batch ids keep
+    // growing, and the claim rule tells this epoch's entries by batch >= bfirst (index.hip).
     hipStream_t ist = ctx->stB;
-    HIPCK(launch_index_clear(ctx->d_tab, ctx->cfg.index_log2, ctx->d_alloc, a, ist));
+    const bool clear = fresh || ctx->epoch >= 255;
+    ctx->epoch = clear ? 1 : ctx->epoch + 1;
+    if (fresh) ctx->batch = 0;
+    ctx->bfirst = ctx->batch + 1;
+    HIPCK(launch_index_clear(ctx->d_tab, clear ? ctx->cfg.index_log2 : -1, ctx->d_alloc, a, ist));
+    if (fresh)
+        for (int i = 0; i < 2; i++)
+            if (ctx->d_scratch[i]) {
+                HIPCK(hipMemsetAsync(ctx->d_scratch[i], 0, sizeof(IndexEntry) << ctx->scratch_log2, ist));
+                ctx->scratch_epoch[i] = 0;
+            }
     ctx->h_alloc = a;
-    ctx->batch = 0;
     ctx->have_alloc = 0;
     ctx->containers.clear();
     ctx->slot_owner.clear();
@@ -576,7 +597,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
             rc = set_err(ctx, HDRF_E_HIP, "hipMemset failed");
     }
     ctx->timing = c.timing != 0;
-    if (!rc) rc = init_state(ctx);
+    if (!rc) rc = init_state(ctx, true);
     if (rc) {
         fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
         free_all(ctx);
@@ -607,7 +628,7 @@ extern "C" int hdrf_reset(hdrf_ctx *ctx)
     for (int i = 0; i < hdrf_ctx::kRx; i++)
         if (ctx->rx[i].state.load() == 1)
             return set_err(ctx, HDRF_E_INVAL, "a block is being received (hdrf_submit_slot or hdrf_rx_cancel first)");
-    return init_state(ctx);
+    return init_state(ctx, false);
 }
 
 // container id -> slot bookkeeping after a batch
@@ -812,7 +833,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     Marker mb;
     mb.ev = ctx->timing ? S.evB : nullptr;
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_tab, c.index_log2, cur,
-                       tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap, S.d_flags, S.d_tilesum, ctx->ntiles,
+                       ctx->bfirst, tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap, S.d_flags, S.d_tilesum, ctx->ntiles,
                        S.d_err, Bst, &mb, decide_desig ? S.d_dcnt : nullptr));
     HIPCK(launch_index_finalize(S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, ctx->d_tab, S.d_slot, S.d_flags, S.d_dcnt,
                                 Bst));
@@ -1886,9 +1907,14 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig,
                      S.d_queue, ctx->sha_long, st, &mk));
     // local aggregation: a fresh scratch table, every entry "created" in batch 1
-    HIPCK(hipMemsetAsync(ctx->d_scratch[si], 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
+    // (a fresh scratch table per batch: the next epoch of the slot's table, cleared every 255 uses)
+    if (++ctx->scratch_epoch[si] > 255) {
+        HIPCK(hipMemsetAsync(ctx->d_scratch[si], 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
+        ctx->scratch_epoch[si] = 1;
+    }
+    const unsigned long long skey = ((unsigned long long)ctx->scratch_epoch[si] << 56) | tag_bits(ctx);
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_scratch[si],
-                       ctx->scratch_log2, 1u, tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap,
+                       ctx->scratch_log2, 1u, 1u, skey, S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap,
                        S.d_flags, S.d_tilesum, ctx->ntiles, S.d_err, st, &mk));
     HIPCK(launch_gx_emit(c.hasher, S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, S.d_dig, ctx->d_scratch[si],
                          S.d_slot, S.d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gxe[si], S.d_err, st));
@@ -1952,7 +1978,7 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
     hipStream_t st = ctx->stB;
     HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
     HIPCK(launch_gx_owner(ctx->cfg.hasher, x1_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap,
-                          ctx->G, ctx->d_tab, ctx->cfg.index_log2, S.gx_batch, tag_mask(ctx), ctx->d_oslot,
+                          ctx->G, ctx->d_tab, ctx->cfg.index_log2, S.gx_batch, ctx->bfirst, tag_mask(ctx), ctx->d_oslot,
                           ctx->d_oflags, S.d_coll, S.d_ncoll, ctx->coll_cap, x2_send, S.d_err, st));
     // no host round trip: a device error (S.d_err) is read back with the batch by hdrf_gx_place, and
     // the X2 exchange may be enqueued on stream B right behind this kernel (hdrf_gx_stream)
@@ -2405,9 +2431,10 @@ static void entry_digest(const IndexEntry &e, int H, uint8_t *out)
 {
     if (H == 20) {                                   // SHA-1: bytes 0..7 kept in dig[3..4]
         std::memcpy(out, &e.dig[3], 8);
-    } else {
-        unsigned long long tag = (e.batch & 0x80000000u) ? 0ull : e.tag;
-        std::memcpy(out, &tag, 8);
+    } else {                                         // SHA-224: bytes 0..6 in the tag, 7 in ncopy
+        const unsigned long long t = e.tag & kTag56;
+        std::memcpy(out, &t, 7);
+        out[7] = (uint8_t)(e.ncopy >> 8);
     }
     std::memcpy(out + 8, e.dig, H == 20 ? 12 : H - 8);
 }
@@ -2416,21 +2443,19 @@ extern "C" int hdrf_index_get(hdrf_ctx *ctx, const uint8_t *digest, uint8_t out1
 {
     HDRF_LOCK(ctx);
     if (!ctx || !digest) return HDRF_E_INVAL;
-    unsigned long long tag;
-    std::memcpy(&tag, digest, 8);
-    tag &= tag_mask(ctx);
-    const uint32_t z = tag == 0 ? 0x80000000u : 0u;
-    if (tag == 0) tag = 1;
+    uint32_t dw[2];
+    std::memcpy(dw, digest, 8);
+    const unsigned long long key = tag_mask(ctx), tag = tag_word(dw, key);
     const uint64_t mask = (1ull << ctx->cfg.index_log2) - 1;
-    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - ctx->cfg.index_log2);
+    uint64_t h = tag_home(tag, ctx->cfg.index_log2);
     if (int rc = drain(ctx)) return rc;
     for (uint64_t probe = 0; probe <= mask; probe++) {
         IndexEntry e;
         HIPCK(hipMemcpy(&e, ctx->d_tab + h, sizeof e, hipMemcpyDeviceToHost));
-        if (e.tag == 0) return 0;
+        if (!tag_live(e.tag, key)) return 0;
         uint8_t full[28];
         entry_digest(e, ctx->H, full);
-        if (e.tag == tag && (e.batch & 0x80000000u) == z && std::memcmp(full, digest, ctx->H) == 0) {
+        if (e.tag == tag && std::memcmp(full, digest, ctx->H) == 0) {
             if (out11) encode_value(e, out11);
             return 1;
         }
@@ -2481,7 +2506,8 @@ extern "C" int64_t hdrf_index_count(hdrf_ctx *ctx)
     std::vector<IndexEntry> tab;
     if (int rc = fetch_table(ctx, tab)) return rc;
     int64_t n = 0;
-    for (auto &e : tab) n += e.tag != 0;
+    const unsigned long long key = tag_mask(ctx);
+    for (auto &e : tab) n += tag_live(e.tag, key);
     return n;
 }
 
@@ -2493,8 +2519,9 @@ extern "C" int64_t hdrf_index_dump(hdrf_ctx *ctx, uint8_t *keys, uint8_t *vals, 
     if (int rc = fetch_table(ctx, tab)) return rc;
     const int H = ctx->H;
     std::vector<std::vector<uint8_t>> rows;
+    const unsigned long long key = tag_mask(ctx);
     for (auto &e : tab) {
-        if (e.tag == 0) continue;
+        if (!tag_live(e.tag, key)) continue;
         std::vector<uint8_t> r(H + 11);
         entry_digest(e, H, r.data());
         encode_value(e, r.data() + H);
@@ -2549,7 +2576,7 @@ extern "C" int hdrf_index_load(hdrf_ctx *ctx, const uint8_t *keys, const uint8_t
     HIPCK(hipMemcpyAsync(R + o_v, vals, (size_t)n * 11, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(R + o_err, 0, 4, st));
     HIPCK(launch_index_load(ctx->cfg.hasher, (const uint32_t *)(R + o_dw), R + o_v, (int)n, ctx->d_tab,
-                            ctx->cfg.index_log2, tag_mask(ctx), (int *)(R + o_err), st));
+                            ctx->cfg.index_log2, tag_mask(ctx), ++ctx->batch, (int *)(R + o_err), st));
     int err = 0;
     HIPCK(hipMemcpyAsync(&err, R + o_err, 4, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));

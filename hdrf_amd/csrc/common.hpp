@@ -14,6 +14,7 @@
 
 namespace hdrf {
 
+#define HDRF_GLOBAL_FWD __attribute__((address_space(1)))
 constexpr int kWave = 64;
 constexpr int kMaxBatch = 64;        // one bit per block of the batch in IndexEntry::mask
 // Lane walker (chunk.hip): one lane walks one speculative segment of seg_len bytes; a wave holds
@@ -25,17 +26,19 @@ constexpr int kRepairCuts = 4096;    // a repair walk gives up after this many c
 constexpr int kRepairBytes = 2 << 20;  // ... or this many bytes past its start
 constexpr int kSegMinWin = 4;        // seg_len bounds, in units of window + 2 (702 B)
 constexpr int kSegMaxWin = 20;        // seg_len / 702 + 2 + kLaneOver <= kLdsCuts
-constexpr uint64_t kEmptyTag = 0;
 
-// Index entry: 64 B.  tag = first 8 digest bytes (0 remapped to 1 with flag bit 31 of `batch`);
-// `dig` holds digest bytes 8..27.  ncopy/cid/start/stop are the 11-byte Redis value
-// (chunkMeta.getMeta, DN/chunkMeta.java:62-77) in unpacked form.
+// Index entry: 64 B.  tag = the table generation ("epoch", 1..255) in bits 56..63 over the first 7
+// digest bytes; an entry whose tag carries another epoch is EMPTY, so a fresh index (hdrf_reset)
+// is one epoch bump instead of 2^k x 64 B of zero stores (a real clear only every 255 resets and
+// at open).  `dig` holds digest bytes 8..27; the 8th digest byte lives in dig[4] (SHA-1: dig[3..4]
+// hold bytes 0..7) or in ncopy bits 8..15 (SHA-224).  ncopy (bits 0..7) / cid / start / stop are
+// the 11-byte Redis value (chunkMeta.getMeta, DN/chunkMeta.java:62-77) in unpacked form.
 struct alignas(64) IndexEntry {
     unsigned long long tag;
     unsigned long long mask;    // batch-local: bit b = block b of the batch holds the digest
     unsigned long long first;   // batch-local: max over ((63-b)<<32 | chunk index)
-    uint32_t batch;             // batch id that created the entry (| 0x80000000 if tag remapped)
-    uint32_t ncopy;
+    uint32_t batch;             // batch id that created the entry (ids only grow over a context's life)
+    uint32_t ncopy;             // bits 0..7 nCopy, bits 8..15 digest byte 7 (SHA-224)
     uint32_t cid;
     uint32_t start;
     uint32_t stop;
@@ -43,6 +46,47 @@ struct alignas(64) IndexEntry {
 
 };
 static_assert(sizeof(IndexEntry) == 64, "IndexEntry must be one 64-B line");
+
+// Tag key of a table: (epoch << 56) | the tag-bit mask (all ones except under the collision test
+// hook, debug_tag_bits).  tag_word: the entry tag a digest must carry; tag_live: an entry of the
+// current epoch; tag_home: the digest's home slot (independent of the epoch).
+constexpr unsigned long long kTag56 = 0x00FFFFFFFFFFFFFFull;
+__host__ __device__ __forceinline__ unsigned long long tag_word(const uint32_t *dw, unsigned long long key)
+{
+    return ((((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & key) & kTag56) | (key & ~kTag56);
+}
+__host__ __device__ __forceinline__ bool tag_live(unsigned long long t, unsigned long long key)
+{
+    return ((t ^ key) >> 56) == 0;
+}
+__host__ __device__ __forceinline__ uint64_t tag_home(unsigned long long t, int log2cap)
+{
+    return ((t & kTag56) * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
+}
+// the full digest equals the entry's (the caller matched the tag word: bytes 0..6)
+template <int HW>
+__host__ __device__ __forceinline__ bool entry_matches(const IndexEntry &e, const uint32_t *dw)
+{
+#pragma unroll
+    for (int i = 2; i < HW; i++)
+        if (e.dig[i - 2] != dw[i]) return false;
+    if (HW == 5) return e.dig[3] == dw[0] && e.dig[4] == dw[1];
+    return ((e.ncopy >> 8) & 0xffu) == (dw[1] >> 24);
+}
+// a claimed entry's digest bytes (nCopy is written by the chunk that SETs the value)
+template <int HW>
+__device__ __forceinline__ void store_dig(IndexEntry *e, const uint32_t *dw)
+{
+#pragma unroll
+    for (int i = 2; i < HW; i++) e->dig[i - 2] = dw[i];
+    if (HW == 5) { e->dig[3] = dw[0]; e->dig[4] = dw[1]; }
+    else e->ncopy = (dw[1] >> 24) << 8;
+}
+// nCopy (bits 0..7 of ncopy) without touching the SHA-224 digest byte above it
+__device__ __forceinline__ void set_ncopy(IndexEntry *e, uint32_t n)
+{
+    *(HDRF_GLOBAL_FWD uint8_t *)&e->ncopy = (uint8_t)n;
+}
 
 // Per-batch block descriptor (device side).
 struct BlockDesc {

@@ -70,37 +70,14 @@ __device__ __forceinline__ void own_record(IndexEntry *e, uint32_t gpos, uint32_
     atomicAdd(&e->mask, (unsigned long long)cnt);
 }
 
-template <int HW>
-__device__ __forceinline__ bool own_matches(const IndexEntry &e, const uint32_t *dw, uint32_t z)
-{
-    if ((e.batch & 0x80000000u) != z) return false;
-#pragma unroll
-    for (int i = 2; i < HW; i++)
-        if (e.dig[i - 2] != dw[i]) return false;
-    if (HW == 5 && (e.dig[3] != dw[0] || e.dig[4] != dw[1])) return false;
-    return true;
-}
-
-__device__ __forceinline__ unsigned long long own_tag(const uint32_t *dw, uint32_t &zflag, unsigned long long tag_mask)
-{
-    unsigned long long t = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
-    zflag = (t == 0) ? 0x80000000u : 0u;
-    return t == 0 ? 1ull : t;
-}
-
-template <int HW>
-__device__ __forceinline__ void own_store_dig(IndexEntry *e, const uint32_t *dw)
-{
-#pragma unroll
-    for (int i = 2; i < HW; i++) e->dig[i - 2] = dw[i];
-    if (HW == 5) { e->dig[3] = dw[0]; e->dig[4] = dw[1]; }
-}
-
 // oflags bit 3 = applied in claim
+// (claim rules as index.hip idx_claim_kernel: epoch-empty entries are claimed by CAS on the tag read,
+// the claimer initialises the batch-local fields with its own record, entries of earlier batches of
+// this epoch are applied at once, the rest deferred)
 template <int HW>
 __global__ void __launch_bounds__(256) own_claim_kernel(const uint32_t *__restrict__ x1, const int64_t *__restrict__ counts,
                                                         int64_t cap, IndexEntry *__restrict__ tab, int log2cap,
-                                                        uint32_t cur, unsigned long long tag_mask,
+                                                        uint32_t cur, uint32_t bfirst, unsigned long long key,
                                                         uint32_t *__restrict__ oslot, uint8_t *__restrict__ oflags,
                                                         int *__restrict__ err)
 {
@@ -112,44 +89,45 @@ __global__ void __launch_bounds__(256) own_claim_kernel(const uint32_t *__restri
     uint32_t dw[HW];
 #pragma unroll
     for (int q = 0; q < HW; q++) dw[q] = rec[q];
-    uint32_t z;
-    const unsigned long long tag = own_tag(dw, z, tag_mask);
+    const unsigned long long tag = tag_word(dw, key);
     const uint64_t mask = (1ull << log2cap) - 1;
-    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
+    uint64_t h = tag_home(tag, log2cap);
     bool mine = false;
     for (uint64_t probe = 0;; probe++) {
         if (probe > mask) { atomicOr(err, 2); return; }
         IndexEntry *e = tab + h;
         unsigned long long t = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == kEmptyTag) {
-            unsigned long long old = atomicCAS(&e->tag, kEmptyTag, tag);
-            if (old == kEmptyTag) {
-                e->batch = cur | z;
-                own_store_dig<HW>(e, dw);
-                mine = true;
-                break;
-            }
+        while (!tag_live(t, key)) {
+            const unsigned long long old = atomicCAS(&e->tag, t, tag);
+            if (old == t) { mine = true; break; }
             t = old;
+        }
+        if (mine) {
+            e->batch = cur;
+            e->first = (unsigned long long)(0xffffffffu - rec[HW]);    // this record (own_record)
+            e->mask = (unsigned long long)rec[HW + 1];
+            store_dig<HW>(e, dw);
+            break;
         }
         if (t == tag) break;
         h = (h + 1) & mask;
     }
     oslot[r] = (uint32_t)h;
     IndexEntry *e = tab + h;
-    bool apply = mine;
+    bool apply = false;
     if (!mine) {
-        const uint32_t bt = e->batch & 0x7fffffffu;
-        apply = bt != 0 && bt != cur && own_matches<HW>(*e, dw, z);
+        const uint32_t bt = e->batch;
+        apply = bt >= bfirst && bt != cur && entry_matches<HW>(*e, dw);
+        if (apply) own_record(e, rec[HW], rec[HW + 1]);
     }
-    if (apply) own_record(e, rec[HW], rec[HW + 1]);
-    oflags[r] = apply ? 8 : 0;
+    oflags[r] = (mine || apply) ? 8 : 0;
 }
 
 template <int HW>
 __global__ void __launch_bounds__(256) own_apply_kernel(const uint32_t *__restrict__ x1, const int64_t *__restrict__ counts,
                                                         int64_t cap, IndexEntry *__restrict__ tab,
                                                         const uint32_t *__restrict__ oslot, const uint8_t *__restrict__ oflags,
-                                                        unsigned long long tag_mask, uint32_t *__restrict__ coll,
+                                                        uint32_t *__restrict__ coll,
                                                         uint32_t *__restrict__ ncoll, int coll_cap, int *__restrict__ err)
 {
     const int s = blockIdx.y;
@@ -161,10 +139,8 @@ __global__ void __launch_bounds__(256) own_apply_kernel(const uint32_t *__restri
     uint32_t dw[HW];
 #pragma unroll
     for (int q = 0; q < HW; q++) dw[q] = rec[q];
-    uint32_t z;
-    (void)own_tag(dw, z, tag_mask);
     IndexEntry *e = tab + oslot[r];
-    if (own_matches<HW>(*e, dw, z)) {
+    if (entry_matches<HW>(*e, dw)) {
         own_record(e, rec[HW], rec[HW + 1]);
     } else {
         const uint32_t j = atomicAdd(ncoll, 1u);
@@ -176,7 +152,7 @@ __global__ void __launch_bounds__(256) own_apply_kernel(const uint32_t *__restri
 // exact sequential re-probe of 8-byte tag collisions (one thread)
 template <int HW>
 __global__ void own_slow_kernel(const uint32_t *__restrict__ x1, IndexEntry *__restrict__ tab, int log2cap, uint32_t cur,
-                                unsigned long long tag_mask, uint32_t *__restrict__ oslot,
+                                unsigned long long key, uint32_t *__restrict__ oslot,
                                 const uint32_t *__restrict__ coll, const uint32_t *__restrict__ ncoll, int coll_cap,
                                 int *__restrict__ err)
 {
@@ -188,18 +164,17 @@ __global__ void own_slow_kernel(const uint32_t *__restrict__ x1, IndexEntry *__r
         const uint32_t *rec = x1 + r * (HW + 2);
         uint32_t dw[HW];
         for (int q = 0; q < HW; q++) dw[q] = rec[q];
-        uint32_t z;
-        const unsigned long long tag = own_tag(dw, z, tag_mask);
+        const unsigned long long tag = tag_word(dw, key);
         uint64_t h = (oslot[r] + 1) & mask;
         for (uint64_t probe = 0;; probe++) {
             if (probe > mask) { *err |= 2; return; }
             IndexEntry *e = tab + h;
-            if (e->tag == kEmptyTag) {
-                e->tag = tag; e->batch = cur | z; e->mask = 0; e->first = 0;
-                own_store_dig<HW>(e, dw);
+            if (!tag_live(e->tag, key)) {
+                e->tag = tag; e->batch = cur; e->mask = 0; e->first = 0;
+                store_dig<HW>(e, dw);
                 break;
             }
-            if (e->tag == tag && own_matches<HW>(*e, dw, z)) break;
+            if (e->tag == tag && entry_matches<HW>(*e, dw)) break;
             h = (h + 1) & mask;
         }
         oslot[r] = (uint32_t)h;
@@ -234,12 +209,12 @@ __global__ void __launch_bounds__(256) own_decide_kernel(const uint32_t *__restr
     const uint32_t gpos = x1[r * rw + rw - 2];
     const uint32_t h = oslot[r];
     IndexEntry *e = tab + h;
-    const bool created = (e->batch & 0x7fffffffu) == cur;
+    const bool created = e->batch == cur;
     const bool holds = (uint32_t)e->first == 0xffffffffu - gpos;
     if (holds) {
         const uint32_t cnt = (uint32_t)e->mask;
         // chunkMeta.process: nCopy = old + 1 per later block (DN/chunkMeta.java:35-60), 1 when new
-        e->ncopy = (created ? cnt : e->ncopy + cnt) & 0xffu;
+        set_ncopy(e, created ? cnt : e->ncopy + cnt);
     }
     x2[2 * r] = h;
     x2[2 * r + 1] = (created ? 1u : 0u) | (holds ? 2u : 0u);
@@ -331,7 +306,7 @@ hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int ca
 }
 
 hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts, int64_t max_count, int64_t cap, int G,
-                           IndexEntry *tab, int log2cap, uint32_t cur, unsigned long long tag_mask, uint32_t *oslot,
+                           IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst, unsigned long long tag_mask, uint32_t *oslot,
                            uint8_t *oflags, uint32_t *coll, uint32_t *ncoll, int coll_cap, uint32_t *x2, int *err,
                            hipStream_t st)
 {
@@ -339,16 +314,16 @@ hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts
     dim3 g(gx_tiles(max_count), G);
     if (hipError_t e = hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st)) return e;
     if (hasher == 0) {
-        hipLaunchKernelGGL(own_claim_kernel<5>, g, dim3(256), 0, st, x1, counts, cap, tab, log2cap, cur, tag_mask, oslot,
-                           oflags, err);
-        hipLaunchKernelGGL(own_apply_kernel<5>, g, dim3(256), 0, st, x1, counts, cap, tab, oslot, oflags, tag_mask, coll,
+        hipLaunchKernelGGL(own_claim_kernel<5>, g, dim3(256), 0, st, x1, counts, cap, tab, log2cap, cur, bfirst, tag_mask,
+                           oslot, oflags, err);
+        hipLaunchKernelGGL(own_apply_kernel<5>, g, dim3(256), 0, st, x1, counts, cap, tab, oslot, oflags, coll,
                            ncoll, coll_cap, err);
         hipLaunchKernelGGL(own_slow_kernel<5>, dim3(1), dim3(64), 0, st, x1, tab, log2cap, cur, tag_mask, oslot, coll,
                            ncoll, coll_cap, err);
     } else {
-        hipLaunchKernelGGL(own_claim_kernel<7>, g, dim3(256), 0, st, x1, counts, cap, tab, log2cap, cur, tag_mask, oslot,
-                           oflags, err);
-        hipLaunchKernelGGL(own_apply_kernel<7>, g, dim3(256), 0, st, x1, counts, cap, tab, oslot, oflags, tag_mask, coll,
+        hipLaunchKernelGGL(own_claim_kernel<7>, g, dim3(256), 0, st, x1, counts, cap, tab, log2cap, cur, bfirst, tag_mask,
+                           oslot, oflags, err);
+        hipLaunchKernelGGL(own_apply_kernel<7>, g, dim3(256), 0, st, x1, counts, cap, tab, oslot, oflags, coll,
                            ncoll, coll_cap, err);
         hipLaunchKernelGGL(own_slow_kernel<7>, dim3(1), dim3(64), 0, st, x1, tab, log2cap, cur, tag_mask, oslot, coll,
                            ncoll, coll_cap, err);

@@ -21,33 +21,6 @@
 
 namespace hdrf {
 
-// tag = first 8 digest bytes (masked by tag_mask: all ones except under the collision test hook);
-// a zero tag is remapped to 1 with bit 31 of `batch` set.  For SHA-1 the entry's spare dig[3..4]
-// also hold digest bytes 0..7, so verification never depends on the tag alone.
-__device__ __forceinline__ unsigned long long make_tag(const uint32_t *dw, uint32_t &zflag,
-                                                       unsigned long long tag_mask)
-{
-    unsigned long long t = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
-    zflag = (t == 0) ? 0x80000000u : 0u;
-    return t == 0 ? 1ull : t;
-}
-
-__device__ __forceinline__ uint64_t home_slot(unsigned long long tag, int log2cap)
-{
-    return (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
-}
-
-template <int HW>
-__device__ __forceinline__ bool entry_matches(const IndexEntry &e, const uint32_t *dw, uint32_t z)
-{
-    if ((e.batch & 0x80000000u) != z) return false;
-#pragma unroll
-    for (int i = 2; i < HW; i++)
-        if (e.dig[i - 2] != dw[i]) return false;
-    if (HW == 5 && (e.dig[3] != dw[0] || e.dig[4] != dw[1])) return false;
-    return true;
-}
-
 // Block b holds the digest: set its batch-mask bit.  Only a REPEAT inside one block (the bit was
 // already set) records its key in `first` = max((63-b)<<32 | k+1); decide completes the max over
 // the minimum block's occurrences when that block has repeats.  One returning atomic per chunk.
@@ -58,25 +31,20 @@ __device__ __forceinline__ void record_occurrence(IndexEntry *e, int b, int k)
     if (old & bit) atomicMax(&e->first, ((unsigned long long)(63 - b) << 32) | (unsigned)(k + 1));
 }
 
-template <int HW>
-__device__ __forceinline__ void store_dig(IndexEntry *e, const uint32_t *dw)
-{
-#pragma unroll
-    for (int i = 2; i < HW; i++) e->dig[i - 2] = dw[i];
-    if (HW == 5) { e->dig[3] = dw[0]; e->dig[4] = dw[1]; }
-}
-
 // ---- claim: grid (ceil(cap_blk/256), nblocks) ---------------------------------------------
-// Probe by tag; CAS-claim empty slots.  The chunk's block bit / last occurrence are applied right
-// here when the digest is known to match: the claimer (its digest IS the entry's), or an entry
-// created by an earlier batch (its digest bytes are immutable).  Only tag hits on entries created
-// in this batch by another lane are deferred to apply (their digest bytes may not be visible yet).
-// flags bit 3 = applied.
+// Probe by tag; CAS-claim empty slots (an entry of an older epoch is empty: the CAS replaces the
+// tag it read).  The chunk's block bit / last occurrence are applied right here when the digest is
+// known to match: the claimer (its digest IS the entry's: it initialises the batch-local fields
+// with its own occurrence), or an entry created by an earlier batch of this epoch (batch in
+// [bfirst, cur): its digest bytes are immutable).  Tag hits on entries created in this batch by
+// another lane are deferred to apply (their digest bytes may not be visible yet) — and so is a
+// stale `batch` of the previous epoch read between another lane's CAS and its batch store (such
+// ids are < bfirst).  flags bit 3 = applied.
 template <int HW>
 __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                         const uint32_t *__restrict__ digests,
                                                         IndexEntry *__restrict__ tab, int log2cap, uint32_t cur,
-                                                        unsigned long long tag_mask,
+                                                        uint32_t bfirst, unsigned long long key,
                                                         uint32_t *__restrict__ slot, uint8_t *__restrict__ flags,
                                                         int *__restrict__ err)
 {
@@ -87,38 +55,38 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
     uint32_t dw[HW];
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
-    uint32_t z;
-    const unsigned long long tag = make_tag(dw, z, tag_mask);
+    const unsigned long long tag = tag_word(dw, key);
     const uint64_t mask = (1ull << log2cap) - 1;
-    uint64_t h = home_slot(tag, log2cap);
+    uint64_t h = tag_home(tag, log2cap);
     bool mine = false;
     for (uint64_t probe = 0;; probe++) {
         if (probe > mask) { atomicOr(err, 2); return; }           // table full
         IndexEntry *e = tab + h;
         unsigned long long t = __hip_atomic_load(&e->tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == kEmptyTag) {
-            unsigned long long old = atomicCAS(&e->tag, kEmptyTag, tag);
-            if (old == kEmptyTag) {
-                e->batch = cur | z;
-                store_dig<HW>(e, dw);
-                mine = true;
-                break;
-            }
+        while (!tag_live(t, key)) {                                // empty: claim it
+            const unsigned long long old = atomicCAS(&e->tag, t, tag);
+            if (old == t) { mine = true; break; }
             t = old;
+        }
+        if (mine) {
+            e->batch = cur;
+            e->mask = 1ull << b;                                   // this chunk's occurrence
+            e->first = 0;
+            store_dig<HW>(e, dw);
+            break;
         }
         if (t == tag) break;
         h = (h + 1) & mask;
     }
     slot[c] = (uint32_t)h;
     IndexEntry *e = tab + h;
-    bool apply = mine;
+    bool apply = false;
     if (!mine) {
-        // batch only moves 0 -> cur inside this launch; a stale 0 just defers the chunk
-        const uint32_t bt = e->batch & 0x7fffffffu;
-        apply = bt != 0 && bt != cur && entry_matches<HW>(*e, dw, z);
+        const uint32_t bt = e->batch;
+        apply = bt >= bfirst && bt != cur && entry_matches<HW>(*e, dw);
+        if (apply) record_occurrence(e, b, k);
     }
-    if (apply) record_occurrence(e, b, k);
-    flags[c] = apply ? 8 : 0;
+    flags[c] = (mine || apply) ? 8 : 0;
 }
 
 // ---- apply: deferred chunks — verify full digest, record block membership / last occurrence
@@ -126,7 +94,7 @@ template <int HW>
 __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                         const uint32_t *__restrict__ digests,
                                                         IndexEntry *__restrict__ tab, const uint32_t *__restrict__ slot,
-                                                        const uint8_t *__restrict__ flags, unsigned long long tag_mask,
+                                                        const uint8_t *__restrict__ flags,
                                                         uint32_t *__restrict__ coll, uint32_t *__restrict__ ncoll,
                                                         int coll_cap, int *__restrict__ err)
 {
@@ -138,10 +106,8 @@ __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__rest
     uint32_t dw[HW];
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
-    uint32_t z;
-    (void)make_tag(dw, z, tag_mask);
     IndexEntry *e = tab + slot[c];
-    if (entry_matches<HW>(*e, dw, z)) {
+    if (entry_matches<HW>(*e, dw)) {
         record_occurrence(e, b, k);
     } else {
         uint32_t i = atomicAdd(ncoll, 1u);
@@ -153,7 +119,7 @@ __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__rest
 // ---- slow path: one thread, exact sequential re-probe of tag-collided chunks --------------
 template <int HW>
 __global__ void idx_slow_kernel(int cap_blk, const uint32_t *__restrict__ digests, IndexEntry *__restrict__ tab,
-                                int log2cap, uint32_t cur, unsigned long long tag_mask, uint32_t *__restrict__ slot,
+                                int log2cap, uint32_t cur, unsigned long long key, uint32_t *__restrict__ slot,
                                 const uint32_t *__restrict__ coll, const uint32_t *__restrict__ ncoll, int coll_cap,
                                 int *__restrict__ err)
 {
@@ -165,18 +131,17 @@ __global__ void idx_slow_kernel(int cap_blk, const uint32_t *__restrict__ digest
         const int b = (int)(c / (uint32_t)cap_blk), k = (int)(c % (uint32_t)cap_blk);
         uint32_t dw[HW];
         for (int q = 0; q < HW; q++) dw[q] = digests[(size_t)c * HW + q];
-        uint32_t z;
-        const unsigned long long tag = make_tag(dw, z, tag_mask);
+        const unsigned long long tag = tag_word(dw, key);
         uint64_t h = (slot[c] + 1) & mask;
         for (uint64_t probe = 0;; probe++) {
             if (probe > mask) { *err |= 2; return; }
             IndexEntry *e = tab + h;
-            if (e->tag == kEmptyTag) {
-                e->tag = tag; e->batch = cur | z; e->mask = 0; e->first = 0;
+            if (!tag_live(e->tag, key)) {
+                e->tag = tag; e->batch = cur; e->mask = 0; e->first = 0;
                 store_dig<HW>(e, dw);
                 break;
             }
-            if (e->tag == tag && entry_matches<HW>(*e, dw, z)) break;
+            if (e->tag == tag && entry_matches<HW>(*e, dw)) break;
             h = (h + 1) & mask;
         }
         slot[c] = (uint32_t)h;
@@ -211,7 +176,7 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
         const unsigned long long m = e->mask;
         const unsigned long long f = e->first;
         const int minb = __builtin_ctzll(m);            // first block of the batch holding it
-        const bool created = (e->batch & 0x7fffffffu) == cur;
+        const bool created = e->batch == cur;
         const bool is_new = created && b == minb;
         // the min block repeats the digest: every occurrence there joins the max so the
         // designated writer (last occurrence, chunkMeta SET order) is known after this kernel
@@ -302,26 +267,31 @@ template <int HW>
 __global__ void __launch_bounds__(256) idx_load_kernel(const uint32_t *__restrict__ dw_all,
                                                        const uint8_t *__restrict__ vals, int n,
                                                        IndexEntry *__restrict__ tab, int log2cap,
-                                                       unsigned long long tag_mask, int *__restrict__ err)
+                                                       unsigned long long key, uint32_t bload, int *__restrict__ err)
 {
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= n) return;
     uint32_t dw[HW];
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = dw_all[(size_t)k * HW + i];
-    unsigned long long tag = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
-    const uint32_t z = tag == 0 ? 0x80000000u : 0u;
-    if (tag == 0) tag = 1;
+    const unsigned long long tag = tag_word(dw, key);
     const uint64_t mask = (1ull << log2cap) - 1;
-    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
+    uint64_t h = tag_home(tag, log2cap);
     for (uint64_t probe = 0; probe <= mask; probe++, h = (h + 1) & mask) {
-        if (atomicCAS(&tab[h].tag, kEmptyTag, tag) != kEmptyTag) continue;
+        unsigned long long t = tab[h].tag;
+        bool mine = false;
+        while (!tag_live(t, key)) {
+            const unsigned long long old = atomicCAS(&tab[h].tag, t, tag);
+            if (old == t) { mine = true; break; }
+            t = old;
+        }
+        if (!mine) continue;
         IndexEntry &e = tab[h];
         const uint8_t *v = vals + (size_t)k * 11;           // chunkMeta.process, DN/chunkMeta.java:35-60
         e.mask = 0;
         e.first = 0;
-        e.batch = z;
-        e.ncopy = v[0];
+        e.batch = bload;                                    // a batch before every batch that follows
+        e.ncopy = v[0] | (HW == 7 ? (dw[1] >> 24) << 8 : 0u);
         e.cid = ((uint32_t)v[1] << 16) | ((uint32_t)v[2] << 8) | v[3];
         e.start = ((uint32_t)v[4] << 16) | ((uint32_t)v[5] << 8) | v[6] | ((uint32_t)(v[10] & 0xF0) << 20);
         e.stop = ((uint32_t)v[7] << 16) | ((uint32_t)v[8] << 8) | v[9] | ((uint32_t)(v[10] & 0x0F) << 24);
@@ -334,14 +304,14 @@ __global__ void __launch_bounds__(256) idx_load_kernel(const uint32_t *__restric
 }
 
 hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals, int n, IndexEntry *tab, int log2cap,
-                             unsigned long long tag_mask, int *err, hipStream_t st)
+                             unsigned long long key, uint32_t bload, int *err, hipStream_t st)
 {
     if (n <= 0) return hipSuccess;
     const dim3 g((n + 255) / 256);
     if (hasher == 0)
-        hipLaunchKernelGGL(idx_load_kernel<5>, g, dim3(256), 0, st, dw, vals, n, tab, log2cap, tag_mask, err);
+        hipLaunchKernelGGL(idx_load_kernel<5>, g, dim3(256), 0, st, dw, vals, n, tab, log2cap, key, bload, err);
     else
-        hipLaunchKernelGGL(idx_load_kernel<7>, g, dim3(256), 0, st, dw, vals, n, tab, log2cap, tag_mask, err);
+        hipLaunchKernelGGL(idx_load_kernel<7>, g, dim3(256), 0, st, dw, vals, n, tab, log2cap, key, bload, err);
     return hipGetLastError();
 }
 
@@ -350,7 +320,7 @@ hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals
 template <int HW>
 __global__ void __launch_bounds__(256) idx_probe_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                         const uint32_t *__restrict__ digests, const uint32_t *__restrict__ slot,
-                                                        int log2cap, unsigned long long tag_mask,
+                                                        int log2cap, unsigned long long key,
                                                         unsigned long long *__restrict__ stats)
 {
     const int b = blockIdx.y;
@@ -362,10 +332,8 @@ __global__ void __launch_bounds__(256) idx_probe_kernel(const BlockState *__rest
         uint32_t dw[HW];
 #pragma unroll
         for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
-        uint32_t z;
-        const unsigned long long tag = make_tag(dw, z, tag_mask);
         const uint64_t mask = (1ull << log2cap) - 1;
-        d = ((uint64_t)slot[c] - home_slot(tag, log2cap)) & mask;
+        d = ((uint64_t)slot[c] - tag_home(tag_word(dw, key), log2cap)) & mask;
     }
     // wave reductions, one atomic per wave
     unsigned long long s = d, m = d, n = on ? 1ull : 0ull;
@@ -393,15 +361,17 @@ hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, in
 
 hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st)
 {
-    const uint64_t n16 = (sizeof(IndexEntry) << log2cap) / 16;
+    // log2cap < 0: seed the allocator only (a reset that bumps the index epoch)
+    const uint64_t n16 = log2cap < 0 ? 0 : (sizeof(IndexEntry) << log2cap) / 16;
     uint64_t g = (n16 + 255) / 256;
     if (g > 8192) g = 8192;
+    if (g < 1) g = 1;
     hipLaunchKernelGGL(idx_clear_kernel, dim3((unsigned)g), dim3(256), 0, st, (u32x4 *)tab, n16, d_alloc, a);
     return hipGetLastError();
 }
 
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
-                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,
+                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst,
                         unsigned long long tag_mask, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
                         int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt)
@@ -411,20 +381,20 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
     static const int lds = [] { const char *e = getenv("HDRF_CLAIM_LDS"); return e ? atoi(e) : 0; }();
     if (hipError_t e = hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st)) return e;
     if (hasher == 0) {
-        hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
-                           slot, flags, err);
+        hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, bfirst,
+                           tag_mask, slot, flags, err);
         mk->mark(st);
-        hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, tag_mask, coll,
+        hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, coll,
                            ncoll,
                            coll_cap, err);
         mk->mark(st);
         hipLaunchKernelGGL(idx_slow_kernel<5>, dim3(1), dim3(64), 0, st, cap_blk, digests, tab, log2cap, cur, tag_mask, slot,
                            coll, ncoll, coll_cap, err);
     } else {
-        hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, tag_mask,
-                           slot, flags, err);
+        hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, bfirst,
+                           tag_mask, slot, flags, err);
         mk->mark(st);
-        hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, tag_mask, coll,
+        hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, coll,
                            ncoll,
                            coll_cap, err);
         mk->mark(st);

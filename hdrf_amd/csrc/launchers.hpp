@@ -55,7 +55,7 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
                       const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
                       hipStream_t st, Marker *mk);   // queue: 65 words; [64] = long chunks seen
 hipError_t launch_index_load(int hasher, const uint32_t *dw, const uint8_t *vals, int n, IndexEntry *tab, int log2cap,
-                             unsigned long long tag_mask, int *err, hipStream_t st);
+                             unsigned long long key, uint32_t bload, int *err, hipStream_t st);
 // GzipCodec read side (inflate.hip): one raw deflate stream -> dst; res[0] = length or < 0, res[1] =
 // bytes consumed.  CRC-32 of fixed-size pieces of a buffer.
 int64_t inflate_chunks(int64_t slen);
@@ -67,12 +67,13 @@ hipError_t launch_inflate_pack(const uint32_t *scratch, int64_t n, uint8_t *dst,
 struct CrcOp { uint32_t m[32]; };       // GF(2) operator "append k zero bytes" (columns)
 hipError_t launch_crc32_pieces(const uint8_t *data, int64_t n, const CrcOp &op1k, uint32_t *crc, hipStream_t st);
 hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *digests,
-                              const uint32_t *slot, int log2cap, unsigned long long tag_mask,
+                              const uint32_t *slot, int log2cap, unsigned long long key,
                               unsigned long long *stats, hipStream_t st);
+// (log2cap < 0: only the allocator seed; a reset that bumps the index epoch)
 hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st);
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
-                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur,
-                        unsigned long long tag_mask, uint32_t *slot,
+                        const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst,
+                        unsigned long long key, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
                         int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt = nullptr);
 // (dcnt: idx_finalize follows and hands place the designated chunks; decide settles the chunks
@@ -115,7 +116,7 @@ hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int ca
                           uint32_t gbase, int G, uint32_t *x1, int64_t cap, unsigned long long *counts, int *err,
                           hipStream_t st);
 hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts, int64_t max_count, int64_t cap, int G,
-                           IndexEntry *tab, int log2cap, uint32_t cur, unsigned long long tag_mask, uint32_t *oslot,
+                           IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst, unsigned long long key, uint32_t *oslot,
                            uint8_t *oflags, uint32_t *coll, uint32_t *ncoll, int coll_cap, uint32_t *x2, int *err,
                            hipStream_t st);
 hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int ntiles, const uint32_t *offsets,
@@ -189,10 +190,10 @@ hipError_t launch_lz4(const ClosedRec *closed, const uint32_t *nclosed, int clos
 // read side (read.hip): lookup + scan (gather = false), then the copy (gather = true)
 size_t rd_chunk_bytes();
 hipError_t launch_gx_locate(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
-                            unsigned long long tag_mask, int G, int rank, uint32_t *loc, int *err, hipStream_t st);
+                            unsigned long long key, int G, int rank, uint32_t *loc, int *err, hipStream_t st);
 hipError_t launch_rd_gather(const void *chunks, int n, const uint64_t *bases, uint8_t *out, hipStream_t st);
 hipError_t launch_reconstruct(int hasher, const uint32_t *dig, int n, const IndexEntry *tab, int log2cap,
-                              unsigned long long tag_mask, const uint32_t *cids, const uint64_t *bases, int ncont,
+                              unsigned long long key, const uint32_t *cids, const uint64_t *bases, int ncont,
                               void *chunks, uint64_t *total, uint8_t *out, int *err, hipStream_t st, bool gather);
 hipError_t launch_corpus(uint8_t *dev, const uint32_t *d_roots, int64_t nblocks, int64_t spb, int64_t seg_bytes,
                          uint64_t seed, int mixed, hipStream_t st);

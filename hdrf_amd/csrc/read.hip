@@ -27,21 +27,15 @@ struct RdChunk {
 // probe the index for one digest (the open addressing of index.hip); nullptr when absent
 template <int HW>
 __device__ const IndexEntry *rd_probe(const uint32_t *dw, const IndexEntry *__restrict__ tab, int log2cap,
-                                      unsigned long long tag_mask)
+                                      unsigned long long key)
 {
-    unsigned long long tag = ((unsigned long long)dw[0] | ((unsigned long long)dw[1] << 32)) & tag_mask;
-    const uint32_t z = tag == 0 ? 0x80000000u : 0u;
-    if (tag == 0) tag = 1;
+    const unsigned long long tag = tag_word(dw, key);
     const uint64_t mask = (1ull << log2cap) - 1;
-    uint64_t h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - log2cap);
+    uint64_t h = tag_home(tag, log2cap);
     for (uint64_t probe = 0; probe <= mask; probe++) {
         const IndexEntry &e = tab[h];
-        if (e.tag == kEmptyTag) return nullptr;
-        bool match = e.tag == tag && (e.batch & 0x80000000u) == z;
-#pragma unroll
-        for (int i = 2; i < HW; i++) match = match && e.dig[i - 2] == dw[i];
-        if (HW == 5) match = match && e.dig[3] == dw[0] && e.dig[4] == dw[1];
-        if (match) return &e;
+        if (!tag_live(e.tag, key)) return nullptr;           // empty (or of an older epoch)
+        if (e.tag == tag && entry_matches<HW>(e, dw)) return &e;
         h = (h + 1) & mask;
     }
     return nullptr;

@@ -402,10 +402,10 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
         } else if (desig) {                                // designated: final index value
             const uint32_t cnt = dcnt ? (uint32_t)dcnt[c] : (uint32_t)__popcll(e->mask);
             if (f & 4) {
-                e->ncopy = cnt & 0xffu;
+                set_ncopy(e, cnt);
                 e->cid = cid; e->start = pos; e->stop = pos + ((f & 1) && do_copy ? len : 0u);
             } else {
-                e->ncopy = (e->ncopy + cnt) & 0xffu;
+                set_ncopy(e, e->ncopy + cnt);
             }
             if (!dcnt) {
                 e->mask = 0;

@@ -614,3 +614,54 @@ def test_probe_stats_count_every_chunk():
         ctx.host_free(pinned)
         ctx.close()
     assert lens[1] > lens[0]
+
+
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_reset_epochs_are_fresh_indexes(hasher):
+    """hdrf_reset makes a fresh DataNode index by bumping the table's epoch (common.hpp: an entry
+    tagged with an older epoch is empty) instead of clearing 2^k x 64 B.  The same blocks reduced
+    again after a reset find their own previous-epoch entries at the very slots they probe (same
+    digests, same tags); batched, the claims race those stale entries.  Every round equals a fresh
+    oracle, index dump included — also after 300 resets (the 255-epoch wrap clears the table), and
+    an index restored into a reset context (hdrf_index_load) is live and decides the next block."""
+    roots = corpus_roots(33, 500000, 6, 4)
+    blocks = [corpus_block_host(33, roots, b, 4, 1 << 20) for b in range(6)]
+    size = len(blocks[0])
+    ctx = Context(hasher=hasher, container_max=1 << 22, **SMALL)
+    dev = ctx.dev_alloc(size * 6 + 4096)
+    ctx.h2d(dev, np.concatenate(blocks))
+    ids = list(range(60, 66))
+
+    def one_round(tag):
+        ora = Oracle(hasher=hasher, max_size=1 << 22)
+        ctx.reduce_batch([dev + i * size for i in range(3)], [size] * 3, [size * (6 - i) + 4096 for i in range(3)],
+                         ids[:3])
+        for i in range(3):
+            compare_block(ctx.batch_result(i), ora.reduce(blocks[i], ids[i]), tag=f"{tag} batch0 block {i}")
+        for i in range(3, 6):
+            compare_block(ctx.reduce_block(blocks[i], ids[i]), ora.reduce(blocks[i], ids[i]), tag=f"{tag} block {i}")
+        compare_state(ctx, ora, ids, tag=tag)
+        return ora
+
+    one_round("epoch 1")
+    for r in range(2):
+        ctx.reset()
+        one_round(f"after reset {r + 1}")
+    for _ in range(300):
+        ctx.reset()
+    ora = one_round("after 300 resets")
+    keys, vals = ctx.index_dump()
+    ctx.reset()
+    assert ctx.index_count() == 0, "a reset index holds no entry"
+    ctx.index_load(keys, vals)
+    k2, v2 = ctx.index_dump()
+    assert np.array_equal(k2, keys) and np.array_equal(v2, vals), "restored index differs"
+    extra = make_block("random", 7, 300_000)
+    extra = np.concatenate([blocks[2][:400_000], extra])
+    g = ctx.reduce_block(extra, 99)
+    o = ora.reduce(extra, 99)
+    for f in ("offsets", "digests", "is_new"):
+        assert np.array_equal(g[f], o[f]), f"restored index: {f} differs"
+    assert g["store_size"] == o["store_size"]
+    ctx.dev_free(dev)
+    ctx.close()
