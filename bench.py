@@ -114,6 +114,18 @@ def parse():
                     help="config5 packets: 'cpp' runs tests/cpp/packet_driver.cpp (native receiver threads on the "
                          "C-ABI the JNI binding calls, durable containers drained after every block) as a child "
                          "process and reports its rate")
+    ap.add_argument("--compressor", type=int, choices=[0, 1, 2], default=0,
+                    help="DataNode.compressor (DN/DataNode.java:438): 1 dedup, 2 dedup + Lz4Codec closed containers "
+                         "(the reference's default); 0 = the workload's own (config4 2, else 1)")
+    ap.add_argument("--mirror", choices=["ring", "socket", "none"], default="ring",
+                    help="config5 native packets: every packet forwarded downstream before it is appended "
+                         "(mirrorPacketTo, DN/BlockReceiver.java:635-641): 'ring' a byte ring drained by a consumer "
+                         "thread per receiver, 'socket' an AF_UNIX stream socket, 'none' a single-replica write")
+    ap.add_argument("--packet-batch", action="store_true",
+                    help="config5 native packets: every receive round's blocks submitted as one batch "
+                         "(hdrf_submit_slots) instead of one block per batch (hdrf_submit_slot)")
+    ap.add_argument("--mixed", action="store_true",
+                    help="config5: config 4's mixed-entropy corpus instead of config 2's")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
                     help="config4: mixed-entropy blocks (random/text/binary), dedup + Lz4Codec containers; "
                          "config5: host-resident (pinned) blocks streamed H2D on a side stream (PCIe-inclusive)")
@@ -121,7 +133,8 @@ def parse():
 
 
 def packet_driver_line(a):
-    """config5 through the native packet driver (a child process; this process never touches the GPU)."""
+    """config5 through the native packet driver (a child process; this process touches the GPU only
+    after it, for the link probe)."""
     import subprocess
     exe = os.path.join(ROOT, "tools", "_build", "packet_driver")
     if not os.path.exists(exe):
@@ -129,24 +142,54 @@ def packet_driver_line(a):
         exe = ge.build_packet_driver()
     nb = 128 if a.blocks == 512 else a.blocks
     pk = a.packet_kib or 64
+    compressor = a.compressor or 1
+    cmd = [exe, str(nb), str(a.block_mib), str(pk), str(a.packet_threads), str(a.steps), "--compressor",
+           str(compressor), "--mirror", a.mirror, "--arena-slots", str(a.arena_slots or 512)]
+    cmd += ["--batch"] * a.packet_batch + ["--mixed"] * a.mixed
     t0 = time.perf_counter()
-    r = subprocess.run([exe, str(nb), str(a.block_mib), str(pk), str(a.packet_threads), str(a.steps)],
-                       capture_output=True, text=True, timeout=1500)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=1500)
     wall = time.perf_counter() - t0
     if r.returncode != 0:
-        raise SystemExit("packet driver failed: %s %s" % (r.stdout[-2000:], r.stderr[-2000:]))
+        raise SystemExit("packet driver failed (%d): %s %s" % (r.returncode, r.stdout[-2000:], r.stderr[-2000:]))
     d = json.loads(r.stdout.strip().splitlines()[-1])
     S = a.block_mib << 20
+    import torch
+    link = link_probe(torch, 0, S)
+    drained = d["drained_bytes_last_step"]
     line = {"metric": METRIC, "value": d["GB_s"], "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": 1,
             "ms_per_step": round(nb * S / d["GB_s"] / 1e6, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "config5: %d x %d MiB host-resident (pinned) blocks, 50%% dup, %d KiB packets from %d "
-                                   "native receiver threads (hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot, "
-                                   "one block per submit, FIFO), durable containers drained after every block, "
-                                   "fresh index per step" % (nb, a.block_mib, pk, a.packet_threads),
+            "config": {"workload": "config5: %d x %d MiB host-resident (pinned) blocks, 50%% dup%s, %d KiB packets from %d "
+                                   "native receiver threads, each packet mirrored downstream (%s) before "
+                                   "hdrf_append_packet, %s, FIFO, compressor %d, durable containers drained after "
+                                   "every batch, fresh index per step"
+                                   % (nb, a.block_mib, ", mixed entropy" if a.mixed else "", pk, a.packet_threads,
+                                      a.mirror, "hdrf_submit_slots (a receive round per batch)" if a.packet_batch
+                                      else "hdrf_submit_slot (one block per batch)", compressor),
                        "blocks_per_gpu": nb, "block_bytes": S, "parallelism": "dp1"},
-            "roofline": None, "cpu_baseline": None, "packet_driver": d, "driver_wall_s": round(wall, 2)}
+            "roofline": None, "cpu_baseline": None, "mirror": a.mirror != "none", "packet_driver": d,
+            "driver_wall_s": round(wall, 2)}
+    line["pcie"] = pcie_entry(d["GB_s"], nb * S, drained, nb * S / d["GB_s"] / 1e9, link)
     print(json.dumps(line), flush=True)
+
+
+def pcie_entry(value, h2d_bytes, d2h_bytes, step_s, link):
+    """The link figures of a config-5 line: the raw probes and what the step moved over PCIe."""
+    moved = (h2d_bytes + d2h_bytes) / step_s / 1e9
+    return {"h2d_GB_s_raw_copy": round(link["h2d"], 2), "d2h_GB_s_raw_copy": round(link["d2h"], 2),
+            "bidirectional_GB_s_raw_copy": round(link["bidir"], 2),
+            "bidirectional_split_GB_s": {"h2d": round(link["bidir_h2d"], 2), "d2h": round(link["bidir_d2h"], 2)},
+            "value_over_raw_copy": round(value / link["h2d"], 4),
+            "value_over_bidirectional_raw": round(value / link["bidir_h2d"], 4),
+            "link_GB_s": round(moved, 2), "link_frac_of_bidirectional_raw": round(moved / link["bidir"], 4),
+            "drained_container_bytes_per_step": int(d2h_bytes),
+            "d2h_GB_s_drain": round(d2h_bytes / step_s / 1e9, 2),
+            "raw_copy": "pinned host <-> HBM, 128 MiB hipMemcpyAsync pieces, 4 in flight per stream, timed with HIP "
+                        "events (torch); bidirectional: H2D and D2H streams at once",
+            "value_over_bidirectional_raw_def": "value / the H2D rate the link sustains while D2H runs at once",
+            "note": "value is PCIe-inclusive: host buffers -> HBM -> reduced, and every container file "
+                    "(retain_containers, the JNI binding's mode) drained D2H to pinned host memory after each "
+                    "completed batch, inside the timed region"}
 
 
 def main():
@@ -194,13 +237,13 @@ def main():
     # One node, one index: at N > 1 the GPUs are ranks of ONE reduction over the global block
     # sequence (hdrf_amd/node.py): a global corpus of world*nb blocks, every global batch takes B
     # blocks from each rank (rank-major), the index is partitioned by digest prefix.
-    mixed = a.workload == "config4"
     host = a.workload == "config5"
+    mixed = a.workload == "config4" or (host and a.mixed)
     if (mixed or host) and world > 1:
         raise SystemExit("config4/config5 run on single-node contexts only")
     if host and a.blocks == 512:
         nb = 128                                         # 16 GiB of pinned host memory
-    compressor = 2 if mixed else 1
+    compressor = a.compressor or (2 if mixed else 1)
     # config 5 is the DataNode write path: durable containers (retain_containers, as the JNI binding
     # opens it) handed out to pinned host memory after every completed batch, inside the timed region
     ctx = Context(device=local, hasher=a.hasher, max_block_bytes=S, max_batch_blocks=B, index_log2=a.index_log2,
@@ -220,13 +263,13 @@ def main():
     total = nb * S + 4096
     dev = ctx.dev_alloc(total)
     ctx.corpus_fill(dev, roots, nb, spb, seg, seed, mixed=mixed)
-    hbuf, h2d_gbs, dbuf = None, None, None
+    hbuf, link, dbuf = None, None, None
     drained = {"events": 0, "bytes": 0}
     if host:                                             # the DataNode's received blocks, in host memory
         hbuf = ctx.host_alloc(nb * S)
         ctx.L.hdrf_memcpy_d2h(ctx._h, hbuf.ctypes.data, dev, nb * S)
         dbuf = None if a.no_drain else ctx.host_alloc(1 << 30)   # the drained container files (pinned)
-        h2d_gbs = raw_h2d_rate(torch, local, S)
+        link = link_probe(torch, local, S)
     batches = []
     for b0 in range(0, nb, B):
         k = min(B, nb - b0)
@@ -421,7 +464,7 @@ def main():
                        "sq_insts_valu_per_launch": int(sha_prof["sq_insts_valu"])}
     place = hbm_entry(STAGES[9])
     lz4 = None
-    if mixed:
+    if compressor == 2:
         # the LZ4 pass per batch: closed containers read + Lz4Codec files written, over the stage's
         # average time from the place kernel's end to the pack kernel's end on its LZ4 stream (two
         # batches' passes overlap, so this is a latency, not an exclusive share of the GPU)
@@ -480,7 +523,7 @@ def main():
              "index": "one node-global index over %d GPU(s), partitioned by digest prefix" % world}
 
     compression = None
-    if mixed:
+    if compressor == 2:
         st = ctx.stats()
         stored = st["closed_file_bytes"] + st["open_bytes"]
         compression = {"closed_containers": st["closed_containers"], "closed_raw_bytes": st["closed_raw_bytes"],
@@ -524,7 +567,7 @@ def main():
                                           "mixed-entropy (random/text/binary) " if mixed else "",
                                           a.dup_ppm // 10000, a.seg_mib, "1" if a.hasher == 0 else "224",
                                           "local" if world == 1 else "node-global (RCCL all-to-all)",
-                                          " + Lz4Codec on closed containers" if mixed else "",
+                                          " + Lz4Codec on closed containers" if compressor == 2 else "",
                                           " + recipes (device store)" if a.keep_recipes else ", no recipes"),
                            "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks_per_gpu": B,
                            "parallelism": "dp%d: blocks sharded by rank; one index partitioned by digest prefix"
@@ -535,27 +578,18 @@ def main():
         if read_side:
             line["read_side"] = read_side
         if host:
-            line["config"]["workload"] = ("config5: %d x %d MiB host-resident (pinned) blocks, %d%% dup, streamed "
+            line["config"]["workload"] = ("config5: %d x %d MiB host-resident (pinned) blocks, %d%% dup%s, streamed "
                                           "H2D on a side stream overlapped with the reduction (%s), "
-                                          "chunk+SHA-1+local index+container store, fresh index per step"
-                                          % (nb, a.block_mib, a.dup_ppm // 10000,
+                                          "chunk+SHA-1+local index+container store%s, durable containers drained "
+                                          "after every batch, fresh index per step"
+                                          % (nb, a.block_mib, a.dup_ppm // 10000, ", mixed entropy" if mixed else "",
                                              ("%d KiB packets, %d receiver threads, hdrf_append_packet + hdrf_submit_slot, "
                                               "one block per submit" % (a.packet_kib, a.packet_threads)) if a.packet_kib else
-                                             "whole blocks, hdrf_submit_host"))
-            line["pcie"] = {"h2d_GB_s_raw_copy": round(h2d_gbs, 2), "value_over_raw_copy": round(value / h2d_gbs, 4),
-                            "raw_copy": "pinned host -> HBM, 128 MiB hipMemcpyAsync pieces, 4 in flight on one "
-                                        "stream, timed with HIP events (torch)",
-                            "link_GB_s": round((nb * S + drained["bytes"] / max(1, a.steps)) / (el / a.steps) / 1e9, 2),
-                            "link_frac_of_raw_copy": round((nb * S + drained["bytes"] / max(1, a.steps)) / (el / a.steps)
-                                                           / 1e9 / h2d_gbs, 4),
-                            "link_note": "H2D block bytes + D2H container bytes per second over the measured raw "
-                                         "copy rate: the PCIe link carries both directions at about that total rate",
-                            "drained_container_bytes_per_step": drained["bytes"] // max(1, a.steps),
-                            "drained_events_per_step": drained["events"] // max(1, a.steps),
-                            "d2h_GB_s_drain": round(drained["bytes"] / max(1, a.steps) / (el / a.steps) / 1e9, 2),
-                            "note": "value is PCIe-inclusive: host buffers -> HBM -> reduced, and every container "
-                                    "file (retain_containers, the JNI binding's mode) drained D2H to pinned host "
-                                    "memory after each completed batch, inside the timed region"}
+                                             "whole blocks, hdrf_submit_host",
+                                             " + Lz4Codec on closed containers" if compressor == 2 else ""))
+            line["pcie"] = pcie_entry(value, nb * S, drained["bytes"] / max(1, a.steps), el / a.steps, link)
+            line["pcie"]["drained_events_per_step"] = drained["events"] // max(1, a.steps)
+            line["config"]["compressor"] = compressor
         if node is not None and node.phase_ms.get("batches"):
             nbt = node.phase_ms["batches"]
             line["node_back_ms_per_batch"] = {k: round(v / nbt, 3) for k, v in node.phase_ms.items() if k != "batches"}
@@ -571,27 +605,57 @@ def main():
         dist.destroy_process_group()
 
 
-def raw_h2d_rate(torch, device, piece):
-    """The bare link: pinned host -> HBM in `piece`-byte async copies, 4 in flight on one stream
-    (the shape of the library's own H2D copies), 16 GiB, timed with HIP events."""
+def link_probe(torch, device, piece):
+    """The bare link: pinned host -> HBM (H2D), HBM -> pinned host (D2H), and both at once on two
+    streams, in `piece`-byte async copies, 4 in flight per stream (the shape of the library's own
+    copies), 16 GiB per direction, timed with HIP events."""
     n = 4
     src = torch.empty(n * piece, dtype=torch.uint8, pin_memory=True)
+    hdst = torch.empty(n * piece, dtype=torch.uint8, pin_memory=True)
     dst = torch.empty(n * piece, dtype=torch.uint8, device="cuda:%d" % device)
-    s = torch.cuda.Stream(device=device)
+    dsrc = torch.empty(n * piece, dtype=torch.uint8, device="cuda:%d" % device)
+    s1, s2 = torch.cuda.Stream(device=device), torch.cuda.Stream(device=device)
     reps = max(1, (16 << 30) // (n * piece))
-    with torch.cuda.stream(s):
-        for i in range(n):                                # warm-up
-            dst[i * piece:(i + 1) * piece].copy_(src[i * piece:(i + 1) * piece], non_blocking=True)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(reps):
+
+    def h2d(s):
+        with torch.cuda.stream(s):
             for i in range(n):
                 dst[i * piece:(i + 1) * piece].copy_(src[i * piece:(i + 1) * piece], non_blocking=True)
-        e1.record(s)
-    e1.synchronize()
-    rate = reps * n * piece / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del src, dst
-    return rate
+
+    def d2h(s):
+        with torch.cuda.stream(s):
+            for i in range(n):
+                hdst[i * piece:(i + 1) * piece].copy_(dsrc[i * piece:(i + 1) * piece], non_blocking=True)
+
+    def timed(dirs):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record(s1)
+        s2.wait_event(e0)
+        ends = []
+        for s, f in dirs:
+            for _ in range(reps):
+                f(s)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(s)
+            ends.append(e)
+        for e in ends:
+            s1.wait_event(e)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(s1)
+        e1.synchronize()
+        return [e0.elapsed_time(e) * 1e-3 for e in ends], e0.elapsed_time(e1) * 1e-3
+
+    h2d(s1)
+    d2h(s2)                                               # warm-up
+    torch.cuda.synchronize()
+    nbytes = reps * n * piece
+    (t_h,), _ = timed([(s1, h2d)])
+    (t_d,), _ = timed([(s2, d2h)])
+    (t_bh, t_bd), t_b = timed([(s1, h2d), (s2, d2h)])
+    del src, hdst, dst, dsrc
+    torch.cuda.empty_cache()
+    return {"h2d": nbytes / t_h / 1e9, "d2h": nbytes / t_d / 1e9, "bidir": 2 * nbytes / t_b / 1e9,
+            "bidir_h2d": nbytes / t_bh / 1e9, "bidir_d2h": nbytes / t_bd / 1e9}
 
 
 def read_bench(ctx, dev, S, m, hasher, compressor):
@@ -625,8 +689,8 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1, gpu_res=None):
     """CPU oracle (C restatement of the reference) on the first m blocks of the same corpus, timed
     in BASELINE.md's two shapes plus one thread:
       reference  the reference's own concurrency, blocks serialised: per block 1 chunking thread,
-                 3 threadedHasher threads over the chunk ranges, then the ordered index/store part
-                 (DN/DataDeduplicator.java:122-204, :578-641)
+                 3 threadedHasher threads over the chunk ranges, then the ordered index part and 3
+                 concurrent threadedStorer threads (DN/DataDeduplicator.java:122-204, :578-641, :652-836)
       all_cores  every usable core (sched_getaffinity): chunk + hash of later blocks on N-1 worker
                  threads ahead of 1 ordered index/store thread
     All check per-block storeSize == the GPU's (bit-exact dedup ratio); the all-cores run also
@@ -670,8 +734,8 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1, gpu_res=None):
     sample = "first %d of the same blocks (%.1f GiB), oracle/hdrf_oracle.c%s" % (
         m, m * S / 2**30, " with lz4 r123 containers" if compressor == 2 else "")
     out = {"value": round(m * S / tp / 1e9, 4), "unit": "GB/s", "cores": nthr + 1, "kind": "port",
-           "sample": sample + ", all usable cores: %d chunk+hash worker threads + 1 ordered index/store thread, %.1f s"
-                     % (nthr, tp),
+           "sample": sample + ", all usable cores: %d chunk+hash worker threads + 1 ordered index thread with 3 "
+                              "concurrent storer threads per block, %.1f s" % (nthr, tp),
            "store_size_mismatches": mism(ssp),
            "chunk_check": {"blocks": m, "chunks": n_chunks, "mismatches": chunk_bad,
                            "what": "per chunk: END offset, digest, is_new (GPU from a fresh index over the same "
@@ -679,8 +743,10 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1, gpu_res=None):
            "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
            "usable_cores": usable,
            "reference_shape": {"value": round(m * S / tr / 1e9, 4), "unit": "GB/s", "cores": 4,
-                               "threads": "per block 1 chunking + 3 hasher threads, then the ordered part; "
-                                          "blocks serialised", "seconds": round(tr, 2),
+                               "threads": "per block 1 chunking + 3 hasher threads, then the ordered part with 3 "
+                                          "concurrent storer threads (each closing%s its own containers); blocks "
+                                          "serialised" % (" and LZ4-compressing" if compressor == 2 else ""),
+                               "seconds": round(tr, 2),
                                "store_size_mismatches": mism(ssr)},
            "single_thread": {"value": round(m * S / t1 / 1e9, 4), "unit": "GB/s", "cores": 1,
                              "seconds": round(t1, 2), "store_size_mismatches": mism(ss1)}}

@@ -97,7 +97,7 @@ struct Slot {
     hipEvent_t placed = nullptr;              // compressor 2: the batch's place kernel finished (stream B2)
     hipEvent_t idx_done = nullptr;            // index stage (claim .. finalize) of the batch done (stream B)
     hipEvent_t lz_done = nullptr;             // compressor 2: its closed containers are Lz4Codec files
-    int rx_release = -1;                      // packet path: receive buffer to free when the batch completes
+    uint32_t rx_release = 0;                  // packet path: receive buffers (bit mask) freed when the batch completes
     uint32_t gx_batch = 0;                    // node-global: index batch id of the batch in this slot
     bool gx_compressed = false;               // node-global compressor 2: hdrf_gx_compress ran for the batch
     RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
@@ -505,7 +505,7 @@ static int init_state(hdrf_ctx *ctx, bool fresh)
     ctx->handed.clear();
     ctx->lost = false;
     for (auto &r : ctx->rx) { r.state = 0; r.len = 0; r.fill = 0; r.busy[0] = r.busy[1] = false; }
-    for (auto &S : ctx->sl) S.rx_release = -1;
+    for (auto &S : ctx->sl) S.rx_release = 0;
     return 0;
 }
 
@@ -1040,11 +1040,12 @@ static int wait_one(hdrf_ctx *ctx)
     S.pending = false;
     HIPCK(hipEventSynchronize(S.back_done));
     if (ctx->cfg.compressor == 2) HIPCK(hipEventSynchronize(S.lz_done));
-    if (S.rx_release >= 0) {                           // its receive buffer is free again
-        ctx->rx[S.rx_release].state = 0;
-        ctx->rx[S.rx_release].len = 0;
-        S.rx_release = -1;
-    }
+    for (int i = 0; i < hdrf_ctx::kRx; i++)            // its receive buffers are free again
+        if (S.rx_release >> i & 1) {
+            ctx->rx[i].state = 0;
+            ctx->rx[i].len = 0;
+        }
+    S.rx_release = 0;
     return complete_slot(ctx, si, true);
 }
 
@@ -1152,24 +1153,45 @@ extern "C" int hdrf_rx_cancel(hdrf_ctx *ctx, int32_t rx)
     return 0;
 }
 
-extern "C" int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx)
+// n received blocks (receive buffers in arrival order) as ONE batch: the DataNode hands over every
+// block whose last packet has arrived since its previous submit, so the batch's kernels, index and
+// store passes are shared by those blocks instead of running once per block.
+extern "C" int hdrf_submit_slots(hdrf_ctx *ctx, int32_t n, const int32_t *rxs)
 {
     HDRF_LOCK(ctx);
-    if (!ctx || rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state.load() != 1)
-        return ctx ? set_err(ctx, HDRF_E_INVAL, "bad receive buffer") : HDRF_E_INVAL;
+    if (!ctx) return HDRF_E_INVAL;
+    if (n < 1 || n > ctx->max_batch || !rxs) return set_err(ctx, HDRF_E_INVAL, "bad receive-buffer list");
+    uint32_t mask = 0;
+    for (int i = 0; i < n; i++) {
+        const int32_t rx = rxs[i];
+        if (rx < 0 || rx >= hdrf_ctx::kRx || ctx->rx[rx].state.load() != 1 || (mask >> rx & 1))
+            return set_err(ctx, HDRF_E_INVAL, "bad receive buffer");
+        mask |= 1u << rx;
+    }
     if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)     // every submit pairs with one hdrf_wait_batch
         return set_err(ctx, HDRF_E_CAPACITY, "pipeline full: hdrf_wait_batch first");
-    hdrf_ctx::Rx &r = ctx->rx[rx];
-    HIPCK(rx_flush(ctx, r));
-    HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, ctx->stC));
+    std::vector<const uint8_t *> p(n);
+    std::vector<uint64_t> len(n), readable(n), id(n);
+    for (int i = 0; i < n; i++) {
+        hdrf_ctx::Rx &r = ctx->rx[rxs[i]];
+        HIPCK(rx_flush(ctx, r));
+        HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, ctx->stC));
+        p[i] = r.d;
+        len[i] = r.len;
+        readable[i] = (uint64_t)ctx->cfg.max_block_bytes + kSlack + 256;
+        id[i] = r.id;
+    }
     Slot &S = ctx->sl[ctx->nsub % kSlots];
     HIPCK(hipEventRecord(S.copy_done, ctx->stC));
-    const uint8_t *p = r.d;
-    const uint64_t len = r.len, readable = (uint64_t)ctx->cfg.max_block_bytes + kSlack + 256, id = r.id;
-    if (int rc = submit(ctx, 1, &p, &len, &readable, &id, true)) return rc;
-    S.rx_release = rx;
-    r.state = 2;
+    if (int rc = submit(ctx, n, p.data(), len.data(), readable.data(), id.data(), true)) return rc;
+    S.rx_release = mask;
+    for (int i = 0; i < n; i++) ctx->rx[rxs[i]].state = 2;
     return 0;
+}
+
+extern "C" int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx)
+{
+    return hdrf_submit_slots(ctx, 1, &rx);
 }
 
 extern "C" int hdrf_submit_batch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,

@@ -32,7 +32,7 @@ EXPORTS = [
     "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
     "hdrf_container_unload", "hdrf_index_load", "hdrf_allocator_load", "hdrf_recipe_load",
     "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
-    "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot", "hdrf_rx_cancel",
+    "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot", "hdrf_submit_slots", "hdrf_rx_cancel",
     "hdrf_gx_read_locate", "hdrf_gx_read_fill", "hdrf_gx_flush_fn", "hdrf_gx_alloc_scan",
     "hdrf_set_lzop_mtime",
 ]
@@ -128,6 +128,7 @@ def load():
         "hdrf_rx_begin": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int32)]),
         "hdrf_append_packet": (ctypes.c_int, [_vp, ctypes.c_int32, _vp, ctypes.c_uint64]),
         "hdrf_submit_slot": (ctypes.c_int, [_vp, ctypes.c_int32]),
+        "hdrf_submit_slots": (ctypes.c_int, [_vp, ctypes.c_int32, _vp]),
         "hdrf_rx_cancel": (ctypes.c_int, [_vp, ctypes.c_int32]),
         "hdrf_probe_stats": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                             ctypes.POINTER(ctypes.c_int64)]),
@@ -299,6 +300,11 @@ class Context:
 
     def submit_slot(self, rx):
         self._ck(self.L.hdrf_submit_slot(self._h, rx))
+
+    def submit_slots(self, rxs):
+        """Received blocks (receive buffers in arrival order) submitted as one batch."""
+        a = (ctypes.c_int32 * len(rxs))(*rxs)
+        self._ck(self.L.hdrf_submit_slots(self._h, len(rxs), a))
 
     def rx_cancel(self, rx):
         self._ck(self.L.hdrf_rx_cancel(self._h, rx))

@@ -133,10 +133,14 @@ int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *host_
  * lost mid-block; the reference drops bf1): its receiver must have stopped appending.  A packet
  * that would take the block past max_block_bytes is refused (HDRF_E_INVAL) and copies nothing.
  * hdrf_reset refuses (HDRF_E_INVAL) while a buffer is receiving; hdrf_close requires every
- * receiver to have stopped. */
+ * receiver to have stopped.  hdrf_submit_slots submits n <= max_batch_blocks received blocks
+ * (receive buffers listed in arrival order) as ONE batch: a DataNode whose receivers finished several
+ * blocks since its last submit hands them over together (the FIFO order is the list order), so the
+ * per-batch index / store passes are shared; the buffers are free again when that batch completes. */
 int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx);
 int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data, uint64_t len);
 int hdrf_submit_slot(hdrf_ctx *ctx, int32_t rx);
+int hdrf_submit_slots(hdrf_ctx *ctx, int32_t n, const int32_t *rx);
 int hdrf_rx_cancel(hdrf_ctx *ctx, int32_t rx);
 /* Stream-mode schemes (DataNode.compressor 0/3/4/5: the whole block through a Hadoop codec,
  * DN/BlockReceiver.java:822-894,1238-1256).  codec 4 = Lz4Codec, 0 = SnappyCodec, 3 = LzopCodec

@@ -14,8 +14,10 @@ import java.nio.ByteBuffer;
  * DataDeduplicator.java:124-158) take arrive() when the block is received and pass the ticket to
  * reduce(ticket, ...) from the block's own DDRunner-style thread.
  * Durability: containers are kept in HBM until drainContainers(chunkDir) has written them; call it
- * after reductions (a reduction that could overwrite an undrained container fails with
- * IOException "drain ... first": drain and retry).
+ * after every awaitOldest().  A reduction that could overwrite an undrained container fails with
+ * IOException naming its recovery: "hdrf_drain_containers first" (drain, then retry) or, when the
+ * blocks still in flight are what fills the ring, "hdrf_wait_batch, then hdrf_drain_containers"
+ * (awaitOldest(), drainContainers(), then retry).
  */
 public final class HipReductionScheme extends ReductionScheme {
   static { System.loadLibrary("hdrf_jni"); }   // libhdrf_jni.so -> libhdrf.so
@@ -24,7 +26,13 @@ public final class HipReductionScheme extends ReductionScheme {
 
   /** hasher: DataNode.hasher (0 SHA-1, 1 SHA-224); compressor: DataNode.compressor (1, 2). */
   public HipReductionScheme(int hasher, int compressor, int device, long maxBlockBytes) throws IOException {
-    ctx = open0(hasher, compressor, device, maxBlockBytes);
+    this(hasher, compressor, device, maxBlockBytes, 16);
+  }
+
+  /** maxBatchBlocks: most blocks one submitBlocks() hands over together (1..16). */
+  public HipReductionScheme(int hasher, int compressor, int device, long maxBlockBytes, int maxBatchBlocks)
+      throws IOException {
+    ctx = open0(hasher, compressor, device, maxBlockBytes, maxBatchBlocks);
   }
 
   @Override
@@ -102,6 +110,15 @@ public final class HipReductionScheme extends ReductionScheme {
   }
 
   /**
+   * Every block whose last packet arrived since the previous submit, handed over as ONE batch in
+   * arrival order (the FIFO order is the array order): the blocks share one pass of the index and
+   * store kernels.  One awaitOldest() completes the whole batch.
+   */
+  public void submitBlocks(int[] rx) throws IOException {
+    submitSlots0(ctx, rx);
+  }
+
+  /**
    * Abandon a block being received (the client was lost mid-block; BlockReceiver drops bf1): the
    * receive buffer is free again.  Call it from BlockReceiver's error path, after the receiver
    * thread stopped calling packet().
@@ -156,7 +173,8 @@ public final class HipReductionScheme extends ReductionScheme {
     if (ctx != 0) { close0(ctx); ctx = 0; }
   }
 
-  private static native long open0(int hasher, int compressor, int device, long maxBlockBytes) throws IOException;
+  private static native long open0(int hasher, int compressor, int device, long maxBlockBytes, int maxBatchBlocks)
+      throws IOException;
   private static native byte[] reconstruct0(long ctx, long blockId) throws IOException;
   private static native void reduce0(long ctx, ByteBuffer direct, int len, long blockId) throws IOException;
   private static native void submit0(long ctx, ByteBuffer direct, int len, long blockId) throws IOException;
@@ -176,6 +194,7 @@ public final class HipReductionScheme extends ReductionScheme {
   private static native int rxBegin0(long ctx, long blockId) throws IOException;
   private static native void packet0(long ctx, int rx, ByteBuffer pkt, int off, int len) throws IOException;
   private static native void submitSlot0(long ctx, int rx) throws IOException;
+  private static native void submitSlots0(long ctx, int[] rx) throws IOException;
   private static native void rxCancel0(long ctx, int rx) throws IOException;
   private static native byte[] streamDecode0(long ctx, int codec, byte[] file, long blockId) throws IOException;
 }

@@ -26,7 +26,7 @@ static void throw_io(JNIEnv *env, hdrf_ctx *ctx, int rc)
 #define JFN(name) Java_org_apache_hadoop_hdfs_server_datanode_HipReductionScheme_##name
 
 JNIEXPORT jlong JNICALL JFN(open0)(JNIEnv *env, jclass cls, jint hasher, jint compressor, jint device,
-                                   jlong max_block)
+                                   jlong max_block, jint max_batch)
 {
     (void)cls;
     hdrf_cfg cfg;
@@ -37,7 +37,7 @@ JNIEXPORT jlong JNICALL JFN(open0)(JNIEnv *env, jclass cls, jint hasher, jint co
     cfg.retain_containers = 1;        /* durable: nothing leaves HBM before drain0 wrote its file */
     cfg.device = device;
     cfg.max_block_bytes = max_block;  /* dfs.blocksize */
-    cfg.max_batch_blocks = 1;
+    cfg.max_batch_blocks = max_batch; /* blocks per submitBlocks() batch (1..64; 16 receive buffers) */
     hdrf_ctx *ctx = NULL;
     int rc = hdrf_open(&cfg, &ctx);
     if (rc) { throw_io(env, NULL, rc); return 0; }
@@ -184,6 +184,22 @@ JNIEXPORT void JNICALL JFN(submitSlot0)(JNIEnv *env, jclass cls, jlong h, jint r
     (void)cls;
     hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
     int rc = hdrf_submit_slot(ctx, rx);
+    if (rc) throw_io(env, ctx, rc);
+}
+
+/* every block whose last packet arrived since the previous submit, as ONE batch (FIFO = array order) */
+JNIEXPORT void JNICALL JFN(submitSlots0)(JNIEnv *env, jclass cls, jlong h, jintArray rxs)
+{
+    (void)cls;
+    hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    const jsize n = (*env)->GetArrayLength(env, rxs);
+    jint *r = (*env)->GetIntArrayElements(env, rxs, NULL);
+    if (!r) { throw_io(env, ctx, HDRF_E_NOMEM); return; }
+    int32_t tmp[16];
+    int rc = (n < 1 || n > 16) ? HDRF_E_INVAL : 0;
+    for (jsize i = 0; !rc && i < n; i++) tmp[i] = (int32_t)r[i];
+    (*env)->ReleaseIntArrayElements(env, rxs, r, JNI_ABORT);
+    if (!rc) rc = hdrf_submit_slots(ctx, (int32_t)n, tmp);
     if (rc) throw_io(env, ctx, rc);
 }
 

@@ -238,8 +238,10 @@ struct hdrf_oracle {
     kvmap index;
     int have_alloc;
     uint8_t alloc[24];              /* Redis key "blockID" */
-    container *cont; int64_t ncont, ccap;
+    /* one table per storer range (id >> 22): the range's storer thread is the only writer */
+    container *cont[4]; int64_t ncont[4], ccap[4];
     recipe *rec; int64_t nrec, rcap;
+    int mt_store;                   /* 1: the storer ranges run on concurrent threads (CPU baselines) */
 };
 
 hdrf_oracle *hdrf_oracle_new(int hasher, int compressor, uint32_t max_size)
@@ -259,25 +261,30 @@ void hdrf_oracle_free(hdrf_oracle *o)
 {
     if (!o) return;
     kv_free(&o->index);
-    for (int64_t i = 0; i < o->ncont; i++) { free(o->cont[i].data); free(o->cont[i].cdata); }
+    for (int r = 0; r < 4; r++) {
+        for (int64_t i = 0; i < o->ncont[r]; i++) { free(o->cont[r][i].data); free(o->cont[r][i].cdata); }
+        free(o->cont[r]);
+    }
     for (int64_t i = 0; i < o->nrec; i++) free(o->rec[i].data);
-    free(o->cont); free(o->rec); free(o);
+    free(o->rec); free(o);
 }
 
-static container *cont_find(hdrf_oracle *o, uint32_t id)
+static container *cont_find(const hdrf_oracle *o, uint32_t id)
 {
-    for (int64_t i = o->ncont - 1; i >= 0; i--)
-        if (o->cont[i].id == id) return &o->cont[i];
+    const int r = (int)(id >> 22) & 3;
+    for (int64_t i = o->ncont[r] - 1; i >= 0; i--)
+        if (o->cont[r][i].id == id) return &o->cont[r][i];
     return NULL;
 }
 
 static container *cont_create(hdrf_oracle *o, uint32_t id)
 {
-    if (o->ncont == o->ccap) {
-        o->ccap = o->ccap ? o->ccap * 2 : 16;
-        o->cont = (container *)realloc(o->cont, (size_t)o->ccap * sizeof(container));
+    const int r = (int)(id >> 22) & 3;
+    if (o->ncont[r] == o->ccap[r]) {
+        o->ccap[r] = o->ccap[r] ? o->ccap[r] * 2 : 16;
+        o->cont[r] = (container *)realloc(o->cont[r], (size_t)o->ccap[r] * sizeof(container));
     }
-    container *c = &o->cont[o->ncont++];
+    container *c = &o->cont[r][o->ncont[r]++];
     memset(c, 0, sizeof *c);
     c->id = id;
     return c;
@@ -375,6 +382,62 @@ int64_t hdrf_oracle_reduce(hdrf_oracle *o, const uint8_t *data, int64_t size, in
                          store_size_out);
 }
 
+/* One threadedStorer (:702-836) over chunks [start, stop): appends the range's new chunks to its
+ * container chain lastBlockID[t] (its own table of containers: the ranges never share one), closes
+ * (and under compressor 2 compresses) a container when the next chunk would pass maxSize, and
+ * encodes every chunk's value into setv. */
+typedef struct {
+    hdrf_oracle *o;
+    const uint8_t *data;
+    chunk_meta *cm;
+    uint8_t *setv;
+    int64_t start, stop, storeSize;
+    int64_t *lastBlockID;
+    int t;
+} store_job;
+
+static void *store_range(void *arg)
+{
+    store_job *j = (store_job *)arg;
+    hdrf_oracle *o = j->o;
+    chunk_meta *cm = j->cm;
+    int64_t *lastBlockID = j->lastBlockID;
+    const int t = j->t;
+    if (j->storeSize == 0) {                                                /* :713-719 */
+        for (int64_t k = j->start; k < j->stop; k++) meta_encode(&cm[k], j->setv + k * 11);
+        return NULL;
+    }
+    container *c = cont_find(o, (uint32_t)lastBlockID[t]);                  /* :723-737 */
+    int64_t curPos;
+    if (c) curPos = c->len; else { c = cont_create(o, (uint32_t)lastBlockID[t]); curPos = 0; }
+    int64_t bufpos = 0;                                                     /* bufferBB.position() */
+    for (int64_t k = j->start; k < j->stop; k++) {
+        if (cm[k].newChunk) {
+            if (curPos + cm[k].length > (int64_t)o->max_size) {            /* :748 buffer full */
+                c->closed = 1;                                              /* :754-786 rewrite prev||buf */
+                if (o->compressor == 2) {                                   /* :770-779 Lz4Codec stream */
+                    c->cdata = (uint8_t *)malloc((size_t)hdrf_oracle_hadoop_lz4_bound(c->len));
+                    c->clen = hdrf_oracle_hadoop_lz4_frame(c->data, c->len, c->cdata);
+                }
+                bufpos = 0; curPos = 0;                                     /* :790-791 */
+                lastBlockID[t]++;                                           /* :792 */
+                lastBlockID[t + 4] = 0;                                     /* :793 */
+                c = cont_find(o, (uint32_t)lastBlockID[t]);                /* :794-795 createNewFile */
+                if (!c) c = cont_create(o, (uint32_t)lastBlockID[t]);
+            }
+            cont_append(c, j->data + cm[k].bbStart, cm[k].length);         /* :798 */
+            bufpos += cm[k].length;
+            cm[k].blockID = lastBlockID[t];                                 /* :799 */
+            cm[k].blockStart = (int32_t)curPos;                             /* :800 setBlockStartStop */
+            cm[k].blockStop = (int32_t)(curPos + cm[k].length);
+            curPos += cm[k].length;                                         /* :801 */
+        }
+        meta_encode(&cm[k], j->setv + k * 11);                              /* :803 SET digest -> meta */
+    }
+    lastBlockID[t + 4] = bufpos;                                            /* :808 */
+    return NULL;
+}
+
 /* The ordered part (FIFO turn, :124-204): Redis lookups, checkChunk, storers, SETs, storeDB.
  * Takes ownership of off/dig. */
 static int64_t reduce_hashed(hdrf_oracle *o, const uint8_t *data, int64_t size, int64_t block_id, uint32_t *off,
@@ -411,41 +474,18 @@ static int64_t reduce_hashed(hdrf_oracle *o, const uint8_t *data, int64_t size, 
     /* :184 storeChunksMT :511-532 -> threadedStorer.run :702-836 */
     int nThread = n < 25 ? 1 : 3;
     uint8_t *setv = (uint8_t *)malloc((size_t)n * 11 + 1);
+    store_job sj[3];
+    pthread_t sth[3];
+    int sstarted[3] = {0, 0, 0};
     for (int t = 0; t < nThread; t++) {
-        int64_t start = n * t / nThread, stop = n * (t + 1) / nThread;      /* :682-683 */
-        if (storeSize == 0) {                                               /* :713-719 */
-            for (int64_t k = start; k < stop; k++) meta_encode(&cm[k], setv + k * 11);
-            continue;
-        }
-        container *c = cont_find(o, (uint32_t)lastBlockID[t]);              /* :723-737 */
-        int64_t curPos;
-        if (c) curPos = c->len; else { c = cont_create(o, (uint32_t)lastBlockID[t]); curPos = 0; }
-        int64_t bufpos = 0;                                                 /* bufferBB.position() */
-        for (int64_t k = start; k < stop; k++) {
-            if (cm[k].newChunk) {
-                if (curPos + cm[k].length > (int64_t)o->max_size) {        /* :748 buffer full */
-                    c->closed = 1;                                          /* :754-786 rewrite prev||buf */
-                    if (o->compressor == 2) {                               /* :770-779 Lz4Codec stream */
-                        c->cdata = (uint8_t *)malloc((size_t)hdrf_oracle_hadoop_lz4_bound(c->len));
-                        c->clen = hdrf_oracle_hadoop_lz4_frame(c->data, c->len, c->cdata);
-                    }
-                    bufpos = 0; curPos = 0;                                 /* :790-791 */
-                    lastBlockID[t]++;                                       /* :792 */
-                    lastBlockID[t + 4] = 0;                                 /* :793 */
-                    c = cont_find(o, (uint32_t)lastBlockID[t]);            /* :794-795 createNewFile */
-                    if (!c) c = cont_create(o, (uint32_t)lastBlockID[t]);
-                }
-                cont_append(c, data + cm[k].bbStart, cm[k].length);        /* :798 */
-                bufpos += cm[k].length;
-                cm[k].blockID = lastBlockID[t];                             /* :799 */
-                cm[k].blockStart = (int32_t)curPos;                         /* :800 setBlockStartStop */
-                cm[k].blockStop = (int32_t)(curPos + cm[k].length);
-                curPos += cm[k].length;                                     /* :801 */
-            }
-            meta_encode(&cm[k], setv + k * 11);                             /* :803 SET digest -> meta */
-        }
-        lastBlockID[t + 4] = bufpos;                                        /* :808 */
+        sj[t] = (store_job){o, data, cm, setv, n * t / nThread, n * (t + 1) / nThread, storeSize, lastBlockID, t};
+        /* the reference runs the ranges on three threadedStorer threads (:676-697), each closing and
+         * compressing its own containers; the CPU baselines do too (o->mt_store) */
+        if (o->mt_store && nThread > 1) sstarted[t] = pthread_create(&sth[t], NULL, store_range, &sj[t]) == 0;
+        if (!sstarted[t]) store_range(&sj[t]);
     }
+    for (int t = 0; t < nThread; t++)
+        if (sstarted[t]) pthread_join(sth[t], NULL);
     /* Pipelined SETs: thread 0's, then thread 1's, then thread 2's (each in chunk order).
      * Cross-thread order is racy in the reference; this fixes "last occurrence in chunk order wins". */
     for (int64_t k = 0; k < n; k++) kv_set(&o->index, dig + k * H, setv + k * 11);
@@ -534,6 +574,7 @@ int64_t hdrf_oracle_reduce_many_out(hdrf_oracle *o, const uint8_t *const *blocks
                                     const hdrf_oracle_out *out, int64_t *counts)
 {
     if (nthreads < 1) nthreads = 1;
+    o->mt_store = 1;                     /* CPU baseline: three concurrent storers per block */
     hash_pool p;
     memset(&p, 0, sizeof p);
     p.jobs = (hash_job *)calloc((size_t)(nblocks > 0 ? nblocks : 1), sizeof(hash_job));
@@ -567,6 +608,7 @@ int64_t hdrf_oracle_reduce_many_out(hdrf_oracle *o, const uint8_t *const *blocks
     for (int64_t i = 0; i < nblocks; i++) { free(p.jobs[i].off); free(p.jobs[i].dig); }
     free(th);
     free(p.jobs);
+    o->mt_store = 0;
     return rc < 0 ? rc : nblocks;
 }
 
@@ -601,14 +643,16 @@ int64_t hdrf_oracle_reduce_ref_shape(hdrf_oracle *o, const uint8_t *const *block
 {
     if (nhash < 1) nhash = 1;
     if (nhash > 64) nhash = 64;
-    for (int64_t i = 0; i < nblocks; i++) {
+    o->mt_store = 1;                     /* the three threadedStorer threads (:676-697) run at once */
+    int64_t rc = nblocks;
+    for (int64_t i = 0; i < nblocks && rc >= 0; i++) {
         const int64_t ocap = sizes[i] / 700 + 2;
         uint32_t *off = (uint32_t *)malloc((size_t)ocap * sizeof(uint32_t));
-        if (!off) return -2;
+        if (!off) { rc = -2; break; }
         const int64_t n = hdrf_oracle_chunk(blocks[i], sizes[i], off, ocap);
-        if (n < 0) { free(off); return -1; }
+        if (n < 0) { free(off); rc = -1; break; }
         uint8_t *dig = (uint8_t *)malloc((size_t)n * o->H + 1);
-        if (!dig) { free(off); return -2; }
+        if (!dig) { free(off); rc = -2; break; }
         pthread_t th[64];
         hash_range rg[64];
         int started[64] = {0};
@@ -622,10 +666,11 @@ int64_t hdrf_oracle_reduce_ref_shape(hdrf_oracle *o, const uint8_t *const *block
             if (started[t]) pthread_join(th[t], NULL);
         int64_t ss = 0;
         const int64_t r = reduce_hashed(o, blocks[i], sizes[i], ids[i], off, n, dig, NULL, NULL, NULL, NULL, &ss);
-        if (r < 0) return r;
+        if (r < 0) { rc = r; break; }
         if (store_sizes) store_sizes[i] = ss;
     }
-    return nblocks;
+    o->mt_store = 0;
+    return rc;
 }
 
 int hdrf_oracle_index_get(const hdrf_oracle *o, const uint8_t *digest, uint8_t out11[11])
@@ -683,17 +728,14 @@ int64_t hdrf_oracle_recipe(const hdrf_oracle *o, int64_t block_id, uint8_t *out,
 
 int64_t hdrf_oracle_container(const hdrf_oracle *o, uint32_t id, uint8_t *out, int64_t cap, int *closed)
 {
-    for (int64_t i = 0; i < o->ncont; i++)
-        if (o->cont[i].id == id) {
-            const container *c = &o->cont[i];
-            if (closed) *closed = c->closed;
-            const uint8_t *src = c->cdata ? c->cdata : c->data;   /* closed + compressor 2: the LZ4 file */
-            const int64_t len = c->cdata ? c->clen : c->len;
-            if (cap < len) return -(len + 2);
-            if (len) memcpy(out, src, (size_t)len);
-            return len;
-        }
-    return -1;
+    const container *c = cont_find(o, id);
+    if (!c) return -1;
+    if (closed) *closed = c->closed;
+    const uint8_t *src = c->cdata ? c->cdata : c->data;   /* closed + compressor 2: the LZ4 file */
+    const int64_t len = c->cdata ? c->clen : c->len;
+    if (cap < len) return -(len + 2);
+    if (len) memcpy(out, src, (size_t)len);
+    return len;
 }
 
 /* ------------------------------------------------------------------------------------------ */

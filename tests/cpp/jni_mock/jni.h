@@ -17,6 +17,7 @@ typedef jobject jclass;
 typedef jobject jarray;
 typedef jarray jbyteArray;
 typedef jarray jlongArray;
+typedef jarray jintArray;
 typedef jobject jstring;
 typedef uint8_t jboolean;
 
@@ -30,6 +31,8 @@ struct JNINativeInterface_ {
     jsize (*GetArrayLength)(JNIEnv *env, jarray array);
     jlong *(*GetLongArrayElements)(JNIEnv *env, jlongArray array, unsigned char *isCopy);
     void (*ReleaseLongArrayElements)(JNIEnv *env, jlongArray array, jlong *elems, jint mode);
+    jint *(*GetIntArrayElements)(JNIEnv *env, jintArray array, jboolean *isCopy);
+    void (*ReleaseIntArrayElements)(JNIEnv *env, jintArray array, jint *elems, jint mode);
     jbyteArray (*NewByteArray)(JNIEnv *env, jsize len);
     void (*SetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, const jbyte *buf);
     const char *(*GetStringUTFChars)(JNIEnv *env, jstring string, jboolean *isCopy);

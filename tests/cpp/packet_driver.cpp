@@ -1,22 +1,42 @@
 // packet_driver.cpp — the DataNode's packet-granular write path driven from native threads
-// through the C-ABI the JNI binding calls (BASELINE config 5; VERDICT r2 "no native driver of the
-// 64 KiB-packet path").
+// through the C-ABI the JNI binding calls (BASELINE config 5: "JNI-backed GPU ReductionScheme with
+// overlapped H2D copies under concurrent block writes incl. block mirroring").
 //
-// Reference shape: BlockReceiver.receivePacket appends every received packet to bf1
-// (DN/BlockReceiver.java:877-896; dfs.client-write-packet-size 64 KiB, hdfs-default.xml:1079-1080),
-// one DataXceiver thread per block, and the finished block is handed to the reducer
-// (:1258-1261).  Here T receiver threads each own one block at a time and call
-// hdrf_append_packet once per packet from pinned host memory; the main thread opens receive
-// buffers (hdrf_rx_begin) in block order, submits the received blocks in that order
-// (hdrf_submit_slot: the FIFO); a completer thread completes them (hdrf_wait_batch, which blocks
-// without the context lock) and drains the durable containers after every completed block
-// (hdrf_drain_containers, as hdrf_jni.c does) while the receivers take the next blocks.
+// Reference shape: BlockReceiver.receivePacket forwards every received packet to the next DataNode
+// of the write pipeline FIRST (packetReceiver.mirrorPacketTo(mirrorOut), DN/BlockReceiver.java:
+// 635-641) and then appends it to bf1 (:877-896; dfs.client-write-packet-size 64 KiB,
+// hdfs-default.xml:1079-1080), one DataXceiver thread per block; the finished block is handed to
+// the reducer (:1258-1261).  Here T receiver threads each own one block at a time; per packet they
+// forward it to their mirror (below) and then call hdrf_append_packet from pinned host memory.  The
+// main thread opens receive buffers (hdrf_rx_begin) in block order and submits the received blocks
+// in that order (the FIFO): one block per submit (hdrf_submit_slot, the reference's per-block
+// DDRunner) or every block of a receive round as one batch (--batch: hdrf_submit_slots).  A completer
+// thread completes the batches (hdrf_wait_batch, which blocks without the context lock) and drains the
+// durable containers after every completed batch (hdrf_drain_containers, as hdrf_jni.c does) while
+// the receivers take the next blocks.
 //
-// usage: packet_driver BLOCKS BLOCK_MIB PACKET_KIB THREADS STEPS [OUT_FILE]
+// Mirror (the downstream DataNode's end of mirrorOut), one consumer thread per receiver:
+//   ring    the packet is copied into a 32 MiB byte ring the consumer drains (mirrorOut as a
+//           buffered stream whose reader keeps up; the default)
+//   socket  the packet is written to an AF_UNIX stream socket the consumer reads (a loopback link)
+//   none    no mirroring (a single-replica write)
+// The consumer checksums every block it receives; after the run each block's mirrored checksum
+// must equal the checksum of the block's bytes ("mirror_ok").
+//
+// usage: packet_driver BLOCKS BLOCK_MIB PACKET_KIB THREADS STEPS [OUT_DIR] [--compressor C]
+//          [--mirror ring|socket|none] [--batch] [--mixed] [--container-kib K] [--arena-slots N]
+//          [--index-log2 L]
 //   The corpus is BASELINE config 2's (1 MiB segments, 50 % cross-block duplicates, seed
-//   20251015), generated on the device and copied to pinned host memory before the timed steps.
-//   Prints one JSON line; OUT_FILE (optional) receives "block n_chunks store_size" per block of
-//   the last step (the parity test compares them with the oracle).
+//   20251015; --mixed: config 4's mixed-entropy segments), generated on the device and copied to
+//   pinned host memory before the timed steps.  Prints one JSON line.  OUT_DIR (optional) receives
+//   the last step's results: blocks.txt ("block n_chunks store_size"), blk_<b>.bin per block
+//   (offsets u32[n], digests u8[n*H], is_new u8[n]) and containers.bin (the chunkDir the drained
+//   events built: records [u32 id][u32 closed][u64 len][bytes]); the parity test compares them
+//   with the oracle.
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -24,7 +44,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -65,10 +87,115 @@ static std::vector<uint32_t> corpus_roots(uint64_t seed, uint32_t dup_ppm, int64
         }                                                                                      \
     } while (0)
 
+// Position-keyed checksum of a byte stream fed in arbitrary pieces (the mirror's check that every
+// packet arrived downstream once, in order): sum over 8-byte words w_i of w_i * (2i + 1).
+struct StreamSum {
+    uint64_t sum = 0, word = 0, pos = 0;       // pos: bytes consumed
+    void feed(const uint8_t *p, uint64_t n)
+    {
+        while (n && (pos & 7)) {               // finish a partial word
+            word |= (uint64_t)*p++ << (8 * (pos & 7));
+            if ((++pos & 7) == 0) { sum += word * (2 * (pos / 8 - 1) + 1); word = 0; }
+            n--;
+        }
+        uint64_t i = pos / 8, s = 0;
+        const uint64_t nw = n / 8;
+        for (uint64_t k = 0; k < nw; k++) {
+            uint64_t w;
+            std::memcpy(&w, p + 8 * k, 8);
+            s += w * (2 * (i + k) + 1);
+        }
+        sum += s;
+        pos += 8 * nw;
+        p += 8 * nw;
+        n -= 8 * nw;
+        while (n) {
+            word |= (uint64_t)*p++ << (8 * (pos & 7));
+            if ((++pos & 7) == 0) { sum += word * (2 * (pos / 8 - 1) + 1); word = 0; }
+            n--;
+        }
+    }
+    uint64_t finish() const { return (pos & 7) ? sum + word * (2 * (pos / 8) + 1) : sum; }
+};
+
+// spin briefly, then sleep: an idle mirror consumer must not hold a core the receivers need
+static void backoff(int &spins)
+{
+    if (++spins < 64) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+}
+
+// One receiver's mirror: the packets of its blocks (blocks r, r + T, ... of every step, each S bytes)
+// go downstream in order; the consumer checksums each block.
+struct Mirror {
+    static constexpr uint64_t kRing = 32ull << 20;
+    int mode = 0;                                 // 1 ring, 2 socket
+    std::vector<uint8_t> ring;
+    alignas(64) std::atomic<uint64_t> head{0};    // bytes produced
+    alignas(64) std::atomic<uint64_t> tail{0};    // bytes consumed
+    int fd[2] = {-1, -1};
+    std::thread th;
+
+    void push(const uint8_t *p, uint64_t n)
+    {
+        if (mode == 2) {
+            while (n) {
+                const ssize_t w = write(fd[0], p, n);
+                if (w <= 0) { std::perror("mirror write"); std::exit(1); }
+                p += w;
+                n -= (uint64_t)w;
+            }
+            return;
+        }
+        while (n) {
+            const uint64_t h = head.load(std::memory_order_relaxed);
+            uint64_t room;
+            int spins = 0;
+            while ((room = kRing - (h - tail.load(std::memory_order_acquire))) == 0) backoff(spins);
+            const uint64_t off = h % kRing, m = std::min({n, room, kRing - off});
+            std::memcpy(ring.data() + off, p, m);
+            head.store(h + m, std::memory_order_release);
+            p += m;
+            n -= m;
+        }
+    }
+    // the consumer: `blocks` blocks of S bytes, checksums into sums[k]
+    void consume(int64_t blocks, int64_t S, uint64_t *sums)
+    {
+        std::vector<uint8_t> buf(mode == 2 ? (1u << 20) : 0);
+        for (int64_t k = 0; k < blocks; k++) {
+            StreamSum cs;
+            int64_t left = S;
+            while (left) {
+                if (mode == 2) {
+                    const ssize_t r = read(fd[1], buf.data(), (size_t)std::min<int64_t>(left, (int64_t)buf.size()));
+                    if (r <= 0) { std::perror("mirror read"); std::exit(1); }
+                    cs.feed(buf.data(), (uint64_t)r);
+                    left -= r;
+                    continue;
+                }
+                const uint64_t t = tail.load(std::memory_order_relaxed);
+                uint64_t avail;
+                int spins = 0;
+                while ((avail = head.load(std::memory_order_acquire) - t) == 0) backoff(spins);
+                const uint64_t off = t % kRing, m = std::min<uint64_t>({avail, (uint64_t)left, kRing - off});
+                cs.feed(ring.data() + off, m);
+                tail.store(t + m, std::memory_order_release);
+                left -= (int64_t)m;
+            }
+            sums[k] = cs.finish();
+        }
+    }
+};
+
 int main(int argc, char **argv)
 {
     if (argc < 6) {
-        std::fprintf(stderr, "usage: %s BLOCKS BLOCK_MIB PACKET_KIB THREADS STEPS [OUT_FILE]\n", argv[0]);
+        std::fprintf(stderr,
+                     "usage: %s BLOCKS BLOCK_MIB PACKET_KIB THREADS STEPS [OUT_DIR] [--compressor C] "
+                     "[--mirror ring|socket|none] [--batch] [--mixed] [--container-kib K] [--arena-slots N] "
+                     "[--index-log2 L]\n",
+                     argv[0]);
         return 2;
     }
     const int64_t nb = std::atoll(argv[1]);
@@ -76,36 +203,89 @@ int main(int argc, char **argv)
     const int64_t P = std::atoll(argv[3]) << 10;
     const int T = std::atoi(argv[4]);
     const int steps = std::atoi(argv[5]);
-    const char *out_file = argc > 6 ? argv[6] : nullptr;
+    const char *out_dir = nullptr;
+    int compressor = 1, mirror_mode = 1, mixed = 0, index_log2 = 27;
+    bool batch = false;
+    int64_t container = 1ll << 25, arena = 512;
+    for (int i = 6; i < argc; i++) {
+        const std::string a = argv[i];
+        const char *v = i + 1 < argc ? argv[i + 1] : "";
+        if (a == "--compressor") compressor = std::atoi(v), i++;
+        else if (a == "--mirror") {
+            const std::string m = v;
+            mirror_mode = m == "none" ? 0 : m == "socket" ? 2 : m == "ring" ? 1 : -1;
+            i++;
+        } else if (a == "--batch") batch = true;
+        else if (a == "--mixed") mixed = 1;
+        else if (a == "--container-kib") container = std::atoll(v) << 10, i++;
+        else if (a == "--arena-slots") arena = std::atoll(v), i++;
+        else if (a == "--index-log2") index_log2 = std::atoi(v), i++;
+        else if (a.size() && a[0] != '-' && !out_dir) out_dir = argv[i];
+        else {
+            std::fprintf(stderr, "bad argument %s\n", a.c_str());
+            return 2;
+        }
+    }
     const int64_t seg = 1 << 20, spb = S / seg;
-    if (nb < 1 || S < seg || P < 1 || T < 1 || T > 16 || steps < 1) return 2;
+    if (nb < 1 || S < seg || P < 1 || T < 1 || T > 16 || steps < 1 || mirror_mode < 0 ||
+        (compressor != 1 && compressor != 2))
+        return 2;
 
     hdrf_ctx *ctx = nullptr;
     hdrf_cfg cfg;
     hdrf_default_cfg(&cfg);
     cfg.max_block_bytes = S;
-    cfg.max_batch_blocks = 1;
-    cfg.index_log2 = 27;
-    cfg.arena_slots = 512;
+    cfg.max_batch_blocks = batch ? T : 1;
+    cfg.index_log2 = index_log2;
+    cfg.arena_slots = arena;
+    cfg.container_max = (uint32_t)container;
+    cfg.compressor = compressor;
     cfg.retain_containers = std::getenv("HDRF_DRIVER_NODRAIN") ? 0 : 1;
     if (int rc = hdrf_open(&cfg, &ctx)) {
         std::fprintf(stderr, "hdrf_open: %d\n", rc);
         return 1;
     }
+    const int H = hdrf_digest_len(ctx);
     // corpus on the device, then into pinned host memory (the received blocks)
     std::vector<uint32_t> roots = corpus_roots(20251015ull, 500000, nb, spb);
     void *dev = nullptr, *host = nullptr, *dbuf = nullptr;
     const int64_t dcap = 256ll << 20;
     CK(hdrf_dev_alloc(ctx, (uint64_t)(nb * S), &dev));
-    CK(hdrf_corpus_fill(ctx, (uint8_t *)dev, roots.data(), nb, spb, seg, 20251015ull));
+    CK(hdrf_corpus_fill_kind(ctx, (uint8_t *)dev, roots.data(), nb, spb, seg, 20251015ull, mixed));
     CK(hdrf_host_alloc(ctx, (uint64_t)(nb * S), &host));
     CK(hdrf_host_alloc(ctx, (uint64_t)dcap, &dbuf));
     CK(hdrf_memcpy_d2h(ctx, host, dev, (uint64_t)(nb * S)));
     CK(hdrf_dev_free(ctx, dev));
 
+    // mirrors: one per receiver index, alive over all steps
+    std::vector<Mirror> mirrors(mirror_mode ? T : 0);
+    std::vector<std::vector<uint64_t>> msum(mirrors.size());
+    for (int r = 0; r < (int)mirrors.size(); r++) {
+        Mirror &m = mirrors[(size_t)r];
+        m.mode = mirror_mode;
+        if (mirror_mode == 1) m.ring.resize(Mirror::kRing);
+        else {
+            if (socketpair(AF_UNIX, SOCK_STREAM, 0, m.fd)) { std::perror("socketpair"); return 1; }
+            int sz = 4 << 20;
+            setsockopt(m.fd[0], SOL_SOCKET, SO_SNDBUF, &sz, sizeof sz);
+            setsockopt(m.fd[1], SOL_SOCKET, SO_RCVBUF, &sz, sizeof sz);
+        }
+        int64_t mine = 0;                                   // blocks r, r + T, ... per step
+        for (int64_t b = r; b < nb; b += T) mine++;
+        msum[(size_t)r].assign((size_t)(mine * (steps + 1)), 0);
+        m.th = std::thread([&m, &msum, r, mine, steps, S]() { m.consume(mine * (steps + 1), S, msum[(size_t)r].data()); });
+    }
+
     std::vector<int64_t> n_chunks((size_t)nb), store((size_t)nb);
+    struct BlockOut {
+        std::vector<uint32_t> off;
+        std::vector<uint8_t> dig, isnew;
+    };
+    std::vector<BlockOut> bout(out_dir ? (size_t)nb : 0);
+    std::map<uint32_t, std::pair<std::vector<uint8_t>, uint32_t>> disk;      // the last step's chunkDir
+    bool capture = false;
     std::vector<hdrf_container_event> ev(4096);
-    int64_t drained_bytes = 0, done = 0;
+    int64_t drained_bytes = 0, drained_events = 0, done = 0, batches = 0;
     auto drain = [&]() {
         for (;;) {
             int64_t need = 0;
@@ -115,7 +295,24 @@ int main(int argc, char **argv)
                 std::exit(1);
             }
             if (n == 0) return;
-            for (int64_t i = 0; i < n; i++) drained_bytes += ev[(size_t)i].nbytes;
+            for (int64_t i = 0; i < n; i++) {
+                const hdrf_container_event &e = ev[(size_t)i];
+                drained_bytes += e.nbytes;
+                if (!capture) continue;
+                auto &f = disk[e.id];
+                const uint8_t *src = (const uint8_t *)dbuf + e.data_off;
+                if (e.closed) f.first.assign(src, src + e.nbytes);
+                else {
+                    if ((int64_t)f.first.size() != e.file_off) {
+                        std::fprintf(stderr, "append to %u at %lld, file has %zu\n", e.id, (long long)e.file_off,
+                                     f.first.size());
+                        std::exit(1);
+                    }
+                    f.first.insert(f.first.end(), src, src + e.nbytes);
+                }
+                f.second = (uint32_t)e.closed;
+            }
+            drained_events += n;
         }
     };
     const bool no_drain = std::getenv("HDRF_DRIVER_NODRAIN") != nullptr;      // A/B only
@@ -123,10 +320,25 @@ int main(int argc, char **argv)
     // (round-3 c1 shape); default: a completer thread does it while the receivers run, as the
     // reference's reducer/storer runs apart from the DataXceiver threads.
     const bool serial = std::getenv("HDRF_DRIVER_SERIAL") != nullptr;
-    auto complete = [&]() {
+    std::vector<int64_t> batch_len;                 // blocks per submitted batch, in order
+    auto complete = [&](int64_t bi) {
         CK(hdrf_wait_batch(ctx));
-        CK(hdrf_batch_info(ctx, 0, &n_chunks[(size_t)done], &store[(size_t)done]));
-        done++;
+        const int64_t k = batch_len[(size_t)bi];
+        for (int64_t i = 0; i < k; i++) {
+            const int64_t b = done + i;
+            CK(hdrf_batch_info(ctx, (int32_t)i, &n_chunks[(size_t)b], &store[(size_t)b]));
+            if (capture) {
+                BlockOut &o = bout[(size_t)b];
+                const int64_t n = n_chunks[(size_t)b];
+                o.off.resize((size_t)n);
+                o.dig.resize((size_t)(n * H));
+                o.isnew.resize((size_t)n);
+                CK(hdrf_batch_offsets(ctx, (int32_t)i, o.off.data(), n));
+                CK(hdrf_batch_digests(ctx, (int32_t)i, o.dig.data(), n * H));
+                CK(hdrf_batch_is_new(ctx, (int32_t)i, o.isnew.data(), n));
+            }
+        }
+        done += k;
         if (!no_drain) drain();
     };
     const int kDepth = 5, kRx = 16;                // HDRF_PIPELINE_DEPTH, receive buffers (hdrf.h)
@@ -134,42 +346,51 @@ int main(int argc, char **argv)
     for (int step = 0; step <= steps; step++) {    // step 0: warm-up
         CK(hdrf_reset(ctx));
         done = 0;
-        drained_bytes = 0;
+        drained_bytes = drained_events = 0;
+        capture = out_dir && step == steps;
+        if (capture) disk.clear();
         std::mutex mu;
         std::condition_variable cv;
-        int64_t submitted = 0, completed = 0;      // guarded by mu
+        int64_t submitted = 0, completed = 0;      // batches, guarded by mu
+        int64_t blocks_in_flight = 0;              // guarded by mu
+        batch_len.clear();
+        batch_len.reserve((size_t)nb);
+        const int64_t nbatch = batch ? (nb + T - 1) / T : nb;
         std::thread completer;
+        auto on_complete = [&](int64_t c) {
+            std::lock_guard<std::mutex> lk(mu);
+            completed = c + 1;
+            blocks_in_flight -= batch_len[(size_t)c];
+        };
         if (!serial)
             completer = std::thread([&]() {
-                for (int64_t c = 0; c < nb; c++) {
+                for (int64_t c = 0; c < nbatch; c++) {
                     {
                         std::unique_lock<std::mutex> lk(mu);
                         cv.wait(lk, [&] { return submitted > c; });
                     }
-                    complete();
-                    {
-                        std::lock_guard<std::mutex> lk(mu);
-                        completed = c + 1;
-                    }
+                    complete(c);
+                    on_complete(c);
                     cv.notify_all();
                 }
             });
-        auto in_flight = [&]() { std::lock_guard<std::mutex> lk(mu); return submitted - completed; };
-        auto wait_until = [&](int64_t max_in_flight) {          // completer frees slots / buffers
+        auto serial_complete_one = [&]() {
+            complete(completed);
+            on_complete(completed);
+        };
+        // the receive round may open k buffers once at most kRx - k are held by blocks in flight, and
+        // a submit needs a free pipeline slot
+        auto wait_until = [&](int64_t max_blocks, int64_t max_batches) {
             std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return submitted - completed <= max_in_flight; });
+            cv.wait(lk, [&] { return blocks_in_flight <= max_blocks && submitted - completed <= max_batches; });
         };
         const auto t0 = std::chrono::steady_clock::now();
         for (int64_t g = 0; g < nb; g += T) {
             const int k = (int)std::min<int64_t>(T, nb - g);
             if (serial) {
-                while (in_flight() + k > kRx || in_flight() >= kDepth) {
-                    complete();
-                    std::lock_guard<std::mutex> lk(mu);
-                    completed++;
-                }
+                while (blocks_in_flight + k > kRx) serial_complete_one();
             } else {
-                wait_until(kRx - k);
+                wait_until(kRx - k, kDepth);
             }
             std::vector<int32_t> rx((size_t)k);
             for (int i = 0; i < k; i++) CK(hdrf_rx_begin(ctx, (uint64_t)(g + i), &rx[(size_t)i]));
@@ -178,62 +399,114 @@ int main(int argc, char **argv)
             for (int i = 0; i < k; i++)
                 th.emplace_back([&, i]() {
                     const uint8_t *b = (const uint8_t *)host + (g + i) * S;
-                    for (int64_t o = 0; o < S; o += P)
-                        if (hdrf_append_packet(ctx, rx[(size_t)i], b + o, (uint64_t)std::min(P, S - o))) bad++;
+                    Mirror *m = mirrors.empty() ? nullptr : &mirrors[(size_t)i];
+                    for (int64_t o = 0; o < S; o += P) {
+                        const uint64_t n = (uint64_t)std::min(P, S - o);
+                        if (m) m->push(b + o, n);                  // mirrorPacketTo before bf1.put (:635-641)
+                        if (hdrf_append_packet(ctx, rx[(size_t)i], b + o, n)) bad++;
+                    }
                 });
             for (auto &t : th) t.join();
             if (bad) {
                 std::fprintf(stderr, "append failed: %s\n", hdrf_last_error(ctx));
                 return 1;
             }
-            for (int i = 0; i < k; i++) {
+            // submit in arrival (block) order: the whole round as one batch, or block by block
+            const int per = batch ? k : 1;
+            for (int i = 0; i < k; i += per) {
                 if (serial) {
-                    if (in_flight() >= kDepth) {
-                        complete();
-                        std::lock_guard<std::mutex> lk(mu);
-                        completed++;
-                    }
+                    if (submitted - completed >= kDepth) serial_complete_one();
                 } else {
-                    wait_until(kDepth - 1);
+                    wait_until(kRx, kDepth - 1);
                 }
-                CK(hdrf_submit_slot(ctx, rx[(size_t)i]));
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    batch_len.push_back(per);
+                }
+                if (per == 1) CK(hdrf_submit_slot(ctx, rx[(size_t)i]));
+                else CK(hdrf_submit_slots(ctx, per, rx.data() + i));
                 {
                     std::lock_guard<std::mutex> lk(mu);
                     submitted++;
+                    blocks_in_flight += per;
                 }
                 cv.notify_all();
             }
         }
         if (serial)
-            while (in_flight()) {
-                complete();
-                std::lock_guard<std::mutex> lk(mu);
-                completed++;
-            }
+            while (completed < submitted) serial_complete_one();
         else
             completer.join();
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        batches = nbatch;
         if (step > 0) {
             total_s += s;
             best = std::max(best, nb * S / s / 1e9);
         }
     }
+    // the mirror received every block of every step once, in order
+    bool mirror_ok = true;
+    int64_t mirrored = 0;
+    for (auto &m : mirrors) m.th.join();
+    if (!mirrors.empty()) {
+        std::vector<uint64_t> want((size_t)nb);
+        for (int64_t b = 0; b < nb; b++) {
+            StreamSum cs;
+            cs.feed((const uint8_t *)host + b * S, (uint64_t)S);
+            want[(size_t)b] = cs.finish();
+        }
+        for (int r = 0; r < T; r++) {
+            int64_t k = 0;
+            for (int step = 0; step <= steps; step++)
+                for (int64_t b = r; b < nb; b += T, k++) {
+                    mirror_ok &= msum[(size_t)r][(size_t)k] == want[(size_t)b];
+                    mirrored += S;
+                }
+        }
+        for (auto &m : mirrors)
+            if (m.mode == 2) { close(m.fd[0]); close(m.fd[1]); }
+    }
     int64_t stored = 0, chunks = 0;
     for (int64_t b = 0; b < nb; b++) { stored += store[(size_t)b]; chunks += n_chunks[(size_t)b]; }
     std::printf("{\"driver\": \"tests/cpp/packet_driver.cpp\", \"blocks\": %lld, \"block_bytes\": %lld, "
                 "\"packet_bytes\": %lld, \"threads\": %d, \"steps\": %d, \"GB_s\": %.3f, \"best_GB_s\": %.3f, "
-                "\"packets_per_step\": %lld, \"stored_bytes\": %lld, \"chunks\": %lld, "
-                "\"drained_bytes_last_step\": %lld}\n",
+                "\"packets_per_step\": %lld, \"stored_bytes\": %lld, \"chunks\": %lld, \"compressor\": %d, "
+                "\"corpus\": \"%s\", \"mirror\": \"%s\", \"mirror_ok\": %s, \"mirrored_bytes\": %lld, "
+                "\"submit\": \"%s\", \"batches_per_step\": %lld, \"container_bytes\": %lld, "
+                "\"drained_bytes_last_step\": %lld, \"drained_events_last_step\": %lld}\n",
                 (long long)nb, (long long)S, (long long)P, T, steps, nb * S * steps / total_s / 1e9, best,
-                (long long)(nb * ((S + P - 1) / P)), (long long)stored, (long long)chunks, (long long)drained_bytes);
-    if (out_file) {
-        FILE *f = std::fopen(out_file, "w");
+                (long long)(nb * ((S + P - 1) / P)), (long long)stored, (long long)chunks, compressor,
+                mixed ? "mixed" : "config2", mirror_mode == 0 ? "none" : mirror_mode == 1 ? "ring" : "socket",
+                mirror_ok ? "true" : "false", (long long)mirrored,
+                batch ? "hdrf_submit_slots (one batch per receive round)" : "hdrf_submit_slot (one block per batch)",
+                (long long)batches, (long long)container, (long long)drained_bytes, (long long)drained_events);
+    if (out_dir) {
+        const std::string d = out_dir;
+        FILE *f = std::fopen((d + "/blocks.txt").c_str(), "w");
         for (int64_t b = 0; b < nb; b++)
             std::fprintf(f, "%lld %lld %lld\n", (long long)b, (long long)n_chunks[(size_t)b], (long long)store[(size_t)b]);
         std::fclose(f);
+        for (int64_t b = 0; b < nb; b++) {
+            FILE *g = std::fopen((d + "/blk_" + std::to_string(b) + ".bin").c_str(), "wb");
+            const BlockOut &o = bout[(size_t)b];
+            std::fwrite(o.off.data(), 4, o.off.size(), g);
+            std::fwrite(o.dig.data(), 1, o.dig.size(), g);
+            std::fwrite(o.isnew.data(), 1, o.isnew.size(), g);
+            std::fclose(g);
+        }
+        FILE *c = std::fopen((d + "/containers.bin").c_str(), "wb");
+        for (auto &kv : disk) {
+            const uint32_t id = kv.first, closed = kv.second.second;
+            const uint64_t n = kv.second.first.size();
+            std::fwrite(&id, 4, 1, c);
+            std::fwrite(&closed, 4, 1, c);
+            std::fwrite(&n, 8, 1, c);
+            std::fwrite(kv.second.first.data(), 1, n, c);
+        }
+        std::fclose(c);
     }
     hdrf_host_free(ctx, host);
     hdrf_host_free(ctx, dbuf);
     hdrf_close(ctx);
-    return 0;
+    return mirror_ok ? 0 : 3;
 }
