@@ -172,6 +172,10 @@ struct hdrf_ctx {
     unsigned long long *d_gxe[2] = {nullptr, nullptr};  // [G] X1 records emitted per peer, per slot
     unsigned long long *d_gx_counts = nullptr;   // [G] X3 records emitted per peer (back phases)
     int64_t *d_gx_rcounts = nullptr;             // [G] records received per peer
+    // [G] X3 records each source will send this owner: one per record that holds its created entry's
+    // minimum block (own_decide), so the X3 receive counts need no exchange of their own
+    unsigned long long *d_gx_x3exp = nullptr;
+    std::vector<int64_t> gx_x3recv;
     uint32_t *d_oslot = nullptr;
     uint8_t *d_oflags = nullptr;
     const uint32_t *gx_x2 = nullptr;             // responses of the back batch (caller's buffer)
@@ -355,7 +359,7 @@ static void free_all(hdrf_ctx *ctx)
     ctx->rchunks.clear();
     void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch[0],
                     ctx->d_scratch[1], ctx->d_gxe[0], ctx->d_gxe[1], ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot,
-                    ctx->d_oflags, ctx->d_carena, ctx->d_fn};
+                    ctx->d_oflags, ctx->d_carena, ctx->d_fn, ctx->d_gx_x3exp};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
@@ -588,7 +592,8 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         if ((rc = dalloc(ctx, &ctx->d_scratch[0], (size_t)1 << lg)) || (rc = dalloc(ctx, &ctx->d_scratch[1], (size_t)1 << lg)) ||
             (rc = dalloc(ctx, &ctx->d_gxe[0], 64)) || (rc = dalloc(ctx, &ctx->d_gxe[1], 64)) ||
             (rc = dalloc(ctx, &ctx->d_gx_counts, 64)) ||
-            (rc = dalloc(ctx, &ctx->d_gx_rcounts, 64)) || (rc = dalloc(ctx, &ctx->d_oslot, nrec)) ||
+            (rc = dalloc(ctx, &ctx->d_gx_rcounts, 64)) || (rc = dalloc(ctx, &ctx->d_gx_x3exp, 64)) ||
+            (rc = dalloc(ctx, &ctx->d_oslot, nrec)) ||
             (rc = dalloc(ctx, &ctx->d_oflags, nrec))) {
         }
         // owner slots start defined (hdrf_gx_owner's kernels never read a slot the claim did not write
@@ -1999,9 +2004,10 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
     hipStream_t st = ctx->stB;
     HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(ctx->d_gx_x3exp, 0, sizeof(unsigned long long) * ctx->G, st));
     HIPCK(launch_gx_owner(ctx->cfg.hasher, x1_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap,
                           ctx->G, ctx->d_tab, ctx->cfg.index_log2, S.gx_batch, ctx->bfirst, tag_mask(ctx), ctx->d_oslot,
-                          ctx->d_oflags, S.d_coll, S.d_ncoll, ctx->coll_cap, x2_send, S.d_err, st));
+                          ctx->d_oflags, S.d_coll, S.d_ncoll, ctx->coll_cap, x2_send, ctx->d_gx_x3exp, S.d_err, st));
     // no host round trip: a device error (S.d_err) is read back with the batch by hdrf_gx_place, and
     // the X2 exchange may be enqueued on stream B right behind this kernel (hdrf_gx_stream)
     ctx->gx_bphase = 1;
@@ -2209,8 +2215,9 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     if (ctx->gx_scanned) HIPCK(hipMemcpyAsync(&got, ctx->d_alloc, sizeof got, hipMemcpyDeviceToHost, st));
     // the node's allocator after the last rank (the next batch and the "blockID" view start here)
     if (alloc_final) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_final, sizeof(AllocState), hipMemcpyHostToDevice, st));
-    std::vector<unsigned long long> cnt(ctx->G);
+    std::vector<unsigned long long> cnt(ctx->G), x3e(ctx->G);
     HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(x3e.data(), ctx->d_gx_x3exp, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nb, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nb, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
@@ -2231,7 +2238,19 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
     S.gx_compressed = false;
     if (int rc = complete_slot(ctx, si, false)) return rc;
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
+    ctx->gx_x3recv.assign(x3e.begin(), x3e.end());
     ctx->gx_bphase = 4;
+    return 0;
+}
+
+// The X3 receive counts this owner's decisions imply (valid from hdrf_gx_place to hdrf_gx_commit):
+// the X3 exchange needs no count exchange of its own.
+extern "C" int hdrf_gx_x3_counts(hdrf_ctx *ctx, int64_t *recv_counts)
+{
+    HDRF_LOCK(ctx);
+    if (int rc = gx_check(ctx, 4)) return rc;
+    if (!recv_counts) return set_err(ctx, HDRF_E_INVAL, "null counts");
+    for (int s = 0; s < ctx->G; s++) recv_counts[s] = ctx->gx_x3recv[(size_t)s];
     return 0;
 }
 
@@ -2304,8 +2323,12 @@ extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int6
     HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 4)) return rc;
     if (!x3_recv || !recv_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
-    for (int s = 0; s < ctx->G; s++)
+    for (int s = 0; s < ctx->G; s++) {
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
+        if (recv_counts[s] != ctx->gx_x3recv[(size_t)s])
+            return set_err(ctx, HDRF_E_DEVICE, "X3 receive count from rank " + std::to_string(s) +
+                                                   " disagrees with this owner's decisions");
+    }
     Slot &S = ctx->sl[ctx->gx_nback % 2];
     // compressor 2: the containers this rank closed must be Lz4Codec files before the batch commits
     // (container reads of closed containers take their bytes from the compressed arena)

@@ -186,7 +186,9 @@ __global__ void own_slow_kernel(const uint32_t *__restrict__ x1, IndexEntry *__r
 }
 
 // response per record: {owner slot, bit0 created this batch, bit1 record holds the minimum block}.
-// The record holding the minimum block (exactly one per entry) finalises nCopy.
+// The record holding the minimum block (exactly one per entry) finalises nCopy; when the entry was
+// created this batch its source will send one X3 location (its designated chunk), counted per source
+// in x3exp (the X3 receive counts, no exchange needed).
 // After a claim error (table full: a record's oslot was never written; collision list overflow:
 // its oslot names an entry holding another digest) no record touches the table again: every
 // response is "not created, not the minimum" so the sources designate nothing and send no X3
@@ -195,7 +197,7 @@ __global__ void __launch_bounds__(256) own_decide_kernel(const uint32_t *__restr
                                                          const int64_t *__restrict__ counts, int64_t cap,
                                                          IndexEntry *__restrict__ tab, const uint32_t *__restrict__ oslot,
                                                          uint32_t cur, uint32_t *__restrict__ x2,
-                                                         const int *__restrict__ err)
+                                                         unsigned long long *__restrict__ x3exp, const int *__restrict__ err)
 {
     const int s = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -218,6 +220,9 @@ __global__ void __launch_bounds__(256) own_decide_kernel(const uint32_t *__restr
     }
     x2[2 * r] = h;
     x2[2 * r + 1] = (created ? 1u : 0u) | (holds ? 2u : 0u);
+    // the lanes still here are a prefix of the wave (i < counts[s]; err is uniform): lane 0 counts
+    const unsigned long long m3 = ballot64(created && holds);
+    if (lane_id() == 0 && m3) atomicAdd(x3exp + s, (unsigned long long)__popcll(m3));
 }
 
 __global__ void __launch_bounds__(256) own_finish_kernel(const uint32_t *__restrict__ x2, const int64_t *__restrict__ counts,
@@ -307,8 +312,8 @@ hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int ca
 
 hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts, int64_t max_count, int64_t cap, int G,
                            IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst, unsigned long long tag_mask, uint32_t *oslot,
-                           uint8_t *oflags, uint32_t *coll, uint32_t *ncoll, int coll_cap, uint32_t *x2, int *err,
-                           hipStream_t st)
+                           uint8_t *oflags, uint32_t *coll, uint32_t *ncoll, int coll_cap, uint32_t *x2,
+                           unsigned long long *x3exp, int *err, hipStream_t st)
 {
     const int HW = hasher == 0 ? 5 : 7;
     dim3 g(gx_tiles(max_count), G);
@@ -328,7 +333,7 @@ hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts
         hipLaunchKernelGGL(own_slow_kernel<7>, dim3(1), dim3(64), 0, st, x1, tab, log2cap, cur, tag_mask, oslot, coll,
                            ncoll, coll_cap, err);
     }
-    hipLaunchKernelGGL(own_decide_kernel, g, dim3(256), 0, st, x1, HW + 2, counts, cap, tab, oslot, cur, x2, err);
+    hipLaunchKernelGGL(own_decide_kernel, g, dim3(256), 0, st, x1, HW + 2, counts, cap, tab, oslot, cur, x2, x3exp, err);
     hipLaunchKernelGGL(own_finish_kernel, g, dim3(256), 0, st, x2, counts, cap, tab, err);
     return hipGetLastError();
 }

@@ -117,8 +117,8 @@ hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int ca
                           hipStream_t st);
 hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts, int64_t max_count, int64_t cap, int G,
                            IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst, unsigned long long key, uint32_t *oslot,
-                           uint8_t *oflags, uint32_t *coll, uint32_t *ncoll, int coll_cap, uint32_t *x2, int *err,
-                           hipStream_t st);
+                           uint8_t *oflags, uint32_t *coll, uint32_t *ncoll, int coll_cap, uint32_t *x2,
+                           unsigned long long *x3exp, int *err, hipStream_t st);
 hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int ntiles, const uint32_t *offsets,
                             const IndexEntry *scratch, const uint32_t *slot, const uint32_t *x2, uint8_t *flags,
                             uint32_t *tilesum, hipStream_t st);

@@ -40,13 +40,19 @@ __device__ __forceinline__ int put_len(uint8_t *out, int op, int len)
     return op + n255 + 1;
 }
 
-// LDS of one wave's hash table.  byU16 (blocks < 64 KiB + 11): 8192 u16 entries, 16 KiB.  byU32
-// (larger blocks, <= 262,144 B): 4096 positions < 2^18 kept as a u16 low half + a 2-bit high part
-// (16 per dword, updated with LDS atomics), 9 KiB, so a CU holds 17 compressing waves instead of
-// 10 with u32 entries (the kernel is bound by waves in flight: each match waits on one read at
-// its candidate position).
-constexpr int kLzTabU16 = 16384;
-constexpr int kLzTabU32 = 9216;
+// LDS of one wave's hash table.  byU16 (blocks < 64 KiB + 11): 8192 u16 entries (16 KiB) + a 2-bit
+// tag per entry (2 KiB).  byU32 (larger blocks, <= 262,144 B): 4096 positions < 2^18 kept as a u16
+// low half (8 KiB) + a 4-bit nibble per entry (2 KiB, 8 per dword, updated with LDS atomics): bits
+// 0-1 the position's bits 16-17, bits 2-3 the tag.  10 KiB: 16 compressing waves per CU (the VGPR
+// limit) fill the CU's 160 KiB.
+// The tag is two bits of the hash product just below the table index bits: a function of the
+// entry's 4-byte value, so a candidate whose tag differs from the tag of the bytes being matched
+// cannot match (the sequential code's 4-byte compare fails) and is rejected without loading its
+// bytes; only tag hits (true matches and 1 in 4 of the false candidates) pay the dependent global
+// round trip (tools: a CPU count of the parse on the config-4 corpus finds 23 % (text) and 57 %
+// (binary records) of the chain candidates false).
+constexpr int kLzTabU16 = 16384 + 2048;
+constexpr int kLzTabU32 = 8192 + 2048;
 
 #ifdef HDRF_LZ4_PROF
 // profiling build only (scripts/r02_lzp.sh): shader-clock time per parse phase, summed over waves
@@ -71,41 +77,60 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
     const bool u16 = n < k64KLimit;
     const int hshift = u16 ? 32 - 13 : 32 - 12;
     unsigned short *tab16 = (unsigned short *)tabmem;   // byU16 entries, or the byU32 low halves
-    uint32_t *tabhi = (uint32_t *)(tabmem + 8192);      // byU32 bits 16-17, entry h at word h/16
+    uint32_t *tabx = (uint32_t *)(tabmem + (u16 ? 16384 : 8192));   // byU16: 2-bit tags; byU32: nibbles
+    auto hash = [&](uint32_t v) -> uint32_t { return (v * 2654435761u) >> hshift; };
+    auto tagof = [&](uint32_t v) -> uint32_t { return ((v * 2654435761u) >> (hshift - 2)) & 3u; };
     {
+        // every entry starts at position 0 (the zeroed table of LZ4_compress) with the tag of the
+        // bytes there
+        const uint32_t t0 = n >= 4 ? tagof(rd32u(src)) : 0u;
+        const uint32_t xw = u16 ? t0 * 0x55555555u : (t0 << 2) * 0x11111111u;
         uint32_t *t32 = (uint32_t *)tabmem;
-        const int nw = (u16 ? kLzTabU16 : kLzTabU32) / 4;
-        for (int i = l; i < nw; i += 64) t32[i] = 0;
+        const int nw0 = (u16 ? 16384 : 8192) / 4, nw = (u16 ? kLzTabU16 : kLzTabU32) / 4;
+        for (int i = l; i < nw; i += 64) t32[i] = i < nw0 ? 0u : xw;
     }
     __builtin_amdgcn_s_waitcnt(0);
     asm volatile("" ::: "memory");
-    auto tget = [&](uint32_t h) -> int {
-        return u16 ? (int)tab16[h] : (int)tab16[h] | (int)(((tabhi[h >> 4] >> (2 * (h & 15))) & 3u) << 16);
-    };
-    auto tput = [&](uint32_t h, int p) {
-        tab16[h] = (unsigned short)p;
-        if (!u16) {
-            const uint32_t sh = 2 * (h & 15);
-            const uint32_t cur = (tabhi[h >> 4] >> sh) & 3u, want = ((uint32_t)p >> 16) & 3u;
-            if (cur != want) atomicXor(&tabhi[h >> 4], (cur ^ want) << sh);   // lanes share words
+    // entry h: position and tag
+    auto tget = [&](uint32_t h, uint32_t &tg) -> int {
+        if (u16) {
+            tg = (tabx[h >> 4] >> (2 * (h & 15))) & 3u;
+            return (int)tab16[h];
         }
+        const uint32_t nb = (tabx[h >> 3] >> (4 * (h & 7))) & 15u;
+        tg = nb >> 2;
+        return (int)tab16[h] | (int)((nb & 3u) << 16);
     };
-    auto hash = [&](uint32_t v) -> uint32_t { return (v * 2654435761u) >> hshift; };
-    auto tswap = [&](uint32_t h, int p) -> int {    // old entry, then p (one read of each word)
+    auto xupd = [&](uint32_t h, int p, uint32_t tg) -> uint32_t {   // old nibble / tag field, then p, tg
+        if (u16) {
+            const uint32_t sh = 2 * (h & 15);
+            const uint32_t cur = (tabx[h >> 4] >> sh) & 3u;
+            if (cur != tg) atomicXor(&tabx[h >> 4], (cur ^ tg) << sh);   // lanes share words
+            return cur;
+        }
+        const uint32_t sh = 4 * (h & 7);
+        const uint32_t cur = (tabx[h >> 3] >> sh) & 15u, want = (((uint32_t)p >> 16) & 3u) | (tg << 2);
+        if (cur != want) atomicXor(&tabx[h >> 3], (cur ^ want) << sh);
+        return cur;
+    };
+    auto tput = [&](uint32_t h, int p, uint32_t tg) {
+        tab16[h] = (unsigned short)p;
+        xupd(h, p, tg);
+    };
+    auto tswap = [&](uint32_t h, int p, uint32_t tg, uint32_t &otg) -> int {   // old entry, then (p, tg)
         const int lo = (int)tab16[h];
         tab16[h] = (unsigned short)p;
-        if (u16) return lo;
-        const uint32_t sh = 2 * (h & 15);
-        const uint32_t cur = (tabhi[h >> 4] >> sh) & 3u, want = ((uint32_t)p >> 16) & 3u;
-        if (cur != want) atomicXor(&tabhi[h >> 4], (cur ^ want) << sh);   // lanes share words
-        return lo | (int)(cur << 16);
+        const uint32_t cur = xupd(h, p, tg);
+        if (u16) { otg = cur; return lo; }
+        otg = cur >> 2;
+        return lo | (int)((cur & 3u) << 16);
     };
 
     const int mflimit = n - kMfLimit, matchlimit = n - kLastLit;
     int op = 0, anchor = 0, ip = 0;
     LZP_INIT
     if (n >= kMfLimit + 1) {
-        if (l == 0) tput(hash(rd32u(src)), 0);        // first byte
+        if (l == 0) { const uint32_t v0 = rd32u(src); tput(hash(v0), 0, tagof(v0)); }   // first byte
         ip = 1;
         int fip = ip, attempts = (1 << 6) + 3, m = kLzFirstBatch;
         // Windows: lane l holds the 4 bytes at wb + 4l (forward) and at wb + dr + 4l (the
@@ -153,18 +178,24 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             // tags into the entries and reading them back.  Equal hashes: attempt i reads the
             // position of the last earlier attempt with its hash (else the pre-batch entry), found
             // with one ballot per hash bit; each hash keeps its last attempt up to the first match.
+            const uint32_t vt = tagof(v);
             int old = 0;
-            if (valid) old = tget(h);
+            uint32_t otg = 0;
+            if (valid) old = tget(h, otg);
             asm volatile("" ::: "memory");
             if (valid) tab16[h] = (unsigned short)l;
             asm volatile("" ::: "memory");
             const uint32_t tg = valid ? (uint32_t)tab16[h] : 0u;
             const bool collide = ballot64(valid && tg != (uint32_t)l) != 0;
             asm volatile("" ::: "memory");
-            if (valid) tab16[h] = (unsigned short)old;     // (the high parts were not touched)
+            if (valid) tab16[h] = (unsigned short)old;     // (the high parts and tags were not touched)
             asm volatile("" ::: "memory");
             unsigned long long eq = 0;
             int ref = old;
+            // the candidate's bytes: an earlier attempt of this batch is this wave's own value (no
+            // load); a table entry whose tag differs from v's cannot hold v (no load); else load
+            bool known = false;
+            uint32_t cv = ~v;
             if (collide) {
                 eq = vmask;
 #pragma unroll
@@ -176,17 +207,19 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 const unsigned long long below = eq & ((1ull << l) - 1ull);
                 const int prev = below ? 63 - __builtin_clzll(below) : l;
                 const int pipl = __builtin_amdgcn_ds_bpermute(prev << 2, ipl);
-                if (below) ref = pipl;
+                const uint32_t pv = (uint32_t)__builtin_amdgcn_ds_bpermute(prev << 2, (int)v);
+                if (below) { ref = pipl; cv = pv; known = true; }
             }
-            const uint32_t cv = rd32u(src + ref);          // ref is a position < n in every lane
-            const bool ok = valid && ref + kMaxDist >= ipl && cv == v;
+            const bool in = valid && ref + kMaxDist >= ipl;
+            if (in && !known && otg == vt) cv = rd32u(src + ref);   // ref is a position < n
+            const bool ok = in && cv == v;
             const unsigned long long okm = ballot64(ok);
             LZN(0);
             {                                             // commit: attempts up to the first match
                 const int last = okm ? __builtin_ctzll(okm) : 63;
                 const unsigned long long upto = last == 63 ? ~0ull : ((2ull << last) - 1ull);
                 const unsigned long long later = (l == 63 || !collide) ? 0ull : (eq & upto & (~0ull << (l + 1)));
-                if (valid && l <= last && !later) tput(h, ipl);
+                if (valid && l <= last && !later) tput(h, ipl, vt);
                 asm volatile("" ::: "memory");
             }
             LZP(0);
@@ -316,29 +349,35 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     // table: [h2] = ip - 2, r = [h0], [h0] = ip.  Distinct hashes: lanes 0 and 1
                     // do the two slots in one pass; equal hashes: r is ip - 2.
                     const uint32_t Nw = wload(ip);        // in flight under the table update
-                    const uint32_t h2 = hash(v2), h0 = hash(v0);
+                    const uint32_t h2 = hash(v2), h0 = hash(v0), t2 = tagof(v2), t0 = tagof(v0);
                     int r = 0;
+                    uint32_t rt = 0;
                     asm volatile("" ::: "memory");
                     if (h2 == h0) {
-                        if (l == 0) tput(h0, ip);
+                        if (l == 0) tput(h0, ip, t0);
                         r = ip - 2;
+                        rt = t2;
                     } else {
-                        if (l < 2) r = tswap(l == 0 ? h2 : h0, l == 0 ? ip - 2 : ip);
+                        uint32_t ot = 0;
+                        if (l < 2) r = tswap(l == 0 ? h2 : h0, l == 0 ? ip - 2 : ip, l == 0 ? t2 : t0, ot);
                         r = (int)rdlane((uint32_t)r, 1);
+                        rt = rdlane(ot, 1);
                     }
                     asm volatile("" ::: "memory");
                     LZP(3);
                     if (r + kMaxDist >= ip) {
-                        const uint32_t Cw = wload(r);      // one round trip
-                        const bool chain = rdlane(Cw, 0) == v0;
-                        LZP(4);
-                        if (chain) {
-                            LZN(2);
-                            mref = r;
-                            tpos = op++;
-                            tok = 0;
-                            Fw = Nw; Rw = Cw; have = true; hwb = ip;
-                            continue;
+                        if (rt == t0) {                    // a tag miss cannot chain: no load
+                            const uint32_t Cw = wload(r);  // one round trip
+                            const bool chain = rdlane(Cw, 0) == v0;
+                            LZP(4);
+                            if (chain) {
+                                LZN(2);
+                                mref = r;
+                                tpos = op++;
+                                tok = 0;
+                                Fw = Nw; Rw = Cw; have = true; hwb = ip;
+                                continue;
+                            }
                         }
                         Sw = Nw; sb = ip; swok = true;     // the search after the break starts in it
                     }

@@ -26,7 +26,7 @@ EXPORTS = [
     "hdrf_container_read", "hdrf_dev_alloc", "hdrf_dev_free", "hdrf_memcpy_h2d", "hdrf_memcpy_d2h",
     "hdrf_synchronize", "hdrf_corpus_fill", "hdrf_corpus_fill_kind", "hdrf_stage_times", "hdrf_reset",
     "hdrf_gx_layout_get", "hdrf_gx_front", "hdrf_gx_front_launch", "hdrf_gx_front_wait", "hdrf_gx_owner", "hdrf_gx_decide", "hdrf_gx_flush",
-    "hdrf_gx_place", "hdrf_gx_commit", "hdrf_gx_stream", "hdrf_gx_alloc_io", "hdrf_gx_piece", "hdrf_gx_compress", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
+    "hdrf_gx_place", "hdrf_gx_x3_counts", "hdrf_gx_commit", "hdrf_gx_stream", "hdrf_gx_alloc_io", "hdrf_gx_piece", "hdrf_gx_compress", "hdrf_get_stats", "hdrf_submit_batch", "hdrf_wait_batch",
     "hdrf_batch_nblocks", "hdrf_reconstruct", "hdrf_reconstruct_block", "hdrf_submit_host",
     "hdrf_host_alloc", "hdrf_host_free", "hdrf_stream_block", "hdrf_stream_block_host", "hdrf_lz4_file_decode",
     "hdrf_stream_file_decode", "hdrf_gzip_match_pass", "hdrf_gzip_parse", "hdrf_container_load",
@@ -197,13 +197,17 @@ def load():
         "hdrf_gx_decide": (ctypes.c_int, [_vp, _vp]),
         "hdrf_gx_flush": (ctypes.c_int, [_vp, _u8p, _u8p]),
         "hdrf_gx_place": (ctypes.c_int, [_vp, _u8p, _vp, _i64p]),
+        "hdrf_gx_x3_counts": (ctypes.c_int, [_vp, _i64p]),
         "hdrf_gx_commit": (ctypes.c_int, [_vp, _vp, _i64p]),
         "hdrf_gx_stream": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p)]),
         "hdrf_gx_alloc_io": (ctypes.c_int, [_vp, _u8p, _u8p]),
         "hdrf_gx_piece": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_int32]),
         "hdrf_gx_compress": (ctypes.c_int, [_vp]),
     }
+    ab_build = bool(os.environ.get("HDRF_LIB_PATH"))
     for name, (res, args) in sig.items():
+        if ab_build and not hasattr(L, name):
+            continue                 # an older build under A/B (HDRF_LIB_PATH) lacks a newer entry point
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
@@ -718,6 +722,12 @@ class Context:
 
     def gx_compress(self):
         return self._ck(self.L.hdrf_gx_compress(self._h))
+
+    def gx_x3_counts(self):
+        """X3 receive counts implied by this owner's decisions (after gx_place)."""
+        cnt = np.zeros(self.cfg.n_ranks, np.int64)
+        self._ck(self.L.hdrf_gx_x3_counts(self._h, _p(cnt, _i64p)))
+        return cnt
 
     def gx_commit(self, x3_recv, recv_counts):
         rc = np.ascontiguousarray(recv_counts, np.int64)

@@ -261,7 +261,7 @@ class NodeRank:
         if int(ctx.cfg.compressor) == 2:
             self._compress()
         t5 = time.perf_counter()
-        r3 = xc.counts(c3)
+        r3 = ctx.gx_x3_counts()          # implied by this owner's decisions: no count exchange
         xc.records(self.x3s, self.x3r, c3, r3, cap, w3)
         t6 = time.perf_counter()
         ctx.gx_commit(self.x3r.data_ptr(), r3)

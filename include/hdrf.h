@@ -353,7 +353,8 @@ int hdrf_reset(hdrf_ctx *ctx);
  *   hdrf_gx_alloc_scan <- every rank's descriptor: its allocator in + the node's after the batch
  *   hdrf_gx_flush  <- alloc_in (from the scan; or, without the scan, rank r gets rank r-1's
  *                     state over a rank-to-rank chain, rank 0 the node's)
- *   hdrf_gx_place  -> X3 send (locations of new entries)     all-to-all X3
+ *   hdrf_gx_place  -> X3 send (locations of new entries)     all-to-all X3 (receive counts from
+ *                     hdrf_gx_x3_counts: no count exchange)
  *   hdrf_gx_commit <- X3 recv
  * hdrf_reduce_block / hdrf_reduce_batch return HDRF_E_INVAL on such a context. */
 #define HDRF_ALLOC_STATE_BYTES 128
@@ -404,6 +405,10 @@ int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, 
 int hdrf_gx_alloc_io(hdrf_ctx *ctx, uint8_t *alloc_in, uint8_t *alloc_out);
 int hdrf_gx_piece(hdrf_ctx *ctx, uint32_t id, uint64_t off, uint64_t n, void *dev, int32_t write);
 int hdrf_gx_compress(hdrf_ctx *ctx);
+/* X3 receive counts (int64[n_ranks]) implied by this owner's hdrf_gx_owner decisions: one location
+ * per entry created this batch, from the rank holding its minimum block.  Valid from hdrf_gx_place to
+ * hdrf_gx_commit; hdrf_gx_commit refuses (HDRF_E_DEVICE) receive counts that differ from them. */
+int hdrf_gx_x3_counts(hdrf_ctx *ctx, int64_t *recv_counts);
 int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts);
 /* The stream the back phases (hdrf_gx_owner .. hdrf_gx_commit) run on (a hipStream_t).  A caller
  * that enqueues its X1 / X2 record exchanges on it (RCCL collectives issued on this stream,
