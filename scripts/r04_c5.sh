@@ -11,6 +11,8 @@ run() {   # name, args...
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); p=d.get('pcie',{}); print(sys.argv[2], d['value'], 'mirror', d.get('mirror'), 'bidir', p.get('bidirectional_GB_s_raw_copy'), 'h2d', p.get('h2d_GB_s_raw_copy'), 'v/bidir', p.get('value_over_bidirectional_raw'), 'drain', p.get('d2h_GB_s_drain'))" gpurun_out/r04_c5_${n}_$V.json.log $n
 }
 run pk64_c1_ring --packet-driver cpp --packet-kib 64 --mirror ring --compressor 1
+run pk64_c1_ring_r2 --packet-driver cpp --packet-kib 64 --mirror ring --compressor 1
+run pk64_c1_ring_r3 --packet-driver cpp --packet-kib 64 --mirror ring --compressor 1
 run pk64_c1_ring_batch --packet-driver cpp --packet-kib 64 --mirror ring --compressor 1 --packet-batch
 run pk64_c2_ring --packet-driver cpp --packet-kib 64 --mirror ring --compressor 2
 run pk64_c2_ring_batch --packet-driver cpp --packet-kib 64 --mirror ring --compressor 2 --packet-batch

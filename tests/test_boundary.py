@@ -333,6 +333,59 @@ def test_packet_receive_matches_oracle():
     ctx.close()
 
 
+def test_packet_rounds_submitted_as_batches():
+    """hdrf_submit_slots (JNI submitBlocks): the blocks received in one round go in as ONE batch in
+    the order listed (the FIFO), a round of 1, 3 and 4 blocks including an empty one; the per-block
+    results and the final state equal the sequential oracle's.  A repeated or unknown receive
+    buffer, or more blocks than max_batch_blocks, is refused before anything is submitted, and the
+    buffers are free again once the batch completes."""
+    rng = np.random.default_rng(73)
+    blocks = _blocks(73, 8, 700_000)
+    blocks[5] = np.zeros(0, np.uint8)
+    ids = [8600 + i for i in range(len(blocks))]
+    ctx = Context(container_max=1 << 20, max_block_bytes=2 << 20, max_batch_blocks=4, index_log2=20, arena_slots=64)
+    ora = Oracle(max_size=1 << 20)
+    rounds = [[0], [1, 2, 3], [4, 5, 6, 7]]
+    pending = []
+    for rnd in rounds:
+        rxs = [ctx.rx_begin(ids[b]) for b in rnd]
+        for b, rx in zip(rnd, rxs):
+            o = 0
+            while o < len(blocks[b]):
+                n = int(rng.choice([1000, 65536, 300_001]))
+                p = np.ascontiguousarray(blocks[b][o:o + n])
+                ctx.append_packet(rx, p.ctypes.data, len(p))
+                o += n
+        if len(rxs) > 1:
+            with pytest.raises(HdrfError) as ei:                  # the same buffer twice
+                ctx.submit_slots([rxs[0], rxs[0]])
+            assert ei.value.code == -1
+        with pytest.raises(HdrfError) as ei:                      # more than max_batch_blocks
+            ctx.submit_slots(rxs + [rxs[0]] * (5 - len(rxs)))
+        assert ei.value.code == -1
+        ctx.submit_slots(rxs)
+        pending.append(rnd)
+        if len(pending) == 2:
+            ctx.wait_batch()
+            done = pending.pop(0)
+            assert ctx.last_nblocks() == len(done)
+            for i, b in enumerate(done):
+                compare_block(ctx.batch_result(i), ora.reduce(blocks[b], ids[b]), tag=f"round block {b}")
+    while pending:
+        ctx.wait_batch()
+        done = pending.pop(0)
+        assert ctx.last_nblocks() == len(done)
+        for i, b in enumerate(done):
+            compare_block(ctx.batch_result(i), ora.reduce(blocks[b], ids[b]), tag=f"round block {b}")
+    with pytest.raises(HdrfError):                                # no such receive buffer any more
+        ctx.submit_slots([0])
+    rxs = [ctx.rx_begin(9000 + k) for k in range(16)]             # all sixteen are free again
+    for rx in rxs:
+        ctx.rx_cancel(rx)
+    compare_state(ctx, ora, ids, tag="packet rounds")
+    ctx.close()
+
+
 def test_packet_receivers_on_concurrent_threads():
     """Four receiver threads (one per block, as DataXceiver threads are) append their blocks' ragged
     packets at the same time (hdrf_append_packet takes no context lock); the blocks are then
