@@ -2743,8 +2743,14 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
     for (uint32_t id : ctx->pend_closed) {
         auto it = ctx->containers.find(id);
         if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_DEVICE, "undrained container missing");
-        const bool lz = c.compressor == 2;
-        todo.push_back(Pend{id, 1, 0, lz ? (int64_t)it->second.clen : (int64_t)it->second.len, it->second});
+        if (c.compressor == 2) {                          // the whole Lz4Codec file replaces the raw one
+            todo.push_back(Pend{id, 1, 0, (int64_t)it->second.clen, it->second});
+        } else {
+            // the storer's close rewrites the file as prevData || buffer (:754-786): the bytes already
+            // handed out plus the rest, so only the rest travels (file_off = the bytes handed out)
+            const int64_t done = ctx->handed.count(id) ? ctx->handed[id] : 0;
+            todo.push_back(Pend{id, 1, done, (int64_t)it->second.len - done, it->second});
+        }
     }
     const size_t nclosed = todo.size();
     for (int t = 0; t < c.n_thread; t++) {

@@ -239,8 +239,11 @@ int64_t hdrf_container_read(hdrf_ctx *ctx, uint32_t id, uint8_t *out, int64_t ca
 
 /* Durable containers (cfg.retain_containers = 1): what the storers wrote to chunkDir since the
  * last drain (DN/DataDeduplicator.java:748-818).  Each event is one file operation:
- *   closed = 1   the container closed: (re)write the whole file chunkDir+id with nbytes bytes (raw,
- *                or the Lz4Codec stream under compressor 2; :748-786)
+ *   closed = 1   the container closed (:748-786): write nbytes bytes at file_off of chunkDir+id and
+ *                the file is final.  Under compressor 2 file_off = 0 and the bytes are the whole
+ *                Lz4Codec file (rewrite it).  Under compressor 1 the storer's rewrite (prevData ||
+ *                buffer) leaves the bytes already handed out in place, so only the rest travels:
+ *                file_off = the file's length so far (0 when nothing was handed out yet)
  *   closed = 0   the open container grew: write nbytes bytes at file_off (= the file's length so
  *                far) of chunkDir+id, creating it when file_off == 0 (:806-818)
  * The bytes of event i are out[data_off, data_off + nbytes).  Events come in order (closes in

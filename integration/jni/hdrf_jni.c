@@ -97,7 +97,9 @@ static int write_event(const char *dir, const hdrf_container_event *e, const uin
 {
     char path[4096];
     snprintf(path, sizeof path, "%s%u", dir, e->id);   /* DataNode.chunkDir + id (:754, :811) */
-    FILE *f = fopen(path, (e->closed || e->file_off == 0) ? "wb" : "r+b");
+    /* file_off == 0: (re)write the file (a new container, or a closed Lz4Codec file); otherwise the
+     * bytes go at the file's end (an open container's growth, or a raw container's closing tail) */
+    FILE *f = fopen(path, e->file_off == 0 ? "wb" : "r+b");
     if (!f) return -1;
     int ok = fseeko(f, (off_t)e->file_off, SEEK_SET) == 0 &&
              fwrite(data, 1, (size_t)e->nbytes, f) == (size_t)e->nbytes;

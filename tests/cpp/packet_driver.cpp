@@ -301,8 +301,8 @@ int main(int argc, char **argv)
                 if (!capture) continue;
                 auto &f = disk[e.id];
                 const uint8_t *src = (const uint8_t *)dbuf + e.data_off;
-                if (e.closed) f.first.assign(src, src + e.nbytes);
-                else {
+                if (e.file_off == 0) f.first.assign(src, src + e.nbytes);   // (re)write
+                else {                                                       // the file grows
                     if ((int64_t)f.first.size() != e.file_off) {
                         std::fprintf(stderr, "append to %u at %lld, file has %zu\n", e.id, (long long)e.file_off,
                                      f.first.size());

@@ -110,13 +110,13 @@ def test_threads_with_racing_views_are_serialised():
 def _apply(disk, events):
     """The storer's file operations on a dict chunkDir: closed -> rewrite, open -> write at offset."""
     for cid, closed, off, data in events:
-        if closed:
-            disk[cid] = (bytearray(data), True)
-        else:
+        if off == 0:                                  # (re)write: a new file, or a closed Lz4Codec file
+            disk[cid] = (bytearray(data), bool(closed))
+        else:                                         # the file grows (closed: its last bytes, compressor 1)
             f = disk.get(cid, (bytearray(), False))[0]
             assert len(f) == off, f"append to {cid} at {off}, file has {len(f)}"
             f[off:] = data
-            disk[cid] = (f, False)
+            disk[cid] = (f, bool(closed))
 
 
 @pytest.mark.parametrize("compressor", [1, 2])
