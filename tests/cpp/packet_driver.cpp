@@ -6,14 +6,14 @@
 // of the write pipeline FIRST (packetReceiver.mirrorPacketTo(mirrorOut), DN/BlockReceiver.java:
 // 635-641) and then appends it to bf1 (:877-896; dfs.client-write-packet-size 64 KiB,
 // hdfs-default.xml:1079-1080), one DataXceiver thread per block; the finished block is handed to
-// the reducer (:1258-1261).  Here T receiver threads each own one block at a time; per packet they
-// forward it to their mirror (below) and then call hdrf_append_packet from pinned host memory.  The
-// main thread opens receive buffers (hdrf_rx_begin) in block order and submits the received blocks
-// in that order (the FIFO): one block per submit (hdrf_submit_slot, the reference's per-block
-// DDRunner) or every block of a receive round as one batch (--batch: hdrf_submit_slots).  A completer
-// thread completes the batches (hdrf_wait_batch, which blocks without the context lock) and drains the
-// durable containers after every completed batch (hdrf_drain_containers, as hdrf_jni.c does) while
-// the receivers take the next blocks.
+// the reducer (:1258-1261).  Here T receiver threads (DataXceivers) each take the next block as soon
+// as they finished the last one, open a receive buffer for it (hdrf_rx_begin), and per packet forward
+// it to their mirror (below) and then call hdrf_append_packet from pinned host memory.  The main
+// thread submits the received blocks in block order (the FIFO): one block per submit
+// (hdrf_submit_slot, the reference's per-block DDRunner) or every block received in order since the
+// last submit as one batch (--batch: hdrf_submit_slots).  A completer thread completes the batches
+// (hdrf_wait_batch, which blocks without the context lock) and drains the durable containers after
+// every completed batch (hdrf_drain_containers, as hdrf_jni.c does) while the receivers go on.
 //
 // Mirror (the downstream DataNode's end of mirrorOut), one consumer thread per receiver:
 //   ring    the packet is copied into a 32 MiB byte ring the consumer drains (mirrorOut as a
@@ -125,8 +125,8 @@ static void backoff(int &spins)
     else std::this_thread::sleep_for(std::chrono::microseconds(20));
 }
 
-// One receiver's mirror: the packets of its blocks (blocks r, r + T, ... of every step, each S bytes)
-// go downstream in order; the consumer checksums each block.
+// One receiver's mirror: the packets of the blocks it receives (each S bytes) go downstream in order;
+// the consumer checksums each block until the stream ends.
 struct Mirror {
     static constexpr uint64_t kRing = 32ull << 20;
     int mode = 0;                                 // 1 ring, 2 socket
@@ -159,31 +159,46 @@ struct Mirror {
             n -= m;
         }
     }
-    // the consumer: `blocks` blocks of S bytes, checksums into sums[k]
-    void consume(int64_t blocks, int64_t S, uint64_t *sums)
+    // the consumer: checksums of consecutive S-byte blocks until the stream ends (socket: EOF; ring:
+    // `done` set once every producer has stopped)
+    void consume(int64_t S, std::vector<uint64_t> &sums, const std::atomic<bool> &done)
     {
         std::vector<uint8_t> buf(mode == 2 ? (1u << 20) : 0);
-        for (int64_t k = 0; k < blocks; k++) {
-            StreamSum cs;
-            int64_t left = S;
-            while (left) {
-                if (mode == 2) {
-                    const ssize_t r = read(fd[1], buf.data(), (size_t)std::min<int64_t>(left, (int64_t)buf.size()));
-                    if (r <= 0) { std::perror("mirror read"); std::exit(1); }
-                    cs.feed(buf.data(), (uint64_t)r);
-                    left -= r;
-                    continue;
+        StreamSum cs;
+        int64_t left = S;
+        auto got = [&](const uint8_t *p, uint64_t m) {
+            while (m) {
+                const uint64_t k = std::min<uint64_t>(m, (uint64_t)left);
+                cs.feed(p, k);
+                p += k;
+                m -= k;
+                left -= (int64_t)k;
+                if (left == 0) {
+                    sums.push_back(cs.finish());
+                    cs = StreamSum();
+                    left = S;
                 }
-                const uint64_t t = tail.load(std::memory_order_relaxed);
-                uint64_t avail;
-                int spins = 0;
-                while ((avail = head.load(std::memory_order_acquire) - t) == 0) backoff(spins);
-                const uint64_t off = t % kRing, m = std::min<uint64_t>({avail, (uint64_t)left, kRing - off});
-                cs.feed(ring.data() + off, m);
-                tail.store(t + m, std::memory_order_release);
-                left -= (int64_t)m;
             }
-            sums[k] = cs.finish();
+        };
+        for (;;) {
+            if (mode == 2) {
+                const ssize_t r = read(fd[1], buf.data(), buf.size());
+                if (r < 0) { std::perror("mirror read"); std::exit(1); }
+                if (r == 0) return;                      // the receiver closed its end
+                got(buf.data(), (uint64_t)r);
+                continue;
+            }
+            const uint64_t t = tail.load(std::memory_order_relaxed);
+            const uint64_t avail = head.load(std::memory_order_acquire) - t;
+            if (avail == 0) {
+                if (done.load(std::memory_order_acquire) && head.load(std::memory_order_acquire) == t) return;
+                int spins = 0;
+                backoff(spins);
+                continue;
+            }
+            const uint64_t off = t % kRing, m = std::min<uint64_t>(avail, kRing - off);
+            got(ring.data() + off, m);
+            tail.store(t + m, std::memory_order_release);
         }
     }
 };
@@ -235,7 +250,7 @@ int main(int argc, char **argv)
     hdrf_cfg cfg;
     hdrf_default_cfg(&cfg);
     cfg.max_block_bytes = S;
-    cfg.max_batch_blocks = batch ? T : 1;
+    cfg.max_batch_blocks = batch ? 16 : 1;
     cfg.index_log2 = index_log2;
     cfg.arena_slots = arena;
     cfg.container_max = (uint32_t)container;
@@ -259,7 +274,9 @@ int main(int argc, char **argv)
 
     // mirrors: one per receiver index, alive over all steps
     std::vector<Mirror> mirrors(mirror_mode ? T : 0);
-    std::vector<std::vector<uint64_t>> msum(mirrors.size());
+    std::vector<std::vector<uint64_t>> msum(mirrors.size());        // per receiver: mirrored block sums
+    std::vector<std::vector<int64_t>> mids(mirrors.size());         // per receiver: the blocks it received
+    std::atomic<bool> mirror_done{false};
     for (int r = 0; r < (int)mirrors.size(); r++) {
         Mirror &m = mirrors[(size_t)r];
         m.mode = mirror_mode;
@@ -270,10 +287,7 @@ int main(int argc, char **argv)
             setsockopt(m.fd[0], SOL_SOCKET, SO_SNDBUF, &sz, sizeof sz);
             setsockopt(m.fd[1], SOL_SOCKET, SO_RCVBUF, &sz, sizeof sz);
         }
-        int64_t mine = 0;                                   // blocks r, r + T, ... per step
-        for (int64_t b = r; b < nb; b += T) mine++;
-        msum[(size_t)r].assign((size_t)(mine * (steps + 1)), 0);
-        m.th = std::thread([&m, &msum, r, mine, steps, S]() { m.consume(mine * (steps + 1), S, msum[(size_t)r].data()); });
+        m.th = std::thread([&m, &msum, &mirror_done, r, S]() { m.consume(S, msum[(size_t)r], mirror_done); });
     }
 
     std::vector<int64_t> n_chunks((size_t)nb), store((size_t)nb);
@@ -352,101 +366,156 @@ int main(int argc, char **argv)
         std::mutex mu;
         std::condition_variable cv;
         int64_t submitted = 0, completed = 0;      // batches, guarded by mu
-        int64_t blocks_in_flight = 0;              // guarded by mu
+        int64_t sub_blocks = 0;                    // blocks submitted, guarded by mu
+        std::vector<int32_t> rxof((size_t)nb, -1); // receive buffer of each fully received block (mu)
         batch_len.clear();
         batch_len.reserve((size_t)nb);
-        const int64_t nbatch = batch ? (nb + T - 1) / T : nb;
         std::thread completer;
         auto on_complete = [&](int64_t c) {
-            std::lock_guard<std::mutex> lk(mu);
-            completed = c + 1;
-            blocks_in_flight -= batch_len[(size_t)c];
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                completed = c + 1;
+            }
+            cv.notify_all();                        // receive buffers and a pipeline slot are free again
         };
+        int64_t nbatch = -1;                       // known once the submitter has finished (mu)
         if (!serial)
             completer = std::thread([&]() {
-                for (int64_t c = 0; c < nbatch; c++) {
+                for (int64_t c = 0;; c++) {
                     {
                         std::unique_lock<std::mutex> lk(mu);
-                        cv.wait(lk, [&] { return submitted > c; });
+                        cv.wait(lk, [&] { return submitted > c || (nbatch >= 0 && c >= nbatch); });
+                        if (nbatch >= 0 && c >= nbatch) return;
                     }
                     complete(c);
                     on_complete(c);
-                    cv.notify_all();
                 }
             });
         auto serial_complete_one = [&]() {
-            complete(completed);
-            on_complete(completed);
-        };
-        // the receive round may open k buffers once at most kRx - k are held by blocks in flight, and
-        // a submit needs a free pipeline slot
-        auto wait_until = [&](int64_t max_blocks, int64_t max_batches) {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return blocks_in_flight <= max_blocks && submitted - completed <= max_batches; });
-        };
-        const auto t0 = std::chrono::steady_clock::now();
-        for (int64_t g = 0; g < nb; g += T) {
-            const int k = (int)std::min<int64_t>(T, nb - g);
-            if (serial) {
-                while (blocks_in_flight + k > kRx) serial_complete_one();
-            } else {
-                wait_until(kRx - k, kDepth);
+            int64_t c;
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                c = completed;
             }
-            std::vector<int32_t> rx((size_t)k);
-            for (int i = 0; i < k; i++) CK(hdrf_rx_begin(ctx, (uint64_t)(g + i), &rx[(size_t)i]));
-            std::vector<std::thread> th;
-            std::atomic<int> bad{0};
-            for (int i = 0; i < k; i++)
-                th.emplace_back([&, i]() {
-                    const uint8_t *b = (const uint8_t *)host + (g + i) * S;
-                    Mirror *m = mirrors.empty() ? nullptr : &mirrors[(size_t)i];
+            complete(c);
+            on_complete(c);
+        };
+        std::atomic<int64_t> next_block{0};
+        std::atomic<int> bad{0};
+        const auto t0 = std::chrono::steady_clock::now();
+        // receivers: each takes the next block as soon as its last one is received; a block may start
+        // only kRx blocks ahead of the submit order, so the lowest unsubmitted block always finds a
+        // receive buffer once the batches in flight complete
+        std::vector<std::thread> th;
+        for (int i = 0; i < T; i++)
+            th.emplace_back([&, i]() {
+                Mirror *m = mirrors.empty() ? nullptr : &mirrors[(size_t)i];
+                for (;;) {
+                    const int64_t b = next_block.fetch_add(1);
+                    if (b >= nb) return;
+                    int32_t rx = -1;
+                    for (;;) {
+                        {
+                            std::unique_lock<std::mutex> lk(mu);
+                            cv.wait(lk, [&] { return b < sub_blocks + kRx; });
+                        }
+                        const int rc = hdrf_rx_begin(ctx, (uint64_t)b, &rx);
+                        if (rc == 0) break;
+                        if (rc != HDRF_E_CAPACITY) { bad++; return; }
+                        std::unique_lock<std::mutex> lk(mu);       // all sixteen in use: wait for a completion
+                        const int64_t c0 = completed;
+                        cv.wait_for(lk, std::chrono::milliseconds(5), [&] { return completed != c0; });
+                    }
+                    if (m) mids[(size_t)i].push_back(b);
+                    const uint8_t *src = (const uint8_t *)host + b * S;
                     for (int64_t o = 0; o < S; o += P) {
                         const uint64_t n = (uint64_t)std::min(P, S - o);
-                        if (m) m->push(b + o, n);                  // mirrorPacketTo before bf1.put (:635-641)
-                        if (hdrf_append_packet(ctx, rx[(size_t)i], b + o, n)) bad++;
+                        if (m) m->push(src + o, n);                 // mirrorPacketTo before bf1.put (:635-641)
+                        if (hdrf_append_packet(ctx, rx, src + o, n)) { bad++; return; }
                     }
-                });
-            for (auto &t : th) t.join();
-            if (bad) {
-                std::fprintf(stderr, "append failed: %s\n", hdrf_last_error(ctx));
-                return 1;
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        rxof[(size_t)b] = rx;
+                    }
+                    cv.notify_all();
+                }
+            });
+        // submitter: blocks in order; --batch hands over every block received in order so far (<= 16)
+        int64_t nb_done = 0, nbt = 0;
+        while (nb_done < nb && !bad) {
+            std::vector<int32_t> rxs;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return rxof[(size_t)nb_done] >= 0 || bad; });
+                if (bad) break;
+                const int64_t lim = batch ? 16 : 1;
+                for (int64_t b = nb_done; b < nb && (int64_t)rxs.size() < lim && rxof[(size_t)b] >= 0; b++)
+                    rxs.push_back(rxof[(size_t)b]);
             }
-            // submit in arrival (block) order: the whole round as one batch, or block by block
-            const int per = batch ? k : 1;
-            for (int i = 0; i < k; i += per) {
-                if (serial) {
-                    if (submitted - completed >= kDepth) serial_complete_one();
-                } else {
-                    wait_until(kRx, kDepth - 1);
+            if (serial) {
+                for (;;) {
+                    bool full;
+                    {
+                        std::lock_guard<std::mutex> lk(mu);
+                        full = submitted - completed >= kDepth;
+                    }
+                    if (!full) break;
+                    serial_complete_one();
                 }
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    batch_len.push_back(per);
-                }
-                if (per == 1) CK(hdrf_submit_slot(ctx, rx[(size_t)i]));
-                else CK(hdrf_submit_slots(ctx, per, rx.data() + i));
-                {
-                    std::lock_guard<std::mutex> lk(mu);
-                    submitted++;
-                    blocks_in_flight += per;
-                }
-                cv.notify_all();
+            } else {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return submitted - completed <= kDepth - 1; });
             }
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                batch_len.push_back((int64_t)rxs.size());
+            }
+            if (rxs.size() == 1) CK(hdrf_submit_slot(ctx, rxs[0]));
+            else CK(hdrf_submit_slots(ctx, (int32_t)rxs.size(), rxs.data()));
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                submitted++;
+                sub_blocks += (int64_t)rxs.size();
+            }
+            cv.notify_all();
+            nb_done += (int64_t)rxs.size();
+            nbt++;
         }
+        for (auto &t : th) t.join();
+        if (bad) {
+            std::fprintf(stderr, "receive failed: %s\n", hdrf_last_error(ctx));
+            return 1;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            nbatch = nbt;
+        }
+        cv.notify_all();
         if (serial)
-            while (completed < submitted) serial_complete_one();
+            while (true) {
+                bool left;
+                {
+                    std::lock_guard<std::mutex> lk(mu);
+                    left = completed < submitted;
+                }
+                if (!left) break;
+                serial_complete_one();
+            }
         else
             completer.join();
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        batches = nbatch;
+        batches = nbt;
         if (step > 0) {
             total_s += s;
             best = std::max(best, nb * S / s / 1e9);
         }
     }
-    // the mirror received every block of every step once, in order
+    // the mirror received every block of every step once, in the order its receiver took them
     bool mirror_ok = true;
     int64_t mirrored = 0;
+    mirror_done.store(true, std::memory_order_release);
+    for (auto &m : mirrors)
+        if (m.mode == 2) close(m.fd[0]);                       // EOF for the socket consumers
     for (auto &m : mirrors) m.th.join();
     if (!mirrors.empty()) {
         std::vector<uint64_t> want((size_t)nb);
@@ -455,16 +524,18 @@ int main(int argc, char **argv)
             cs.feed((const uint8_t *)host + b * S, (uint64_t)S);
             want[(size_t)b] = cs.finish();
         }
+        int64_t nmir = 0;
         for (int r = 0; r < T; r++) {
-            int64_t k = 0;
-            for (int step = 0; step <= steps; step++)
-                for (int64_t b = r; b < nb; b += T, k++) {
-                    mirror_ok &= msum[(size_t)r][(size_t)k] == want[(size_t)b];
-                    mirrored += S;
-                }
+            mirror_ok &= msum[(size_t)r].size() == mids[(size_t)r].size();
+            for (size_t k = 0; k < msum[(size_t)r].size() && k < mids[(size_t)r].size(); k++) {
+                mirror_ok &= msum[(size_t)r][k] == want[(size_t)mids[(size_t)r][k]];
+                mirrored += S;
+            }
+            nmir += (int64_t)mids[(size_t)r].size();
         }
+        mirror_ok &= nmir == nb * (steps + 1);
         for (auto &m : mirrors)
-            if (m.mode == 2) { close(m.fd[0]); close(m.fd[1]); }
+            if (m.mode == 2) close(m.fd[1]);
     }
     int64_t stored = 0, chunks = 0;
     for (int64_t b = 0; b < nb; b++) { stored += store[(size_t)b]; chunks += n_chunks[(size_t)b]; }
@@ -478,7 +549,8 @@ int main(int argc, char **argv)
                 (long long)(nb * ((S + P - 1) / P)), (long long)stored, (long long)chunks, compressor,
                 mixed ? "mixed" : "config2", mirror_mode == 0 ? "none" : mirror_mode == 1 ? "ring" : "socket",
                 mirror_ok ? "true" : "false", (long long)mirrored,
-                batch ? "hdrf_submit_slots (one batch per receive round)" : "hdrf_submit_slot (one block per batch)",
+                batch ? "hdrf_submit_slots (the blocks received in order since the last submit, <= 16)"
+                      : "hdrf_submit_slot (one block per batch)",
                 (long long)batches, (long long)container, (long long)drained_bytes, (long long)drained_events);
     if (out_dir) {
         const std::string d = out_dir;

@@ -1,7 +1,8 @@
 """The native packet-receive driver (tests/cpp/packet_driver.cpp): receiver threads calling the
 C-ABI the JNI binding calls, one 64 KiB packet at a time (DN/BlockReceiver.java:877-896), each
 packet mirrored downstream first (mirrorPacketTo, :635-641), blocks submitted in arrival order
-(one per batch, or a receive round per batch through hdrf_submit_slots) and the durable containers
+(one per batch, or every block received in order since the last submit as one batch through
+hdrf_submit_slots) and the durable containers
 drained after every completed batch.  On the GPU every block's chunk END offsets, digests, is_new
 and storeSize, and every container file the drains built, equal the sequential oracle's on the same
 corpus; the mirror received every block intact."""
@@ -53,7 +54,8 @@ def test_packet_driver_matches_oracle(tmp_path, compressor, mirror, batch, mixed
     assert r.returncode == 0
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["mirror_ok"] is True and line["mirrored_bytes"] == 2 * nb * (mib << 20)   # warm-up + 1 step
-    assert line["batches_per_step"] == (2 if batch else nb)
+    # batched: the blocks received in order since the last submit go together (timing decides how many)
+    assert (1 <= line["batches_per_step"] <= nb) if batch else line["batches_per_step"] == nb
     got = np.loadtxt(str(tmp_path / "blocks.txt"), dtype=np.int64).reshape(-1, 3)
     roots = corpus_roots(20251015, 500000, nb, mib)
     ora = Oracle(compressor=compressor, max_size=cmax)
