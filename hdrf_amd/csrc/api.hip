@@ -218,6 +218,8 @@ struct hdrf_ctx {
         uint8_t *h = nullptr;                   // pinned staging, 2 x kRingChunk
         hipEvent_t ev[2] = {nullptr, nullptr};  // H2D of each staging chunk
         bool busy[2] = {false, false};
+        hipStream_t st = nullptr;               // HDRF_RX_STREAMS=1: this buffer's own H2D stream
+        hipEvent_t done = nullptr;              //   (its copies then never queue behind other receivers')
         int cur = 0;
         uint64_t fill = 0, dst = 0;             // bytes in the current chunk, their block offset
         uint64_t len = 0, id = 0;
@@ -378,6 +380,8 @@ static void free_all(hdrf_ctx *ctx)
         if (r.h) (void)hipHostFree(r.h);
         for (auto e : r.ev)
             if (e) (void)hipEventDestroy(e);
+        if (r.done) (void)hipEventDestroy(r.done);
+        if (r.st) (void)hipStreamDestroy(r.st);
     }
 }
 
@@ -1064,13 +1068,15 @@ static int wait_one(hdrf_ctx *ctx)
 // only that buffer's state, not the context lock: receivers of different blocks copy in parallel.
 // (touches only the receive buffer and stream C, so it runs without the context lock; the caller
 // records an error under the lock)
+static hipStream_t rx_stream(hdrf_ctx *ctx, const hdrf_ctx::Rx &r) { return r.st ? r.st : ctx->stC; }
+
 static hipError_t rx_flush(hdrf_ctx *ctx, hdrf_ctx::Rx &r)
 {
     if (r.fill == 0) return hipSuccess;
     const int c = r.cur;
     hipError_t e = hipMemcpyAsync(r.d + r.dst, r.h + (uint64_t)c * ctx->kRingChunk, r.fill, hipMemcpyHostToDevice,
-                                  ctx->stC);
-    if (e == hipSuccess) e = hipEventRecord(r.ev[c], ctx->stC);
+                                  rx_stream(ctx, r));
+    if (e == hipSuccess) e = hipEventRecord(r.ev[c], rx_stream(ctx, r));
     if (e != hipSuccess) return e;
     r.busy[c] = true;
     r.cur = c ^ 1;
@@ -1094,6 +1100,11 @@ extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
         if (!r.h) {
             HIPCK(hipHostMalloc((void **)&r.h, 2 * ctx->kRingChunk));
             for (auto &e : r.ev) HIPCK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            static const bool own = [] { const char *e = getenv("HDRF_RX_STREAMS"); return e && atoi(e) != 0; }();
+            if (own) {
+                HIPCK(hipStreamCreateWithFlags(&r.st, hipStreamNonBlocking));
+                HIPCK(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+            }
         }
         r.len = 0;
         r.fill = 0;
@@ -1180,7 +1191,11 @@ extern "C" int hdrf_submit_slots(hdrf_ctx *ctx, int32_t n, const int32_t *rxs)
     for (int i = 0; i < n; i++) {
         hdrf_ctx::Rx &r = ctx->rx[rxs[i]];
         HIPCK(rx_flush(ctx, r));
-        HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, ctx->stC));
+        HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, rx_stream(ctx, r)));
+        if (r.st) {                                    // the batch's copies complete on stream C's clock
+            HIPCK(hipEventRecord(r.done, r.st));
+            HIPCK(hipStreamWaitEvent(ctx->stC, r.done, 0));
+        }
         p[i] = r.d;
         len[i] = r.len;
         readable[i] = (uint64_t)ctx->cfg.max_block_bytes + kSlack + 256;
