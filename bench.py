@@ -146,10 +146,9 @@ def packet_driver_line(a):
     cmd = [exe, str(nb), str(a.block_mib), str(pk), str(a.packet_threads), str(a.steps), "--compressor",
            str(compressor), "--mirror", a.mirror, "--arena-slots", str(a.arena_slots or 512)]
     cmd += ["--batch"] * a.packet_batch + ["--mixed"] * a.mixed
-    # the library's streams (chunking, SHA, index, store, copies, drains, LZ4) need their own hardware
-    # queues, as in the in-process lines (main() sets the same before HIP initialises)
+    # (the child keeps HIP's default hardware queues: GPU_MAX_HW_QUEUES 4 / 8 / 6, with and without
+    # per-receive-buffer H2D streams, all within the run-to-run spread, profiles/r04_c5_f_queues_ab.txt)
     env = dict(os.environ)
-    env.setdefault("GPU_MAX_HW_QUEUES", "8")
     t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=1500, env=env)
     wall = time.perf_counter() - t0
