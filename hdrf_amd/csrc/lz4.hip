@@ -113,9 +113,17 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         if (cur != want) atomicXor(&tabx[h >> 3], (cur ^ want) << sh);
         return cur;
     };
-    auto tput = [&](uint32_t h, int p, uint32_t tg) {
-        tab16[h] = (unsigned short)p;
-        xupd(h, p, tg);
+    auto tput = [&](uint32_t h, int p, uint32_t tg) {   // no read of the entry: two non-returning
+        tab16[h] = (unsigned short)p;                    // LDS atomics clear and set its field (lanes
+        if (u16) {                                       // of one wave touch disjoint fields)
+            const uint32_t sh = 2 * (h & 15);
+            atomicAnd(&tabx[h >> 4], ~(3u << sh));
+            atomicOr(&tabx[h >> 4], tg << sh);
+        } else {
+            const uint32_t sh = 4 * (h & 7);
+            atomicAnd(&tabx[h >> 3], ~(15u << sh));
+            atomicOr(&tabx[h >> 3], ((((uint32_t)p >> 16) & 3u) | (tg << 2)) << sh);
+        }
     };
     auto tswap = [&](uint32_t h, int p, uint32_t tg, uint32_t &otg) -> int {   // old entry, then (p, tg)
         const int lo = (int)tab16[h];
