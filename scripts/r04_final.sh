@@ -25,3 +25,7 @@ timeout -k 10 400 python -u bench.py --workload config5 --steps 3 --packet-drive
 tail -1 gpurun_out/r04_c5_pk64_c1_ring_$V.json.log | cut -c1-200
 timeout -k 10 400 python -u bench.py --workload config5 --steps 3 --packet-driver cpp --packet-kib 64 --mirror ring --compressor 2 > gpurun_out/r04_c5_pk64_c2_ring_$V.json.log 2>&1 || { tail -20 gpurun_out/r04_c5_pk64_c2_ring_$V.json.log; exit 1; }
 tail -1 gpurun_out/r04_c5_pk64_c2_ring_$V.json.log | cut -c1-200
+# the multi-rank path: two ranks on this one GPU over gloo (a rehearsal of bench.py --gpus N, not a
+# measurement: both ranks share the device)
+HDRF_BENCH_SAME_DEVICE=1 timeout -k 10 400 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29655 bench.py --gpus 2 --steps 2 --warmup 1 --blocks 64 --no-cpu > gpurun_out/r04_g2_$V.log 2>&1 || { tail -30 gpurun_out/r04_g2_$V.log; exit 1; }
+tail -1 gpurun_out/r04_g2_$V.log | cut -c1-300
