@@ -219,22 +219,6 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 if (below) { ref = pipl; cv = pv; known = true; }
             }
             const bool in = valid && ref + kMaxDist >= ipl;
-            // the first attempt that can still match (a tag hit, or an earlier attempt's equal bytes)
-            // is the match unless its 4 bytes differ: its window pair for the catch-up goes out with
-            // the candidate loads, so a match found here costs one round trip instead of two
-            int spec = -1;
-            {
-                const unsigned long long potm = ballot64(in && (known ? cv == v : otg == vt));
-                if (potm) {
-                    const int q = __builtin_ctzll(potm);
-                    const int qip = (int)rdlane((uint32_t)ipl, q), qref = (int)rdlane((uint32_t)ref, q);
-                    if (qip - anchor <= 64 && qip >= 64 && qref >= 64) {
-                        Fw = wload(qip - 64);
-                        Rw = wload(qref - 64);
-                        spec = q;
-                    }
-                }
-            }
             if (in && !known && otg == vt) cv = rd32u(src + ref);   // ref is a position < n
             const bool ok = in && cv == v;
             const unsigned long long okm = ballot64(ok);
@@ -258,12 +242,9 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 bool fast = ip - anchor <= 64 && ip >= 64 && mref >= 64;
                 if (fast) {
                     // one window pair at ip - 64: catch-up, literals and the first extension step
-                    // (already loaded when the match is the batch's first possible one)
                     const int wb0 = ip - 64, d0 = mref - ip;
-                    if (istar != spec) {
-                        Fw = wload(wb0);
-                        Rw = wload(wb0 + d0);
-                    }
+                    Fw = wload(wb0);
+                    Rw = wload(wb0 + d0);
                     const uint32_t x = Fw ^ Rw;
                     int hstop = -1;                        // highest stop byte in [wb0, ip)
 #pragma unroll
