@@ -35,16 +35,18 @@ class Exchange:
         # the phase that reads a receive buffer is ordered after the exchange on the device, with no
         # host synchronisation in between
         self.stream = stream if self.nccl else None
+        # host-known metadata (X1 send counts, known once the front half was waited; flush-function
+        # descriptors; allocator images) goes rank to rank over a gloo group on the CPU, so no
+        # exchange makes the host wait on a device stream (an RCCL exchange of host values would
+        # copy them to the GPU and back).  Collective: every rank builds its Exchange in order.
+        self.meta = dist.new_group(backend="gloo") if self.nccl else None
 
     def counts(self, send_counts):
-        """Every rank's send counts -> this rank's receive counts (int64[G])."""
-        if self.nccl:
-            s = torch.as_tensor(np.asarray(send_counts, np.int64), device=self.device)
-        else:
-            s = torch.as_tensor(np.asarray(send_counts, np.int64))
+        """Every rank's send counts -> this rank's receive counts (int64[G]); host to host."""
+        s = torch.as_tensor(np.asarray(send_counts, np.int64))
         r = torch.empty_like(s)
-        dist.all_to_all_single(r, s)
-        return r.cpu().numpy()
+        dist.all_to_all_single(r, s, group=self.meta)
+        return r.numpy()
 
     def records(self, send, recv, send_counts, recv_counts, cap, words):
         G = self.G
@@ -77,38 +79,33 @@ class Exchange:
             torch.cuda.current_stream(recv.device).synchronize()
 
     def all_gather_i64(self, arr):
-        """Every rank's int64 array (lengths may differ) -> list in rank order."""
-        dev = self.device if self.nccl else None
-        n = torch.tensor([len(arr)], dtype=torch.int64, device=dev)
+        """Every rank's int64 array (lengths may differ) -> list in rank order; host to host."""
+        n = torch.tensor([len(arr)], dtype=torch.int64)
         ns = [torch.empty_like(n) for _ in range(self.G)]
-        dist.all_gather(ns, n)
-        ns = [int(x.item()) for x in ns]
-        m = max(ns)
-        t = torch.zeros(m, dtype=torch.int64, device=dev)
-        t[:len(arr)] = torch.as_tensor(np.asarray(arr, np.int64), device=dev)
+        dist.all_gather(ns, n, group=self.meta)
+        ns = [int(x[0]) for x in ns]
+        t = torch.zeros(max(ns), dtype=torch.int64)
+        t[:len(arr)] = torch.as_tensor(np.asarray(arr, np.int64))
         out = [torch.empty_like(t) for _ in range(self.G)]
-        dist.all_gather(out, t)
-        return [o[:k].cpu().numpy() for o, k in zip(out, ns)]
+        dist.all_gather(out, t, group=self.meta)
+        return [o[:k].numpy() for o, k in zip(out, ns)]
 
     def chain_alloc(self, alloc_prev_batch, flush):
         """Rank r flushes after rank r-1 (rank 0 starts from the node's state); returns the node's
-        allocator state after the last rank, known to every rank."""
+        allocator state after the last rank, known to every rank (host images, over the meta group)."""
         G, r = self.G, self.rank
-        dev = self.device if self.nccl else None
         if r == 0:
             a_in = alloc_prev_batch
         else:
-            t = torch.empty(ALLOC_STATE_BYTES, dtype=torch.uint8, device=dev)
-            dist.recv(t, src=r - 1)
-            a_in = t.cpu().numpy()
+            t = torch.empty(ALLOC_STATE_BYTES, dtype=torch.uint8)
+            dist.recv(t, src=r - 1, group=self.meta)
+            a_in = t.numpy()
         a_out = flush(a_in)
         if r + 1 < G:
-            t = torch.as_tensor(a_out, device=dev)
-            dist.send(t, dst=r + 1)
-        fin = torch.as_tensor(a_out, device=dev) if r == G - 1 else torch.empty(ALLOC_STATE_BYTES, dtype=torch.uint8,
-                                                                                 device=dev)
-        dist.broadcast(fin, src=G - 1)
-        return fin.cpu().numpy()
+            dist.send(torch.as_tensor(a_out), dst=r + 1, group=self.meta)
+        fin = torch.as_tensor(a_out).clone() if r == G - 1 else torch.empty(ALLOC_STATE_BYTES, dtype=torch.uint8)
+        dist.broadcast(fin, src=G - 1, group=self.meta)
+        return fin.numpy()
 
 
 def alloc_fields(a):
