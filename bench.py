@@ -485,9 +485,9 @@ def main():
                "algorithmic_bytes_per_launch": int(lz_bytes),
                "traffic": pmc.get("lz4_seg_kernel<false>", {}).get("hbm_bytes_per_launch"),
                "limiter": "latency of the greedy parse's per-sequence chain (one wave per 261,100-B segment; "
-                          "101 VGPRs allow 4 waves/SIMD, the 9 KiB LDS table 17/CU; half of wave time at s_waitcnt "
-                          "on the candidate load and table round trips); profiles/r02_lz4_phases.txt, "
-                          "profiles/r03_c4_v1_pmc.txt"}
+                          "104 VGPRs allow 4 waves/SIMD, the 10 KiB tagged LDS table 16/CU; VALU issue ~0.08 per "
+                          "cycle per SIMD, ~half of wave time at s_waitcnt on table round trips and candidate "
+                          "loads); profiles/r02_lz4_phases.txt, profiles/r04_lz4_pmc_ab.txt"}
     # the line's roofline: the dominant kernel of the critical chain
     top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place, "B2: store": place,
            "B: index": place, "L: LZ4": lz4}[crit]

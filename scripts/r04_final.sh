@@ -15,6 +15,8 @@ TAG=r04_$V EXTRA_GROUPS="SQ_INSTS_VALU" bash scripts/r02_traffic.sh > gpurun_out
 mkdir -p profiles && cp gpurun_out/r04_${V}_traffic.json profiles/r04_${V}_traffic.json
 timeout -k 10 600 python -u bench.py > gpurun_out/r04_bench_$V.json.log 2>&1 || { tail -20 gpurun_out/r04_bench_$V.json.log; exit 1; }
 tail -1 gpurun_out/r04_bench_$V.json.log | cut -c1-300
+TAG=r04_c4$V WORKLOAD=config4 ARGS="--workload config4 --steps 1 --warmup 0 --no-cpu --no-alone" bash scripts/r02_traffic.sh > gpurun_out/r04_c4traffic_$V.txt 2>&1 || { tail -20 gpurun_out/r04_c4traffic_$V.txt; exit 1; }
+cp gpurun_out/r04_c4${V}_traffic.json profiles/r04_c4${V}_traffic.json
 timeout -k 10 600 python -u bench.py --workload config4 > gpurun_out/r04_c4_$V.json.log 2>&1 || { tail -20 gpurun_out/r04_c4_$V.json.log; exit 1; }
 tail -1 gpurun_out/r04_c4_$V.json.log | cut -c1-200
 timeout -k 10 400 python -u bench.py --workload config5 --steps 3 > gpurun_out/r04_c5_whole_c1_$V.json.log 2>&1 || { tail -20 gpurun_out/r04_c5_whole_c1_$V.json.log; exit 1; }
