@@ -122,6 +122,8 @@ struct hdrf_ctx {
     hipStream_t stG = nullptr;   // stream G: the granule-max pass (HDRF_GMAX_STREAM), ahead of W
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
     hipStream_t stD = nullptr;   // stream D: container drain D2H (beside the H2D copies on C)
+    hipStream_t stR = nullptr;   // stream R: recipe copies of completed batches (off C: a kernel
+                                 // there waited for CU slots and stalled the next batch's H2D copies)
     XferJob *h_xfer = nullptr;   // drain copy jobs (pinned, read by xfer_kernel)
     int xfer_cap = 0;
     hipStream_t stL[2] = {};     // compressor 2: LZ4 streams, alternating by batch (off stream B)
@@ -371,6 +373,7 @@ static void free_all(hdrf_ctx *ctx)
     if (ctx->stG) (void)hipStreamDestroy(ctx->stG);
     if (ctx->stC) (void)hipStreamDestroy(ctx->stC);
     if (ctx->stD) (void)hipStreamDestroy(ctx->stD);
+    if (ctx->stR) (void)hipStreamDestroy(ctx->stR);
     if (ctx->h_xfer) (void)hipHostFree(ctx->h_xfer);
     for (auto L : ctx->stL)
         if (L) (void)hipStreamDestroy(L);
@@ -456,6 +459,7 @@ static int drain(hdrf_ctx *ctx)
     while (ctx->nwait < ctx->nsub)
         if (int r = wait_one(ctx)) rc = rc ? rc : r;
     HIPCK(hipStreamSynchronize(ctx->stC));
+    HIPCK(hipStreamSynchronize(ctx->stR));
     for (auto L : ctx->stL) HIPCK(hipStreamSynchronize(L));
     HIPCK(hipStreamSynchronize(ctx->stG));
     HIPCK(hipStreamSynchronize(ctx->stW));
@@ -557,6 +561,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         hipStreamCreateWithPriority(&ctx->stG, hipStreamNonBlocking, pw) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stD, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stR, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[0], hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[1], hipStreamNonBlocking) != hipSuccess) {
         free_all(ctx);
@@ -1015,8 +1020,8 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) ctx->stats.open_bytes += ctx->h_alloc.cur[t];
     // recipes (SET longToBytes(id,4) -> BE32 size | digests): the block's digests are copied on
-    // the device into the recipe store on the copy stream (off stream B, the critical chain);
-    // the slot's next SHA waits for the copies
+    // the device into the recipe store on stream R (off stream B, the critical chain, and off the
+    // H2D copy stream C); the slot's next SHA waits for the copies
     int nj = 0;
     for (int b = 0; b < nblocks; b++) {
         const uint32_t key = (uint32_t)S.ids[b];
@@ -1030,9 +1035,9 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
         }
     }
     if (nj) {
-        HIPCK(hipMemcpyAsync(S.d_rjobs, S.h_rjobs, sizeof(RecipeCopy) * nj, hipMemcpyHostToDevice, ctx->stC));
-        HIPCK(launch_recipe_copy(S.d_rjobs, nj, ctx->stC));
-        HIPCK(hipEventRecord(S.recipe_done, ctx->stC));
+        HIPCK(hipMemcpyAsync(S.d_rjobs, S.h_rjobs, sizeof(RecipeCopy) * nj, hipMemcpyHostToDevice, ctx->stR));
+        HIPCK(launch_recipe_copy(S.d_rjobs, nj, ctx->stR));
+        HIPCK(hipEventRecord(S.recipe_done, ctx->stR));
         S.recipe_pending = true;
     }
     return 0;
@@ -1191,7 +1196,8 @@ extern "C" int hdrf_submit_slots(hdrf_ctx *ctx, int32_t n, const int32_t *rxs)
     for (int i = 0; i < n; i++) {
         hdrf_ctx::Rx &r = ctx->rx[rxs[i]];
         HIPCK(rx_flush(ctx, r));
-        HIPCK(hipMemsetAsync(r.d + r.len, 0, kSlack, rx_stream(ctx, r)));
+        // (no slack fill: the kernels never depend on the bytes past a block's end, as for caller
+        // buffers, and a fill kernel on the copy stream waited for CU slots and stalled the copies)
         if (r.st) {                                    // the batch's copies complete on stream C's clock
             HIPCK(hipEventRecord(r.done, r.st));
             HIPCK(hipStreamWaitEvent(ctx->stC, r.done, 0));
@@ -1251,8 +1257,11 @@ extern "C" int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *c
     std::vector<uint64_t> rd(nblocks);
     for (int b = 0; b < nblocks; b++) {
         uint8_t *d = S.d_hstage + (uint64_t)b * stride;
+        // Only the copies go on stream C.  The 64 readable bytes past the block end are not filled:
+        // the kernels never depend on them (device batches hand over arbitrary bytes there, e.g. the
+        // next block), and a fill kernel between the copies waited for CU slots behind the drain and
+        // the reduction, stalling the copy engine 8-10 ms per 16-block batch (config 5 trace, r04).
         if (len[b]) HIPCK(hipMemcpyAsync(d, host_data[b], len[b], hipMemcpyHostToDevice, ctx->stC));
-        HIPCK(hipMemsetAsync(d + len[b], 0, kSlack, ctx->stC));
         ptrs[b] = d;
         rd[b] = stride * (uint64_t)(ctx->max_batch - b);
     }

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 4: config-5 whole-block timeline (kernel + memory-copy trace, no counters): where the step
+# spends the ~130 ms beyond the H2D bytes' time.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
+export TMPDIR=/tmp
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $R/gpurun_out/c5trace -o run -- python3 $R/bench.py --workload config5 --steps 2 --warmup 1 --no-cpu > $R/gpurun_out/c5trace.log 2>&1) || { tail -20 gpurun_out/c5trace.log; exit 1; }
+tail -1 gpurun_out/c5trace.log | cut -c1-200
+ls gpurun_out/c5trace/*/ 2>/dev/null | head; ls gpurun_out/c5trace | head
