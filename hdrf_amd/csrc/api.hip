@@ -1075,10 +1075,45 @@ static int wait_one(hdrf_ctx *ctx)
 // records an error under the lock)
 static hipStream_t rx_stream(hdrf_ctx *ctx, const hdrf_ctx::Rx &r) { return r.st ? r.st : ctx->stC; }
 
+// Packet bytes into the pinned staging chunk with non-temporal 16-B stores: the receiver thread does
+// not read the destination lines first (a plain copy of a 64 KiB packet fetches them for ownership)
+// and leaves nothing dirty in its caches for the copy engine's reads.  HDRF_RX_NT=0: std::memcpy.
+static void copy_nt(uint8_t *dst, const uint8_t *src, uint64_t n)
+{
+    typedef long long v2 __attribute__((vector_size(16)));
+    uint64_t head = (16 - ((uintptr_t)dst & 15)) & 15;
+    if (head > n) head = n;
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    const uint64_t n64 = n >> 6;
+    for (uint64_t i = 0; i < n64; i++) {
+        v2 a, b, c, d;
+        std::memcpy(&a, src + 64 * i, 16);
+        std::memcpy(&b, src + 64 * i + 16, 16);
+        std::memcpy(&c, src + 64 * i + 32, 16);
+        std::memcpy(&d, src + 64 * i + 48, 16);
+        __builtin_nontemporal_store(a, (v2 *)(dst + 64 * i));
+        __builtin_nontemporal_store(b, (v2 *)(dst + 64 * i + 16));
+        __builtin_nontemporal_store(c, (v2 *)(dst + 64 * i + 32));
+        __builtin_nontemporal_store(d, (v2 *)(dst + 64 * i + 48));
+    }
+    std::memcpy(dst + 64 * n64, src + 64 * n64, n & 63);
+}
+
+static bool rx_nt()
+{
+    static const bool on = [] { const char *e = getenv("HDRF_RX_NT"); return !e || atoi(e) != 0; }();
+    return on;
+}
+
 static hipError_t rx_flush(hdrf_ctx *ctx, hdrf_ctx::Rx &r)
 {
     if (r.fill == 0) return hipSuccess;
     const int c = r.cur;
+    // the chunk's non-temporal stores are globally visible before the copy engine is told to read it
+    std::atomic_thread_fence(std::memory_order_seq_cst);
     hipError_t e = hipMemcpyAsync(r.d + r.dst, r.h + (uint64_t)c * ctx->kRingChunk, r.fill, hipMemcpyHostToDevice,
                                   rx_stream(ctx, r));
     if (e == hipSuccess) e = hipEventRecord(r.ev[c], rx_stream(ctx, r));
@@ -1138,7 +1173,8 @@ extern "C" int hdrf_append_packet(hdrf_ctx *ctx, int32_t rx, const uint8_t *data
     while (len) {
         if (r.fill == 0) r.dst = r.len;
         const uint64_t n = std::min(len, ctx->kRingChunk - r.fill);
-        std::memcpy(r.h + (uint64_t)r.cur * ctx->kRingChunk + r.fill, data, n);
+        if (rx_nt()) copy_nt(r.h + (uint64_t)r.cur * ctx->kRingChunk + r.fill, data, n);
+        else std::memcpy(r.h + (uint64_t)r.cur * ctx->kRingChunk + r.fill, data, n);
         r.fill += n;
         r.len += n;
         data += n;

@@ -540,21 +540,31 @@ __global__ void __launch_bounds__(256) recipe_copy_kernel(const RecipeCopy *__re
 // Container drain (api.hip hdrf_drain_containers) into pinned host memory: the CUs write the bytes
 // straight across PCIe (the host buffer is device-mapped), so the D2H of a DataNode's container files
 // runs beside the SDMA engine's H2D copies of the next blocks instead of queueing behind them.
-// grid (jobs, pieces): workgroup (j, y) copies piece y (kXferPiece bytes) of job j.
+// Items (job j, piece y of kXferPiece bytes), numbered y * jobs + j.  Default grid: one workgroup
+// per item, every CU writing across PCIe at once.  HDRF_XFER_WGS = W > 0: W workgroups loop over the
+// items, which caps the drain's write rate (the link is shared with the next blocks' H2D copies).
 constexpr uint64_t kXferPiece = 256 << 10;
-__global__ void __launch_bounds__(256) xfer_kernel(const XferJob *__restrict__ jobs)
+__global__ void __launch_bounds__(256) xfer_kernel(const XferJob *__restrict__ jobs, int njobs, uint32_t pieces)
 {
-    const XferJob J = jobs[blockIdx.x];
-    const uint64_t o = (uint64_t)blockIdx.y * kXferPiece;
-    if (o >= J.n) return;
-    const uint64_t n = J.n - o < kXferPiece ? J.n - o : kXferPiece;
-    wg_copy<false>((uint8_t *)(uintptr_t)(J.dst + o), (const uint8_t *)(uintptr_t)(J.src + o), (uint32_t)n);
+    const uint64_t total = (uint64_t)njobs * pieces, step = (uint64_t)gridDim.x * gridDim.y;
+    for (uint64_t it = blockIdx.x + (uint64_t)blockIdx.y * gridDim.x; it < total; it += step) {
+        const XferJob J = jobs[it % (uint64_t)njobs];
+        const uint64_t o = (it / (uint64_t)njobs) * kXferPiece;
+        if (o >= J.n) continue;
+        const uint64_t n = J.n - o < kXferPiece ? J.n - o : kXferPiece;
+        wg_copy<false>((uint8_t *)(uintptr_t)(J.dst + o), (const uint8_t *)(uintptr_t)(J.src + o), (uint32_t)n);
+    }
 }
 
 hipError_t launch_xfer(const XferJob *jobs, int n, uint64_t max_bytes, hipStream_t st)
 {
+    static const int wgs = [] { const char *e = getenv("HDRF_XFER_WGS"); return e ? atoi(e) : 0; }();
     const uint64_t pieces = (max_bytes + kXferPiece - 1) / kXferPiece;
-    if (n > 0 && pieces > 0) hipLaunchKernelGGL(xfer_kernel, dim3(n, (unsigned)pieces), dim3(256), 0, st, jobs);
+    if (n <= 0 || pieces == 0) return hipGetLastError();
+    if (wgs > 0)
+        hipLaunchKernelGGL(xfer_kernel, dim3((unsigned)wgs), dim3(256), 0, st, jobs, n, (uint32_t)pieces);
+    else
+        hipLaunchKernelGGL(xfer_kernel, dim3(n, (unsigned)pieces), dim3(256), 0, st, jobs, n, (uint32_t)pieces);
     return hipGetLastError();
 }
 
