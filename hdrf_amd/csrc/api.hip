@@ -2839,6 +2839,15 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
     int64_t k = 0, used = 0;
     int nj = 0;
     uint64_t maxj = 0;
+    // CU drain grid: one workgroup per ~256 MiB of this drain, at least 5 (each writes ~7.5 GB/s), so
+    // a batch's container files cross the link in about the time of the next batch's block copies
+    // instead of as fast as possible beside them (config 5 whole blocks: 50.0 / 50.1 GB/s with 5
+    // workgroups, 49.8 / 48.5 with 4, 41.5 with 3, 47.3 / 47.4 with one per item;
+    // profiles/r04_drain_wgs_ab.txt).  HDRF_XFER_WGS = W overrides (0: one workgroup per item).
+    static const int wgs_env = [] { const char *e = getenv("HDRF_XFER_WGS"); return e ? atoi(e) : -1; }();
+    int64_t drain_bytes = 0;
+    for (const Pend &e : todo) drain_bytes += e.n;
+    const int wgs = wgs_env >= 0 ? wgs_env : (int)std::max<int64_t>(5, (drain_bytes + (256ll << 20) - 1) / (256ll << 20));
     for (const Pend &e : todo) {
         if (k >= ev_cap || used + e.n > out_cap) {
             if (need) *need = e.n;
@@ -2848,7 +2857,7 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
                                                              : ctx->d_arena + (size_t)e.ci.slot * c.container_max;
         if (e.n && mapped) {
             if (nj == ctx->xfer_cap) {                    // job list full: flush it
-                HIPCK(launch_xfer(ctx->h_xfer, nj, maxj, ctx->stD));
+                HIPCK(launch_xfer(ctx->h_xfer, nj, maxj, wgs, ctx->stD));
                 HIPCK(hipStreamSynchronize(ctx->stD));
                 nj = 0;
                 maxj = 0;
@@ -2863,7 +2872,7 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
         used += e.n;
         k++;
     }
-    if (nj) HIPCK(launch_xfer(ctx->h_xfer, nj, maxj, ctx->stD));
+    if (nj) HIPCK(launch_xfer(ctx->h_xfer, nj, maxj, wgs, ctx->stD));
     HIPCK(hipStreamSynchronize(ctx->stD));
     // the emitted ones are handed over
     const size_t kc = std::min<size_t>((size_t)k, nclosed);

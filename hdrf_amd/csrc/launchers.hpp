@@ -134,7 +134,7 @@ hipError_t launch_recipe_copy(const RecipeCopy *jobs, int n, hipStream_t st);
 struct XferJob {
     uint64_t src, dst, n;
 };
-hipError_t launch_xfer(const XferJob *jobs, int n, uint64_t max_bytes, hipStream_t st);
+hipError_t launch_xfer(const XferJob *jobs, int n, uint64_t max_bytes, int wgs, hipStream_t st);
 // stream mode (compressor 4): pieces of one block -> LZ4 blocks (stage) -> framed file
 struct LzPiece {
     uint64_t src;            // offset in the block

@@ -540,9 +540,10 @@ __global__ void __launch_bounds__(256) recipe_copy_kernel(const RecipeCopy *__re
 // Container drain (api.hip hdrf_drain_containers) into pinned host memory: the CUs write the bytes
 // straight across PCIe (the host buffer is device-mapped), so the D2H of a DataNode's container files
 // runs beside the SDMA engine's H2D copies of the next blocks instead of queueing behind them.
-// Items (job j, piece y of kXferPiece bytes), numbered y * jobs + j.  Default grid: one workgroup
-// per item, every CU writing across PCIe at once.  HDRF_XFER_WGS = W > 0: W workgroups loop over the
-// items, which caps the drain's write rate (the link is shared with the next blocks' H2D copies).
+// Items (job j, piece y of kXferPiece bytes), numbered y * jobs + j; `wgs` workgroups loop over them
+// (0: one workgroup per item).  The drain shares the link with the next blocks' H2D copies: at full
+// grid it writes ~50 GB/s and the copies under it drop from 55.7 to 44.6 GB/s (config 5 trace, r04);
+// a few workgroups (~7.5 GB/s each) spread the same bytes over the next batch's copy time instead.
 constexpr uint64_t kXferPiece = 256 << 10;
 __global__ void __launch_bounds__(256) xfer_kernel(const XferJob *__restrict__ jobs, int njobs, uint32_t pieces)
 {
@@ -556,9 +557,8 @@ __global__ void __launch_bounds__(256) xfer_kernel(const XferJob *__restrict__ j
     }
 }
 
-hipError_t launch_xfer(const XferJob *jobs, int n, uint64_t max_bytes, hipStream_t st)
+hipError_t launch_xfer(const XferJob *jobs, int n, uint64_t max_bytes, int wgs, hipStream_t st)
 {
-    static const int wgs = [] { const char *e = getenv("HDRF_XFER_WGS"); return e ? atoi(e) : 0; }();
     const uint64_t pieces = (max_bytes + kXferPiece - 1) / kXferPiece;
     if (n <= 0 || pieces == 0) return hipGetLastError();
     if (wgs > 0)
