@@ -122,8 +122,9 @@ struct hdrf_ctx {
     hipStream_t stG = nullptr;   // stream G: the granule-max pass (HDRF_GMAX_STREAM), ahead of W
     hipStream_t stC = nullptr;   // stream C: H2D copies of host-submitted batches
     hipStream_t stD = nullptr;   // stream D: container drain D2H (beside the H2D copies on C)
-    hipStream_t stR = nullptr;   // stream R: recipe copies of completed batches (off C: a kernel
-                                 // there waited for CU slots and stalled the next batch's H2D copies)
+    hipStream_t stR = nullptr;   // stream R: recipe copies once host batches use stream C (there a
+                                 // kernel waited for CU slots and stalled the next batch's H2D copies)
+    bool host_copies = false;    // hdrf_submit_host / hdrf_rx_begin ran: stream C carries H2D copies
     XferJob *h_xfer = nullptr;   // drain copy jobs (pinned, read by xfer_kernel)
     int xfer_cap = 0;
     hipStream_t stL[2] = {};     // compressor 2: LZ4 streams, alternating by batch (off stream B)
@@ -459,7 +460,7 @@ static int drain(hdrf_ctx *ctx)
     while (ctx->nwait < ctx->nsub)
         if (int r = wait_one(ctx)) rc = rc ? rc : r;
     HIPCK(hipStreamSynchronize(ctx->stC));
-    HIPCK(hipStreamSynchronize(ctx->stR));
+    if (ctx->stR) HIPCK(hipStreamSynchronize(ctx->stR));
     for (auto L : ctx->stL) HIPCK(hipStreamSynchronize(L));
     HIPCK(hipStreamSynchronize(ctx->stG));
     HIPCK(hipStreamSynchronize(ctx->stW));
@@ -562,10 +563,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         hipStreamCreateWithFlags(&ctx->stC, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stD, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&ctx->stL[0], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&ctx->stL[1], hipStreamNonBlocking) != hipSuccess ||
-        // created last: streams take hardware queues in creation order, and a stream created before
-        // the LZ4 streams moved them onto the queues of streams A and B (config 4 40.4 -> 32.9 GB/s)
-        hipStreamCreateWithFlags(&ctx->stR, hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&ctx->stL[1], hipStreamNonBlocking) != hipSuccess) {
         free_all(ctx);
         delete ctx;
         return HDRF_E_HIP;
@@ -1022,8 +1020,11 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
     for (int t = 0; t < c.n_thread; t++)
         if (ctx->h_alloc.exists[t]) ctx->stats.open_bytes += ctx->h_alloc.cur[t];
     // recipes (SET longToBytes(id,4) -> BE32 size | digests): the block's digests are copied on
-    // the device into the recipe store on stream R (off stream B, the critical chain, and off the
-    // H2D copy stream C); the slot's next SHA waits for the copies
+    // the device into the recipe store off stream B (the critical chain): on stream C, or on stream R
+    // once host batches put H2D copies on C (a recipe kernel there held back the copies queued behind
+    // it).  R exists only then: one more stream from the open on changed how the hardware queues are
+    // shared and config 4's two LZ4 passes stopped overlapping (40.5 -> 34.2 GB/s,
+    // profiles/r04_c4_stream_ab.txt).  The slot's next SHA waits for the copies.
     int nj = 0;
     for (int b = 0; b < nblocks; b++) {
         const uint32_t key = (uint32_t)S.ids[b];
@@ -1037,9 +1038,11 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
         }
     }
     if (nj) {
-        HIPCK(hipMemcpyAsync(S.d_rjobs, S.h_rjobs, sizeof(RecipeCopy) * nj, hipMemcpyHostToDevice, ctx->stR));
-        HIPCK(launch_recipe_copy(S.d_rjobs, nj, ctx->stR));
-        HIPCK(hipEventRecord(S.recipe_done, ctx->stR));
+        if (ctx->host_copies && !ctx->stR) HIPCK(hipStreamCreateWithFlags(&ctx->stR, hipStreamNonBlocking));
+        hipStream_t rs = ctx->host_copies ? ctx->stR : ctx->stC;
+        HIPCK(hipMemcpyAsync(S.d_rjobs, S.h_rjobs, sizeof(RecipeCopy) * nj, hipMemcpyHostToDevice, rs));
+        HIPCK(launch_recipe_copy(S.d_rjobs, nj, rs));
+        HIPCK(hipEventRecord(S.recipe_done, rs));
         S.recipe_pending = true;
     }
     return 0;
@@ -1154,6 +1157,7 @@ extern "C" int hdrf_rx_begin(hdrf_ctx *ctx, uint64_t block_id, int32_t *rx)
         r.id = block_id;
         r.state.store(1);
         ctx->rx_used = true;                       // packet mode: drains on the copy engine
+        ctx->host_copies = true;
         *rx = i;
         return 0;
     }
@@ -1286,6 +1290,7 @@ extern "C" int hdrf_submit_host(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *c
     if (ctx->nsub - ctx->nwait >= (uint64_t)kSlots)     // every submit pairs with one hdrf_wait_batch
         return set_err(ctx, HDRF_E_CAPACITY, "pipeline full: hdrf_wait_batch first");
     Slot &S = ctx->sl[ctx->nsub % kSlots];
+    ctx->host_copies = true;
     const uint64_t stride = ((uint64_t)ctx->cfg.max_block_bytes + kSlack + 255) & ~(uint64_t)255;
     if (!S.d_hstage) {                                 // first host batch of this slot
         HIPCK(hipMalloc((void **)&S.d_hstage, stride * ctx->max_batch));
