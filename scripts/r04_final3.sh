@@ -5,7 +5,7 @@
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p gpurun_out
-V=${V:-h}
+V=${V:-i}
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > gpurun_out/r04_tests_$V.log 2>&1 || { tail -40 gpurun_out/r04_tests_$V.log; exit 1; }
 tail -1 gpurun_out/r04_tests_$V.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r04_smoke_$V.log 2>&1 || { tail -20 gpurun_out/r04_smoke_$V.log; exit 1; }
