@@ -2846,11 +2846,11 @@ extern "C" int64_t hdrf_drain_containers(hdrf_ctx *ctx, hdrf_container_event *ev
     int64_t k = 0, used = 0;
     int nj = 0;
     uint64_t maxj = 0;
-    // CU drain grid: one workgroup per ~256 MiB of this drain, at least 5 (each writes ~7.5 GB/s), so
-    // a batch's container files cross the link in about the time of the next batch's block copies
-    // instead of as fast as possible beside them (config 5 whole blocks: 50.0 / 50.1 GB/s with 5
-    // workgroups, 49.8 / 48.5 with 4, 41.5 with 3, 47.3 / 47.4 with one per item;
-    // profiles/r04_drain_wgs_ab.txt).  HDRF_XFER_WGS = W overrides (0: one workgroup per item).
+    // CU drain grid: one workgroup per ~256 MiB of this drain, at least 5.  Five workgroups still drain
+    // a config-5 batch in ~19.5 ms, but the next blocks' H2D copies beside them keep 54.9 GB/s, where
+    // a full grid's flood of PCIe writes cut them to 44.6 (config 5 whole blocks: 50.0 / 50.1 GB/s
+    // with 5 workgroups, 49.8 / 48.5 with 4, 41.5 with 3, 47.3 / 47.4 with one per item;
+    // profiles/r04_drain_wgs_ab.txt, r04_c5_trace3.txt).  HDRF_XFER_WGS = W overrides (0: one per item).
     static const int wgs_env = [] { const char *e = getenv("HDRF_XFER_WGS"); return e ? atoi(e) : -1; }();
     int64_t drain_bytes = 0;
     for (const Pend &e : todo) drain_bytes += e.n;

@@ -541,9 +541,9 @@ __global__ void __launch_bounds__(256) recipe_copy_kernel(const RecipeCopy *__re
 // straight across PCIe (the host buffer is device-mapped), so the D2H of a DataNode's container files
 // runs beside the SDMA engine's H2D copies of the next blocks instead of queueing behind them.
 // Items (job j, piece y of kXferPiece bytes), numbered y * jobs + j; `wgs` workgroups loop over them
-// (0: one workgroup per item).  The drain shares the link with the next blocks' H2D copies: at full
-// grid it writes ~50 GB/s and the copies under it drop from 55.7 to 44.6 GB/s (config 5 trace, r04);
-// a few workgroups (~7.5 GB/s each) spread the same bytes over the next batch's copy time instead.
+// (0: one workgroup per item).  The drain shares the link with the next blocks' H2D copies: a full
+// grid's flood of writes cuts the copies under it from 55.7 to 44.6 GB/s (config 5 trace, r04); five
+// workgroups drain about as fast and leave the copies at 54.9 GB/s.
 constexpr uint64_t kXferPiece = 256 << 10;
 __global__ void __launch_bounds__(256) xfer_kernel(const XferJob *__restrict__ jobs, int njobs, uint32_t pieces)
 {
