@@ -129,6 +129,10 @@ def parse():
                          "(hdrf_submit_slots) instead of one block per batch (hdrf_submit_slot)")
     ap.add_argument("--mixed", action="store_true",
                     help="config5: config 4's mixed-entropy corpus instead of config 2's")
+    ap.add_argument("--no-sub", action="store_true",
+                    help="config 2 at N=1 also runs short config-4 and config-5 lines (the reference's default "
+                         "compressor 2, DN/DataNode.java:438) as child processes before its own run and carries "
+                         "them under \"configs\"; this turns them off")
     ap.add_argument("--workload", choices=["config2", "config4", "config5"], default="config2",
                     help="config4: mixed-entropy blocks (random/text/binary), dedup + Lz4Codec containers; "
                          "config5: host-resident (pinned) blocks streamed H2D on a side stream (PCIe-inclusive)")
@@ -179,6 +183,46 @@ def packet_driver_line(a):
     print(json.dumps(line), flush=True)
 
 
+SUB_RUNS = {
+    # config 4: mixed-entropy blocks, dedup + Lz4Codec on closed containers (compressor 2), depth 5;
+    # the CPU leg checks the container files of its sample
+    "config4": ["--workload", "config4", "--steps", "2", "--warmup", "1", "--cpu-sample-blocks", "8"],
+    # config 5: host-resident whole blocks under the reference default (compressor 2), every container
+    # file drained D2H after each completed batch, PCIe-inclusive
+    "config5": ["--workload", "config5", "--compressor", "2", "--steps", "2", "--warmup", "1",
+                "--cpu-sample-blocks", "8"],
+}
+
+
+def sub_configs():
+    """The short config-4 / config-5 lines, each in a child process (run before this process touches
+    the GPU, so each child has the whole card): {name: its JSON line without the per-stage table}."""
+    import subprocess
+    out = {}
+    for name, args in SUB_RUNS.items():
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__)] + args + ["--no-sub"], capture_output=True,
+                               text=True, timeout=420, env=dict(os.environ))
+            lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode != 0 or not lines:
+                out[name] = {"error": "rc %d: %s" % (r.returncode, (r.stderr or r.stdout)[-600:])}
+                continue
+            d = json.loads(lines[-1])
+        except Exception as e:                       # a failed sub-line never voids the headline
+            out[name] = {"error": repr(e)[:600]}
+            continue
+        d.pop("stages", None)
+        if isinstance(d.get("roofline"), dict):
+            d["roofline"].pop("alone", None)
+        d["command"] = "python bench.py " + " ".join(args)
+        d["wall_s"] = round(time.perf_counter() - t0, 1)
+        out[name] = d
+        print("sub-line %s: %.3f %s (%.0f s)" % (name, d.get("value") or 0, d.get("unit"), d["wall_s"]),
+              file=sys.stderr, flush=True)
+    return out
+
+
 def pcie_entry(value, h2d_bytes, d2h_bytes, step_s, link):
     """The link figures of a config-5 line: the raw probes and what the step moved over PCIe."""
     moved = (h2d_bytes + d2h_bytes) / step_s / 1e9
@@ -217,6 +261,9 @@ def main():
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    subs = None
+    if world == 1 and a.workload == "config2" and not a.no_sub and not a.serial:
+        subs = sub_configs()                             # before this process initialises the GPU
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import numpy as np
     import torch
@@ -583,6 +630,8 @@ def main():
                 "roofline": roofline, "cpu_baseline": cpu, "dedup": dedup, "stages": stages}
         if compression:
             line["compression"] = compression
+        if subs:
+            line["configs"] = subs
         if read_side:
             line["read_side"] = read_side
         if host:

@@ -1105,6 +1105,12 @@ static void copy_nt(uint8_t *dst, const uint8_t *src, uint64_t n)
         __builtin_nontemporal_store(d, (v2 *)(dst + 64 * i + 48));
     }
     std::memcpy(dst + 64 * n64, src + 64 * n64, n & 63);
+    // Non-temporal stores are weakly ordered: fence them here, on the thread that wrote them, so
+    // the staged bytes are visible before any later store of this thread (the hand-off of the block
+    // to another thread that queues its last chunk's copy, e.g. hdrf_submit_slots from a submitter).
+#if !defined(__HIP_DEVICE_COMPILE__)
+    __builtin_ia32_sfence();
+#endif
 }
 
 static bool rx_nt()
@@ -2360,9 +2366,18 @@ extern "C" int hdrf_gx_piece(hdrf_ctx *ctx, uint32_t id, uint64_t off, uint64_t 
 extern "C" int hdrf_gx_compress(hdrf_ctx *ctx)
 {
     HDRF_LOCK(ctx);
-    if (int rc = gx_check(ctx, 4)) return rc;
+    if (!ctx) return HDRF_E_INVAL;
+    // every return path leaves the queued hdrf_gx_piece writes complete (their source buffers may be
+    // released by the caller as soon as this returns)
+    if (int rc = gx_check(ctx, 4)) {
+        if (ctx->stB) (void)hipStreamSynchronize(ctx->stB);
+        return rc;
+    }
     const hdrf_cfg &c = ctx->cfg;
-    if (c.compressor != 2) return 0;
+    if (c.compressor != 2) {
+        HIPCK(hipStreamSynchronize(ctx->stB));
+        return 0;
+    }
     Slot &S = ctx->sl[ctx->gx_nback % 2];
     const uint32_t nclosed = *S.h_nclosed;
     if (!nclosed || S.gx_compressed) {                  // once per batch: a second call changes nothing

@@ -216,10 +216,14 @@ class NodeRank:
         held = [(cid, a, b, rb.to(self.device)) for cid, a, b, rb in bufs]
         if held:
             torch.cuda.synchronize(self.device)
-        for cid, a, b, t in held:
-            ctx.gx_piece(cid, a, b - a, t.data_ptr(), write=True)
-        n = ctx.gx_compress()
-        del held
+        try:
+            for cid, a, b, t in held:
+                ctx.gx_piece(cid, a, b - a, t.data_ptr(), write=True)
+            n = ctx.gx_compress()        # synchronises the back stream on every return path
+        finally:
+            if held:                     # a raised call: the queued writes still read `held`
+                ctx.synchronize()
+            del held
         return n
 
     def reduce_batch(self, dev_ptrs, lens, readable, block_ids, gbase):

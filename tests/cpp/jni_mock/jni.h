@@ -1,6 +1,8 @@
-/* Minimal stand-in for a JDK's jni.h, for a compile-only check of integration/jni/hdrf_jni.c in
- * this JDK-less image (tests/test_cpp_scheme.py).  Only the types and the JNIEnv functions the
- * shim calls, with the JNI specification's signatures; nothing is linked or run. */
+/* Minimal stand-in for a JDK's jni.h in this JDK-less image: the types and the JNIEnv functions
+ * integration/jni/hdrf_jni.c calls, with the JNI specification's signatures (the table's layout is
+ * this header's own, not the JDK's).  tests/cpp/jni_driver.c implements the table (direct buffers,
+ * arrays, strings, a pending exception per thread) and drives the shim's entry points the way a
+ * DataNode's HipReductionScheme would (tests/test_jni.py). */
 #pragma once
 #include <stdint.h>
 

@@ -38,16 +38,21 @@ def _read_containers(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("compressor,mirror,batch,mixed", [(1, "socket", False, False), (2, "ring", True, True)])
-def test_packet_driver_matches_oracle(tmp_path, compressor, mirror, batch, mixed):
+@pytest.mark.parametrize("compressor,mirror,batch,mixed,nb,mib,cmax,slots", [
+    (1, "socket", False, False, 6, 8, 1 << 20, 512),
+    (2, "ring", True, True, 6, 8, 1 << 20, 512),
+    # the bench's shape (config 5, the reference default compressor 2): 128 MiB blocks, 32 MiB
+    # containers, 512 arena slots, mixed-entropy corpus, receive rounds handed over as batches
+    (2, "ring", True, True, 8, 128, 1 << 25, 512),
+])
+def test_packet_driver_matches_oracle(tmp_path, compressor, mirror, batch, mixed, nb, mib, cmax, slots):
     from hdrf_amd.corpus import corpus_block_host, corpus_roots
     from oracle.oracle import Oracle
     exe = os.path.join(ROOT, "tools", "_build", "packet_driver")
     if not os.path.exists(exe):
         exe = _driver()
-    nb, mib, cmax = 6, 8, 1 << 20
     args = [exe, str(nb), str(mib), "64", "4", "1", str(tmp_path), "--compressor", str(compressor), "--mirror", mirror,
-            "--container-kib", str(cmax >> 10), "--index-log2", "20"]
+            "--container-kib", str(cmax >> 10), "--index-log2", "20" if mib <= 8 else "24", "--arena-slots", str(slots)]
     args += ["--batch"] * batch + ["--mixed"] * mixed
     r = subprocess.run(args, capture_output=True, text=True, timeout=300)
     print(r.stdout, r.stderr)
@@ -83,3 +88,4 @@ def test_packet_driver_matches_oracle(tmp_path, compressor, mirror, batch, mixed
             assert cid in disk, f"container {cid} never drained"
             assert disk[cid][0] == bytes(od) and disk[cid][1] == oc, f"container {cid} file differs"
     assert n_cont == len(disk) and n_closed >= 6, (n_cont, n_closed)
+    print(f"{nb} x {mib} MiB blocks: {n_cont} container files ({n_closed} closed) equal the oracle's")
