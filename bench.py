@@ -48,6 +48,16 @@ if os.environ.get("HDRF_SPLIT_B", "1") not in ("", "0"):
 else:
     CHAINS["B: index+store"] = _INDEX + _STORE
 CHAINS["L: LZ4"] = ["compress(lz4_seg/lz4_pack)"]
+# node-global ranks (N > 1, hdrf_amd/node.py): the front on W / A / X, the back phases and the gaps the
+# exchanges fill on stream B, the arena copy on B2 (api.hip gx_collect)
+CHAINS_GX = {"W: chunking": CHAINS["W: chunking"], "A: SHA": ["sha(sha_chunk_kernel)"],
+             "X: local aggregation": ["gx_local(scratch claim/apply/decide + gx_emit)"],
+             "B: back (owner .. commit + exchanges)": [
+                 "gx_x1(X1 all-to-all + host)", "gx_owner(own_claim..own_finish)", "gx_x2(X2 all-to-all)",
+                 "gx_decide(gx_decide + x3want)", "scan(tile/chunk_scan)", "gx_flush_fn(fn_info/fn_chain/fn_pack)",
+                 "gx_allgather(flush descriptors)", "gx_alloc_scan(gx_scan_kernel)", "flush(flush_kernel)",
+                 "gx_place_meta(place_kernel part 1)", "gx_x3(X3 all-to-all + host)", "gx_commit(own_commit)"],
+             "B2: arena copy": ["place(place_kernel)"]}
 SHA_MIX_CEILING_WI_NS = 425.0  # tools/sha_peak.hip: the SHA-1 instruction mix on register-resident data
 
 
@@ -497,7 +507,8 @@ def main():
                                  if k in pmc), {}).get("hbm_bytes_per_launch")}
 
     # per-stream chains: the batch period is set by the longest one (the critical path)
-    chains = {c: round(sum(avg[s] for s in st), 4) for c, st in CHAINS.items()}
+    chain_def = CHAINS_GX if world > 1 else CHAINS
+    chains = {c: round(sum(avg[s] for s in st), 4) for c, st in chain_def.items()}
     crit = max(chains, key=chains.get)
     chunk_ms = chains["W: chunking"]
     chunking = {"kernels": "gmax + lane walk + stitch (one batch, in pipeline)", "avg_batch_ms": chunk_ms,
@@ -537,8 +548,18 @@ def main():
                           "loads); profiles/r02_lz4_phases.txt, profiles/r04_lz4_pmc_ab.txt"}
     # the line's roofline: the dominant kernel of the critical chain
     top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place, "B2: store": place,
-           "B: index": place, "L: LZ4": lz4}[crit]
+           "B: index": place, "L: LZ4": lz4, "B2: arena copy": place}.get(crit)
+    if top is None:
+        # a node-global chain without an HBM-bound kernel of its own (local aggregation; the back
+        # phases, whose time is index atomics and the exchanges): the line names the dominant HBM kernel
+        # of the rank's pipeline, place, and says which chain set the period
+        top = dict(place)
+        top["note"] = "critical chain %s has no HBM-streaming kernel; the entry is place_kernel's" % crit
     roofline = dict(top)
+    if world > 1:
+        roofline["front_period_ms"] = round(max(chains[c] for c in ("W: chunking", "A: SHA", "X: local aggregation")), 4)
+        roofline["front_period_note"] = ("per-rank front half (chunking | SHA | local aggregation on three streams, "
+                                         "batches overlapped): the longest of the three chains per batch")
     roofline.update({"traffic_source": pmc_src, "critical_path": crit, "chains_ms_per_batch": chains,
                      "batch_period_ms": round(el / a.steps / nbatch * 1e3, 4),
                      "chunking": chunking, "sha": sha, "place": place})

@@ -108,6 +108,35 @@ struct Slot {
     uint8_t *d_hstage = nullptr;              // host path: device copies of the batch's blocks
     uint64_t hstage_stride = 0;
     hipEvent_t evW[4] = {}, evA[3] = {}, evB[10] = {};   // stage markers (timing)
+    // node-global mode: the slot's host side of a batch (pinned: front counts, count uploads, the
+    // place read-back), whether a batch used the slot, and whether its arena copy ran on stream B2
+    struct GxHost *h_gx = nullptr;
+    std::vector<int64_t> gx_c1;               // X1 send counts of the batch in the slot
+    bool gx_inuse = false, gx_split = false;
+    hipEvent_t gx_meta = nullptr;             // placement (part 1) and its read-back done (stream B)
+};
+
+// Pinned per-slot exchange with the host in node-global mode: what hdrf_gx_front_wait and
+// hdrf_gx_place_wait read, and the receive counts hdrf_gx_owner / hdrf_gx_commit upload (a pageable
+// source would make hipMemcpyAsync wait for the stream).
+struct GxHost {
+    unsigned long long front_cnt[64];         // X1 records emitted per owner (gx_emit)
+    int front_err, commit_err;
+    int64_t up_r1[64], up_r3[64];             // X1 / X3 receive counts (uploads)
+    unsigned long long c3[64], x3e[64], x3want[64];   // X3 send counts, X3 receive counts, X2-implied sends
+    AllocState st[4];                         // [0] allocator in [1] predicted [2] node final [3] flush walk result
+};
+
+// Per-batch timing of the node-global phases (cfg.timing): HIP events on the streams each phase runs
+// on, in a ring indexed by the batch's sequence number, collected once the batch has completed.
+enum GxEv {
+    kW0 = 0, kA0 = 4, kX0 = 7, kG0 = 11, kG1, kG2, kG3, kG4, kG5, kG6, kG7, kG8, kG9, kG10, kG11, kG12, kG13,
+    kP0, kP1, kGxEv
+};
+constexpr int kGxRing = 8;
+struct GxTime {
+    hipEvent_t ev[kGxEv] = {};
+    uint32_t rec = 0;                         // bit e: ev[e] was recorded for this batch
 };
 
 }  // namespace
@@ -149,7 +178,7 @@ struct hdrf_ctx {
     uint32_t batch = 0;                              // batch ids: grow over the context's life (never reset)
     uint32_t epoch = 1;                              // index generation in the tag words (1..255)
     uint32_t bfirst = 1;                             // first batch id of the current epoch
-    uint32_t scratch_epoch[2] = {0, 0};              // node-global: generation of each scratch table
+    uint32_t scratch_epoch[kSlots] = {};             // node-global: generation of each scratch table
     int have_alloc = 0;
     int last_nblocks = 0;
     AllocState h_alloc{};
@@ -169,10 +198,20 @@ struct hdrf_ctx {
     int G = 1, rank = 0;
     // Two batches can be in the node-global pipeline: the front half of batch k+1 (slot (k+1)%2,
     // stream A) runs while batch k goes through its exchanges and back phases (slot k%2, stream B).
-    IndexEntry *d_scratch[2] = {nullptr, nullptr};   // per-slot local aggregation table
+    IndexEntry *d_scratch[kSlots] = {};         // per-slot local aggregation table
     int scratch_log2 = 0;
     int64_t gx_cap = 0;
-    unsigned long long *d_gxe[2] = {nullptr, nullptr};  // [G] X1 records emitted per peer, per slot
+    int gx_depth = 3;                            // node-global batches in flight (HDRF_GX_DEPTH, 2..kSlots)
+    hipStream_t stX = nullptr;                   // node-global: local aggregation + X1 records (front)
+    unsigned long long *d_gxe[kSlots] = {};      // [G] X1 records emitted per peer, per slot
+    unsigned long long *d_x3want = nullptr;      // [G] X3 records the X2 responses call for (sender check)
+    AllocState *d_gxst = nullptr;                // [4] device allocator scan: in, predicted, node final, walk
+    int *d_gx_err = nullptr;                     // errors of hdrf_gx_commit (reported by the next place / sync)
+    uint64_t fn_bytes = 0, fn_mcap = 0;          // packed flush descriptor (hdrf_gx_flush_fn_dev)
+    int gx_dscan = 0;                            // the back batch's allocator came from the device scan
+    bool gx_place_pending = false;               // hdrf_gx_place_launch ran, hdrf_gx_place_wait not yet
+    GxTime gxt[kGxRing];
+    uint64_t gxt_done = 0;                       // batches whose phase times were collected
     unsigned long long *d_gx_counts = nullptr;   // [G] X3 records emitted per peer (back phases)
     int64_t *d_gx_rcounts = nullptr;             // [G] records received per peer
     // [G] X3 records each source will send this owner: one per record that holds its created entry's
@@ -277,6 +316,8 @@ static int device_error(hdrf_ctx *ctx, int herr)
     if (herr & 192) m += " (chunking: speculative list overflow / inconsistent stitch)";
     if (herr & 4) m += " (tag-collision list full)";
     if (herr & 256) m += " (node-global: an X3 location names no index entry)";
+    if (herr & 512) m += " (node-global: malformed flush descriptor in the allocator scan)";
+    if (herr & 1024) m += " (node-global: flush function candidate table overflow or runaway chain)";
     return set_err(ctx, (herr & kErrCapacity) ? HDRF_E_CAPACITY : HDRF_E_DEVICE, m);
 }
 
@@ -337,11 +378,12 @@ static void free_slot(Slot &S)
                    S.d_lzwork};
     for (void *p : dev)
         if (p) (void)hipFree(p);
-    void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_long, S.h_closed, S.h_filelen, S.h_desc};
+    void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_long, S.h_closed, S.h_filelen, S.h_desc,
+                    S.h_gx};
     for (void *p : host)
         if (p) (void)hipHostFree(p);
     hipEvent_t evs[] = {S.walk_done, S.front_done, S.back_done, S.copy_done, S.recipe_done, S.placed, S.lz_done,
-                        S.gmax_done, S.idx_done};
+                        S.gmax_done, S.idx_done, S.gx_meta};
     if (S.d_rjobs) (void)hipFree(S.d_rjobs);
     if (S.h_rjobs) (void)hipHostFree(S.h_rjobs);
     if (S.d_hstage) (void)hipFree(S.d_hstage);
@@ -362,11 +404,19 @@ static void free_all(hdrf_ctx *ctx)
     ctx->loaded.clear();
     for (auto p : ctx->rchunks) (void)hipFree(p);
     ctx->rchunks.clear();
-    void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_scratch[0],
-                    ctx->d_scratch[1], ctx->d_gxe[0], ctx->d_gxe[1], ctx->d_gx_counts, ctx->d_gx_rcounts, ctx->d_oslot,
-                    ctx->d_oflags, ctx->d_carena, ctx->d_fn, ctx->d_gx_x3exp};
+    void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_gx_counts,
+                    ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags, ctx->d_carena, ctx->d_fn, ctx->d_gx_x3exp,
+                    ctx->d_x3want, ctx->d_gxst, ctx->d_gx_err};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    for (int i = 0; i < kSlots; i++) {
+        if (ctx->d_scratch[i]) (void)hipFree(ctx->d_scratch[i]);
+        if (ctx->d_gxe[i]) (void)hipFree(ctx->d_gxe[i]);
+    }
+    for (auto &T : ctx->gxt)
+        for (auto e : T.ev)
+            if (e) (void)hipEventDestroy(e);
+    if (ctx->stX) (void)hipStreamDestroy(ctx->stX);
     if (ctx->st) (void)hipStreamDestroy(ctx->st);
     if (ctx->stB) (void)hipStreamDestroy(ctx->stB);
     if (ctx->stB2) (void)hipStreamDestroy(ctx->stB2);
@@ -439,7 +489,8 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         hipEventCreateWithFlags(&S.placed, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.lz_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.gmax_done, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&S.idx_done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&S.idx_done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.gx_meta, hipEventDisableTiming) != hipSuccess)
         return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
     for (auto &e : S.evW)
         if (hipEventCreate(&e) != hipSuccess) return set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
@@ -467,6 +518,7 @@ static int drain(hdrf_ctx *ctx)
     HIPCK(hipStreamSynchronize(ctx->st));
     HIPCK(hipStreamSynchronize(ctx->stB));
     HIPCK(hipStreamSynchronize(ctx->stB2));
+    if (ctx->stX) HIPCK(hipStreamSynchronize(ctx->stX));
     return rc;
 }
 
@@ -492,7 +544,7 @@ static int init_state(hdrf_ctx *ctx, bool fresh)
     ctx->bfirst = ctx->batch + 1;
     HIPCK(launch_index_clear(ctx->d_tab, clear ? ctx->cfg.index_log2 : -1, ctx->d_alloc, a, ist));
     if (fresh)
-        for (int i = 0; i < 2; i++)
+        for (int i = 0; i < kSlots; i++)
             if (ctx->d_scratch[i]) {
                 HIPCK(hipMemsetAsync(ctx->d_scratch[i], 0, sizeof(IndexEntry) << ctx->scratch_log2, ist));
                 ctx->scratch_epoch[i] = 0;
@@ -511,6 +563,12 @@ static int init_state(hdrf_ctx *ctx, bool fresh)
     ctx->last_nblocks = 0;
     ctx->gx_nfront = ctx->gx_nfwait = ctx->gx_nback = 0;
     ctx->gx_bphase = 0;
+    ctx->gx_dscan = ctx->gx_scanned = 0;
+    ctx->gx_place_pending = false;
+    ctx->gxt_done = 0;
+    for (auto &T : ctx->gxt) T.rec = 0;
+    for (auto &S : ctx->sl) S.gx_inuse = S.gx_split = false;
+    if (ctx->d_gx_err) HIPCK(hipMemsetAsync(ctx->d_gx_err, 0, sizeof(int), ist));
     ctx->stats = hdrf_stats{};
     ctx->pend_closed.clear();
     for (auto &u : ctx->undrained) u = 0;
@@ -597,9 +655,26 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         while (lg < 31 && (double)(1ull << lg) < expect) lg++;
         ctx->scratch_log2 = lg;
         ctx->gx_cap = (int64_t)nchunk;
+        // batches in the node-global pipeline: the fronts of the next ones (chunking on W, SHA on A,
+        // local aggregation on X) run while the oldest goes through its exchanges and back phases
+        const char *gd = getenv("HDRF_GX_DEPTH");
+        ctx->gx_depth = std::max(2, std::min(kSlots, gd ? atoi(gd) : 3));
+        ctx->fn_mcap = gx_fn_mcap(c.container_max, c.window, B);
+        ctx->fn_bytes = gx_fn_bytes(c.container_max, c.window, B);
         const size_t nrec = (size_t)ctx->G * (size_t)ctx->gx_cap;
-        if ((rc = dalloc(ctx, &ctx->d_scratch[0], (size_t)1 << lg)) || (rc = dalloc(ctx, &ctx->d_scratch[1], (size_t)1 << lg)) ||
-            (rc = dalloc(ctx, &ctx->d_gxe[0], 64)) || (rc = dalloc(ctx, &ctx->d_gxe[1], 64)) ||
+        for (int i = 0; i < ctx->gx_depth && !rc; i++)
+            if ((rc = dalloc(ctx, &ctx->d_scratch[i], (size_t)1 << lg)) || (rc = dalloc(ctx, &ctx->d_gxe[i], 64)) ||
+                (rc = halloc(ctx, &ctx->sl[i].h_gx, 1))) {
+            }
+        if (!rc && hipStreamCreateWithFlags(&ctx->stX, hipStreamNonBlocking) != hipSuccess)
+            rc = set_err(ctx, HDRF_E_HIP, "hipStreamCreate failed");
+        if (!rc && c.timing)
+            for (auto &T : ctx->gxt)
+                for (auto &e : T.ev)
+                    if (!rc && hipEventCreate(&e) != hipSuccess) rc = set_err(ctx, HDRF_E_HIP, "hipEventCreate failed");
+        if (rc) {
+        } else if ((rc = dalloc(ctx, &ctx->d_x3want, 64)) || (rc = dalloc(ctx, &ctx->d_gxst, 4)) ||
+            (rc = dalloc(ctx, &ctx->d_gx_err, 1)) ||
             (rc = dalloc(ctx, &ctx->d_gx_counts, 64)) ||
             (rc = dalloc(ctx, &ctx->d_gx_rcounts, 64)) || (rc = dalloc(ctx, &ctx->d_gx_x3exp, 64)) ||
             (rc = dalloc(ctx, &ctx->d_oslot, nrec)) ||
@@ -607,7 +682,8 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
         }
         // owner slots start defined (hdrf_gx_owner's kernels never read a slot the claim did not write
         // once an error is raised, but a defined value keeps any later misuse inside the table)
-        if (!rc && hipMemset(ctx->d_oslot, 0, sizeof(uint32_t) * nrec) != hipSuccess)
+        if (!rc && (hipMemset(ctx->d_oslot, 0, sizeof(uint32_t) * nrec) != hipSuccess ||
+                    hipMemset(ctx->d_gx_err, 0, sizeof(int)) != hipSuccess))
             rc = set_err(ctx, HDRF_E_HIP, "hipMemset failed");
     }
     ctx->timing = c.timing != 0;
@@ -1976,11 +2052,62 @@ extern "C" int hdrf_gx_layout_get(hdrf_ctx *ctx, hdrf_gx_layout *out)
     out->x1_words = ctx->HW + 2;
     out->x2_words = 2;
     out->x3_words = 4;
+    out->depth = ctx->gx_depth;
+    out->fn_bytes = (int64_t)ctx->fn_bytes;
     return 0;
 }
 
-// Front half of a node-global batch (chunking, SHA, local aggregation, X1 records), launched on
-// stream A into slot nfront % 2 without waiting: it overlaps the previous batch's back phases.
+// ---- node-global pipeline ----------------------------------------------------
+// A batch's front half runs like the single-node pipeline: chunking on stream W, SHA on stream A,
+// then the local aggregation and its X1 records on stream X, in slot seq % gx_depth, so the fronts
+// of the next batches run while the oldest batch goes through its exchanges and back phases on
+// stream B.  The back half enqueues without host round trips: the allocator scan runs on the
+// device (hdrf_gx_flush_fn_dev -> all-gather of fixed-size descriptors -> hdrf_gx_alloc_scan_dev),
+// placement and its read-back are one event the host waits for (the X3 counts size the X3
+// exchange), the arena copy runs on stream B2 beside the next batch's owner phases, and the commit
+// is not waited for (its errors are reported by the next place or hdrf_gx_sync).
+
+static void gx_mark(hdrf_ctx *ctx, uint64_t seq, int e, hipStream_t st)
+{
+    if (!ctx->timing) return;
+    GxTime &T = ctx->gxt[seq % kGxRing];
+    if (hipEventRecord(T.ev[e], st) == hipSuccess) T.rec |= 1u << e;
+}
+
+// phase times of completed batches, in order (wait: block until they are complete)
+static void gx_collect(hdrf_ctx *ctx, bool wait, uint64_t upto)
+{
+    if (!ctx->timing) return;
+    while (ctx->gxt_done < upto && ctx->gxt_done < ctx->gx_nback) {
+        const uint64_t k = ctx->gxt_done;
+        GxTime &T = ctx->gxt[k % kGxRing];
+        const auto has = [&](int e) { return (T.rec >> e & 1) != 0; };
+        for (int e : {(int)kG13, (int)kP1})
+            if (has(e)) {
+                if (wait) (void)hipEventSynchronize(T.ev[e]);
+                else if (hipEventQuery(T.ev[e]) != hipSuccess) return;
+            }
+        const auto add = [&](int stage, int a, int b) {
+            if (has(a) && has(b)) ctx->stage_ms[stage] += elapsed(T.ev[a], T.ev[b]);
+        };
+        add(11, kW0, kW0 + 1); add(0, kW0 + 1, kW0 + 2); add(1, kW0 + 2, kW0 + 3);
+        add(2, kA0, kA0 + 1);
+        add(12, kX0, kX0 + 3);
+        add(13, kG0, kG1); add(20, kG1, kG2); add(14, kG2, kG3); add(7, kG3, kG4);
+        add(15, kG5, kG6); add(21, kG6, kG7); add(16, kG7, kG8); add(8, kG8, kG9);
+        add(17, kG10, kG11); add(22, kG11, kG12); add(18, kG12, kG13);
+        add(9, kP0, kP1);
+        if (k > 0) {                                    // X1 + host gap: the previous commit to this owner phase
+            GxTime &Pv = ctx->gxt[(k - 1) % kGxRing];
+            if ((Pv.rec >> kG13 & 1) && has(kG0)) ctx->stage_ms[19] += elapsed(Pv.ev[kG13], T.ev[kG0]);
+        }
+        ctx->gxt_done++;
+    }
+}
+
+// Front half of a node-global batch (chunking, SHA, local aggregation, X1 records), launched into
+// slot nfront % gx_depth without waiting.  The slot's previous batch must have left it: its back
+// phases (stream B) and its arena copy (stream B2) are waited for on the device.
 extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                                     const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase,
                                     uint32_t *x1_send)
@@ -1988,72 +2115,91 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
     if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
-    if (ctx->gx_nfront != ctx->gx_nfwait || ctx->gx_nfront - ctx->gx_nback >= 2)
-        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front_launch: a front is pending or two batches are in flight");
+    const uint64_t D = (uint64_t)ctx->gx_depth;
+    if (ctx->gx_nfront - ctx->gx_nback >= D)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front_launch: " + std::to_string(D) +
+                                              " batches in the node-global pipeline (commit the oldest first)");
     if (!x1_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
-    const int si = (int)(ctx->gx_nfront % 2);
+    const uint64_t seq = ctx->gx_nfront;
+    const int si = (int)(seq % D);
     Slot &S = ctx->sl[si];
     const hdrf_cfg &c = ctx->cfg;
+    // the timing ring entry is reused: the batch kGxRing - 1 back (and everything before) is collected
+    if (ctx->timing) {
+        if (seq + 2 > (uint64_t)kGxRing) gx_collect(ctx, true, seq + 2 - kGxRing);
+        ctx->gxt[seq % kGxRing].rec = 0;
+    }
+    hipStream_t W = ctx->stW, A = ctx->st, X = ctx->stX;
+    if (S.gx_inuse) {                                   // the slot's previous batch is done with it
+        HIPCK(hipStreamWaitEvent(W, S.back_done, 0));
+        if (S.gx_split) HIPCK(hipStreamWaitEvent(W, S.placed, 0));
+    }
     if (int rc = prepare_blocks(ctx, S, nblocks, dev_data, len, readable)) return rc;
     S.gx_batch = ++ctx->batch;
-    hipStream_t st = ctx->st;
-    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, st));
-    Marker mk;
-    mk.ev = ctx->timing ? S.evB : nullptr;             // 9 markers: gmax, walk .. slow+decide, end
+    HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, W));
+    GxTime &T = ctx->gxt[seq % kGxRing];
+    Marker mw, ma, mx;
+    mw.ev = ctx->timing ? &T.ev[kW0] : nullptr;
     HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs,
                           chunk_scratch(S, c.compressor), c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst,
-                          S.d_off, ctx->cap_blk, S.d_err, st, &mk));
-    if (S.recipe_pending) HIPCK(hipStreamWaitEvent(st, S.recipe_done, 0));
-    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig,
-                     S.d_queue, ctx->sha_long, st, &mk));
-    // local aggregation: a fresh scratch table, every entry "created" in batch 1
-    // (a fresh scratch table per batch: the next epoch of the slot's table, cleared every 255 uses)
+                          S.d_off, ctx->cap_blk, S.d_err, W, &mw));
+    mw.mark(W);
+    HIPCK(hipEventRecord(S.walk_done, W));
+    HIPCK(hipStreamWaitEvent(A, S.walk_done, 0));
+    if (S.recipe_pending) HIPCK(hipStreamWaitEvent(A, S.recipe_done, 0));
+    ma.ev = ctx->timing ? &T.ev[kA0] : nullptr;
+    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig, S.d_queue, ctx->sha_long, A,
+                     &ma));
+    ma.mark(A);
+    HIPCK(hipEventRecord(S.idx_done, A));               // (node-global: "the batch's digests are ready")
+    // local aggregation: a fresh scratch table (the next epoch of the slot's table, cleared every 255
+    // uses), every entry "created" in batch 1
+    HIPCK(hipStreamWaitEvent(X, S.idx_done, 0));
     if (++ctx->scratch_epoch[si] > 255) {
-        HIPCK(hipMemsetAsync(ctx->d_scratch[si], 0, sizeof(IndexEntry) << ctx->scratch_log2, st));
+        HIPCK(hipMemsetAsync(ctx->d_scratch[si], 0, sizeof(IndexEntry) << ctx->scratch_log2, X));
         ctx->scratch_epoch[si] = 1;
     }
     const unsigned long long skey = ((unsigned long long)ctx->scratch_epoch[si] << 56) | tag_bits(ctx);
+    mx.ev = ctx->timing ? &T.ev[kX0] : nullptr;
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_scratch[si],
                        ctx->scratch_log2, 1u, 1u, skey, S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap,
-                       S.d_flags, S.d_tilesum, ctx->ntiles, S.d_err, st, &mk));
+                       S.d_flags, S.d_tilesum, ctx->ntiles, S.d_err, X, &mx));
     HIPCK(launch_gx_emit(c.hasher, S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, S.d_dig, ctx->d_scratch[si],
-                         S.d_slot, S.d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gxe[si], S.d_err, st));
-    mk.mark(st);
-    HIPCK(hipEventRecord(S.front_done, st));
+                         S.d_slot, S.d_flags, gbase, ctx->G, x1_send, ctx->gx_cap, ctx->d_gxe[si], S.d_err, X));
+    mx.mark(X);
+    HIPCK(hipMemcpyAsync(S.h_gx->front_cnt, ctx->d_gxe[si], sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, X));
+    HIPCK(hipMemcpyAsync(&S.h_gx->front_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, X));
+    HIPCK(hipEventRecord(S.front_done, X));
+    if (ctx->timing) T.rec |= 0xFu << kW0 | 0x7u << kA0 | 0xFu << kX0;
     S.nblocks = nblocks;
     S.lens.assign(len, len + nblocks);
     S.ids.assign(nblocks, 0);
     if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
+    S.gx_inuse = true;
+    S.gx_split = false;
     ctx->gx_nfront++;
     return 0;
 }
 
-// Wait for the launched front; its per-peer X1 record counts -> send_counts[G].
+// Wait for the oldest launched front; its per-peer X1 record counts -> send_counts[G].
 extern "C" int hdrf_gx_front_wait(hdrf_ctx *ctx, int64_t *send_counts)
 {
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
-    if (ctx->gx_nfront != ctx->gx_nfwait + 1) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front_wait: no front pending");
+    if (ctx->gx_nfront <= ctx->gx_nfwait) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front_wait: no front pending");
     if (!send_counts) return set_err(ctx, HDRF_E_INVAL, "null counts");
-    const int si = (int)(ctx->gx_nfwait % 2);
+    const int si = (int)(ctx->gx_nfwait % (uint64_t)ctx->gx_depth);
     Slot &S = ctx->sl[si];
-    hipStream_t st = ctx->st;
-    std::vector<unsigned long long> cnt(ctx->G);
-    int herr = 0;
-    HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gxe[si], sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
+    HIPCK(hipEventSynchronize(S.front_done));
     ctx->gx_nfwait++;
-    if (ctx->timing)
-        ctx->stage_ms[11] += elapsed(S.evB[0], S.evB[1]);
-    if (ctx->timing)
-        for (int i = 0; i < 7; i++) ctx->stage_ms[i] += elapsed(S.evB[i + 1], S.evB[i + 2]);
+    const int herr = S.h_gx->front_err;
     if (herr) {
-        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
-        HIPCK(hipStreamSynchronize(st));
+        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->stX));
+        HIPCK(hipStreamSynchronize(ctx->stX));
         return device_error(ctx, herr);
     }
-    for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
+    S.gx_c1.assign(ctx->G, 0);
+    for (int d = 0; d < ctx->G; d++) send_counts[d] = S.gx_c1[(size_t)d] = (int64_t)S.h_gx->front_cnt[d];
     return 0;
 }
 
@@ -2063,24 +2209,33 @@ extern "C" int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *cons
 {
     HDRF_LOCK(ctx);
     if (!send_counts) return ctx ? set_err(ctx, HDRF_E_INVAL, "null counts") : HDRF_E_INVAL;
+    if (ctx && ctx->gx_nfront != ctx->gx_nfwait)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_front: launched fronts are pending (hdrf_gx_front_wait)");
     if (int rc = hdrf_gx_front_launch(ctx, nblocks, dev_data, len, readable, block_ids, gbase, x1_send)) return rc;
     return hdrf_gx_front_wait(ctx, send_counts);
 }
+
+static Slot &gx_back_slot(hdrf_ctx *ctx) { return ctx->sl[ctx->gx_nback % (uint64_t)ctx->gx_depth]; }
+static int gx_back_si(hdrf_ctx *ctx) { return (int)(ctx->gx_nback % (uint64_t)ctx->gx_depth); }
 
 extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64_t *recv_counts, uint32_t *x2_send)
 {
     HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 0)) return rc;
-    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    Slot &S = gx_back_slot(ctx);
     if (!x1_recv || !recv_counts || !x2_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     for (int s = 0; s < ctx->G; s++)
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
     hipStream_t st = ctx->stB;
-    HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
+    const uint64_t seq = ctx->gx_nback;
+    gx_mark(ctx, seq, kG0, st);
+    std::memcpy(S.h_gx->up_r1, recv_counts, sizeof(int64_t) * ctx->G);
+    HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, S.h_gx->up_r1, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(ctx->d_gx_x3exp, 0, sizeof(unsigned long long) * ctx->G, st));
     HIPCK(launch_gx_owner(ctx->cfg.hasher, x1_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap,
                           ctx->G, ctx->d_tab, ctx->cfg.index_log2, S.gx_batch, ctx->bfirst, tag_mask(ctx), ctx->d_oslot,
                           ctx->d_oflags, S.d_coll, S.d_ncoll, ctx->coll_cap, x2_send, ctx->d_gx_x3exp, S.d_err, st));
+    gx_mark(ctx, seq, kG1, st);
     // no host round trip: a device error (S.d_err) is read back with the batch by hdrf_gx_place, and
     // the X2 exchange may be enqueued on stream B right behind this kernel (hdrf_gx_stream)
     ctx->gx_bphase = 1;
@@ -2099,16 +2254,23 @@ extern "C" int hdrf_gx_decide(hdrf_ctx *ctx, const uint32_t *x2_recv)
 {
     HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 1)) return rc;
-    const int si = (int)(ctx->gx_nback % 2);
+    const int si = gx_back_si(ctx);
     Slot &S = ctx->sl[si];
     if (!x2_recv) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
     hipStream_t st = ctx->stB;
+    const uint64_t seq = ctx->gx_nback;
     const int nb = S.nblocks;
+    gx_mark(ctx, seq, kG2, st);
     HIPCK(launch_gx_decide(S.d_bst, nb, ctx->cap_blk, ctx->ntiles, S.d_off, ctx->d_scratch[si], S.d_slot, x2_recv,
                            S.d_flags, S.d_tilesum, st));
+    // the X3 records the owners' answers call for (checked against place_kernel's own counts)
+    HIPCK(launch_gx_x3want(x2_recv, ctx->d_gxe[si], max_count(S.gx_c1.data(), ctx->G), ctx->gx_cap, ctx->G,
+                           ctx->d_x3want, st));
+    gx_mark(ctx, seq, kG3, st);
     const StoreParams P = store_params(ctx, nb);
     HIPCK(launch_store_scan(P, S.d_bst, S.d_off, S.d_flags, S.d_tilesum, S.d_tilepre, S.d_store,
                             S.d_pre, st));
+    gx_mark(ctx, seq, kG4, st);
     ctx->gx_x2 = x2_recv;
     ctx->gx_bphase = 2;
     return 0;
@@ -2118,29 +2280,37 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
 {
     HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 2)) return rc;
-    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    Slot &S = gx_back_slot(ctx);
     hipStream_t st = ctx->stB;
     if (alloc_in) {
+        ctx->gx_dscan = 0;                             // a host-given allocator replaces the device scan's
         std::memcpy(&ctx->gx_ain, alloc_in, sizeof(AllocState));
-        HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_in, sizeof(AllocState), hipMemcpyHostToDevice, st));
-    } else {
-        HIPCK(hipMemcpyAsync(&ctx->gx_ain, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
+        S.h_gx->st[0] = ctx->gx_ain;
+        HIPCK(hipMemcpyAsync(ctx->d_alloc, &S.h_gx->st[0], sizeof(AllocState), hipMemcpyHostToDevice, st));
+    } else if (!ctx->gx_dscan) {
+        HIPCK(hipMemcpyAsync(&S.h_gx->st[0], ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
     }
     HIPCK(hipMemsetAsync(S.d_nclosed, 0, sizeof(uint32_t), st));
     const StoreParams P = store_params(ctx, S.nblocks);
     HIPCK(launch_store_flush(P, S.d_bst, S.d_store, S.d_pre, ctx->d_alloc, S.d_rstate, S.d_ev,
                              S.d_closed, S.d_nclosed, S.d_err, st));
-    if (!alloc_out && ctx->gx_scanned) {                // the scan knows the result: no host round trip
-        ctx->gx_aout = ctx->gx_expect;
+    gx_mark(ctx, ctx->gx_nback, kG9, st);
+    if (!alloc_out && (ctx->gx_scanned || ctx->gx_dscan)) {   // the scan knows the result: no host round trip
+        if (ctx->gx_scanned) ctx->gx_aout = ctx->gx_expect;
         ctx->gx_bphase = 3;
         return 0;
     }
     AllocState a{};
-    HIPCK(hipMemcpyAsync(&a, ctx->d_alloc, sizeof a, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&S.h_gx->st[3], ctx->d_alloc, sizeof a, hipMemcpyDeviceToHost, st));
+    if (ctx->gx_dscan) HIPCK(hipMemcpyAsync(S.h_gx->st, ctx->d_gxst, 2 * sizeof a, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    a = S.h_gx->st[3];
+    if (!alloc_in) ctx->gx_ain = S.h_gx->st[0];
     ctx->gx_aout = a;
     if (ctx->gx_scanned && std::memcmp(&a, &ctx->gx_expect, sizeof a) != 0)
         return set_err(ctx, HDRF_E_DEVICE, "allocator scan disagrees with the flush walk");
+    if (ctx->gx_dscan && std::memcmp(&a, &S.h_gx->st[1], sizeof a) != 0)
+        return set_err(ctx, HDRF_E_DEVICE, "device allocator scan disagrees with the flush walk");
     if (alloc_out) {
         std::memset(alloc_out, 0, HDRF_ALLOC_STATE_BYTES);
         std::memcpy(alloc_out, &a, sizeof a);
@@ -2150,31 +2320,47 @@ extern "C" int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *al
 }
 
 // ---- allocator scan: every rank's flush walk as a function of the incoming allocator ------
-// (store.hip fn_info / fn_chain).  Descriptor, int64 words: n_thread, then per range t
+// (store.hip fn_info / fn_chain).  Host descriptor, int64 words: n_thread, then per range t
 // {any, S, base_last, S_last, m, m x (v, final container start, closes after the first)}.
 static int grow(hdrf_ctx *ctx, uint8_t **p, uint64_t *cap, uint64_t need);
+
+// fn_info / fn_chain into the context's scratch (the candidate rows per range); returns the scratch
+static int gx_flush_rows(hdrf_ctx *ctx, Slot &S, int *err, uint8_t **F_out)
+{
+    hipStream_t st = ctx->stB;
+    const StoreParams P = store_params(ctx, S.nblocks);
+    const int64_t kcap = (int64_t)ctx->max_batch * ctx->cap_blk + 1;
+    const uint64_t o_fr = 64 * 4 * sizeof(FnBlock), o_k = o_fr + 256, o_out = o_k + 256;
+    if (int rc = grow(ctx, &ctx->d_fn, &ctx->fn_cap, o_out + (uint64_t)P.n_thread * kcap * 24)) return rc;
+    uint8_t *F = ctx->d_fn;
+    HIPCK(hipMemsetAsync(F + o_k, 0, 64, st));
+    HIPCK(launch_flush_fn(P, S.d_bst, S.d_store, S.d_pre, (FnBlock *)F, (FnRange *)(F + o_fr), (uint64_t *)(F + o_out),
+                          kcap, (unsigned long long *)(F + o_k), err, st));
+    *F_out = F;
+    return 0;
+}
 
 extern "C" int64_t hdrf_gx_flush_fn(hdrf_ctx *ctx, int64_t *desc, int64_t cap)
 {
     HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 2)) return rc;
-    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    Slot &S = gx_back_slot(ctx);
     hipStream_t st = ctx->stB;
-    const StoreParams P = store_params(ctx, S.nblocks);
-    const int nt = P.n_thread;
+    const int nt = ctx->cfg.n_thread;
     const int64_t kcap = (int64_t)ctx->max_batch * ctx->cap_blk + 1;
-    const uint64_t o_fr = 64 * 4 * sizeof(FnBlock), o_k = o_fr + 256, o_err = o_k + 64, o_out = o_err + 192;
-    if (int rc = grow(ctx, &ctx->d_fn, &ctx->fn_cap, o_out + (uint64_t)nt * kcap * 24)) return rc;
-    uint8_t *F = ctx->d_fn;
-    HIPCK(hipMemsetAsync(F + o_k, 0, 64 + 4, st));
-    HIPCK(launch_flush_fn(P, S.d_bst, S.d_store, S.d_pre, (FnBlock *)F, (FnRange *)(F + o_fr), (uint64_t *)(F + o_out),
-                          kcap, (unsigned long long *)(F + o_k), (int *)(F + o_err), st));
+    const uint64_t o_fr = 64 * 4 * sizeof(FnBlock), o_k = o_fr + 256, o_out = o_k + 256;
+    uint8_t *F = nullptr;
+    // (the function's own error word after the rows; read back with the rows' counts)
+    if (int rc = grow(ctx, &ctx->d_fn, &ctx->fn_cap, o_out + (uint64_t)nt * kcap * 24 + 64)) return rc;
+    int *d_err = (int *)(ctx->d_fn + o_out + (uint64_t)nt * kcap * 24);
+    HIPCK(hipMemsetAsync(d_err, 0, sizeof(int), st));
+    if (int rc = gx_flush_rows(ctx, S, d_err, &F)) return rc;
     FnRange fr[4];
     unsigned long long K[4];
     int herr = 0;
     HIPCK(hipMemcpyAsync(fr, F + o_fr, sizeof(FnRange) * nt, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(K, F + o_k, 8 * nt, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(&herr, F + o_err, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&herr, d_err, 4, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     if (herr) return set_err(ctx, HDRF_E_DEVICE, "flush function: candidate table overflow or runaway chain");
     std::vector<uint64_t> rows[4];
@@ -2203,6 +2389,28 @@ extern "C" int64_t hdrf_gx_flush_fn(hdrf_ctx *ctx, int64_t *desc, int64_t cap)
     }
     std::copy(d.begin(), d.end(), desc);
     return (int64_t)d.size();
+}
+
+// The same function packed on the device into a fixed-size descriptor of hdrf_gx_layout.fn_bytes
+// (store.hip fn_pack_kernel), enqueued on the back stream: the ranks all-gather the descriptors
+// there and hdrf_gx_alloc_scan_dev composes them, with no host round trip.
+extern "C" int hdrf_gx_flush_fn_dev(hdrf_ctx *ctx, void *dev_desc)
+{
+    HDRF_LOCK(ctx);
+    if (int rc = gx_check(ctx, 2)) return rc;
+    if (!dev_desc) return set_err(ctx, HDRF_E_INVAL, "null descriptor buffer");
+    Slot &S = gx_back_slot(ctx);
+    hipStream_t st = ctx->stB;
+    const int nt = ctx->cfg.n_thread;
+    const int64_t kcap = (int64_t)ctx->max_batch * ctx->cap_blk + 1;
+    const uint64_t o_fr = 64 * 4 * sizeof(FnBlock), o_k = o_fr + 256, o_out = o_k + 256;
+    gx_mark(ctx, ctx->gx_nback, kG5, st);
+    uint8_t *F = nullptr;
+    if (int rc = gx_flush_rows(ctx, S, S.d_err, &F)) return rc;
+    HIPCK(launch_fn_pack(nt, (const FnRange *)(F + o_fr), (const uint64_t *)(F + o_out), kcap,
+                         (const unsigned long long *)(F + o_k), ctx->fn_mcap, dev_desc, S.d_err, st));
+    gx_mark(ctx, ctx->gx_nback, kG6, st);
+    return 0;
 }
 
 // one rank's flush function applied to the allocator A (the walk of store.hip flush_kernel)
@@ -2269,40 +2477,121 @@ extern "C" int hdrf_gx_alloc_scan(hdrf_ctx *ctx, const int64_t *descs, const int
     return 0;
 }
 
-extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts)
+// The same composition on the device over the all-gathered descriptors (G x fn_bytes, rank order):
+// the node's allocator after the previous batch (on the device already) -> this rank's incoming
+// state for hdrf_gx_flush(ctx, NULL, NULL), its predicted result (checked by hdrf_gx_place) and the
+// node's state after the batch (installed by hdrf_gx_place).  Enqueued on the back stream.
+extern "C" int hdrf_gx_alloc_scan_dev(hdrf_ctx *ctx, const void *dev_descs)
+{
+    HDRF_LOCK(ctx);
+    if (int rc = gx_check(ctx, 2)) return rc;
+    if (!dev_descs) return set_err(ctx, HDRF_E_INVAL, "null descriptors");
+    Slot &S = gx_back_slot(ctx);
+    hipStream_t st = ctx->stB;
+    gx_mark(ctx, ctx->gx_nback, kG7, st);
+    HIPCK(launch_gx_scan(dev_descs, ctx->fn_bytes, ctx->G, ctx->cfg.rank, ctx->cfg.n_thread,
+                         (uint32_t)(ctx->cfg.arena_slots / 4), ctx->cfg.container_max, ctx->d_alloc, ctx->d_gxst,
+                         S.d_err, st));
+    gx_mark(ctx, ctx->gx_nback, kG8, st);
+    ctx->gx_dscan = 1;
+    ctx->gx_scanned = 0;
+    return 0;
+}
+
+// Placement of the back batch: on stream B the per-chunk container positions, the X3 location
+// records and the read-back the host needs (hdrf_gx_place_wait); the arena copy of the new chunks
+// runs on stream B2 (compressor 2 keeps it on B: its LZ4 pass reads the containers there).
+extern "C" int hdrf_gx_place_launch(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send)
 {
     HDRF_LOCK(ctx);
     if (int rc = gx_check(ctx, 3)) return rc;
-    const int si = (int)(ctx->gx_nback % 2);
+    if (ctx->gx_place_pending) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_place_launch: a placement is pending");
+    const int si = gx_back_si(ctx);
     Slot &S = ctx->sl[si];
-    if (!x3_send || !send_counts) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    if (!x3_send) return set_err(ctx, HDRF_E_INVAL, "null exchange buffer");
+    if (!alloc_final && !ctx->gx_dscan)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_place: the node's allocator (alloc_final) is needed without the device scan");
     hipStream_t st = ctx->stB;
+    const uint64_t seq = ctx->gx_nback;
     const int nb = S.nblocks;
     const StoreParams P = store_params(ctx, nb);
+    const bool split = ctx->cfg.compressor != 2;
     GxPlace gx;
     gx.x2 = ctx->gx_x2; gx.x3 = x3_send; gx.cap = ctx->gx_cap; gx.counts = ctx->d_gx_counts; gx.G = ctx->G;
+    gx.part = split ? 1 : 0;
+    gx_mark(ctx, seq, kG10, st);
     HIPCK(launch_store_place(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_pre, S.d_rstate, S.d_ev, S.d_slot,
                              ctx->d_scratch[si], ctx->d_arena, S.d_pcid, S.d_ppos, gx, st));
-    // the flush walk's own result, checked against the scan's prediction after the sync below
-    AllocState got{};
-    if (ctx->gx_scanned) HIPCK(hipMemcpyAsync(&got, ctx->d_alloc, sizeof got, hipMemcpyDeviceToHost, st));
-    // the node's allocator after the last rank (the next batch and the "blockID" view start here)
-    if (alloc_final) HIPCK(hipMemcpyAsync(ctx->d_alloc, alloc_final, sizeof(AllocState), hipMemcpyHostToDevice, st));
-    std::vector<unsigned long long> cnt(ctx->G), x3e(ctx->G);
-    HIPCK(hipMemcpyAsync(cnt.data(), ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
-    HIPCK(hipMemcpyAsync(x3e.data(), ctx->d_gx_x3exp, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    // the flush walk's result (checked against the scan), then the node's allocator after the batch
+    // (the next batch and the "blockID" view start from it)
+    HIPCK(hipMemcpyAsync(ctx->d_gxst + 3, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToDevice, st));
+    if (alloc_final) {
+        std::memcpy(&S.h_gx->st[2], alloc_final, sizeof(AllocState));
+        HIPCK(hipMemcpyAsync(ctx->d_alloc, &S.h_gx->st[2], sizeof(AllocState), hipMemcpyHostToDevice, st));
+    } else {
+        HIPCK(hipMemcpyAsync(ctx->d_alloc, ctx->d_gxst + 2, sizeof(AllocState), hipMemcpyDeviceToDevice, st));
+    }
+    GxHost *h = S.h_gx;
+    HIPCK(hipMemcpyAsync(h->c3, ctx->d_gx_counts, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(h->x3e, ctx->d_gx_x3exp, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(h->x3want, ctx->d_x3want, sizeof(unsigned long long) * ctx->G, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&h->commit_err, ctx->d_gx_err, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (ctx->gx_dscan) HIPCK(hipMemcpyAsync(h->st, ctx->d_gxst, 2 * sizeof(AllocState), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(&h->st[3], ctx->d_gxst + 3, sizeof(AllocState), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_bst, S.d_bst, sizeof(BlockState) * nb, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_store, S.d_store, sizeof(uint64_t) * nb, hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_alloc, ctx->d_alloc, sizeof(AllocState), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_err, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_nclosed, S.d_nclosed, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     HIPCK(hipMemcpyAsync(S.h_closed, S.d_closed, sizeof(ClosedRec) * ctx->closed_cap, hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
-    if (ctx->gx_scanned) {
-        ctx->gx_scanned = 0;
-        if (std::memcmp(&got, &ctx->gx_expect, sizeof got) != 0)
+    gx_mark(ctx, seq, kG11, st);
+    HIPCK(hipEventRecord(S.gx_meta, st));
+    if (split) {                                        // the arena copy beside the next batch's owner phases
+        hipStream_t B2 = ctx->stB2;
+        HIPCK(hipStreamWaitEvent(B2, S.gx_meta, 0));
+        gx.part = 2;
+        gx_mark(ctx, seq, kP0, B2);
+        HIPCK(launch_store_place(P, S.d_blocks, S.d_bst, S.d_off, S.d_flags, S.d_pre, S.d_rstate, S.d_ev, S.d_slot,
+                                 ctx->d_scratch[si], ctx->d_arena, S.d_pcid, S.d_ppos, gx, B2));
+        gx_mark(ctx, seq, kP1, B2);
+        HIPCK(hipEventRecord(S.placed, B2));
+        S.gx_split = true;
+    }
+    ctx->gx_place_pending = true;
+    return 0;
+}
+
+// Wait for the placement's read-back: this rank's X3 send counts (send_counts[G]), the checks of
+// the allocator scan and of the X3 counts, and the host bookkeeping of the batch.
+extern "C" int hdrf_gx_place_wait(hdrf_ctx *ctx, int64_t *send_counts)
+{
+    HDRF_LOCK(ctx);
+    if (int rc = gx_check(ctx, 3)) return rc;
+    if (!ctx->gx_place_pending) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_place_wait: no placement launched");
+    if (!send_counts) return set_err(ctx, HDRF_E_INVAL, "null counts");
+    const int si = gx_back_si(ctx);
+    Slot &S = ctx->sl[si];
+    GxHost *h = S.h_gx;
+    HIPCK(hipEventSynchronize(S.gx_meta));
+    ctx->gx_place_pending = false;
+    if (h->commit_err) {                               // an earlier batch's commit (not waited for)
+        HIPCK(hipMemsetAsync(ctx->d_gx_err, 0, sizeof(int), ctx->stB));
+        HIPCK(hipStreamSynchronize(ctx->stB));
+        const int e = h->commit_err;
+        h->commit_err = 0;
+        return device_error(ctx, e);
+    }
+    if (ctx->gx_dscan) {
+        ctx->gx_ain = h->st[0];
+        ctx->gx_aout = h->st[3];
+        if (!*S.h_err && std::memcmp(&h->st[3], &h->st[1], sizeof(AllocState)) != 0)
+            return set_err(ctx, HDRF_E_DEVICE, "device allocator scan disagrees with this rank's flush walk");
+    } else if (ctx->gx_scanned) {
+        if (std::memcmp(&h->st[3], &ctx->gx_expect, sizeof(AllocState)) != 0)
             return set_err(ctx, HDRF_E_DEVICE, "allocator scan disagrees with this rank's flush walk");
     }
+    ctx->gx_scanned = 0;
+    ctx->gx_dscan = 0;
     // the open containers this rank's flush walk started and ended in hold its placed chunks even
     // when another rank closes them (the node read, hdrf_gx_read_fill, gathers from them)
     for (const AllocState *a : {&ctx->gx_ain, &ctx->gx_aout})
@@ -2310,10 +2599,24 @@ extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t
             if (a->exists[t] && !ctx->containers.count(a->id[t])) note_container(ctx, a->id[t], a->slot[t], a->cur[t], 0);
     S.gx_compressed = false;
     if (int rc = complete_slot(ctx, si, false)) return rc;
-    for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)cnt[d];
-    ctx->gx_x3recv.assign(x3e.begin(), x3e.end());
+    for (int d = 0; d < ctx->G; d++)
+        if (h->c3[d] != h->x3want[d])
+            return set_err(ctx, HDRF_E_DEVICE, "X3 send count to rank " + std::to_string(d) + " (" +
+                                                   std::to_string(h->c3[d]) + ") disagrees with its X2 answers (" +
+                                                   std::to_string(h->x3want[d]) + ")");
+    for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)h->c3[d];
+    ctx->gx_x3recv.assign(h->x3e, h->x3e + ctx->G);
     ctx->gx_bphase = 4;
+    gx_collect(ctx, false, ctx->gx_nback);
     return 0;
+}
+
+extern "C" int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts)
+{
+    HDRF_LOCK(ctx);
+    if (!send_counts) return ctx ? set_err(ctx, HDRF_E_INVAL, "null exchange buffer") : HDRF_E_INVAL;
+    if (int rc = hdrf_gx_place_launch(ctx, alloc_final, x3_send)) return rc;
+    return hdrf_gx_place_wait(ctx, send_counts);
 }
 
 // The X3 receive counts this owner's decisions imply (valid from hdrf_gx_place to hdrf_gx_commit):
@@ -2337,7 +2640,8 @@ extern "C" int hdrf_gx_alloc_io(hdrf_ctx *ctx, uint8_t *alloc_in, uint8_t *alloc
 {
     HDRF_LOCK(ctx);
     if (!ctx || ctx->G < 2 || !alloc_in || !alloc_out) return ctx ? set_err(ctx, HDRF_E_INVAL, "bad arguments") : HDRF_E_INVAL;
-    if (ctx->gx_bphase != 3 && ctx->gx_bphase != 4) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_alloc_io after hdrf_gx_flush");
+    if (ctx->gx_bphase != 4 && !(ctx->gx_bphase == 3 && !ctx->gx_place_pending && !ctx->gx_dscan))
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_alloc_io after hdrf_gx_flush (or hdrf_gx_place with the device scan)");
     std::memset(alloc_in, 0, HDRF_ALLOC_STATE_BYTES);
     std::memcpy(alloc_in, &ctx->gx_ain, sizeof(AllocState));
     std::memset(alloc_out, 0, HDRF_ALLOC_STATE_BYTES);
@@ -2349,11 +2653,16 @@ extern "C" int hdrf_gx_piece(hdrf_ctx *ctx, uint32_t id, uint64_t off, uint64_t 
 {
     HDRF_LOCK(ctx);
     if (!ctx || ctx->G < 2 || (n && !dev)) return ctx ? set_err(ctx, HDRF_E_INVAL, "bad arguments") : HDRF_E_INVAL;
+    if (write && ctx->cfg.compressor != 2)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_piece: writes are the compressor-2 head-piece gather only");
     auto it = ctx->containers.find(id);
     if (it == ctx->containers.end()) return set_err(ctx, HDRF_E_NOTFOUND, "container not resident on this rank");
     if (off > ctx->cfg.container_max || n > ctx->cfg.container_max - off) return set_err(ctx, HDRF_E_INVAL, "piece outside the container");
     uint8_t *p = ctx->d_arena + (size_t)it->second.slot * ctx->cfg.container_max + off;
     if (n) {
+        // (an arena copy of this rank's place on stream B2 must have landed before a read)
+        for (auto &S : ctx->sl)
+            if (S.gx_inuse && S.gx_split) HIPCK(hipStreamWaitEvent(ctx->stB, S.placed, 0));
         HIPCK(hipMemcpyAsync(write ? (void *)p : dev, write ? (const void *)dev : (const void *)p, n, hipMemcpyDeviceToDevice,
                              ctx->stB));
         // a read hands the bytes to the caller (who ships them to the closer): complete on return; a
@@ -2378,7 +2687,7 @@ extern "C" int hdrf_gx_compress(hdrf_ctx *ctx)
         HIPCK(hipStreamSynchronize(ctx->stB));
         return 0;
     }
-    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    Slot &S = gx_back_slot(ctx);
     const uint32_t nclosed = *S.h_nclosed;
     if (!nclosed || S.gx_compressed) {                  // once per batch: a second call changes nothing
         HIPCK(hipStreamSynchronize(ctx->stB));         // (hdrf_gx_piece writes are complete on return)
@@ -2400,6 +2709,8 @@ extern "C" int hdrf_gx_compress(hdrf_ctx *ctx)
     return (int)nclosed;
 }
 
+// The owners' commit of the X3 locations: enqueued on the back stream and not waited for (an
+// error it raises is reported by the next hdrf_gx_place or by hdrf_gx_sync).
 extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts)
 {
     HDRF_LOCK(ctx);
@@ -2411,23 +2722,37 @@ extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int6
             return set_err(ctx, HDRF_E_DEVICE, "X3 receive count from rank " + std::to_string(s) +
                                                    " disagrees with this owner's decisions");
     }
-    Slot &S = ctx->sl[ctx->gx_nback % 2];
+    Slot &S = gx_back_slot(ctx);
     // compressor 2: the containers this rank closed must be Lz4Codec files before the batch commits
     // (container reads of closed containers take their bytes from the compressed arena)
     if (ctx->cfg.compressor == 2 && *S.h_nclosed && !S.gx_compressed)
         return set_err(ctx, HDRF_E_INVAL, "compressor 2: hdrf_gx_compress must run between hdrf_gx_place and hdrf_gx_commit");
     hipStream_t st = ctx->stB;
-    HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, recv_counts, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
+    const uint64_t seq = ctx->gx_nback;
+    std::memcpy(S.h_gx->up_r3, recv_counts, sizeof(int64_t) * ctx->G);
+    gx_mark(ctx, seq, kG12, st);
+    HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, S.h_gx->up_r3, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
     HIPCK(launch_gx_commit(x3_recv, ctx->d_gx_rcounts, max_count(recv_counts, ctx->G), ctx->gx_cap, ctx->G, ctx->d_tab,
-                           ctx->cfg.index_log2, S.d_err, st));
-    int herr = 0;
-    HIPCK(hipMemcpyAsync(&herr, S.d_err, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCK(hipStreamSynchronize(st));
+                           ctx->cfg.index_log2, ctx->d_gx_err, st));
+    gx_mark(ctx, seq, kG13, st);
+    HIPCK(hipEventRecord(S.back_done, st));
     ctx->gx_bphase = 0;
     ctx->gx_nback++;
+    return 0;
+}
+
+// Complete every node-global batch in flight (all streams) and report an error of the last commits.
+extern "C" int hdrf_gx_sync(hdrf_ctx *ctx)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
+    if (int rc = drain(ctx)) return rc;
+    int herr = 0;
+    HIPCK(hipMemcpy(&herr, ctx->d_gx_err, sizeof(int), hipMemcpyDeviceToHost));
+    gx_collect(ctx, true, ctx->gx_nback);
     if (herr) {
-        HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), st));
-        HIPCK(hipStreamSynchronize(st));
+        HIPCK(hipMemset(ctx->d_gx_err, 0, sizeof(int)));
         return device_error(ctx, herr);
     }
     return 0;

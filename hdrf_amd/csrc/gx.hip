@@ -275,6 +275,31 @@ __global__ void __launch_bounds__(256) gx_decide_kernel(const BlockState *__rest
         tilesum[(size_t)b * ntiles + blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
 }
 
+// ---- source: X3 records this rank must send each owner = the responses "created, holds the
+// minimum" it received (one designated chunk per such record emits one location).  place_kernel's
+// own counts are checked against these, so a sender whose X3 counts disagree with the owners' X2
+// answers (which the owners count for their receive side, own_decide) fails at hdrf_gx_place.
+// grid (ceil(max sent / 256), G)
+__global__ void __launch_bounds__(256) gx_x3want_kernel(const uint32_t *__restrict__ x2,
+                                                        const unsigned long long *__restrict__ sent, int64_t cap,
+                                                        unsigned long long *__restrict__ want)
+{
+    const int d = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool ok = i < (int64_t)sent[d] && (x2[2 * ((size_t)d * cap + i) + 1] & 3u) == 3u;
+    const unsigned long long m = ballot64(ok);
+    if (lane_id() == 0 && m) atomicAdd(want + d, (unsigned long long)__popcll(m));
+}
+
+hipError_t launch_gx_x3want(const uint32_t *x2, const unsigned long long *sent, int64_t max_sent, int64_t cap, int G,
+                            unsigned long long *want, hipStream_t st)
+{
+    if (hipError_t e = hipMemsetAsync(want, 0, sizeof(unsigned long long) * G, st)) return e;
+    hipLaunchKernelGGL(gx_x3want_kernel, dim3(std::max<int64_t>(1, (max_sent + 255) / 256), G), dim3(256), 0, st, x2,
+                       sent, cap, want);
+    return hipGetLastError();
+}
+
 // ---- owner: commit locations of entries created this batch (X3) ---------------------------
 __global__ void __launch_bounds__(256) own_commit_kernel(const uint32_t *__restrict__ x3, const int64_t *__restrict__ counts,
                                                          int64_t cap, IndexEntry *__restrict__ tab, uint64_t tab_n,

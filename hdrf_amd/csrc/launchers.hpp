@@ -6,7 +6,10 @@ namespace hdrf {
 
 // Stage markers: when timing is on, a HIP event is recorded on the launch stream at every
 // stage boundary (kernels of one stream run in order, so event deltas are kernel times).
-constexpr int kNumStages = 12;  // walk, stitch, sha, (unused), claim, apply, slow+decide, scan, flush, place, compress, gmax
+// walk, stitch, sha, (unused), claim, apply, slow+decide, scan, flush, place, compress, gmax, then the
+// node-global phases: local aggregation, owner, decide, flush function, allocator scan, placement,
+// commit, and the X1 / X2 / descriptor all-gather / X3 exchanges (api.hip gx_collect)
+constexpr int kNumStages = 23;
 struct Marker {
     hipEvent_t *ev = nullptr;   // kNumStages + 1 events
     int next = 0;
@@ -85,7 +88,27 @@ struct GxPlace {
     int64_t cap = 0;
     unsigned long long *counts = nullptr;  // [G]
     int G = 1;
+    int part = 0;                          // 0 the whole place pass; 1 placement + index/X3 writes only
+                                           // (no arena copy); 2 the arena copy only (node-global split)
 };
+// Node-global allocator scan on the device (store.hip): this rank's flush function packed into a
+// fixed-size descriptor (gx_fn_bytes), and the composition of every rank's descriptor (rank order)
+// from the node's allocator after the previous batch.
+struct GxFnHead {            // descriptor header (the rows follow, per range t: mcap x GxFnRow)
+    uint64_t n_thread, mcap;
+    uint64_t any[4], S[4], base_last[4], S_last[4], m[4];
+};
+struct GxFnRow {             // first close point v (stream prefix), fill after the batch S - cs, closes - 1
+    uint32_t v, cur, n, pad;
+};
+uint64_t gx_fn_mcap(uint32_t cmax, int window, int max_batch);
+uint64_t gx_fn_bytes(uint32_t cmax, int window, int max_batch);
+hipError_t launch_fn_pack(int n_thread, const FnRange *fr, const uint64_t *rows, int64_t kcap,
+                          const unsigned long long *K, uint64_t mcap, void *desc, int *err, hipStream_t st);
+// states[0] = this rank's allocator in, [1] its predicted flush result, [2] the node's after the batch;
+// `alloc` (the node's state after the previous batch) becomes states[0]
+hipError_t launch_gx_scan(const void *descs, uint64_t fn_bytes, int G, int rank, int n_thread, uint32_t per,
+                          uint32_t cmax, AllocState *alloc, AllocState *states, int *err, hipStream_t st);
 
 hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const BlockState *bst,
                         const uint32_t *offsets, const uint8_t *flags, const uint32_t *tilesum, uint32_t *tilepre,
@@ -122,6 +145,8 @@ hipError_t launch_gx_owner(int hasher, const uint32_t *x1, const int64_t *counts
 hipError_t launch_gx_decide(const BlockState *bst, int nblocks, int cap_blk, int ntiles, const uint32_t *offsets,
                             const IndexEntry *scratch, const uint32_t *slot, const uint32_t *x2, uint8_t *flags,
                             uint32_t *tilesum, hipStream_t st);
+hipError_t launch_gx_x3want(const uint32_t *x2, const unsigned long long *sent, int64_t max_sent, int64_t cap, int G,
+                            unsigned long long *want, hipStream_t st);
 hipError_t launch_gx_commit(const uint32_t *x3, const int64_t *counts, int64_t max_count, int64_t cap, int G,
                             IndexEntry *tab, int log2cap, int *err, hipStream_t st);
 // recipes (storeDB): a batch's digests copied into the device recipe store

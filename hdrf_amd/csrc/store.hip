@@ -272,7 +272,7 @@ __global__ void __launch_bounds__(256) fn_chain_kernel(StoreParams P, const uint
         w = sb[b].off + (c > sb[b].c0 ? (uint64_t)(pb[c - 1] - sb[b].base) : 0ull);
     }
     if (v > (uint64_t)P.cmax) return;
-    if (i >= kcap) { atomicOr(err, 64); return; }
+    if (i >= kcap) { atomicOr(err, 1024); return; }
     atomicMax(K + t, (unsigned long long)(i + 1));
     uint64_t *o = out + ((size_t)t * kcap + i) * 3;
     o[0] = v;
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(256) fn_chain_kernel(StoreParams P, const uint
         int b = -1;                                    // first active block ending past thr
         for (int q = 0; q < nb && b < 0; q++)
             if (sb[q].act && (int64_t)(sb[q].off + sb[q].S) > thr) b = q;
-        if (b < 0 || n > (uint64_t)P.ev_cap * 64) { atomicOr(err, 64); return; }
+        if (b < 0 || n > (uint64_t)P.ev_cap * 64) { atomicOr(err, 1024); return; }
         const uint32_t *pb = pre + (size_t)b * P.cap_blk;
         const uint64_t lim = (uint64_t)(thr - (int64_t)sb[b].off) + sb[b].base;   // first pb[c] > lim
         uint32_t lo = sb[b].c0, hi = sb[b].c1;
@@ -297,6 +297,139 @@ __global__ void __launch_bounds__(256) fn_chain_kernel(StoreParams P, const uint
     }
     o[1] = (uint64_t)cs;
     o[2] = n;
+}
+
+// ---- the flush function as a fixed-size descriptor (node-global allocator scan on the device) ----
+// fn_chain leaves K[t] candidate rows per range, rows that repeat the previous prefix flagged; the
+// distinct prefixes v <= cmax are at most cmax / (window + 2) + nblocks + 1 (every chunk is >= window
+// + 2 bytes except a block's last), so the packed descriptor has a fixed size and ranks exchange it
+// with one all-gather of equal parts.  grid n_thread x 256
+uint64_t gx_fn_mcap(uint32_t cmax, int window, int max_batch)
+{
+    return (uint64_t)cmax / (uint64_t)(window + 2) + (uint64_t)max_batch + 2;
+}
+uint64_t gx_fn_bytes(uint32_t cmax, int window, int max_batch)
+{
+    return (sizeof(GxFnHead) + 4 * gx_fn_mcap(cmax, window, max_batch) * sizeof(GxFnRow) + 255) & ~(uint64_t)255;
+}
+
+__global__ void __launch_bounds__(256) fn_pack_kernel(int n_thread, const FnRange *__restrict__ fr,
+                                                      const uint64_t *__restrict__ rows, int64_t kcap,
+                                                      const unsigned long long *__restrict__ K, uint64_t mcap,
+                                                      uint8_t *__restrict__ desc, int *__restrict__ err)
+{
+    __shared__ uint32_t s_w[4];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    GxFnHead *h = (GxFnHead *)desc;
+    GxFnRow *out = (GxFnRow *)(desc + sizeof(GxFnHead)) + (size_t)t * mcap;
+    const FnRange R = fr[t];
+    const uint64_t k = K[t];
+    uint32_t m = 0;
+    for (uint64_t base = 0; base < k; base += 256) {
+        const uint64_t i = base + tid;
+        const uint64_t *r = rows + ((size_t)t * kcap + i) * 3;
+        const bool keep = i < k && !(r[2] >> 63);
+        const uint32_t incl = wave_incl_scan(keep ? 1u : 0u);
+        if (lane_id() == 63) s_w[tid >> 6] = incl;
+        __syncthreads();
+        uint32_t off = m;
+        for (int w = 0; w < (tid >> 6); w++) off += s_w[w];
+        const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (keep) {
+            const uint64_t j = off + incl - 1;
+            if (j < mcap) {
+                GxFnRow row;
+                row.v = (uint32_t)r[0];
+                row.cur = (uint32_t)(R.S - r[1]);               // S - cs <= cmax
+                row.n = (uint32_t)r[2];
+                row.pad = 0;
+                out[j] = row;
+            } else {
+                atomicOr(err, 1024);
+            }
+        }
+        m += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        if (t == 0) { h->n_thread = (uint64_t)n_thread; h->mcap = mcap; }
+        h->any[t] = R.any; h->S[t] = R.S; h->base_last[t] = R.base_last; h->S_last[t] = R.S_last;
+        h->m[t] = m;
+        if (R.any && (m == 0 || out[0].v != 0)) atomicOr(err, 1024);   // the first candidate is v = 0
+    }
+}
+
+hipError_t launch_fn_pack(int n_thread, const FnRange *fr, const uint64_t *rows, int64_t kcap,
+                          const unsigned long long *K, uint64_t mcap, void *desc, int *err, hipStream_t st)
+{
+    hipLaunchKernelGGL(fn_pack_kernel, dim3(n_thread), dim3(256), 0, st, n_thread, fr, rows, kcap, K, mcap,
+                       (uint8_t *)desc, err);
+    return hipGetLastError();
+}
+
+// The node's allocator through every rank's flush function, rank order (api.hip gx_apply_fn on the
+// device): lane t < n_thread evaluates range t, the ranges are independent.  One wave.
+__global__ void __launch_bounds__(64) gx_scan_kernel(const uint8_t *__restrict__ descs, uint64_t fn_bytes, int G,
+                                                     int rank, int n_thread, uint32_t per, uint32_t cmax,
+                                                     AllocState *__restrict__ alloc, AllocState *__restrict__ states,
+                                                     int *__restrict__ err)
+{
+    const int t = lane_id();
+    __shared__ AllocState sA;
+    if (t == 0) sA = *alloc;
+    __syncthreads();
+    for (int r = 0; r < G; r++) {
+        if (r == rank && t == 0) states[0] = sA;
+        __syncthreads();
+        const GxFnHead *h = (const GxFnHead *)(descs + (size_t)r * fn_bytes);
+        const GxFnRow *rows = (const GxFnRow *)(descs + (size_t)r * fn_bytes + sizeof(GxFnHead));
+        if (t == 0 && (h->n_thread != (uint64_t)n_thread || sizeof(GxFnHead) + 4 * h->mcap * sizeof(GxFnRow) > fn_bytes))
+            atomicOr(err, 512);
+        if (t < n_thread && h->n_thread == (uint64_t)n_thread && h->any[t]) {
+            const uint64_t m = h->m[t], S = h->S[t];
+            const GxFnRow *v = rows + (size_t)t * h->mcap;
+            const int64_t x = sA.exists[t] ? (int64_t)sA.cur[t] : 0;
+            int64_t cs = -x, n = 0;
+            uint32_t cur = (uint32_t)((int64_t)S + x);
+            if (x + (int64_t)S > (int64_t)cmax) {
+                if (m == 0 || m > h->mcap) {
+                    atomicOr(err, 512);
+                } else {
+                    const uint64_t thr = (uint64_t)((int64_t)cmax - x);   // largest v <= thr (v_0 = 0)
+                    uint64_t lo = 0, hi = m;
+                    while (hi - lo > 1) {
+                        const uint64_t mid = (lo + hi) >> 1;
+                        if ((uint64_t)v[mid].v <= thr) lo = mid; else hi = mid;
+                    }
+                    cur = v[lo].cur;
+                    cs = (int64_t)S - (int64_t)cur;
+                    n = 1 + (int64_t)v[lo].n;
+                }
+            }
+            const uint32_t base = (uint32_t)t * per;
+            sA.id[t] += (uint32_t)n;
+            sA.slot[t] = base + (uint32_t)(((int64_t)(sA.slot[t] - base) + n) % per);
+            sA.cur[t] = cur;
+            sA.exists[t] = 1;
+            const int64_t bl = (int64_t)h->base_last[t];
+            sA.pos[t] = (uint32_t)((int64_t)h->S_last[t] - (cs - bl > 0 ? cs - bl : 0));
+        }
+        __syncthreads();
+        if (r == rank && t == 0) states[1] = sA;
+        __syncthreads();
+    }
+    if (t == 0) {
+        states[2] = sA;
+        *alloc = states[0];                                  // the flush walk starts from this rank's state
+    }
+}
+
+hipError_t launch_gx_scan(const void *descs, uint64_t fn_bytes, int G, int rank, int n_thread, uint32_t per,
+                          uint32_t cmax, AllocState *alloc, AllocState *states, int *err, hipStream_t st)
+{
+    hipLaunchKernelGGL(gx_scan_kernel, dim3(1), dim3(64), 0, st, (const uint8_t *)descs, fn_bytes, G, rank, n_thread,
+                       per, cmax, alloc, states, err);
+    return hipGetLastError();
 }
 
 // workgroup-cooperative copy of one contiguous run (16-B aligned destination stores)
@@ -382,9 +515,12 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
                 pos = (uint32_t)((int64_t)X0 - cs);
                 do_copy = len > 0;
             }
-            place_cid[c] = cid;
-            place_pos[c] = pos;
+            if (gx.part != 2) {
+                place_cid[c] = cid;
+                place_pos[c] = pos;
+            }
         }
+        if (gx.part != 2) {                                // (the copy part: part 1 wrote the index)
         bool desig = (f & 2) != 0;                         // in the entry's min block ...
         IndexEntry *e = tab + slot[c];
         if (dcnt) desig = (f & 32) != 0;                   // (idx_finalize already decided and cleared)
@@ -412,7 +548,9 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
                 e->first = 0;
             }
         }
+        }
     }
+    if (gx.part == 1) return;                              // placement part: no arena copy
     // ---- runs: consecutive new chunks of this tile that are contiguous in one container are
     //      one contiguous source span and one contiguous destination span -> one copy each
     __shared__ uint32_t s_cid[256], s_pend[256], s_flag[256];
@@ -492,7 +630,7 @@ hipError_t launch_store_place(const StoreParams &P, const BlockDesc *d_blocks, c
                               uint8_t *arena, uint32_t *place_cid, uint32_t *place_pos, const GxPlace &gx,
                               hipStream_t st, const uint8_t *dcnt)
 {
-    if (gx.x3)
+    if (gx.x3 && gx.part != 2)
         if (hipError_t e = hipMemsetAsync(gx.counts, 0, sizeof(unsigned long long) * gx.G, st)) return e;
     if (stream_knobs() & 2)
         hipLaunchKernelGGL(place_kernel<true>, dim3(P.ntiles, P.nblocks), dim3(256), P.place_lds, st, P, d_blocks, bst,

@@ -34,7 +34,8 @@ EXPORTS = [
     "hdrf_drain_containers", "hdrf_ticket_take", "hdrf_ticket_cancel", "hdrf_reduce_block_ticketed",
     "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot", "hdrf_submit_slots", "hdrf_rx_cancel",
     "hdrf_gx_read_locate", "hdrf_gx_read_fill", "hdrf_gx_flush_fn", "hdrf_gx_alloc_scan",
-    "hdrf_set_lzop_mtime",
+    "hdrf_set_lzop_mtime", "hdrf_gx_flush_fn_dev", "hdrf_gx_alloc_scan_dev", "hdrf_gx_place_launch",
+    "hdrf_gx_place_wait", "hdrf_gx_sync",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -45,7 +46,13 @@ PIPELINE_DEPTH = 5          # HDRF_PIPELINE_DEPTH: batches in flight
 STAGES = ["walk(lane_walk_kernel)", "stitch(repair/path/count/scan/copy/fallback)", "sha(sha_chunk_kernel)",
           "sha_tail(none: padding inside the sha kernel)", "index_claim(idx_claim_kernel)", "index_apply(idx_apply_kernel)",
           "index_slow_decide(idx_slow/decide)", "scan(tile/chunk_scan)", "flush(flush_kernel)",
-          "place(place_kernel)", "compress(lz4_seg/lz4_pack)", "gmax(gmax_kernel)"]
+          "place(place_kernel)", "compress(lz4_seg/lz4_pack)", "gmax(gmax_kernel)",
+          # node-global contexts (hdrf_gx_*): the front's local aggregation, the back phases and the
+          # gaps on the back stream the caller's exchanges fill (X1 includes the host's turn-around)
+          "gx_local(scratch claim/apply/decide + gx_emit)", "gx_owner(own_claim..own_finish)",
+          "gx_decide(gx_decide + x3want)", "gx_flush_fn(fn_info/fn_chain/fn_pack)", "gx_alloc_scan(gx_scan_kernel)",
+          "gx_place_meta(place_kernel part 1)", "gx_commit(own_commit)", "gx_x1(X1 all-to-all + host)",
+          "gx_x2(X2 all-to-all)", "gx_allgather(flush descriptors)", "gx_x3(X3 all-to-all + host)"]
 
 
 class HdrfError(RuntimeError):
@@ -78,7 +85,7 @@ class Stats(ctypes.Structure):
 
 class GxLayout(ctypes.Structure):
     _fields_ = [("cap", ctypes.c_int64), ("x1_words", ctypes.c_int32), ("x2_words", ctypes.c_int32),
-                ("x3_words", ctypes.c_int32)]
+                ("x3_words", ctypes.c_int32), ("depth", ctypes.c_int32), ("fn_bytes", ctypes.c_int64)]
 
 
 class BlockResult(ctypes.Structure):
@@ -203,6 +210,11 @@ def load():
         "hdrf_gx_alloc_io": (ctypes.c_int, [_vp, _u8p, _u8p]),
         "hdrf_gx_piece": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_int32]),
         "hdrf_gx_compress": (ctypes.c_int, [_vp]),
+        "hdrf_gx_flush_fn_dev": (ctypes.c_int, [_vp, _vp]),
+        "hdrf_gx_alloc_scan_dev": (ctypes.c_int, [_vp, _vp]),
+        "hdrf_gx_place_launch": (ctypes.c_int, [_vp, _u8p, _vp]),
+        "hdrf_gx_place_wait": (ctypes.c_int, [_vp, _i64p]),
+        "hdrf_gx_sync": (ctypes.c_int, [_vp]),
     }
     ab_build = bool(os.environ.get("HDRF_LIB_PATH"))
     for name, (res, args) in sig.items():
@@ -694,6 +706,29 @@ class Context:
         af = None if alloc_final is None else _p(np.ascontiguousarray(alloc_final, np.uint8))
         self._ck(self.L.hdrf_gx_place(self._h, af, x3_send, _p(cnt, _i64p)))
         return cnt
+
+    def gx_place_launch(self, alloc_final, x3_send):
+        """Placement + X3 records + read-back enqueued (the arena copy on its own stream); alloc_final
+        None after gx_alloc_scan_dev.  gx_place_wait() returns the X3 send counts."""
+        self._gx_af = None if alloc_final is None else np.ascontiguousarray(alloc_final, np.uint8)
+        self._ck(self.L.hdrf_gx_place_launch(self._h, None if self._gx_af is None else _p(self._gx_af), x3_send))
+
+    def gx_place_wait(self):
+        cnt = np.zeros(self.cfg.n_ranks, np.int64)
+        self._ck(self.L.hdrf_gx_place_wait(self._h, _p(cnt, _i64p)))
+        return cnt
+
+    def gx_flush_fn_dev(self, dev_desc):
+        """This rank's flush function packed on the device into dev_desc (layout.fn_bytes)."""
+        self._ck(self.L.hdrf_gx_flush_fn_dev(self._h, dev_desc))
+
+    def gx_alloc_scan_dev(self, dev_descs):
+        """Compose every rank's descriptor (G x fn_bytes on the device, rank order) on the device."""
+        self._ck(self.L.hdrf_gx_alloc_scan_dev(self._h, dev_descs))
+
+    def gx_sync(self):
+        """Complete the node-global batches in flight; raises a commit's device error."""
+        self._ck(self.L.hdrf_gx_sync(self._h))
 
     def gx_read_locate(self, digests):
         """Node-global read, step 1: locations {cid, start, stop, placing rank + 1} of the recipe

@@ -78,6 +78,25 @@ class Exchange:
         if recv.is_cuda:
             torch.cuda.current_stream(recv.device).synchronize()
 
+    def all_gather_dev(self, send, recv):
+        """Every rank's equal-size device buffer `send` -> `recv` (G x len, rank order).  RCCL: enqueued
+        on the library's back stream (no host sync); gloo: staged through host memory."""
+        if self.nccl:
+            if self.stream is not None:
+                with torch.cuda.stream(self.stream):
+                    dist.all_gather_into_tensor(recv, send)
+                return
+            dist.all_gather_into_tensor(recv, send)
+            torch.cuda.current_stream(self.device).synchronize()
+            return
+        if send.is_cuda:
+            torch.cuda.synchronize(send.device)
+        parts = [torch.empty(send.numel(), dtype=send.dtype) for _ in range(self.G)]
+        dist.all_gather(parts, send.cpu())
+        recv.copy_(torch.cat(parts))
+        if recv.is_cuda:
+            torch.cuda.current_stream(recv.device).synchronize()
+
     def all_gather_i64(self, arr):
         """Every rank's int64 array (lengths may differ) -> list in rank order; host to host."""
         n = torch.tensor([len(arr)], dtype=torch.int64)
@@ -169,16 +188,24 @@ class NodeRank:
         self.xc = Exchange(self.G, self.rank, self.device, ext)
         lay = ctx.gx_layout()
         self.cap, self.w = int(lay.cap), (int(lay.x1_words), int(lay.x2_words), int(lay.x3_words))
+        self.depth = int(lay.depth)
         n = self.G * self.cap
         mk = lambda w: torch.empty(n * w, dtype=torch.int32, device=self.device)  # noqa: E731
-        self.x1s, self.x1r = mk(self.w[0]), mk(self.w[0])
-        self.x1s2 = mk(self.w[0])      # second X1 send buffer: the next batch's front fills it
+        # one X1 send buffer per batch in the pipeline: the fronts of the next batches fill theirs
+        self.x1sb = [mk(self.w[0]) for _ in range(self.depth)]
+        self.x1s, self.x1r = self.x1sb[0], mk(self.w[0])
         self.x2s, self.x2r = mk(self.w[1]), mk(self.w[1])
         self.x3s, self.x3r = mk(self.w[2]), mk(self.w[2])
-        self.alloc = None          # node allocator after the last batch (None: initial state)
+        # the packed flush descriptors (device allocator scan): this rank's and every rank's
+        self.fn_send = torch.zeros(int(lay.fn_bytes), dtype=torch.uint8, device=self.device)
+        self.fn_recv = torch.zeros(self.G * int(lay.fn_bytes), dtype=torch.uint8, device=self.device)
+        self.alloc = None          # node allocator after the last batch (host scan / chain; None: initial state)
         self.pieces = ContainerPieces(int(ctx.cfg.n_thread))   # compressor 2: head-piece plan
         self.phase_ms = {}         # host wall time per back phase, summed over batches
-        self.chain = os.environ.get("HDRF_NODE_CHAIN") == "1"   # A/B: the old rank-to-rank chain
+        # A/B: the rank-to-rank allocator chain (HDRF_NODE_CHAIN=1) or the host-side scan over a gloo
+        # all-gather of the descriptors (HDRF_NODE_SCAN=host); default: the device scan
+        self.chain = os.environ.get("HDRF_NODE_CHAIN") == "1"
+        self.host_scan = os.environ.get("HDRF_NODE_SCAN") == "host"
 
     def reset(self):
         self.ctx.reset()
@@ -226,73 +253,96 @@ class NodeRank:
             del held
         return n
 
+    def _tick(self, key, t0):
+        t = time.perf_counter()
+        self.phase_ms[key] = self.phase_ms.get(key, 0.0) + 1e3 * (t - t0)
+        return t
+
+    def _back_enqueue(self, c1, r1, x1s):
+        """X1 .. placement of the oldest waited batch, enqueued on the back stream (the device scan:
+        no host wait; the chain and host-scan A/B forms wait where they must)."""
+        ctx, xc, cap, (w1, w2, w3) = self.ctx, self.xc, self.cap, self.w
+        t = time.perf_counter()
+        xc.records(x1s, self.x1r, c1, r1, cap, w1)
+        ctx.gx_owner(self.x1r.data_ptr(), r1, self.x2s.data_ptr())
+        xc.records(self.x2s, self.x2r, r1, c1, cap, w2)           # responses retrace X1
+        ctx.gx_decide(self.x2r.data_ptr())
+        if self.chain:                                   # the rank-to-rank allocator chain
+            self.alloc = xc.chain_alloc(self.alloc, ctx.gx_flush)
+            ctx.gx_place_launch(self.alloc, self.x3s.data_ptr())
+        elif self.host_scan:                             # descriptors over gloo, scanned on every host
+            descs = xc.all_gather_i64(ctx.gx_flush_fn())
+            a_in, self.alloc = ctx.gx_alloc_scan(descs)
+            ctx.gx_flush(a_in, want_out=False)
+            ctx.gx_place_launch(self.alloc, self.x3s.data_ptr())
+        else:                                            # descriptors all-gathered and scanned on the device
+            ctx.gx_flush_fn_dev(self.fn_send.data_ptr())
+            xc.all_gather_dev(self.fn_send, self.fn_recv)
+            ctx.gx_alloc_scan_dev(self.fn_recv.data_ptr())
+            ctx.gx_flush(None, want_out=False)
+            ctx.gx_place_launch(None, self.x3s.data_ptr())
+        self._tick("enqueue x1..place", t)
+
+    def _back_finish(self):
+        """Wait for the placement's read-back, then X3 and the owners' commit (not waited for)."""
+        ctx, xc, cap, w3 = self.ctx, self.xc, self.cap, self.w[2]
+        t = time.perf_counter()
+        c3 = ctx.gx_place_wait()
+        t = self._tick("place wait", t)
+        if int(ctx.cfg.compressor) == 2:
+            self._compress()
+            t = self._tick("compress", t)
+        r3 = ctx.gx_x3_counts()          # implied by this owner's decisions: no count exchange
+        xc.records(self.x3s, self.x3r, c3, r3, cap, w3)
+        ctx.gx_commit(self.x3r.data_ptr(), r3)
+        self._tick("x3+commit", t)
+        self.phase_ms["batches"] = self.phase_ms.get("batches", 0) + 1
+
     def reduce_batch(self, dev_ptrs, lens, readable, block_ids, gbase):
         """Reduce this rank's blocks of one global batch; gbase = its first batch position."""
         torch.cuda.current_stream(self.device).synchronize()
         c1 = self.ctx.gx_front(dev_ptrs, lens, readable, block_ids, gbase, self.x1s.data_ptr())
-        self._back(c1, self.x1s)
-
-    def _back(self, c1, x1s):
-        """Exchanges and back phases of the batch whose front was waited (X1 counts c1)."""
-        ctx, xc, cap, (w1, w2, w3) = self.ctx, self.xc, self.cap, self.w
-        tm = self.phase_ms
-        t0 = time.perf_counter()
-        r1 = xc.counts(c1)
-        xc.records(x1s, self.x1r, c1, r1, cap, w1)
-        t1 = time.perf_counter()
-        ctx.gx_owner(self.x1r.data_ptr(), r1, self.x2s.data_ptr())
-        t2 = time.perf_counter()
-        xc.records(self.x2s, self.x2r, r1, c1, cap, w2)           # responses retrace X1
-        t3 = time.perf_counter()
-        ctx.gx_decide(self.x2r.data_ptr())
-        if self.chain:                                   # the rank-to-rank allocator chain
-            self.alloc = xc.chain_alloc(self.alloc, ctx.gx_flush)
-            ta = tb = time.perf_counter()
-        else:
-            # the allocator as an exclusive scan of the ranks' flush functions: one all-gather
-            # instead of a rank-to-rank chain (hdrf_gx_flush_fn / hdrf_gx_alloc_scan)
-            desc = ctx.gx_flush_fn()
-            ta = time.perf_counter()
-            descs = xc.all_gather_i64(desc)
-            tb = time.perf_counter()
-            a_in, self.alloc = ctx.gx_alloc_scan(descs)
-            ctx.gx_flush(a_in, want_out=False)
-        t4 = time.perf_counter()
-        c3 = ctx.gx_place(self.alloc, self.x3s.data_ptr())
-        if int(ctx.cfg.compressor) == 2:
-            self._compress()
-        t5 = time.perf_counter()
-        r3 = ctx.gx_x3_counts()          # implied by this owner's decisions: no count exchange
-        xc.records(self.x3s, self.x3r, c3, r3, cap, w3)
-        t6 = time.perf_counter()
-        ctx.gx_commit(self.x3r.data_ptr(), r3)
-        t7 = time.perf_counter()
-        for k, (a, b) in zip(("x1", "owner", "x2", "decide+flush_fn" if not self.chain else "decide+flush chain",
-                              "fn all_gather", "scan+flush", "place", "x3", "commit"),
-                             ((t0, t1), (t1, t2), (t2, t3), (t3, ta), (ta, tb), (tb, t4), (t4, t5), (t5, t6), (t6, t7))):
-            tm[k] = tm.get(k, 0.0) + 1e3 * (b - a)
-        tm["batches"] = tm.get("batches", 0) + 1
+        self._back_enqueue(c1, self.xc.counts(c1), self.x1s)
+        self._back_finish()
+        self.ctx.gx_sync()
 
     def reduce_batches(self, batches, done=None):
         """Pipelined node-global reduction of a sequence of this rank's batches
-        [(dev_ptrs, lens, readable, block_ids, gbase), ...]: the front half (chunking, SHA, local
-        aggregation) of batch k+1 runs on the GPU while batch k is exchanged and stored.
-        done(k) is called after batch k committed (its hdrf_batch_* views are valid then)."""
-        ctx = self.ctx
-        bufs = (self.x1s, self.x1s2)
+        [(dev_ptrs, lens, readable, block_ids, gbase), ...]: the fronts (chunking, SHA, local
+        aggregation) of the next `depth` - 1 batches run on the GPU while the oldest is exchanged and
+        stored.  done(k) is called after batch k's placement was waited for (its hdrf_batch_* views
+        are valid then)."""
+        ctx, xc, D = self.ctx, self.xc, self.depth
         torch.cuda.current_stream(self.device).synchronize()
-        if not batches:
+        n = len(batches)
+        if not n:
             return
-        ctx.gx_front_launch(*batches[0], bufs[0].data_ptr())
+        launched = 0
+
+        def launch():
+            nonlocal launched
+            ctx.gx_front_launch(*batches[launched], self.x1sb[launched % D].data_ptr())
+            launched += 1
+
+        while launched < min(D, n):
+            launch()
+        t = time.perf_counter()
         c1 = ctx.gx_front_wait()
-        for k in range(len(batches)):
-            if k + 1 < len(batches):
-                ctx.gx_front_launch(*batches[k + 1], bufs[(k + 1) % 2].data_ptr())
-            self._back(c1, bufs[k % 2])
+        r1 = xc.counts(c1)
+        self._tick("front wait+counts", t)
+        for k in range(n):
+            self._back_enqueue(c1, r1, self.x1sb[k % D])
+            if k + 1 < n:                                # host work while the back stream runs
+                t = time.perf_counter()
+                c1 = ctx.gx_front_wait()
+                r1 = xc.counts(c1)
+                self._tick("front wait+counts", t)
+            self._back_finish()
             if done is not None:
                 done(k)
-            if k + 1 < len(batches):
-                c1 = ctx.gx_front_wait()
+            if launched < n:                             # batch k's slot: the device waits for its back
+                launch()
+        ctx.gx_sync()
 
     def reconstruct_block(self, block_id, reader):
         """DataConstructor(blkID, recipe).data on the node (DN/DataConstructor.java:73-250,360-417):

@@ -319,7 +319,11 @@ int hdrf_corpus_fill_kind(hdrf_ctx *ctx, uint8_t *dev, const uint32_t *roots_hos
  * the streams the stages run on (cfg.timing = 1): [0] lane_walk_kernel, [1] stitch (repair / path /
  * count / scan / copy / fallback), [2] sha_full_kernel, [3] sha_tail_kernel, [4] idx_claim_kernel,
  * [5] idx_apply_kernel, [6] idx_slow+decide, [7] new-byte scans, [8] flush_kernel, [9] place_kernel,
- * [10] lz4 (compressor 2), [11] gmax_kernel (granule maxima). */
+ * [10] lz4 (compressor 2), [11] gmax_kernel (granule maxima); node-global contexts also
+ * [12] local aggregation + X1 records, [13] owner claim..finish, [14] gx_decide, [15] flush function,
+ * [16] device allocator scan, [17] placement (part 1), [18] commit, and the gaps on the back stream
+ * that the caller's exchanges fill: [19] X1 (+ the host), [20] X2, [21] descriptor all-gather,
+ * [22] X3 (+ the host); [7] / [8] / [9] are the scans, the flush walk and the arena copy. */
 int hdrf_stage_times(hdrf_ctx *ctx, double *ms, int32_t n, int32_t reset);
 /* Reduction totals since the last reset (this context's blocks): the dedup / compression ratio
  * of the node is logical_bytes / (closed_file_bytes + open_bytes [+ recipe_bytes]). */
@@ -354,6 +358,7 @@ int hdrf_reset(hdrf_ctx *ctx);
  *   hdrf_gx_decide <- X2 recv
  *   hdrf_gx_flush_fn -> this rank's flush descriptor             all-gather of the descriptors
  *   hdrf_gx_alloc_scan <- every rank's descriptor: its allocator in + the node's after the batch
+ *                     (or the device forms: hdrf_gx_flush_fn_dev / hdrf_gx_alloc_scan_dev)
  *   hdrf_gx_flush  <- alloc_in (from the scan; or, without the scan, rank r gets rank r-1's
  *                     state over a rank-to-rank chain, rank 0 the node's)
  *   hdrf_gx_place  -> X3 send (locations of new entries)     all-to-all X3 (receive counts from
@@ -366,14 +371,19 @@ typedef struct {
     int32_t x1_words;        /* u32 words per X1 record (digest words + batch position + count) */
     int32_t x2_words;        /* 2: owner slot, flags */
     int32_t x3_words;        /* 4: owner slot, container id, start, stop */
+    int32_t depth;           /* node-global batches in flight (fronts launched ahead, HDRF_GX_DEPTH) */
+    int64_t fn_bytes;        /* bytes of one rank's packed flush descriptor (hdrf_gx_flush_fn_dev) */
 } hdrf_gx_layout;
 int hdrf_gx_layout_get(hdrf_ctx *ctx, hdrf_gx_layout *out);
 int hdrf_gx_front(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                   const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send,
                   int64_t *send_counts);
-/* hdrf_gx_front split in two: launch the front half of batch k+1 (stream A, its own slot) before
- * running batch k's owner .. commit phases (stream B), then wait for its X1 send counts.  At most
- * two batches are in the node-global pipeline; the phases of a batch stay in order. */
+/* hdrf_gx_front split in two: launch the front halves of the next batches (chunking on one stream,
+ * SHA on a second, the local aggregation and X1 records on a third, each batch in its own slot)
+ * before running the oldest batch's owner .. commit phases (the back stream), then wait for the
+ * oldest launched front's X1 send counts.  At most hdrf_gx_layout.depth batches are in the
+ * node-global pipeline (launched and not committed); fronts are waited and backs run in launch
+ * order.  A slot is reused only after its previous batch's back phases finished on the device. */
 int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data, const uint64_t *len,
                          const uint64_t *readable, const uint64_t *block_ids, uint32_t gbase, uint32_t *x1_send);
 int hdrf_gx_front_wait(hdrf_ctx *ctx, int64_t *send_counts);
@@ -394,8 +404,23 @@ int hdrf_gx_alloc_scan(hdrf_ctx *ctx, const int64_t *descs, const int64_t *lens,
  * state); alloc_out receives the state after this rank's blocks (NULL after a scan: no host
  * round trip). */
 int hdrf_gx_flush(hdrf_ctx *ctx, const uint8_t *alloc_in, uint8_t *alloc_out);
-/* alloc_final: the node's state after the last rank's flush (becomes this context's state). */
+/* The allocator scan without host round trips (the back stream's order only): hdrf_gx_flush_fn_dev
+ * (after hdrf_gx_decide) writes this rank's flush function as a fixed-size descriptor of
+ * hdrf_gx_layout.fn_bytes into dev_desc; the caller all-gathers the G descriptors into dev_descs
+ * (rank order, G x fn_bytes, e.g. an RCCL all-gather enqueued on hdrf_gx_stream); then
+ * hdrf_gx_alloc_scan_dev composes them on the device from the node's allocator after the previous
+ * batch, and hdrf_gx_flush(ctx, NULL, NULL) and hdrf_gx_place(ctx, NULL, ...) use the result
+ * (hdrf_gx_place checks the flush walk against the scan's prediction). */
+int hdrf_gx_flush_fn_dev(hdrf_ctx *ctx, void *dev_desc);
+int hdrf_gx_alloc_scan_dev(hdrf_ctx *ctx, const void *dev_descs);
+/* alloc_final: the node's state after the last rank's flush (becomes this context's state; NULL
+ * after hdrf_gx_alloc_scan_dev, which computed it).  hdrf_gx_place = hdrf_gx_place_launch (placement,
+ * X3 records and their read-back on the back stream, the arena copy on a stream of its own) +
+ * hdrf_gx_place_wait (waits for the read-back: this rank's X3 send counts; the scan and the X3
+ * counts are checked, the batch's hdrf_batch_* views become valid). */
 int hdrf_gx_place(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send, int64_t *send_counts);
+int hdrf_gx_place_launch(hdrf_ctx *ctx, const uint8_t *alloc_final, uint32_t *x3_send);
+int hdrf_gx_place_wait(hdrf_ctx *ctx, int64_t *send_counts);
 /* Node-global compressor 2 (between hdrf_gx_place and hdrf_gx_commit): every rank's allocator
  * state before and after its flush walk (hdrf_gx_alloc_io, 128 B each; all-gathered by the caller,
  * they tell every rank which rank holds which bytes of each container); the head pieces of a
@@ -412,7 +437,11 @@ int hdrf_gx_compress(hdrf_ctx *ctx);
  * per entry created this batch, from the rank holding its minimum block.  Valid from hdrf_gx_place to
  * hdrf_gx_commit; hdrf_gx_commit refuses (HDRF_E_DEVICE) receive counts that differ from them. */
 int hdrf_gx_x3_counts(hdrf_ctx *ctx, int64_t *recv_counts);
+/* Enqueued on the back stream and not waited for: a device error it raises is reported by the next
+ * hdrf_gx_place or by hdrf_gx_sync. */
 int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int64_t *recv_counts);
+/* Complete every node-global batch in flight on this rank (all streams); reports a commit error. */
+int hdrf_gx_sync(hdrf_ctx *ctx);
 /* The stream the back phases (hdrf_gx_owner .. hdrf_gx_commit) run on (a hipStream_t).  A caller
  * that enqueues its X1 / X2 record exchanges on it (RCCL collectives issued on this stream,
  * torch.cuda.ExternalStream in hdrf_amd/node.py) needs no host synchronisation between an exchange

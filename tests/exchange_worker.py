@@ -57,6 +57,13 @@ def main():
     # descriptors of different lengths for the allocator scan
     got = xc.all_gather_i64(np.arange(3 + 5 * r, dtype=np.int64) * (r + 1))
     assert [g.tolist() for g in got] == [(np.arange(3 + 5 * q) * (q + 1)).tolist() for q in range(G)], got
+    # equal-size device buffers (the packed flush descriptors of the device allocator scan)
+    fs = torch.arange(40, dtype=torch.uint8) + 50 * r
+    fr = torch.zeros(G * 40, dtype=torch.uint8)
+    if nccl:
+        fs, fr = fs.to(dev), fr.to(dev)
+    xc.all_gather_dev(fs, fr)
+    assert fr.cpu().tolist() == [int(x) for q in range(G) for x in (torch.arange(40) + 50 * q).tolist()]
     print("exchange ok", r, "nccl" if nccl else "gloo", flush=True)
     dist.destroy_process_group()
 

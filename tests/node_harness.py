@@ -86,41 +86,69 @@ class Loopback:
             ctxs[d].gx_commit(self.x3r[d].data_ptr(), r3[d])
 
 
-    def batches_pipelined(self, per_rank_batches, done=None):
-        """per_rank_batches[j][r] = rank r's share of global batch j.  Front halves of batch j+1
-        are launched before batch j's exchanges (hdrf_gx_front_launch / _wait), as NodeRank does."""
+    def batches_pipelined(self, per_rank_batches, done=None, scan="device"):
+        """per_rank_batches[j][r] = rank r's share of global batch j, run as NodeRank.reduce_batches
+        does: the fronts of `depth` batches launched ahead (each rank's slot reused only after its
+        previous batch's back phases), the oldest batch's back phases meanwhile.  scan="device":
+        the packed flush descriptors all-gathered (region copies here) and composed on the device
+        (hdrf_gx_flush_fn_dev / hdrf_gx_alloc_scan_dev), placement launched and waited separately;
+        scan="host": the host descriptors and hdrf_gx_alloc_scan (the A/B form)."""
         G, ctxs = self.G, self.ctxs
         n = len(per_rank_batches)
-        x1b = [self.x1s, [torch.zeros_like(t) for t in self.x1s]]
+        lay = ctxs[0].gx_layout()
+        D, fnb = int(lay.depth), int(lay.fn_bytes)
+        x1b = [self.x1s] + [[torch.zeros_like(t) for t in self.x1s] for _ in range(D - 1)]
+        fn_send = [torch.zeros(fnb, dtype=torch.uint8, device=self.dev) for _ in range(G)]
+        fn_recv = [torch.zeros(G * fnb, dtype=torch.uint8, device=self.dev) for _ in range(G)]
+        launched = 0
 
-        def launch(j):
-            per = per_rank_batches[j]
+        def launch():
+            nonlocal launched
+            per = per_rank_batches[launched]
             gb = np.cumsum([0] + [len(p[0]) for p in per])
             for r in range(G):
-                ctxs[r].gx_front_launch(*per[r], int(gb[r]), x1b[j % 2][r].data_ptr())
+                ctxs[r].gx_front_launch(*per[r], int(gb[r]), x1b[launched % D][r].data_ptr())
+            launched += 1
 
-        launch(0)
+        while launched < min(D, n):
+            launch()
         c1 = [ctxs[r].gx_front_wait() for r in range(G)]
         for j in range(n):
-            if j + 1 < n:
-                launch(j + 1)
-            send = x1b[j % 2]
+            send = x1b[j % D]
             r1 = self._a2a(send, self.x1r, c1, self.w[0])
             for d in range(G):
                 ctxs[d].gx_owner(self.x1r[d].data_ptr(), r1[d], self.x2s[d].data_ptr())
             self._a2a(self.x2s, self.x2r, r1, self.w[1])
             for r in range(G):
                 ctxs[r].gx_decide(self.x2r[r].data_ptr())
-            # allocator scan (NodeRank's path): every rank's flush function, no chain
-            descs = [ctxs[r].gx_flush_fn() for r in range(G)]
-            fin = None
-            for r in range(G):
-                a_in, a_fin = ctxs[r].gx_alloc_scan(descs)
-                assert fin is None or np.array_equal(fin, a_fin), "ranks disagree on the node allocator"
-                fin = a_fin
-                ctxs[r].gx_flush(a_in, want_out=(r % 2 == 0))   # both the checked and the async form
-            a = self.alloc = fin
-            c3 = [ctxs[r].gx_place(a, self.x3s[r].data_ptr()) for r in range(G)]
+            if scan == "device":
+                for r in range(G):
+                    ctxs[r].gx_flush_fn_dev(fn_send[r].data_ptr())
+                torch.cuda.synchronize()                 # (the phases only enqueue on the contexts' streams)
+                for d in range(G):
+                    for r in range(G):
+                        fn_recv[d][r * fnb:(r + 1) * fnb].copy_(fn_send[r])
+                torch.cuda.synchronize()
+                for r in range(G):
+                    ctxs[r].gx_alloc_scan_dev(fn_recv[r].data_ptr())
+                    ctxs[r].gx_flush(None, want_out=(r % 2 == 0))   # both the checked and the async form
+                for r in range(G):
+                    ctxs[r].gx_place_launch(None, self.x3s[r].data_ptr())
+                if j + 1 < n:
+                    c1n = [ctxs[r].gx_front_wait() for r in range(G)]
+                c3 = [ctxs[r].gx_place_wait() for r in range(G)]
+            else:
+                descs = [ctxs[r].gx_flush_fn() for r in range(G)]
+                fin = None
+                for r in range(G):
+                    a_in, a_fin = ctxs[r].gx_alloc_scan(descs)
+                    assert fin is None or np.array_equal(fin, a_fin), "ranks disagree on the node allocator"
+                    fin = a_fin
+                    ctxs[r].gx_flush(a_in, want_out=(r % 2 == 0))
+                a = self.alloc = fin
+                c3 = [ctxs[r].gx_place(a, self.x3s[r].data_ptr()) for r in range(G)]
+                if j + 1 < n:
+                    c1n = [ctxs[r].gx_front_wait() for r in range(G)]
             self._compress()
             r3 = self._a2a(self.x3s, self.x3r, c3, self.w[2])
             for d in range(G):
@@ -128,7 +156,11 @@ class Loopback:
             if done is not None:
                 done(j)
             if j + 1 < n:
-                c1 = [ctxs[r].gx_front_wait() for r in range(G)]
+                c1 = c1n
+            if launched < n:
+                launch()
+        for c in ctxs:
+            c.gx_sync()
 
 
 def loopback_read(ctxs, reader, block_id):

@@ -101,13 +101,17 @@ def test_node_loopback_matches_single_sequence(G, hasher, sched):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("G,hasher", [(2, 1), (3, 0), (8, 1)])
-def test_node_loopback_pipelined_matches_single_sequence(G, hasher):
-    """The pipelined phase order (hdrf_gx_front_launch of batch j+1 before batch j's exchanges,
-    two slots, front on stream A, back phases on stream B) gives the same bytes as the oracle."""
+@pytest.mark.parametrize("G,hasher,scan,depth", [(2, 1, "device", 3), (3, 0, "host", 2), (8, 1, "device", 4),
+                                                 (4, 0, "device", 5)])
+def test_node_loopback_pipelined_matches_single_sequence(G, hasher, scan, depth, monkeypatch):
+    """The pipelined phase order (the fronts of `depth` batches launched ahead on the chunking, SHA
+    and aggregation streams, each rank's slot reused only after its previous batch's back phases;
+    the back phases on stream B, the arena copy on B2; the allocator scan on the device over the
+    all-gathered packed descriptors, or on the host) gives the same bytes as the oracle."""
     import torch  # noqa: F401
     from node_harness import Loopback, merged_index, open_ranks
     from oracle.oracle import Oracle
+    monkeypatch.setenv("HDRF_GX_DEPTH", str(depth))
 
     cmax = 1 << 20
     sched = [([2, 1, 2] * 3)[:G], ([1, 2, 1] * 3)[:G], ([2, 2, 1] * 3)[:G], ([1, 1, 2] * 3)[:G]]
@@ -139,7 +143,8 @@ def test_node_loopback_pipelined_matches_single_sequence(G, hasher):
         for r, i, gi in where[j]:
             compare_block(ctxs[r].batch_result(i), ora.reduce(blocks[gi], 0x700 + gi),
                           tag=f"pipelined G={G} batch {j} rank {r} block {i}")
-    lb.batches_pipelined(per_batch, done)
+    assert int(ctxs[0].gx_layout().depth) == depth
+    lb.batches_pipelined(per_batch, done, scan=scan)
     from node_harness import loopback_read
     for wj in where:
         for r, i, gi in wj:
@@ -457,3 +462,38 @@ def test_exchange_rccl_gpu():
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("exchange ok 0 nccl") == 1, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_node_bench_rehearsal_two_ranks_one_device(tmp_path):
+    """The N > 1 bench line (two ranks sharing cuda:0 over gloo, HDRF_BENCH_SAME_DEVICE=1: a rehearsal
+    of --gpus 2, not a measurement) carries non-zero times for every stream of the node-global
+    pipeline (front: chunking / SHA / local aggregation; back: owner .. commit with the device
+    allocator scan; arena copy), and its dedup result equals the 1-rank line's on the same global
+    corpus (rank-major global batches are the global block order)."""
+    import json
+    common = ["--block-mib", "16", "--batch", "4", "--steps", "1", "--warmup", "1", "--index-log2", "22",
+              "--arena-slots", "128", "--no-cpu", "--no-sub", "--no-alone"]
+    env = dict(os.environ, HDRF_BENCH_SAME_DEVICE="1", PYTHONPATH=ROOT)
+    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                         "127.0.0.1", "--master-port", "29651", os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                         "--blocks", "12"] + common, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r2.returncode == 0, r2.stdout[-3000:] + r2.stderr[-3000:]
+    l2 = json.loads([x for x in r2.stdout.splitlines() if x.startswith("{")][-1])
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--blocks", "24"] + common, cwd=ROOT,
+                        env=dict(os.environ, PYTHONPATH=ROOT), capture_output=True, text=True, timeout=400)
+    assert r1.returncode == 0, r1.stdout[-3000:] + r1.stderr[-3000:]
+    l1 = json.loads([x for x in r1.stdout.splitlines() if x.startswith("{")][-1])
+    print(json.dumps(l2["roofline"]["chains_ms_per_batch"]), l2["roofline"].get("front_period_ms"))
+    print(json.dumps(l2.get("node_back_ms_per_batch")))
+    for k in ("stored_bytes", "chunks", "logical_bytes"):
+        assert l2["dedup"][k] == l1["dedup"][k], (k, l2["dedup"][k], l1["dedup"][k])
+    chains = l2["roofline"]["chains_ms_per_batch"]
+    assert set(chains) == {"W: chunking", "A: SHA", "X: local aggregation", "B: back (owner .. commit + exchanges)",
+                           "B2: arena copy"}
+    assert all(v > 0 for v in chains.values()), chains
+    st = l2["stages"]
+    for k in ("place(place_kernel)", "flush(flush_kernel)", "gx_owner(own_claim..own_finish)",
+              "gx_alloc_scan(gx_scan_kernel)", "gx_commit(own_commit)", "gx_local(scratch claim/apply/decide + gx_emit)"):
+        assert st[k]["ms_per_step"] > 0, (k, st[k])
+    assert l2["roofline"]["frac"] > 0 and l2["roofline"]["front_period_ms"] > 0
