@@ -103,6 +103,7 @@ struct Slot {
     RecipeCopy *h_rjobs = nullptr, *d_rjobs = nullptr;   // recipe copies of the batch (storeDB)
     hipEvent_t recipe_done = nullptr;         // the copies read d_dig: the slot's next SHA waits
     bool recipe_pending = false;
+    bool gen_reset = false;                   // the batch starts a fresh index generation (hdrf_reset_async)
     hipEvent_t walk_done = nullptr, front_done = nullptr, back_done = nullptr, gmax_done = nullptr;
     hipEvent_t copy_done = nullptr;          // host path: the batch's H2D copies landed
     uint8_t *d_hstage = nullptr;              // host path: device copies of the batch's blocks
@@ -178,6 +179,8 @@ struct hdrf_ctx {
     uint32_t batch = 0;                              // batch ids: grow over the context's life (never reset)
     uint32_t epoch = 1;                              // index generation in the tag words (1..255)
     uint32_t bfirst = 1;                             // first batch id of the current epoch
+    bool gen_pending = false;                        // hdrf_reset_async: the next submit starts a generation
+    bool gen_clear = false;                          //   ... whose epoch wrapped (the table is cleared)
     uint32_t scratch_epoch[kSlots] = {};             // node-global: generation of each scratch table
     int have_alloc = 0;
     int last_nblocks = 0;
@@ -522,15 +525,38 @@ static int drain(hdrf_ctx *ctx)
     return rc;
 }
 
-static int init_state(hdrf_ctx *ctx, bool fresh)
+static AllocState initial_alloc(const hdrf_ctx *ctx)
 {
-    (void)drain(ctx);
     AllocState a{};
     for (int t = 0; t < 4; t++) {
         a.id[t] = (uint32_t)t << 22;                 // utilities.bytesToBlockID, absent key (DN/utilities.java:36-50)
         // (node-global mode: the one allocator of the node, carried rank to rank by hdrf_gx_flush)
         a.slot[t] = (uint32_t)t * (uint32_t)(ctx->cfg.arena_slots / 4);   // per-range slot rings
     }
+    return a;
+}
+
+// the host side of a fresh DataNode: containers, recipes, allocator view, totals
+static void reset_host(hdrf_ctx *ctx)
+{
+    ctx->h_alloc = initial_alloc(ctx);
+    ctx->have_alloc = 0;
+    ctx->containers.clear();
+    ctx->slot_owner.clear();
+    for (auto &kv : ctx->loaded) (void)hipFree(kv.second.ptr);
+    ctx->loaded.clear();
+    ctx->recipes.clear();
+    ctx->rcur = 0;
+    ctx->rhead = 0;
+    ctx->lengths.clear();
+    ctx->stats = hdrf_stats{};
+}
+
+static int init_state(hdrf_ctx *ctx, bool fresh)
+{
+    (void)drain(ctx);
+    ctx->gen_pending = false;
+    const AllocState a = initial_alloc(ctx);
     for (auto &S : ctx->sl) HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
     // the index and allocator belong to the back stream (also for the node-global back phases).
@@ -549,17 +575,8 @@ static int init_state(hdrf_ctx *ctx, bool fresh)
                 HIPCK(hipMemsetAsync(ctx->d_scratch[i], 0, sizeof(IndexEntry) << ctx->scratch_log2, ist));
                 ctx->scratch_epoch[i] = 0;
             }
-    ctx->h_alloc = a;
-    ctx->have_alloc = 0;
-    ctx->containers.clear();
-    ctx->slot_owner.clear();
-    for (auto &kv : ctx->loaded) (void)hipFree(kv.second.ptr);
-    ctx->loaded.clear();
-    ctx->recipes.clear();
-    ctx->rcur = 0;
-    ctx->rhead = 0;
-    for (auto &S : ctx->sl) S.recipe_pending = false;
-    ctx->lengths.clear();
+    reset_host(ctx);
+    for (auto &S : ctx->sl) S.recipe_pending = S.gen_reset = false;
     ctx->last_nblocks = 0;
     ctx->gx_nfront = ctx->gx_nfwait = ctx->gx_nback = 0;
     ctx->gx_bphase = 0;
@@ -569,7 +586,6 @@ static int init_state(hdrf_ctx *ctx, bool fresh)
     for (auto &T : ctx->gxt) T.rec = 0;
     for (auto &S : ctx->sl) S.gx_inuse = S.gx_split = false;
     if (ctx->d_gx_err) HIPCK(hipMemsetAsync(ctx->d_gx_err, 0, sizeof(int), ist));
-    ctx->stats = hdrf_stats{};
     ctx->pend_closed.clear();
     for (auto &u : ctx->undrained) u = 0;
     ctx->inflight_bound = 0;
@@ -719,6 +735,29 @@ extern "C" int hdrf_reset(hdrf_ctx *ctx)
         if (ctx->rx[i].state.load() == 1)
             return set_err(ctx, HDRF_E_INVAL, "a block is being received (hdrf_submit_slot or hdrf_rx_cancel first)");
     return init_state(ctx, false);
+}
+
+// A fresh DataNode without draining the pipeline (bench steps back to back, a DataNode's volume
+// re-initialised while blocks are in flight): the batches already submitted complete against the
+// old state; the next submit starts a new index generation (the next epoch of the tag words, so no
+// table clear), the allocator is re-seeded on the index stream after the old batches' store part,
+// and the host side (containers, recipes, allocator view, totals) is reset when that batch is
+// completed (wait_one), after every older batch.  Single-node ring-arena contexts.
+extern "C" int hdrf_reset_async(hdrf_ctx *ctx)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G > 1 || ctx->cfg.retain_containers)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async: single-node contexts without durable containers (hdrf_reset)");
+    for (int i = 0; i < hdrf_ctx::kRx; i++)
+        if (ctx->rx[i].state.load() == 1)
+            return set_err(ctx, HDRF_E_INVAL, "a block is being received (hdrf_submit_slot or hdrf_rx_cancel first)");
+    if (ctx->nsub == ctx->nwait && !ctx->gen_pending) return init_state(ctx, false);   // nothing in flight
+    ctx->gen_clear = ctx->gen_clear || ctx->epoch >= 255;
+    ctx->epoch = ctx->epoch >= 255 ? 1 : ctx->epoch + 1;
+    ctx->bfirst = ctx->batch + 1;
+    ctx->gen_pending = true;
+    return 0;
 }
 
 // container id -> slot bookkeeping after a batch
@@ -885,6 +924,8 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
     S.lens.assign(len, len + nblocks);
     S.nblocks = nblocks;
+    S.gen_reset = ctx->gen_pending;                   // the first batch of a fresh generation (hdrf_reset_async)
+    ctx->gen_pending = false;
     const uint32_t cur = ++ctx->batch;
     // chunking runs on its own stream W (HDRF_STREAMS=2: shares stream A with SHA).  Measured with
     // the two-pass lane walker (r02): three streams 992 GB/s vs two 919 — the walk's latency-bound
@@ -918,6 +959,14 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     // batch-local state out of the index (designated chunks, block counts, entries cleared), so the
     // next batch's index part may run while this batch is stored on stream B2
     HIPCK(hipStreamWaitEvent(Bst, S.front_done, 0));
+    if (S.gen_reset) {
+        // a fresh generation: the old batches' store part (stream B2: place writes index values, the
+        // flush walk the allocator) is finished before this index part claims entries of the new epoch;
+        // then the allocator is re-seeded (and the table cleared when the epoch wrapped)
+        if (ctx->nsub > ctx->nwait) HIPCK(hipStreamWaitEvent(Bst, ctx->sl[(ctx->nsub - 1) % kSlots].back_done, 0));
+        HIPCK(launch_index_clear(ctx->d_tab, ctx->gen_clear ? c.index_log2 : -1, ctx->d_alloc, initial_alloc(ctx), Bst));
+        ctx->gen_clear = false;
+    }
     // HDRF_DECIDE_DESIG=0 (A/B): idx_finalize reads every designated entry (round-3 c2 behaviour)
     static const bool decide_desig = [] { const char *e = getenv("HDRF_DECIDE_DESIG"); return !e || atoi(e) != 0; }();
     Marker mb;
@@ -965,7 +1014,8 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         for (uint64_t j = ctx->nsub - 1; j + 1 > ctx->nwait; j--) {   // in flight, newest first
             const Slot &Pj = ctx->sl[j % kSlots];
             sum += Pj.lz_bound;
-            if (sum + 1 >= per) HIPCK(hipStreamWaitEvent(B2, Pj.lz_done, 0));
+            // (a fresh generation restarts every ring at its first slot: every pass in flight first)
+            if (sum + 1 >= per || S.gen_reset) HIPCK(hipStreamWaitEvent(B2, Pj.lz_done, 0));
             if (j == 0) break;
         }
     }
@@ -1141,6 +1191,10 @@ static int wait_one(hdrf_ctx *ctx)
             ctx->rx[i].len = 0;
         }
     S.rx_release = 0;
+    if (S.gen_reset) {                                   // the first batch of a fresh generation
+        reset_host(ctx);
+        S.gen_reset = false;
+    }
     return complete_slot(ctx, si, true);
 }
 

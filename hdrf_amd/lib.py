@@ -35,7 +35,7 @@ EXPORTS = [
     "hdrf_probe_stats", "hdrf_rx_begin", "hdrf_append_packet", "hdrf_submit_slot", "hdrf_submit_slots", "hdrf_rx_cancel",
     "hdrf_gx_read_locate", "hdrf_gx_read_fill", "hdrf_gx_flush_fn", "hdrf_gx_alloc_scan",
     "hdrf_set_lzop_mtime", "hdrf_gx_flush_fn_dev", "hdrf_gx_alloc_scan_dev", "hdrf_gx_place_launch",
-    "hdrf_gx_place_wait", "hdrf_gx_sync",
+    "hdrf_gx_place_wait", "hdrf_gx_sync", "hdrf_reset_async",
 ]
 
 ALLOC_STATE_BYTES = 128     # HDRF_ALLOC_STATE_BYTES
@@ -193,6 +193,7 @@ def load():
                                                  ctypes.c_uint64, ctypes.c_int32]),
         "hdrf_stage_times": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int32, ctypes.c_int32]),
         "hdrf_reset": (ctypes.c_int, [_vp]),
+        "hdrf_reset_async": (ctypes.c_int, [_vp]),
         "hdrf_get_stats": (ctypes.c_int, [_vp, ctypes.POINTER(Stats)]),
         "hdrf_gx_layout_get": (ctypes.c_int, [_vp, ctypes.POINTER(GxLayout)]),
         "hdrf_gx_front_launch": (ctypes.c_int, [_vp, ctypes.c_int32, ctypes.POINTER(_vp), _u64p, _u64p, _u64p,
@@ -623,6 +624,10 @@ class Context:
 
     def reset(self):
         self._ck(self.L.hdrf_reset(self._h))
+
+    def reset_async(self):
+        """A fresh DataNode from the next submit on, without draining the batches in flight."""
+        self._ck(self.L.hdrf_reset_async(self._h))
 
     def stats(self):
         st = Stats()

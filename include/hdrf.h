@@ -343,6 +343,10 @@ int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out);
  * the batches in flight first.  HDRF_E_INVAL while a packet receive is open (hdrf_rx_begin not
  * yet followed by hdrf_submit_slot or hdrf_rx_cancel). */
 int hdrf_reset(hdrf_ctx *ctx);
+/* The same without completing the batches in flight (single-node contexts, cfg.retain_containers = 0):
+ * they complete against the old state, and the next hdrf_submit_batch starts the fresh DataNode, so
+ * its front half overlaps the old batches' back halves.  Views complete every batch first, as always. */
+int hdrf_reset_async(hdrf_ctx *ctx);
 
 /* ---- Node-global index over n_ranks GPUs (BASELINE config 3) -------------------
  * All DataNodes of one host share one Redis (JedisPool("localhost"), DN/DataDeduplicator.java:119),
