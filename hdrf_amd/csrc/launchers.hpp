@@ -96,7 +96,7 @@ struct GxPlace {
 // Node-global allocator scan on the device (store.hip): this rank's flush function packed into a
 // fixed-size descriptor (gx_fn_bytes), and the composition of every rank's descriptor (rank order)
 // from the node's allocator after the previous batch.
-struct GxFnHead {            // descriptor header (the rows follow, per range t: mcap x GxFnRow)
+struct GxFnHead {            // descriptor header (the rows follow, per range t < 3: mcap x GxFnRow)
     uint64_t n_thread, mcap;
     uint64_t any[4], S[4], base_last[4], S_last[4], m[4];
 };

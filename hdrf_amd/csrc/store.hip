@@ -310,7 +310,7 @@ uint64_t gx_fn_mcap(uint32_t cmax, int window, int max_batch)
 }
 uint64_t gx_fn_bytes(uint32_t cmax, int window, int max_batch)
 {
-    return (sizeof(GxFnHead) + 4 * gx_fn_mcap(cmax, window, max_batch) * sizeof(GxFnRow) + 255) & ~(uint64_t)255;
+    return (sizeof(GxFnHead) + 3 * gx_fn_mcap(cmax, window, max_batch) * sizeof(GxFnRow) + 255) & ~(uint64_t)255;   // <= 3 ranges
 }
 
 __global__ void __launch_bounds__(256) fn_pack_kernel(int n_thread, const FnRange *__restrict__ fr,
@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(64) gx_scan_kernel(const uint8_t *__restrict__
         __syncthreads();
         const GxFnHead *h = (const GxFnHead *)(descs + (size_t)r * fn_bytes);
         const GxFnRow *rows = (const GxFnRow *)(descs + (size_t)r * fn_bytes + sizeof(GxFnHead));
-        if (t == 0 && (h->n_thread != (uint64_t)n_thread || sizeof(GxFnHead) + 4 * h->mcap * sizeof(GxFnRow) > fn_bytes))
+        if (t == 0 && (h->n_thread != (uint64_t)n_thread || sizeof(GxFnHead) + 3 * h->mcap * sizeof(GxFnRow) > fn_bytes))
             atomicOr(err, 512);
         if (t < n_thread && h->n_thread == (uint64_t)n_thread && h->any[t]) {
             const uint64_t m = h->m[t], S = h->S[t];
