@@ -167,7 +167,6 @@ struct hdrf_ctx {
     int res = 0;                   // slot of the last completed batch (hdrf_batch_* views)
     // node state (shared by all batches)
     IndexEntry *d_tab = nullptr;
-    uint32_t *d_seen = nullptr, *d_multi = nullptr;   // home-slot bitmaps of the sole-chunk path (index.hip)
     uint8_t *d_arena = nullptr;
     uint8_t *d_carena = nullptr;                 // compressor 2: Lz4Codec files of closed containers
     uint64_t cslot = 0;
@@ -410,7 +409,7 @@ static void free_all(hdrf_ctx *ctx)
     ctx->rchunks.clear();
     void *ptrs[] = {ctx->d_tab, ctx->d_arena, ctx->d_alloc, ctx->d_stage, ctx->d_rd, ctx->d_gx_counts,
                     ctx->d_gx_rcounts, ctx->d_oslot, ctx->d_oflags, ctx->d_carena, ctx->d_fn, ctx->d_gx_x3exp,
-                    ctx->d_x3want, ctx->d_gxst, ctx->d_gx_err, ctx->d_seen, ctx->d_multi};
+                    ctx->d_x3want, ctx->d_gxst, ctx->d_gx_err};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     for (int i = 0; i < kSlots; i++) {
@@ -657,15 +656,6 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
     if (!rc && ((rc = dalloc(ctx, &ctx->d_tab, (size_t)1 << c.index_log2)) ||
                 (rc = dalloc(ctx, &ctx->d_arena, (size_t)c.arena_slots * c.container_max + 256)) ||
                 (rc = dalloc(ctx, &ctx->d_alloc, 1)))) {
-    }
-    // the sole-chunk index path (single-node contexts; HDRF_SOLE=0 turns it off for A/B runs): two
-    // bitmaps of one bit per table slot, zero between batches
-    static const bool sole = [] { const char *e = getenv("HDRF_SOLE"); return !e || atoi(e) != 0; }();
-    if (!rc && sole && c.n_ranks == 1) {
-        const size_t words = ((size_t)1 << c.index_log2) / 32 + 1;
-        if (!(rc = dalloc(ctx, &ctx->d_seen, words)) && !(rc = dalloc(ctx, &ctx->d_multi, words)) &&
-            (hipMemset(ctx->d_seen, 0, words * 4) != hipSuccess || hipMemset(ctx->d_multi, 0, words * 4) != hipSuccess))
-            rc = set_err(ctx, HDRF_E_HIP, "hipMemset failed");
     }
     if (!rc && c.compressor == 2) {
         ctx->cslot = lz4_slot_bytes(c.container_max);
@@ -981,18 +971,11 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     static const bool decide_desig = [] { const char *e = getenv("HDRF_DECIDE_DESIG"); return !e || atoi(e) != 0; }();
     Marker mb;
     mb.ev = ctx->timing ? S.evB : nullptr;
-    const bool sole = decide_desig && ctx->d_multi;
     HIPCK(launch_index(c.hasher, S.d_bst, nblocks, ctx->cap_blk, S.d_off, S.d_dig, ctx->d_tab, c.index_log2, cur,
                        ctx->bfirst, tag_mask(ctx), S.d_slot, S.d_coll, S.d_ncoll, ctx->coll_cap, S.d_flags, S.d_tilesum, ctx->ntiles,
-                       S.d_err, Bst, &mb, decide_desig ? S.d_dcnt : nullptr, sole ? ctx->d_seen : nullptr,
-                       sole ? ctx->d_multi : nullptr));
+                       S.d_err, Bst, &mb, decide_desig ? S.d_dcnt : nullptr));
     HIPCK(launch_index_finalize(S.d_bst, nblocks, ctx->cap_blk, ctx->ntiles, ctx->d_tab, S.d_slot, S.d_flags, S.d_dcnt,
                                 Bst));
-    if (sole) {                                         // the home-slot bitmaps, zero for the next batch
-        const size_t bytes = (((size_t)1 << c.index_log2) / 32 + 1) * 4;
-        HIPCK(hipMemsetAsync(ctx->d_seen, 0, bytes, Bst));
-        HIPCK(hipMemsetAsync(ctx->d_multi, 0, bytes, Bst));
-    }
     if (ctx->timing) HIPCK(hipEventRecord(S.evB[9], Bst));
     HIPCK(hipEventRecord(S.idx_done, Bst));
     // ---- back, store part, in block order on stream B2 (scans, flush walk, place, read-back)

@@ -31,30 +31,6 @@ __device__ __forceinline__ void record_occurrence(IndexEntry *e, int b, int k)
     if (old & bit) atomicMax(&e->first, ((unsigned long long)(63 - b) << 32) | (unsigned)(k + 1));
 }
 
-// ---- home-slot pass (single-node contexts): a chunk is SOLE when no other chunk of the batch has
-// its home slot (then no other chunk has its digest: equal digests have equal tags and homes).  A
-// sole chunk's entry is touched by no other chunk of the batch, so its decision needs no batch-local
-// state: claim resolves it (created, or an earlier batch's entry) without the mask / first atomics,
-// decide without reading the entry, finalize without clearing it; only the chunks whose homes repeat
-// (intra-batch repeats, home collisions) take the mask / first path.  seen / multi: one bit per
-// slot (2^log2cap bits each, cleared after every batch); the second and later setters mark multi.
-// grid (ceil(cap_blk/256), nblocks)
-template <int HW>
-__global__ void __launch_bounds__(256) idx_home_kernel(const BlockState *__restrict__ bst, int cap_blk,
-                                                       const uint32_t *__restrict__ digests, int log2cap,
-                                                       unsigned long long key, uint32_t *__restrict__ seen,
-                                                       uint32_t *__restrict__ multi)
-{
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= bst[b].n_chunks) return;
-    const size_t c = (size_t)b * cap_blk + k;
-    const uint32_t dw[2] = {digests[c * HW], digests[c * HW + 1]};
-    const uint64_t h = tag_home(tag_word(dw, key), log2cap);
-    const uint32_t bit = 1u << (h & 31);
-    if (atomicOr(seen + (h >> 5), bit) & bit) atomicOr(multi + (h >> 5), bit);
-}
-
 // ---- claim: grid (ceil(cap_blk/256), nblocks) ---------------------------------------------
 // Probe by tag; CAS-claim empty slots (an entry of an older epoch is empty: the CAS replaces the
 // tag it read).  The chunk's block bit / last occurrence are applied right here when the digest is
@@ -70,7 +46,7 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
                                                         IndexEntry *__restrict__ tab, int log2cap, uint32_t cur,
                                                         uint32_t bfirst, unsigned long long key,
                                                         uint32_t *__restrict__ slot, uint8_t *__restrict__ flags,
-                                                        int *__restrict__ err, const uint32_t *__restrict__ multi)
+                                                        int *__restrict__ err)
 {
     const int b = blockIdx.y;
     const int k = blockIdx.x * 256 + threadIdx.x;
@@ -82,8 +58,6 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
     const unsigned long long tag = tag_word(dw, key);
     const uint64_t mask = (1ull << log2cap) - 1;
     uint64_t h = tag_home(tag, log2cap);
-    // (multi == nullptr: every chunk takes the mask / first path, as node-global aggregation does)
-    const bool sole = multi && !((multi[h >> 5] >> (h & 31)) & 1u);
     bool mine = false;
     for (uint64_t probe = 0;; probe++) {
         if (probe > mask) { atomicOr(err, 2); return; }           // table full
@@ -96,7 +70,7 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
         }
         if (mine) {
             e->batch = cur;
-            e->mask = sole ? 0ull : 1ull << b;                     // this chunk's occurrence
+            e->mask = 1ull << b;                                   // this chunk's occurrence
             e->first = 0;
             store_dig<HW>(e, dw);
             break;
@@ -110,10 +84,9 @@ __global__ void __launch_bounds__(256) idx_claim_kernel(const BlockState *__rest
     if (!mine) {
         const uint32_t bt = e->batch;
         apply = bt >= bfirst && bt != cur && entry_matches<HW>(*e, dw);
-        if (apply && !sole) record_occurrence(e, b, k);           // (a sole chunk's entry: no other toucher)
+        if (apply) record_occurrence(e, b, k);
     }
-    // bit 3 resolved here; bit 6 created by this chunk; bit 7 sole
-    flags[c] = (uint8_t)(((mine || apply) ? 8 : 0) | (mine ? 64 : 0) | (sole ? 128 : 0));
+    flags[c] = (mine || apply) ? 8 : 0;
 }
 
 // ---- apply: deferred chunks — verify full digest, record block membership / last occurrence
@@ -121,7 +94,7 @@ template <int HW>
 __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                         const uint32_t *__restrict__ digests,
                                                         IndexEntry *__restrict__ tab, const uint32_t *__restrict__ slot,
-                                                        uint8_t *__restrict__ flags,
+                                                        const uint8_t *__restrict__ flags,
                                                         uint32_t *__restrict__ coll, uint32_t *__restrict__ ncoll,
                                                         int coll_cap, int *__restrict__ err)
 {
@@ -129,17 +102,14 @@ __global__ void __launch_bounds__(256) idx_apply_kernel(const BlockState *__rest
     const int k = blockIdx.x * 256 + threadIdx.x;
     if (k >= bst[b].n_chunks) return;
     const size_t c = (size_t)b * cap_blk + k;
-    const uint8_t f = flags[c];
-    if (f & 8) return;
+    if (flags[c] & 8) return;
     uint32_t dw[HW];
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
     IndexEntry *e = tab + slot[c];
     if (entry_matches<HW>(*e, dw)) {
-        if (f & 128) flags[c] = (uint8_t)(f | 8);                  // a sole chunk: an earlier entry
-        else record_occurrence(e, b, k);
+        record_occurrence(e, b, k);
     } else {
-        if (f & 128) flags[c] = 0;                                 // the exact slow path: mask / first
         uint32_t i = atomicAdd(ncoll, 1u);
         if ((int)i < coll_cap) coll[i] = (uint32_t)c;
         else atomicOr(err, 4);
@@ -200,19 +170,7 @@ __global__ void __launch_bounds__(256) idx_decide_kernel(const BlockState *__res
     const int k = blockIdx.x * 256 + threadIdx.x;
     const int n = bst[b].n_chunks;
     uint32_t newlen = 0;
-    if (k < n && dcnt && (flags[(size_t)b * cap_blk + k] & 128)) {
-        // a sole chunk (idx_home_kernel): the only chunk of the batch on its entry, so it is in the
-        // entry's min block, designated, holding it in one block; new iff it created the entry — no
-        // read of the entry (and idx_finalize has nothing to clear)
-        const size_t c = (size_t)b * cap_blk + k;
-        const bool created = (flags[c] & 64) != 0;
-        dcnt[c] = 1;
-        flags[c] = (uint8_t)((created ? 1 : 0) | 2 | (created ? 4 : 0) | 32 | 128);
-        if (created) {
-            const uint32_t *off = offsets + (size_t)b * cap_blk;
-            newlen = off[k] - (k ? off[k - 1] : 0u);
-        }
-    } else if (k < n) {
+    if (k < n) {
         const size_t c = (size_t)b * cap_blk + k;
         IndexEntry *e = tab + slot[c];
         const unsigned long long m = e->mask;
@@ -264,7 +222,7 @@ __global__ void __launch_bounds__(256) idx_finalize_kernel(const BlockState *__r
     if (k >= bst[b].n_chunks) return;
     const size_t c = (size_t)b * cap_blk + k;
     const uint8_t f = flags[c];
-    if (!(f & 2) || (f & 128)) return;                 // not in the min block; a sole chunk (nothing set)
+    if (!(f & 2)) return;                              // not in the entry's min block
     IndexEntry *e = tab + slot[c];
     if (!(f & 32)) {                                   // not settled by idx_decide:
         if ((f & 16) && (uint32_t)e->first != (uint32_t)(k + 1)) return;   // repeats: the last occurrence
@@ -416,24 +374,15 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst,
                         unsigned long long tag_mask, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
-                        int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt, uint32_t *seen,
-                        uint32_t *multi)
+                        int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt)
 {
     mk->mark(st);
     dim3 g(ntiles, nblocks);
     static const int lds = [] { const char *e = getenv("HDRF_CLAIM_LDS"); return e ? atoi(e) : 0; }();
     if (hipError_t e = hipMemsetAsync(ncoll, 0, sizeof(uint32_t), st)) return e;
-    // (sole chunks need idx_finalize's designation bookkeeping: single-node contexts only)
-    if (!dcnt) multi = nullptr;
-    if (multi) {
-        if (hasher == 0)
-            hipLaunchKernelGGL(idx_home_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, log2cap, tag_mask, seen, multi);
-        else
-            hipLaunchKernelGGL(idx_home_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, log2cap, tag_mask, seen, multi);
-    }
     if (hasher == 0) {
         hipLaunchKernelGGL(idx_claim_kernel<5>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, bfirst,
-                           tag_mask, slot, flags, err, multi);
+                           tag_mask, slot, flags, err);
         mk->mark(st);
         hipLaunchKernelGGL(idx_apply_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, coll,
                            ncoll,
@@ -443,7 +392,7 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                            coll, ncoll, coll_cap, err);
     } else {
         hipLaunchKernelGGL(idx_claim_kernel<7>, g, dim3(256), lds, st, bst, cap_blk, digests, tab, log2cap, cur, bfirst,
-                           tag_mask, slot, flags, err, multi);
+                           tag_mask, slot, flags, err);
         mk->mark(st);
         hipLaunchKernelGGL(idx_apply_kernel<7>, g, dim3(256), 0, st, bst, cap_blk, digests, tab, slot, flags, coll,
                            ncoll,

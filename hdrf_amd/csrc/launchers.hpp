@@ -78,11 +78,9 @@ hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst,
                         unsigned long long key, uint32_t *slot,
                         uint32_t *coll, uint32_t *ncoll, int coll_cap, uint8_t *flags, uint32_t *tilesum,
-                        int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt = nullptr,
-                        uint32_t *seen = nullptr, uint32_t *multi = nullptr);
+                        int ntiles, int *err, hipStream_t st, Marker *mk, uint8_t *dcnt = nullptr);
 // (dcnt: idx_finalize follows and hands place the designated chunks; decide settles the chunks
-//  without repeats in their min block itself.  seen / multi (with dcnt): the home-slot bitmaps of the
-//  sole-chunk path, cleared by the caller after the batch's index part)
+//  without repeats in their min block itself)
 // node-global index mode (gx.hip): place_kernel emits (owner slot, cid, start, stop) for new entries
 struct GxPlace {
     const uint32_t *x2 = nullptr;          // owner responses, indexed by scratch IndexEntry::cid
