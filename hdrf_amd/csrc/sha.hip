@@ -418,167 +418,6 @@ __global__ void __launch_bounds__(256) sha_carry_kernel(const BlockDesc *__restr
 }
 
 
-// the absolute 128-B line at block offset lo (may start before the block: those bytes read as 0)
-__device__ __forceinline__ void load_line(const uint8_t *base, int64_t readable, int64_t lo, uint32_t (&R)[32])
-{
-    if (lo >= 0 && lo + 128 <= readable) {
-        const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + lo);
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
-            R[4 * q] = v.x; R[4 * q + 1] = v.y; R[4 * q + 2] = v.z; R[4 * q + 3] = v.w;
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < 32; q++) R[q] = lo + 4 * q >= 0 ? load4_guard(base, lo + 4 * q, readable) : 0u;
-    }
-}
-
-// Window of the line variant: dwords [q, q + 33) of the two lines P ++ R, q in [0, 31] per lane, by
-// a 5-stage barrel shift of selects (191 v_cndmask, no LDS, no memory).
-__device__ __forceinline__ void shift_window(const uint32_t (&P)[32], const uint32_t (&R)[32], uint32_t q, uint32_t (&d)[33])
-{
-    // per-lane masks (all ones where the stage shifts); the blends are on values (bfi), never a
-    // select of element addresses, so the arrays stay in registers
-    const uint32_t m16 = 0u - ((q >> 4) & 1u), m8 = 0u - ((q >> 3) & 1u), m4 = 0u - ((q >> 2) & 1u),
-                   m2 = 0u - ((q >> 1) & 1u), m1 = 0u - (q & 1u);
-    uint32_t y[48], z[40], w[36], v[34];
-#pragma unroll
-    for (int i = 0; i < 48; i++) y[i] = bfi(m16, i + 16 < 32 ? P[i + 16] : R[i - 16], i < 32 ? P[i] : R[i - 32]);
-#pragma unroll
-    for (int i = 0; i < 40; i++) z[i] = bfi(m8, y[i + 8], y[i]);
-#pragma unroll
-    for (int i = 0; i < 36; i++) w[i] = bfi(m4, z[i + 4], z[i]);
-#pragma unroll
-    for (int i = 0; i < 34; i++) v[i] = bfi(m2, w[i + 2], w[i]);
-#pragma unroll
-    for (int i = 0; i < 33; i++) d[i] = bfi(m1, v[i + 1], v[i]);
-}
-
-
-// sha_line (HDRF_SHA_LINE=1): the same lanes, but no 128-B line is fetched twice.  A lane's pair window
-// (132 B from a 4-aligned start) spans the absolute 128-B line L holding its start and line L + 1; the
-// lane carries line L in registers, loads line L + 1 whole (8 x 16 B, aligned) and cuts the window out
-// of the two by shift_window (a per-lane barrel shift: ~190 VALU per 128 B, +15 % over the two
-// compressions' 1236).  Round 3 it lost (SHA was on the critical chain: 1005-1019 vs 1024-1041 GB/s);
-// round 5 re-measures it with the config-2 steps primed, where the store stream sets the period and
-// the fabric's bytes, not SHA's VALU, are the shared resource.  Pairing as sha_iter: a chunk whose
-// block T (the message end) is even starts one block early (a skipped slot), so every iteration steps
-// by 128 B and T is always in the second slot.
-template <int HW>
-__global__ void __launch_bounds__(256) sha_line_kernel(const BlockDesc *__restrict__ blocks,
-                                                       const uint32_t *__restrict__ offsets,
-                                                       const BlockState *__restrict__ bst, int cap_blk,
-                                                       uint32_t *__restrict__ digests, uint32_t *__restrict__ queue,
-                                                       uint32_t thr, int prio)
-{
-    if (blockIdx.y == 0) {                        // the long-chunk lanes (dispatched first)
-        sha_long_lanes<HW>(blocks, offsets, bst, cap_blk, digests, thr, prio & 1);
-        return;
-    }
-    if (prio & 2) __builtin_amdgcn_s_setprio(2);
-    const int b = blockIdx.y - 1;
-    const int n = bst[b].n_chunks;
-    const BlockDesc &bd = blocks[b];
-    const uint8_t *base = bd.data;
-    const int64_t readable = (int64_t)bd.readable;
-    const int64_t bmis = (int64_t)((uintptr_t)base & 127u);     // block start's offset in its line
-    const uint32_t *off = offsets + (size_t)b * cap_blk;
-    uint32_t *db = digests + (size_t)b * cap_blk * HW;
-    const int l = lane_id();
-    int kbP, cntP, kbQ, cntQ;
-    uint32_t SP, EP, SQ, EQ;
-    auto reserve = [&](int &kb, int &cnt, uint32_t &S, uint32_t &E) {
-        uint32_t got = 0;
-        if (l == 0) got = atomicAdd(queue + b, 64u);
-        kb = (int)rdfirst(got);
-        cnt = max(0, min(64, n - kb));
-        const int k = kb + l;
-        E = l < cnt ? ld4(off + k) : 0u;
-        S = (l < cnt && k > 0) ? ld4(off + k - 1) : 0u;
-    };
-    reserve(kbP, cntP, SP, EP);
-    reserve(kbQ, cntQ, SQ, EQ);
-    int head = 0;
-    bool active = false;
-    int k = 0;
-    uint32_t len = 0, T = 0, nb = 0;
-    int b0 = 0;                                   // block index of the window's first slot (-1: skipped)
-    int64_t wb = 0;                               // window start, block offset (b0 * 64 from the chunk)
-    uint32_t st[8];
-    set_iv<HW>(st);
-    uint32_t N0[32];                              // the carried line
-    for (;;) {
-        if (active && b0 >= (int)nb) {            // chain done: the digest
-            store_digest<HW>(db + (size_t)k * HW, st);
-            active = false;
-        }
-        for (;;) {                                 // offer chunks to idle lanes
-            const unsigned long long idle = ballot64(!active);
-            if (!idle) break;
-            if (head >= cntP) {
-                if (cntQ == 0) break;
-                kbP = kbQ; cntP = cntQ; SP = SQ; EP = EQ; head = 0;
-                reserve(kbQ, cntQ, SQ, EQ);
-            }
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0));
-            const int avail = cntP - head;
-            const int idx = min(head + rank, 63);
-            const uint32_t e = (uint32_t)__shfl((int)EP, idx, 64), c0 = (uint32_t)__shfl((int)SP, idx, 64);
-            bool skip = false;
-            if (ballot64(!active && rank < avail && e - c0 >= kShaLong) && l == 0) atomicOr(queue + 64, 1u);
-            if (!active && rank < avail && e - c0 >= thr) {
-                skip = true;
-            } else if (!active && rank < avail) {
-                k = kbP + head + rank;
-                len = e - c0;
-                T = len >> 6;
-                nb = (len + 8) / 64 + 1;
-                const bool teven = (T & 1u) == 0;
-                b0 = teven ? -1 : 0;
-                wb = (int64_t)c0 - (teven ? 64 : 0);
-                set_iv<HW>(st);
-                active = true;
-                load_line(base, readable, ((bmis + wb) & ~(int64_t)127) - bmis, N0);
-            }
-            const int nidle = __popcll(idle);
-            head += min(nidle, avail);
-            if (!ballot64(skip) && nidle <= avail) break;
-        }
-        if (!ballot64(active)) break;
-        const bool data = active && b0 <= (int)T;  // not the length-only block alone
-        const int64_t lo = ((bmis + wb) & ~(int64_t)127) - bmis;   // line L, block offset
-        const uint32_t q0 = (uint32_t)((bmis + wb) & 124);          // window's first dword in L (x4)
-        uint32_t R[32], d[33];
-        if (data) {
-            load_line(base, readable, lo + 128, R);
-            shift_window(N0, R, q0 >> 2, d);
-#pragma unroll
-            for (int i = 0; i < 32; i++) N0[i] = R[i];
-        }
-        if (active) {
-            const uint32_t sel = 0x00010203u + (uint32_t)(wb & 3) * 0x01010101u;
-            uint32_t m[16];
-            if (b0 >= 0) {                        // slot 0 (the length-only block pads)
-#pragma unroll
-                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
-                if (ballot64(b0 > (int)T)) pad_block(m, len, (uint32_t)b0, nb);
-                if (HW == 5) sha1_compress(st, m);
-                else sha256_compress(st, m);
-            }
-            if (b0 + 1 < (int)nb) {               // slot 1 (T pads)
-#pragma unroll
-                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(d[i + 17], d[i + 16], sel);
-                if (ballot64(b0 + 1 == (int)T)) pad_block(m, len, (uint32_t)(b0 + 1), nb);
-                if (HW == 5) sha1_compress(st, m);
-                else sha256_compress(st, m);
-            }
-            b0 += 2;
-            wb += 128;
-        }
-    }
-}
-
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
                       hipStream_t st, Marker *mk)
@@ -608,15 +447,9 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
     // HDRF_SHA_CARRY: 1 = sha_carry (4-block windows, the second pair carried in registers)
     static const bool carryk = [] { const char *e = getenv("HDRF_SHA_CARRY"); return e && atoi(e) != 0; }();
-    // HDRF_SHA_LINE: 1 = sha_line (each line fetched once, window by a register barrel shift)
-    static const bool linek = [] { const char *e = getenv("HDRF_SHA_LINE"); return e && atoi(e) != 0; }();
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
-    if (linek && hasher == 0)
-        hipLaunchKernelGGL(sha_line_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (linek)
-        hipLaunchKernelGGL(sha_line_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
-    else if (carryk && hasher == 0)
+    if (carryk && hasher == 0)
         hipLaunchKernelGGL(sha_carry_kernel<5>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
     else if (carryk)
         hipLaunchKernelGGL(sha_carry_kernel<7>, g, dim3(256), lds, st, d_blocks, offsets, bst, cap_blk, digests, queue, thr, (setprio_mask() >> 2) & 3);
