@@ -261,8 +261,10 @@ def main():
         return packet_driver_line(a)
     if not a.depth:
         # config 2: depth 3 984 -> 1004 GB/s (three A/B pairs, scripts/ab_d23.txt): chunking of batch
-        # k+2 starts while batch k+1 hashes instead of after batch k's read-back
-        a.depth = 5 if a.workload == "config4" else 3
+        # k+2 starts while batch k+1 hashes instead of after batch k's read-back; round 5, primed steps:
+        # depth 4 1071-1103 (mean 1093) vs depth 3 1065-1102 (mean 1084) over three A/B files
+        primed_c2 = a.workload == "config2" and a.gpus == 1 and not a.no_prime and not a.serial
+        a.depth = 5 if a.workload == "config4" else 4 if primed_c2 else 3
     if not a.arena_slots:
         # config 5 keeps durable containers: a submit is refused while the worst-case closes of the
         # batches in flight (<= 2 x new bytes / maxSize + 1 per block and storer range, three 32-block
@@ -479,6 +481,16 @@ def main():
             step()
     drained.update(events=0, bytes=0)
     ctx.stage_times(reset=True)
+    # HDRF_LZ4_PHASES=1 with the profiling build (-DHDRF_LZ4_PROF, scripts/r05_lzp_c4.sh): the LZ4
+    # parse's per-phase shader clocks over the timed steps, inside the pipeline
+    lzp_lib = getattr(ctx.L, "hdrf_debug_lz4_prof", None) if os.environ.get("HDRF_LZ4_PHASES") else None
+    lzp_buf = None
+    if lzp_lib is not None:
+        import ctypes
+        lzp_lib.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+        lzp_buf = (ctypes.c_ulonglong * 16)()
+        ctx.synchronize()
+        lzp_lib(lzp_buf, 1)
     if node is not None:
         node.phase_ms = {}
     barrier()
@@ -495,6 +507,20 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     stage_ms = ctx.stage_times(reset=True)
+    lz4_phases = None
+    if lzp_buf is not None:
+        lzp_lib(lzp_buf, 1)
+        v = list(lzp_buf)
+        tot = sum(v[:8])
+        nbat, nfound, nchain = v[8], v[9], v[10]
+        names = ["search batch", "catch-up+literals", "chain top+extension", "tokens+table", "Cw load+compare",
+                 "-", "last literals", "-"]
+        per_ev = [nbat, nfound, nfound + nchain, nfound + nchain, nfound + nchain, 1, 1, 1]
+        lz4_phases = {"cycles_per_sequence": round(tot / max(1, nfound + nchain), 1),
+                      "search_batches": nbat, "found": nfound, "chained": nchain,
+                      "phases": {names[i]: {"share": round(v[i] / max(1, tot), 4),
+                                            "cyc_per_event": round(v[i] / max(1, per_ev[i]), 1)}
+                                 for i in range(8) if v[i]}}
     alone_ms = None
     alone = (a.alone or (a.workload == "config2" and not a.no_alone)) and not a.no_alone
     if alone and node is None and not a.serial and not host:
@@ -602,6 +628,8 @@ def main():
                      "chunking": chunking, "sha": sha, "place": place})
     if lz4:
         roofline["lz4"] = lz4
+        if lz4_phases:
+            lz4["phases_in_pipeline"] = lz4_phases
     if alone_ms is not None:
         # per-kernel figures of the untimed serial pass (not part of `value`)
         ra = {}
