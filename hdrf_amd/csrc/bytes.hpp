@@ -10,6 +10,14 @@ __device__ __forceinline__ uint32_t rd32u(const uint8_t *p)
     const HDRF_GLOBAL uint32_t *q = gptr<uint32_t>((const void *)(a & ~(uintptr_t)3));
     return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
 }
+// the 4 bytes at base + off, for a wave-uniform base: one global_load_dword with the base in SGPRs
+// and a 32-bit lane offset (the amdhsa target runs with unaligned global access enabled, so the
+// unaligned dword is a single load, against rd32u's aligned pair, 64-bit address and alignbyte)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t *base, uint32_t off)
+{
+    typedef uint32_t __attribute__((aligned(1))) u32u;
+    return *gptr<u32u>((const void *)(base + off));
+}
 __device__ __forceinline__ uint32_t rd8(const uint8_t *p) { return *(const HDRF_GLOBAL uint8_t *)p; }
 __device__ __forceinline__ void wr8(uint8_t *p, uint32_t v) { *(HDRF_GLOBAL uint8_t *)p = (uint8_t)v; }
 

@@ -91,26 +91,16 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
     }
     __builtin_amdgcn_s_waitcnt(0);
     asm volatile("" ::: "memory");
-    // entry h: position and tag
-    auto tget = [&](uint32_t h, uint32_t &tg) -> int {
-        if (u16) {
-            tg = (tabx[h >> 4] >> (2 * (h & 15))) & 3u;
-            return (int)tab16[h];
-        }
-        const uint32_t nb = (tabx[h >> 3] >> (4 * (h & 7))) & 15u;
-        tg = nb >> 2;
-        return (int)tab16[h] | (int)((nb & 3u) << 16);
-    };
     auto xupd = [&](uint32_t h, int p, uint32_t tg) -> uint32_t {   // old nibble / tag field, then p, tg
         if (u16) {
             const uint32_t sh = 2 * (h & 15);
             const uint32_t cur = (tabx[h >> 4] >> sh) & 3u;
-            if (cur != tg) atomicXor(&tabx[h >> 4], (cur ^ tg) << sh);   // lanes share words
-            return cur;
+            atomicXor(&tabx[h >> 4], (cur ^ tg) << sh);   // lanes share words; unconditional (no
+            return cur;                                    // exec-mask branch on the chain)
         }
         const uint32_t sh = 4 * (h & 7);
         const uint32_t cur = (tabx[h >> 3] >> sh) & 15u, want = (((uint32_t)p >> 16) & 3u) | (tg << 2);
-        if (cur != want) atomicXor(&tabx[h >> 3], (cur ^ want) << sh);
+        atomicXor(&tabx[h >> 3], (cur ^ want) << sh);
         return cur;
     };
     auto tput = [&](uint32_t h, int p, uint32_t tg) {   // no read of the entry: two non-returning
@@ -153,7 +143,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         // the last word instead; no such lane's bytes are ever used (every use is bounded by
         // mflimit / matchlimit, at least 5 bytes before n), so one clamp replaces the guards.
         const int nm4 = n - 4;
-        auto wload = [&](int at) -> uint32_t { return rd32u(src + min(at + 4 * l, nm4)); };
+        auto wload = [&](int at) -> uint32_t { return ld32u(src, (uint32_t)min(at + 4 * l, nm4)); };
         auto lane_word = [&](uint32_t w, int o) -> uint32_t {   // bytes [o, o + 4) of a window
             const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((o >> 2) << 2, (int)w);
             const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) + 1) << 2, (int)w);
@@ -177,7 +167,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             bool inwin = swok && fip >= sb && last_at - sb <= 251;
             if (!inwin && last_at - fip <= 251) { Sw = wload(fip); sb = fip; swok = true; inwin = true; }
             const uint32_t vw = lane_word(Sw, (valid && inwin) ? ipl - sb : 0);
-            const uint32_t v = !valid ? 0u : inwin ? vw : rd32u(src + ipl);
+            const uint32_t v = !valid ? 0u : inwin ? vw : ld32u(src, (uint32_t)ipl);
             const uint32_t h = hash(v);
             const unsigned long long vmask = ballot64(valid);
             const int nv = vmask == ~0ull ? 64 : __builtin_ctzll(~vmask);   // valid lanes are a prefix
@@ -186,14 +176,28 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             // tags into the entries and reading them back.  Equal hashes: attempt i reads the
             // position of the last earlier attempt with its hash (else the pre-batch entry), found
             // with one ballot per hash bit; each hash keeps its last attempt up to the first match.
+            // The entry's two reads, the lane-id scatter and its read-back issue back to back (LDS
+            // keeps a wave's operations in order) and are decoded after one round trip.
             const uint32_t vt = tagof(v);
-            int old = 0;
-            uint32_t otg = 0;
-            if (valid) old = tget(h, otg);
-            asm volatile("" ::: "memory");
-            if (valid) tab16[h] = (unsigned short)l;
-            asm volatile("" ::: "memory");
-            const uint32_t tg = valid ? (uint32_t)tab16[h] : 0u;
+            uint32_t r16 = 0, rx = 0, tg = 0;
+            if (valid) {
+                r16 = tab16[h];
+                rx = tabx[u16 ? h >> 4 : h >> 3];
+                asm volatile("" ::: "memory");
+                tab16[h] = (unsigned short)l;
+                asm volatile("" ::: "memory");
+                tg = tab16[h];
+            }
+            int old;
+            uint32_t otg;
+            if (u16) {
+                otg = (rx >> (2 * (h & 15))) & 3u;
+                old = (int)r16;
+            } else {
+                const uint32_t nb = (rx >> (4 * (h & 7))) & 15u;
+                otg = nb >> 2;
+                old = (int)r16 | (int)((nb & 3u) << 16);
+            }
             const bool collide = ballot64(valid && tg != (uint32_t)l) != 0;
             asm volatile("" ::: "memory");
             if (valid) tab16[h] = (unsigned short)old;     // (the high parts and tags were not touched)
@@ -219,7 +223,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 if (below) { ref = pipl; cv = pv; known = true; }
             }
             const bool in = valid && ref + kMaxDist >= ipl;
-            if (in && !known && otg == vt) cv = rd32u(src + ref);   // ref is a position < n
+            if (in && !known && otg == vt) cv = ld32u(src, (uint32_t)ref);   // ref is a position < n
             const bool ok = in && cv == v;
             const unsigned long long okm = ballot64(ok);
             LZN(0);
@@ -240,6 +244,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 int tpos;
                 uint32_t tok;
                 bool fast = ip - anchor <= 64 && ip >= 64 && mref >= 64;
+                int plit = 0, plito = 0;                   // fast path: literals stored with the token
+                uint32_t plitv = 0;
                 if (fast) {
                     // one window pair at ip - 64: catch-up, literals and the first extension step
                     const int wb0 = ip - 64, d0 = mref - ip;
@@ -265,7 +271,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         else tok = (uint32_t)lit << 4;
                         const int o = anchor + l - wb0;    // literal byte l from the window
                         const uint32_t wv = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) & 63) << 2, (int)Fw);
-                        if (l < lit) wr8(out + op + l, wv >> (8 * (o & 3)));
+                        plitv = wv >> (8 * (o & 3)); plit = lit; plito = op;
                         op += lit;
                         have = true;
                         hwb = wb0;
@@ -297,24 +303,30 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     ip = (int)rdfirst((uint32_t)ip); mref = (int)rdfirst((uint32_t)mref);
                     op = (int)rdfirst((uint32_t)op); anchor = (int)rdfirst((uint32_t)anchor);
                     tpos = (int)rdfirst((uint32_t)tpos); tok = rdfirst(tok); hwb = (int)rdfirst((uint32_t)hwb);
-                    if (l == 0) { wr8(out + op, (uint32_t)(ip - mref)); wr8(out + op + 1, (uint32_t)(ip - mref) >> 8); }
+                    // the offset is stored with the token after the extension: a store in flight here
+                    // would be waited for by the window reads' vmcnt waits (gfx9 counts stores in vmcnt)
+                    const int opo = op;
+                    const uint32_t offv = (uint32_t)(ip - mref);
                     op += 2;
                     const int dr = mref - ip;
                     int wb, l0;                            // lanes below l0: the minmatch (and before)
                     if (!have) { Fw = wload(ip); Rw = wload(mref); wb = ip; l0 = 1; }
                     else { wb = hwb; l0 = (ip + 4 - hwb) >> 2; }
                     anchor = ip + 4;
-                    for (;;) {                             // match extension
+                    for (bool next = false;; next = true) {   // match extension
+                        // the next window pair is loaded at the top, so every exit from the loop has
+                        // waited for the pair it compared (no window load is still pending after it,
+                        // so the reads of Fw below do not wait for the sequence's stores)
+                        if (next) { wb += 256; l0 = 0; Fw = wload(wb); Rw = wload(wb + dr); }
                         uint32_t x = Fw ^ Rw;
-                        bool stop = false;
-                        if (wb + 256 > matchlimit) {       // (uniform) the window reaches matchlimit
-                            const int p = wb + 4 * l;
-                            stop = p + 4 > matchlimit;
-                            if (stop) x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
+                        if (wb + 256 > matchlimit) {       // (uniform) the window reaches matchlimit:
+                            const int p = wb + 4 * l;      // a lane past it stops (x made non-zero
+                            if (p + 4 > matchlimit)        // from the first byte at matchlimit on)
+                                x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
                         }
-                        if (l < l0) { x = 0u; stop = false; }
-                        const unsigned long long mm = ballot64(x != 0u || stop);
-                        if (!mm) { wb += 256; l0 = 0; Fw = wload(wb); Rw = wload(wb + dr); continue; }
+                        if (l < l0) x = 0u;
+                        const unsigned long long mm = ballot64(x != 0u);
+                        if (!mm) continue;
                         const int L = __builtin_ctzll(mm);
                         const uint32_t xl = rdlane(x, L);
                         ip = wb + 4 * L + (xl ? (__builtin_ctz(xl) >> 3) : 4);
@@ -336,7 +348,12 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     } else {
                         tok += (uint32_t)ml;
                     }
-                    if (l == 0) wr8(out + tpos, tok);
+                    // the sequence's token, offset and (fast path) literal bytes
+                    auto put_seq = [&]() {
+                        if (l == 0) { wr8(out + tpos, tok); wr8(out + opo, offv); wr8(out + opo + 1, offv >> 8); }
+                        if (plit) { if (l < plit) wr8(out + plito + l, plitv); plit = 0; }
+                    };
+                    put_seq();
                     if (ip > mflimit) { anchor = ip; goto last_literals; }
                     // fill table; test next position (its bytes are in the forward window unless
                     // the match ended right at a window start)
@@ -351,8 +368,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         v2 = (uint32_t)(pA >> (8 * (o2 & 3)));
                         v0 = (uint32_t)(pB >> (8 * ((o2 + 2) & 3)));
                     } else {
-                        v2 = rdfirst(rd32u(src + ip - 2));
-                        v0 = rdfirst(rd32u(src + ip));
+                        v2 = rdfirst(ld32u(src, (uint32_t)(ip - 2)));
+                        v0 = rdfirst(ld32u(src, (uint32_t)ip));
                     }
                     // table: [h2] = ip - 2, r = [h0], [h0] = ip.  Distinct hashes: lanes 0 and 1
                     // do the two slots in one pass; equal hashes: r is ip - 2.
