@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 5: PMC record of the LZ4 parse on config 4 (one step, no CPU leg), HEAD vs the lz4.hip before
-# round 5's chain changes (HDRF_LIB_PATH=hdrf_amd/_build_prev/libhdrf.so): wave-state and issue
+# Round 5: PMC record of the LZ4 parse on config 4 (one step, no CPU leg), HEAD (and, when
+# hdrf_amd/_build_prev exists, the lz4.hip before round 5's chain changes): wave-state and issue
 # counters per lz4_seg_kernel launch, and VALU issue per SIMD-cycle = SQ_INSTS_VALU / (GRBM_GUI_ACTIVE
 # / 8 XCDs x 1024 SIMDs).  One counter group per rocprofv3 run, each under its own kill timer.
 set -o pipefail
@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VMEM SQ_INSTS_LDS SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  for b in head prev; do
+  for b in head $( [ -f $R/hdrf_amd/_build_prev/libhdrf.so ] && echo prev ); do
     if [ $b = prev ]; then E="HDRF_LIB_PATH=$R/hdrf_amd/_build_prev/libhdrf.so"; else E="X=head"; fi
     (cd /tmp && env $E timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/${b}_p$i -o run -- python3 $R/bench.py --workload config4 --steps 1 --warmup 0 --no-cpu --no-alone --no-sub > $OUT/${b}_p$i.log 2>&1) || { echo "pmc pass $i $b ($grp) failed"; tail -5 $OUT/${b}_p$i.log; exit 1; }
     echo "pass $i $b done"
