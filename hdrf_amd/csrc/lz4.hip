@@ -251,14 +251,19 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     const int wb0 = ip - 64, d0 = mref - ip;
                     Fw = wload(wb0);
                     Rw = wload(wb0 + d0);
-                    const uint32_t x = Fw ^ Rw;
-                    int hstop = -1;                        // highest stop byte in [wb0, ip)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int pos = wb0 + 4 * l + j;
-                        const bool st = l < 16 && (pos < anchor || pos + d0 < 0 || ((x >> (8 * j)) & 0xffu) != 0u);
-                        const unsigned long long bm = ballot64(st);
-                        if (bm) hstop = max(hstop, 4 * (63 - __builtin_clzll(bm)) + j);
+                    // highest stop byte in [wb0, ip) (lanes 0-15): a byte that differs, or one before
+                    // the anchor or before the segment start on the reference side (bytes j < lo
+                    // of the lane's word) — one ballot, then the top stop byte of the top lane
+                    uint32_t sx = Fw ^ Rw;
+                    {
+                        const int p0 = wb0 + 4 * l, lo = max(anchor - p0, -(p0 + d0));
+                        if (lo > 0) sx |= lo >= 4 ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
+                    }
+                    const unsigned long long bm = ballot64(l < 16 && sx != 0u);
+                    int hstop = -1;
+                    if (bm) {
+                        const int L = 63 - __builtin_clzll(bm);
+                        hstop = 4 * L + ((31 - __builtin_clz(rdlane(sx, L))) >> 3);
                     }
                     if (hstop < 0) {
                         fast = false;                      // 64 equal bytes: the general catch-up
@@ -334,7 +339,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         break;
                     }
                     LZP(2);
-                    int ml = ip - anchor;
+                    const uint32_t Nw = wload(ip);        // the next position's window: in flight
+                    int ml = ip - anchor;                 // under the stores and the table update
                     if (ml >= 15) {
                         tok += 15;
                         ml -= 15;
@@ -373,7 +379,6 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     }
                     // table: [h2] = ip - 2, r = [h0], [h0] = ip.  Distinct hashes: lanes 0 and 1
                     // do the two slots in one pass; equal hashes: r is ip - 2.
-                    const uint32_t Nw = wload(ip);        // in flight under the table update
                     const uint32_t h2 = hash(v2), h0 = hash(v0), t2 = tagof(v2), t0 = tagof(v0);
                     int r = 0;
                     uint32_t rt = 0;
