@@ -990,10 +990,11 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     // wave per SIMD so SHA keeps its wave slots (measured +1.5-2% on the config-2 bench; alone,
     // place wants full occupancy).  Under compressor 2 the reservation is 16 KiB: place then fits on
     // a CU as soon as one LZ4 wave of a draining pass leaves it (config 4: 36.96 / 37.01 vs 35.92 /
-    // 35.91 GB/s with 40 KiB; 24 KiB 36.5, 9 KiB 36.4; profiles/r02_c4_place_ab.txt).
-    // HDRF_PLACE_LDS overrides the reservation (bytes).
+    // 35.91 GB/s with 40 KiB; 24 KiB 36.5, 9 KiB 36.4; profiles/r02_c4_place_ab.txt).  Round 5, after
+    // the LZ4 parse got shorter: 8 KiB 47.31 / 47.27 vs 16 KiB 47.13 / 47.10, 24 KiB 46.68 / 46.74
+    // (profiles/r05_c4knobs_ab.txt), so 8 KiB.  HDRF_PLACE_LDS overrides the reservation (bytes).
     static const int place_lds_env = [] { const char *e = getenv("HDRF_PLACE_LDS"); return e ? atoi(e) : -1; }();
-    const int place_lds = place_lds_env >= 0 ? place_lds_env : (c.compressor == 2 ? 16384 : 40960);
+    const int place_lds = place_lds_env >= 0 ? place_lds_env : (c.compressor == 2 ? 8192 : 40960);
     if (ctx->nsub > ctx->nwait) P.place_lds = place_lds;
     // HDRF_PLACE_DEEP=1: the place copy keeps four 16-B words per thread in flight instead of two
     static const int place_deep_env = [] { const char *e = getenv("HDRF_PLACE_DEEP"); return e ? atoi(e) : 0; }();
