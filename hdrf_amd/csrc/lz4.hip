@@ -302,7 +302,10 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     have = false;
                 }
                 LZP(1);
-                for (;;) {                                 // _next_match
+                // _next_match: one sequence per iteration, a single exit at the loop condition (the
+                // compiler then keeps the chain a plain loop instead of a dispatch over exit states)
+                bool fin = false;                          // the match reached mflimit: last literals
+                for (bool chain = true; chain;) {
                     // the parse state is wave-uniform: keep it in scalar registers so the
                     // branches on it are scalar branches, not exec-mask regions
                     ip = (int)rdfirst((uint32_t)ip); mref = (int)rdfirst((uint32_t)mref);
@@ -318,25 +321,29 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     if (!have) { Fw = wload(ip); Rw = wload(mref); wb = ip; l0 = 1; }
                     else { wb = hwb; l0 = (ip + 4 - hwb) >> 2; }
                     anchor = ip + 4;
-                    for (bool next = false;; next = true) {   // match extension
-                        // the next window pair is loaded at the top, so every exit from the loop has
-                        // waited for the pair it compared (no window load is still pending after it,
-                        // so the reads of Fw below do not wait for the sequence's stores)
+                    // match extension: the next window pair is loaded at the top of an iteration, so
+                    // the loop's exit has waited for the pair it compared (no window load is still
+                    // pending after it, so the reads of Fw below do not wait for the sequence's stores)
+                    uint32_t x;
+                    unsigned long long mm;
+                    bool next = false;
+                    do {
                         if (next) { wb += 256; l0 = 0; Fw = wload(wb); Rw = wload(wb + dr); }
-                        uint32_t x = Fw ^ Rw;
+                        x = Fw ^ Rw;
                         if (wb + 256 > matchlimit) {       // (uniform) the window reaches matchlimit:
                             const int p = wb + 4 * l;      // a lane past it stops (x made non-zero
                             if (p + 4 > matchlimit)        // from the first byte at matchlimit on)
                                 x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
                         }
                         if (l < l0) x = 0u;
-                        const unsigned long long mm = ballot64(x != 0u);
-                        if (!mm) continue;
+                        mm = ballot64(x != 0u);
+                        next = true;
+                    } while (!mm);
+                    {
                         const int L = __builtin_ctzll(mm);
                         const uint32_t xl = rdlane(x, L);
                         ip = wb + 4 * L + (xl ? (__builtin_ctz(xl) >> 3) : 4);
                         mref = ip + dr;
-                        break;
                     }
                     LZP(2);
                     const uint32_t Nw = wload(ip);        // the next position's window: in flight
@@ -348,71 +355,74 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         for (int k = l; k < 2 * n510; k += 64) wr8(out + op + k, 255);
                         op += 2 * n510;
                         ml -= 510 * n510;
-                        if (ml >= 255) { if (l == 0) wr8(out + op, 255); op++; ml -= 255; }
-                        if (l == 0) wr8(out + op, (uint32_t)ml);
+                        if (ml >= 255) { wr8(out + op, 255); op++; ml -= 255; }
+                        wr8(out + op, (uint32_t)ml);
                         op++;
                     } else {
                         tok += (uint32_t)ml;
                     }
-                    // the sequence's token, offset and (fast path) literal bytes
-                    auto put_seq = [&]() {
-                        if (l == 0) { wr8(out + tpos, tok); wr8(out + opo, offv); wr8(out + opo + 1, offv >> 8); }
-                        if (plit) { if (l < plit) wr8(out + plito + l, plitv); plit = 0; }
-                    };
-                    put_seq();
-                    if (ip > mflimit) { anchor = ip; goto last_literals; }
-                    // fill table; test next position (its bytes are in the forward window unless
-                    // the match ended right at a window start)
-                    const int o2 = ip - 2 - wb;
-                    uint32_t v2, v0;
-                    if (o2 >= 0 && ((o2 + 2) >> 2) + 1 <= 63) {
-                        // three lanes of the window into scalar registers, the two words by 64-bit
-                        // scalar shifts (the hashes below stay scalar too: no VALU round trip)
-                        const int a2 = o2 >> 2, a0 = (o2 + 2) >> 2;
-                        const uint64_t pA = ((uint64_t)rdlane(Fw, a2 + 1) << 32) | rdlane(Fw, a2);
-                        const uint64_t pB = a0 == a2 ? pA : ((uint64_t)rdlane(Fw, a0 + 1) << 32) | (pA >> 32);
-                        v2 = (uint32_t)(pA >> (8 * (o2 & 3)));
-                        v0 = (uint32_t)(pB >> (8 * ((o2 + 2) & 3)));
+                    // the sequence's token, offset and (fast path) literal bytes: uniform bytes at
+                    // uniform addresses, stored by every lane (one coalesced write, no exec-mask
+                    // region on the chain)
+                    wr8(out + tpos, tok); wr8(out + opo, offv); wr8(out + opo + 1, offv >> 8);
+                    if (plit) { if (l < plit) wr8(out + plito + l, plitv); plit = 0; }
+                    chain = false;
+                    if (ip > mflimit) {
+                        fin = true;
                     } else {
-                        v2 = rdfirst(ld32u(src, (uint32_t)(ip - 2)));
-                        v0 = rdfirst(ld32u(src, (uint32_t)ip));
-                    }
-                    // table: [h2] = ip - 2, r = [h0], [h0] = ip.  Distinct hashes: lanes 0 and 1
-                    // do the two slots in one pass; equal hashes: r is ip - 2.
-                    const uint32_t h2 = hash(v2), h0 = hash(v0), t2 = tagof(v2), t0 = tagof(v0);
-                    int r = 0;
-                    uint32_t rt = 0;
-                    asm volatile("" ::: "memory");
-                    if (h2 == h0) {
-                        if (l == 0) tput(h0, ip, t0);
-                        r = ip - 2;
-                        rt = t2;
-                    } else {
-                        uint32_t ot = 0;
-                        if (l < 2) r = tswap(l == 0 ? h2 : h0, l == 0 ? ip - 2 : ip, l == 0 ? t2 : t0, ot);
-                        r = (int)rdlane((uint32_t)r, 1);
-                        rt = rdlane(ot, 1);
-                    }
-                    asm volatile("" ::: "memory");
-                    LZP(3);
-                    if (r + kMaxDist >= ip) {
-                        if (rt == t0) {                    // a tag miss cannot chain: no load
-                            const uint32_t Cw = wload(r);  // one round trip
-                            const bool chain = rdlane(Cw, 0) == v0;
-                            LZP(4);
-                            if (chain) {
-                                LZN(2);
-                                mref = r;
-                                tpos = op++;
-                                tok = 0;
-                                Fw = Nw; Rw = Cw; have = true; hwb = ip;
-                                continue;
-                            }
+                        // fill table; test next position (its bytes are in the forward window unless
+                        // the match ended right at a window start)
+                        const int o2 = ip - 2 - wb;
+                        uint32_t v2, v0;
+                        if (o2 >= 0 && ((o2 + 2) >> 2) + 1 <= 63) {
+                            // three lanes of the window into scalar registers, the two words by 64-bit
+                            // scalar shifts (the hashes below stay scalar too: no VALU round trip)
+                            const int a2 = o2 >> 2, a0 = (o2 + 2) >> 2;
+                            const uint64_t pA = ((uint64_t)rdlane(Fw, a2 + 1) << 32) | rdlane(Fw, a2);
+                            const uint64_t pB = a0 == a2 ? pA : ((uint64_t)rdlane(Fw, a0 + 1) << 32) | (pA >> 32);
+                            v2 = (uint32_t)(pA >> (8 * (o2 & 3)));
+                            v0 = (uint32_t)(pB >> (8 * ((o2 + 2) & 3)));
+                        } else {
+                            v2 = rdfirst(ld32u(src, (uint32_t)(ip - 2)));
+                            v0 = rdfirst(ld32u(src, (uint32_t)ip));
                         }
-                        Sw = Nw; sb = ip; swok = true;     // the search after the break starts in it
+                        // table: [h2] = ip - 2, r = [h0], [h0] = ip.  Distinct hashes: lanes 0 and 1
+                        // do the two slots in one pass; equal hashes: r is ip - 2.
+                        const uint32_t h2 = hash(v2), h0 = hash(v0), t2 = tagof(v2), t0 = tagof(v0);
+                        int r = 0;
+                        uint32_t rt = 0;
+                        asm volatile("" ::: "memory");
+                        if (h2 == h0) {
+                            if (l == 0) tput(h0, ip, t0);
+                            r = ip - 2;
+                            rt = t2;
+                        } else {
+                            uint32_t ot = 0;
+                            if (l < 2) r = tswap(l == 0 ? h2 : h0, l == 0 ? ip - 2 : ip, l == 0 ? t2 : t0, ot);
+                            r = (int)rdlane((uint32_t)r, 1);
+                            rt = rdlane(ot, 1);
+                        }
+                        asm volatile("" ::: "memory");
+                        LZP(3);
+                        const bool near = r + kMaxDist >= ip;
+                        uint32_t Cw = 0;
+                        if (near && rt == t0) {            // a tag miss cannot chain: no load
+                            Cw = wload(r);                 // one round trip
+                            chain = rdlane(Cw, 0) == v0;
+                        }
+                        LZP(4);
+                        if (chain) {
+                            LZN(2);
+                            mref = r;
+                            tpos = op++;
+                            tok = 0;
+                            Fw = Nw; Rw = Cw; have = true; hwb = ip;
+                        } else if (near) {
+                            Sw = Nw; sb = ip; swok = true; // the search after the break starts in it
+                        }
                     }
-                    break;
                 }
+                if (fin) { anchor = ip; break; }           // last literals
                 anchor = ip++;
                 fip = ip;
                 attempts = (1 << 6) + 3;
@@ -425,7 +435,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             m = min(64, 2 * m);
         }
     }
-last_literals:
+
     LZP(5);
     {
         int run = n - anchor;
