@@ -150,9 +150,11 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
         };
         uint32_t Fw = 0, Rw = 0, Sw = 0;
-        bool have = false, swok = false;
+        bool swok = false;
         int hwb = 0, sb = 0;
-        for (;;) {
+        // one exit, at the loop condition (as the chain loop below): the compiler keeps the parse
+        // a plain loop nest instead of a dispatch over exit states
+        for (bool more = true; more;) {
             // ---- match search: a batch of m attempts at once ------------------------------
             // attempt l advances by step_l = (a0 + l) >> 6, which takes only the values q and
             // q + 1 inside one batch, so the attempt positions have a closed form (no scan)
@@ -278,7 +280,6 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         const uint32_t wv = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) & 63) << 2, (int)Fw);
                         plitv = wv >> (8 * (o & 3)); plit = lit; plito = op;
                         op += lit;
-                        have = true;
                         hwb = wb0;
                     }
                 }
@@ -299,7 +300,9 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     else tok = (uint32_t)lit << 4;
                     wave_copy(out + op, src + anchor, lit);
                     op += lit;
-                    have = false;
+                    Fw = wload(ip);                        // the window pair at the match
+                    Rw = wload(mref);
+                    hwb = ip;
                 }
                 LZP(1);
                 // _next_match: one sequence per iteration, a single exit at the loop condition (the
@@ -317,9 +320,9 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     const uint32_t offv = (uint32_t)(ip - mref);
                     op += 2;
                     const int dr = mref - ip;
-                    int wb, l0;                            // lanes below l0: the minmatch (and before)
-                    if (!have) { Fw = wload(ip); Rw = wload(mref); wb = ip; l0 = 1; }
-                    else { wb = hwb; l0 = (ip + 4 - hwb) >> 2; }
+                    // the window pair (Fw, Rw) starts at hwb <= ip; lanes below l0 hold the minmatch
+                    // (and the bytes before it)
+                    int wb = hwb, l0 = (ip + 4 - hwb) >> 2;
                     anchor = ip + 4;
                     // match extension: the next window pair is loaded at the top of an iteration, so
                     // the loop's exit has waited for the pair it compared (no window load is still
@@ -416,23 +419,28 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                             mref = r;
                             tpos = op++;
                             tok = 0;
-                            Fw = Nw; Rw = Cw; have = true; hwb = ip;
+                            Fw = Nw; Rw = Cw; hwb = ip;
                         } else if (near) {
                             Sw = Nw; sb = ip; swok = true; // the search after the break starts in it
                         }
                     }
                 }
-                if (fin) { anchor = ip; break; }           // last literals
-                anchor = ip++;
-                fip = ip;
-                attempts = (1 << 6) + 3;
-                m = kLzFirstBatch;
-                continue;
+                if (fin) {                                 // last literals
+                    anchor = ip;
+                    more = false;
+                } else {
+                    anchor = ip++;
+                    fip = ip;
+                    attempts = (1 << 6) + 3;
+                    m = kLzFirstBatch;
+                }
+            } else if (nv < m) {
+                more = false;                              // the next attempt passes mflimit
+            } else {
+                fip = (int)rdlane((uint32_t)(ipl + step), m - 1);
+                attempts = a0 + m;
+                m = min(64, 2 * m);
             }
-            if (nv < m) break;                             // the next attempt passes mflimit
-            fip = (int)rdlane((uint32_t)(ipl + step), m - 1);
-            attempts = a0 + m;
-            m = min(64, 2 * m);
         }
     }
 
