@@ -245,54 +245,53 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                 int mref = (int)rdlane((uint32_t)ref, istar);
                 int tpos;
                 uint32_t tok;
-                bool fast = ip - anchor <= 64 && ip >= 64 && mref >= 64;
+                const bool fast = ip - anchor <= 64 && ip >= 64 && mref >= 64;
                 int plit = 0, plito = 0;                   // fast path: literals stored with the token
                 uint32_t plitv = 0;
+                // one window pair at ip - 64 (fast case): catch-up, literals and the first extension
+                // step; hstop = the highest stop byte in [wb0, ip) (lanes 0-15): a byte that differs,
+                // or one before the anchor or before the segment start on the reference side (bytes
+                // j < lo of the lane's word) — one ballot, then the top stop byte of the top lane.
+                // No stop byte (64 equal bytes) or not fast: the general catch-up.  (One if / else
+                // on hstop, not two ifs on a flag.)
+                const int wb0 = ip - 64, d0 = mref - ip;
+                int hstop = -1;
                 if (fast) {
-                    // one window pair at ip - 64: catch-up, literals and the first extension step
-                    const int wb0 = ip - 64, d0 = mref - ip;
                     Fw = wload(wb0);
                     Rw = wload(wb0 + d0);
-                    // highest stop byte in [wb0, ip) (lanes 0-15): a byte that differs, or one before
-                    // the anchor or before the segment start on the reference side (bytes j < lo
-                    // of the lane's word) — one ballot, then the top stop byte of the top lane
                     uint32_t sx = Fw ^ Rw;
                     {
                         const int p0 = wb0 + 4 * l, lo = max(anchor - p0, -(p0 + d0));
                         if (lo > 0) sx |= lo >= 4 ? 0xffffffffu : ((1u << (8 * lo)) - 1u);
                     }
                     const unsigned long long bm = ballot64(l < 16 && sx != 0u);
-                    int hstop = -1;
                     if (bm) {
                         const int L = 63 - __builtin_clzll(bm);
                         hstop = 4 * L + ((31 - __builtin_clz(rdlane(sx, L))) >> 3);
                     }
-                    if (hstop < 0) {
-                        fast = false;                      // 64 equal bytes: the general catch-up
-                    } else {
-                        const int back = 63 - hstop;
-                        ip -= back; mref -= back;
-                        tpos = op++;
-                        const int lit = ip - anchor;
-                        if (lit >= 15) { tok = 15u << 4; op = put_len(out, op, lit - 15); }
-                        else tok = (uint32_t)lit << 4;
-                        const int o = anchor + l - wb0;    // literal byte l from the window
-                        const uint32_t wv = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) & 63) << 2, (int)Fw);
-                        plitv = wv >> (8 * (o & 3)); plit = lit; plito = op;
-                        op += lit;
-                        hwb = wb0;
-                    }
                 }
-                if (!fast) {
+                if (hstop >= 0) {
+                    const int back = 63 - hstop;
+                    ip -= back; mref -= back;
+                    tpos = op++;
+                    const int lit = ip - anchor;
+                    if (lit >= 15) { tok = 15u << 4; op = put_len(out, op, lit - 15); }
+                    else tok = (uint32_t)lit << 4;
+                    const int o = anchor + l - wb0;        // literal byte l from the window
+                    const uint32_t wv = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) & 63) << 2, (int)Fw);
+                    plitv = wv >> (8 * (o & 3)); plit = lit; plito = op;
+                    op += lit;
+                    hwb = wb0;
+                } else {
                     // ---- catch up ------------------------------------------------------
-                    for (;;) {
+                    int back;
+                    do {
                         const int k = l + 1;
                         const bool c = ip - k >= anchor && mref - k >= 0 && rd8(src + ip - k) == rd8(src + mref - k);
                         const unsigned long long bad = ballot64(!c);
-                        const int back = bad ? __builtin_ctzll(bad) : 64;
+                        back = bad ? __builtin_ctzll(bad) : 64;
                         ip -= back; mref -= back;
-                        if (back < 64) break;
-                    }
+                    } while (back == 64);
                     // ---- literals ------------------------------------------------------
                     tpos = op++;
                     const int lit = ip - anchor;
