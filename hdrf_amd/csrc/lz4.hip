@@ -150,8 +150,9 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
         };
         uint32_t Fw = 0, Rw = 0, Sw = 0;
-        bool swok = false;
-        int hwb = 0, sb = 0;
+        // sb: the search window Sw's base; far below every position while Sw holds nothing, so one
+        // unsigned compare tests "the batch lies in the window"
+        int hwb = 0, sb = -(1 << 30);
         // one exit, at the loop condition (as the chain loop below): the compiler keeps the parse
         // a plain loop nest instead of a dispatch over exit states
         for (bool more = true; more;) {
@@ -166,8 +167,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             const int ipl = fip + l * q + max(0, l - (64 - rr));       // this lane's attempt
             const bool valid = l < m && ipl + step <= mflimit;
             const int last_at = fip + (m - 1) * q + max(0, m - 1 - (64 - rr));   // lane m-1's attempt
-            bool inwin = swok && fip >= sb && last_at - sb <= 251;
-            if (!inwin && last_at - fip <= 251) { Sw = wload(fip); sb = fip; swok = true; inwin = true; }
+            bool inwin = (uint32_t)(last_at - sb) <= 251u;     // (fip >= sb: last_at >= fip)
+            if (!inwin && last_at - fip <= 251) { Sw = wload(fip); sb = fip; inwin = true; }
             const uint32_t vw = lane_word(Sw, (valid && inwin) ? ipl - sb : 0);
             const uint32_t v = !valid ? 0u : inwin ? vw : ld32u(src, (uint32_t)ipl);
             const uint32_t h = hash(v);
@@ -366,7 +367,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     // the sequence's token, offset and (fast path) literal bytes: uniform bytes at
                     // uniform addresses, stored by every lane (one coalesced write, no exec-mask
                     // region on the chain)
-                    wr8(out + tpos, tok); wr8(out + opo, offv); wr8(out + opo + 1, offv >> 8);
+                    wr8(out + (uint32_t)tpos, tok); wr8(out + (uint32_t)opo, offv); wr8(out + (uint32_t)opo + 1, offv >> 8);
                     if (plit) { if (l < plit) wr8(out + plito + l, plitv); plit = 0; }
                     chain = false;
                     if (ip > mflimit) {
@@ -376,7 +377,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         // the match ended right at a window start)
                         const int o2 = ip - 2 - wb;
                         uint32_t v2, v0;
-                        if (o2 >= 0 && ((o2 + 2) >> 2) + 1 <= 63) {
+                        if ((uint32_t)o2 <= 249u) {            // o2 >= 0, lane (o2 + 2) / 4 + 1 <= 63
                             // three lanes of the window into scalar registers, the two words by 64-bit
                             // scalar shifts (the hashes below stay scalar too: no VALU round trip)
                             const int a2 = o2 >> 2, a0 = (o2 + 2) >> 2;
@@ -420,7 +421,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                             tok = 0;
                             Fw = Nw; Rw = Cw; hwb = ip;
                         } else if (near) {
-                            Sw = Nw; sb = ip; swok = true; // the search after the break starts in it
+                            Sw = Nw; sb = ip;              // the search after the break starts in it
                         }
                     }
                 }
