@@ -6,7 +6,7 @@ Workload (per GPU): a synthetic corpus of 512 blocks x 128 MiB (64 GiB) resident
 duplicates).  One step = one DataNode reducing the whole corpus in block
 order from a fresh index: window-max chunking -> SHA-1 -> GPU index (exact HDRF dedup
 semantics) -> container placement + gather into the container arena, in batches of 32
-blocks (4 GiB), three batches in flight.  value = logical bytes reduced per second over all ranks (GB = 1e9 B).
+blocks (4 GiB), four batches in flight, steps back to back (hdrf_reset_async).  value = logical bytes reduced per second over all ranks (GB = 1e9 B).
 
 Multi-GPU (`torch.distributed.run`, BASELINE config 3): the GPUs of the node are ranks of ONE
 reduction, as the DataNodes of one host share one Redis, allocator and chunkDir in the reference
@@ -103,7 +103,7 @@ def parse():
     ap.add_argument("--keep-recipes", type=int, default=1,
                     help="storeDB's recipe SET per block into the device recipe store (default 1, as the reference)")
     ap.add_argument("--depth", type=int, default=0,
-                    help="batches in flight (1..5, pipelined mode; default 3, config4 5: the LZ4 passes of two "
+                    help="batches in flight (1..5, pipelined mode; default 4 for the primed config-2 line, else 3; config4 5: the LZ4 passes of two "
                          "batches overlap while the front halves of the next ones run)")
     ap.add_argument("--alone", action="store_true",
                     help="after the timed region, one untimed serial pass: per-kernel rooflines without co-running "
@@ -711,6 +711,7 @@ def main():
                                           " + Lz4Codec on closed containers" if compressor == 2 else "",
                                           " + recipes (device store)" if a.keep_recipes else ", no recipes"),
                            "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks_per_gpu": B,
+                           "batches_in_flight": a.depth, "steps_back_to_back": bool(primed),
                            "parallelism": "dp%d: blocks sharded by rank; one index partitioned by digest prefix"
                                           % world},
                 "roofline": roofline, "cpu_baseline": cpu, "dedup": dedup, "stages": stages}
