@@ -605,10 +605,10 @@ def main():
                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "avg_launch_ms": round(lz_ms, 4),
                "algorithmic_bytes_per_launch": int(lz_bytes),
                "traffic": pmc.get("lz4_seg_kernel<false>", {}).get("hbm_bytes_per_launch"),
-               "limiter": "latency of the greedy parse's per-sequence chain (one wave per 261,100-B segment; "
-                          "104 VGPRs allow 4 waves/SIMD, the 10 KiB tagged LDS table 16/CU; VALU issue ~0.08 per "
-                          "cycle per SIMD, ~half of wave time at s_waitcnt on table round trips and candidate "
-                          "loads); profiles/r02_lz4_phases.txt, profiles/r04_lz4_pmc_ab.txt"}
+               "limiter": "latency of the greedy parse's per-sequence dependent chain (one wave per 261,100-B "
+                          "segment; the 10 KiB tagged LDS table allows 16 waves/CU; 99 VGPRs; VALU issue 0.093 and "
+                          "SALU 0.125 per SIMD-cycle, half of wave time at s_waitcnt on the table round trip and the "
+                          "candidate load); profiles/r05_lz4_pmc.txt, profiles/r05_lz4_phases_c4.txt"}
     # the line's roofline: the dominant kernel of the critical chain
     top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place, "B2: store": place,
            "B: index": place, "L: LZ4": lz4, "B2: arena copy": place}.get(crit)
