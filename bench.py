@@ -34,7 +34,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_WI_NS = 1033.0       # v_add_u32 wave-instructions/ns, chip-wide (tools/valu_peak.hip)
 KERNEL_OF = {"gmax(gmax_kernel)": "gmax_kernel" if os.environ.get("HDRF_GMAX_V", "2") == "1" else "gmax2_kernel",
              "walk(lane_walk_kernel)": "lane_walk_kernel",
-             "sha(sha_chunk_kernel)": "sha_carry_kernel" if os.environ.get("HDRF_SHA_CARRY", "0") not in ("", "0")
+             "sha(sha_chunk_kernel)": "sha_carry_kernel" if os.environ.get("HDRF_SHA_CARRY", "1") not in ("", "0")
              else "sha_chunk_kernel", "place(place_kernel)": "place_kernel"}
 # stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index (claim ..
 # finalize), B2 store (scans, flush, place; on stream B itself with HDRF_SPLIT_B=0), L the LZ4 pass

@@ -403,10 +403,10 @@ __global__ void __launch_bounds__(256) sha_chunk_kernel(const BlockDesc *__restr
     sha_chunk_body<HW, false>(blocks, offsets, bst, cap_blk, digests, queue, thr, prio);
 }
 
-// HDRF_SHA_CARRY=1: 4-block windows with the second pair carried in registers (154 VGPRs).  A/B on
-// two boxes: +2.0 % (1032-1039 vs 1012-1017 GB/s) and -0.5 % (1022-1027 vs 1026-1033): its extra
-// line fetches (7.0 vs 6.57 GB per batch) slow the granule pass as much as SHA gains
-// (profiles/r03_sha_carry_ab.txt, profiles/r03_sha_carry_ab2.txt); not the default.
+// sha_carry: 4-block windows with the second pair carried in registers.  Round 3 A/B on two boxes:
+// +2.0 % and -0.5 % (profiles/r03_sha_carry_ab.txt, r03_sha_carry_ab2.txt); round 5, with sha.hip built
+// with uniform regions unstructurized and primed steps: 1136.1 / 1135.2 / 1137.8 vs 1105.2 / 1102.0 /
+// 1101.1 GB/s (profiles/r05_carry_ab.txt) — the default since.  HDRF_SHA_CARRY=0: sha_chunk.
 template <int HW>
 __global__ void __launch_bounds__(256) sha_carry_kernel(const BlockDesc *__restrict__ blocks,
                                                         const uint32_t *__restrict__ offsets,
@@ -445,8 +445,9 @@ hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const 
         return 4 * (e ? atoi(e) : 2);
     }();
     static const int lds = [] { const char *e = getenv("HDRF_SHA_LDS"); return e ? atoi(e) : 0; }();
-    // HDRF_SHA_CARRY: 1 = sha_carry (4-block windows, the second pair carried in registers)
-    static const bool carryk = [] { const char *e = getenv("HDRF_SHA_CARRY"); return e && atoi(e) != 0; }();
+    // HDRF_SHA_CARRY: 1 = sha_carry (4-block windows, the second pair carried in registers; default),
+    // 0 = sha_chunk
+    static const bool carryk = [] { const char *e = getenv("HDRF_SHA_CARRY"); return !e || atoi(e) != 0; }();
     const int wpb = std::max(4, (per_cu * 256 / nblocks) & ~3);
     dim3 g(wpb / 4, nblocks + 1);                  // y = 0: the long-chunk lanes
     if (carryk && hasher == 0)
