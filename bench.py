@@ -111,8 +111,8 @@ def parse():
                          "profiler whose summary must hold only the timed pipeline's kernels)")
     ap.add_argument("--no-alone", action="store_true")
     ap.add_argument("--no-prime", action="store_true",
-                    help="config 2: drain the pipeline and reset synchronously at every step (the round-4 step "
-                         "shape; default: steps back to back, hdrf_reset_async)")
+                    help="drain the pipeline and reset synchronously at every step (the round-4 step shape; "
+                         "default: steps back to back, hdrf_reset_async; config 5 packets are never primed)")
     ap.add_argument("--arena-slots", type=int, default=0,
                     help="32 MiB container slots (4 rings); each ring must hold a batch's closed containers "
                          "(default 512; config4 1792, so a ring also holds the closes of the batches whose LZ4 "
@@ -452,7 +452,9 @@ def main():
     # the previous step's last batches complete), and every batch's results are collected inside the
     # timed region; only the per-step pipeline fill and drain (an empty front or back stream for about
     # one batch chain per step) are gone.  --no-prime: the round-4 shape (drain + reset per step).
-    primed = node is None and not a.serial and not host and not a.no_prime
+    # Config 5 whole blocks (durable containers) too: each step's containers are drained as its
+    # batches complete, the next step's H2D copies start beside the last batches and drains.
+    primed = node is None and not a.serial and not a.no_prime and not (host and a.packet_kib)
 
     def run_primed(nsteps):
         from collections import deque
@@ -467,12 +469,23 @@ def main():
         for _ in range(nsteps):
             ctx.reset_async()
             for k, (ptrs, lens, rd, ids) in enumerate(batches):
+                if host:
+                    # config 5: the streaming shape of step() (H2D of batch k+1 beside the reduction of
+                    # k, containers drained after every completed batch), steps back to back: the
+                    # next step's first copies run beside this step's last batches and drains
+                    ctx.submit_host([hbuf.ctypes.data + (p - dev) for p in ptrs], lens, ids)
+                    q.append(k * B)
+                    if len(q) >= 3:
+                        collect_one()
+                        drain()
+                    continue
                 if len(q) >= a.depth:
                     collect_one()
                 ctx.submit_batch(ptrs, lens, rd, ids)
                 q.append(k * B)
         while q:
             collect_one()
+            drain()
 
     if primed:
         run_primed(a.warmup)

@@ -244,6 +244,7 @@ struct hdrf_ctx {
     std::vector<uint32_t> pend_closed;
     uint32_t undrained[4] = {0, 0, 0, 0};
     uint32_t inflight_bound = 0;
+    uint32_t gen_reserve = 0;                 // hdrf_reset_async (durable): the old generation's open slot
     std::map<uint32_t, int64_t> handed;
     bool lost = false;
     // packet-granular receive (hdrf_rx_begin / hdrf_append_packet / hdrf_submit_slot): device
@@ -589,6 +590,7 @@ static int init_state(hdrf_ctx *ctx, bool fresh)
     ctx->pend_closed.clear();
     for (auto &u : ctx->undrained) u = 0;
     ctx->inflight_bound = 0;
+    ctx->gen_reserve = 0;
     ctx->handed.clear();
     ctx->lost = false;
     for (auto &r : ctx->rx) { r.state = 0; r.len = 0; r.fill = 0; r.busy[0] = r.busy[1] = false; }
@@ -742,13 +744,16 @@ extern "C" int hdrf_reset(hdrf_ctx *ctx)
 // old state; the next submit starts a new index generation (the next epoch of the tag words, so no
 // table clear), the allocator is re-seeded on the index stream after the old batches' store part,
 // and the host side (containers, recipes, allocator view, totals) is reset when that batch is
-// completed (wait_one), after every older batch.  Single-node ring-arena contexts.
+// completed (wait_one), after every older batch.  Single-node contexts.  Durable containers
+// (retain_containers): the old generation's containers are drained as its batches complete, before
+// the new generation's first batch is waited for (that wait fails otherwise: the new generation
+// reuses the container ids); the slot rings continue across the generations, so no slot the old
+// generation may still hand out is reopened early.
 extern "C" int hdrf_reset_async(hdrf_ctx *ctx)
 {
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
-    if (ctx->G > 1 || ctx->cfg.retain_containers)
-        return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async: single-node contexts without durable containers (hdrf_reset)");
+    if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async: single-node contexts (hdrf_reset)");
     for (int i = 0; i < hdrf_ctx::kRx; i++)
         if (ctx->rx[i].state.load() == 1)
             return set_err(ctx, HDRF_E_INVAL, "a block is being received (hdrf_submit_slot or hdrf_rx_cancel first)");
@@ -757,6 +762,9 @@ extern "C" int hdrf_reset_async(hdrf_ctx *ctx)
     ctx->epoch = ctx->epoch >= 255 ? 1 : ctx->epoch + 1;
     ctx->bfirst = ctx->batch + 1;
     ctx->gen_pending = true;
+    // durable containers: the new generation continues every slot ring past the old open container
+    // (idx_clear_kernel), which stays the old generation's until the switch: one more slot held
+    ctx->gen_reserve = ctx->cfg.retain_containers ? 1u : 0u;
     return 0;
 }
 
@@ -910,7 +918,7 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         // what fills the ring, the recovery is hdrf_wait_batch (oldest), then hdrf_drain_containers,
         // then the submit again; the message names the step.
         for (int t = 0; t < c.n_thread; t++)
-            if ((uint64_t)ctx->undrained[t] + ctx->inflight_bound + bound > per - 1)
+            if ((uint64_t)ctx->undrained[t] + ctx->inflight_bound + ctx->gen_reserve + bound > per - 1)
                 return set_err(ctx, HDRF_E_CAPACITY,
                                "container arena: the ring of storer range " + std::to_string(t) + " is full (" +
                                    std::to_string(ctx->undrained[t]) + " undrained closed containers, " +
@@ -964,7 +972,8 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
         // flush walk the allocator) is finished before this index part claims entries of the new epoch;
         // then the allocator is re-seeded (and the table cleared when the epoch wrapped)
         if (ctx->nsub > ctx->nwait) HIPCK(hipStreamWaitEvent(Bst, ctx->sl[(ctx->nsub - 1) % kSlots].back_done, 0));
-        HIPCK(launch_index_clear(ctx->d_tab, ctx->gen_clear ? c.index_log2 : -1, ctx->d_alloc, initial_alloc(ctx), Bst));
+        HIPCK(launch_index_clear(ctx->d_tab, ctx->gen_clear ? c.index_log2 : -1, ctx->d_alloc, initial_alloc(ctx), Bst,
+                                 c.retain_containers ? (uint32_t)(c.arena_slots / 4) : 0u));
         ctx->gen_clear = false;
     }
     // HDRF_DECIDE_DESIG=0 (A/B): idx_finalize reads every designated entry (round-3 c2 behaviour)
@@ -1193,6 +1202,22 @@ static int wait_one(hdrf_ctx *ctx)
         }
     S.rx_release = 0;
     if (S.gen_reset) {                                   // the first batch of a fresh generation
+        if (ctx->cfg.retain_containers) {
+            // every container of the old generation handed out (closed ones, and the bytes of the
+            // open ones): the new generation reuses their ids
+            bool undrained = !ctx->pend_closed.empty();
+            for (int t = 0; t < ctx->cfg.n_thread && ctx->have_alloc; t++) {
+                if (!ctx->h_alloc.exists[t]) continue;
+                auto it = ctx->containers.find(ctx->h_alloc.id[t]);
+                const int64_t done = ctx->handed.count(ctx->h_alloc.id[t]) ? ctx->handed[ctx->h_alloc.id[t]] : 0;
+                if (it != ctx->containers.end() && (int64_t)it->second.len > done) undrained = true;
+            }
+            if (undrained)
+                return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async: the previous generation's containers were not "
+                                                  "drained before its successor's first batch was waited for");
+            ctx->handed.clear();
+            ctx->gen_reserve = 0;
+        }
         reset_host(ctx);
         S.gen_reset = false;
     }

@@ -244,8 +244,12 @@ hipError_t launch_index_finalize(const BlockState *bst, int nblocks, int cap_blk
 // reached ~1 TB/s on the 8.6 GB table) and seed the allocator, both on the stream that owns
 // the index, so the front half of the next batch overlaps the clear.
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// ring_per > 0 (a fresh generation of a durable-container context, hdrf_reset_async): the new
+// generation's allocator keeps every storer range's slot ring where the old one left it, one slot
+// past an open container, so no slot the old generation may still hand out (drain) is reopened
+// before the ring comes round to it (the host's ring check counts that slot until the switch).
 __global__ void __launch_bounds__(256) idx_clear_kernel(u32x4 *__restrict__ p, uint64_t n16, AllocState *alloc,
-                                                        AllocState a)
+                                                        AllocState a, uint32_t ring_per)
 {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -257,7 +261,14 @@ __global__ void __launch_bounds__(256) idx_clear_kernel(u32x4 *__restrict__ p, u
         __builtin_nontemporal_store(z, p + i + 3 * stride);
     }
     for (; i < n16; i += stride) __builtin_nontemporal_store(z, p + i);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *alloc = a;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (ring_per)
+            for (int t = 0; t < 4; t++) {
+                const uint32_t base = (uint32_t)t * ring_per, s = alloc->slot[t];
+                a.slot[t] = alloc->exists[t] ? base + (s - base + 1) % ring_per : s;
+            }
+        *alloc = a;
+    }
 }
 
 // Restore (a Redis dump of the index: digest -> 11-byte chunkMeta value): one thread per entry,
@@ -359,14 +370,15 @@ hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, in
     return hipGetLastError();
 }
 
-hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st)
+hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st,
+                              uint32_t ring_per)
 {
     // log2cap < 0: seed the allocator only (a reset that bumps the index epoch)
     const uint64_t n16 = log2cap < 0 ? 0 : (sizeof(IndexEntry) << log2cap) / 16;
     uint64_t g = (n16 + 255) / 256;
     if (g > 8192) g = 8192;
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(idx_clear_kernel, dim3((unsigned)g), dim3(256), 0, st, (u32x4 *)tab, n16, d_alloc, a);
+    hipLaunchKernelGGL(idx_clear_kernel, dim3((unsigned)g), dim3(256), 0, st, (u32x4 *)tab, n16, d_alloc, a, ring_per);
     return hipGetLastError();
 }
 

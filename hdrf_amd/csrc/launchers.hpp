@@ -73,7 +73,8 @@ hipError_t launch_index_probe(int hasher, const BlockState *bst, int nblocks, in
                               const uint32_t *slot, int log2cap, unsigned long long key,
                               unsigned long long *stats, hipStream_t st);
 // (log2cap < 0: only the allocator seed; a reset that bumps the index epoch)
-hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st);
+hipError_t launch_index_clear(IndexEntry *tab, int log2cap, AllocState *d_alloc, const AllocState &a, hipStream_t st,
+                              uint32_t ring_per = 0);
 hipError_t launch_index(int hasher, const BlockState *bst, int nblocks, int cap_blk, const uint32_t *offsets,
                         const uint32_t *digests, IndexEntry *tab, int log2cap, uint32_t cur, uint32_t bfirst,
                         unsigned long long key, uint32_t *slot,

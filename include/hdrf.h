@@ -343,9 +343,12 @@ int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out);
  * the batches in flight first.  HDRF_E_INVAL while a packet receive is open (hdrf_rx_begin not
  * yet followed by hdrf_submit_slot or hdrf_rx_cancel). */
 int hdrf_reset(hdrf_ctx *ctx);
-/* The same without completing the batches in flight (single-node contexts, cfg.retain_containers = 0):
- * they complete against the old state, and the next hdrf_submit_batch starts the fresh DataNode, so
- * its front half overlaps the old batches' back halves.  Views complete every batch first, as always. */
+/* The same without completing the batches in flight (single-node contexts): they complete against
+ * the old state, and the next submit starts the fresh DataNode, so its front half overlaps the old
+ * batches' back halves.  Views complete every batch first, as always.  cfg.retain_containers: drain
+ * the old batches' containers as they complete (hdrf_wait_batch, hdrf_drain_containers); the wait
+ * for the fresh DataNode's first batch fails with HDRF_E_INVAL if any old container (closed, or
+ * bytes of an open one) was not handed out by then. */
 int hdrf_reset_async(hdrf_ctx *ctx);
 
 /* ---- Node-global index over n_ranks GPUs (BASELINE config 3) -------------------

@@ -1,11 +1,13 @@
 """hdrf_reset_async: a fresh DataNode from the next submit on, without draining the batches in flight
 (the bench's back-to-back steps).  The batches submitted before it complete against the old state,
 those after it against a fresh index, allocator, containers and recipes — each sequence equal to its
-own oracle run, for compressor 1 and 2, across several resets (epochs) and a forced epoch wrap."""
+own oracle run, for compressor 1 and 2, across several resets (epochs) and a forced epoch wrap; with
+durable containers (the streaming DataNode of BASELINE config 5) every generation's drained files
+equal its own oracle's containers while the slot rings wrap across the generations."""
 import numpy as np
 import pytest
 
-from helpers import compare_block, compare_state
+from helpers import compare_block, compare_state, make_block
 from hdrf_amd.corpus import corpus_block_host, corpus_roots
 from hdrf_amd.lib import Context, HdrfError
 from oracle.oracle import Oracle
@@ -60,7 +62,7 @@ def test_reset_async_between_pipelined_sequences(compressor):
 
 def test_reset_async_epoch_wrap_and_refusals():
     """More than 255 generations: the epoch wraps and the table is cleared on the index stream, in
-    order; a durable-container context refuses the asynchronous form."""
+    order."""
     blocks = _blocks(77, 4)
     ctx = Context(container_max=1 << 20, max_block_bytes=1 << 20, max_batch_blocks=2, index_log2=16, arena_slots=32)
     size = len(blocks[0])
@@ -86,8 +88,93 @@ def test_reset_async_epoch_wrap_and_refusals():
     compare_state(ctx, ora, [1, 2, 3, 4], tag="after 260 generations")
     ctx.dev_free(dev)
     ctx.close()
-    d = Context(container_max=1 << 20, max_block_bytes=1 << 20, max_batch_blocks=2, index_log2=16, arena_slots=32,
-                retain_containers=1)
-    with pytest.raises(HdrfError):
-        d.reset_async()
-    d.close()
+
+
+def _durable_blocks(seed, n, size=2 << 20):
+    """~3/4 new random bytes per block (the slot rings wrap), the rest cross-block duplicates."""
+    rng = np.random.default_rng(seed)
+    base = [make_block(k, seed + i, 600_000) for i, k in enumerate(["random", "text", "binary"])]
+    d = size // 8
+    return [np.concatenate([base[int(rng.integers(3))][int(rng.integers(0, 200_000)):][:d] for _ in range(2)] +
+                           [make_block("random", seed + 100 + i, size - 2 * d)]) for i in range(n)]
+
+
+def _apply(disk, events):
+    for cid, closed, off, data in events:
+        if off == 0:
+            disk[cid] = (bytearray(data), bool(closed))
+        else:
+            f = disk.get(cid, (bytearray(), False))[0]
+            assert len(f) == off, f"append to {cid} at {off}, file has {len(f)}"
+            f[off:] = data
+            disk[cid] = (f, bool(closed))
+
+
+def _check_files(disk, ora, tag):
+    alloc = ora.allocator()
+    n = 0
+    for t in range(3):
+        last = int.from_bytes(alloc[3 * t:3 * t + 3], "big")
+        for cid in range(t << 22, last + 1):
+            od, oc = ora.container(cid)
+            if od is None:
+                continue
+            n += 1
+            assert cid in disk and bytes(disk[cid][0]) == bytes(od) and disk[cid][1] == oc, f"{tag}: container {cid}"
+    assert n == len(disk), f"{tag}: {len(disk)} files drained, the oracle has {n}"
+    return n
+
+
+@pytest.mark.parametrize("compressor", [1, 2])
+def test_reset_async_durable_generations(compressor):
+    """Durable containers: three generations of host blocks submitted three deep, hdrf_reset_async
+    between them with the previous generation's batches in flight, a drain after every completed
+    batch.  Each generation's blocks and drained files equal its own oracle run, and the rings of
+    20 slots per range wrap across the generations (the new generation continues each ring past
+    the old open container)."""
+    cmax = 1 << 20
+    gens = [_durable_blocks(91 + 7 * g + compressor, 16) for g in range(3)]
+    ctx = Context(compressor=compressor, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=1,
+                  index_log2=20, arena_slots=80, retain_containers=1)
+    oras = [Oracle(compressor=compressor, max_size=cmax) for _ in gens]
+    disks = [{} for _ in gens]
+    pend = []
+
+    def complete():
+        g, b = pend.pop(0)
+        ctx.wait_batch()
+        compare_block(ctx.batch_result(0), oras[g].reduce(gens[g][b], 0x700 + b), tag=f"gen {g} block {b}")
+        _apply(disks[g], ctx.drain_containers(buf_bytes=1 << 20))
+
+    for g, blocks in enumerate(gens):
+        ctx.reset_async()                              # the previous generation's batches still in flight
+        for b, blk in enumerate(blocks):
+            ctx.submit_host([blk.ctypes.data], [len(blk)], [0x700 + b])
+            pend.append((g, b))
+            if len(pend) == 3:
+                complete()
+    while pend:
+        complete()
+    assert ctx.drain_containers() == []
+    total = sum(_check_files(disks[g], oras[g], f"generation {g}") for g in range(3))
+    assert total > 3 * 20, "the rings of 20 slots per range must have wrapped"
+    compare_state(ctx, oras[2], [0x700 + b for b in range(16)], tag=f"durable generations c{compressor}",
+                  containers=False)
+    ctx.close()
+
+
+def test_reset_async_durable_undrained_refused():
+    """The wait for the new generation's first batch fails when an old container was not handed out:
+    the new generation reuses the container ids."""
+    blocks = _durable_blocks(97, 3)
+    ctx = Context(container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64,
+                  retain_containers=1)
+    ctx.reset_async()
+    ctx.submit_host([blocks[0].ctypes.data], [len(blocks[0])], [1])
+    ctx.reset_async()                                  # block 0 (old generation) still in flight, never drained
+    ctx.submit_host([blocks[1].ctypes.data], [len(blocks[1])], [2])
+    ctx.wait_batch()
+    with pytest.raises(HdrfError) as ei:
+        ctx.wait_batch()
+    assert "drained" in str(ei.value), str(ei.value)
+    ctx.close()
