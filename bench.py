@@ -79,8 +79,10 @@ def load_pmc(want):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    # 20 timed steps (~1.2 s at N=1): the primed pipeline's one fill and drain per timed region are
+    # spread over 320 batches instead of 80
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--blocks", type=int, default=512)
     ap.add_argument("--batch", type=int, default=0,
                     help="blocks per batch (default 32; config5 16: the step's first H2D and last drain, which "
