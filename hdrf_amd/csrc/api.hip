@@ -506,14 +506,18 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
     return 0;
 }
 
-static int wait_one(hdrf_ctx *ctx);
+static int wait_one(hdrf_ctx *ctx, bool force = false);
+static int init_state(hdrf_ctx *ctx, bool fresh);
+static bool gen_undrained(const hdrf_ctx *ctx);
 
 // complete every batch in flight (views, reset, the node-global phases need a quiet context)
 static int drain(hdrf_ctx *ctx)
 {
     int rc = 0;
+    // (forced: a generation switch whose old containers were not drained still completes, and the
+    // context is marked lost until hdrf_reset)
     while (ctx->nwait < ctx->nsub)
-        if (int r = wait_one(ctx)) rc = rc ? rc : r;
+        if (int r = wait_one(ctx, true)) rc = rc ? rc : r;
     HIPCK(hipStreamSynchronize(ctx->stC));
     if (ctx->stR) HIPCK(hipStreamSynchronize(ctx->stR));
     for (auto L : ctx->stL) HIPCK(hipStreamSynchronize(L));
@@ -523,7 +527,16 @@ static int drain(hdrf_ctx *ctx)
     HIPCK(hipStreamSynchronize(ctx->stB));
     HIPCK(hipStreamSynchronize(ctx->stB2));
     if (ctx->stX) HIPCK(hipStreamSynchronize(ctx->stX));
-    return rc;
+    if (rc) return rc;
+    if (ctx->gen_pending) {
+        // hdrf_reset_async with no batch submitted since: the caller of a view or a restore sees the
+        // fresh generation it asked for, applied now (a restore is then not undone by the next submit)
+        if (ctx->cfg.retain_containers && gen_undrained(ctx))
+            return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async is pending and the previous generation's containers "
+                                              "were not drained (hdrf_drain_containers first, or hdrf_reset)");
+        return init_state(ctx, false);
+    }
+    return 0;
 }
 
 static AllocState initial_alloc(const hdrf_ctx *ctx)
@@ -555,8 +568,8 @@ static void reset_host(hdrf_ctx *ctx)
 
 static int init_state(hdrf_ctx *ctx, bool fresh)
 {
+    ctx->gen_pending = false;                        // (before drain: this is the generation switch)
     (void)drain(ctx);
-    ctx->gen_pending = false;
     const AllocState a = initial_alloc(ctx);
     for (auto &S : ctx->sl) HIPCK(hipMemsetAsync(S.d_err, 0, sizeof(int), ctx->st));
     HIPCK(hipStreamSynchronize(ctx->st));
@@ -564,8 +577,10 @@ static int init_state(hdrf_ctx *ctx, bool fresh)
     // A fresh index is a new epoch: every entry tagged with another one is empty (common.hpp), so
     // the 2^k x 64 B table is cleared only at open and once every 255 resets; batch ids keep
     // growing, and the claim rule tells this epoch's entries by batch >= bfirst (index.hip).
+    // (gen_clear: a pending hdrf_reset_async already wrapped the epoch)
     hipStream_t ist = ctx->stB;
-    const bool clear = fresh || ctx->epoch >= 255;
+    const bool clear = fresh || ctx->epoch >= 255 || ctx->gen_clear;
+    ctx->gen_clear = false;
     ctx->epoch = clear ? 1 : ctx->epoch + 1;
     if (fresh) ctx->batch = 0;
     ctx->bfirst = ctx->batch + 1;
@@ -761,10 +776,12 @@ extern "C" int hdrf_reset_async(hdrf_ctx *ctx)
     ctx->gen_clear = ctx->gen_clear || ctx->epoch >= 255;
     ctx->epoch = ctx->epoch >= 255 ? 1 : ctx->epoch + 1;
     ctx->bfirst = ctx->batch + 1;
-    ctx->gen_pending = true;
     // durable containers: the new generation continues every slot ring past the old open container
-    // (idx_clear_kernel), which stays the old generation's until the switch: one more slot held
-    ctx->gen_reserve = ctx->cfg.retain_containers ? 1u : 0u;
+    // (idx_clear_kernel), which stays the old generation's until the switch: one more slot held per
+    // switch still in flight (a second hdrf_reset_async before the first switch was waited for holds
+    // a second one; calls with no submit in between make one switch)
+    if (ctx->cfg.retain_containers && !ctx->gen_pending) ctx->gen_reserve++;
+    ctx->gen_pending = true;
     return 0;
 }
 
@@ -1185,12 +1202,35 @@ static int complete_state(hdrf_ctx *ctx, Slot &S)
 }
 
 
-// Complete the oldest batch in flight (its slot is reusable once this returns).
-static int wait_one(hdrf_ctx *ctx)
+// Durable containers: is any container of the current host generation not yet handed out (closed
+// ones, and the bytes of the open ones)?  A new generation reuses their ids.
+static bool gen_undrained(const hdrf_ctx *ctx)
+{
+    if (!ctx->pend_closed.empty()) return true;
+    for (int t = 0; t < ctx->cfg.n_thread && ctx->have_alloc; t++) {
+        if (!ctx->h_alloc.exists[t]) continue;
+        auto it = ctx->containers.find(ctx->h_alloc.id[t]);
+        auto h = ctx->handed.find(ctx->h_alloc.id[t]);
+        const int64_t done = h != ctx->handed.end() ? h->second : 0;
+        if (it != ctx->containers.end() && (int64_t)it->second.len > done) return true;
+    }
+    return false;
+}
+
+// Complete the oldest batch in flight (its slot is reusable once this returns).  The first batch of
+// a fresh generation (hdrf_reset_async) on a durable context is refused while the old generation's
+// containers are not drained, and stays in flight: hdrf_drain_containers, then hdrf_wait_batch again.
+// force (drain(): a view, a reset or close): it completes anyway and the context is marked lost.
+static int wait_one(hdrf_ctx *ctx, bool force)
 {
     if (ctx->nwait >= ctx->nsub) return set_err(ctx, HDRF_E_INVAL, "no batch in flight");
     const int si = (int)(ctx->nwait % kSlots);
     Slot &S = ctx->sl[si];
+    const bool refused = S.gen_reset && ctx->cfg.retain_containers && gen_undrained(ctx);
+    if (refused && !force)
+        return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async: the previous generation's containers were not "
+                                          "drained before its successor's first batch was waited for "
+                                          "(hdrf_drain_containers, then hdrf_wait_batch again)");
     ctx->nwait++;
     S.pending = false;
     HIPCK(hipEventSynchronize(S.back_done));
@@ -1203,23 +1243,18 @@ static int wait_one(hdrf_ctx *ctx)
     S.rx_release = 0;
     if (S.gen_reset) {                                   // the first batch of a fresh generation
         if (ctx->cfg.retain_containers) {
-            // every container of the old generation handed out (closed ones, and the bytes of the
-            // open ones): the new generation reuses their ids
-            bool undrained = !ctx->pend_closed.empty();
-            for (int t = 0; t < ctx->cfg.n_thread && ctx->have_alloc; t++) {
-                if (!ctx->h_alloc.exists[t]) continue;
-                auto it = ctx->containers.find(ctx->h_alloc.id[t]);
-                const int64_t done = ctx->handed.count(ctx->h_alloc.id[t]) ? ctx->handed[ctx->h_alloc.id[t]] : 0;
-                if (it != ctx->containers.end() && (int64_t)it->second.len > done) undrained = true;
-            }
-            if (undrained)
-                return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async: the previous generation's containers were not "
-                                                  "drained before its successor's first batch was waited for");
             ctx->handed.clear();
-            ctx->gen_reserve = 0;
+            // this switch's ring continuation is over (one per pending durable generation switch)
+            ctx->gen_reserve -= std::min<uint32_t>(ctx->gen_reserve, 1u);
         }
         reset_host(ctx);
         S.gen_reset = false;
+        if (refused) {
+            ctx->lost = true;
+            (void)complete_slot(ctx, si, true);
+            return set_err(ctx, HDRF_E_CAPACITY, "hdrf_reset_async: the previous generation's undrained containers "
+                                                 "were dropped (the context needs hdrf_reset)");
+        }
     }
     return complete_slot(ctx, si, true);
 }
@@ -2672,6 +2707,13 @@ extern "C" int hdrf_gx_place_wait(hdrf_ctx *ctx, int64_t *send_counts)
     }
     ctx->gx_scanned = 0;
     ctx->gx_dscan = 0;
+    // (checked before any host bookkeeping: a failed placement leaves the host state untouched; a
+    // device error is complete_slot's to report)
+    for (int d = 0; d < ctx->G && !*S.h_err; d++)
+        if (h->c3[d] != h->x3want[d])
+            return set_err(ctx, HDRF_E_DEVICE, "X3 send count to rank " + std::to_string(d) + " (" +
+                                                   std::to_string(h->c3[d]) + ") disagrees with its X2 answers (" +
+                                                   std::to_string(h->x3want[d]) + ")");
     // the open containers this rank's flush walk started and ended in hold its placed chunks even
     // when another rank closes them (the node read, hdrf_gx_read_fill, gathers from them)
     for (const AllocState *a : {&ctx->gx_ain, &ctx->gx_aout})
@@ -2679,11 +2721,6 @@ extern "C" int hdrf_gx_place_wait(hdrf_ctx *ctx, int64_t *send_counts)
             if (a->exists[t] && !ctx->containers.count(a->id[t])) note_container(ctx, a->id[t], a->slot[t], a->cur[t], 0);
     S.gx_compressed = false;
     if (int rc = complete_slot(ctx, si, false)) return rc;
-    for (int d = 0; d < ctx->G; d++)
-        if (h->c3[d] != h->x3want[d])
-            return set_err(ctx, HDRF_E_DEVICE, "X3 send count to rank " + std::to_string(d) + " (" +
-                                                   std::to_string(h->c3[d]) + ") disagrees with its X2 answers (" +
-                                                   std::to_string(h->x3want[d]) + ")");
     for (int d = 0; d < ctx->G; d++) send_counts[d] = (int64_t)h->c3[d];
     ctx->gx_x3recv.assign(h->x3e, h->x3e + ctx->G);
     ctx->gx_bphase = 4;
@@ -2822,11 +2859,8 @@ extern "C" int hdrf_gx_commit(hdrf_ctx *ctx, const uint32_t *x3_recv, const int6
 }
 
 // Complete every node-global batch in flight (all streams) and report an error of the last commits.
-extern "C" int hdrf_gx_sync(hdrf_ctx *ctx)
+static int gx_sync_locked(hdrf_ctx *ctx)
 {
-    HDRF_LOCK(ctx);
-    if (!ctx) return HDRF_E_INVAL;
-    if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
     if (int rc = drain(ctx)) return rc;
     int herr = 0;
     HIPCK(hipMemcpy(&herr, ctx->d_gx_err, sizeof(int), hipMemcpyDeviceToHost));
@@ -2836,6 +2870,14 @@ extern "C" int hdrf_gx_sync(hdrf_ctx *ctx)
         return device_error(ctx, herr);
     }
     return 0;
+}
+
+extern "C" int hdrf_gx_sync(hdrf_ctx *ctx)
+{
+    HDRF_LOCK(ctx);
+    if (!ctx) return HDRF_E_INVAL;
+    if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_* needs cfg.n_ranks > 1");
+    return gx_sync_locked(ctx);
 }
 
 static int check_b(hdrf_ctx *ctx, int32_t b)
@@ -3447,6 +3489,8 @@ extern "C" int64_t hdrf_gx_read_locate(hdrf_ctx *ctx, const uint8_t *digests, in
     if (n < 0 || (n && (!digests || !loc))) return set_err(ctx, HDRF_E_INVAL, "bad locate arguments");
     if (n == 0) return 0;
     if (ctx->gx_nfront != ctx->gx_nback) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_read_locate: a batch is in flight");
+    // the last batch's commit (stream B) and arena copy (stream B2) land first; a commit error is reported here
+    if (int rc = gx_sync_locked(ctx)) return rc;
     const uint64_t o_loc = (((uint64_t)n * ctx->H) + 255) & ~255ull, o_err = o_loc + (((uint64_t)n * 16 + 255) & ~255ull);
     if (int rc = grow(ctx, &ctx->d_rd, &ctx->rd_cap, o_err + 256)) return rc;
     uint8_t *R = ctx->d_rd;
@@ -3472,6 +3516,7 @@ extern "C" int64_t hdrf_gx_read_fill(hdrf_ctx *ctx, const uint32_t *loc, int64_t
     if (ctx->G < 2) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_read_* needs cfg.n_ranks > 1");
     if (n < 0 || (n && !loc)) return set_err(ctx, HDRF_E_INVAL, "bad fill arguments");
     if (ctx->gx_nfront != ctx->gx_nback) return set_err(ctx, HDRF_E_INVAL, "hdrf_gx_read_fill: a batch is in flight");
+    if (int rc = gx_sync_locked(ctx)) return rc;
     struct RdChunkH { uint32_t slot, start, len, off; };
     static_assert(sizeof(RdChunkH) == 16, "RdChunk layout");
     if (rd_chunk_bytes() != sizeof(RdChunkH)) return set_err(ctx, HDRF_E_DEVICE, "RdChunk layout");

@@ -296,7 +296,8 @@ int64_t hdrf_reconstruct_block(hdrf_ctx *ctx, uint64_t block_id, uint8_t *out, i
  *      (HDRF_E_NOTFOUND when such a chunk's container left the arena ring);
  *   4. the G partial blocks summed byte-wise (disjoint) on the reading rank are the block; the
  *      returned counts sum to the recipe size.
- * Call between batches (no hdrf_gx_* batch in flight). */
+ * Call between batches (no hdrf_gx_* batch in flight); both first complete the last batch's commit
+ * and arena copy on this rank (as hdrf_gx_sync, whose commit error they report). */
 int64_t hdrf_gx_read_locate(hdrf_ctx *ctx, const uint8_t *digests, int64_t n, uint32_t *loc);
 int64_t hdrf_gx_read_fill(hdrf_ctx *ctx, const uint32_t *loc, int64_t n, uint8_t *dev_out, int64_t cap);
 
@@ -345,10 +346,15 @@ int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out);
 int hdrf_reset(hdrf_ctx *ctx);
 /* The same without completing the batches in flight (single-node contexts): they complete against
  * the old state, and the next submit starts the fresh DataNode, so its front half overlaps the old
- * batches' back halves.  Views complete every batch first, as always.  cfg.retain_containers: drain
- * the old batches' containers as they complete (hdrf_wait_batch, hdrf_drain_containers); the wait
- * for the fresh DataNode's first batch fails with HDRF_E_INVAL if any old container (closed, or
- * bytes of an open one) was not handed out by then. */
+ * batches' back halves.  Views and restores (hdrf_index_*, hdrf_*_load, reconstruct, container
+ * reads, hdrf_synchronize) complete every batch first, as always, and a reset still pending then (no
+ * submit since) is applied before they run, so they see the fresh DataNode and a restore is kept.
+ * cfg.retain_containers: drain the old batches' containers as they complete (hdrf_wait_batch,
+ * hdrf_drain_containers); while any old container (closed, or bytes of an open one) is not handed
+ * out, hdrf_wait_batch on the fresh DataNode's first batch fails with HDRF_E_INVAL and leaves that
+ * batch in flight (drain, then wait again), and the views above fail with HDRF_E_INVAL (a view that
+ * must complete the batch anyway drops those containers and marks the context for hdrf_reset,
+ * HDRF_E_CAPACITY). */
 int hdrf_reset_async(hdrf_ctx *ctx);
 
 /* ---- Node-global index over n_ranks GPUs (BASELINE config 3) -------------------

@@ -245,16 +245,19 @@ JNIEXPORT jbyteArray JNICALL JFN(recipe0)(JNIEnv *env, jclass cls, jlong h, jlon
 {
     (void)cls;
     hdrf_ctx *ctx = (hdrf_ctx *)(intptr_t)h;
+    /* an unknown block throws, as length0 does (the recipe GET of DN/DataConstructor.java:46-72
+     * has nothing to rebuild from) */
     int64_t len = hdrf_block_length(ctx, (uint64_t)id);
-    if (len < 0) return NULL;
+    if (len < 0) { throw_io(env, ctx, (int)len); return NULL; }
     int64_t cap = 4 + (int64_t)hdrf_digest_len(ctx) * (len / 702 + 2);
     uint8_t *tmp = (uint8_t *)malloc((size_t)cap);
+    if (!tmp) { throw_io(env, ctx, HDRF_E_NOMEM); return NULL; }
     int64_t n = hdrf_recipe_get(ctx, (uint64_t)id, tmp, cap);
-    if (n < 0) { free(tmp); throw_io(env, ctx, (int)n); return NULL; }
+    if (n <= 0) { free(tmp); throw_io(env, ctx, n < 0 ? (int)n : HDRF_E_NOTFOUND); return NULL; }
     jbyteArray out = (*env)->NewByteArray(env, (jsize)n);
-    (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);
     free(tmp);
-    return out;
+    return out;                                      /* NULL: OutOfMemoryError is pending */
 }
 
 /* DataConstructor(blkID, recipe).data, served by BlockSender (DN/BlockSender.java:612-619) */
@@ -265,10 +268,11 @@ JNIEXPORT jbyteArray JNICALL JFN(reconstruct0)(JNIEnv *env, jclass cls, jlong h,
     int64_t len = hdrf_block_length(ctx, (uint64_t)id);
     if (len < 0) { throw_io(env, ctx, (int)len); return NULL; }
     uint8_t *tmp = (uint8_t *)malloc((size_t)(len ? len : 1));
+    if (!tmp) { throw_io(env, ctx, HDRF_E_NOMEM); return NULL; }
     int64_t n = hdrf_reconstruct_block(ctx, (uint64_t)id, tmp, len);
     if (n < 0) { free(tmp); throw_io(env, ctx, (int)n); return NULL; }
     jbyteArray out = (*env)->NewByteArray(env, (jsize)n);
-    (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)n, (const jbyte *)tmp);
     free(tmp);
     return out;
 }

@@ -332,6 +332,9 @@ int main(int argc, char **argv)
     jbyteArray none = JFN(reconstruct0)(ENV, NULL, h, 0x7fffffff);
     EXPECT_THROW("reconstruct0(unknown block)");
     rel(none);
+    jbyteArray nor = JFN(recipe0)(ENV, NULL, h, 0x7fffffff);
+    EXPECT_THROW("recipe0(unknown block)");
+    if (nor) { printf("recipe0(unknown block) returned an array\n"); g_fail++; }
 
     /* stream mode (compressor 4 / 0): the block file for 64,512-B packet writes, and its GPU decode */
     const int codecs[2] = {4, 0};

@@ -164,17 +164,93 @@ def test_reset_async_durable_generations(compressor):
 
 
 def test_reset_async_durable_undrained_refused():
-    """The wait for the new generation's first batch fails when an old container was not handed out:
-    the new generation reuses the container ids."""
-    blocks = _durable_blocks(97, 3)
-    ctx = Context(container_max=1 << 20, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64,
+    """The wait for the new generation's first batch fails when an old container was not handed out
+    (the new generation reuses the container ids) and leaves that batch in flight: after
+    hdrf_drain_containers the same wait completes it, the old generation's files equal its oracle's
+    and the new generation's block and state equal a fresh oracle's.  A view that must complete such a
+    batch anyway drops the old containers, reports it, and the context works again after hdrf_reset."""
+    cmax = 1 << 20
+    blocks = _durable_blocks(97, 4)
+    ctx = Context(container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=20, arena_slots=64,
                   retain_containers=1)
     ctx.reset_async()
     ctx.submit_host([blocks[0].ctypes.data], [len(blocks[0])], [1])
     ctx.reset_async()                                  # block 0 (old generation) still in flight, never drained
     ctx.submit_host([blocks[1].ctypes.data], [len(blocks[1])], [2])
     ctx.wait_batch()
+    old, new = Oracle(max_size=cmax), Oracle(max_size=cmax)
+    compare_block(ctx.batch_result(0), old.reduce(blocks[0], 1), tag="old generation block")
+    for _ in range(2):                                 # refused again while nothing was drained
+        with pytest.raises(HdrfError) as ei:
+            ctx.wait_batch()
+        assert "drained" in str(ei.value), str(ei.value)
+    disk = {}
+    _apply(disk, ctx.drain_containers(buf_bytes=1 << 20))
+    assert _check_files(disk, old, "old generation") > 0
+    ctx.wait_batch()                                   # the same batch, now completed
+    compare_block(ctx.batch_result(0), new.reduce(blocks[1], 2), tag="new generation block")
+    compare_state(ctx, new, [2], tag="after the refused switch", containers=False)
+    disk2 = {}
+    _apply(disk2, ctx.drain_containers(buf_bytes=1 << 20))
+    _check_files(disk2, new, "new generation")
+
+    # forced: a view completes the switch batch anyway -> the old containers are dropped, the context is lost
+    ctx.submit_host([blocks[2].ctypes.data], [len(blocks[2])], [3])     # generation 2, never drained
+    ctx.wait_batch()
+    ctx.reset_async()
+    ctx.submit_host([blocks[3].ctypes.data], [len(blocks[3])], [4])     # generation 3
     with pytest.raises(HdrfError) as ei:
-        ctx.wait_batch()
-    assert "drained" in str(ei.value), str(ei.value)
+        ctx.index_count()
+    assert "undrained" in str(ei.value), str(ei.value)
+    ctx.reset()
+    fresh = Oracle(max_size=cmax)
+    ctx.submit_host([blocks[3].ctypes.data], [len(blocks[3])], [4])
+    ctx.wait_batch()
+    compare_block(ctx.batch_result(0), fresh.reduce(blocks[3], 4), tag="after hdrf_reset")
+    ctx.close()
+
+
+def test_reset_async_then_restore_then_submit():
+    """A restore between hdrf_reset_async and the next submit (a DataNode re-initialised while blocks
+    were in flight, then restarted from persisted Redis state and chunkDir files) is kept: the pending
+    generation is applied before the restore, not after it.  The blocks after it equal an oracle that
+    never stopped."""
+    cmax = 1 << 20
+    roots = corpus_roots(131, 500000, 9, 4)
+    blocks = [corpus_block_host(131, roots, b, 4, 1 << 18) for b in range(9)]
+    size = len(blocks[0])
+    ids = [0x900 + b for b in range(9)]
+    ctx = Context(container_max=cmax, max_block_bytes=1 << 20, max_batch_blocks=3, index_log2=18, arena_slots=64)
+    dev = ctx.dev_alloc(size * 9 + 4096)
+    ctx.h2d(dev, np.concatenate(blocks))
+    total = size * 9 + 4096
+
+    def batch(b0):
+        return ([dev + (b0 + i) * size for i in range(3)], [size] * 3, [total - (b0 + i) * size for i in range(3)],
+                ids[b0:b0 + 3])
+
+    ctx.reduce_batch(*batch(0))
+    keys, vals = ctx.index_dump()
+    alloc = ctx.allocator()
+    recipes = {i: ctx.recipe(i) for i in ids[:3]}
+    opens = []
+    for t in range(3):
+        d, closed = ctx.container(int.from_bytes(alloc[3 * t:3 * t + 3], "big"))
+        opens.append(d if d is not None and not closed else None)
+    ctx.submit_batch(*batch(3))                        # in flight across the reset
+    ctx.reset_async()
+    ctx.wait_batch()
+    ctx.index_load(keys, vals)                         # the restore: pending generation applied first
+    ctx.allocator_load(alloc, opens)
+    for i, r in recipes.items():
+        ctx.recipe_load(i, r)
+    ora = Oracle(max_size=cmax)
+    for b in range(3):
+        ora.reduce(blocks[b], ids[b])
+    ctx.submit_batch(*batch(6))
+    ctx.wait_batch()
+    for i in range(3):
+        compare_block(ctx.batch_result(i), ora.reduce(blocks[6 + i], ids[6 + i]), tag=f"after restore, block {i}")
+    compare_state(ctx, ora, ids[:3] + ids[6:], tag="restore after reset_async", containers=False)
+    ctx.dev_free(dev)
     ctx.close()
