@@ -96,7 +96,10 @@ def parse():
     ap.add_argument("--hasher", type=int, default=0)
     ap.add_argument("--cpu-sample-blocks", type=int, default=0,
                     help="blocks of the CPU baseline sample (default: the first batch, checked chunk by chunk)")
-    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true",
+                    help="no CPU leg: neither the timed baseline sample nor the whole-corpus storeSize check")
+    ap.add_argument("--no-corpus-check", action="store_true",
+                    help="skip the whole-corpus check (every block's storeSize from the timed steps vs the oracle)")
     ap.add_argument("--serial", action="store_true",
                     help="one batch at a time (no stream overlap): clean per-kernel stage times")
     ap.add_argument("--read-blocks", type=int, default=0,
@@ -713,6 +716,12 @@ def main():
                     done += 1
         cpu = cpu_baseline(ctx, dev, S, m_cpu, store, a.hasher, compressor, gpu_res)
 
+    if rank == 0 and world == 1 and not a.no_cpu and not a.no_corpus_check:
+        # the metric's "bit-exact dedup ratio" over the WHOLE corpus: every block's storeSize from the
+        # last timed step against the oracle in store-size mode, one batch at a time
+        dedup["oracle_check"] = corpus_check(ctx, dev, S, nb, B, store, a.hasher, compressor,
+                                             hbuf if host else None)
+
     if rank == 0:
         line = {"metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
                 "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True, "scaling": "weak",
@@ -862,7 +871,7 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1, gpu_res=None):
     from oracle.oracle import Oracle
     blks = [ctx.d2h(dev + b * S, S) for b in range(m)]
     ids = list(range(m))
-    usable = len(os.sched_getaffinity(0))
+    usable = cpu_share()
     ora = Oracle(hasher=hasher, compressor=compressor)
     t0 = time.perf_counter()
     ss1 = [ora.reduce(blk, b)["store_size"] for b, blk in enumerate(blks)]
@@ -915,6 +924,56 @@ def cpu_baseline(ctx, dev, S, m, gpu_store, hasher, compressor=1, gpu_res=None):
     if compressor == 2:
         out["container_file_mismatches"], out["containers_checked"] = _check_containers(ctx, dev, S, m, ora, hasher)
     return out
+
+
+def cpu_share():
+    """Host cores this process may use: the affinity mask, capped by a cgroup CPU quota (a GPU box
+    shows the whole machine's CPUs but grants each GPU a share of them)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def corpus_check(ctx, dev, S, nb, B, gpu_store, hasher, compressor, host=None):
+    """Every block's storeSize from the timed steps (DN/DataDeduplicator.java:355: the bytes a block
+    adds to the containers) against the oracle over the whole corpus in block order, so the line's
+    dedup ratio is checked bit for bit, not only on a sample.  The oracle runs in store-size mode
+    (container lengths, no container or recipe bytes in host memory) on the threaded baseline's
+    shape, fed one pinned batch at a time."""
+    import numpy as np
+    from oracle.oracle import Oracle
+    ora = Oracle(hasher=hasher, compressor=compressor, store_only=True)
+    nthr = max(1, cpu_share() - 1)
+    buf = ctx.host_alloc(B * S) if host is None else None
+    ss = []
+    t0 = time.perf_counter()
+    for b0 in range(0, nb, B):
+        k = min(B, nb - b0)
+        if host is None:
+            ctx.L.hdrf_memcpy_d2h(ctx._h, buf.ctypes.data, dev + b0 * S, k * S)
+            src = buf
+        else:
+            src = host[b0 * S:(b0 + k) * S]
+        ss.extend(int(x) for x in ora.reduce_many([src[i * S:(i + 1) * S] for i in range(k)],
+                                                   list(range(b0, b0 + k)), nthr))
+    t = time.perf_counter() - t0
+    if buf is not None:
+        ctx.host_free(buf)
+    ss = np.array(ss, np.int64)
+    stored = int(ss.sum())
+    gpu = np.asarray(gpu_store[:nb], np.int64)
+    return {"blocks": nb, "store_size_mismatches": int((ss != gpu).sum()),
+            "stored_bytes_oracle": stored, "stored_bytes_gpu": int(gpu.sum()),
+            "dedup_ratio_oracle": round(nb * S / max(stored, 1), 6),
+            "dedup_ratio_gpu": round(nb * S / max(int(gpu.sum()), 1), 6),
+            "seconds": round(t, 1), "threads": nthr + 1,
+            "what": "every block's storeSize of the last timed step vs oracle/hdrf_oracle.c in store-size mode "
+                    "(the whole corpus in block order from a fresh index; untimed)"}
 
 
 def _check_containers(ctx, dev, S, m, ora, hasher):

@@ -242,6 +242,8 @@ struct hdrf_oracle {
     container *cont[4]; int64_t ncont[4], ccap[4];
     recipe *rec; int64_t nrec, rcap;
     int mt_store;                   /* 1: the storer ranges run on concurrent threads (CPU baselines) */
+    int store_only;                 /* 1: container and recipe BYTES are not kept (lengths, index values,
+                                       allocator and storeSize are): bench.py's whole-corpus check */
 };
 
 hdrf_oracle *hdrf_oracle_new(int hasher, int compressor, uint32_t max_size)
@@ -256,6 +258,8 @@ hdrf_oracle *hdrf_oracle_new(int hasher, int compressor, uint32_t max_size)
     if (kv_init(&o->index, o->H, 1 << 16)) { free(o); return NULL; }
     return o;
 }
+
+void hdrf_oracle_set_store_only(hdrf_oracle *o, int on) { if (o) o->store_only = on != 0; }
 
 void hdrf_oracle_free(hdrf_oracle *o)
 {
@@ -290,8 +294,9 @@ static container *cont_create(hdrf_oracle *o, uint32_t id)
     return c;
 }
 
-static void cont_append(container *c, const uint8_t *p, int64_t n)
+static void cont_append(container *c, const uint8_t *p, int64_t n, int store_only)
 {
+    if (store_only) { c->len += n; return; }
     if (c->len + n > c->cap) {
         int64_t nc = c->cap ? c->cap : 4096;
         while (nc < c->len + n) nc *= 2;
@@ -415,7 +420,7 @@ static void *store_range(void *arg)
         if (cm[k].newChunk) {
             if (curPos + cm[k].length > (int64_t)o->max_size) {            /* :748 buffer full */
                 c->closed = 1;                                              /* :754-786 rewrite prev||buf */
-                if (o->compressor == 2) {                                   /* :770-779 Lz4Codec stream */
+                if (o->compressor == 2 && !o->store_only) {                 /* :770-779 Lz4Codec stream */
                     c->cdata = (uint8_t *)malloc((size_t)hdrf_oracle_hadoop_lz4_bound(c->len));
                     c->clen = hdrf_oracle_hadoop_lz4_frame(c->data, c->len, c->cdata);
                 }
@@ -425,7 +430,7 @@ static void *store_range(void *arg)
                 c = cont_find(o, (uint32_t)lastBlockID[t]);                /* :794-795 createNewFile */
                 if (!c) c = cont_create(o, (uint32_t)lastBlockID[t]);
             }
-            cont_append(c, j->data + cm[k].bbStart, cm[k].length);         /* :798 */
+            cont_append(c, j->data + cm[k].bbStart, cm[k].length, o->store_only);   /* :798 */
             bufpos += cm[k].length;
             cm[k].blockID = lastBlockID[t];                                 /* :799 */
             cm[k].blockStart = (int32_t)curPos;                             /* :800 setBlockStartStop */
@@ -490,7 +495,7 @@ static int64_t reduce_hashed(hdrf_oracle *o, const uint8_t *data, int64_t size, 
      * Cross-thread order is racy in the reference; this fixes "last occurrence in chunk order wins". */
     for (int64_t k = 0; k < n; k++) kv_set(&o->index, dig + k * H, setv + k * 11);
 
-    /* :190 storeDB :372-392 */
+    /* :190 storeDB :372-392 (store_only: the allocator, no recipe bytes) */
     for (int i = 0; i < 8; i++) {                                           /* utilities.blockIDtoBytes :66-75 */
         o->alloc[i * 3] = (uint8_t)(lastBlockID[i] >> 16);
         o->alloc[i * 3 + 1] = (uint8_t)(lastBlockID[i] >> 8);
@@ -499,8 +504,9 @@ static int64_t reduce_hashed(hdrf_oracle *o, const uint8_t *data, int64_t size, 
     o->have_alloc = 1;
     uint32_t rkey = (uint32_t)block_id;                                     /* longToBytes(filename,4) */
     recipe *r = NULL;
-    for (int64_t i = 0; i < o->nrec; i++) if (o->rec[i].key == rkey) r = &o->rec[i];
-    if (!r) {
+    if (!o->store_only)
+        for (int64_t i = 0; i < o->nrec; i++) if (o->rec[i].key == rkey) r = &o->rec[i];
+    if (!r && !o->store_only) {
         if (o->nrec == o->rcap) {
             o->rcap = o->rcap ? o->rcap * 2 : 16;
             o->rec = (recipe *)realloc(o->rec, (size_t)o->rcap * sizeof(recipe));
@@ -508,12 +514,14 @@ static int64_t reduce_hashed(hdrf_oracle *o, const uint8_t *data, int64_t size, 
         r = &o->rec[o->nrec++];
         r->key = rkey; r->data = NULL;
     }
-    free(r->data);
-    r->len = 4 + n * H;
-    r->data = (uint8_t *)malloc((size_t)r->len);
-    r->data[0] = (uint8_t)(size >> 24); r->data[1] = (uint8_t)(size >> 16);
-    r->data[2] = (uint8_t)(size >> 8);  r->data[3] = (uint8_t)size;
-    memcpy(r->data + 4, dig, (size_t)(n * H));
+    if (r) {
+        free(r->data);
+        r->len = 4 + n * H;
+        r->data = (uint8_t *)malloc((size_t)r->len);
+        r->data[0] = (uint8_t)(size >> 24); r->data[1] = (uint8_t)(size >> 16);
+        r->data[2] = (uint8_t)(size >> 8);  r->data[3] = (uint8_t)size;
+        memcpy(r->data + 4, dig, (size_t)(n * H));
+    }
 
     if (offsets_out) memcpy(offsets_out, off, (size_t)n * sizeof(uint32_t));
     if (digests_out) memcpy(digests_out, dig, (size_t)(n * H));
@@ -728,7 +736,7 @@ int64_t hdrf_oracle_recipe(const hdrf_oracle *o, int64_t block_id, uint8_t *out,
 
 int64_t hdrf_oracle_container(const hdrf_oracle *o, uint32_t id, uint8_t *out, int64_t cap, int *closed)
 {
-    const container *c = cont_find(o, id);
+    const container *c = o->store_only ? NULL : cont_find(o, id);
     if (!c) return -1;
     if (closed) *closed = c->closed;
     const uint8_t *src = c->cdata ? c->cdata : c->data;   /* closed + compressor 2: the LZ4 file */

@@ -38,6 +38,11 @@ void hdrf_oracle_sha224(const uint8_t *msg, uint64_t len, uint8_t out[28]);
 typedef struct hdrf_oracle hdrf_oracle;
 hdrf_oracle *hdrf_oracle_new(int hasher, int compressor, uint32_t max_size);
 void hdrf_oracle_free(hdrf_oracle *o);
+/* Store-size mode (call before the first block): the storers keep container LENGTHS, not bytes, and
+ * no recipe is kept; chunks, digests, dedup decisions, index values, the allocator and storeSize are
+ * unchanged (bench.py checks the whole corpus's storeSize with it, in a few GB of host memory).
+ * hdrf_oracle_container / hdrf_oracle_recipe then report nothing. */
+void hdrf_oracle_set_store_only(hdrf_oracle *o, int on);
 
 /* Reduce one block.  Optional outputs (NULL to skip), each sized for cap chunks:
  *   offsets[n], digests[n*H], is_new[n], values[n*11] (the 11-byte value each chunk SETs).

@@ -36,6 +36,7 @@ def lib():
         L.hdrf_oracle_new.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint32]
         L.hdrf_oracle_new.restype = ctypes.c_void_p
         L.hdrf_oracle_free.argtypes = [ctypes.c_void_p]
+        L.hdrf_oracle_set_store_only.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.hdrf_oracle_reduce.argtypes = [ctypes.c_void_p, _u8p, ctypes.c_int64, ctypes.c_int64,
                                          ctypes.c_int64, _u32p, _u8p, _u8p, _u8p, _i64p]
         L.hdrf_oracle_reduce.restype = ctypes.c_int64
@@ -274,11 +275,15 @@ class _OracleOut(ctypes.Structure):
 class Oracle:
     """Stateful restatement of DataDeduplicator + Redis + chunkDir (one DataNode)."""
 
-    def __init__(self, hasher=0, compressor=1, max_size=1 << 25):
+    def __init__(self, hasher=0, compressor=1, max_size=1 << 25, store_only=False):
+        """store_only: container lengths instead of bytes and no recipes (storeSize, dedup decisions,
+        index values and the allocator unchanged): the whole-corpus dedup-ratio check."""
         self.H = 20 if hasher == 0 else 28
         self.hasher = hasher
         self._h = lib().hdrf_oracle_new(hasher, compressor, max_size)
         assert self._h
+        if store_only:
+            lib().hdrf_oracle_set_store_only(self._h, 1)
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -73,6 +73,58 @@ def test_bench_batches_4gib_depth3_full_state():
     ctx.close()
 
 
+@pytest.mark.timeout(900)
+def test_bench_primed_depth4_reset_async_generations():
+    """The headline's exact timed shape (bench.py run_primed): the bench's context (index_log2 27,
+    512 arena slots, recipes, timing events), 32 x 128 MiB batches, four in flight, steps back to back
+    with hdrf_reset_async — the second generation's first batches are submitted while the first
+    generation's three batches are still in flight.  Both generations reduce the same 96 corpus blocks
+    from a fresh index (as every bench step does), so every block of both equals the one sequential
+    oracle run; after the second generation the full index, allocator, every recipe and every
+    container equal the oracle's."""
+    B, nbatch, depth = 32, 3, 4
+    nb = B * nbatch
+    spb = S // SEG
+    roots = corpus_roots(SEED, 500000, 512, spb)[: nb * spb]
+    ctx = Context(max_block_bytes=S, max_batch_blocks=B, index_log2=27, arena_slots=512, keep_recipes=1, timing=1)
+    total = nb * S + 4096
+    dev = ctx.dev_alloc(total)
+    ctx.corpus_fill(dev, roots, nb, spb, SEG, SEED)
+    blocks = [ctx.d2h(dev + b * S, S) for b in range(nb)]
+    ids = list(range(nb))
+    ora = Oracle()
+    expect = ora.reduce_many_full(blocks, ids, _threads())
+    q = []
+    checked = {0: 0, 1: 0}
+
+    def collect():
+        gen, k = q.pop(0)
+        ctx.wait_batch()
+        assert ctx.last_nblocks() == B
+        for i in range(B):
+            compare_block(ctx.batch_result(i), expect[k * B + i], tag=f"generation {gen} batch {k} block {i}")
+        checked[gen] += 1
+
+    for gen in range(2):
+        ctx.reset_async()
+        if gen == 1:
+            assert len(q) == nbatch, "the first generation's batches must be in flight across the reset"
+        for k in range(nbatch):
+            if len(q) >= depth:
+                collect()
+            g = range(k * B, (k + 1) * B)
+            ctx.submit_batch([dev + b * S for b in g], [S] * B, [total - b * S for b in g], [ids[b] for b in g])
+            q.append((gen, k))
+    while q:
+        collect()
+    assert checked == {0: nbatch, 1: nbatch}
+    compare_state(ctx, ora, ids, tag="second generation, primed bench shape")
+    st = ctx.stats()
+    assert st["blocks"] == nb and st["new_bytes"] == sum(int(e["store_size"]) for e in expect)
+    ctx.dev_free(dev)
+    ctx.close()
+
+
 @pytest.mark.timeout(1200)
 def test_config4_bench_batches_depth5_full_state():
     """BASELINE config 4 at the bench's exact shape (bench.py --workload config4 defaults): mixed-
