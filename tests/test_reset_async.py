@@ -125,17 +125,18 @@ def _check_files(disk, ora, tag):
     return n
 
 
-@pytest.mark.parametrize("compressor", [1, 2])
-def test_reset_async_durable_generations(compressor):
-    """Durable containers: three generations of host blocks submitted three deep, hdrf_reset_async
+@pytest.mark.parametrize("compressor,ngen,nblk,slots", [(1, 3, 16, 80), (2, 3, 16, 80), (1, 12, 2, 40)])
+def test_reset_async_durable_generations(compressor, ngen, nblk, slots):
+    """Durable containers: generations of host blocks submitted three deep, hdrf_reset_async
     between them with the previous generation's batches in flight, a drain after every completed
     batch.  Each generation's blocks and drained files equal its own oracle run, and the rings of
-    20 slots per range wrap across the generations (the new generation continues each ring past
-    the old open container)."""
+    slots / 4 per range wrap across the generations (the new generation continues each ring past
+    the old open container).  Two-block generations put two generation switches in flight at once
+    (each holds one more slot per ring until it is waited for)."""
     cmax = 1 << 20
-    gens = [_durable_blocks(91 + 7 * g + compressor, 16) for g in range(3)]
+    gens = [_durable_blocks(91 + 7 * g + compressor, nblk) for g in range(ngen)]
     ctx = Context(compressor=compressor, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=1,
-                  index_log2=20, arena_slots=80, retain_containers=1)
+                  index_log2=20, arena_slots=slots, retain_containers=1)
     oras = [Oracle(compressor=compressor, max_size=cmax) for _ in gens]
     disks = [{} for _ in gens]
     pend = []
@@ -156,9 +157,9 @@ def test_reset_async_durable_generations(compressor):
     while pend:
         complete()
     assert ctx.drain_containers() == []
-    total = sum(_check_files(disks[g], oras[g], f"generation {g}") for g in range(3))
-    assert total > 3 * 20, "the rings of 20 slots per range must have wrapped"
-    compare_state(ctx, oras[2], [0x700 + b for b in range(16)], tag=f"durable generations c{compressor}",
+    total = sum(_check_files(disks[g], oras[g], f"generation {g}") for g in range(ngen))
+    assert total > slots - slots // 4, "the rings of slots / 4 per range must have wrapped"
+    compare_state(ctx, oras[-1], [0x700 + b for b in range(nblk)], tag=f"durable generations c{compressor}",
                   containers=False)
     ctx.close()
 
@@ -195,8 +196,7 @@ def test_reset_async_durable_undrained_refused():
     _check_files(disk2, new, "new generation")
 
     # forced: a view completes the switch batch anyway -> the old containers are dropped, the context is lost
-    ctx.submit_host([blocks[2].ctypes.data], [len(blocks[2])], [3])     # generation 2, never drained
-    ctx.wait_batch()
+    ctx.submit_host([blocks[2].ctypes.data], [len(blocks[2])], [3])     # generation 2, in flight, never drained
     ctx.reset_async()
     ctx.submit_host([blocks[3].ctypes.data], [len(blocks[3])], [4])     # generation 3
     with pytest.raises(HdrfError) as ei:
