@@ -125,7 +125,7 @@ def _check_files(disk, ora, tag):
     return n
 
 
-@pytest.mark.parametrize("compressor,ngen,nblk,slots", [(1, 3, 16, 80), (2, 3, 16, 80), (1, 12, 2, 40)])
+@pytest.mark.parametrize("compressor,ngen,nblk,slots", [(1, 3, 16, 80), (2, 3, 16, 80), (1, 16, 2, 80)])
 def test_reset_async_durable_generations(compressor, ngen, nblk, slots):
     """Durable containers: generations of host blocks submitted three deep, hdrf_reset_async
     between them with the previous generation's batches in flight, a drain after every completed
