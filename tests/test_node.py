@@ -497,3 +497,21 @@ def test_node_bench_rehearsal_two_ranks_one_device(tmp_path):
               "gx_alloc_scan(gx_scan_kernel)", "gx_commit(own_commit)", "gx_local(scratch claim/apply/decide + gx_emit)"):
         assert st[k]["ms_per_step"] > 0, (k, st[k])
     assert l2["roofline"]["frac"] > 0 and l2["roofline"]["front_period_ms"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_node_loopback_bench_shape_two_ranks():
+    """Node-global ranks at the bench's exact batch shape (scripts/node_loopback.py: G = 2 contexts
+    on one device as the bench opens them — 32 x 128 MiB blocks per rank per global batch, index
+    2^27, 512 arena slots, recipes, timing — the bench's global corpus sharded rank-major, pipelined
+    as NodeRank.reduce_batches): both global batches, 64 blocks of 128 MiB, equal the oracle over the
+    global block order chunk for chunk (offsets, digests, is_new, storeSize)."""
+    import json
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "node_loopback.py"), "--G", "2", "--batches",
+                        "2", "--check", "2"], cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT), capture_output=True,
+                       text=True, timeout=850)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    print(json.dumps(line))
+    assert line["oracle_check"] == {"blocks": 128, "mismatches": 0}, line["oracle_check"]
