@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) gx_emit_kernel(const BlockState *__restri
 #pragma unroll
     for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
     const int d = owner_of(dw[0], G);
-    const unsigned long long i = atomicAdd(counts + d, 1ull);
+    const unsigned long long i = wave_reserve(counts, d);
     if ((int64_t)i >= cap) { atomicOr(err, 16); return; }
     uint32_t *rec = x1 + ((size_t)d * cap + i) * (HW + 2);
 #pragma unroll

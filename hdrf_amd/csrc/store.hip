@@ -530,7 +530,7 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
             if (f & 4) {                                   // owner commits the new entry's location
                 const uint32_t ri = e->cid;
                 const int d = (int)(ri / (uint64_t)gx.cap);
-                const unsigned long long i = atomicAdd(gx.counts + d, 1ull);
+                const unsigned long long i = wave_reserve(gx.counts, d);
                 uint32_t *rec = gx.x3 + ((size_t)d * gx.cap + i) * 4;
                 rec[0] = gx.x2[2 * (size_t)ri];
                 rec[1] = cid; rec[2] = pos; rec[3] = pos + ((f & 1) && do_copy ? len : 0u);

@@ -25,14 +25,16 @@
 //
 // usage: packet_driver BLOCKS BLOCK_MIB PACKET_KIB THREADS STEPS [OUT_DIR] [--compressor C]
 //          [--mirror ring|socket|none] [--batch] [--mixed] [--container-kib K] [--arena-slots N]
-//          [--index-log2 L]
+//          [--index-log2 L] [--out-blocks K] [--out-containers M]
 //   The corpus is BASELINE config 2's (1 MiB segments, 50 % cross-block duplicates, seed
 //   20251015; --mixed: config 4's mixed-entropy segments), generated on the device and copied to
 //   pinned host memory before the timed steps.  Prints one JSON line.  OUT_DIR (optional) receives
 //   the last step's results: blocks.txt ("block n_chunks store_size"), blk_<b>.bin per block
 //   (offsets u32[n], digests u8[n*H], is_new u8[n]) and containers.bin (the chunkDir the drained
 //   events built: records [u32 id][u32 closed][u64 len][bytes]); the parity test compares them
-//   with the oracle.
+//   with the oracle.  With OUT_DIR the results come from one more, untimed step after the timed
+//   ones; --out-blocks K keeps blk_<b>.bin of blocks b < K only, --out-containers M the containers
+//   whose per-range index (id & 0x3FFFFF) is below M (bench.py's sample check).
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -209,7 +211,7 @@ int main(int argc, char **argv)
         std::fprintf(stderr,
                      "usage: %s BLOCKS BLOCK_MIB PACKET_KIB THREADS STEPS [OUT_DIR] [--compressor C] "
                      "[--mirror ring|socket|none] [--batch] [--mixed] [--container-kib K] [--arena-slots N] "
-                     "[--index-log2 L]\n",
+                     "[--index-log2 L] [--out-blocks K] [--out-containers M]\n",
                      argv[0]);
         return 2;
     }
@@ -221,7 +223,7 @@ int main(int argc, char **argv)
     const char *out_dir = nullptr;
     int compressor = 1, mirror_mode = 1, mixed = 0, index_log2 = 27;
     bool batch = false;
-    int64_t container = 1ll << 25, arena = 512;
+    int64_t container = 1ll << 25, arena = 512, out_blocks = -1, out_conts = -1;
     for (int i = 6; i < argc; i++) {
         const std::string a = argv[i];
         const char *v = i + 1 < argc ? argv[i + 1] : "";
@@ -235,6 +237,8 @@ int main(int argc, char **argv)
         else if (a == "--container-kib") container = std::atoll(v) << 10, i++;
         else if (a == "--arena-slots") arena = std::atoll(v), i++;
         else if (a == "--index-log2") index_log2 = std::atoi(v), i++;
+        else if (a == "--out-blocks") out_blocks = std::atoll(v), i++;
+        else if (a == "--out-containers") out_conts = std::atoll(v), i++;
         else if (a.size() && a[0] != '-' && !out_dir) out_dir = argv[i];
         else {
             std::fprintf(stderr, "bad argument %s\n", a.c_str());
@@ -312,7 +316,7 @@ int main(int argc, char **argv)
             for (int64_t i = 0; i < n; i++) {
                 const hdrf_container_event &e = ev[(size_t)i];
                 drained_bytes += e.nbytes;
-                if (!capture) continue;
+                if (!capture || (out_conts >= 0 && (int64_t)(e.id & 0x3FFFFFu) >= out_conts)) continue;
                 auto &f = disk[e.id];
                 const uint8_t *src = (const uint8_t *)dbuf + e.data_off;
                 if (e.file_off == 0) f.first.assign(src, src + e.nbytes);   // (re)write
@@ -341,7 +345,7 @@ int main(int argc, char **argv)
         for (int64_t i = 0; i < k; i++) {
             const int64_t b = done + i;
             CK(hdrf_batch_info(ctx, (int32_t)i, &n_chunks[(size_t)b], &store[(size_t)b]));
-            if (capture) {
+            if (capture && (out_blocks < 0 || b < out_blocks)) {
                 BlockOut &o = bout[(size_t)b];
                 const int64_t n = n_chunks[(size_t)b];
                 o.off.resize((size_t)n);
@@ -357,11 +361,14 @@ int main(int argc, char **argv)
     };
     const int kDepth = 5, kRx = 16;                // HDRF_PIPELINE_DEPTH, receive buffers (hdrf.h)
     double best = 0, total_s = 0;
-    for (int step = 0; step <= steps; step++) {    // step 0: warm-up
+    // step 0: warm-up; steps 1..steps timed; OUT_DIR: one more, untimed step keeps the results
+    const int last = steps + (out_dir ? 1 : 0);
+    int64_t timed_drained_bytes = 0, timed_drained_events = 0;
+    for (int step = 0; step <= last; step++) {
         CK(hdrf_reset(ctx));
         done = 0;
         drained_bytes = drained_events = 0;
-        capture = out_dir && step == steps;
+        capture = out_dir && step == last;
         if (capture) disk.clear();
         std::mutex mu;
         std::condition_variable cv;
@@ -504,10 +511,12 @@ int main(int argc, char **argv)
         else
             completer.join();
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        batches = nbt;
-        if (step > 0) {
+        if (step > 0 && step <= steps) {
+            batches = nbt;
             total_s += s;
             best = std::max(best, nb * S / s / 1e9);
+            timed_drained_bytes = drained_bytes;
+            timed_drained_events = drained_events;
         }
     }
     // the mirror received every block of every step once, in the order its receiver took them
@@ -533,7 +542,7 @@ int main(int argc, char **argv)
             }
             nmir += (int64_t)mids[(size_t)r].size();
         }
-        mirror_ok &= nmir == nb * (steps + 1);
+        mirror_ok &= nmir == nb * (last + 1);
         for (auto &m : mirrors)
             if (m.mode == 2) close(m.fd[1]);
     }
@@ -551,14 +560,15 @@ int main(int argc, char **argv)
                 mirror_ok ? "true" : "false", (long long)mirrored,
                 batch ? "hdrf_submit_slots (the blocks received in order since the last submit, <= 16)"
                       : "hdrf_submit_slot (one block per batch)",
-                (long long)batches, (long long)container, (long long)drained_bytes, (long long)drained_events);
+                (long long)batches, (long long)container, (long long)timed_drained_bytes,
+                (long long)timed_drained_events);
     if (out_dir) {
         const std::string d = out_dir;
         FILE *f = std::fopen((d + "/blocks.txt").c_str(), "w");
         for (int64_t b = 0; b < nb; b++)
             std::fprintf(f, "%lld %lld %lld\n", (long long)b, (long long)n_chunks[(size_t)b], (long long)store[(size_t)b]);
         std::fclose(f);
-        for (int64_t b = 0; b < nb; b++) {
+        for (int64_t b = 0; b < nb && (out_blocks < 0 || b < out_blocks); b++) {
             FILE *g = std::fopen((d + "/blk_" + std::to_string(b) + ".bin").c_str(), "wb");
             const BlockOut &o = bout[(size_t)b];
             std::fwrite(o.off.data(), 4, o.off.size(), g);
