@@ -528,7 +528,7 @@ static int drain(hdrf_ctx *ctx)
     HIPCK(hipStreamSynchronize(ctx->stB2));
     if (ctx->stX) HIPCK(hipStreamSynchronize(ctx->stX));
     if (rc) return rc;
-    if (ctx->gen_pending) {
+    if (ctx->gen_pending && ctx->gx_nfront == ctx->gx_nback) {
         // hdrf_reset_async with no batch submitted since: the caller of a view or a restore sees the
         // fresh generation it asked for, applied now (a restore is then not undone by the next submit)
         if (ctx->cfg.retain_containers && gen_undrained(ctx))
@@ -768,10 +768,18 @@ extern "C" int hdrf_reset_async(hdrf_ctx *ctx)
 {
     HDRF_LOCK(ctx);
     if (!ctx) return HDRF_E_INVAL;
-    if (ctx->G > 1) return set_err(ctx, HDRF_E_INVAL, "hdrf_reset_async: single-node contexts (hdrf_reset)");
     for (int i = 0; i < hdrf_ctx::kRx; i++)
         if (ctx->rx[i].state.load() == 1)
             return set_err(ctx, HDRF_E_INVAL, "a block is being received (hdrf_submit_slot or hdrf_rx_cancel first)");
+    if (ctx->G > 1) {
+        // node-global: the switch is made by the back phases of the next launched front's batch
+        // (hdrf_gx_owner: the next epoch, the node's allocator re-seeded on the back stream after the
+        // old batches' commits; hdrf_gx_place_wait: the host side), since the owner phases of the
+        // batches in flight are still to be enqueued with the old epoch
+        if (ctx->gx_nfront == ctx->gx_nback && !ctx->gen_pending) return init_state(ctx, false);
+        ctx->gen_pending = true;
+        return 0;
+    }
     if (ctx->nsub == ctx->nwait && !ctx->gen_pending) return init_state(ctx, false);   // nothing in flight
     ctx->gen_clear = ctx->gen_clear || ctx->epoch >= 255;
     ctx->epoch = ctx->epoch >= 255 ? 1 : ctx->epoch + 1;
@@ -2292,6 +2300,8 @@ extern "C" int hdrf_gx_front_launch(hdrf_ctx *ctx, int32_t nblocks, const uint8_
     if (block_ids) S.ids.assign(block_ids, block_ids + nblocks);
     S.gx_inuse = true;
     S.gx_split = false;
+    S.gen_reset = ctx->gen_pending;                    // the first batch of a fresh generation (hdrf_reset_async)
+    ctx->gen_pending = false;
     ctx->gx_nfront++;
     return 0;
 }
@@ -2343,6 +2353,22 @@ extern "C" int hdrf_gx_owner(hdrf_ctx *ctx, const uint32_t *x1_recv, const int64
         if (recv_counts[s] < 0 || recv_counts[s] > ctx->gx_cap) return set_err(ctx, HDRF_E_INVAL, "bad receive count");
     hipStream_t st = ctx->stB;
     const uint64_t seq = ctx->gx_nback;
+    if (S.gen_reset) {
+        // a fresh generation (hdrf_reset_async): the next epoch of the partition's tag words (the table
+        // cleared when it wraps), batches from this one on are this generation's, and the node's
+        // allocator re-seeded — on stream B after every older batch's owner..commit phases, and after
+        // the last arena copy on B2 (the new generation reuses the slot rings from their start)
+        hipEvent_t b2;                                 // everything on B2 so far: older batches' copies
+        HIPCK(hipEventCreateWithFlags(&b2, hipEventDisableTiming));
+        HIPCK(hipEventRecord(b2, ctx->stB2));
+        HIPCK(hipStreamWaitEvent(st, b2, 0));
+        HIPCK(hipEventDestroy(b2));
+        const bool clear = ctx->epoch >= 255;
+        ctx->epoch = clear ? 1 : ctx->epoch + 1;
+        ctx->bfirst = S.gx_batch;
+        HIPCK(launch_index_clear(ctx->d_tab, clear ? ctx->cfg.index_log2 : -1, ctx->d_alloc, initial_alloc(ctx), st, 0u));
+        ctx->h_alloc = initial_alloc(ctx);            // (hdrf_gx_alloc_scan, host form, starts from it)
+    }
     gx_mark(ctx, seq, kG0, st);
     std::memcpy(S.h_gx->up_r1, recv_counts, sizeof(int64_t) * ctx->G);
     HIPCK(hipMemcpyAsync(ctx->d_gx_rcounts, S.h_gx->up_r1, sizeof(int64_t) * ctx->G, hipMemcpyHostToDevice, st));
@@ -2707,6 +2733,11 @@ extern "C" int hdrf_gx_place_wait(hdrf_ctx *ctx, int64_t *send_counts)
     }
     ctx->gx_scanned = 0;
     ctx->gx_dscan = 0;
+    if (S.gen_reset && !*S.h_err) {                    // the fresh generation's host side (hdrf_reset_async)
+        reset_host(ctx);
+        ctx->h_alloc = initial_alloc(ctx);
+        S.gen_reset = false;
+    }
     // (checked before any host bookkeeping: a failed placement leaves the host state untouched; a
     // device error is complete_slot's to report)
     for (int d = 0; d < ctx->G && !*S.h_err; d++)

@@ -283,9 +283,11 @@ class NodeRank:
             ctx.gx_place_launch(None, self.x3s.data_ptr())
         self._tick("enqueue x1..place", t)
 
-    def _back_finish(self):
+    def _back_finish(self, new_gen=False):
         """Wait for the placement's read-back, then X3 and the owners' commit (not waited for)."""
         ctx, xc, cap, w3 = self.ctx, self.xc, self.cap, self.w[2]
+        if new_gen:
+            self.pieces.reset()
         t = time.perf_counter()
         c3 = ctx.gx_place_wait()
         t = self._tick("place wait", t)
@@ -306,13 +308,17 @@ class NodeRank:
         self._back_finish()
         self.ctx.gx_sync()
 
-    def reduce_batches(self, batches, done=None):
+    def reduce_batches(self, batches, done=None, gens=()):
         """Pipelined node-global reduction of a sequence of this rank's batches
         [(dev_ptrs, lens, readable, block_ids, gbase), ...]: the fronts (chunking, SHA, local
         aggregation) of the next `depth` - 1 batches run on the GPU while the oldest is exchanged and
         stored.  done(k) is called after batch k's placement was waited for (its hdrf_batch_* views
-        are valid then)."""
+        are valid then).  gens: the batches that start a fresh DataNode (every rank the same):
+        hdrf_reset_async before their fronts, so the node's steps run back to back, the previous
+        generation's last batches completing while the next one's fronts run (bench.py's primed
+        steps, as at N = 1)."""
         ctx, xc, D = self.ctx, self.xc, self.depth
+        gens = set(gens)
         torch.cuda.current_stream(self.device).synchronize()
         n = len(batches)
         if not n:
@@ -321,6 +327,8 @@ class NodeRank:
 
         def launch():
             nonlocal launched
+            if launched in gens:
+                ctx.reset_async()
             ctx.gx_front_launch(*batches[launched], self.x1sb[launched % D].data_ptr())
             launched += 1
 
@@ -331,13 +339,15 @@ class NodeRank:
         r1 = xc.counts(c1)
         self._tick("front wait+counts", t)
         for k in range(n):
+            if k in gens:
+                self.alloc = None                        # (the chain / host-scan forms' node allocator)
             self._back_enqueue(c1, r1, self.x1sb[k % D])
             if k + 1 < n:                                # host work while the back stream runs
                 t = time.perf_counter()
                 c1 = ctx.gx_front_wait()
                 r1 = xc.counts(c1)
                 self._tick("front wait+counts", t)
-            self._back_finish()
+            self._back_finish(k in gens)
             if done is not None:
                 done(k)
             if launched < n:                             # batch k's slot: the device waits for its back

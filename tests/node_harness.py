@@ -86,14 +86,16 @@ class Loopback:
             ctxs[d].gx_commit(self.x3r[d].data_ptr(), r3[d])
 
 
-    def batches_pipelined(self, per_rank_batches, done=None, scan="device"):
+    def batches_pipelined(self, per_rank_batches, done=None, scan="device", gens=()):
         """per_rank_batches[j][r] = rank r's share of global batch j, run as NodeRank.reduce_batches
         does: the fronts of `depth` batches launched ahead (each rank's slot reused only after its
         previous batch's back phases), the oldest batch's back phases meanwhile.  scan="device":
         the packed flush descriptors all-gathered (region copies here) and composed on the device
         (hdrf_gx_flush_fn_dev / hdrf_gx_alloc_scan_dev), placement launched and waited separately;
-        scan="host": the host descriptors and hdrf_gx_alloc_scan (the A/B form)."""
+        scan="host": the host descriptors and hdrf_gx_alloc_scan (the A/B form).  gens: the global
+        batches that start a fresh DataNode (hdrf_reset_async on every rank before their fronts)."""
         G, ctxs = self.G, self.ctxs
+        gens = set(gens)
         n = len(per_rank_batches)
         lay = ctxs[0].gx_layout()
         D, fnb = int(lay.depth), int(lay.fn_bytes)
@@ -106,6 +108,9 @@ class Loopback:
             nonlocal launched
             per = per_rank_batches[launched]
             gb = np.cumsum([0] + [len(p[0]) for p in per])
+            if launched in gens:
+                for c in ctxs:
+                    c.reset_async()
             for r in range(G):
                 ctxs[r].gx_front_launch(*per[r], int(gb[r]), x1b[launched % D][r].data_ptr())
             launched += 1
@@ -114,6 +119,9 @@ class Loopback:
             launch()
         c1 = [ctxs[r].gx_front_wait() for r in range(G)]
         for j in range(n):
+            if j in gens:
+                self.alloc = None
+                self.pieces.reset()
             send = x1b[j % D]
             r1 = self._a2a(send, self.x1r, c1, self.w[0])
             for d in range(G):

@@ -515,3 +515,63 @@ def test_node_loopback_bench_shape_two_ranks():
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     print(json.dumps(line))
     assert line["oracle_check"] == {"blocks": 128, "mismatches": 0}, line["oracle_check"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,compressor,scan", [(2, 1, "device"), (3, 2, "device"), (2, 1, "host")])
+def test_node_loopback_reset_async_generations(G, compressor, scan, monkeypatch):
+    """Node-global hdrf_reset_async (bench.py's primed N > 1 steps): three generations of two or three
+    global batches, each started with hdrf_reset_async on every rank before its first front while the
+    previous generation's batches are still in the pipeline.  Every block equals a fresh oracle per
+    generation (the switch is made by the first new batch's owner phase: the next epoch, the node's
+    allocator re-seeded after the old commits and arena copies); after the last generation the
+    merged index and the allocator are that generation's oracle's."""
+    import torch  # noqa: F401
+    from node_harness import Loopback, merged_index, open_ranks
+    from oracle.oracle import Oracle
+    monkeypatch.setenv("HDRF_GX_DEPTH", "3")
+    cmax = 1 << 20
+    gens_sched = [[[2] * G, [1] * G, [2] * G], [[1] * G, [2] * G], [[2] * G, [1] * G, [1] * G]]
+    ctxs = open_ranks(G, compressor=compressor, container_max=cmax, max_block_bytes=4 << 20, max_batch_blocks=4,
+                      index_log2=20, arena_slots=256)
+    lb = Loopback(ctxs)
+    devs, per_batch, where, starts = [], [], [], []
+    oras, blocks_of = [], []
+    for q, sched in enumerate(gens_sched):
+        seq = _plan(sched)
+        blocks = _mixed_blocks(61 + q, len(seq), 500_000)
+        blocks_of.append(blocks)
+        oras.append(Oracle(compressor=compressor, max_size=cmax))
+        starts.append(len(per_batch))
+        g = 0
+        for per in sched:
+            pr, wj = [], []
+            for r, n in enumerate(per):
+                ptrs, lens, rd, ids = [], [], [], []
+                for i in range(n):
+                    blk = blocks[g]
+                    p = ctxs[r].dev_alloc(len(blk) + 4096)
+                    ctxs[r].h2d(p, blk)
+                    devs.append((ctxs[r], p))
+                    ptrs.append(p); lens.append(len(blk)); rd.append(len(blk) + 4096); ids.append(0x900 + g)
+                    wj.append((q, r, i, g))
+                    g += 1
+                pr.append((ptrs, lens, rd, ids))
+            per_batch.append(pr)
+            where.append(wj)
+
+    def done(j):
+        for q, r, i, gi in where[j]:
+            compare_block(ctxs[r].batch_result(i), oras[q].reduce(blocks_of[q][gi], 0x900 + gi),
+                          tag=f"generation {q} batch {j} rank {r} block {i}")
+    lb.batches_pipelined(per_batch, done, scan=scan, gens=starts)
+    gk, gv = merged_index(ctxs)
+    ok, ov = oras[-1].index_dump()
+    assert np.array_equal(gk, ok) and np.array_equal(gv, ov), "node index after the last generation differs"
+    for r, c in enumerate(ctxs):
+        assert c.allocator() == oras[-1].allocator()
+        assert c.stats()["blocks"] == sum(per[r] for per in gens_sched[-1]), "the totals are the last generation's"
+    for c, p in devs:
+        c.dev_free(p)
+    for c in ctxs:
+        c.close()
