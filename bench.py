@@ -195,14 +195,14 @@ def packet_driver_line(a):
         raise SystemExit("packet driver failed (%d): %s %s" % (r.returncode, r.stdout[-2000:], r.stderr[-2000:]))
     d = json.loads(r.stdout.strip().splitlines()[-1])
     S = a.block_mib << 20
+    import torch                              # (torch initialises HIP before libhdrf does in this process)
+    link = link_probe(torch, 0, S)
     check = None
     if out_dir:
         try:
             check = packet_check(out_dir, nb, a.block_mib, compressor, a.mixed)
         finally:
             shutil.rmtree(out_dir, ignore_errors=True)
-    import torch
-    link = link_probe(torch, 0, S)
     drained = d["drained_bytes_last_step"]
     line = {"metric": METRIC, "value": d["GB_s"], "unit": "GB/s", "n_gpus": 1, "steps": a.steps, "warmup": 1,
             "ms_per_step": round(nb * S / d["GB_s"] / 1e6, 3), "higher_is_better": True, "scaling": "weak",
@@ -556,9 +556,25 @@ def main():
     # one batch chain per step) are gone.  --no-prime: the round-4 shape (drain + reset per step).
     # Config 5 whole blocks (durable containers) too: each step's containers are drained as its
     # batches complete, the next step's H2D copies start beside the last batches and drains.
-    primed = node is None and not a.serial and not a.no_prime and not (host and a.packet_kib)
+    primed = not a.serial and not a.no_prime and not (host and a.packet_kib)
+
+    def run_primed_node(nsteps):
+        # N > 1: every step's batches in one pipelined sequence, hdrf_reset_async on every rank before
+        # the first front of each step (hdrf_amd/node.py reduce_batches gens), so the previous step's
+        # last batches complete while the next step's fronts run — the N = 1 step shape
+        nbatch = len(batches)
+        seq = [(ptrs, lens, rd, ids, rank * B) for _ in range(nsteps) for ptrs, lens, rd, ids in batches]
+
+        def done(k):
+            k0 = (k % nbatch) * B
+            for i in range(ctx.last_nblocks()):
+                n_chunks[k0 + i], store[k0 + i] = ctx.batch_info(i)
+
+        node.reduce_batches(seq, done, gens=[s * nbatch for s in range(nsteps)])
 
     def run_primed(nsteps):
+        if node is not None:
+            return run_primed_node(nsteps)
         from collections import deque
         q = deque()
 
@@ -832,7 +848,7 @@ def main():
                                           " + Lz4Codec on closed containers" if compressor == 2 else "",
                                           " + recipes (device store)" if a.keep_recipes else ", no recipes"),
                            "blocks_per_gpu": nb, "block_bytes": S, "batch_blocks_per_gpu": B,
-                           "batches_in_flight": a.depth, "steps_back_to_back": bool(primed),
+                           "batches_in_flight": node.depth if node is not None else a.depth, "steps_back_to_back": bool(primed),
                            "parallelism": "dp%d: blocks sharded by rank; one index partitioned by digest prefix"
                                           % world},
                 "roofline": roofline, "cpu_baseline": cpu, "dedup": dedup, "stages": stages}
