@@ -252,35 +252,26 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 
 __device__ __forceinline__ unsigned long long ballot64(bool p) { return __ballot(p); }
 
-// Reserve one slot of counter counts[d] for every calling lane (d per lane, any number of distinct
-// counters): one atomic per distinct d per wave instead of one per lane.  The node-global record
-// regions (gx_emit, place part 1) are filled through a handful of counters (one per owner rank),
-// and one returning atomic per chunk on those few addresses serialised at the memory side
-// (2.3 M per 4 GiB batch: gx_emit 30.8 ms, place part 1 20 ms, profiles/r06_lb2_kernel_stats.csv).
-// Call from lanes in the same control flow; the slots a wave takes are contiguous per counter.
-__device__ __forceinline__ unsigned long long wave_reserve(unsigned long long *counts, int d)
+// Reserve one slot of counter counts[d] for every lane that wants one (256 threads; every thread of
+// the workgroup calls it, in uniform control flow): the lanes count in LDS, then one global atomic
+// per (workgroup, counter) takes the workgroup's slots (d < G <= 64; s_cnt / s_base: LDS [64]).  The
+// node-global record regions are filled through G counters, one per owner rank: one returning
+// atomic per chunk on those few addresses serialised at the memory side (gx_emit 30.8 ms and place
+// part 1 ~20 ms per 4 GiB batch, profiles/r06_lb2_kernel_stats.csv), one per wave still ~1.5 ms.
+__device__ __forceinline__ unsigned long long wg_reserve(unsigned long long *counts, int d, bool want, int G,
+                                                         uint32_t *s_cnt, unsigned long long *s_base)
 {
-    bool todo = true;
-    unsigned long long idx = 0;
-    const unsigned long long lt = (1ull << lane_id()) - 1ull;
-    for (;;) {
-        const unsigned long long pend = ballot64(todo);
-        if (!pend) break;
-        const int leader = __builtin_ctzll(pend);
-        const int dl = __builtin_amdgcn_readlane(d, leader);
-        const bool mine = todo && d == dl;
-        const unsigned long long m = ballot64(mine);
-        unsigned long long base = 0;
-        if (lane_id() == leader) base = atomicAdd(counts + dl, (unsigned long long)__popcll(m));
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, leader);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), leader);
-        if (mine) {
-            idx = (((unsigned long long)hi << 32) | lo) + (unsigned long long)__popcll(m & lt);
-            todo = false;
-        }
-    }
-    return idx;
+    const int t = (int)threadIdx.x;
+    if (t < G) s_cnt[t] = 0u;
+    __syncthreads();
+    uint32_t li = 0;
+    if (want) li = atomicAdd(&s_cnt[d], 1u);
+    __syncthreads();
+    if (t < G && s_cnt[t]) s_base[t] = atomicAdd(counts + t, (unsigned long long)s_cnt[t]);
+    __syncthreads();
+    return want ? s_base[d] + li : 0ull;
 }
+
 
 // Bounds-checked 16-B load (bytes >= avail read as 0).
 __device__ __noinline__ uint4 load16_guard(const uint8_t *base, int64_t off, int64_t avail)

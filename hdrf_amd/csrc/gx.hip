@@ -28,9 +28,13 @@ namespace hdrf {
 
 __device__ __forceinline__ int owner_of(uint32_t dw0, int G) { return (int)(dw0 % (uint32_t)G); }
 
-// ---- gx_emit: grid (ntiles, nblocks) over the local batch ---------------------------------
+// ---- gx_emit: grid (ceil(ntiles / kEmitTiles), nblocks) over the local batch -----------------
 // The chunk designated in the scratch table (min local block, its last occurrence) emits the
-// digest's record.  scratch.cid <- response index (owner * cap + i).
+// digest's record.  scratch.cid <- response index (owner * cap + i).  A workgroup takes kEmitTiles
+// tiles of 256 chunks and reserves its records with one atomic per owner (wg_reserve): one atomic
+// per record on the G counters serialised at the memory side (30.8 ms per 4 GiB batch, one per
+// wave still 1.5 ms; profiles/r06_lb2_kernel_stats.csv, r06_lb2b_kernel_stats.csv).
+constexpr int kEmitTiles = 4;
 template <int HW>
 __global__ void __launch_bounds__(256) gx_emit_kernel(const BlockState *__restrict__ bst, int cap_blk,
                                                       const uint32_t *__restrict__ digests,
@@ -39,26 +43,52 @@ __global__ void __launch_bounds__(256) gx_emit_kernel(const BlockState *__restri
                                                       uint32_t *__restrict__ x1, int64_t cap,
                                                       unsigned long long *__restrict__ counts, int *__restrict__ err)
 {
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= bst[b].n_chunks) return;
-    const size_t c = (size_t)b * cap_blk + k;
-    const uint8_t f = flags[c];
-    if (!(f & 2)) return;                                   // not in the digest's min local block
-    IndexEntry *e = scratch + slot[c];
-    if ((f & 16) && (uint32_t)e->first != (uint32_t)(k + 1)) return;   // not its last occurrence
-    uint32_t dw[HW];
+    __shared__ uint32_t s_cnt[64];
+    __shared__ unsigned long long s_base[64];
+    const int b = blockIdx.y, t = (int)threadIdx.x;
+    const int n = bst[b].n_chunks;
+    if ((int)blockIdx.x * kEmitTiles * 256 >= n) return;     // (uniform)
+    if (t < G) s_cnt[t] = 0u;
+    __syncthreads();
+    bool want[kEmitTiles];
+    int dd[kEmitTiles];
+    uint32_t li[kEmitTiles];
 #pragma unroll
-    for (int i = 0; i < HW; i++) dw[i] = digests[c * HW + i];
-    const int d = owner_of(dw[0], G);
-    const unsigned long long i = wave_reserve(counts, d);
-    if ((int64_t)i >= cap) { atomicOr(err, 16); return; }
-    uint32_t *rec = x1 + ((size_t)d * cap + i) * (HW + 2);
+    for (int j = 0; j < kEmitTiles; j++) {
+        const int k = ((int)blockIdx.x * kEmitTiles + j) * 256 + t;
+        want[j] = false;
+        dd[j] = 0;
+        li[j] = 0;
+        if (k < n) {
+            const size_t c = (size_t)b * cap_blk + k;
+            const uint8_t f = flags[c];
+            // in the digest's min local block, and its last occurrence there
+            if ((f & 2) && (!(f & 16) || (uint32_t)scratch[slot[c]].first == (uint32_t)(k + 1))) {
+                want[j] = true;
+                dd[j] = owner_of(digests[c * HW], G);
+                li[j] = atomicAdd(&s_cnt[dd[j]], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    if (t < G && s_cnt[t]) s_base[t] = atomicAdd(counts + t, (unsigned long long)s_cnt[t]);
+    __syncthreads();
 #pragma unroll
-    for (int q = 0; q < HW; q++) rec[q] = dw[q];
-    rec[HW] = gbase + (uint32_t)b;                          // batch position of the min block
-    rec[HW + 1] = (uint32_t)__popcll(e->mask);              // local blocks holding the digest
-    e->cid = (uint32_t)((size_t)d * cap + i);
+    for (int j = 0; j < kEmitTiles; j++) {
+        if (!want[j]) continue;
+        const int k = ((int)blockIdx.x * kEmitTiles + j) * 256 + t;
+        const size_t c = (size_t)b * cap_blk + k;
+        const int d = dd[j];
+        const unsigned long long i = s_base[d] + li[j];
+        if ((int64_t)i >= cap) { atomicOr(err, 16); continue; }
+        IndexEntry *e = scratch + slot[c];
+        uint32_t *rec = x1 + ((size_t)d * cap + i) * (HW + 2);
+#pragma unroll
+        for (int q = 0; q < HW; q++) rec[q] = digests[c * HW + q];
+        rec[HW] = gbase + (uint32_t)b;                          // batch position of the min block
+        rec[HW + 1] = (uint32_t)__popcll(e->mask);              // local blocks holding the digest
+        e->cid = (uint32_t)((size_t)d * cap + i);
+    }
 }
 
 // ---- owner side: grid (ceil(cap/256), G) over the records received from each source ------
@@ -199,30 +229,40 @@ __global__ void __launch_bounds__(256) own_decide_kernel(const uint32_t *__restr
                                                          uint32_t cur, uint32_t *__restrict__ x2,
                                                          unsigned long long *__restrict__ x3exp, const int *__restrict__ err)
 {
+    __shared__ uint32_t s_n;
     const int s = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= counts[s]) return;
-    const size_t r = (size_t)s * cap + i;
-    if (*err & 6) {
-        x2[2 * r] = 0;
-        x2[2 * r + 1] = 0;
-        return;
+    const int64_t cnt_s = counts[s];
+    if ((int64_t)blockIdx.x * 256 >= cnt_s) return;          // (uniform)
+    if (threadIdx.x == 0) s_n = 0u;
+    __syncthreads();
+    bool want3 = false;
+    if (i < cnt_s) {
+        const size_t r = (size_t)s * cap + i;
+        if (*err & 6) {
+            x2[2 * r] = 0;
+            x2[2 * r + 1] = 0;
+        } else {
+            const uint32_t gpos = x1[r * rw + rw - 2];
+            const uint32_t h = oslot[r];
+            IndexEntry *e = tab + h;
+            const bool created = e->batch == cur;
+            const bool holds = (uint32_t)e->first == 0xffffffffu - gpos;
+            if (holds) {
+                const uint32_t cnt = (uint32_t)e->mask;
+                // chunkMeta.process: nCopy = old + 1 per later block (DN/chunkMeta.java:35-60), 1 when new
+                set_ncopy(e, created ? cnt : e->ncopy + cnt);
+            }
+            x2[2 * r] = h;
+            x2[2 * r + 1] = (created ? 1u : 0u) | (holds ? 2u : 0u);
+            want3 = created && holds;
+        }
     }
-    const uint32_t gpos = x1[r * rw + rw - 2];
-    const uint32_t h = oslot[r];
-    IndexEntry *e = tab + h;
-    const bool created = e->batch == cur;
-    const bool holds = (uint32_t)e->first == 0xffffffffu - gpos;
-    if (holds) {
-        const uint32_t cnt = (uint32_t)e->mask;
-        // chunkMeta.process: nCopy = old + 1 per later block (DN/chunkMeta.java:35-60), 1 when new
-        set_ncopy(e, created ? cnt : e->ncopy + cnt);
-    }
-    x2[2 * r] = h;
-    x2[2 * r + 1] = (created ? 1u : 0u) | (holds ? 2u : 0u);
-    // the lanes still here are a prefix of the wave (i < counts[s]; err is uniform): lane 0 counts
-    const unsigned long long m3 = ballot64(created && holds);
-    if (lane_id() == 0 && m3) atomicAdd(x3exp + s, (unsigned long long)__popcll(m3));
+    // the X3 records this owner will receive from source s: one atomic per workgroup
+    const unsigned long long m3 = ballot64(want3);
+    if (lane_id() == 0 && m3) atomicAdd(&s_n, (uint32_t)__popcll(m3));
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) atomicAdd(x3exp + s, (unsigned long long)s_n);
 }
 
 __global__ void __launch_bounds__(256) own_finish_kernel(const uint32_t *__restrict__ x2, const int64_t *__restrict__ counts,
@@ -284,11 +324,17 @@ __global__ void __launch_bounds__(256) gx_x3want_kernel(const uint32_t *__restri
                                                         const unsigned long long *__restrict__ sent, int64_t cap,
                                                         unsigned long long *__restrict__ want)
 {
+    __shared__ uint32_t s_n;
     const int d = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if ((int64_t)blockIdx.x * 256 >= (int64_t)sent[d]) return;   // (uniform)
+    if (threadIdx.x == 0) s_n = 0u;
+    __syncthreads();
     const bool ok = i < (int64_t)sent[d] && (x2[2 * ((size_t)d * cap + i) + 1] & 3u) == 3u;
     const unsigned long long m = ballot64(ok);
-    if (lane_id() == 0 && m) atomicAdd(want + d, (unsigned long long)__popcll(m));
+    if (lane_id() == 0 && m) atomicAdd(&s_n, (uint32_t)__popcll(m));   // one global atomic per workgroup
+    __syncthreads();
+    if (threadIdx.x == 0 && s_n) atomicAdd(want + d, (unsigned long long)s_n);
 }
 
 hipError_t launch_gx_x3want(const uint32_t *x2, const unsigned long long *sent, int64_t max_sent, int64_t cap, int G,
@@ -325,7 +371,7 @@ hipError_t launch_gx_emit(int hasher, const BlockState *bst, int nblocks, int ca
                           hipStream_t st)
 {
     if (hipError_t e = hipMemsetAsync(counts, 0, sizeof(unsigned long long) * G, st)) return e;
-    dim3 g(ntiles, nblocks);
+    dim3 g((ntiles + kEmitTiles - 1) / kEmitTiles, nblocks);
     if (hasher == 0)
         hipLaunchKernelGGL(gx_emit_kernel<5>, g, dim3(256), 0, st, bst, cap_blk, digests, scratch, slot, flags, gbase, G,
                            x1, cap, counts, err);

@@ -489,8 +489,8 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
     const size_t c = (size_t)b * P.cap_blk + k;
     const uint32_t *off = offsets + (size_t)b * P.cap_blk;
     uint8_t f = 0;
-    uint32_t start = 0, len = 0, cid = 0, pos = 0, aslot = 0;
-    bool do_copy = false;
+    uint32_t start = 0, len = 0, cid = 0, pos = 0, aslot = 0, x3_ri = 0;
+    bool do_copy = false, x3_want = false;
     if (k < n) {
         f = flags[c];
         start = k ? off[k - 1] : 0u;
@@ -528,12 +528,8 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
             desig = (uint32_t)e->first == (uint32_t)(k + 1);
         if (desig && gx.x3) {                              // node-global index (gx.hip): the
             if (f & 4) {                                   // owner commits the new entry's location
-                const uint32_t ri = e->cid;
-                const int d = (int)(ri / (uint64_t)gx.cap);
-                const unsigned long long i = wave_reserve(gx.counts, d);
-                uint32_t *rec = gx.x3 + ((size_t)d * gx.cap + i) * 4;
-                rec[0] = gx.x2[2 * (size_t)ri];
-                rec[1] = cid; rec[2] = pos; rec[3] = pos + ((f & 1) && do_copy ? len : 0u);
+                x3_ri = e->cid;                            // (its X3 record, written below)
+                x3_want = true;
             }
         } else if (desig) {                                // designated: final index value
             const uint32_t cnt = dcnt ? (uint32_t)dcnt[c] : (uint32_t)__popcll(e->mask);
@@ -548,6 +544,17 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
                 e->first = 0;
             }
         }
+        }
+    }
+    if (gx.x3 && gx.part != 2) {                          // (uniform) the X3 location records, one
+        __shared__ uint32_t s_cnt[64];                     // global atomic per (workgroup, owner): one per
+        __shared__ unsigned long long s_base[64];          // record serialised at the memory side (gx.hip)
+        const int d = (int)(x3_ri / (uint64_t)gx.cap);
+        const unsigned long long i = wg_reserve(gx.counts, x3_want ? d : 0, x3_want, gx.G, s_cnt, s_base);
+        if (x3_want) {
+            uint32_t *rec = gx.x3 + ((size_t)d * gx.cap + i) * 4;
+            rec[0] = gx.x2[2 * (size_t)x3_ri];
+            rec[1] = cid; rec[2] = pos; rec[3] = pos + ((f & 1) && do_copy ? len : 0u);
         }
     }
     if (gx.part == 1) return;                              // placement part: no arena copy
