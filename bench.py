@@ -217,7 +217,9 @@ def packet_driver_line(a):
                        "blocks_per_gpu": nb, "block_bytes": S, "parallelism": "dp1"},
             "roofline": None, "cpu_baseline": None, "mirror": a.mirror != "none", "mirror_ok": d.get("mirror_ok"),
             "packet_driver": d, "driver_wall_s": round(wall, 2), "oracle_check": check,
-            "rate_note": "value = the mean over the timed steps (packet_driver.GB_s); best_GB_s the fastest step"}
+            "rate_note": "value = bytes of all timed steps / their time (packet_driver.GB_s); per-step rates, their "
+                         "median and the fastest step beside it (host-side receive copies: the rate moves with the "
+                         "shared host's memory load, DESIGN.md §11)"}
     line["pcie"] = pcie_entry(d["GB_s"], nb * S, drained, nb * S / d["GB_s"] / 1e9, link)
     print(json.dumps(line), flush=True)
 
@@ -235,7 +237,7 @@ SUB_RUNS = {
     # receive round submitted as one batch (hdrf_submit_slots, the JNI's submitSlots0), compressor 2,
     # durable containers drained after every batch
     "config5_packets": ["--workload", "config5", "--packet-driver", "cpp", "--packet-batch", "--compressor", "2",
-                        "--mirror", "ring", "--steps", "3"],
+                        "--mirror", "ring", "--steps", "5"],
 }
 
 

@@ -361,6 +361,7 @@ int main(int argc, char **argv)
     };
     const int kDepth = 5, kRx = 16;                // HDRF_PIPELINE_DEPTH, receive buffers (hdrf.h)
     double best = 0, total_s = 0;
+    std::vector<double> step_rate;                 // GB/s of every timed step
     // step 0: warm-up; steps 1..steps timed; OUT_DIR: one more, untimed step keeps the results
     const int last = steps + (out_dir ? 1 : 0);
     int64_t timed_drained_bytes = 0, timed_drained_events = 0;
@@ -515,6 +516,7 @@ int main(int argc, char **argv)
             batches = nbt;
             total_s += s;
             best = std::max(best, nb * S / s / 1e9);
+            step_rate.push_back(nb * S / s / 1e9);
             timed_drained_bytes = drained_bytes;
             timed_drained_events = drained_events;
         }
@@ -548,13 +550,25 @@ int main(int argc, char **argv)
     }
     int64_t stored = 0, chunks = 0;
     for (int64_t b = 0; b < nb; b++) { stored += store[(size_t)b]; chunks += n_chunks[(size_t)b]; }
+    std::vector<double> sorted_rate = step_rate;
+    std::sort(sorted_rate.begin(), sorted_rate.end());
+    const double median = sorted_rate.empty() ? 0.0 : sorted_rate[sorted_rate.size() / 2];
+    std::string rates = "[";
+    for (size_t i = 0; i < step_rate.size(); i++) {
+        char b[32];
+        std::snprintf(b, sizeof b, "%s%.3f", i ? ", " : "", step_rate[i]);
+        rates += b;
+    }
+    rates += "]";
     std::printf("{\"driver\": \"tests/cpp/packet_driver.cpp\", \"blocks\": %lld, \"block_bytes\": %lld, "
                 "\"packet_bytes\": %lld, \"threads\": %d, \"steps\": %d, \"GB_s\": %.3f, \"best_GB_s\": %.3f, "
+                "\"median_GB_s\": %.3f, \"step_GB_s\": %s, "
                 "\"packets_per_step\": %lld, \"stored_bytes\": %lld, \"chunks\": %lld, \"compressor\": %d, "
                 "\"corpus\": \"%s\", \"mirror\": \"%s\", \"mirror_ok\": %s, \"mirrored_bytes\": %lld, "
                 "\"submit\": \"%s\", \"batches_per_step\": %lld, \"container_bytes\": %lld, "
                 "\"drained_bytes_last_step\": %lld, \"drained_events_last_step\": %lld}\n",
-                (long long)nb, (long long)S, (long long)P, T, steps, nb * S * steps / total_s / 1e9, best,
+                (long long)nb, (long long)S, (long long)P, T, steps, nb * S * steps / total_s / 1e9, best, median,
+                rates.c_str(),
                 (long long)(nb * ((S + P - 1) / P)), (long long)stored, (long long)chunks, compressor,
                 mixed ? "mixed" : "config2", mirror_mode == 0 ? "none" : mirror_mode == 1 ? "ring" : "socket",
                 mirror_ok ? "true" : "false", (long long)mirrored,
