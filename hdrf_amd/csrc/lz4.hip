@@ -29,6 +29,15 @@ constexpr int kLzSegBound = kLzMaxIn + kLzMaxIn / 255 + 16;
 constexpr int kLzSegStride = kLzSegBound + 4;    // per-segment stride of the unpacked layout
 constexpr int kMfLimit = 12, kLastLit = 5, kMaxDist = 65535, k64KLimit = 65536 + kMfLimit - 1;
 constexpr int kLzFirstBatch = 8;                 // attempts per batch after a match (then 16, 32, 64)
+// Bytes of one lane window (forward, reference, search, candidate): 4 per lane over kLzWin / 4
+// lanes; with 128 the upper 32 lanes load the lower 32 lanes' words again (no extra line
+// requests) and take no part in the compares.  HDRF_LZ4_WIN (A/B builds): 256 or 128.
+#ifndef HDRF_LZ4_WIN
+#define HDRF_LZ4_WIN 256
+#endif
+constexpr int kLzWin = HDRF_LZ4_WIN;
+constexpr int kLzWinLanes = kLzWin / 4;
+static_assert(kLzWin == 256 || kLzWin == 128, "LZ4 window: 256 or 128 bytes");
 
 // length >= 15 continuation bytes (255 ... rest); returns the new output offset
 __device__ __forceinline__ int put_len(uint8_t *out, int op, int len)
@@ -143,7 +152,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         // the last word instead; no such lane's bytes are ever used (every use is bounded by
         // mflimit / matchlimit, at least 5 bytes before n), so one clamp replaces the guards.
         const int nm4 = n - 4;
-        auto wload = [&](int at) -> uint32_t { return ld32u(src, (uint32_t)min(at + 4 * l, nm4)); };
+        const int lw = l & (kLzWinLanes - 1);                // this lane's word of a window
+        auto wload = [&](int at) -> uint32_t { return ld32u(src, (uint32_t)min(at + 4 * lw, nm4)); };
         auto lane_word = [&](uint32_t w, int o) -> uint32_t {   // bytes [o, o + 4) of a window
             const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((o >> 2) << 2, (int)w);
             const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(((o >> 2) + 1) << 2, (int)w);
@@ -167,8 +177,8 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
             const int ipl = fip + l * q + max(0, l - (64 - rr));       // this lane's attempt
             const bool valid = l < m && ipl + step <= mflimit;
             const int last_at = fip + (m - 1) * q + max(0, m - 1 - (64 - rr));   // lane m-1's attempt
-            bool inwin = (uint32_t)(last_at - sb) <= 251u;     // (fip >= sb: last_at >= fip)
-            if (!inwin && last_at - fip <= 251) { Sw = wload(fip); sb = fip; inwin = true; }
+            bool inwin = (uint32_t)(last_at - sb) <= (uint32_t)(kLzWin - 5);     // (fip >= sb: last_at >= fip)
+            if (!inwin && last_at - fip <= kLzWin - 5) { Sw = wload(fip); sb = fip; inwin = true; }
             const uint32_t vw = lane_word(Sw, (valid && inwin) ? ipl - sb : 0);
             const uint32_t v = !valid ? 0u : inwin ? vw : ld32u(src, (uint32_t)ipl);
             const uint32_t h = hash(v);
@@ -331,14 +341,14 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                     unsigned long long mm;
                     bool next = false;
                     do {
-                        if (next) { wb += 256; l0 = 0; Fw = wload(wb); Rw = wload(wb + dr); }
+                        if (next) { wb += kLzWin; l0 = 0; Fw = wload(wb); Rw = wload(wb + dr); }
                         x = Fw ^ Rw;
-                        if (wb + 256 > matchlimit) {       // (uniform) the window reaches matchlimit:
+                        if (wb + kLzWin > matchlimit) {    // (uniform) the window reaches matchlimit:
                             const int p = wb + 4 * l;      // a lane past it stops (x made non-zero
                             if (p + 4 > matchlimit)        // from the first byte at matchlimit on)
                                 x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
                         }
-                        if (l < l0) x = 0u;
+                        if (l < l0 || l >= kLzWinLanes) x = 0u;
                         mm = ballot64(x != 0u);
                         next = true;
                     } while (!mm);
@@ -377,7 +387,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                         // the match ended right at a window start)
                         const int o2 = ip - 2 - wb;
                         uint32_t v2, v0;
-                        if ((uint32_t)o2 <= 249u) {            // o2 >= 0, lane (o2 + 2) / 4 + 1 <= 63
+                        if ((uint32_t)o2 <= (uint32_t)(kLzWin - 7)) {   // o2 >= 0, lane (o2 + 2) / 4 + 1 < kLzWinLanes
                             // three lanes of the window into scalar registers, the two words by 64-bit
                             // scalar shifts (the hashes below stay scalar too: no VALU round trip)
                             const int a2 = o2 >> 2, a0 = (o2 + 2) >> 2;
