@@ -59,6 +59,22 @@ CHAINS_GX = {"W: chunking": CHAINS["W: chunking"], "A: SHA": ["sha(sha_chunk_ker
                  "gx_place_meta(place_kernel part 1)", "gx_x3(X3 all-to-all + host)", "gx_commit(own_commit)"],
              "B2: arena copy": ["place(place_kernel)"]}
 SHA_MIX_CEILING_WI_NS = 425.0  # tools/sha_peak.hip: the SHA-1 instruction mix on register-resident data
+HBM_ACHIEVABLE_GBS = 6300.0    # MI355X_MICROARCH.md HBM section: ~6.3 TB/s achievable
+# kernels launched per batch in the config-2 pipeline (the rest once); setup kernels are not counted
+_PIPE_SKIP = ("corpus_kernel", "__amd_rocclr", "idx_clear_kernel", "_config")
+_PIPE_LAUNCHES = {"lane_repair_kernel": 2}
+
+
+def pipeline_traffic(pmc):
+    """Counted HBM bytes of one batch: every pipeline kernel's per-launch figure x its launches per batch
+    (None without a PMC file for this workload, or for a workload with an LZ4 pass per batch)."""
+    if not pmc or any(k.startswith("lz4") for k in pmc):
+        return None
+    tot = 0
+    for k, v in pmc.items():
+        if isinstance(v, dict) and "hbm_bytes_per_launch" in v and not any(k.startswith(s) for s in _PIPE_SKIP):
+            tot += v["hbm_bytes_per_launch"] * _PIPE_LAUNCHES.get(k, 1)
+    return tot or None
 
 
 def load_pmc(want):
@@ -759,6 +775,18 @@ def main():
     roofline.update({"traffic_source": pmc_src, "critical_path": crit, "chains_ms_per_batch": chains,
                      "batch_period_ms": round(el / a.steps / nbatch * 1e3, 4),
                      "chunking": chunking, "sha": sha, "place": place})
+    pipe = pipeline_traffic(pmc)
+    if pipe and world == 1:
+        # the whole pipeline against the fabric: every kernel's counted HBM bytes per batch (PMC, the same
+        # workload) over the measured batch period, beside the guide's achievable rate
+        period_s = el / a.steps / nbatch
+        roofline["pipeline"] = {"counted_bytes_per_batch": int(pipe), "counted_bytes_per_logical_byte":
+                                round(pipe / S_batch, 3), "achieved": round(pipe / period_s / 1e9, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(pipe / period_s / 1e9 / HBM_PEAK_GBS, 4),
+                                "frac_of_achievable": round(pipe / period_s / 1e9 / HBM_ACHIEVABLE_GBS, 4),
+                                "achievable": HBM_ACHIEVABLE_GBS,
+                                "what": "sum over the batch's kernels of 2 x FETCH_SIZE + WRITE_SIZE per launch x launches "
+                                        "per batch, divided by the batch period of this run"}
     if lz4:
         roofline["lz4"] = lz4
         if lz4_phases:
