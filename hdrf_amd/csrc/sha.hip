@@ -150,18 +150,27 @@ __device__ __forceinline__ void load_win(const uint8_t *base, uint64_t readable,
 }
 
 // sha_carry: the 65 dwords (260 B) of four blocks at pos (4-aligned down); the second pair's half
-// is carried in registers to the lane's next iteration.
-__device__ __forceinline__ void load_win65(const uint8_t *base, uint64_t readable, uint32_t pos, uint32_t d[65])
+// is carried in registers to the lane's next iteration.  HDRF_SHA_CLAMP (build flag): the 16-B loads
+// past the chunk's last byte (end = its END offset) re-read the last one that holds chunk bytes, so a
+// chain's final window requests no line beyond the chunk (the padding never reads those bytes:
+// pad_block zeroes every word after the message end).
+#ifndef HDRF_SHA_CLAMP
+#define HDRF_SHA_CLAMP 0
+#endif
+__device__ __forceinline__ void load_win65(const uint8_t *base, uint64_t readable, uint32_t pos, uint32_t end,
+                                           uint32_t d[65])
 {
     const uint32_t apos = pos & ~3u;
     if ((uint64_t)apos + 260u <= readable) {
         const HDRF_GLOBAL uint32_t *p = gptr<uint32_t>(base + apos);
+        // the last 16-B load with a chunk byte in it (end > pos: the window starts inside the chunk)
+        const uint32_t qmax = HDRF_SHA_CLAMP ? (end - 1u - apos) >> 4 : 16u;
 #pragma unroll
         for (int q = 0; q < 16; q++) {
-            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * q);
+            u32x4a v = *(const HDRF_GLOBAL u32x4a *)(p + 4 * min((uint32_t)q, qmax));
             d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
         }
-        d[64] = p[64];
+        d[64] = p[HDRF_SHA_CLAMP ? min(64u, (end - 1u - apos) >> 2) : 64u];
     } else {
 #pragma unroll
         for (int q = 0; q < 65; q++) d[q] = load4_guard(base, (int64_t)apos + 4 * q, (int64_t)readable);
@@ -381,7 +390,7 @@ __device__ __forceinline__ void sha_chunk_body(const BlockDesc *__restrict__ blo
                     // four blocks even when the chain has fewer left: a third branch loading only
                     // 132 B for the last pair made the wave wait twice (SHA 2.55 -> 2.85 ms per
                     // batch, profiles/r03_sha_carry_trim_ab.txt)
-                    load_win65(base, readable, pos, dw);
+                    load_win65(base, readable, pos, s0 + len, dw);
                 }
                 sha_compute<HW>(dw, pos, len, T, nb, bi, two, st);
                 carry = !carry && two && bi + 2u < nb;
