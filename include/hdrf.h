@@ -344,9 +344,11 @@ int hdrf_get_stats(hdrf_ctx *ctx, hdrf_stats *out);
  * the batches in flight first.  HDRF_E_INVAL while a packet receive is open (hdrf_rx_begin not
  * yet followed by hdrf_submit_slot or hdrf_rx_cancel). */
 int hdrf_reset(hdrf_ctx *ctx);
-/* The same without completing the batches in flight (single-node contexts): they complete against
- * the old state, and the next submit starts the fresh DataNode, so its front half overlaps the old
- * batches' back halves.  Views and restores (hdrf_index_*, hdrf_*_load, reconstruct, container
+/* The same without completing the batches in flight: they complete against the old state, and the
+ * next submit (node-global contexts: the next hdrf_gx_front_launch, every rank alike) starts the fresh
+ * DataNode, so its front half overlaps the old batches' back halves.  Node-global contexts make the
+ * switch in that batch's hdrf_gx_owner (the old batches' owner phases, enqueued after this call, still
+ * use the old index epoch) and reset the host side in its hdrf_gx_place_wait.  Views and restores (hdrf_index_*, hdrf_*_load, reconstruct, container
  * reads, hdrf_synchronize) complete every batch first, as always, and a reset still pending then (no
  * submit since) is applied before they run, so they see the fresh DataNode and a restore is kept.
  * cfg.retain_containers: drain the old batches' containers as they complete (hdrf_wait_batch,
