@@ -546,23 +546,28 @@ __global__ void __launch_bounds__(256) place_kernel(StoreParams P, const BlockDe
         }
         }
     }
+    // the runs' LDS (below); the X3 reservation borrows s_cid / s_pend, so the kernel keeps its
+    // single-node LDS size: its own 768 B (7952 instead of 7184 B per workgroup) shifted the config-2
+    // balance between the place copy and the chunking chain (B2 3.6 -> 3.9 ms per batch) and cost
+    // 4.7 % (1103 vs 1054 GB/s, three A/B pairs, profiles/r06_placelds_ab.txt)
+    __shared__ uint32_t s_cid[256], s_flag[256];
+    __shared__ __attribute__((aligned(8))) uint32_t s_pend[256];
+    __shared__ uint32_t r_src[256], r_end[256], r_dst_lo[256], r_dst_hi[256];
+    __shared__ uint32_t s_wsum[4];
     if (gx.x3 && gx.part != 2) {                          // (uniform) the X3 location records, one
-        __shared__ uint32_t s_cnt[64];                     // global atomic per (workgroup, owner): one per
-        __shared__ unsigned long long s_base[64];          // record serialised at the memory side (gx.hip)
-        const int d = (int)(x3_ri / (uint64_t)gx.cap);
-        const unsigned long long i = wg_reserve(gx.counts, x3_want ? d : 0, x3_want, gx.G, s_cnt, s_base);
+        const int d = (int)(x3_ri / (uint64_t)gx.cap);     // global atomic per (workgroup, owner): one per
+        const unsigned long long i =                       // record serialised at the memory side (gx.hip)
+            wg_reserve(gx.counts, x3_want ? d : 0, x3_want, gx.G, s_cid, (unsigned long long *)s_pend);
         if (x3_want) {
             uint32_t *rec = gx.x3 + ((size_t)d * gx.cap + i) * 4;
             rec[0] = gx.x2[2 * (size_t)x3_ri];
             rec[1] = cid; rec[2] = pos; rec[3] = pos + ((f & 1) && do_copy ? len : 0u);
         }
+        __syncthreads();                                   // (s_cid / s_pend are rewritten below)
     }
     if (gx.part == 1) return;                              // placement part: no arena copy
     // ---- runs: consecutive new chunks of this tile that are contiguous in one container are
     //      one contiguous source span and one contiguous destination span -> one copy each
-    __shared__ uint32_t s_cid[256], s_pend[256], s_flag[256];
-    __shared__ uint32_t r_src[256], r_end[256], r_dst_lo[256], r_dst_hi[256];
-    __shared__ uint32_t s_wsum[4];
     const int tid = threadIdx.x;
     s_cid[tid] = do_copy ? cid : 0xffffffffu;
     s_pend[tid] = pos + len;
