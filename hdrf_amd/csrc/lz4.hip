@@ -152,7 +152,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
         // the last word instead; no such lane's bytes are ever used (every use is bounded by
         // mflimit / matchlimit, at least 5 bytes before n), so one clamp replaces the guards.
         const int nm4 = n - 4;
-        const int lw = l & (kLzWinLanes - 1);                // this lane's word of a window
+        const int lw = kLzWinLanes == 64 ? l : (l & (kLzWinLanes - 1));   // this lane's word of a window
         auto wload = [&](int at) -> uint32_t { return ld32u(src, (uint32_t)min(at + 4 * lw, nm4)); };
         auto lane_word = [&](uint32_t w, int o) -> uint32_t {   // bytes [o, o + 4) of a window
             const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((o >> 2) << 2, (int)w);
@@ -348,7 +348,7 @@ __device__ __forceinline__ int lz4_block(const uint8_t *src, int n, uint8_t *out
                             if (p + 4 > matchlimit)        // from the first byte at matchlimit on)
                                 x = p < matchlimit ? x | (0xffffffffu << (8 * (matchlimit - p))) : 0xffffffffu;
                         }
-                        if (l < l0 || l >= kLzWinLanes) x = 0u;
+                        if (l < l0 || (kLzWinLanes < 64 && l >= kLzWinLanes)) x = 0u;   // (256: the round-5 code)
                         mm = ballot64(x != 0u);
                         next = true;
                     } while (!mm);
