@@ -677,14 +677,23 @@ hipError_t launch_store(const StoreParams &P, const BlockDesc *d_blocks, const B
 }
 
 // storeDB's recipe SET (DN/DataDeduplicator.java:372-392): copy each block's digests (already
-// contiguous in the batch slot) into the device recipe store; grid (n, 8) x 256
+// contiguous in the batch slot) into the device recipe store; grid (n, kRecipeWgs) x 256, 16 B per
+// lane per step (4-B aligned dwordx4: the digest rows and the store's records are 4-B aligned).  The
+// copy runs on stream C beside the pipeline: with one dword per lane and 8 workgroups per block it held
+// 256 workgroups for ~540 us per batch (profiles/r06_c2_kernel_stats.csv).
+typedef uint32_t u32x4r __attribute__((ext_vector_type(4), aligned(4)));
+constexpr int kRecipeWgs = 32;
 __global__ void __launch_bounds__(256) recipe_copy_kernel(const RecipeCopy *__restrict__ jobs, int n)
 {
     if ((int)blockIdx.x >= n) return;
     const RecipeCopy j = jobs[blockIdx.x];
     const uint32_t *src = (const uint32_t *)(uintptr_t)j.src;
     uint32_t *dst = (uint32_t *)(uintptr_t)j.dst;
-    for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < j.words; i += gridDim.y * 256) dst[i] = src[i];
+    const uint32_t nq = j.words >> 2, stride = gridDim.y * 256;
+    for (uint32_t i = blockIdx.y * 256 + threadIdx.x; i < nq; i += stride)
+        *(u32x4r *)(dst + 4 * i) = *(const u32x4r *)(src + 4 * i);
+    const uint32_t t = 4 * nq + blockIdx.y * 256 + threadIdx.x;     // the last words (< 4)
+    if (t < j.words && blockIdx.y * 256 + threadIdx.x < 4) dst[t] = src[t];
 }
 
 // Container drain (api.hip hdrf_drain_containers) into pinned host memory: the CUs write the bytes
@@ -720,7 +729,7 @@ hipError_t launch_xfer(const XferJob *jobs, int n, uint64_t max_bytes, int wgs, 
 
 hipError_t launch_recipe_copy(const RecipeCopy *jobs, int n, hipStream_t st)
 {
-    if (n > 0) hipLaunchKernelGGL(recipe_copy_kernel, dim3(n, 8), dim3(256), 0, st, jobs, n);
+    if (n > 0) hipLaunchKernelGGL(recipe_copy_kernel, dim3(n, kRecipeWgs), dim3(256), 0, st, jobs, n);
     return hipGetLastError();
 }
 
