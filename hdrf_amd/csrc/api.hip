@@ -49,6 +49,11 @@ struct Slot {
     BlockDesc *d_blocks = nullptr;
     uint32_t *d_spec = nullptr;
     SegMeta *d_meta = nullptr;
+    // the fused front (HDRF_FUSED=1, lanehash.hip): per-cut and per-boundary digests, fix-up marks
+    uint32_t *d_sdig = nullptr, *d_bdig = nullptr, *d_nlist = nullptr;
+    int *d_gmneed = nullptr;
+    uint8_t *d_need = nullptr;
+    size_t sdig_words = 0, bdig_segs = 0;
     uint8_t *d_gm = nullptr;                  // granule maxima [B][gstride] (chunking pass 1)
     int gstride = 0;
     int64_t max_len = 0;                      // longest block of the batch in this slot
@@ -161,6 +166,8 @@ struct hdrf_ctx {
     // chunks >= 64 KiB were seen in the last completed batch: sha_full hashes them on dedicated
     // lanes (sha.hip); off otherwise, where the scan for them costs config 2 ~3 %
     bool sha_long = false;
+    bool fused = false;                              // the fused chunk + fingerprint front (fused_front)
+    int n_cu = 256;                                  // compute units of the device (the fused pass's segment sizing)
     int max_batch = 0, cap_blk = 0, ntiles = 0, ev_cap = 0, closed_cap = 0, coll_cap = 0;
     Slot sl[kSlots];
     uint64_t nsub = 0, nwait = 0;  // batches submitted / completed
@@ -379,7 +386,7 @@ static void free_slot(Slot &S)
     void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_slot,
                    S.d_pre, S.d_flags, S.d_dcnt, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
                    S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err,
-                   S.d_lzwork};
+                   S.d_lzwork, S.d_sdig, S.d_bdig, S.d_need, S.d_nlist, S.d_gmneed};
     for (void *p : dev)
         if (p) (void)hipFree(p);
     void *host[] = {S.h_bst, S.h_store, S.h_alloc, S.h_err, S.h_nclosed, S.h_long, S.h_closed, S.h_filelen, S.h_desc,
@@ -507,6 +514,7 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
 }
 
 static int wait_one(hdrf_ctx *ctx, bool force = false);
+static bool fused_front();
 static int init_state(hdrf_ctx *ctx, bool fresh);
 static bool gen_undrained(const hdrf_ctx *ctx);
 
@@ -720,6 +728,12 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
             rc = set_err(ctx, HDRF_E_HIP, "hipMemset failed");
     }
     ctx->timing = c.timing != 0;
+    ctx->fused = fused_front();
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device) == hipSuccess && ncu > 0)
+            ctx->n_cu = ncu;
+    }
     if (!rc) rc = init_state(ctx, true);
     if (rc) {
         fprintf(stderr, "hdrf_open: %s\n", ctx->err.c_str());
@@ -818,6 +832,15 @@ static ChunkScratch chunk_scratch(Slot &S, int compressor = 1)
     return X;
 }
 
+// HDRF_FUSED=1: the front cuts and hashes in one pass over the bytes (lanehash.hip) instead of the
+// granule pass + lane walk (chunk.hip) followed by the SHA lanes (sha.hip); single-node contexts.
+// Read when a context opens, so a process may hold contexts of both kinds (the tests do).
+static bool fused_front()
+{
+    const char *e = getenv("HDRF_FUSED");
+    return e && atoi(e) != 0;
+}
+
 // Validate a batch and fill the slot's (pinned) descriptors: the lane segmentation of the chunking
 // pass (chunk.hip).  seg_len = segment_bytes / 63 rounded down to a multiple of window + 2, within
 // [4, 20] x 702 B.  Grows the slot's speculative lists when needed (the slot's previous batch has
@@ -841,7 +864,23 @@ static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t
     // one lane per segment: a block of any size has thousands of lanes, so the segment length
     // follows segment_bytes alone (shorter segments only raise the share of boundaries whose
     // chains have not met within the next segment, which then take the repair pass)
-    const int wins = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / unit)));
+    int wins = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / unit)));
+    if (ctx->fused) {
+        // the fused pass (lanehash.hip): every lane does the same work (its segment, 64 B per step),
+        // so a second, partial round of waves costs as much as a full one — the shortest segments
+        // whose waves fit one round (16 per CU at its 99 VGPRs; 4 GiB batch: 24 windows, 4064 waves)
+        const int64_t cap_waves = (int64_t)ctx->n_cu * 16;
+        auto waves_for = [&](int wn) {
+            int64_t wv = 0;
+            for (int b = 0; b < nblocks; b++) {
+                const int64_t ns = std::max<int64_t>(1, ((int64_t)len[b] + (int64_t)wn * unit - 1) / ((int64_t)wn * unit));
+                wv += (ns + kWaveSegs - 1) / kWaveSegs;
+            }
+            return wv;
+        };
+        wins = kSegMinWin;
+        while (wins < kSegMaxWinF && waves_for(wins) > cap_waves) wins++;
+    }
     (void)total;
     const int seg_len = wins * unit;
     int seg0 = 0, wave0 = 0;
@@ -891,6 +930,28 @@ static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t
         S.spec_words = 0;
         if (int rc = dalloc(ctx, &S.d_spec, words)) return rc;
         S.spec_words = words;
+    }
+    if (ctx->fused) {
+        if (!S.d_need)
+            if (int rc = dalloc(ctx, &S.d_need, (size_t)ctx->max_batch * ctx->cap_blk)) return rc;
+        if (!S.d_nlist)
+            if (int rc = dalloc(ctx, &S.d_nlist, (size_t)ctx->max_batch * ctx->cap_blk)) return rc;
+        if (!S.d_gmneed)
+            if (int rc = dalloc(ctx, &S.d_gmneed, (size_t)ctx->max_batch)) return rc;
+        if (words * ctx->HW > S.sdig_words) {
+            (void)hipFree(S.d_sdig);
+            S.d_sdig = nullptr;
+            S.sdig_words = 0;
+            if (int rc = dalloc(ctx, &S.d_sdig, words * ctx->HW)) return rc;
+            S.sdig_words = words * ctx->HW;
+        }
+        if ((size_t)seg0 + 1 > S.bdig_segs) {
+            (void)hipFree(S.d_bdig);
+            S.d_bdig = nullptr;
+            S.bdig_segs = 0;
+            if (int rc = dalloc(ctx, &S.d_bdig, ((size_t)seg0 + 1) * ctx->HW)) return rc;
+            S.bdig_segs = (size_t)seg0 + 1;
+        }
     }
     return 0;
 }
@@ -974,18 +1035,27 @@ static int submit(hdrf_ctx *ctx, int32_t nblocks, const uint8_t *const *dev_data
     HIPCK(hipMemcpyAsync(S.d_blocks, S.h_desc, sizeof(BlockDesc) * nblocks, hipMemcpyHostToDevice, G));
     Marker mw;
     mw.ev = ctx->timing ? S.evW : nullptr;
+    // (the fused front writes d_dig on W: after the recipe copies of the slot's previous batch read it)
+    const bool fz_on = ctx->fused;
+    if (fz_on && S.recipe_pending) HIPCK(hipStreamWaitEvent(W, S.recipe_done, 0));
+    const FusedFront fz{c.hasher, S.d_sdig, S.d_bdig, S.d_dig, S.d_need, S.d_gmneed};
     HIPCK(launch_chunking(S.d_blocks, nblocks, S.max_len, S.max_nseg, S.total_waves, S.total_segs,
                           chunk_scratch(S, c.compressor), c.window, c.max_chunk, S.d_spec, S.spec_cap, S.d_meta, S.d_bst,
-                          S.d_off, ctx->cap_blk, S.d_err, W, &mw, G, S.gmax_done));
+                          S.d_off, ctx->cap_blk, S.d_err, W, &mw, G, S.gmax_done, fz_on ? &fz : nullptr));
     mw.mark(W);
     HIPCK(hipEventRecord(S.walk_done, W));
-    // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig)
+    // ---- fingerprints on A (after the recipe copies of the slot's previous batch read d_dig); the fused
+    // front leaves only the chunks marked in d_need (each block's last one, repairs, fallbacks)
     HIPCK(hipStreamWaitEvent(A, S.walk_done, 0));
     if (S.recipe_pending) HIPCK(hipStreamWaitEvent(A, S.recipe_done, 0));
     Marker ma;
     ma.ev = ctx->timing ? S.evA : nullptr;
-    HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig, S.d_queue, ctx->sha_long, A,
-                     &ma));
+    if (fz_on)
+        HIPCK(launch_sha_need(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig, S.d_queue, S.d_need,
+                              S.d_nlist, A, &ma));
+    else
+        HIPCK(launch_sha(c.hasher, S.d_blocks, nblocks, S.d_off, S.d_bst, ctx->cap_blk, S.d_dig, S.d_queue, ctx->sha_long, A,
+                         &ma));
     ma.mark(A);
     HIPCK(hipEventRecord(S.front_done, A));
     // ---- back, index part, in block order on stream B: claim .. decide, then idx_finalize takes the

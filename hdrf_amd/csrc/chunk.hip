@@ -520,10 +520,13 @@ __device__ __forceinline__ uint32_t gmax16_s(uint4 v)
 
 // 1a'. the same pass, 15 VALU per granule, and the 16 granule bytes of a thread (256 apart) staged
 // through LDS so each thread writes one 16-B word of consecutive maxima (1 store instead of 16).
-template <bool NT>
+// COND (the fused front): only the blocks whose cond[b] is set (a boundary of theirs went to the
+// repair walk, whose long searches and the sequential fallback read the maxima)
+template <bool NT, bool COND = false>
 __global__ void __launch_bounds__(256) gmax2_kernel(const BlockDesc *__restrict__ blocks, uint8_t *__restrict__ gm,
-                                                    int gstride, int prio)
+                                                    int gstride, int prio, const int *__restrict__ cond = nullptr)
 {
+    if (COND && cond[blockIdx.y] == 0) return;
     if (prio) __builtin_amdgcn_s_setprio(2);
     __shared__ __attribute__((aligned(16))) uint8_t s_g[kGmPerWg];
     const BlockDesc bd = blocks[blockIdx.y];
@@ -1164,6 +1167,7 @@ __global__ void __launch_bounds__(256) stitch_count_kernel(const BlockDesc *__re
     const int nj = nr;                                     // local indices: jump j0 + i at i
     SegMeta *mt = meta + bd.seg0;
     int from = 0, cnt = 0, ext = -1;
+    bool entered_by_jump = false;
     if (k < nseg && k <= term) {
         const int i0 = j0 < 0 ? 1 : 0;                     // local entry 0 is jump j0 (none when j0 < 0)
         int lo = i0, hi = nj;                              // last jump with source < k
@@ -1175,6 +1179,7 @@ __global__ void __launch_bounds__(256) stitch_count_kernel(const BlockDesc *__re
             over = tgt > k;                                // jumped over
             target = tgt == k;
         }
+        entered_by_jump = target;
         if (!over) {
             const SegMeta m = mt[k];
             if (k == 0) from = 0;
@@ -1192,6 +1197,7 @@ __global__ void __launch_bounds__(256) stitch_count_kernel(const BlockDesc *__re
         mt[k].cp_n = ext >= 0 ? ext : cnt;                 // list cuts; the repair's cuts follow (emit)
         mt[k].pad[0] = cnt;
         mt[k].pad[1] = ext;
+        mt[k].pad[2] = k == 0 ? 0 : (entered_by_jump ? 2 : 1);   // how the path entered (fused digests)
     }
     uint32_t total;
     (void)wg_excl_scan((uint32_t)cnt, s_w, total);
@@ -1227,12 +1233,43 @@ __global__ void __launch_bounds__(256) stitch_scan_kernel(const BlockDesc *__res
     }
 }
 
+// With the fused pass (lanehash.hip, sdig != nullptr) the digests of the copied list cuts move to the
+// batch's digest rows too and their need[] flags are cleared: list cut from + i of segment k ends a
+// chunk of lane k's chain that starts on the path for i > 0, and for i == 0 at the block start (k == 0);
+// the first cut after a sync is the chunk lane k - 1 cut up to the shared cut (bdig[k]), on the path
+// when segment k - 1 contributed a cut of its own (or is segment 0).  A jump target's first cut, the
+// repair's cuts and the fallback's are hashed by the fix-up pass (sha.hip).
+// the wave's 64 segments one after another, every lane copying words of one segment's digest rows
+template <int HW>
+__device__ __forceinline__ void copy_digests_wave(int n_l, int G, int from, int dst, bool head, int k, int cap,
+                                                  const uint32_t *__restrict__ sdig, const uint32_t *__restrict__ bdig,
+                                                  uint32_t *__restrict__ dig, uint8_t *__restrict__ need)
+{
+    const int l = lane_id();
+    for (int j = 0; j < 64; j++) {
+        const int nj = __shfl(n_l, j, 64);
+        if (nj == 0) continue;
+        const int Gj = __shfl(G, j, 64), fj = __shfl(from, j, 64), dj = __shfl(dst, j, 64), kj = __shfl(k, j, 64);
+        const bool hj = __shfl((int)head, j, 64) != 0;
+        for (int t = l; t < nj * HW; t += 64) {
+            const int i = t / HW, wd = t - i * HW;
+            const uint32_t *ds = (i > 0 || kj == 0) ? sdig + ((size_t)Gj * cap + fj + i) * HW : (hj ? bdig + (size_t)Gj * HW : nullptr);
+            if (ds) dig[(size_t)(dj + i) * HW + wd] = ds[wd];
+        }
+        for (int i = l; i < nj; i += 64)
+            if (i > 0 || kj == 0 || hj) need[dj + i] = 0;
+    }
+}
 __global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__restrict__ blocks,
                                                           SegMeta *__restrict__ meta,
                                                           const uint32_t *__restrict__ spec, int cap,
                                                           const uint32_t *__restrict__ wgsum, int maxw,
                                                           const BlockState *__restrict__ bst,
-                                                          uint32_t *__restrict__ offsets, int cap_blk)
+                                                          uint32_t *__restrict__ offsets, int cap_blk,
+                                                          const uint32_t *__restrict__ sdig = nullptr,
+                                                          const uint32_t *__restrict__ bdig = nullptr,
+                                                          uint32_t *__restrict__ dig = nullptr,
+                                                          uint8_t *__restrict__ need = nullptr, int HW = 0)
 {
     __shared__ uint32_t s_w[4];
     const int b = blockIdx.y, t = threadIdx.x;
@@ -1253,6 +1290,15 @@ __global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__res
         uint32_t *out = offsets + (size_t)b * cap_blk + dst;
         for (int i = 0; i < n; i++) out[i] = src[i];
     }
+    if (sdig) {                                           // (uniform) the fused pass's digests
+        const bool mine = k < nseg && cnt > 0;
+        const int n_l = mine ? meta[G].cp_n : 0, from_l = mine ? meta[G].cp_from : 0;
+        const bool head = mine && (k == 0 || (meta[G].pad[2] == 1 && (k == 1 || meta[G - 1].pad[0] > 0)));
+        uint32_t *drow = dig + (size_t)b * cap_blk * HW;
+        uint8_t *nrow = need + (size_t)b * cap_blk;
+        if (HW == 5) copy_digests_wave<5>(n_l, G, from_l, (int)dst, head, k, cap, sdig, bdig, drow, nrow);
+        else copy_digests_wave<7>(n_l, G, from_l, (int)dst, head, k, cap, sdig, bdig, drow, nrow);
+    }
 }
 
 // 4. fallback + drop-last/append-size: one wave per block.  A block whose path ends at a failed
@@ -1262,7 +1308,8 @@ __global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__res
 __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__restrict__ blocks, int w, int maxlen,
                                                            uint32_t *__restrict__ offsets, int cap_blk,
                                                            BlockState *__restrict__ bst, const uint8_t *__restrict__ gm,
-                                                           int gstride, int *__restrict__ err, int prio)
+                                                           int gstride, int *__restrict__ err, int prio,
+                                                           uint8_t *__restrict__ need = nullptr)
 {    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
 
     const int b = blockIdx.x;
@@ -1294,6 +1341,7 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
         off[n - 1] = (uint32_t)bd.len;
         s.n_chunks = n;
         bst[b] = s;
+        if (need) need[(size_t)b * cap_blk + n - 1] = 1;  // [off[n - 2], len): not a chunk any lane cut
     }
 }
 
@@ -1309,14 +1357,61 @@ int setprio_mask()
     return m;
 }
 
+// The fused front (HDRF_FUSED=1): lanehash.hip's pass cuts and hashes the lane segments; the granule
+// maxima are computed only when a boundary was queued for the repair walk (whose long searches and the
+// sequential fallback read them); then the stitch as in the two-pass front, carrying the digests.
+// Stage markers: the granule slot stays empty, the walk slot times the fused pass, the stitch slot the
+// conditional granule pass, repair, stitch and fallback.
+static hipError_t launch_fused_front(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int total_waves, int nsegs,
+                                     const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
+                                     SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err,
+                                     hipStream_t st, Marker *mk, const FusedFront &fz, int maxw)
+{
+    mk->mark(st);
+    hipError_t e = hipMemsetAsync(X.rq_count, 0, sizeof(int), st);
+    if (e == hipSuccess) e = hipMemsetAsync(X.irr, 0, sizeof(uint32_t) * (size_t)(nsegs / 32 + 2), st);
+    if (e == hipSuccess) e = hipMemsetAsync(fz.need, 1, (size_t)nblocks * cap_blk, st);
+    if (e == hipSuccess) e = hipMemsetAsync(fz.gm_need, 0, sizeof(int) * (size_t)nblocks, st);
+    if (e != hipSuccess) return e;
+    const int prio = setprio_mask();
+    mk->mark(st);
+    if ((e = launch_lane_hash(fz.hasher, d_blocks, nblocks, total_waves, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count,
+                              X.rq_cap, X.irr, fz.sdig, fz.bdig, fz.gm_need, err, st)) != hipSuccess)
+        return e;
+    mk->mark(st);
+    const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
+    hipLaunchKernelGGL((gmax2_kernel<true, true>), dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm,
+                       X.gstride, (prio >> 4) & 1, (const int *)fz.gm_need);
+    const int rgrid = 512;
+    const int HW = fz.hasher == 0 ? 5 : 7;
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0, (prio >> 1) & 1);
+    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
+                       (prio >> 1) & 1);
+    hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt, X.jcap,
+                       X.wgsum, maxw, err);
+    hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
+                       cap_blk, err);
+    hipLaunchKernelGGL(stitch_copy_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, spec, spec_cap,
+                       X.wgsum, maxw, bst, offsets, cap_blk, (const uint32_t *)fz.sdig, (const uint32_t *)fz.bdig,
+                       fz.dig, fz.need, HW);
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1, (prio >> 1) & 1);
+    hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
+                       cap_blk, bst, X.gm, X.gstride, err, (prio >> 1) & 1, fz.need);
+    return hipGetLastError();
+}
+
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
-                           Marker *mk, hipStream_t stg, hipEvent_t gdone)
+                           Marker *mk, hipStream_t stg, hipEvent_t gdone, const FusedFront *fz)
 {
     if ((max_len + 15) / 16 + 4 * kGmWin > X.gstride) return hipErrorInvalidValue;
     const int maxw = (max_nseg + 255) / 256;
     if (maxw > X.maxw) return hipErrorInvalidValue;
+    if (fz) return launch_fused_front(d_blocks, nblocks, max_len, total_waves, nsegs, X, w, maxlen, spec, spec_cap, meta,
+                                      bst, offsets, cap_blk, err, st, mk, *fz, maxw);
     const bool split = stg && stg != st && gdone;     // granule pass on its own stream, the walk waits for it
     hipStream_t sg = split ? stg : st;
     mk->mark(sg);

@@ -26,6 +26,10 @@ constexpr int kRepairCuts = 4096;    // a repair walk gives up after this many c
 constexpr int kRepairBytes = 2 << 20;  // ... or this many bytes past its start
 constexpr int kSegMinWin = 4;        // seg_len bounds, in units of window + 2 (702 B)
 constexpr int kSegMaxWin = 20;        // seg_len / 702 + 2 + kLaneOver <= kLdsCuts
+// the fused chunk + fingerprint pass (lanehash.hip) sizes its segments for one round of its waves,
+// which needs longer segments on a 4 GiB batch (24 windows): its own list bound
+constexpr int kSegMaxWinF = 28;
+constexpr int kLdsCutsF = 40;        // kSegMaxWinF + 2 + kLaneOver <= kLdsCutsF
 
 // Index entry: 64 B.  tag = the table generation ("epoch", 1..255) in bits 56..63 over the first 7
 // digest bytes; an entry whose tag carries another epoch is EMPTY, so a fresh index (hdrf_reset)

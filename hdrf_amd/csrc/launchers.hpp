@@ -50,10 +50,27 @@ struct ChunkScratch {
     int ring = 1;            // lane walk: granule maxima through the LDS ring (off beside LZ4 passes)
 };
 int setprio_mask();   // HDRF_SETPRIO (chunk.hip)
+// The fused chunk + fingerprint pass (lanehash.hip, HDRF_FUSED=1): its digest outputs.
+struct FusedFront {
+    int hasher;
+    uint32_t *sdig;          // [segments][spec_cap][HW]: the digest of every cut of a lane's chain
+    uint32_t *bdig;          // [segments][HW]: the chunk ending at the cut where lane k met segment k + 1
+    uint32_t *dig;           // the batch's digest rows [nblocks][cap_blk][HW]
+    uint8_t *need;           // [nblocks][cap_blk]: 1 = left to the fix-up hash (launch_sha_need)
+    int *gm_need;            // [nblocks]: a boundary of the block went to the repair walk (granule maxima)
+};
 hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_len, int max_nseg, int total_waves,
                            int nsegs, const ChunkScratch &X, int w, int maxlen, uint32_t *spec, int spec_cap,
                            SegMeta *meta, BlockState *bst, uint32_t *offsets, int cap_blk, int *err, hipStream_t st,
-                           Marker *mk, hipStream_t stg = nullptr, hipEvent_t gdone = nullptr);   // stg: gmax pass stream
+                           Marker *mk, hipStream_t stg = nullptr, hipEvent_t gdone = nullptr,   // stg: gmax pass stream
+                           const FusedFront *fz = nullptr);
+hipError_t launch_lane_hash(int hasher, const BlockDesc *d_blocks, int nblocks, int total_waves, int w, int maxlen,
+                            uint32_t *spec, int cap, SegMeta *meta, int *rq, int *rq_count, int rq_cap, uint32_t *irr,
+                            uint32_t *sdig, uint32_t *bdig, int *gm_need, int *err, hipStream_t st);
+// the fused pass's fix-up: the chunks whose need[] byte is set, compacted into list (nblocks x cap_blk)
+hipError_t launch_sha_need(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
+                           const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, const uint8_t *need,
+                           uint32_t *list, hipStream_t st, Marker *mk);
 hipError_t launch_sha(int hasher, const BlockDesc *d_blocks, int nblocks, const uint32_t *offsets,
                       const BlockState *bst, int cap_blk, uint32_t *digests, uint32_t *queue, bool long_lanes,
                       hipStream_t st, Marker *mk);   // queue: 65 words; [64] = long chunks seen
