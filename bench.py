@@ -36,6 +36,11 @@ KERNEL_OF = {"gmax(gmax_kernel)": "gmax_kernel" if os.environ.get("HDRF_GMAX_V",
              "walk(lane_walk_kernel)": "lane_walk_kernel",
              "sha(sha_chunk_kernel)": "sha_carry_kernel" if os.environ.get("HDRF_SHA_CARRY", "1") not in ("", "0")
              else "sha_chunk_kernel", "place(place_kernel)": "place_kernel"}
+# the fused chunk + fingerprint front (HDRF_FUSED, hdrf_amd/csrc/lanehash.hip; mirrors api.hip fused_front()):
+# the walk slot times lane_hash_kernel, the granule slot is empty, the SHA slot is the listed fix-up
+FUSED = os.environ.get("HDRF_FUSED", "0") not in ("", "0")
+if FUSED:
+    KERNEL_OF["walk(lane_walk_kernel)"] = "lane_hash_kernel"
 # stages per stream (hdrf_amd/csrc/api.hip submit): W chunking, A fingerprints, B index (claim ..
 # finalize), B2 store (scans, flush, place; on stream B itself with HDRF_SPLIT_B=0), L the LZ4 pass
 # of closed containers (compressor 2; two LZ4 streams alternating by batch)
@@ -87,6 +92,7 @@ def load_pmc(want):
         d = json.load(open(f))
         cfg = dict(d.get("_config", {}))
         cfg.setdefault("workload", "config2")
+        cfg.setdefault("front", "two-pass")
         if all(cfg.get(k) == v for k, v in want.items()):
             return d, os.path.relpath(f, ROOT)
     return {}, None
@@ -694,7 +700,9 @@ def main():
     S_batch = nb * S / nbatch
     per_launch = {   # algorithmic HBM bytes per launch
         "gmax(gmax_kernel)": S_batch * (1 + 1 / 16),                      # read block bytes, write granule maxima
-        "walk(lane_walk_kernel)": S_batch / 16 + 4 * chunks_step / nbatch,  # read maxima, write cuts
+        "walk(lane_walk_kernel)": (S_batch + (4 + 4 * (5 if a.hasher == 0 else 7)) * chunks_step / nbatch if FUSED
+                                   else S_batch / 16 + 4 * chunks_step / nbatch),  # fused: bytes in, cuts + digests out;
+                                                                                   # walk: read maxima, write cuts
         STAGES[2]: S_batch + 40 * chunks_step / nbatch,                   # read chunk bytes + offsets, write mid-state
         STAGES[9]: (2 * new_bytes + 16 * chunks_step) / nbatch,           # read+write new bytes, chunk metadata
     }
@@ -706,7 +714,7 @@ def main():
             d["GB_s"] = round(per_launch[name] / (avg[name] * 1e-3) / 1e9, 1)
         stages[name] = d
     pmc, pmc_src = load_pmc({"blocks": nb, "block_mib": a.block_mib, "batch": B, "n_gpus": world,
-                             "hasher": a.hasher, "workload": a.workload})
+                             "hasher": a.hasher, "workload": a.workload, "front": "fused" if FUSED else "two-pass"})
     sha_k = KERNEL_OF[STAGES[2]] + ("<5>" if a.hasher == 0 else "<7>")
 
     def hbm_entry(name):
@@ -723,7 +731,8 @@ def main():
     chains = {c: round(sum(avg[s] for s in st), 4) for c, st in chain_def.items()}
     crit = max(chains, key=chains.get)
     chunk_ms = chains["W: chunking"]
-    chunking = {"kernels": "gmax + lane walk + stitch (one batch, in pipeline)", "avg_batch_ms": chunk_ms,
+    chunking = {"kernels": ("lane_hash (cuts and SHA in one pass over the bytes) + stitch (one batch, in pipeline)"
+                            if FUSED else "gmax + lane walk + stitch (one batch, in pipeline)"), "avg_batch_ms": chunk_ms,
                 "achieved": round(S_batch / (chunk_ms * 1e-3) / 1e9, 1) if chunk_ms > 0 else None,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s (block bytes chunked)",
                 "frac": round(S_batch / (chunk_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if chunk_ms > 0 else None,
@@ -759,7 +768,17 @@ def main():
                           "SALU 0.125 per SIMD-cycle, half of wave time at s_waitcnt on the table round trip and the "
                           "candidate load); profiles/r05_lz4_pmc.txt, profiles/r05_lz4_phases_c4.txt"}
     # the line's roofline: the dominant kernel of the critical chain
-    top = {"W: chunking": chunking["gmax"], "A: SHA": sha, "B: index+store": place, "B2: store": place,
+    if FUSED:
+        # the fused pass is the front: block bytes read once; int-VALU the other bound (SHA-1's mix)
+        fz = chunking["walk"]
+        fz_prof = next((pmc[k] for k in ("lane_hash_kernel<5>", "lane_hash_kernel<7>") if k in pmc), {})
+        if fz_prof.get("sq_insts_valu") and avg["walk(lane_walk_kernel)"] > 0:
+            wi_ns = fz_prof["sq_insts_valu"] / (avg["walk(lane_walk_kernel)"] * 1e6)
+            fz["valu"] = {"wave_instr_per_ns": round(wi_ns, 1), "peak": VALU_PEAK_WI_NS,
+                          "frac": round(wi_ns / VALU_PEAK_WI_NS, 4), "mix_ceiling": SHA_MIX_CEILING_WI_NS,
+                          "frac_of_mix_ceiling": round(wi_ns / SHA_MIX_CEILING_WI_NS, 4),
+                          "sq_insts_valu_per_launch": int(fz_prof["sq_insts_valu"])}
+    top = {"W: chunking": chunking["walk"] if FUSED else chunking["gmax"], "A: SHA": sha, "B: index+store": place, "B2: store": place,
            "B: index": place, "L: LZ4": lz4, "B2: arena copy": place}.get(crit)
     if top is None:
         # a node-global chain without an HBM-bound kernel of its own (local aggregation; the back

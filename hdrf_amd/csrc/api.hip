@@ -865,6 +865,9 @@ static int prepare_blocks(hdrf_ctx *ctx, Slot &S, int32_t nblocks, const uint8_t
     // follows segment_bytes alone (shorter segments only raise the share of boundaries whose
     // chains have not met within the next segment, which then take the repair pass)
     int wins = std::max(kSegMinWin, std::min(kSegMaxWin, (int)(c.segment_bytes / kWaveSegs / unit)));
+    // HDRF_SEG_WINS (A/B): the two-pass front's segment length in windows, over segment_bytes
+    static const int wins_env = [] { const char *e = getenv("HDRF_SEG_WINS"); return e ? atoi(e) : 0; }();
+    if (wins_env > 0 && !ctx->fused) wins = std::max(kSegMinWin, std::min(kSegMaxWin, wins_env));
     if (ctx->fused) {
         // the fused pass (lanehash.hip): every lane does the same work (its segment, 64 B per step),
         // so a second, partial round of waves costs as much as a full one — the shortest segments

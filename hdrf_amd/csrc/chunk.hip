@@ -373,8 +373,9 @@ __device__ __forceinline__ bool process_view(const WalkCfg &c, Chain &ch, const 
             else { ch.ended = true; return false; }
         } else {
             ch.q = max(ch.q, T + 2048);                                // continue after the advance
-            if (ch.lim > T + 4096) {
-                // long search: the granule maxima say where the next candidate byte can be
+            if (c.gm && ch.lim > T + 4096) {
+                // long search: the granule maxima say where the next candidate byte can be (without
+                // them — the fused front computes none — the search goes on tile by tile)
                 const int q2 = gm_skip(c.gm, ch.q, ch.lim, ch.state == kSearchFF ? 0xffu : ch.m);
                 if (q2 >= T + 4096) { ch.q = min(q2, ch.lim); ch.jump = true; }
             }
@@ -970,7 +971,7 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
         const bool first = n == 0 && s_k == 0;
         WalkCfg W;
         W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
-        W.w = w; W.maxlen = maxlen; W.gm = gm + (size_t)bi * gstride;
+        W.w = w; W.maxlen = maxlen; W.gm = gm ? gm + (size_t)bi * gstride : nullptr;
         if (!emit) {
             CountSink sink;
             sink.cap = kRepairCuts; sink.cnt = 0; sink.stage = 0;
@@ -1239,25 +1240,44 @@ __global__ void __launch_bounds__(256) stitch_scan_kernel(const BlockDesc *__res
 // the first cut after a sync is the chunk lane k - 1 cut up to the shared cut (bdig[k]), on the path
 // when segment k - 1 contributed a cut of its own (or is segment 0).  A jump target's first cut, the
 // repair's cuts and the fallback's are hashed by the fix-up pass (sha.hip).
-// the wave's 64 segments one after another, every lane copying words of one segment's digest rows
+// the wave's 64 segments four at a time, a 16-lane group per segment, one digest row per lane: the
+// loads of up to 48 rows per segment are issued before any store (one memory round trip per four
+// segments; one segment per step with a word per lane left the stitch 0.55 ms slower per batch)
 template <int HW>
 __device__ __forceinline__ void copy_digests_wave(int n_l, int G, int from, int dst, bool head, int k, int cap,
                                                   const uint32_t *__restrict__ sdig, const uint32_t *__restrict__ bdig,
                                                   uint32_t *__restrict__ dig, uint8_t *__restrict__ need)
 {
-    const int l = lane_id();
-    for (int j = 0; j < 64; j++) {
+    const int l = lane_id(), r = l & 15;
+    for (int j0 = 0; j0 < 64; j0 += 4) {
+        const int j = j0 + (l >> 4);
         const int nj = __shfl(n_l, j, 64);
-        if (nj == 0) continue;
+        if (!ballot64(nj > 0)) continue;
         const int Gj = __shfl(G, j, 64), fj = __shfl(from, j, 64), dj = __shfl(dst, j, 64), kj = __shfl(k, j, 64);
         const bool hj = __shfl((int)head, j, 64) != 0;
-        for (int t = l; t < nj * HW; t += 64) {
-            const int i = t / HW, wd = t - i * HW;
-            const uint32_t *ds = (i > 0 || kj == 0) ? sdig + ((size_t)Gj * cap + fj + i) * HW : (hj ? bdig + (size_t)Gj * HW : nullptr);
-            if (ds) dig[(size_t)(dj + i) * HW + wd] = ds[wd];
+        uint32_t v[3][HW];
+        bool ok[3];
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = r + 16 * u;
+            ok[u] = i < nj && (i > 0 || kj == 0 || hj);
+            const uint32_t *ds = (i > 0 || kj == 0) ? sdig + ((size_t)Gj * cap + fj + i) * HW : bdig + (size_t)Gj * HW;
+#pragma unroll
+            for (int w = 0; w < HW; w++) v[u][w] = ok[u] ? ds[w] : 0u;
         }
-        for (int i = l; i < nj; i += 64)
-            if (i > 0 || kj == 0 || hj) need[dj + i] = 0;
+#pragma unroll
+        for (int u = 0; u < 3; u++) {
+            const int i = r + 16 * u;
+            if (!ok[u]) continue;
+#pragma unroll
+            for (int w = 0; w < HW; w++) dig[(size_t)(dj + i) * HW + w] = v[u][w];
+            need[dj + i] = 0;
+        }
+        for (int i = r + 48; i < nj; i += 16) {           // (longer lists than kSegMaxWinF allows: none)
+#pragma unroll
+            for (int w = 0; w < HW; w++) dig[(size_t)(dj + i) * HW + w] = sdig[((size_t)Gj * cap + fj + i) * HW + w];
+            need[dj + i] = 0;
+        }
     }
 }
 __global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__restrict__ blocks,
@@ -1319,7 +1339,7 @@ __global__ void __launch_bounds__(64) spec_fallback_kernel(const BlockDesc *__re
     if (s.fail_dst >= 0) {
         WalkCfg W;
         W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
-        W.w = w; W.maxlen = maxlen; W.gm = gm + (size_t)b * gstride;
+        W.w = w; W.maxlen = maxlen; W.gm = gm ? gm + (size_t)b * gstride : nullptr;
         const bool first = s.fail_dst == 0;
         const int p0 = first ? 0 : (int)off[s.fail_dst - 1];
         ListSink sink;
@@ -1379,13 +1399,20 @@ static hipError_t launch_fused_front(const BlockDesc *d_blocks, int nblocks, int
                               X.rq_cap, X.irr, fz.sdig, fz.bdig, fz.gm_need, err, st)) != hipSuccess)
         return e;
     mk->mark(st);
-    const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
-    hipLaunchKernelGGL((gmax2_kernel<true, true>), dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm,
-                       X.gstride, (prio >> 4) & 1, (const int *)fz.gm_need);
+    // HDRF_FUSED_GM=1: the granule maxima of the blocks with a repaired boundary (the repair walk's
+    // long searches skip by them); default none: a boundary of every 4 GiB batch's blocks goes to the
+    // repair walk, so the pass ran over the whole batch (4.56 GB, profiles/r06_fz_traffic.json)
+    static const bool fz_gm = [] { const char *v = getenv("HDRF_FUSED_GM"); return v && atoi(v) != 0; }();
+    const uint8_t *gm = fz_gm ? X.gm : nullptr;
+    if (fz_gm) {
+        const int gx = (int)(((max_len + 15) / 16 + kGmPerWg - 1) / kGmPerWg);
+        hipLaunchKernelGGL((gmax2_kernel<true, true>), dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm,
+                           X.gstride, (prio >> 4) & 1, (const int *)fz.gm_need);
+    }
     const int rgrid = 512;
     const int HW = fz.hasher == 0 ? 5 : 7;
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0, (prio >> 1) & 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 0, (prio >> 1) & 1);
     hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
                        (prio >> 1) & 1);
     hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt, X.jcap,
@@ -1396,9 +1423,9 @@ static hipError_t launch_fused_front(const BlockDesc *d_blocks, int nblocks, int
                        X.wgsum, maxw, bst, offsets, cap_blk, (const uint32_t *)fz.sdig, (const uint32_t *)fz.bdig,
                        fz.dig, fz.need, HW);
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1, (prio >> 1) & 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 1, (prio >> 1) & 1);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
-                       cap_blk, bst, X.gm, X.gstride, err, (prio >> 1) & 1, fz.need);
+                       cap_blk, bst, gm, X.gstride, err, (prio >> 1) & 1, fz.need);
     return hipGetLastError();
 }
 

@@ -67,7 +67,9 @@ __device__ __forceinline__ unsigned long long bits_le(int b)     // bits 0..b
     return b < 0 ? 0ull : (b >= 63 ? ~0ull : ((2ull << b) - 1ull));
 }
 
-// the 17 dwords (68 B) of one block at pos (4-aligned down); past the readable bytes they read as 0
+// the 17 dwords (68 B) of one block at pos (4-aligned down).  Near the end of the readable bytes the
+// words past it re-read the last readable word: no byte at or past the block's length is ever used
+// (the chunk rule reads up to size - 1, pad_block clears the words after a message)
 __device__ __forceinline__ void load17(const uint8_t *base, uint64_t readable, uint32_t pos, uint32_t d[17])
 {
     const uint32_t apos = pos & ~3u;
@@ -80,8 +82,9 @@ __device__ __forceinline__ void load17(const uint8_t *base, uint64_t readable, u
         }
         d[16] = q[16];
     } else {
+        const uint32_t lim = (uint32_t)((readable - 4u) & ~3ull);
 #pragma unroll
-        for (int i = 0; i < 17; i++) d[i] = load4_guard(base, (int64_t)apos + 4 * i, (int64_t)readable);
+        for (int i = 0; i < 17; i++) d[i] = *gptr<uint32_t>(base + min(apos + 4u * i, lim));
     }
 }
 
@@ -151,79 +154,68 @@ __global__ void __launch_bounds__(256, 4) lane_hash_kernel(const BlockDesc *__re
     for (;;) {
         if (!ballot64(active && l < kWaveSegs)) break;
         if (!active) continue;
-        // one compression per lane and step, at one site: the block is the chunk's next 64 bytes
-        // (padded in place when the cut is in it) or the length-only block of the chunk cut last step
-        uint32_t m[16];
+        // One compression per lane and step, one code path for every lane (the lanes of a wave are
+        // at different places of their chunks, so a branch per case would run every case each step):
+        // the block is the chunk's next 64 bytes — padded in place when the cut is in it — or the
+        // length-only block of the chunk cut last step (pad_block zeroes whatever the words held).
         const bool padstep = pend;
-        int jb = -1, pos = 0;
-        uint32_t len = 0, nb = 0;
-        if (padstep) {
-#pragma unroll
-            for (int i = 0; i < 16; i++) m[i] = 0u;
-            nb = (plen + 8) / 64 + 1;
-            pad_block(m, plen, nb - 1, nb);
-        } else {
+        const int pos = p + 64 * blk;                      // (a pad step: the next chunk's start)
+        if (!padstep) {
             if (blk == 0 && p + w > size - 1) { active = walking = false; continue; }   // window incomplete
-            pos = p + 64 * blk;
             if (walking && pos - 64 > over_lim) { sync = kSyncFail; active = walking = false; continue; }   // byte cap
-            {
-                const uint32_t sel = 0x00010203u + ((uint32_t)pos & 3u) * 0x01010101u;
-#pragma unroll
-                for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(dn[i + 1], dn[i], sel);
-            }
-            // ---- window: running signed maxima over the words; the snapshot at window word wsw ----
-            uint32_t ro = wodd, re = wev, so = 0, se = 0;
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                if (i == wsw) {                            // (uniform) the window's last word: its bytes
-                    const uint32_t keep = wsb == 3 ? 0xffffffffu : ~(0xffffffffu >> (8 * (wsb + 1)));
-                    const uint32_t x = (m[i] & keep) | (0x80808080u & ~keep);   // after byte wo: -128
-                    so = pkmax_s(ro, x);
-                    se = pkmax_s(re, x << 8);
-                }
-                ro = pkmax_s(ro, m[i]);
-                re = pkmax_s(re, m[i] << 8);
-            }
-            uint32_t Mb = M;                               // the threshold this block's search uses
-            if (blk < wb) {
-                wodd = ro; wev = re;
-            } else if (blk == wb) {
-                int mx = smax_of(so, se) + 128;            // biased
-                if (!first) mx = max(mx, 0x80);            // mValue reset to 0 after a cut (:281)
-                M = Mb = (uint32_t)mx;
-            }
-            // ---- search: the first byte >= M in [w + 1, ub] (chunk-relative), ub = min(maxlen, size - 1 - p)
-            const int ub = min(maxlen, size - 1 - p);
-            const int sa = blk < wb ? 64 : (blk == wb ? wo + 1 : 0), sb = ub - 64 * blk;
-            bool ended = false;
-            if (blk >= wb) {
-                unsigned long long hit;
-                if (Mb == 0) {
-                    hit = ~0ull;                           // every byte qualifies
-                } else {
-                    const uint32_t C = __builtin_amdgcn_perm(256u - Mb, 256u - Mb, 0u), Cm = C & 0x7f7f7f7fu;
-                    uint32_t q[4];
-#pragma unroll
-                    for (int g = 0; g < 4; g++)
-                        q[g] = gather_be(ge_bits(m[4 * g], C, Cm), ge_bits(m[4 * g + 1], C, Cm),
-                                         ge_bits(m[4 * g + 2], C, Cm), ge_bits(m[4 * g + 3], C, Cm));
-                    hit = (unsigned long long)(q[0] | (q[1] << 16)) | ((unsigned long long)(q[2] | (q[3] << 16)) << 32);
-                }
-                hit &= bits_ge(sa) & bits_le(sb);
-                if (hit) {
-                    jb = __builtin_ctzll(hit);
-                } else if (sb <= 63) {                     // the search range ends in this block
-                    if (ub == maxlen) jb = sb;             // forced cut at p + maxlen (:288-294)
-                    else ended = true;                     // the data ended: no more cuts
-                }
-            }
-            if (ended) { active = walking = false; continue; }
-            if (jb >= 0) {                                 // the cut j = pos + jb: chunk [p, j + 1)
-                len = (uint32_t)(64 * blk + jb + 1);
-                nb = (len + 8) / 64 + 1;
-                pad_block(m, len, (uint32_t)blk, nb);
-            }
         }
+        uint32_t m[16];
+        {
+            const uint32_t sel = 0x00010203u + ((uint32_t)pos & 3u) * 0x01010101u;
+#pragma unroll
+            for (int i = 0; i < 16; i++) m[i] = __builtin_amdgcn_perm(dn[i + 1], dn[i], sel);
+        }
+        // ---- window: running signed maxima over the words; the snapshot at window word wsw --------
+        uint32_t ro = wodd, re = wev, so = 0, se = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            if (i == wsw) {                                // (uniform) the window's last word: its bytes
+                const uint32_t keep = wsb == 3 ? 0xffffffffu : ~(0xffffffffu >> (8 * (wsb + 1)));
+                const uint32_t x = (m[i] & keep) | (0x80808080u & ~keep);   // after byte wo: -128
+                so = pkmax_s(ro, x);
+                se = pkmax_s(re, x << 8);
+            }
+            ro = pkmax_s(ro, m[i]);
+            re = pkmax_s(re, m[i] << 8);
+        }
+        int mx = smax_of(so, se) + 128;                    // biased
+        if (!first) mx = max(mx, 0x80);                    // mValue reset to 0 after a cut (:281)
+        const uint32_t Mb = blk == wb ? (uint32_t)mx : M;  // the threshold this block's search uses
+        if (!padstep) {
+            if (blk < wb) { wodd = ro; wev = re; }
+            if (blk == wb) M = Mb;
+        }
+        // ---- search: the first byte >= M in [w + 1, ub] (chunk-relative), ub = min(maxlen, size - 1 - p)
+        const int ub = min(maxlen, size - 1 - p);
+        const int sa = blk < wb ? 64 : (blk == wb ? wo + 1 : 0), sb = ub - 64 * blk;
+        unsigned long long hit;
+        {
+            const uint32_t C = __builtin_amdgcn_perm(256u - Mb, 256u - Mb, 0u), Cm = C & 0x7f7f7f7fu;
+            uint32_t q[4];
+#pragma unroll
+            for (int g = 0; g < 4; g++)
+                q[g] = gather_be(ge_bits(m[4 * g], C, Cm), ge_bits(m[4 * g + 1], C, Cm), ge_bits(m[4 * g + 2], C, Cm),
+                                 ge_bits(m[4 * g + 3], C, Cm));
+            hit = (unsigned long long)(q[0] | (q[1] << 16)) | ((unsigned long long)(q[2] | (q[3] << 16)) << 32);
+            if (Mb == 0) hit = ~0ull;                      // every byte qualifies
+            hit &= bits_ge(sa) & bits_le(sb);
+        }
+        int jb = -1;
+        if (hit) jb = __builtin_ctzll(hit);
+        else if (sb <= 63 && sa <= 63 && ub == maxlen) jb = sb;   // forced cut at p + maxlen (:288-294)
+        if (!padstep && jb < 0 && sa <= 63 && sb <= 63) { active = walking = false; continue; }   // data ended
+        if (padstep) jb = -1;
+        // padding: the cut's block (length in place when it fits), the length-only block, or none
+        uint32_t len, pj, nb;
+        if (padstep) { len = plen; nb = (plen + 8) / 64 + 1; pj = nb - 1; }
+        else if (jb >= 0) { len = (uint32_t)(64 * blk + jb + 1); nb = (len + 8) / 64 + 1; pj = (uint32_t)blk; }
+        else { len = (uint32_t)(64 * blk + 64); pj = (uint32_t)blk; nb = pj + 2; }   // a full block: unchanged
+        pad_block(m, len, pj, nb);
         if (!padstep)                                      // the next data step's block: the chunk's next
             load17(base, readable, (uint32_t)(jb < 0 ? pos + 64 : pos + jb + 1), dn);   // 64 B, or the next chunk
         if (HW == 5) sha1_compress(st, m);
