@@ -728,7 +728,7 @@ extern "C" int hdrf_open(const hdrf_cfg *cfg_in, hdrf_ctx **out)
             rc = set_err(ctx, HDRF_E_HIP, "hipMemset failed");
     }
     ctx->timing = c.timing != 0;
-    ctx->fused = fused_front();
+    ctx->fused = fused_front() && c.n_ranks <= 1;     // (node-global fronts keep the two-pass front)
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device) == hipSuccess && ncu > 0)
