@@ -674,6 +674,9 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // next unit is prefetched into registers at the end of a chunk step once the window has moved into
 // the ring's second unit (after the step's raw load was waited for, so that wait never covers the
 // prefetch), and written into the ring when the window reaches it.  12 KiB of LDS per wave.
+#ifndef HDRF_WALK_LINE
+#define HDRF_WALK_LINE 0
+#endif
 constexpr int kRingU = 4 * kGmWin;       // granules per ring unit (= the window)
 constexpr int kRingDw = 2 * kGmWin;      // ring dwords per lane (lanes read at their own, unrelated
 constexpr int kRingPitch = kRingDw;      // offsets, so rows are not padded)
@@ -683,6 +686,10 @@ struct GmRing {
     int w0 = 0;                          // the last window start
     int pfg = -1;                        // granule of the unit held in pf (-1: none)
     uint4 pf[kGmWin / 4];
+#if HDRF_WALK_LINE
+    int pfg2 = -1;                       // the unit held in pf2: a line's second half (-1: none)
+    uint4 pf2[kGmWin / 4];
+#endif
     __device__ __forceinline__ void put(int g, const uint4 (&v)[kGmWin / 4])
     {
 #pragma unroll
@@ -698,12 +705,30 @@ struct GmRing {
         for (int i = 0; i < kGmWin / 4; i++) v[i] = ld16(gmb + g + 16 * i);
         put(g, v);
     }
+    // HDRF_WALK_LINE (build flag, A/B): a unit that starts a 128-B line is fetched with the line's
+    // second half, which is kept in pf2 for the next unit (a unit is half a line: fetched apart, a line's
+    // halves come from memory twice when the first was evicted between the lane's chunk steps)
     __device__ __forceinline__ void prefetch(const uint8_t *gmb)
     {
         if (on && pfg != rb + 2 * kRingU && w0 >= rb + kRingU / 2) {
             pfg = rb + 2 * kRingU;
+#if HDRF_WALK_LINE
+            if (pfg2 == pfg) {
+#pragma unroll
+                for (int i = 0; i < kGmWin / 4; i++) pf[i] = pf2[i];
+                pfg2 = -1;
+                return;
+            }
+#endif
 #pragma unroll
             for (int i = 0; i < kGmWin / 4; i++) pf[i] = ld16(gmb + pfg + 16 * i);
+#if HDRF_WALK_LINE
+            if ((pfg & 127) == 0) {
+#pragma unroll
+                for (int i = 0; i < kGmWin / 4; i++) pf2[i] = ld16(gmb + pfg + kRingU + 16 * i);
+                pfg2 = pfg + kRingU;
+            }
+#endif
         }
     }
     bool on = true;                      // false: HDRF_WALK_RING=0, the maxima straight from memory (A/B)
@@ -725,6 +750,9 @@ struct GmRing {
         if (W0 < rb || W0 > rb + kRingU) {
             if (W0 <= rb + 2 * kRingU) {                          // the window moved on by one unit
                 if (pfg == rb + 2 * kRingU) put(pfg, pf);
+#if HDRF_WALK_LINE
+                else if (pfg2 == rb + 2 * kRingU) put(pfg2, pf2);
+#endif
                 else fill(gmb, rb + 2 * kRingU);
                 rb += kRingU;
             } else {                                              // first use, or a long search jumped
