@@ -675,7 +675,7 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // the ring's second unit (after the step's raw load was waited for, so that wait never covers the
 // prefetch), and written into the ring when the window reaches it.  12 KiB of LDS per wave.
 #ifndef HDRF_WALK_LINE
-#define HDRF_WALK_LINE 0
+#define HDRF_WALK_LINE 1                 // (0: half-line units, the A/B baseline; profiles/r06_walkline*_ab.txt)
 #endif
 constexpr int kRingU = 4 * kGmWin;       // granules per ring unit (= the window)
 constexpr int kRingDw = 2 * kGmWin;      // ring dwords per lane (lanes read at their own, unrelated
@@ -705,9 +705,11 @@ struct GmRing {
         for (int i = 0; i < kGmWin / 4; i++) v[i] = ld16(gmb + g + 16 * i);
         put(g, v);
     }
-    // HDRF_WALK_LINE (build flag, A/B): a unit that starts a 128-B line is fetched with the line's
+    // HDRF_WALK_LINE (build flag, default 1): a unit that starts a 128-B line is fetched with the line's
     // second half, which is kept in pf2 for the next unit (a unit is half a line: fetched apart, a line's
-    // halves come from memory twice when the first was evicted between the lane's chunk steps)
+    // halves came from memory twice when the first was evicted between the lane's chunk steps; half the
+    // ring's scattered 16-B load instructions).  Walk counted bytes 1.20 -> 1.11 GB per batch; config 2
+    // 1098 / 1105 / 1110 vs 1058 / 1057 / 1056 and 1113 / 1118 / 1116 vs 1114 / 1104 / 1106 GB/s on two boxes
     __device__ __forceinline__ void prefetch(const uint8_t *gmb)
     {
         if (on && pfg != rb + 2 * kRingU && w0 >= rb + kRingU / 2) {
