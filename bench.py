@@ -87,6 +87,8 @@ def load_pmc(want):
     scripts/traffic.py -> profiles/*_traffic.json) taken on this same workload (`want`: the
     workload's `_config` keys; a file without "workload" was taken on config 2)."""
     import glob
+    want = dict(want)
+    want.setdefault("front", "two-pass")            # (a fused-front pass, §6b, is only its own workload's)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json")))   # names sort by round, version
     for f in reversed(files):
         d = json.load(open(f))

@@ -48,3 +48,14 @@ def test_named_kernels_have_committed_traffic(monkeypatch):
     d, _ = b.load_pmc(dict(WANT, workload="config2"))
     for name, kern in b.KERNEL_OF.items():
         assert any(kern + t in d for t in ("", "<5>", "<true>")), (name, kern)
+
+
+def test_fused_front_traffic_is_its_own(monkeypatch):
+    """The fused front's PMC file is matched only when the line runs that front; the
+    two-pass line keeps the two-pass file whatever sorts newest."""
+    b = _bench(monkeypatch)
+    d2, src2 = b.load_pmc(dict(WANT, workload="config2"))
+    df, srcf = b.load_pmc(dict(WANT, workload="config2", front="fused"))
+    assert src2 and srcf and src2 != srcf
+    assert "lane_hash_kernel<5>" in df and "lane_hash_kernel<5>" not in d2
+    assert "sha_carry_kernel<5>" in d2
