@@ -674,6 +674,9 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // next unit is prefetched into registers at the end of a chunk step once the window has moved into
 // the ring's second unit (after the step's raw load was waited for, so that wait never covers the
 // prefetch), and written into the ring when the window reaches it.  12 KiB of LDS per wave.
+#ifndef HDRF_COOP
+#define HDRF_COOP 0                      // (build flag, A/B) wave-cooperative list and offsets copies
+#endif
 #ifndef HDRF_WALK_LINE
 #define HDRF_WALK_LINE 1                 // (0: half-line units, the A/B baseline; profiles/r06_walkline*_ab.txt)
 #endif
@@ -926,10 +929,29 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
         if (overflow) active = false;
     }
     if (overflow && real) atomicOr(err, 64);
+#if HDRF_COOP
+    {
+        // the wave's lists, written together: its 63 segments' lists are consecutive rows of `cap`
+        // words (segment G at G * cap), so the lanes store the rows' words in order (coalesced) instead
+        // of each lane walking its own row (63 scattered streams of ~15 stores)
+        const int nreal = min(kWaveSegs, nseg - wl * kWaveSegs);
+        uint32_t *rows = spec + (size_t)(bd.seg0 + wl * kWaveSegs) * cap;
+        int j = l / cap, i = l - (l / cap) * cap;
+        const int jstep = 64 / cap, istep = 64 - (64 / cap) * cap;
+        for (int t = l; t < nreal * cap; t += 64) {
+            if (i < (int)vcnt[j]) rows[t] = (uint32_t)((wl * kWaveSegs + j) * Ls) + (uint32_t)vcuts[j * kLdsCuts + i];
+            j += jstep;
+            i += istep;
+            if (i >= cap) { i -= cap; j++; }
+        }
+    }
+#endif
     if (real) {
         const int G = bd.seg0 + k;
+#if !HDRF_COOP
         uint32_t *list = spec + (size_t)G * cap;
         for (int i = 0; i < n; i++) list[i] = (uint32_t)s + (uint32_t)vcuts[l * kLdsCuts + i];
+#endif
         if (n_main < 0) n_main = n;
         SegMeta m;
         m.n_main = n_main; m.n_over = n - n_main; m.sync = sync; m.jmp = 0; m.jj = 0; m.n_ext = 0; m.ext_dst = -1;
@@ -1335,11 +1357,34 @@ __global__ void __launch_bounds__(256) stitch_copy_kernel(const BlockDesc *__res
     if (k < nseg && cnt > 0) {
         const int ext = meta[G].pad[1];
         if (ext >= 0) meta[G].ext_dst = (int)dst + ext;  // the repair's cuts (emit pass)
+#if !HDRF_COOP
         const int n = meta[G].cp_n, from = meta[G].cp_from;
         const uint32_t *src = spec + (size_t)G * cap + from;
         uint32_t *out = offsets + (size_t)b * cap_blk + dst;
         for (int i = 0; i < n; i++) out[i] = src[i];
+#endif
     }
+#if HDRF_COOP
+    {                                                     // (uniform) the pieces, 16 lanes per segment
+        const bool mine = k < nseg && cnt > 0;
+        const int n_l = mine ? meta[G].cp_n : 0, from_l = mine ? meta[G].cp_from : 0;
+        const int l = lane_id(), r = l & 15;
+        uint32_t *orow = offsets + (size_t)b * cap_blk;
+        for (int j0 = 0; j0 < 64; j0 += 4) {
+            const int jj = j0 + (l >> 4);
+            const int nj = __shfl(n_l, jj, 64);
+            if (!ballot64(nj > 0)) continue;
+            const int Gj = __shfl(G, jj, 64), fj = __shfl(from_l, jj, 64), dj = __shfl((int)dst, jj, 64);
+            uint32_t v[3];
+#pragma unroll
+            for (int u = 0; u < 3; u++) v[u] = r + 16 * u < nj ? spec[(size_t)Gj * cap + fj + r + 16 * u] : 0u;
+#pragma unroll
+            for (int u = 0; u < 3; u++)
+                if (r + 16 * u < nj) orow[dj + r + 16 * u] = v[u];
+            for (int i = r + 48; i < nj; i += 16) orow[dj + i] = spec[(size_t)Gj * cap + fj + i];
+        }
+    }
+#endif
     if (sdig) {                                           // (uniform) the fused pass's digests
         const bool mine = k < nseg && cnt > 0;
         const int n_l = mine ? meta[G].cp_n : 0, from_l = mine ? meta[G].cp_from : 0;
