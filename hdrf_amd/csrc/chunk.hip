@@ -675,8 +675,8 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // the ring's second unit (after the step's raw load was waited for, so that wait never covers the
 // prefetch), and written into the ring when the window reaches it.  12 KiB of LDS per wave.
 #ifndef HDRF_COOP
-#define HDRF_COOP 0                      // (build flag, A/B) wave-cooperative list and offsets copies
-#endif
+#define HDRF_COOP 1                      // wave-cooperative list and offsets copies (0: per-lane rows, the A/B
+#endif                                   // baseline; profiles/r06_coop*_ab.txt)
 #ifndef HDRF_WALK_LINE
 #define HDRF_WALK_LINE 1                 // (0: half-line units, the A/B baseline; profiles/r06_walkline*_ab.txt)
 #endif
