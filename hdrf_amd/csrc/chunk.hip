@@ -677,6 +677,9 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32;
 #ifndef HDRF_COOP
 #define HDRF_COOP 1                      // wave-cooperative list and offsets copies (0: per-lane rows, the A/B
 #endif                                   // baseline; profiles/r06_coop*_ab.txt)
+#ifndef HDRF_COOP_META
+#define HDRF_COOP_META 0                 // (build flag, A/B) the walk's SegMeta records stored together
+#endif
 #ifndef HDRF_WALK_LINE
 #define HDRF_WALK_LINE 1                 // (0: half-line units, the A/B baseline; profiles/r06_walkline*_ab.txt)
 #endif
@@ -953,16 +956,37 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
         for (int i = 0; i < n; i++) list[i] = (uint32_t)s + (uint32_t)vcuts[l * kLdsCuts + i];
 #endif
         if (n_main < 0) n_main = n;
+#if !HDRF_COOP_META
         SegMeta m;
         m.n_main = n_main; m.n_over = n - n_main; m.sync = sync; m.jmp = 0; m.jj = 0; m.n_ext = 0; m.ext_dst = -1;
         m.cp_from = 0; m.cp_n = 0; m.cp_dst = 0; m.pad[0] = m.pad[1] = m.pad[2] = 0;
         meta[G] = m;
+#endif
         if (k < nseg - 1 && sync < 0) atomicOr(irr + (G >> 5), 1u << (G & 31));   // irregular boundary
         if (sync == kSyncFail) {
             const int q = atomicAdd(rq_count, 1);
             if (q < rq_cap) rq[q] = G;                        // beyond rq_cap: no repair, stitch falls back
         }
     }
+#if HDRF_COOP_META
+    {
+        // the wave's SegMeta records (consecutive, 13 words each) through its LDS list rows, which the
+        // list copy above has read: each lane stages its record, the lanes store the words in order
+        static_assert(sizeof(SegMeta) == 52 && 63 * 52 <= 64 * kLdsCuts * 2, "SegMeta staging");
+        const int nreal = min(kWaveSegs, nseg - wl * kWaveSegs);
+        __attribute__((address_space(3))) volatile uint32_t *st32 =
+            (__attribute__((address_space(3))) volatile uint32_t *)vcuts;
+        if (real) {
+            const int nm = n_main < 0 ? n : n_main;
+            const uint32_t w[13] = {(uint32_t)nm, (uint32_t)(n - nm), (uint32_t)sync, 0u, 0u, 0u, 0xffffffffu,
+                                    0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int i = 0; i < 13; i++) st32[l * 13 + i] = w[i];
+        }
+        uint32_t *mrow = (uint32_t *)(meta + bd.seg0 + wl * kWaveSegs);
+        for (int t = l; t < nreal * 13; t += 64) mrow[t] = st32[t];
+    }
+#endif
 }
 
 // 2. repair: one wave per failed boundary k (queued by the lane walk), the exact sequential walker
