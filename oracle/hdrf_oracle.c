@@ -817,9 +817,12 @@ void hdrf_oracle_java_random_bytes(int64_t seed, int32_t buffer_len, int64_t tot
  *      len <= 261,100      : BE32 len | BE32 clen | block
  *      len  > 261,100      : BE32 len | (BE32 clen | block) per 261,100-B segment | BE32 0
  *  - block: lz4 r123 LZ4_compress() (hadoop-common native Lz4Compressor.c), restated below.
- * Parity of the compressed bytes against Hadoop is UNPINNED (neither is present here); the
- * restatement is pinned by exact round trips through an independent decoder (liblz4 1.9.3's
- * LZ4_decompress_safe in tests) and the GPU must equal it byte for byte. */
+ * Hadoop and r123 are not present here.  The restatement is pinned against a real liblz4 (the one
+ * pyarrow 25.0.0 bundles, >= 1.9): run under the three rules where liblz4 >= 1.9 parses
+ * differently from r123 (lz4_compress_rules below) it equals liblz4's LZ4_compress_default byte
+ * for byte on every input tests/test_lz4_liblz4.py tries, and its r123 output decodes through
+ * liblz4's decoder; the three r123 rules themselves are restated, not pinned.  The GPU must equal
+ * the r123-rule output byte for byte. */
 #define LZ4_MINMATCH 4
 #define LZ4_MFLIMIT 12
 #define LZ4_LASTLITERALS 5
@@ -831,32 +834,51 @@ void hdrf_oracle_java_random_bytes(int64_t seed, int32_t buffer_len, int64_t tot
 #define HADOOP_LZ4_MAX_INPUT 261100
 
 static uint32_t lz_rd32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static int max_i(int a, int b) { return a > b ? a : b; }
+static uint32_t lz_hash5(const uint8_t *p)              /* liblz4 >= 1.9 LZ4_hash5, byU32, little endian */
+{
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return (uint32_t)(((v << 24) * 889523592379ull) >> (64 - 12));
+}
 
 int64_t hdrf_oracle_lz4_bound(int64_t n) { return n + n / 255 + 16; }
 
-/* LZ4_compress_generic(noDict, notLimited, byU16 when n < 64 KiB + 11 else byU32) */
-int64_t hdrf_oracle_lz4_compress(const uint8_t *src, int64_t n, uint8_t *dst)
+/* LZ4_compress_generic(noDict, notLimited, byU16 when n < 64 KiB + 11 else byU32).
+ *
+ * `rules` (test infrastructure only, never r123): the three places where liblz4 >= 1.9 on a 64-bit
+ * host parses differently from r123, so that the same restatement can be compared byte for byte
+ * with a modern liblz4 (pyarrow's bundled one, tests/test_lz4_liblz4.py):
+ *   bit 0  the search steps: 1, then searchMatchNb++ >> skipTrigger from 1 << skipTrigger, so
+ *          step k is (63 + k) >> 6 (r123: (67 + k) >> 6, growing 4 attempts earlier);
+ *   bit 1  the search gives up when the next position passes mflimit + 1 (r123: mflimit);
+ *   bit 2  byU32 tables hash 5 bytes, ((v64 << 24) * 889523592379) >> (64 - 12) (r123: 4 bytes).
+ * Everything else — table fill, catch-up, the test of the next position, token / length / offset
+ * coding, last literals — is the shared code, which is what the comparison pins. */
+static int64_t lz4_compress_rules(const uint8_t *src, int64_t n, uint8_t *dst, int rules)
 {
     const int hlog = n < LZ4_64KLIMIT ? 13 : 12;           /* LZ4_HASHLOG(+1 for byU16), MEMORY_USAGE 14 */
+    const int hash5 = (rules & 4) && n >= LZ4_64KLIMIT;
     uint32_t *table = (uint32_t *)calloc((size_t)1 << hlog, sizeof(uint32_t));
     const uint8_t *ip = src, *anchor = src;
     const uint8_t *const iend = src + n, *const mflimit = iend - LZ4_MFLIMIT, *const matchlimit = iend - LZ4_LASTLITERALS;
+    const uint8_t *const slimit = (rules & 2) ? mflimit + 1 : mflimit;
     uint8_t *op = dst;
-#define LZH(p) ((uint32_t)(lz_rd32(p) * 2654435761u) >> (32 - hlog))
+#define LZH(p) (hash5 ? lz_hash5(p) : (uint32_t)(lz_rd32(p) * 2654435761u) >> (32 - hlog))
     if (n >= LZ4_MFLIMIT + 1) {                            /* LZ4_minLength */
         table[LZH(ip)] = 0;                                /* first byte */
         ip++;
         uint32_t fh = LZH(ip);
         for (;;) {
-            int attempts = (1 << LZ4_SKIPSTRENGTH) + 3;
+            int attempts = (1 << LZ4_SKIPSTRENGTH) + ((rules & 1) ? -1 : 3);
             const uint8_t *fip = ip, *ref;
             uint8_t *token;
             do {                                           /* find a match */
                 const uint32_t h = fh;
-                const int step = attempts++ >> LZ4_SKIPSTRENGTH;
+                const int step = max_i(1, attempts++ >> LZ4_SKIPSTRENGTH);
                 ip = fip;
                 fip = ip + step;
-                if (fip > mflimit) goto last_literals;
+                if (fip > slimit) goto last_literals;
                 fh = LZH(fip);
                 ref = src + table[h];
                 table[h] = (uint32_t)(ip - src);
@@ -920,6 +942,14 @@ last_literals:
 #undef LZH
     free(table);
     return op - dst;
+}
+
+int64_t hdrf_oracle_lz4_compress(const uint8_t *src, int64_t n, uint8_t *dst) { return lz4_compress_rules(src, n, dst, 0); }
+
+/* test infrastructure: the same parse under liblz4 >= 1.9's rules (above) */
+int64_t hdrf_oracle_lz4_compress_modern(const uint8_t *src, int64_t n, uint8_t *dst, int rules)
+{
+    return lz4_compress_rules(src, n, dst, rules);
 }
 
 /* LZ4 block decoder (test helper; returns decoded length or -1 on malformed input) */

@@ -87,6 +87,7 @@ int64_t hdrf_oracle_container(const hdrf_oracle *o, uint32_t id, uint8_t *out, i
  * reference tree: compressed-byte parity vs Hadoop UNPINNED; see hdrf_oracle.c. */
 int64_t hdrf_oracle_lz4_bound(int64_t n);
 int64_t hdrf_oracle_lz4_compress(const uint8_t *src, int64_t n, uint8_t *dst);
+int64_t hdrf_oracle_lz4_compress_modern(const uint8_t *src, int64_t n, uint8_t *dst, int rules);   /* tests: liblz4 >= 1.9 rules */
 int64_t hdrf_oracle_lz4_decompress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
 int64_t hdrf_oracle_hadoop_lz4_bound(int64_t n);
 int64_t hdrf_oracle_hadoop_lz4_frame(const uint8_t *src, int64_t n, uint8_t *dst);

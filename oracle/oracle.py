@@ -66,6 +66,8 @@ def lib():
         for name in ("hdrf_oracle_lz4_compress", "hdrf_oracle_hadoop_lz4_frame"):
             getattr(L, name).argtypes = [_u8p, ctypes.c_int64, _u8p]
             getattr(L, name).restype = ctypes.c_int64
+        L.hdrf_oracle_lz4_compress_modern.argtypes = [_u8p, ctypes.c_int64, _u8p, ctypes.c_int]
+        L.hdrf_oracle_lz4_compress_modern.restype = ctypes.c_int64
         L.hdrf_oracle_reduce_many.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
                                               ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                               ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
@@ -191,6 +193,16 @@ def lz4_block(data):
     buf = a if a.size else np.zeros(1, np.uint8)
     out = np.zeros(lib().hdrf_oracle_lz4_bound(a.size), np.uint8)
     n = lib().hdrf_oracle_lz4_compress(_p(buf), a.size, _p(out))
+    return out[:n].tobytes()
+
+
+def lz4_block_modern(data, rules=7):
+    """The same parse under liblz4 >= 1.9's rules (hdrf_oracle.c lz4_compress_rules; tests only):
+    compared byte for byte with pyarrow's bundled liblz4 to pin the shared encoder."""
+    a = _as_u8(data)
+    buf = a if a.size else np.zeros(1, np.uint8)
+    out = np.zeros(lib().hdrf_oracle_lz4_bound(a.size), np.uint8)
+    n = lib().hdrf_oracle_lz4_compress_modern(_p(buf), a.size, _p(out), rules)
     return out[:n].tobytes()
 
 
