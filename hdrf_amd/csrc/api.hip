@@ -66,6 +66,7 @@ struct Slot {
     uint32_t *d_wgsum = nullptr;              // [B][maxw_cap]
     int maxw_cap = 0;
     int *d_rq = nullptr, *d_rq_count = nullptr;   // failed speculative boundaries (repair queue), meta_cap entries
+    uint32_t *d_rqkeep = nullptr;             // [kRqKeep][64] cuts of the short repair walks
     size_t spec_words = 0, meta_cap = 0;      // capacity of d_spec (u32) / d_meta (segments), grown on demand
     int total_waves = 0, total_segs = 0, spec_cap = 0;   // lane walk of the batch in this slot
     BlockState *d_bst = nullptr;
@@ -383,7 +384,7 @@ extern "C" int hdrf_default_cfg(hdrf_cfg *cfg)
 
 static void free_slot(Slot &S)
 {
-    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_bst, S.d_off, S.d_dig, S.d_slot,
+    void *dev[] = {S.d_blocks, S.d_spec, S.d_meta, S.d_gm, S.d_irr, S.d_path, S.d_jx, S.d_jt, S.d_wgsum, S.d_rq, S.d_rq_count, S.d_rqkeep, S.d_bst, S.d_off, S.d_dig, S.d_slot,
                    S.d_pre, S.d_flags, S.d_dcnt, S.d_tilesum, S.d_tilepre, S.d_store, S.d_rstate, S.d_ev, S.d_closed,
                    S.d_nclosed, S.d_coll, S.d_ncoll, S.d_pcid, S.d_ppos, S.d_queue, S.d_segclen, S.d_filelen, S.d_err,
                    S.d_lzwork, S.d_sdig, S.d_bdig, S.d_need, S.d_nlist, S.d_gmneed};
@@ -471,7 +472,8 @@ static int alloc_slot(hdrf_ctx *ctx, Slot &S)
         (rc = dalloc(ctx, &S.d_jx, (size_t)B * S.jcap)) || (rc = dalloc(ctx, &S.d_jt, (size_t)B * S.jcap)) ||
         (rc = dalloc(ctx, &S.d_irr, S.meta_cap / 32 + 2)) ||
         (rc = dalloc(ctx, &S.d_meta, S.meta_cap)) || (rc = dalloc(ctx, &S.d_rq, S.meta_cap)) ||
-        (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_bst, B)) ||
+        (rc = dalloc(ctx, &S.d_rq_count, 1)) || (rc = dalloc(ctx, &S.d_rqkeep, (size_t)kRqKeep * 64)) ||
+        (rc = dalloc(ctx, &S.d_bst, B)) ||
         (rc = dalloc(ctx, &S.d_off, nchunk)) || (rc = dalloc(ctx, &S.d_dig, nchunk * ctx->HW)) ||
         (rc = dalloc(ctx, &S.d_slot, nchunk)) ||
         (rc = dalloc(ctx, &S.d_pre, nchunk)) || (rc = dalloc(ctx, &S.d_flags, nchunk)) || (rc = dalloc(ctx, &S.d_dcnt, nchunk)) ||
@@ -827,6 +829,7 @@ static ChunkScratch chunk_scratch(Slot &S, int compressor = 1)
     ChunkScratch X;
     X.ring = compressor == 2 ? 0 : 1;
     X.gm = S.d_gm; X.gstride = S.gstride; X.rq = S.d_rq; X.rq_count = S.d_rq_count; X.rq_cap = (int)S.meta_cap;
+    X.rqkeep = S.d_rqkeep;
     X.irr = S.d_irr; X.path = S.d_path; X.jx = S.d_jx; X.jt = S.d_jt; X.jcap = S.jcap; X.wgsum = S.d_wgsum;
     X.maxw = S.maxw_cap;
     return X;

@@ -412,15 +412,18 @@ struct ListSink {
     }
 };
 
-// Cut sink that only counts (the repair pass finds where a chain merges before anything is written).
-struct CountSink {
+// Cut sink of the repair's count pass: counts, and keeps the first 64 cuts in a VGPR (lane i = cut
+// i; the fast path stages through the same register), so a walk that met its shared cut within 64
+// cuts hands the n_ext - 1 cuts before it to the emit pass without a second walk.
+struct KeepSink {
     int cap;
     int cnt;
     uint32_t stage;
     __device__ __forceinline__ void store64(int, uint32_t) {}
-    __device__ __forceinline__ bool push(uint32_t)
+    __device__ __forceinline__ bool push(uint32_t cut)
     {
         if (cnt >= cap) return false;
+        if (lane_id() == (cnt & 63)) stage = cut;
         cnt++;
         return true;
     }
@@ -994,8 +997,9 @@ __global__ void __launch_bounds__(256) lane_walk_kernel(const BlockDesc *__restr
 //    of the segment m = c / seg_len holding it (m > k); once found at index j, segment k's chain
 //    continues as segment m's from there (kSyncJump, k + jmp = m, jj = j, n_ext cuts walked); no
 //    shared cut within kRepairCuts cuts / kRepairBytes bytes, or the block end: kSyncGiveUp.
-//    emit (after the stitch placed it): the same walk writes its n_ext - 1 cuts before the shared
-//    one into the block's offsets, for repairs on the block's path.
+//    emit (after the stitch placed it): the n_ext - 1 cuts before the shared one go into the block's
+//    offsets, for repairs on the block's path — copied from what the find pass kept when there were
+//    at most 63 of them (queue entries below kRqKeep), else by the same walk again.
 struct MergeStop {
     const uint32_t *spec;
     const SegMeta *meta;
@@ -1027,7 +1031,7 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
                                                           const uint32_t *__restrict__ spec, int cap,
                                                           SegMeta *__restrict__ meta, uint32_t *__restrict__ offsets,
                                                           int cap_blk, const uint8_t *__restrict__ gm, int gstride,
-                                                          int emit, int prio)
+                                                          int emit, int prio, uint32_t *__restrict__ keep)
 {    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
 
     const int nw = gridDim.x * 4;
@@ -1041,6 +1045,11 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
         const int k = G - bd.seg0;
         const SegMeta m = meta[G];
         if (emit && (m.sync != kSyncJump || m.ext_dst < 0 || m.n_ext <= 1)) continue;
+        if (emit && q < kRqKeep && m.n_ext <= 64) {      // kept by the count pass (same q, same walk)
+            if (lane_id() < m.n_ext - 1)
+                offsets[(size_t)bi * cap_blk + m.ext_dst + lane_id()] = keep[(size_t)q * 64 + lane_id()];
+            continue;
+        }
         const int n = m.n_main + m.n_over;
         const int s_k = k * bd.seg_len;
         const int p0 = n > 0 ? (int)spec[(size_t)G * cap + n - 1] : s_k;
@@ -1049,12 +1058,14 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
         W.base = bd.data; W.avail = (int)min(bd.readable, (uint64_t)0x7fffffff); W.size = (int)bd.len;
         W.w = w; W.maxlen = maxlen; W.gm = gm ? gm + (size_t)bi * gstride : nullptr;
         if (!emit) {
-            CountSink sink;
+            KeepSink sink;
             sink.cap = kRepairCuts; sink.cnt = 0; sink.stage = 0;
             MergeStop st;
             st.spec = spec; st.meta = meta; st.cap = cap; st.seg0 = bd.seg0; st.k = k; st.nseg = bd.nseg;
             st.Ls = bd.seg_len; st.lim_cut = p0 + kRepairBytes;
             (void)walk_chain(W, p0, first, sink, st);
+            if (st.status == 1 && q < kRqKeep && sink.cnt <= 64 && lane_id() < sink.cnt - 1)
+                keep[(size_t)q * 64 + lane_id()] = sink.stage;
             if (lane_id() == 0) {
                 if (st.status == 1) {
                     meta[G].jmp = st.res_m - k;
@@ -1511,7 +1522,7 @@ static hipError_t launch_fused_front(const BlockDesc *d_blocks, int nblocks, int
     const int rgrid = 512;
     const int HW = fz.hasher == 0 ? 5 : 7;
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 0, (prio >> 1) & 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 0, (prio >> 1) & 1, X.rqkeep);
     hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
                        (prio >> 1) & 1);
     hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt, X.jcap,
@@ -1522,7 +1533,7 @@ static hipError_t launch_fused_front(const BlockDesc *d_blocks, int nblocks, int
                        X.wgsum, maxw, bst, offsets, cap_blk, (const uint32_t *)fz.sdig, (const uint32_t *)fz.bdig,
                        fz.dig, fz.need, HW);
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 1, (prio >> 1) & 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 1, (prio >> 1) & 1, X.rqkeep);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
                        cap_blk, bst, gm, X.gstride, err, (prio >> 1) & 1, fz.need);
     return hipGetLastError();
@@ -1580,7 +1591,7 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     mk->mark(st);
     const int rgrid = 512;                             // 2048 repair waves loop over the queue
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0, (prio >> 1) & 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0, (prio >> 1) & 1, X.rqkeep);
     hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
                        (prio >> 1) & 1);
     hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt, X.jcap,
@@ -1590,7 +1601,7 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     hipLaunchKernelGGL(stitch_copy_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, spec, spec_cap,
                        X.wgsum, maxw, bst, offsets, cap_blk);
     hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
-                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1, (prio >> 1) & 1);
+                       w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1, (prio >> 1) & 1, X.rqkeep);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
                        cap_blk, bst, X.gm, X.gstride, err, (prio >> 1) & 1);
     return hipGetLastError();

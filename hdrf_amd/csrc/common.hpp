@@ -24,6 +24,7 @@ constexpr int kLaneOver = 8;         // overrun cuts a lane may record past its 
 constexpr int kLdsCuts = 30;         // LDS list of every lane (u16 offsets from its segment start)
 constexpr int kRepairCuts = 4096;    // a repair walk gives up after this many cuts ...
 constexpr int kRepairBytes = 2 << 20;  // ... or this many bytes past its start
+constexpr int kRqKeep = 16384;       // repair-queue entries whose cuts the count pass keeps (64 words each)
 constexpr int kSegMinWin = 4;        // seg_len bounds, in units of window + 2 (702 B)
 constexpr int kSegMaxWin = 20;        // seg_len / 702 + 2 + kLaneOver <= kLdsCuts
 // the fused chunk + fingerprint pass (lanehash.hip) sizes its segments for one round of its waves,

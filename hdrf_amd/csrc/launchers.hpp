@@ -40,6 +40,8 @@ struct ChunkScratch {
     int gstride;
     int *rq, *rq_count;      // repair queue (rq_cap entries)
     int rq_cap;
+    uint32_t *rqkeep;        // [kRqKeep][64]: the cuts a repair walk found, when it found at most 63 before
+                             // the shared one (the emit pass copies them instead of walking again)
     uint32_t *irr;           // irregular-boundary bitmask over the batch's segments (+2 words)
     PathInfo *path;          // [nblocks]
     int *jx;                 // [nblocks][jcap] on-path jump sources
