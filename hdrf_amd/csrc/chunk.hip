@@ -1025,7 +1025,7 @@ struct MergeStop {
     __device__ __forceinline__ int cnt_thr() const { return 0x7fffffff; }
 };
 
-__global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
+__global__ void __launch_bounds__(64) lane_repair_kernel(const BlockDesc *__restrict__ blocks, int nblocks,
                                                           const int *__restrict__ rq, const int *__restrict__ rq_count,
                                                           int rq_cap, int w, int maxlen,
                                                           const uint32_t *__restrict__ spec, int cap,
@@ -1034,9 +1034,9 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
                                                           int emit, int prio, uint32_t *__restrict__ keep)
 {    if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
 
-    const int nw = gridDim.x * 4;
+    const int nw = gridDim.x;
     const int cnt = min(*rq_count, rq_cap);
-    for (int q = blockIdx.x * 4 + wave_id(); q < cnt; q += nw) {
+    for (int q = blockIdx.x; q < cnt; q += nw) {
         const int G = __builtin_amdgcn_readfirstlane(rq[q]);
         int bi = 0;
         for (int i = 1; i < nblocks; i++)
@@ -1096,11 +1096,11 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
 //    cuts; the segments jumped over are off the path); the path ends at the last segment, at a chain
 //    that ran to the block end, or at a failed boundary (seg k keeps all its cuts and the sequential
 //    fallback continues from the last one).  Four wide kernels:
-//      path   one workgroup per block: the irregular boundaries (not "synced to k + 1"; a bitmask the
+//      path   one wave per block: the irregular boundaries (not "synced to k + 1"; a bitmask the
 //             lane walk wrote) are compacted in order with their status, thread 0 follows the path
 //             through them (LDS only) and writes the on-path jumps, the terminal and the fallback flag
 //      count  one thread per segment: its piece (first list index, cuts, repair cuts) + workgroup sums
-//      scan   one workgroup per block: prefix over the workgroup sums; n_cuts / fail_dst
+//      scan   one wave per block: prefix over the workgroup sums; n_cuts / fail_dst
 //      copy   one thread per segment: workgroup prefix -> destination; the piece is copied
 // The irregular boundaries are compacted kStitchNodes at a time (a window of the ordered node list
 // in LDS); thread 0 follows the path through a window and the next window is loaded when the path
@@ -1111,7 +1111,7 @@ __global__ void __launch_bounds__(256) lane_repair_kernel(const BlockDesc *__res
 // (path) and 2 KiB (count) let both start beside a compressor-2 LZ4 pass (16 KiB free per CU).
 constexpr int kStitchNodes = 1024;
 
-__global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__restrict__ blocks,
+__global__ void __launch_bounds__(64) stitch_path_kernel(const BlockDesc *__restrict__ blocks,
                                                           const uint32_t *__restrict__ irr,
                                                           const SegMeta *__restrict__ meta,
                                                           PathInfo *__restrict__ path, int *__restrict__ jx_all,
@@ -1120,7 +1120,6 @@ __global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__res
     if (prio) __builtin_amdgcn_s_setprio(3);        // latency-bound chain: issue before co-running waves
     __shared__ int s_nx[kStitchNodes];       // compacted irregular nodes of the window (ascending)
     __shared__ uint32_t s_nv[kStitchNodes];  // status: bit 31 jump (jmp in bits 0..23, jj in 24..29), bit 30 end
-    __shared__ uint32_t s_sum[256];
     __shared__ int s_go;
     const int b = blockIdx.x, t = threadIdx.x;
     const BlockDesc bd = blocks[b];
@@ -1135,20 +1134,13 @@ __global__ void __launch_bounds__(256) stitch_path_kernel(const BlockDesc *__res
         const int rem = nb - 32 * i;
         return rem >= 32 ? v : (v & ((1u << rem) - 1u));
     };
-    const int per = (nwords + 255) >> 8;
+    const int per = (nwords + 63) >> 6;       // one wave per block: a run of words per lane
     const int w0 = min(nwords, t * per), w1 = min(nwords, w0 + per);
     uint32_t cnt = 0;
     for (int i = w0; i < w1; i++) cnt += (uint32_t)__popc(word(i));
-    s_sum[t] = cnt;
-    __syncthreads();
-    for (int d = 1; d < 256; d <<= 1) {
-        const uint32_t x = t >= d ? s_sum[t - d] : 0u;
-        __syncthreads();
-        s_sum[t] += x;
-        __syncthreads();
-    }
-    const uint32_t pos0 = s_sum[t] - cnt;    // this thread's first node in the ordered list
-    const int tot = (int)s_sum[255];
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t pos0 = incl - cnt;        // this lane's first node in the ordered list
+    const int tot = (int)rdlane(incl, 63);
     int *jx = jx_all + (size_t)b * jcap;
     uint32_t *jt = jt_all + (size_t)b * jcap;
     int cur = 0, nj = 0, term = nseg - 1, fb = 0;        // thread 0's path state
@@ -1292,24 +1284,21 @@ __global__ void __launch_bounds__(256) stitch_count_kernel(const BlockDesc *__re
     if (t == 0) wgsum[(size_t)b * maxw + blockIdx.x] = total;
 }
 
-__global__ void __launch_bounds__(256) stitch_scan_kernel(const BlockDesc *__restrict__ blocks,
-                                                          const PathInfo *__restrict__ path,
-                                                          uint32_t *__restrict__ wgsum, int maxw,
-                                                          BlockState *__restrict__ bst, int cap_blk,
-                                                          int *__restrict__ err)
+__global__ void __launch_bounds__(64) stitch_scan_kernel(const BlockDesc *__restrict__ blocks,
+                                                         const PathInfo *__restrict__ path,
+                                                         uint32_t *__restrict__ wgsum, int maxw,
+                                                         BlockState *__restrict__ bst, int cap_blk,
+                                                         int *__restrict__ err)
 {
-    __shared__ uint32_t s_w[4];
-    const int b = blockIdx.x, t = threadIdx.x;
+    const int b = blockIdx.x, t = threadIdx.x;          // one wave per block
     const int nw = (blocks[b].nseg + 255) >> 8;
     uint32_t run = 0;
-    for (int i0 = 0; i0 < nw; i0 += 256) {
+    for (int i0 = 0; i0 < nw; i0 += 64) {
         const int i = i0 + t;
         const uint32_t v = i < nw ? wgsum[(size_t)b * maxw + i] : 0u;
-        uint32_t total;
-        const uint32_t ex = wg_excl_scan(v, s_w, total);
-        if (i < nw) wgsum[(size_t)b * maxw + i] = run + ex;
-        run += total;
-        __syncthreads();
+        const uint32_t incl = wave_incl_scan(v);
+        if (i < nw) wgsum[(size_t)b * maxw + i] = run + incl - v;
+        run += rdlane(incl, 63);
     }
     if (t == 0) {
         BlockState s;
@@ -1519,20 +1508,20 @@ static hipError_t launch_fused_front(const BlockDesc *d_blocks, int nblocks, int
         hipLaunchKernelGGL((gmax2_kernel<true, true>), dim3(gx > 0 ? gx : 1, nblocks), dim3(256), 0, st, d_blocks, X.gm,
                            X.gstride, (prio >> 4) & 1, (const int *)fz.gm_need);
     }
-    const int rgrid = 512;
+    const int rgrid = 2048;                            // single-wave workgroups (below)
     const int HW = fz.hasher == 0 ? 5 : 7;
-    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(64), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
                        w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 0, (prio >> 1) & 1, X.rqkeep);
-    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
+    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
                        (prio >> 1) & 1);
     hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt, X.jcap,
                        X.wgsum, maxw, err);
-    hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
+    hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
                        cap_blk, err);
     hipLaunchKernelGGL(stitch_copy_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, spec, spec_cap,
                        X.wgsum, maxw, bst, offsets, cap_blk, (const uint32_t *)fz.sdig, (const uint32_t *)fz.bdig,
                        fz.dig, fz.need, HW);
-    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(64), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
                        w, maxlen, spec, spec_cap, meta, offsets, cap_blk, gm, X.gstride, 1, (prio >> 1) & 1, X.rqkeep);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
                        cap_blk, bst, gm, X.gstride, err, (prio >> 1) & 1, fz.need);
@@ -1589,18 +1578,20 @@ hipError_t launch_chunking(const BlockDesc *d_blocks, int nblocks, int64_t max_l
     hipLaunchKernelGGL(lane_walk_kernel<false>, dim3((total_waves + 3) / 4), dim3(256), walk_lds, st, d_blocks, nblocks, total_waves,
                        X.gm, X.gstride, w, maxlen, spec, spec_cap, meta, X.rq, X.rq_count, X.rq_cap, X.irr, err, ring_on, prio & 1);
     mk->mark(st);
-    const int rgrid = 512;                             // 2048 repair waves loop over the queue
-    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+    // 2048 repair waves loop over the queue, one per workgroup: the chain's small kernels start in
+    // whatever wave slots the co-running kernels leave (a 4-wave workgroup needs four on one CU)
+    const int rgrid = 2048;
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(64), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
                        w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 0, (prio >> 1) & 1, X.rqkeep);
-    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
+    hipLaunchKernelGGL(stitch_path_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, X.irr, meta, X.path, X.jx, X.jt, X.jcap,
                        (prio >> 1) & 1);
     hipLaunchKernelGGL(stitch_count_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, X.path, X.jx, X.jt, X.jcap,
                        X.wgsum, maxw, err);
-    hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(256), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
+    hipLaunchKernelGGL(stitch_scan_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, X.path, X.wgsum, maxw, bst,
                        cap_blk, err);
     hipLaunchKernelGGL(stitch_copy_kernel, dim3(maxw, nblocks), dim3(256), 0, st, d_blocks, meta, spec, spec_cap,
                        X.wgsum, maxw, bst, offsets, cap_blk);
-    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(256), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
+    hipLaunchKernelGGL(lane_repair_kernel, dim3(rgrid), dim3(64), 0, st, d_blocks, nblocks, X.rq, X.rq_count, X.rq_cap,
                        w, maxlen, spec, spec_cap, meta, offsets, cap_blk, X.gm, X.gstride, 1, (prio >> 1) & 1, X.rqkeep);
     hipLaunchKernelGGL(spec_fallback_kernel, dim3(nblocks), dim3(64), 0, st, d_blocks, w, maxlen, offsets,
                        cap_blk, bst, X.gm, X.gstride, err, (prio >> 1) & 1);
