@@ -82,6 +82,16 @@ def pipeline_traffic(pmc):
     return tot or None
 
 
+# template arguments a kernel's name carries in the PMC files (gmax2's defaulted COND is spelled out
+# since round 6: "gmax2_kernel<true, false>")
+PMC_SUFFIXES = ("", "<5>", "<7>", "<true>", "<false>", "<true, false>", "<false, false>")
+
+
+def pmc_lookup(pmc, kern):
+    """The PMC entry of kernel `kern` (any of its template instances above), or {}."""
+    return next((pmc[kern + t] for t in PMC_SUFFIXES if kern + t in pmc), {})
+
+
 def load_pmc(want):
     """Per-launch PMC figures of the newest committed rocprofv3 pass (scripts/r02_traffic.sh ->
     scripts/traffic.py -> profiles/*_traffic.json) taken on this same workload (`want`: the
@@ -725,8 +735,7 @@ def main():
         return {"bound": "hbm", "kernel": KERNEL_OF[name], "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_ms": round(ms, 4),
                 "algorithmic_bytes_per_launch": int(per_launch[name]),
-                "traffic": next((pmc[k] for k in (KERNEL_OF[name] + t for t in ("", "<5>", "<7>", "<true>", "<false>"))
-                                 if k in pmc), {}).get("hbm_bytes_per_launch")}
+                "traffic": pmc_lookup(pmc, KERNEL_OF[name]).get("hbm_bytes_per_launch")}
 
     # per-stream chains: the batch period is set by the longest one (the critical path)
     chain_def = CHAINS_GX if world > 1 else CHAINS
