@@ -150,3 +150,35 @@ def test_hadoop_frames_decode_segment_by_segment_through_liblz4():
         p += 4 + clen
         off += seg.size
     assert f[p:] == b"\x00\x00\x00\x00"
+
+
+def _decode_lz4codec(f):
+    """An Lz4Codec (BlockCompressorStream) file decoded group by group, each block by liblz4."""
+    out, p = [], 0
+    while p < len(f):
+        ulen = int.from_bytes(f[p:p + 4], "big")
+        p += 4
+        got = 0
+        while got < ulen:
+            clen = int.from_bytes(f[p:p + 4], "big")
+            seg = min(261100, ulen - got)
+            out.append(pa.decompress(f[p + 4:p + 4 + clen], decompressed_size=seg, codec="lz4_raw", asbytes=True))
+            p += 4 + clen
+            got += seg
+    return b"".join(out)
+
+
+@pytest.mark.gpu
+def test_gpu_lz4codec_files_decode_through_liblz4():
+    """The product's bytes themselves (the GPU Lz4Codec pass, no oracle in between) decode through
+    liblz4 to the input: every data kind at the table-switch and segment sizes, and config-4 corpus
+    blocks split into several 261,100-B segments."""
+    from hdrf_amd.lib import Context
+    ctx = Context(max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=16, arena_slots=16)
+    cases = [make_block(k, 21 + n, n) for k in KINDS for n in (13, 4096, 65546, 65547, 261100, 600000)]
+    roots = corpus_roots(6, 500000, 2, 8)
+    cases += [corpus_block_host(6, roots, b, 8, 1 << 18, mixed=True) for b in range(2)]
+    for i, d in enumerate(cases):
+        f = ctx.stream_block_host(4, 1, d, [d.size])
+        assert _decode_lz4codec(f) == d.tobytes(), f"case {i} ({d.size} B)"
+    ctx.close()
