@@ -153,3 +153,41 @@ def test_stream_codec4_is_the_lz4_stream():
     d = make_block("text", 2, 300_000).tobytes()
     w = [PKT] * 4 + [300_000 - 4 * PKT]
     assert hadoop_stream(4, d, w) == hadoop_lz4_stream(d, w)
+
+
+def _varint(b, p):
+    v = s = 0
+    while True:
+        c = b[p]
+        p += 1
+        v |= (c & 0x7F) << s
+        s += 7
+        if c < 0x80:
+            return v, p
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not HAVE_PA, reason="pyarrow snappy not present")
+def test_gpu_snappycodec_files_decode_through_pyarrow_snappy():
+    """The product's SnappyCodec files (the GPU stream pass, no oracle in between) decode group by
+    group, block by block, through pyarrow's libsnappy to the input, for packet-sized and single writes."""
+    from hdrf_amd.lib import Context
+    ctx = Context(max_block_bytes=4 << 20, max_batch_blocks=1, index_log2=16, arena_slots=16)
+    kinds = ["random", "zeros", "ff", "text", "lowent", "periodic", "sparse", "binary"]
+    d = np.concatenate([make_block(k, 300 + i, 150_001) for i, k in enumerate(kinds)])
+    for writes in ([d.size], [64_512] * (d.size // 64_512) + [d.size % 64_512], [1000, 0, 250_000, d.size - 251_000]):
+        f = ctx.stream_block_host(0, 81, d, writes)
+        out, p = [], 0
+        while p < len(f):
+            ulen = int.from_bytes(f[p:p + 4], "big")
+            p += 4
+            got = 0
+            while got < ulen:
+                clen = int.from_bytes(f[p:p + 4], "big")
+                blk = f[p + 4:p + 4 + clen]
+                n, _ = _varint(blk, 0)
+                out.append(pa.decompress(blk, decompressed_size=n, codec="snappy", asbytes=True))
+                p += 4 + clen
+                got += n
+        assert b"".join(out) == d.tobytes(), writes
+    ctx.close()
