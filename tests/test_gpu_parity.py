@@ -665,3 +665,23 @@ def test_reset_epochs_are_fresh_indexes(hasher):
     assert g["store_size"] == o["store_size"]
     ctx.dev_free(dev)
     ctx.close()
+
+
+@pytest.mark.parametrize("hasher", [0, 1])
+def test_product_against_independent_restatements(hasher):
+    """No C oracle in between: the GPU's chunk END offsets equal the literal Python closed form of
+    DataDeduplicator.chunking (oracle/pyref.py chunking_closed_form, DN/DataDeduplicator.java:264-307)
+    and every digest equals hashlib's SHA-1 / SHA-224 of the chunk's bytes (DN/utilities.java:98-137)."""
+    import hashlib
+    from oracle import pyref
+    h = hashlib.sha1 if hasher == 0 else hashlib.sha224
+    ctx = Context(hasher=hasher, segment_bytes=1 << 16, **SMALL)
+    for i, kind in enumerate(["random", "text", "lowent", "binary", "sparse", "periodic", "zeros"]):
+        blk = make_block(kind, 500 + i, 700_000 + 977 * i)
+        g = ctx.reduce_block(blk, 7000 + i)
+        raw = blk.tobytes()
+        assert list(g["offsets"]) == pyref.chunking_closed_form(raw), kind
+        starts = [0] + list(g["offsets"][:-1])
+        for j, (a, b) in enumerate(zip(starts, g["offsets"])):
+            assert bytes(g["digests"][j]) == h(raw[a:b]).digest(), (kind, j)
+    ctx.close()
