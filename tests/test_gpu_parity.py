@@ -685,3 +685,40 @@ def test_product_against_independent_restatements(hasher):
         for j, (a, b) in enumerate(zip(starts, g["offsets"])):
             assert bytes(g["digests"][j]) == h(raw[a:b]).digest(), (kind, j)
     ctx.close()
+
+
+def test_dedup_semantics_against_python_transliteration():
+    """The whole reduction with no C oracle in between: a sequence of blocks with cross-block and
+    intra-block duplicates through the GPU and through oracle/pyref.py's literal Python DataDeduplicator
+    (dict Redis, hashlib; DN/DataDeduplicator.java:108-217, chunkMeta.java:35-77): the same cuts,
+    digests, dedup decisions and storeSize per block, then the same index (every key, 11-byte value),
+    allocator ("blockID"), recipes and container bytes — with 1.1 MB containers so flushes happen."""
+    from oracle import pyref
+    cmax = 1_100_000
+    ctx = Context(container_max=cmax, **SMALL)
+    ref = pyref.PyRef(max_size=cmax)
+    base = [make_block(k, 900 + i, 1_000_000 + 1311 * i) for i, k in enumerate(["random", "text", "binary", "lowent"])]
+    blocks = [base[0], base[1], base[0].copy(), np.concatenate([base[2][:500_000], base[1][100_000:]]),
+              np.concatenate([base[3], base[3]]), base[2], make_block("random", 950, 30_000)]
+    ids = []
+    for i, blk in enumerate(blocks):
+        bid = 0x3100 + i
+        g, r = ctx.reduce_block(blk, bid), ref.reduce(blk.tobytes(), bid)
+        assert list(g["offsets"]) == r["offsets"], i
+        assert [bytes(x) for x in g["digests"]] == r["digests"], i
+        assert list(g["is_new"]) == r["is_new"], i
+        assert g["store_size"] == r["store_size"], i
+        ids.append(bid)
+    keys, vals = ctx.index_dump()
+    gidx = {bytes(k): bytes(v) for k, v in zip(keys, vals)}
+    ridx = {k: v for k, v in ref.redis.items() if len(k) == 20}
+    assert gidx == ridx
+    assert ctx.allocator() == ref.redis[b"blockID"]
+    for bid in ids:
+        assert ctx.recipe(bid) == ref.redis[(bid & 0xFFFFFFFF).to_bytes(4, "big")], bid
+    for cid, data in ref.files.items():
+        got, closed = ctx.container(cid)
+        assert got == bytes(data), cid
+        assert closed == (cid in ref.closed), cid
+    assert ref.closed                                  # (the sequence does close containers)
+    ctx.close()
